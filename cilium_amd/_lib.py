@@ -1,0 +1,122 @@
+"""ctypes binding of libgpuflow (include/gpuflow.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()``
+(``cilium_amd/libgpuflow.so``).  There is no fallback: if it is missing the
+import fails loudly.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpuflow.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libgpuflow.so not found at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; g.build()'`")
+
+lib = C.CDLL(LIB_PATH)
+
+GF_MAX_L4_INGRESS = 64
+GF_STATS_WORDS = 512
+
+
+class gf_map_info(C.Structure):
+    _fields_ = [("map_type", C.c_uint32), ("key_size", C.c_uint32), ("value_size", C.c_uint32),
+                ("max_entries", C.c_uint32), ("map_flags", C.c_uint32), ("n_entries", C.c_uint32),
+                ("device_bytes", C.c_uint64)]
+
+
+class gf_pkt_cols(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("len", C.c_void_p), ("ethertype", C.c_void_p),
+                ("saddr4", C.c_void_p), ("daddr4", C.c_void_p), ("proto", C.c_void_p),
+                ("l4_off", C.c_void_p), ("l4w0", C.c_void_p), ("l4w3", C.c_void_p),
+                ("saddr6", C.c_void_p), ("daddr6", C.c_void_p), ("src_identity", C.c_void_p),
+                ("ifindex", C.c_void_p), ("lxc_id", C.c_void_p), ("tc_index", C.c_void_p),
+                ("flow_hash", C.c_void_p)]
+
+
+class gf_frames(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("snap_stride", C.c_uint32), ("snap", C.c_void_p), ("len", C.c_void_p)]
+
+
+class gf_pkt_cols_out(C.Structure):
+    _fields_ = [("ethertype", C.c_void_p), ("saddr4", C.c_void_p), ("daddr4", C.c_void_p),
+                ("proto", C.c_void_p), ("l4_off", C.c_void_p), ("l4w0", C.c_void_p), ("l4w3", C.c_void_p),
+                ("saddr6", C.c_void_p), ("daddr6", C.c_void_p)]
+
+
+class gf_xdp_cfg(C.Structure):
+    _fields_ = [("cidr4_hmap", C.c_int), ("cidr4_lmap", C.c_int), ("cidr6_hmap", C.c_int),
+                ("cidr6_lmap", C.c_int), ("lxc_map", C.c_int)]
+
+
+class gf_lb_cfg(C.Structure):
+    _fields_ = [("lb4_services", C.c_int), ("lb6_services", C.c_int), ("flags", C.c_uint32),
+                ("redirect_ifindex", C.c_uint32)]
+
+
+class gf_l4_allow(C.Structure):
+    _fields_ = [("port", C.c_uint16), ("proxy", C.c_uint16), ("nexthdr", C.c_uint8), ("pad", C.c_uint8 * 3)]
+
+
+class gf_lxc_cfg(C.Structure):
+    _fields_ = [("lxc_id", C.c_uint32), ("seclabel", C.c_uint32), ("policy_map", C.c_int),
+                ("ct_map4", C.c_int), ("ct_map6", C.c_int), ("cidr4_ingress_map", C.c_int),
+                ("cidr6_ingress_map", C.c_int), ("revnat4_map", C.c_int), ("revnat6_map", C.c_int),
+                ("flags", C.c_uint32), ("n_l4_ingress", C.c_uint32),
+                ("l4_ingress", gf_l4_allow * GF_MAX_L4_INGRESS)]
+
+
+class gf_node_cfg(C.Structure):
+    _fields_ = [("host_ifindex", C.c_uint32)]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+VP = C.c_void_p
+_sig("gf_map_create", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
+_sig("gf_map_update_elem", C.c_int, C.c_int, VP, VP, C.c_uint64)
+_sig("gf_map_lookup_elem", C.c_int, C.c_int, VP, VP)
+_sig("gf_map_delete_elem", C.c_int, C.c_int, VP)
+_sig("gf_map_get_next_key", C.c_int, C.c_int, VP, VP)
+_sig("gf_map_update_batch", C.c_int, C.c_int, VP, VP, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32))
+_sig("gf_map_get_info", C.c_int, C.c_int, C.POINTER(gf_map_info))
+_sig("gf_obj_pin", C.c_int, C.c_int, C.c_char_p)
+_sig("gf_obj_get", C.c_int, C.c_char_p)
+_sig("gf_obj_close", C.c_int, C.c_int)
+_sig("gf_obj_unpin", C.c_int, C.c_char_p)
+_sig("gf_now_sec", C.c_uint32)
+_sig("gf_parse_frames", C.c_int, C.POINTER(gf_frames), C.POINTER(gf_pkt_cols_out), VP)
+_sig("gf_xdp_prog_load", C.c_int, C.POINTER(gf_xdp_cfg))
+_sig("gf_xdp_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), VP, VP)
+_sig("gf_lb_prog_load", C.c_int, C.POINTER(gf_lb_cfg))
+_sig("gf_lb_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), VP, VP, VP)
+_sig("gf_lxc_prog_load", C.c_int, C.POINTER(gf_lxc_cfg))
+_sig("gf_policy_array_create", C.c_int)
+_sig("gf_policy_array_update", C.c_int, C.c_int, C.c_uint32, C.c_int)
+_sig("gf_node_config", C.c_int, C.POINTER(gf_node_cfg))
+_sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c_uint32, VP, VP)
+_sig("gf_set_stats_sink", C.c_int, VP)
+_sig("gf_dev_alloc", VP, C.c_size_t)
+_sig("gf_dev_free", C.c_int, VP)
+_sig("gf_memcpy_h2d", C.c_int, VP, VP, C.c_size_t, VP)
+_sig("gf_memcpy_d2h", C.c_int, VP, VP, C.c_size_t, VP)
+_sig("gf_stream_sync", C.c_int, VP)
+_sig("gf_device_count", C.c_int)
+_sig("gf_version", C.c_char_p)
+
+# Every symbol the C header declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "gf_map_create", "gf_map_update_elem", "gf_map_lookup_elem", "gf_map_delete_elem",
+    "gf_map_get_next_key", "gf_map_update_batch", "gf_map_get_info", "gf_obj_pin", "gf_obj_get",
+    "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
+    "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
+    "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
+    "gf_policy_ingress_classify", "gf_set_stats_sink", "gf_dev_alloc", "gf_dev_free",
+    "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
+]

@@ -1,0 +1,133 @@
+// gf_common.h — table layouts shared by the host shadow (gf_maps.cpp) and the
+// HIP kernels (gf_kernels.hip) of libgpuflow.
+//
+// Exact-match hash maps (kernel BPF_MAP_TYPE_HASH / LRU_HASH semantics, see
+// DESIGN.md) use open addressing with linear probing over fixed-size slots:
+//
+//   inline layout (slot <= 128 B, never straddles a 128-B L2 line):
+//     [ key (ksz B) | state (1 B) | pad | value (vsz B) at voff | pad ]
+//   split layout (key+value > 128 B, e.g. endpoint_info 112 B):
+//     slots: [ key | state | pad ]  (pow2 stride)   vals: vsz B per slot
+//
+// state: 0 empty, 1 full, 2 deleted (tombstone), 3 busy (device insert in
+// flight).  Device inserts only ever claim EMPTY slots; tombstones are reused
+// by host-side rebuilds only (see the CT concurrency note in DESIGN.md).
+//
+// The hash is a murmur3-style mix over the key as little-endian u32 words
+// (zero-padded), identical on host and device.
+//
+// LPM tries (kernel BPF_MAP_TYPE_LPM_TRIE) are only ever queried by the
+// datapath for membership ("is there a stored prefix covering addr"):
+// bpf_xdp.c:112 and maps.h:129,139 test the lookup result against NULL.  The
+// device form is therefore a coverage trie: a 2^R-entry root table followed by
+// 8-bit-stride nodes {full bitmap[256], child bitmap[256], child_base}.
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define GF_HD __host__ __device__ __forceinline__
+#else
+#define GF_HD inline
+#endif
+
+enum : uint8_t { GF_SLOT_EMPTY = 0, GF_SLOT_FULL = 1, GF_SLOT_TOMB = 2, GF_SLOT_BUSY = 3 };
+
+struct gf_htab_desc {
+    uint8_t  *slots;       // nslots * slot_size
+    uint8_t  *vals;        // split layout only (nslots * vsz), else nullptr
+    uint32_t *count;       // device element counter (inserts / deletes)
+    uint64_t  mask;        // nslots - 1 (0 with slots == nullptr => empty map)
+    uint32_t  ksz, vsz, slot_size, voff;
+    uint32_t  split, max_entries;
+};
+
+struct gf_trie_desc {
+    const uint32_t *root;  // 2^root_bits entries: 0 empty, ~0u full, else node+1
+    const uint8_t  *nodes; // 128 B nodes
+    uint32_t root_bits;    // 8 or 16; 0 => map absent/empty (never matches)
+    uint32_t addr_bytes;   // 4 or 16
+};
+#define GF_TRIE_NODE_BYTES 128u
+#define GF_TRIE_FULL 0xFFFFFFFFu
+
+GF_HD uint32_t gf_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+GF_HD uint32_t gf_hash_words(const uint32_t *w, int nw, uint32_t nbytes) {
+    uint32_t h = 0x9747b28cu ^ nbytes;
+    for (int i = 0; i < nw; i++) {
+        uint32_t k = w[i] * 0xcc9e2d51u;
+        k = gf_rotl32(k, 15);
+        k *= 0x1b873593u;
+        h ^= k;
+        h = gf_rotl32(h, 13);
+        h = h * 5u + 0xe6546b64u;
+    }
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
+// Layout rule (host decides, device reads from the descriptor).
+GF_HD uint32_t gf_pow2ceil32(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+GF_HD void gf_htab_layout(uint32_t ksz, uint32_t vsz, uint32_t *slot_size, uint32_t *voff,
+                          uint32_t *split) {
+    uint32_t hdr = ksz + 1;
+    uint32_t align = vsz >= 8 ? 8u : (vsz >= 4 ? 4u : 1u);
+    uint32_t vo = (hdr + align - 1) / align * align;
+    uint32_t inl = gf_pow2ceil32(vo + vsz);
+    if (inl < 16) inl = 16;
+    if (inl <= 128) { *slot_size = inl; *voff = vo; *split = 0; return; }
+    uint32_t ks = gf_pow2ceil32(hdr);
+    if (ks < 16) ks = 16;
+    *slot_size = ks; *voff = 0; *split = 1;
+}
+
+// Unordered-address-pair group hash (flow group of the CT ordering rule).
+GF_HD uint32_t gf_pair_hash4(uint32_t a, uint32_t b) {
+    uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    uint32_t w[2] = {lo, hi};
+    return gf_hash_words(w, 2, 8);
+}
+GF_HD uint32_t gf_pair_hash6(const uint32_t *a, const uint32_t *b) {
+    // lexicographic byte compare of the two 16-byte addresses
+    int less = 0;
+    for (int i = 0; i < 4; i++) {
+        uint32_t x = a[i], y = b[i];
+        if (x != y) {
+            // compare as big-endian bytes
+            uint32_t xb = ((x & 0xff) << 24) | ((x & 0xff00) << 8) | ((x >> 8) & 0xff00) | (x >> 24);
+            uint32_t yb = ((y & 0xff) << 24) | ((y & 0xff00) << 8) | ((y >> 8) & 0xff00) | (y >> 24);
+            less = xb < yb;
+            break;
+        }
+    }
+    const uint32_t *lo = less ? a : b, *hi = less ? b : a;
+    uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return gf_hash_words(w, 8, 32);
+}
+
+// Packed per-packet record used by the ingress kernel after grouping
+// (32 B, one dwordx4 x2 load).  cls: bits0-1 L3 class (0 other, 1 v4, 2 v6),
+// bit 2 TC_INDEX_F_SKIP_PROXY.
+struct __attribute__((aligned(16))) gf_rec {
+    uint32_t saddr, daddr, len, l4w0, src_identity, ifindex;
+    uint16_t lxc_id;
+    int16_t  l4_off;
+    uint16_t l4w3;
+    uint8_t  proto, cls;
+};
+static_assert(sizeof(gf_rec) == 32, "gf_rec must be 32 bytes");
+
+// Device-side endpoint program (lxc) configuration.
+#define GF_MAX_L4 64
+struct gf_l4_allow_dev { uint16_t port, proxy; uint8_t nexthdr, pad[3]; };
+struct gf_lxc_dev {
+    uint32_t flags, lxc_id, seclabel, n_l4;
+    gf_htab_desc policy, ct4, ct6, revnat4, revnat6;
+    gf_trie_desc cidr4, cidr6;
+    gf_l4_allow_dev l4[GF_MAX_L4];
+};

@@ -1,0 +1,159 @@
+// gf_device.h — device-side table probes for gfx950 (one packet per lane).
+//
+// Every probe is a plain global load of the slot header (dwordx4 where the
+// slot allows it), compare, and linear step; the table descriptor lives in
+// kernel arguments (SGPRs).  Values are read/written in place.
+#pragma once
+#include "gf_common.h"
+
+#define GF_EFAULT 14
+
+namespace gfd {
+
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t *p, uint32_t (&w)[NW]) {
+    int k = 0;
+#pragma unroll
+    for (; k + 4 <= NW; k += 4) {
+        uint4 v = *reinterpret_cast<const uint4 *>(p + 4 * k);
+        w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+    }
+    if (NW - k >= 2) {
+        uint2 v = *reinterpret_cast<const uint2 *>(p + 4 * k);
+        w[k] = v.x; w[k + 1] = v.y;
+        k += 2;
+    }
+    if (NW - k == 1) w[k] = *reinterpret_cast<const uint32_t *>(p + 4 * k);
+}
+
+template <int KSZ>
+__device__ __forceinline__ uint32_t key_hash(const uint32_t *kw) {
+    return gf_hash_words(kw, (KSZ + 3) / 4, KSZ);
+}
+
+// Exact-match probe; returns slot index or -1.
+template <int KSZ>
+__device__ __forceinline__ int64_t ht_find(const gf_htab_desc &d, const uint32_t *kw, uint32_t h) {
+    if (!d.slots) return -1;
+    constexpr int SW = KSZ / 4, SB = KSZ % 4, NW = SW + 1;
+    uint64_t i = h & d.mask;
+    for (uint64_t p = 0; p <= d.mask; p++) {
+        const uint8_t *s = d.slots + i * d.slot_size;
+        uint32_t w[NW];
+        load_words<NW>(s, w);
+        uint32_t st = (w[SW] >> (8 * SB)) & 0xff;
+        if (st == GF_SLOT_EMPTY) return -1;
+        if (st == GF_SLOT_FULL) {
+            bool eq = true;
+#pragma unroll
+            for (int k = 0; k < SW; k++) eq &= (w[k] == kw[k]);
+            if (SB) eq &= ((w[SW] & ((1u << (8 * SB)) - 1u)) == kw[SW]);
+            if (eq) return (int64_t)i;
+        }
+        i = (i + 1) & d.mask;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ uint8_t *ht_val(const gf_htab_desc &d, uint64_t i) {
+    return d.split ? d.vals + i * d.vsz : d.slots + i * d.slot_size + d.voff;
+}
+
+// Insert-or-replace (map_update_elem BPF_ANY) for keys owned by the calling
+// lane (flow-group exclusivity).  VW = value words.  Returns 0,
+// or -E2BIG (7) when a new key would exceed max_entries (strict mode) or no
+// empty slot is left.  *added is incremented for a new key.
+template <int KSZ, int VW>
+__device__ __forceinline__ int ht_upsert(const gf_htab_desc &d, const uint32_t *kw, const uint32_t *vw,
+                                         bool strict, int *added) {
+    constexpr int SW = KSZ / 4, SB = KSZ % 4;
+    uint32_t h = key_hash<KSZ>(kw);
+    int64_t f = ht_find<KSZ>(d, kw, h);
+    if (f >= 0) {
+        uint32_t *v = reinterpret_cast<uint32_t *>(ht_val(d, (uint64_t)f));
+#pragma unroll
+        for (int k = 0; k < VW; k++) v[k] = vw[k];
+        return 0;
+    }
+    if (strict) {
+        uint32_t old = atomicAdd(d.count, 1u);
+        if (old >= d.max_entries) { atomicSub(d.count, 1u); return -7; }
+    }
+    uint64_t i = h & d.mask;
+    for (uint64_t p = 0; p <= d.mask; p++) {
+        uint8_t *s = d.slots + i * d.slot_size;
+        uint32_t *sw = reinterpret_cast<uint32_t *>(s + 4 * SW);
+        uint32_t cur = *reinterpret_cast<volatile uint32_t *>(sw);
+        for (;;) {
+            uint32_t st = (cur >> (8 * SB)) & 0xff;
+            if (st != GF_SLOT_EMPTY) break;
+            uint32_t keep = SB ? (kw[SW] & ((1u << (8 * SB)) - 1u)) : 0u;
+            uint32_t want = keep | ((uint32_t)GF_SLOT_BUSY << (8 * SB));
+            uint32_t seen = atomicCAS(sw, cur, want);
+            if (seen == cur) {
+                uint32_t *ks = reinterpret_cast<uint32_t *>(s);
+#pragma unroll
+                for (int k = 0; k < SW; k++) ks[k] = kw[k];
+                uint32_t *v = reinterpret_cast<uint32_t *>(ht_val(d, i));
+#pragma unroll
+                for (int k = 0; k < VW; k++) v[k] = vw[k];
+                __atomic_store_n(sw, keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)), __ATOMIC_RELAXED);
+                if (!strict) (*added)++;
+                return 0;
+            }
+            cur = seen;
+        }
+        i = (i + 1) & d.mask;
+    }
+    if (strict) atomicSub(d.count, 1u);
+    return -7;
+}
+
+template <int KSZ>
+__device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t *kw, bool strict, int *added) {
+    constexpr int SW = KSZ / 4, SB = KSZ % 4;
+    int64_t f = ht_find<KSZ>(d, kw, key_hash<KSZ>(kw));
+    if (f < 0) return;
+    uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + (uint64_t)f * d.slot_size + 4 * SW);
+    uint32_t cur = *sw;
+    uint32_t nv = (cur & ~(0xffu << (8 * SB))) | ((uint32_t)GF_SLOT_TOMB << (8 * SB));
+    __atomic_store_n(sw, nv, __ATOMIC_RELAXED);
+    if (strict) atomicSub(d.count, 1u);
+    else (*added)--;
+}
+
+// Coverage-trie membership of an address given as raw (LE-loaded) words.
+__device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_t *aw) {
+    if (!t.root_bits) return false;
+    auto byte_at = [&](uint32_t k) -> uint32_t { return (aw[k >> 2] >> (8 * (k & 3))) & 0xffu; };
+    uint32_t idx = t.root_bits == 16 ? ((byte_at(0) << 8) | byte_at(1)) : byte_at(0);
+    uint32_t e = t.root[idx];
+    if (e == 0) return false;
+    if (e == GF_TRIE_FULL) return true;
+    uint32_t node = e - 1;
+    for (uint32_t k = t.root_bits / 8; k < t.addr_bytes; k++) {
+        uint32_t b = byte_at(k);
+        const uint64_t *nd = reinterpret_cast<const uint64_t *>(t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES);
+        uint32_t w = b >> 6, bit = b & 63;
+        if ((nd[w] >> bit) & 1ull) return true;
+        uint64_t cw = nd[4 + w];
+        if (!((cw >> bit) & 1ull)) return false;
+        uint32_t rank = __popcll(cw & ((1ull << bit) - 1ull));
+        for (uint32_t j = 0; j < w; j++) rank += __popcll(nd[4 + j]);
+        node = reinterpret_cast<const uint32_t *>(nd)[16] + rank;
+    }
+    return false;
+}
+
+// skb_load_bytes / store / csum_replace bound rules (see oracle.c).
+__device__ __forceinline__ bool skb_ok(int32_t off, uint32_t n, uint32_t len) {
+    return (uint32_t)off <= 0xffffu && (uint64_t)(uint32_t)off + n <= len;
+}
+__device__ __forceinline__ bool l4csum_ok(int32_t off, uint32_t len) {
+    return (uint32_t)off <= 0xffffu && !(off & 1) && (uint64_t)(uint32_t)off + 2 <= len;
+}
+__device__ __forceinline__ uint32_t csum_l4_offset(uint32_t nexthdr) {
+    return nexthdr == 6 ? 16u : nexthdr == 17 ? 6u : nexthdr == 58 ? 2u : 0u;
+}
+
+}  // namespace gfd

@@ -1,0 +1,130 @@
+// gf_internal.h — host-side objects of libgpuflow (maps, programs, registry).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include <map>
+#include <memory>
+#include <mutex>
+#include "gf_common.h"
+#include "../../include/gpuflow.h"
+
+namespace gf {
+
+std::recursive_mutex &big_lock();
+
+// ---- device buffer ----
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf();
+    int ensure(size_t n);   // (re)allocate to exactly n bytes, contents undefined
+    void release();
+};
+
+int hip_ok(hipError_t e, const char *what);
+
+// ---- LPM key ordering (kernel trie post-order, kernel/bpf/lpm_trie.c) ----
+struct LpmKeyLess {
+    uint32_t data_bytes;
+    bool operator()(const std::string &a, const std::string &b) const;
+};
+
+// ---- exact-match hash table (host shadow, same layout as the device) ----
+struct HTab {
+    uint32_t ksz = 0, vsz = 0, slot_size = 0, voff = 0, split = 0;
+    uint64_t nslots = 0;
+    std::vector<uint8_t> slots, vals;
+    uint64_t count = 0, tombs = 0;
+    void init(uint32_t k, uint32_t v, uint64_t n);
+    uint32_t hash(const uint8_t *key) const;
+    int64_t find(const uint8_t *key) const;
+    uint8_t *val(uint64_t i) { return split ? &vals[i * vsz] : &slots[i * slot_size + voff]; }
+    const uint8_t *key(uint64_t i) const { return &slots[i * slot_size]; }
+    uint8_t state(uint64_t i) const { return slots[i * slot_size + ksz]; }
+    void set_state(uint64_t i, uint8_t s) { slots[i * slot_size + ksz] = s; }
+    int64_t insert_new(const uint8_t *key, const uint8_t *value);  // caller checked absence
+    void erase(uint64_t i);
+    void rehash(uint64_t new_nslots);
+};
+
+enum class ObjKind { Map, ProgXdp, ProgLb, ProgLxc, PolicyArray };
+
+struct Obj {
+    ObjKind kind;
+    explicit Obj(ObjKind k) : kind(k) {}
+    virtual ~Obj() {}
+};
+
+struct Map : Obj {
+    uint32_t type, ksz, vsz, max_entries, flags;
+    // hash types
+    HTab ht;
+    bool host_valid = true;     // host shadow up to date
+    bool dev_valid = false;     // HBM replica up to date
+    bool fixed_capacity = false; // device inserts into this map (CT): nslots sized by max_entries
+    DevBuf d_slots, d_vals, d_count;
+    // LPM
+    std::map<std::string, std::string, LpmKeyLess> lpm;   // orig key bytes -> value
+    uint32_t lpm_len_cnt[129] = {0};
+    bool trie_dirty = true;
+    DevBuf d_root, d_nodes;
+    uint32_t trie_root_bits = 0;
+
+    Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f);
+    bool is_lpm() const { return type == GF_MAP_TYPE_LPM_TRIE; }
+    uint32_t lpm_bits() const { return (ksz - 4) * 8; }
+    uint32_t n_entries() const { return is_lpm() ? (uint32_t)lpm.size() : (uint32_t)ht.count; }
+
+    // host ops (kernel syscall semantics)
+    int update(const uint8_t *key, const uint8_t *value, uint64_t flags);
+    int lookup(const uint8_t *key, uint8_t *value);
+    int erase(const uint8_t *key);
+    int next_key(const uint8_t *key, uint8_t *next);
+
+    // coherence
+    int pull();                       // device -> host if !host_valid
+    int push(hipStream_t s);          // host -> device if !dev_valid / trie dirty
+    void device_modified() { host_valid = false; }
+    void make_fixed_capacity();
+    gf_htab_desc hdesc();             // requires push() done
+    gf_trie_desc tdesc();             // requires push() done
+    uint64_t device_bytes() const { return d_slots.bytes + d_vals.bytes + d_root.bytes + d_nodes.bytes; }
+};
+
+struct ProgXdp : Obj {
+    gf_xdp_cfg cfg{};
+    std::shared_ptr<Map> m4h, m4l, m6h, m6l, lxc;
+    ProgXdp() : Obj(ObjKind::ProgXdp) {}
+};
+struct ProgLb : Obj {
+    gf_lb_cfg cfg{};
+    std::shared_ptr<Map> lb4, lb6;
+    ProgLb() : Obj(ObjKind::ProgLb) {}
+};
+struct ProgLxc : Obj {
+    gf_lxc_cfg cfg{};
+    std::shared_ptr<Map> policy, ct4, ct6, cidr4, cidr6, revnat4, revnat6;
+    ProgLxc() : Obj(ObjKind::ProgLxc) {}
+};
+struct PolicyArray : Obj {
+    std::map<uint32_t, std::shared_ptr<ProgLxc>> slots;   // lxc_id -> prog
+    // device image
+    DevBuf d_slot_of_lxc;      // uint16[65536]: 0 = empty, else cfg index + 1
+    DevBuf d_cfgs;             // gf_lxc_dev[]
+    bool dirty = true;
+    PolicyArray() : Obj(ObjKind::PolicyArray) {}
+};
+
+std::shared_ptr<Obj> get_obj(int handle);
+std::shared_ptr<Map> get_map(int handle);
+int new_handle(std::shared_ptr<Obj> o);
+uint32_t host_ifindex();
+uint64_t *stats_sink();
+
+// trie builder (host)
+void build_trie(const Map &m, std::vector<uint32_t> &root, std::vector<uint8_t> &nodes,
+                uint32_t &root_bits);
+
+}  // namespace gf

@@ -1,0 +1,1005 @@
+// gf_kernels.hip — gfx950 kernels of libgpuflow and the program/classify C ABI.
+//
+//   k_parse     raw frames -> SoA header columns   (skb_load_bytes rules)
+//   k_xdp       bpf/bpf_xdp.c:88-184               one packet per lane
+//   k_lb        bpf/bpf_lb.c:58-212 + lib/lb.h      one packet per lane
+//   k_ing_pack  columns -> 32-B records + flow-group key (unordered addr pair)
+//   (rocPRIM stable radix sort of (group, index) + exclusive scan)
+//   k_ing_run   bpf/bpf_lxc.c:745-1024 handle_policy: one flow-group queue per
+//               lane, packets of a queue in batch order (CT ordering rule)
+#include "gf_internal.h"
+#include "gf_device.h"
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <errno.h>
+#include <string.h>
+
+using namespace gf;
+using namespace gfd;
+
+#define BLOCK 256
+
+// ---------------------------------------------------------------- constants
+enum {
+    TC_OK = 0, TC_SHOT = 2, TC_REDIRECT = 7, XDP_DROP_ = 1, XDP_PASS_ = 2,
+    D_POLICY = -133, D_INVALID = -134, D_CT_INVALID_HDR = -135, D_CT_UNKNOWN_PROTO = -137,
+    D_UNKNOWN_L3 = -139, D_MISSED_TAIL_CALL = -140, D_WRITE_ERROR = -141, D_UNKNOWN_L4 = -142,
+    D_CSUM_L4 = -154, D_CT_CREATE_FAILED = -155, D_NO_SERVICE = -158, D_POLICY_L4 = -159,
+};
+enum { CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3 };
+enum { ACT_UNSPEC = 0, ACT_CREATE = 1, ACT_CLOSE = 2 };
+#define F_RX_CLOSING 1u
+#define F_TX_CLOSING 2u
+#define F_LB_LOOPBACK 8u
+#define F_SEEN_NON_SYN 16u
+
+// ---------------------------------------------------------------- stats
+struct Stats {
+    uint32_t *lds;
+    __device__ void init() {
+        for (int k = threadIdx.x; k < 272; k += blockDim.x) lds[k] = 0;
+        __syncthreads();
+    }
+    __device__ void add(uint32_t bin) { atomicAdd(&lds[bin], 1u); }
+    __device__ void flush(unsigned long long *g) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < 272; k += blockDim.x)
+            if (lds[k]) atomicAdd(&g[k], (unsigned long long)lds[k]);
+    }
+};
+
+// ================================================================ parse
+__device__ __forceinline__ uint32_t fbyte(const uint8_t *f, uint32_t cap, uint32_t off) {
+    return off < cap ? f[off] : 0u;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_parse(gf_frames fr, gf_pkt_cols_out o) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < fr.n; i += gridDim.x * blockDim.x) {
+        const uint8_t *f = fr.snap + (size_t)i * fr.snap_stride;
+        uint32_t len = fr.len[i];
+        uint32_t cap = fr.snap_stride < len ? fr.snap_stride : len;
+        uint16_t et = len >= 14 ? (uint16_t)((fbyte(f, cap, 12) << 8) | fbyte(f, cap, 13)) : 0;
+        uint32_t sa = 0, da = 0, w0 = 0; uint16_t w3 = 0; uint8_t proto = 0; int l4 = 0;
+        uint32_t s6[4] = {0, 0, 0, 0}, d6[4] = {0, 0, 0, 0};
+        bool have = false;
+        if (et == 0x0800 && len >= 34) {
+            for (int k = 0; k < 4; k++) { sa |= fbyte(f, cap, 26 + k) << (8 * k); da |= fbyte(f, cap, 30 + k) << (8 * k); }
+            proto = (uint8_t)fbyte(f, cap, 23);
+            l4 = 14 + (fbyte(f, cap, 14) & 0xf) * 4;
+            have = true;
+        } else if (et == 0x86DD && len >= 54) {
+            for (int k = 0; k < 16; k++) {
+                s6[k >> 2] |= fbyte(f, cap, 22 + k) << (8 * (k & 3));
+                d6[k >> 2] |= fbyte(f, cap, 38 + k) << (8 * (k & 3));
+            }
+            // ipv6_hdrlen, bpf/lib/ipv6.h:61-98 (AUTH length chosen by the NEXT header, as written)
+            uint8_t nh = (uint8_t)fbyte(f, cap, 20);
+            int hl = 40, res = -156;
+            for (int it = 0; it < 4; it++) {
+                if (nh == 59) { res = -156; goto done; }
+                if (nh == 44) { res = -157; goto done; }
+                if (nh == 0 || nh == 43 || nh == 51 || nh == 60) {
+                    int off = 14 + hl;
+                    if (!skb_ok(off, 2, len)) { res = -134; goto done; }
+                    uint32_t onh = fbyte(f, cap, off), ohl = fbyte(f, cap, off + 1);
+                    nh = (uint8_t)onh;
+                    if (nh == 51) hl += (int)(ohl + 2) << 2; else hl += (int)(ohl + 1) << 3;
+                    continue;
+                }
+                res = hl;
+                proto = nh;
+                goto done;
+            }
+            res = -156;
+        done:
+            if (res < 0) proto = (uint8_t)fbyte(f, cap, 20);
+            l4 = 14 + res;
+            have = true;
+        }
+        if (have) {
+            for (int k = 0; k < 4; k++) {
+                int64_t off = (int64_t)l4 + k;
+                if (off >= 0 && off < (int64_t)len) w0 |= fbyte(f, cap, (uint32_t)off) << (8 * k);
+            }
+            for (int k = 0; k < 2; k++) {
+                int64_t off = (int64_t)l4 + 12 + k;
+                if (off >= 0 && off < (int64_t)len) w3 |= (uint16_t)(fbyte(f, cap, (uint32_t)off) << (8 * k));
+            }
+        }
+        o.ethertype[i] = et; o.saddr4[i] = sa; o.daddr4[i] = da; o.proto[i] = proto;
+        o.l4_off[i] = (int16_t)l4; o.l4w0[i] = w0; o.l4w3[i] = w3;
+        if (o.saddr6) reinterpret_cast<uint4 *>(o.saddr6)[i] = make_uint4(s6[0], s6[1], s6[2], s6[3]);
+        if (o.daddr6) reinterpret_cast<uint4 *>(o.daddr6)[i] = make_uint4(d6[0], d6[1], d6[2], d6[3]);
+    }
+}
+
+// ================================================================ XDP
+struct XdpDev {
+    gf_htab_desc h4, h6, lxc;
+    gf_trie_desc l4, l6;
+    uint32_t has_h4, has_h6;
+};
+
+__device__ __forceinline__ bool lxc_has4(const gf_htab_desc &lxc, uint32_t daddr) {
+    uint32_t kw[5] = {daddr, 0, 0, 0, 1u};          // endpoint_key {ip4, pad.., family=1}
+    return ht_find<20>(lxc, kw, key_hash<20>(kw)) >= 0;
+}
+__device__ __forceinline__ bool lxc_has6(const gf_htab_desc &lxc, const uint32_t *d) {
+    uint32_t kw[5] = {d[0], d[1], d[2], d[3], 2u};
+    return ht_find<20>(lxc, kw, key_hash<20>(kw)) >= 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t *verdict,
+                                               unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    if (stats) st.init();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += gridDim.x * blockDim.x) {
+        uint32_t len = c.len[i];
+        uint32_t et = c.ethertype[i];
+        uint8_t v;
+        if (len < 14) v = XDP_DROP_;
+        else if (et == 0x0800) {
+            if (len < 34) v = XDP_DROP_;
+            else {
+                uint32_t sa = c.saddr4[i];
+                bool drop = false;
+                if (x.has_h4) {
+                    if (trie_lookup(x.l4, &sa)) drop = true;
+                    else { uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
+                }
+                v = drop ? XDP_DROP_ : (lxc_has4(x.lxc, c.daddr4[i]) ? XDP_PASS_ : XDP_DROP_);
+            }
+        } else if (et == 0x86DD) {
+            if (len < 54 || !c.saddr6 || !c.daddr6) v = XDP_DROP_;
+            else {
+                uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
+                uint32_t sw[4] = {s.x, s.y, s.z, s.w};
+                bool drop = false;
+                if (x.has_h6) {
+                    if (trie_lookup(x.l6, sw)) drop = true;
+                    else { uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
+                }
+                if (drop) v = XDP_DROP_;
+                else {
+                    uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+                    uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+                    v = lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
+                }
+            }
+        } else v = XDP_PASS_;
+        verdict[i] = v;
+        if (stats) st.add(256 + v);
+    }
+    if (stats) st.flush(stats);
+}
+
+// ================================================================ LB
+struct LbDev {
+    gf_htab_desc s4, s6;
+    uint32_t flags;
+};
+
+__device__ __forceinline__ int lb_checks(const LbDev &L, uint32_t len, int l4_off, uint32_t nh,
+                                         uint32_t key_dport, uint32_t svc_port, bool v6, uint16_t *new_dport) {
+    uint32_t co = csum_l4_offset(nh);
+    if ((co || v6) && !l4csum_ok(l4_off + (int)co, len)) return D_CSUM_L4;
+    if ((L.flags & GF_LB_F_L4) && svc_port && key_dport != svc_port && (nh == 6 || nh == 17)) {
+        if (!l4csum_ok(l4_off + (int)co, len)) return D_CSUM_L4;
+        if (!skb_ok(l4_off + 2, 2, len)) return D_WRITE_ERROR;
+        *new_dport = (uint16_t)svc_port;
+    }
+    return TC_OK;
+}
+
+// returns program result (TC_OK pass / TC_REDIRECT translated / negative error)
+__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o) {
+    if (len < 34) return D_INVALID;
+    uint32_t nh = c.proto[i], daddr = c.daddr4[i];
+    int l4_off = c.l4_off[i];
+    uint32_t dport = 0;
+    if (L.flags & GF_LB_F_L4) {
+        if (nh == 6 || nh == 17) {
+            if (!skb_ok(l4_off + 2, 2, len)) return -GF_EFAULT;
+            dport = c.l4w0[i] >> 16;
+        } else if (nh != 1 && nh != 58) return TC_OK;     // DROP_UNKNOWN_L4 -> pass
+    }
+    const uint8_t *svc = nullptr;
+    if ((L.flags & GF_LB_F_L4) && dport) {
+        uint32_t kw[2] = {daddr, dport};
+        int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
+        if (!svc) dport = 0;
+    }
+    if (!svc && (L.flags & GF_LB_F_L3)) {
+        uint32_t kw[2] = {daddr, dport};
+        int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
+    }
+    if (!svc) return TC_OK;
+    uint32_t count = *reinterpret_cast<const uint16_t *>(svc + 6);
+    uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
+    uint32_t kw[2] = {daddr, dport | (slave << 16)};
+    int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+    if (f < 0) return D_NO_SERVICE;
+    const uint8_t *be = ht_val(L.s4, f);
+    uint32_t target = *reinterpret_cast<const uint32_t *>(be);
+    uint32_t port = *reinterpret_cast<const uint16_t *>(be + 4);
+    uint32_t rn = *reinterpret_cast<const uint16_t *>(be + 8);
+    uint16_t nd = 0;
+    int r = lb_checks(L, len, l4_off, nh, dport, port, false, &nd);
+    if (r < 0) return r;
+    o.slave = (uint16_t)slave; o.new_dport = nd; o.rev_nat = (uint16_t)rn; o.new_daddr4 = target;
+    return TC_REDIRECT;
+}
+
+__device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t *nd6) {
+    if (len < 54 || !c.daddr6) return D_INVALID;
+    uint32_t nh = c.proto[i];
+    int l4_off = c.l4_off[i];
+    uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+    uint32_t dport = 0;
+    if (L.flags & GF_LB_F_L4) {
+        if (nh == 6 || nh == 17) {
+            if (!skb_ok(l4_off + 2, 2, len)) return -GF_EFAULT;
+            dport = c.l4w0[i] >> 16;
+        } else if (nh != 1 && nh != 58) return TC_OK;
+    }
+    const uint8_t *svc = nullptr;
+    if ((L.flags & GF_LB_F_L4) && dport) {
+        uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
+        int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
+        if (!svc) dport = 0;
+    }
+    if (!svc && (L.flags & GF_LB_F_L3)) {
+        uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
+        int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
+    }
+    if (!svc) return TC_OK;
+    uint32_t count = *reinterpret_cast<const uint16_t *>(svc + 18);
+    uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
+    uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport | (slave << 16)};
+    int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+    if (f < 0) return D_NO_SERVICE;
+    const uint8_t *be = ht_val(L.s6, f);
+    uint32_t t[4];
+    for (int k = 0; k < 4; k++) t[k] = *reinterpret_cast<const uint32_t *>(be + 4 * k);
+    uint32_t port = *reinterpret_cast<const uint16_t *>(be + 16);
+    uint32_t rn = *reinterpret_cast<const uint16_t *>(be + 20);
+    if (rn) t[3] |= rn;
+    uint16_t ndp = 0;
+    int r = lb_checks(L, len, l4_off, nh, dport, port, true, &ndp);
+    if (r < 0) return r;
+    o.slave = (uint16_t)slave; o.new_dport = ndp; o.rev_nat = (uint16_t)rn;
+    for (int k = 0; k < 4; k++) nd6[k] = t[k];
+    return TC_REDIRECT;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out *out, uint8_t *nd6,
+                                              unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    if (stats) st.init();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += gridDim.x * blockDim.x) {
+        gf_lb_out o{};
+        uint32_t n6[4] = {0, 0, 0, 0};
+        uint32_t len = c.len[i], et = c.ethertype[i];
+        int ret = TC_OK;
+        bool v6 = false;
+        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ret = lb_v6(L, c, i, len, o, n6); } }
+        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o); }
+        if (ret < 0 || ret == TC_SHOT) {
+            o = gf_lb_out{};
+            o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
+            n6[0] = n6[1] = n6[2] = n6[3] = 0;
+        } else {
+            o.action = ((L.flags & GF_LB_F_REDIRECT) && ret == TC_REDIRECT) ? TC_REDIRECT : TC_OK;
+        }
+        out[i] = o;
+        if (nd6 && v6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
+        else if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(0, 0, 0, 0);
+        if (stats) { st.add(o.reason); st.add(256 + o.action); }
+    }
+    if (stats) st.flush(stats);
+}
+
+// ================================================================ ingress (handle_policy)
+struct IngCtx {
+    const gf_lxc_dev *cfgs;
+    const uint16_t *slot_of;
+    const uint8_t *saddr6, *daddr6;
+    uint32_t now, host_ifindex;
+    uint32_t strict;   // bit0: CT inserts check max_entries with atomics
+};
+
+struct CtState { uint32_t rev_nat, loopback; };
+
+// __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS)
+template <int KSZ>
+__device__ __forceinline__ int ct_probe(const gf_htab_desc &d, const uint32_t *kw, int action, bool syn,
+                                        uint32_t len, uint32_t now, bool acct, CtState &st) {
+    int64_t f = ht_find<KSZ>(d, kw, key_hash<KSZ>(kw));
+    if (f < 0) return CT_NEW;
+    uint8_t *e = ht_val(d, (uint64_t)f);
+    uint4 c = *reinterpret_cast<uint4 *>(e + 32);       // lifetime, flags|rev_nat, unused, src_sec_id
+    uint32_t life = c.x, fl = c.y & 0xffffu, rn = c.y >> 16;
+    if (!(fl & F_RX_CLOSING) || !(fl & F_TX_CLOSING)) {  // ct_entry_alive -> ct_update_timeout
+        if (!syn) fl |= F_SEEN_NON_SYN;
+        life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+    }
+    st.rev_nat = rn;
+    st.loopback = (fl >> 3) & 1u;
+    if (acct) {                                         // rx_packets/rx_bytes (exclusive lane)
+        unsigned long long *rx = reinterpret_cast<unsigned long long *>(e);
+        rx[0] += 1ull;
+        rx[1] += (unsigned long long)len;
+    }
+    if (action == ACT_CREATE) {
+        if (fl & (F_RX_CLOSING | F_TX_CLOSING)) {
+            fl &= ~(F_RX_CLOSING | F_TX_CLOSING);
+            if (!syn) fl |= F_SEEN_NON_SYN;
+            life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+        }
+    } else if (action == ACT_CLOSE) {
+        fl |= F_RX_CLOSING;
+        if ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) life = now + 10u;
+    }
+    c.x = life;
+    c.y = (c.y & 0xffff0000u) | fl;
+    *reinterpret_cast<uint2 *>(e + 32) = make_uint2(c.x, c.y);
+    return CT_ESTABLISHED;
+}
+
+// ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0)
+template <int KSZ, int TW>
+__device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
+                                         uint32_t len, uint32_t now, bool strict, int *added) {
+    constexpr int NHW = TW - 1;                        // word holding nexthdr | flags << 8
+    uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
+    uint32_t fl = (nh == 6) ? 0u : F_SEEN_NON_SYN;      // ct_update_timeout(syn = nexthdr == TCP)
+    uint32_t life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+    uint32_t v[12] = {1u, 0u, len, 0u, 0u, 0u, 0u, 0u, life, fl | (rev_nat << 16), 0u, src_sec};
+    if (ht_upsert<KSZ, 12>(d, t, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+    uint32_t it[TW];
+#pragma unroll
+    for (int k = 0; k < TW; k++) it[k] = t[k];
+    it[NHW - 1] = 0;                                    // sport = dport = 0
+    it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
+    v[9] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
+    if (ht_upsert<KSZ, 12>(d, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+    return 0;
+}
+
+// l4_proxy_lookup (ingress) + BPF_L4_MAP semantics, bpf/lib/l4.h:151-217, common.h:105-127
+__device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh, uint32_t dport) {
+    if (nh != 6 && nh != 17) return 0;
+    uint32_t n = c->n_l4;
+    if (!n) return 0;
+    for (uint32_t k = 0; k < n; k++) {
+        gf_l4_allow_dev a = c->l4[k];
+        if (a.port && a.port == dport) {
+            if (a.nexthdr && a.nexthdr == nh) return a.proxy;   // first match decides
+        }
+    }
+    return 0;
+}
+
+__device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, uint32_t len) {
+    unsigned long long *p = reinterpret_cast<unsigned long long *>(ht_val(d, (uint64_t)f) + 8);
+    atomicAdd(&p[0], 1ull);
+    atomicAdd(&p[1], (unsigned long long)len);
+}
+
+// __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168)
+__device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t identity, uint32_t dport,
+                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr) {
+    if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
+    if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
+    const gf_htab_desc pd = c->policy;
+    int64_t f;
+    if (flags & GF_LXC_F_HAVE_L4_POLICY) {
+        uint32_t kw[2] = {identity, dport | (proto << 16)};
+        f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        if (f >= 0) goto proxy;
+    }
+    {
+        uint32_t kw[2] = {identity, 0u};
+        f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        if (f >= 0) { policy_count(pd, f, len); return TC_OK; }
+    }
+    if (flags & GF_LXC_F_HAVE_L4_POLICY) {
+        uint32_t kw[2] = {0u, dport | (proto << 16)};
+        f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        if (f >= 0) goto proxy;
+    }
+    goto deny;
+proxy: {
+        policy_count(pd, f, len);
+        uint32_t pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
+        if (pp) return (int)pp;
+        return l4_proxy_lookup(c, proto, dport);
+    }
+deny:
+    if (identity < 256) {                               // identity_is_reserved
+        if (v6) { if (trie_lookup(c->cidr6, cidr_addr)) return TC_OK; }
+        else { if (trie_lookup(c->cidr4, cidr_addr)) return TC_OK; }
+    }
+    return D_POLICY;
+}
+
+// __lb{4,6}_rev_nat verdict-affecting checks (lb.h:217-293, 447-512)
+__device__ __forceinline__ int rev_nat_checks(uint32_t len, int l4_off, uint32_t nh, uint32_t nat_port,
+                                              uint32_t l4w0, bool v6) {
+    uint32_t co = csum_l4_offset(nh);
+    if (nat_port) {
+        if (nh == 6 || nh == 17) {
+            if (!skb_ok(l4_off, 2, len)) return -GF_EFAULT;
+            if (nat_port != (l4w0 & 0xffffu)) {
+                if (!l4csum_ok(l4_off + (int)co, len)) return D_CSUM_L4;
+                if (!skb_ok(l4_off, 2, len)) return D_WRITE_ERROR;
+            }
+        } else if (nh != 1 && nh != 58) return D_UNKNOWN_L4;
+    }
+    if (v6) { if (!l4csum_ok(l4_off + (int)co, len)) return D_CSUM_L4; }
+    else if (co && !l4csum_ok(l4_off + (int)co, len)) return D_CSUM_L4;
+    return 0;
+}
+
+// ipv{4,6}_redirect_to_host_port verdict-affecting checks (lib/lxc.h:96-205)
+__device__ __forceinline__ int redirect_checks(uint32_t len, int l4_off, uint32_t nh) {
+    uint32_t co = csum_l4_offset(nh);
+    if (!l4csum_ok(l4_off + (int)co, len)) return D_WRITE_ERROR;
+    if (!skb_ok(l4_off + 2, 2, len)) return D_WRITE_ERROR;
+    return 0;
+}
+
+// ct_lookup4/6 header part: fills tuple port/flag words, returns action or error
+__device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint32_t &pw, uint32_t &tfl,
+                                     int &action, bool &syn) {
+    uint32_t len = r.len;
+    int off = r.l4_off;
+    action = ACT_UNSPEC; syn = false;
+    if ((!v6 && nh == 1) || (v6 && nh == 58)) {
+        if (!skb_ok(off, 1, len)) return D_CT_INVALID_HDR;
+        uint32_t type = r.l4w0 & 0xffu;
+        pw = 0;
+        if (!v6) {
+            if (type == 3 || type == 11 || type == 12) tfl |= 2u;
+            else if (type == 0) pw = 8u;                         // dport = ICMP_ECHO
+            else { if (type == 8) pw = 8u << 16; action = ACT_CREATE; }
+        } else {
+            if (type >= 1 && type <= 4) tfl |= 2u;
+            else if (type == 129) pw = 128u;
+            else { if (type == 128) pw = 128u << 16; action = ACT_CREATE; }
+        }
+        return 0;
+    }
+    if (nh == 6) {
+        if (!skb_ok(off + 12, 2, len)) return D_CT_INVALID_HDR;
+        uint32_t w = r.l4w3;
+        bool fin = (w >> 8) & 1, sy = (w >> 9) & 1, rst = (w >> 10) & 1;
+        action = (rst || fin) ? ACT_CLOSE : ACT_CREATE;
+        syn = sy;
+        if (!skb_ok(off, 4, len)) return D_CT_INVALID_HDR;
+        pw = r.l4w0;
+        return 0;
+    }
+    if (nh == 17) {
+        if (!skb_ok(off, 4, len)) return D_CT_INVALID_HDR;
+        pw = r.l4w0;
+        action = ACT_CREATE;
+        return 0;
+    }
+    return D_CT_UNKNOWN_PROTO;
+}
+
+// ipv4_policy, bpf/bpf_lxc.c:865-970
+__device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, int &fwd,
+                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added) {
+    uint32_t len = r.len;
+    if (len < 34) return D_INVALID;
+    uint32_t nh = r.proto;
+    uint32_t t[4] = {r.daddr, r.saddr, 0u, nh};
+    uint32_t tfl = 0;                                   // TUPLE_F_OUT (ingress)
+    int action; bool syn;
+    int e = ct_l4(nh, false, r, t[2], tfl, action, syn);
+    if (e < 0) return e;
+    t[3] = nh | (tfl << 8);
+    bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
+    const gf_htab_desc ct = c->ct4;
+    CtState st{0, 0};
+    int ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st);
+    if (ret != CT_NEW) {
+        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
+    } else {
+        uint32_t tmp = t[0]; t[0] = t[1]; t[1] = tmp;  // ipv4_ct_tuple_reverse
+        t[2] = (t[2] >> 16) | (t[2] << 16);
+        tfl ^= 1u;
+        t[3] = nh | (tfl << 8);
+        ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st);
+    }
+    fwd = ret;
+    if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
+        const gf_htab_desc rn = c->revnat4;
+        uint32_t kw[1] = {st.rev_nat};
+        int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
+        if (f >= 0) {
+            const uint8_t *nat = ht_val(rn, f);
+            int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 4), r.l4w0, false);
+            if (r2 < 0) return r2;
+            t[1] = *reinterpret_cast<const uint32_t *>(nat);   // tuple->saddr = nat->address
+        }
+    }
+    uint32_t orig_sip = r.saddr;
+    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) ht_delete<14>(ct, t, X.strict & 1, added);
+        return D_POLICY;
+    }
+    if (r.cls & 4) verdict = 0;                         // skip_proxy
+    if (ret == CT_NEW) {
+        ret = ct_create<14, 4>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, added);
+        if (ret < 0) return ret;
+        ofl |= GF_INGRESS_F_CREATED;
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        int r3 = redirect_checks(len, r.l4_off, nh);
+        if (r3 < 0) return r3;
+        ifindex = X.host_ifindex;
+        ofl |= GF_INGRESS_F_PROXY;
+        proxy = (uint16_t)verdict;
+    }
+    return 0;
+}
+
+// ipv6_policy, bpf/bpf_lxc.c:745-862
+__device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, uint32_t i,
+                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added) {
+    uint32_t len = r.len;
+    if (len < 54) return D_INVALID;
+    if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
+    uint32_t nh = r.proto;
+    uint4 d = reinterpret_cast<const uint4 *>(X.daddr6)[i];
+    uint4 s = reinterpret_cast<const uint4 *>(X.saddr6)[i];
+    uint32_t t[10] = {d.x, d.y, d.z, d.w, s.x, s.y, s.z, s.w, 0u, nh};
+    uint32_t co = csum_l4_offset(nh);
+    uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
+    if (rn_new && co && !l4csum_ok(r.l4_off + (int)co, len)) return D_CSUM_L4;
+    uint32_t tfl = 0;
+    int action; bool syn;
+    int e = ct_l4(nh, true, r, t[8], tfl, action, syn);
+    if (e < 0) return e;
+    t[9] = nh | (tfl << 8);
+    bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
+    const gf_htab_desc ct = c->ct6;
+    CtState st{0, 0};
+    int ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st);
+    if (ret != CT_NEW) {
+        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
+    } else {
+        for (int k = 0; k < 4; k++) { uint32_t tmp = t[k]; t[k] = t[4 + k]; t[4 + k] = tmp; }
+        t[8] = (t[8] >> 16) | (t[8] << 16);
+        tfl ^= 1u;
+        t[9] = nh | (tfl << 8);
+        ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st);
+    }
+    fwd = ret;
+    if (st.rev_nat) {
+        const gf_htab_desc rn = c->revnat6;
+        uint32_t kw[1] = {st.rev_nat};
+        int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
+        if (f >= 0) {
+            const uint8_t *nat = ht_val(rn, f);
+            int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 16), r.l4w0, true);
+            if (r2 < 0) return r2;
+        }
+    }
+    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) ht_delete<40>(ct, t, X.strict & 1, added);
+        return D_POLICY;
+    }
+    if (r.cls & 4) verdict = 0;
+    if (ret == CT_NEW) {
+        ret = ct_create<40, 10>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, added);
+        if (ret < 0) return ret;
+        ofl |= GF_INGRESS_F_CREATED;
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        int r3 = redirect_checks(len, r.l4_off, nh);
+        if (r3 < 0) return r3;
+        ifindex = X.host_ifindex;
+        ofl |= GF_INGRESS_F_PROXY;
+        proxy = (uint16_t)verdict;
+    }
+    return 0;
+}
+
+// handle_policy, bpf/bpf_lxc.c:980-1024
+__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, int *added) {
+    gf_ingress_out o{};
+    uint32_t sl = X.slot_of[r.lxc_id];
+    if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }
+    const gf_lxc_dev *c = X.cfgs + (sl - 1);
+    uint32_t flags = c->flags;
+    int fwd = 0, ret;
+    uint8_t fl = 0;
+    uint16_t proxy = 0;
+    uint32_t ifindex = r.ifindex;
+    uint32_t cls = r.cls & 3u;
+    if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
+    else if (cls == 2) ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added);
+    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added);
+    else ret = D_UNKNOWN_L3;
+    o.ct_ret = (uint8_t)fwd;
+    if (ret < 0 || ret == TC_SHOT) {
+        o.action = TC_SHOT; o.reason = (uint8_t)(-ret); o.flags = fl & GF_INGRESS_F_CREATED;
+        return o;
+    }
+    o.flags = fl;
+    o.proxy_port = proxy;
+    o.ifindex_lo = (uint16_t)ifindex;
+    o.action = ifindex ? TC_REDIRECT : TC_OK;
+    return o;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmask, gf_rec *rec, uint32_t *keys,
+                                                    uint32_t *vals, uint32_t *cnt) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c.n) return;
+    gf_rec r;
+    uint32_t et = c.ethertype[i];
+    r.len = c.len[i];
+    r.saddr = c.saddr4[i]; r.daddr = c.daddr4[i];
+    r.l4w0 = c.l4w0[i]; r.l4w3 = c.l4w3[i];
+    r.src_identity = c.src_identity ? c.src_identity[i] : 0u;
+    r.ifindex = c.ifindex ? c.ifindex[i] : 0u;
+    r.lxc_id = c.lxc_id ? c.lxc_id[i] : 0;
+    r.l4_off = c.l4_off[i];
+    r.proto = c.proto[i];
+    uint32_t cls = et == 0x0800 ? 1u : et == 0x86DD ? 2u : 0u;
+    if (c.tc_index && (c.tc_index[i] & 1)) cls |= 4u;
+    r.cls = (uint8_t)cls;
+    uint32_t h;
+    if ((cls & 3) == 2 && c.saddr6) {
+        uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
+        uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+        uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
+        h = gf_pair_hash6(sw, dw);
+    } else {
+        h = gf_pair_hash4(r.saddr, r.daddr);
+    }
+    uint32_t q = h & qmask;
+    rec[i] = r;
+    keys[i] = q;
+    vals[i] = i;
+    atomicAdd(&cnt[q], 1u);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ing_run(IngCtx X, uint32_t nq, const uint32_t *off, const uint32_t *cnt,
+                                                   const uint32_t *perm, const gf_rec *rec, gf_ingress_out *out,
+                                                   uint32_t *ct4_count, uint32_t *ct6_count,
+                                                   unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    if (stats) st.init();
+    uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    int added = 0;
+    if (q < nq) {
+        uint32_t b = off[q], e = b + cnt[q];
+        for (uint32_t j = b; j < e; j++) {
+            uint32_t i = perm[j];
+            gf_rec r = rec[i];
+            gf_ingress_out o = handle_policy(X, r, i, &added);
+            out[i] = o;
+            if (stats) { st.add(o.reason); st.add(256 + o.action); st.add(264 + (o.ct_ret & 3)); }
+        }
+    }
+    // Net CT element-count change (non-strict mode); CT maps of one batch share the
+    // counter of the map the packets used (ct4 for v4, ct6 for v6 are accounted together
+    // when they are the same map; see gf_policy_ingress_classify).
+    if (!(X.strict & 1) && added && ct4_count) atomicAdd(ct4_count, (uint32_t)added);
+    if (stats) st.flush(stats);
+}
+
+// ================================================================ host: programs
+namespace {
+
+struct Workspace {
+    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp;
+};
+Workspace &ws() { static Workspace w; return w; }
+
+int check_cols(const gf_pkt_cols *p) {
+    if (!p) return -EFAULT;
+    if (p->n == 0) return 0;
+    if (!p->len || !p->ethertype || !p->saddr4 || !p->daddr4 || !p->proto || !p->l4_off || !p->l4w0 || !p->l4w3)
+        return -EFAULT;
+    return 1;
+}
+
+uint32_t grid_for(uint32_t n) {
+    uint32_t g = (n + BLOCK - 1) / BLOCK;
+    return g < 1 ? 1 : (g > 65535u * 8 ? 65535u * 8 : g);
+}
+
+int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
+
+}  // namespace
+
+extern "C" {
+
+int gf_parse_frames(const gf_frames *fr, gf_pkt_cols_out *o, void *stream) {
+    if (!fr || !o) return -EFAULT;
+    if (fr->n == 0) return 0;
+    if (!fr->snap || !fr->len || !o->ethertype || !o->saddr4 || !o->daddr4 || !o->proto || !o->l4_off ||
+        !o->l4w0 || !o->l4w3)
+        return -EFAULT;
+    if (fr->snap_stride < 14) return -EINVAL;
+    hipLaunchKernelGGL(k_parse, dim3(grid_for(fr->n)), dim3(BLOCK), 0, (hipStream_t)stream, *fr, *o);
+    return hip_ok(hipGetLastError(), "k_parse");
+}
+
+int gf_xdp_prog_load(const gf_xdp_cfg *cfg) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!cfg) return -EFAULT;
+    auto p = std::make_shared<ProgXdp>();
+    p->cfg = *cfg;
+    auto bind = [](int h, uint32_t ksz, bool lpm, std::shared_ptr<Map> &out) -> int {
+        if (!h) return 0;
+        auto m = get_map(h);
+        if (!m) return -EBADF;
+        if (m->ksz != ksz || m->is_lpm() != lpm) return -EINVAL;
+        out = m;
+        return 0;
+    };
+    int r;
+    if ((r = bind(cfg->cidr4_hmap, 8, false, p->m4h))) return r;
+    if ((r = bind(cfg->cidr4_lmap, 8, true, p->m4l))) return r;
+    if ((r = bind(cfg->cidr6_hmap, 20, false, p->m6h))) return r;
+    if ((r = bind(cfg->cidr6_lmap, 20, true, p->m6l))) return r;
+    if ((r = bind(cfg->lxc_map, 20, false, p->lxc))) return r;
+    if (!p->lxc) return -EINVAL;
+    return new_handle(p);
+}
+
+int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(prog);
+    if (!o || o->kind != ObjKind::ProgXdp) return -EBADF;
+    auto p = std::static_pointer_cast<ProgXdp>(o);
+    int c = check_cols(pkts);
+    if (c <= 0) return c;
+    if (!verdict) return -EFAULT;
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    if ((r = push_map(p->m4h, s)) || (r = push_map(p->m4l, s)) || (r = push_map(p->m6h, s)) ||
+        (r = push_map(p->m6l, s)) || (r = push_map(p->lxc, s)))
+        return r;
+    XdpDev x{};
+    if (p->m4h) { x.h4 = p->m4h->hdesc(); x.has_h4 = 1; }
+    if (p->m6h) { x.h6 = p->m6h->hdesc(); x.has_h6 = 1; }
+    if (p->m4l) x.l4 = p->m4l->tdesc();
+    if (p->m6l) x.l6 = p->m6l->tdesc();
+    x.lxc = p->lxc->hdesc();
+    hipLaunchKernelGGL(k_xdp, dim3(grid_for(pkts->n)), dim3(BLOCK), 0, s, *pkts, x, verdict,
+                       (unsigned long long *)stats_sink());
+    return hip_ok(hipGetLastError(), "k_xdp");
+}
+
+int gf_lb_prog_load(const gf_lb_cfg *cfg) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!cfg) return -EFAULT;
+    auto p = std::make_shared<ProgLb>();
+    p->cfg = *cfg;
+    if (cfg->lb4_services) {
+        p->lb4 = get_map(cfg->lb4_services);
+        if (!p->lb4) return -EBADF;
+        if (p->lb4->ksz != 8 || p->lb4->vsz != 12 || p->lb4->is_lpm()) return -EINVAL;
+    }
+    if (cfg->lb6_services) {
+        p->lb6 = get_map(cfg->lb6_services);
+        if (!p->lb6) return -EBADF;
+        if (p->lb6->ksz != 20 || p->lb6->vsz != 24 || p->lb6->is_lpm()) return -EINVAL;
+    }
+    return new_handle(p);
+}
+
+int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *nd6, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(prog);
+    if (!o || o->kind != ObjKind::ProgLb) return -EBADF;
+    auto p = std::static_pointer_cast<ProgLb>(o);
+    int c = check_cols(pkts);
+    if (c <= 0) return c;
+    if (!out) return -EFAULT;
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    if ((r = push_map(p->lb4, s)) || (r = push_map(p->lb6, s))) return r;
+    LbDev L{};
+    if (p->lb4) L.s4 = p->lb4->hdesc();
+    if (p->lb6) L.s6 = p->lb6->hdesc();
+    L.flags = p->cfg.flags;
+    hipLaunchKernelGGL(k_lb, dim3(grid_for(pkts->n)), dim3(BLOCK), 0, s, *pkts, L, out, nd6,
+                       (unsigned long long *)stats_sink());
+    return hip_ok(hipGetLastError(), "k_lb");
+}
+
+int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!cfg) return -EFAULT;
+    if (cfg->n_l4_ingress > GF_MAX_L4_INGRESS) return -E2BIG;
+    auto p = std::make_shared<ProgLxc>();
+    p->cfg = *cfg;
+    struct B { int h; uint32_t k, v; bool lpm; std::shared_ptr<Map> *out; };
+    B binds[] = {
+        {cfg->policy_map, 8, 24, false, &p->policy}, {cfg->ct_map4, 14, 48, false, &p->ct4},
+        {cfg->ct_map6, 40, 48, false, &p->ct6},      {cfg->cidr4_ingress_map, 8, 0, true, &p->cidr4},
+        {cfg->cidr6_ingress_map, 20, 0, true, &p->cidr6}, {cfg->revnat4_map, 2, 6, false, &p->revnat4},
+        {cfg->revnat6_map, 2, 18, false, &p->revnat6},
+    };
+    for (auto &b : binds) {
+        if (!b.h) continue;
+        auto m = get_map(b.h);
+        if (!m) return -EBADF;
+        if (m->ksz != b.k || m->is_lpm() != b.lpm || (!b.lpm && m->vsz != b.v)) return -EINVAL;
+        *b.out = m;
+    }
+    if (p->ct4) p->ct4->make_fixed_capacity();
+    if (p->ct6) p->ct6->make_fixed_capacity();
+    return new_handle(p);
+}
+
+int gf_policy_array_create(void) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    return new_handle(std::make_shared<PolicyArray>());
+}
+
+int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    if (lxc_id > 0xffff) return -E2BIG;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    if (!prog) { a->slots.erase(lxc_id); a->dirty = true; return 0; }
+    auto po = get_obj(prog);
+    if (!po || po->kind != ObjKind::ProgLxc) return -EINVAL;
+    a->slots[lxc_id] = std::static_pointer_cast<ProgLxc>(po);
+    a->dirty = true;
+    return 0;
+}
+
+int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
+                               void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    int c = check_cols(pkts);
+    if (c <= 0) return c;
+    if (!out) return -EFAULT;
+    if (pkts->n > (1u << 30)) return -E2BIG;
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    // 1. sync tables, build the device program table
+    std::vector<std::shared_ptr<ProgLxc>> progs;
+    std::map<ProgLxc *, uint32_t> index;
+    std::vector<uint16_t> slot_of(65536, 0);
+    bool any_v6 = false;
+    for (auto &kv : a->slots) {
+        auto &p = kv.second;
+        auto it = index.find(p.get());
+        if (it == index.end()) {
+            if (progs.size() >= 65535) return -E2BIG;
+            it = index.emplace(p.get(), (uint32_t)progs.size()).first;
+            progs.push_back(p);
+        }
+        slot_of[kv.first] = (uint16_t)(it->second + 1);
+    }
+    std::vector<gf_lxc_dev> cfgs(progs.size());
+    std::vector<std::shared_ptr<Map>> ctmaps;
+    for (size_t k = 0; k < progs.size(); k++) {
+        auto &p = progs[k];
+        for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6})
+            if ((r = push_map(m, s))) return r;
+        gf_lxc_dev &d = cfgs[k];
+        memset(&d, 0, sizeof d);
+        d.flags = p->cfg.flags; d.lxc_id = p->cfg.lxc_id; d.seclabel = p->cfg.seclabel;
+        d.n_l4 = p->cfg.n_l4_ingress;
+        for (uint32_t j = 0; j < d.n_l4; j++) {
+            d.l4[j].port = p->cfg.l4_ingress[j].port; d.l4[j].proxy = p->cfg.l4_ingress[j].proxy;
+            d.l4[j].nexthdr = p->cfg.l4_ingress[j].nexthdr;
+        }
+        if (p->policy) d.policy = p->policy->hdesc();
+        if (p->ct4) { d.ct4 = p->ct4->hdesc(); ctmaps.push_back(p->ct4); }
+        if (p->ct6) { d.ct6 = p->ct6->hdesc(); ctmaps.push_back(p->ct6); any_v6 = true; }
+        if (p->cidr4) d.cidr4 = p->cidr4->tdesc();
+        if (p->cidr6) d.cidr6 = p->cidr6->tdesc();
+        if (p->revnat4) d.revnat4 = p->revnat4->hdesc();
+        if (p->revnat6) d.revnat6 = p->revnat6->hdesc();
+    }
+    // CT maps: one counter is tracked in non-strict mode, so all programs must share
+    // one CT map per family (the production layout: cilium_ct4_global / ct6_global).
+    std::shared_ptr<Map> ct4m, ct6m;
+    for (auto &p : progs) {
+        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
+        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
+    }
+    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
+    // strict (exact max_entries accounting) only when a batch could fill a CT map
+    uint32_t strict = 0;
+    for (auto &m : {ct4m, ct6m}) {
+        if (!m) continue;
+        uint64_t upper = m->ht.count;  // host view (exact after pull/push)
+        if (!m->host_valid) {
+            uint32_t dc = 0;
+            if (hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count")) return -EIO;
+            upper = dc;
+        }
+        if (upper + 2ull * pkts->n > m->max_entries) strict = 1;
+    }
+    if (a->dirty || a->d_cfgs.bytes != cfgs.size() * sizeof(gf_lxc_dev) || true) {
+        if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
+        if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cfgs.size()) * sizeof(gf_lxc_dev)))) return r;
+        if (hip_ok(hipMemcpy(a->d_slot_of_lxc.p, slot_of.data(), 65536 * 2, hipMemcpyHostToDevice), "slots")) return -EIO;
+        if (!cfgs.empty() &&
+            hip_ok(hipMemcpy(a->d_cfgs.p, cfgs.data(), cfgs.size() * sizeof(gf_lxc_dev), hipMemcpyHostToDevice), "cfgs"))
+            return -EIO;
+        a->dirty = false;
+    }
+    // 2. group by flow group (stable radix sort of (group, index))
+    uint32_t n = pkts->n;
+    uint32_t qbits = 10;
+    while (qbits < 22 && (1u << qbits) * 48u < n) qbits++;
+    uint32_t nq = 1u << qbits;
+    Workspace &w = ws();
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
+        (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
+        (r = grow(w.cnt, (size_t)nq * 4)) || (r = grow(w.off, (size_t)nq * 4)))
+        return r;
+    (void)any_v6;   // IPv6 packets in a batch without v6 columns are dropped (DROP_INVALID)
+    size_t sort_bytes = 0, scan_bytes = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
+                              (uint32_t *)w.perm.p, n, 0, qbits, s);
+    (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
+                            rocprim::plus<uint32_t>(), s);
+    if ((r = grow(w.tmp, std::max(sort_bytes, scan_bytes) + 256))) return r;
+    if (hip_ok(hipMemsetAsync(w.cnt.p, 0, (size_t)nq * 4, s), "memset cnt")) return -EIO;
+    hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, nq - 1,
+                       (gf_rec *)w.rec.p, (uint32_t *)w.keys.p, (uint32_t *)w.vals.p, (uint32_t *)w.cnt.p);
+    if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
+    size_t tb = w.tmp.bytes;
+    if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
+                                         (uint32_t *)w.perm.p, n, 0, qbits, s), "radix_sort_pairs"))
+        return -EIO;
+    tb = w.tmp.bytes;
+    if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
+                                       rocprim::plus<uint32_t>(), s), "exclusive_scan"))
+        return -EIO;
+    // 3. run handle_policy per flow-group queue
+    IngCtx X{};
+    X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
+    X.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
+    X.saddr6 = pkts->saddr6; X.daddr6 = pkts->daddr6;
+    X.now = now_sec; X.host_ifindex = host_ifindex();
+    X.strict = strict;
+    // Non-strict mode accounts the net element change per map; with both families
+    // present each lane's `added` mixes them, so v6 batches use strict mode.
+    if (ct4m && ct6m) X.strict = 1;
+    uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : (ct6m ? (uint32_t *)ct6m->d_count.p : nullptr);
+    hipLaunchKernelGGL(k_ing_run, dim3((nq + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, nq, (const uint32_t *)w.off.p,
+                       (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cnt4,
+                       (uint32_t *)nullptr, (unsigned long long *)stats_sink());
+    if ((r = hip_ok(hipGetLastError(), "k_ing_run"))) return r;
+    for (auto &p : progs) {
+        if (p->policy) p->policy->device_modified();
+    }
+    if (ct4m) ct4m->device_modified();
+    if (ct6m) ct6m->device_modified();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,615 @@
+// gf_maps.cpp — host side of libgpuflow: object registry, the map API that
+// replaces the bpf(2) syscall under pkg/bpf (pkg/bpf/bpf.go:84-274), host
+// shadows of every map, their HBM replicas, and the coverage-trie builder.
+//
+// Kernel semantics restated (Linux 6.x kernel/bpf/hashtab.c, lpm_trie.c; the
+// kernel is not part of /root/reference, see DESIGN.md "Oracle"):
+//   htab: exact match over key_size bytes; update flags ANY/NOEXIST/EXIST
+//         (-EINVAL otherwise, -EEXIST/-ENOENT by flag); a NEW key when
+//         count == max_entries -> -E2BIG (replacing an existing key is fine);
+//         get_next_key: absent/NULL key -> first key, -ENOENT at the end.
+//   trie: prefixlen > max -> -EINVAL; NEW key when full -> -ENOSPC; lookup =
+//         longest stored prefix with len <= key.prefixlen that matches;
+//         get_next_key in post-order (more specific prefixes first).
+//   LRU_HASH is treated as HASH without eviction (parity mode; LRU eviction
+//   order is nondeterministic in the kernel — parity configs never fill).
+#include "gf_internal.h"
+#include <string.h>
+#include <errno.h>
+#include <time.h>
+#include <algorithm>
+#include <deque>
+#include <unordered_map>
+
+namespace gf {
+
+std::recursive_mutex &big_lock() {
+    static std::recursive_mutex m;
+    return m;
+}
+
+int hip_ok(hipError_t e, const char *what) {
+    if (e == hipSuccess) return 0;
+    fprintf(stderr, "gpuflow: %s failed: %s\n", what, hipGetErrorString(e));
+    return -EIO;
+}
+
+DevBuf::~DevBuf() { release(); }
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr; bytes = 0;
+}
+int DevBuf::ensure(size_t n) {
+    if (n == bytes && p) return 0;
+    release();
+    if (n == 0) return 0;
+    if (hip_ok(hipMalloc(&p, n), "hipMalloc")) { p = nullptr; return -ENOMEM; }
+    bytes = n;
+    return 0;
+}
+
+// ------------------------------------------------------------------ HTab
+void HTab::init(uint32_t k, uint32_t v, uint64_t n) {
+    ksz = k; vsz = v;
+    gf_htab_layout(k, v, &slot_size, &voff, &split);
+    nslots = n;
+    slots.assign(nslots * slot_size, 0);
+    if (split) vals.assign(nslots * vsz, 0); else vals.clear();
+    count = 0; tombs = 0;
+}
+
+uint32_t HTab::hash(const uint8_t *key) const {
+    uint32_t w[16] = {0};
+    memcpy(w, key, ksz);
+    return gf_hash_words(w, (int)((ksz + 3) / 4), ksz);
+}
+
+int64_t HTab::find(const uint8_t *key) const {
+    if (!nslots) return -1;
+    uint64_t mask = nslots - 1, i = hash(key) & mask;
+    for (uint64_t p = 0; p < nslots; p++) {
+        uint8_t st = state(i);
+        if (st == GF_SLOT_EMPTY) return -1;
+        if (st == GF_SLOT_FULL && memcmp(this->key(i), key, ksz) == 0) return (int64_t)i;
+        i = (i + 1) & mask;
+    }
+    return -1;
+}
+
+int64_t HTab::insert_new(const uint8_t *key, const uint8_t *value) {
+    uint64_t mask = nslots - 1, i = hash(key) & mask;
+    for (uint64_t p = 0; p < nslots; p++) {
+        uint8_t st = state(i);
+        if (st == GF_SLOT_EMPTY || st == GF_SLOT_TOMB) {
+            if (st == GF_SLOT_TOMB) tombs--;
+            uint8_t *s = &slots[i * slot_size];
+            memset(s, 0, slot_size);
+            memcpy(s, key, ksz);
+            s[ksz] = GF_SLOT_FULL;
+            memcpy(val(i), value, vsz);
+            count++;
+            return (int64_t)i;
+        }
+        i = (i + 1) & mask;
+    }
+    return -1;
+}
+
+void HTab::erase(uint64_t i) {
+    set_state(i, GF_SLOT_TOMB);
+    count--; tombs++;
+}
+
+void HTab::rehash(uint64_t n) {
+    std::vector<uint8_t> os, ov;
+    os.swap(slots); ov.swap(vals);
+    uint64_t on = nslots;
+    uint32_t oss = slot_size;
+    init(ksz, vsz, n);
+    for (uint64_t i = 0; i < on; i++) {
+        if (os[i * oss + ksz] != GF_SLOT_FULL) continue;
+        const uint8_t *v = split ? &ov[i * vsz] : &os[i * oss + voff];
+        insert_new(&os[i * oss], v);
+    }
+}
+
+// ------------------------------------------------------------------ LPM order
+static inline int key_bit(const std::string &k, uint32_t bit) {
+    return (((uint8_t)k[4 + bit / 8]) >> (7 - bit % 8)) & 1;
+}
+bool LpmKeyLess::operator()(const std::string &a, const std::string &b) const {
+    uint32_t la, lb, maxb = data_bytes * 8;
+    memcpy(&la, a.data(), 4); memcpy(&lb, b.data(), 4);
+    if (la > maxb) la = maxb;
+    if (lb > maxb) lb = maxb;
+    uint32_t m = std::min(la, lb);
+    for (uint32_t k = 0; k < m; k++) {
+        int ba = key_bit(a, k), bb = key_bit(b, k);
+        if (ba != bb) return ba < bb;
+    }
+    if (la == lb) return false;
+    return la > lb;   // post-order: the more specific prefix first
+}
+
+// ------------------------------------------------------------------ Map
+Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
+    : Obj(ObjKind::Map), type(t), ksz(k), vsz(v), max_entries(m), flags(f),
+      lpm(LpmKeyLess{k > 4 ? k - 4 : 0}) {
+    if (!is_lpm()) {
+        if (type == GF_MAP_TYPE_LRU_HASH) { fixed_capacity = true; ht.init(k, v, 0); ht.nslots = gf_pow2ceil32(std::max<uint32_t>(64, 2 * m)); }
+        else ht.init(k, v, 64);
+    }
+}
+
+// Fixed-capacity maps are materialized lazily: slots.size()==0 means all-empty.
+static void materialize(HTab &h) {
+    if (h.slots.empty() && h.nslots) {
+        h.slots.assign(h.nslots * h.slot_size, 0);
+        if (h.split) h.vals.assign(h.nslots * h.vsz, 0);
+    }
+}
+
+void Map::make_fixed_capacity() {
+    if (is_lpm() || fixed_capacity) return;
+    pull();
+    uint64_t want = gf_pow2ceil32(std::max<uint32_t>(64, 2 * max_entries));
+    fixed_capacity = true;
+    if (want != ht.nslots) ht.rehash(want);
+    dev_valid = false;
+}
+
+int Map::pull() {
+    if (is_lpm() || host_valid) return 0;
+    materialize(ht);
+    if (hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize")) return -EIO;
+    if (d_slots.p && hip_ok(hipMemcpy(ht.slots.data(), d_slots.p, ht.slots.size(), hipMemcpyDeviceToHost), "pull slots")) return -EIO;
+    if (ht.split && d_vals.p && hip_ok(hipMemcpy(ht.vals.data(), d_vals.p, ht.vals.size(), hipMemcpyDeviceToHost), "pull vals")) return -EIO;
+    // recount (device inserts/deletes)
+    uint64_t c = 0, t = 0;
+    for (uint64_t i = 0; i < ht.nslots; i++) {
+        uint8_t st = ht.state(i);
+        if (st == GF_SLOT_FULL) c++;
+        else if (st == GF_SLOT_TOMB) t++;
+    }
+    ht.count = c; ht.tombs = t;
+    host_valid = true;
+    return 0;
+}
+
+int Map::push(hipStream_t s) {
+    if (is_lpm()) {
+        if (!trie_dirty && d_root.p) return 0;
+        std::vector<uint32_t> root; std::vector<uint8_t> nodes; uint32_t rb = 0;
+        build_trie(*this, root, nodes, rb);
+        int r;
+        if ((r = d_root.ensure(root.size() * 4))) return r;
+        if ((r = d_nodes.ensure(std::max<size_t>(nodes.size(), GF_TRIE_NODE_BYTES)))) return r;
+        if (hip_ok(hipMemcpy(d_root.p, root.data(), root.size() * 4, hipMemcpyHostToDevice), "push trie root")) return -EIO;
+        if (!nodes.empty() && hip_ok(hipMemcpy(d_nodes.p, nodes.data(), nodes.size(), hipMemcpyHostToDevice), "push trie nodes")) return -EIO;
+        trie_root_bits = rb;
+        trie_dirty = false;
+        return 0;
+    }
+    if (dev_valid) return 0;
+    int r;
+    if ((r = d_slots.ensure(ht.nslots * ht.slot_size))) return r;
+    if (ht.split && (r = d_vals.ensure(ht.nslots * ht.vsz))) return r;
+    if ((r = d_count.ensure(8))) return r;
+    if (ht.slots.empty()) {
+        if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
+        if (ht.split && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
+    } else {
+        if (hip_ok(hipMemcpyAsync(d_slots.p, ht.slots.data(), ht.slots.size(), hipMemcpyHostToDevice, s), "push slots")) return -EIO;
+        if (ht.split && hip_ok(hipMemcpyAsync(d_vals.p, ht.vals.data(), ht.vals.size(), hipMemcpyHostToDevice, s), "push vals")) return -EIO;
+    }
+    uint32_t cnt[2] = {(uint32_t)ht.count, 0};
+    if (hip_ok(hipMemcpyAsync(d_count.p, cnt, 8, hipMemcpyHostToDevice, s), "push count")) return -EIO;
+    if (hip_ok(hipStreamSynchronize(s), "push sync")) return -EIO;
+    dev_valid = true;
+    return 0;
+}
+
+gf_htab_desc Map::hdesc() {
+    gf_htab_desc d{};
+    d.slots = (uint8_t *)d_slots.p;
+    d.vals = (uint8_t *)d_vals.p;
+    d.count = (uint32_t *)d_count.p;
+    d.mask = ht.nslots ? ht.nslots - 1 : 0;
+    d.ksz = ksz; d.vsz = vsz; d.slot_size = ht.slot_size; d.voff = ht.voff;
+    d.split = ht.split; d.max_entries = max_entries;
+    return d;
+}
+
+gf_trie_desc Map::tdesc() {
+    gf_trie_desc d{};
+    d.root = (const uint32_t *)d_root.p;
+    d.nodes = (const uint8_t *)d_nodes.p;
+    d.root_bits = lpm.empty() ? 0 : trie_root_bits;
+    d.addr_bytes = ksz - 4;
+    return d;
+}
+
+int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
+    if (fl > GF_EXIST) return -EINVAL;
+    if (is_lpm()) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        if (plen > lpm_bits()) return -EINVAL;
+        std::string k((const char *)key, ksz);
+        auto it = lpm.find(k);
+        if (it != lpm.end()) {
+            if (fl == GF_NOEXIST) return -EEXIST;
+            lpm.erase(it);
+            lpm.emplace(k, std::string((const char *)value, vsz));
+            trie_dirty = true;
+            return 0;
+        }
+        if (fl == GF_EXIST) return -ENOENT;
+        if (lpm.size() >= max_entries) return -ENOSPC;
+        lpm.emplace(k, std::string((const char *)value, vsz));
+        lpm_len_cnt[plen]++;
+        trie_dirty = true;
+        return 0;
+    }
+    int r = pull(); if (r) return r;
+    materialize(ht);
+    int64_t i = ht.find(key);
+    if (i >= 0) {
+        if (fl == GF_NOEXIST) return -EEXIST;
+        memcpy(ht.val((uint64_t)i), value, vsz);
+        dev_valid = false;
+        return 0;
+    }
+    if (fl == GF_EXIST) return -ENOENT;
+    if (ht.count >= max_entries) return -E2BIG;
+    if (fixed_capacity) {
+        if ((ht.count + ht.tombs + 1) * 4 > ht.nslots * 3) ht.rehash(ht.nslots);
+    } else if ((ht.count + ht.tombs + 1) * 2 > ht.nslots) {
+        ht.rehash(std::max<uint64_t>(64, gf_pow2ceil32((uint32_t)((ht.count + 1) * 4))));
+    }
+    if (ht.insert_new(key, value) < 0) return -E2BIG;
+    dev_valid = false;
+    return 0;
+}
+
+int Map::lookup(const uint8_t *key, uint8_t *value) {
+    if (is_lpm()) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        if (plen > lpm_bits()) plen = lpm_bits();
+        std::string probe((const char *)key, ksz);
+        for (int l = (int)plen; l >= 0; l--) {
+            if (!lpm_len_cnt[l]) continue;
+            uint32_t ul = (uint32_t)l;
+            memcpy(&probe[0], &ul, 4);
+            auto it = lpm.find(probe);
+            if (it != lpm.end()) { memcpy(value, it->second.data(), vsz); return 0; }
+        }
+        return -ENOENT;
+    }
+    int r = pull(); if (r) return r;
+    if (ht.slots.empty()) return -ENOENT;
+    int64_t i = ht.find(key);
+    if (i < 0) return -ENOENT;
+    memcpy(value, ht.val((uint64_t)i), vsz);
+    return 0;
+}
+
+int Map::erase(const uint8_t *key) {
+    if (is_lpm()) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        if (plen > lpm_bits()) return -EINVAL;
+        auto it = lpm.find(std::string((const char *)key, ksz));
+        if (it == lpm.end()) return -ENOENT;
+        lpm.erase(it);
+        lpm_len_cnt[plen]--;
+        trie_dirty = true;
+        return 0;
+    }
+    int r = pull(); if (r) return r;
+    if (ht.slots.empty()) return -ENOENT;
+    int64_t i = ht.find(key);
+    if (i < 0) return -ENOENT;
+    ht.erase((uint64_t)i);
+    dev_valid = false;
+    return 0;
+}
+
+int Map::next_key(const uint8_t *key, uint8_t *next) {
+    if (is_lpm()) {
+        if (lpm.empty()) return -ENOENT;
+        auto it = lpm.end();
+        if (key) {
+            uint32_t plen; memcpy(&plen, key, 4);
+            if (plen <= lpm_bits()) {
+                auto f = lpm.find(std::string((const char *)key, ksz));
+                if (f != lpm.end()) { it = f; ++it; if (it == lpm.end()) return -ENOENT;
+                    memcpy(next, it->first.data(), ksz); return 0; }
+            }
+        }
+        memcpy(next, lpm.begin()->first.data(), ksz);
+        return 0;
+    }
+    int r = pull(); if (r) return r;
+    if (ht.slots.empty() || ht.count == 0) return -ENOENT;
+    uint64_t start = 0;
+    if (key) {
+        int64_t i = ht.find(key);
+        if (i >= 0) start = (uint64_t)i + 1;
+    }
+    for (uint64_t i = start; i < ht.nslots; i++)
+        if (ht.state(i) == GF_SLOT_FULL) { memcpy(next, ht.key(i), ksz); return 0; }
+    return -ENOENT;
+}
+
+// ------------------------------------------------------------------ trie build
+struct BNode {
+    uint64_t full[4] = {0, 0, 0, 0};
+    BNode *child[256];
+    BNode() { memset(child, 0, sizeof child); }
+    ~BNode() { for (auto c : child) delete c; }
+};
+
+static inline uint32_t addr_bits(const uint8_t *a, uint32_t from, uint32_t n) {
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < n; k++) v = (v << 1) | ((a[(from + k) / 8] >> (7 - (from + k) % 8)) & 1);
+    return v;
+}
+
+void build_trie(const Map &m, std::vector<uint32_t> &root, std::vector<uint8_t> &nodes, uint32_t &root_bits) {
+    const uint32_t W = m.lpm_bits();
+    const uint32_t R = m.lpm.size() > 256 ? 16 : 8;
+    root_bits = R;
+    std::vector<uint8_t> rfull(1u << R, 0);
+    std::vector<BNode *> rchild(1u << R, nullptr);
+    for (auto &kv : m.lpm) {
+        uint32_t L; memcpy(&L, kv.first.data(), 4);
+        const uint8_t *a = (const uint8_t *)kv.first.data() + 4;
+        if (L <= R) {
+            uint32_t start = L ? addr_bits(a, 0, L) << (R - L) : 0, cnt = 1u << (R - L);
+            for (uint32_t e = start; e < start + cnt; e++) { rfull[e] = 1; delete rchild[e]; rchild[e] = nullptr; }
+            continue;
+        }
+        uint32_t idx = addr_bits(a, 0, R);
+        if (rfull[idx]) continue;
+        if (!rchild[idx]) rchild[idx] = new BNode();
+        BNode *n = rchild[idx];
+        uint32_t d = R;
+        for (;;) {
+            uint32_t b = addr_bits(a, d, 8);
+            if (L <= d + 8) {
+                uint32_t span = 1u << (d + 8 - L), st = b & ~(span - 1);
+                for (uint32_t e = st; e < st + span; e++) {
+                    n->full[e >> 6] |= 1ull << (e & 63);
+                    delete n->child[e]; n->child[e] = nullptr;
+                }
+                break;
+            }
+            if ((n->full[b >> 6] >> (b & 63)) & 1) break;
+            if (!n->child[b]) n->child[b] = new BNode();
+            n = n->child[b];
+            d += 8;
+        }
+        (void)W;
+    }
+    // BFS serialization: children of a node are contiguous, in byte order.
+    root.assign(1u << R, 0);
+    std::vector<BNode *> order;
+    std::deque<BNode *> q;
+    for (uint32_t e = 0; e < (1u << R); e++) {
+        if (rfull[e]) root[e] = GF_TRIE_FULL;
+        else if (rchild[e]) { root[e] = (uint32_t)order.size() + 1; order.push_back(rchild[e]); q.push_back(rchild[e]); }
+    }
+    std::unordered_map<BNode *, uint32_t> base;
+    size_t head = 0;
+    while (head < order.size()) {
+        BNode *n = order[head++];
+        base[n] = (uint32_t)order.size();
+        for (int b = 0; b < 256; b++)
+            if (n->child[b] && !((n->full[b >> 6] >> (b & 63)) & 1)) order.push_back(n->child[b]);
+    }
+    nodes.assign(order.size() * GF_TRIE_NODE_BYTES, 0);
+    for (size_t i = 0; i < order.size(); i++) {
+        BNode *n = order[i];
+        uint8_t *o = &nodes[i * GF_TRIE_NODE_BYTES];
+        uint64_t ch[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 256; b++)
+            if (n->child[b] && !((n->full[b >> 6] >> (b & 63)) & 1)) ch[b >> 6] |= 1ull << (b & 63);
+        memcpy(o, n->full, 32);
+        memcpy(o + 32, ch, 32);
+        uint32_t cb = base[n];
+        memcpy(o + 64, &cb, 4);
+    }
+    for (auto c : rchild) delete c;
+}
+
+// ------------------------------------------------------------------ registry
+struct Registry {
+    std::map<int, std::shared_ptr<Obj>> handles;
+    std::map<std::string, std::shared_ptr<Obj>> pins;
+    int next = 3;      // like fds: 0/1/2 are never handed out
+    uint32_t host_ifindex = 1;
+    uint64_t *stats = nullptr;
+};
+static Registry &reg() { static Registry r; return r; }
+
+std::shared_ptr<Obj> get_obj(int h) {
+    auto &r = reg();
+    auto it = r.handles.find(h);
+    return it == r.handles.end() ? nullptr : it->second;
+}
+std::shared_ptr<Map> get_map(int h) {
+    auto o = get_obj(h);
+    if (!o || o->kind != ObjKind::Map) return nullptr;
+    return std::static_pointer_cast<Map>(o);
+}
+int new_handle(std::shared_ptr<Obj> o) {
+    auto &r = reg();
+    int h = r.next++;
+    r.handles[h] = std::move(o);
+    return h;
+}
+uint32_t host_ifindex() { return reg().host_ifindex; }
+uint64_t *stats_sink() { return reg().stats; }
+
+}  // namespace gf
+
+using namespace gf;
+
+// ================================================================== C ABI
+extern "C" {
+
+int gf_map_create(uint32_t map_type, uint32_t key_size, uint32_t value_size,
+                  uint32_t max_entries, uint32_t map_flags) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!key_size || !value_size || !max_entries) return -EINVAL;
+    switch (map_type) {
+    case GF_MAP_TYPE_HASH:
+    case GF_MAP_TYPE_LRU_HASH:
+        if (map_flags & ~(GF_F_NO_PREALLOC | GF_F_NO_COMMON_LRU)) return -EINVAL;
+        if (key_size > 512) return -E2BIG;
+        if (key_size > 64) return -EINVAL;          /* libgpuflow limit (all path keys <= 40 B) */
+        break;
+    case GF_MAP_TYPE_LPM_TRIE:
+        /* trie_alloc checks (kernel/bpf/lpm_trie.c) */
+        if (!(map_flags & GF_F_NO_PREALLOC) || (map_flags & ~GF_F_NO_PREALLOC)) return -EINVAL;
+        if (key_size < 5 || key_size > 4 + 16) return -EINVAL;  /* libgpuflow: IPv4/IPv6 tries */
+        if (value_size > 4096) return -EINVAL;
+        break;
+    default:
+        return -EINVAL;
+    }
+    auto m = std::make_shared<Map>(map_type, key_size, value_size, max_entries, map_flags);
+    return new_handle(m);
+}
+
+int gf_map_update_elem(int h, const void *key, const void *value, uint64_t flags) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    if (!key || !value) return -EFAULT;
+    return m->update((const uint8_t *)key, (const uint8_t *)value, flags);
+}
+
+int gf_map_update_batch(int h, const void *keys, const void *values, uint32_t n,
+                        uint64_t flags, uint32_t *n_done) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (n_done) *n_done = 0;
+    if (!m) return -EBADF;
+    if (n && (!keys || !values)) return -EFAULT;
+    for (uint32_t i = 0; i < n; i++) {
+        int r = m->update((const uint8_t *)keys + (size_t)i * m->ksz,
+                          (const uint8_t *)values + (size_t)i * m->vsz, flags);
+        if (r) return r;
+        if (n_done) *n_done = i + 1;
+    }
+    return 0;
+}
+
+int gf_map_lookup_elem(int h, const void *key, void *value) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    if (!key || !value) return -EFAULT;
+    return m->lookup((const uint8_t *)key, (uint8_t *)value);
+}
+
+int gf_map_delete_elem(int h, const void *key) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    if (!key) return -EFAULT;
+    return m->erase((const uint8_t *)key);
+}
+
+int gf_map_get_next_key(int h, const void *key, void *next_key) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    if (!next_key) return -EFAULT;
+    return m->next_key((const uint8_t *)key, (uint8_t *)next_key);
+}
+
+int gf_map_get_info(int h, gf_map_info *info) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    if (!info) return -EFAULT;
+    m->pull();
+    info->map_type = m->type; info->key_size = m->ksz; info->value_size = m->vsz;
+    info->max_entries = m->max_entries; info->map_flags = m->flags;
+    info->n_entries = m->n_entries();
+    info->device_bytes = m->device_bytes();
+    return 0;
+}
+
+int gf_obj_pin(int h, const char *path) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(h);
+    if (!o) return -EBADF;
+    if (!path || !*path) return -EINVAL;
+    auto &r = reg();
+    if (r.pins.count(path)) return -EEXIST;
+    r.pins[path] = o;
+    return 0;
+}
+
+int gf_obj_get(const char *path) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!path) return -EFAULT;
+    auto &r = reg();
+    auto it = r.pins.find(path);
+    if (it == r.pins.end()) return -ENOENT;
+    return new_handle(it->second);
+}
+
+int gf_obj_unpin(const char *path) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!path) return -EFAULT;
+    return reg().pins.erase(path) ? 0 : -ENOENT;
+}
+
+int gf_obj_close(int h) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    return reg().handles.erase(h) ? 0 : -EBADF;
+}
+
+uint32_t gf_now_sec(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint32_t)((uint64_t)ts.tv_sec + (uint64_t)ts.tv_nsec / 1000000000ull);
+}
+
+int gf_node_config(const gf_node_cfg *cfg) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!cfg) return -EFAULT;
+    reg().host_ifindex = cfg->host_ifindex;
+    return 0;
+}
+
+int gf_set_stats_sink(uint64_t *dev_counters) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    reg().stats = dev_counters;
+    return 0;
+}
+
+void *gf_dev_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    return p;
+}
+int gf_dev_free(void *p) { return hip_ok(hipFree(p), "hipFree"); }
+int gf_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+    return hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream), "h2d");
+}
+int gf_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+    return hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream), "d2h");
+}
+int gf_stream_sync(void *stream) { return hip_ok(hipStreamSynchronize((hipStream_t)stream), "sync"); }
+int gf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+const char *gf_version(void) { return "gpuflow 0.1 (gfx950)"; }
+
+}  // extern "C"

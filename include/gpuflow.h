@@ -1,0 +1,303 @@
+/*
+ * gpuflow.h — C ABI of libgpuflow, the MI355X-native replacement for the
+ * kernel side of Cilium's BPF map syscalls and its per-packet verdict
+ * programs (reference: carlanton/cilium 1.0.0-rc9, /root/reference).
+ *
+ * Plain C: pointers, sizes and integer handles only.  Every entry point
+ * returns 0 / a positive handle on success and -errno on failure, the way
+ * the bpf(2) syscall wrappers in pkg/bpf/bpf.go see the kernel.
+ *
+ * Two groups of entry points:
+ *
+ *  1. Map API (drop-in for pkg/bpf/bpf.go) — host shadow + HBM replica.
+ *     gf_map_create        <- bpf.CreateMap        pkg/bpf/bpf.go:84-112
+ *     gf_map_update_elem   <- bpf.UpdateElement    pkg/bpf/bpf.go:129-149
+ *     gf_map_lookup_elem   <- bpf.LookupElement    pkg/bpf/bpf.go:153-172
+ *     gf_map_delete_elem   <- bpf.DeleteElement    pkg/bpf/bpf.go:175-192
+ *     gf_map_get_next_key  <- bpf.GetNextKey       pkg/bpf/bpf.go:195-213
+ *     gf_obj_pin           <- bpf.ObjPin           pkg/bpf/bpf.go:224-243
+ *     gf_obj_get           <- bpf.ObjGet           pkg/bpf/bpf.go:246-266
+ *     gf_obj_close         <- bpf.ObjClose         pkg/bpf/bpf.go:269-274
+ *     gf_map_get_info      <- bpf.GetMapInfo       pkg/bpf/map.go:171-209 (fdinfo parse)
+ *     gf_now_sec           <- bpf.GetMtime()/1e9   pkg/bpf/bpf.go:426-435, bpf/lib/utils.h:58-64
+ *
+ *  2. Program API (replaces the BPF programs of the hot path).  A "program"
+ *     binds map handles the way the compile-time #defines of the generated
+ *     headers do (pkg/endpoint/bpf.go:156-330, bpf/filter_config.h,
+ *     bpf/lxc_config.h, bpf/netdev_config.h); a classify call runs the
+ *     program over one batch of packets that is resident in HBM.
+ *     gf_xdp_classify            <- xdp_start/check_filters   bpf/bpf_xdp.c:88-184
+ *     gf_lb_classify             <- from_netdev (bpf_lb)      bpf/bpf_lb.c:58-212
+ *     gf_policy_ingress_classify <- handle_policy/ipv{4,6}_policy bpf/bpf_lxc.c:745-1024
+ *     gf_parse_frames            <- the skb_load_bytes()/revalidate_data() header
+ *                                   accesses of those programs (bpf/lib/common.h:67-87,
+ *                                   bpf/lib/ipv4.h:45-48, bpf/lib/ipv6.h:61-98)
+ *
+ * Host/device contract: map updates go to the host shadow and are pushed to
+ * the HBM replica at the next classify call (batch boundary; a documented
+ * relaxation of the kernel's per-element RCU visibility).  Maps the
+ * datapath writes (CT entries, policy counters) are device-authoritative:
+ * the next host-side access pulls the HBM copy back first.
+ *
+ * All batch/column/output pointers passed to classify calls are DEVICE
+ * pointers (hipMalloc / torch CUDA tensors).  `stream` is a hipStream_t
+ * (NULL = default stream).  Classify calls are asynchronous w.r.t. the host
+ * except for the table sync they may perform before launching.
+ */
+#ifndef GPUFLOW_H
+#define GPUFLOW_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- map types (enum bpf_map_type subset, pkg/bpf/bpf.go:38-52) ---- */
+#define GF_MAP_TYPE_HASH      1
+#define GF_MAP_TYPE_ARRAY     2
+#define GF_MAP_TYPE_PROG_ARRAY 3
+#define GF_MAP_TYPE_LRU_HASH  9
+#define GF_MAP_TYPE_LPM_TRIE  11
+
+/* update flags (pkg/bpf/bpf.go:73-75) */
+#define GF_ANY     0
+#define GF_NOEXIST 1
+#define GF_EXIST   2
+
+/* map flags (pkg/bpf/bpf.go:77-78) */
+#define GF_F_NO_PREALLOC   (1u << 0)
+#define GF_F_NO_COMMON_LRU (1u << 1)
+
+/* ---- return codes of the datapath (bpf/include/bpf/api.h:17-25,
+ *      bpf/include/linux/bpf.h:622-624) ---- */
+#define GF_TC_ACT_OK        0
+#define GF_TC_ACT_SHOT      2
+#define GF_TC_ACT_REDIRECT  7
+#define GF_XDP_DROP         1
+#define GF_XDP_PASS         2
+
+/* CT lookup results (bpf/lib/common.h:310-315) */
+#define GF_CT_NEW         0
+#define GF_CT_ESTABLISHED 1
+#define GF_CT_REPLY       2
+#define GF_CT_RELATED     3
+
+/* drop reasons are reported as u8 = -DROP_* (bpf/lib/common.h:224-256) */
+#define GF_DROP_INVALID            134
+#define GF_DROP_POLICY             133
+#define GF_DROP_CT_INVALID_HDR     135
+#define GF_DROP_CT_UNKNOWN_PROTO   137
+#define GF_DROP_UNKNOWN_L3         139
+#define GF_DROP_MISSED_TAIL_CALL   140
+#define GF_DROP_WRITE_ERROR        141
+#define GF_DROP_UNKNOWN_L4         142
+#define GF_DROP_CSUM_L3            153
+#define GF_DROP_CSUM_L4            154
+#define GF_DROP_CT_CREATE_FAILED   155
+#define GF_DROP_INVALID_EXTHDR     156
+#define GF_DROP_FRAG_NOSUPPORT     157
+#define GF_DROP_NO_SERVICE         158
+#define GF_DROP_POLICY_L4          159
+
+/* ======================= 1. Map API ======================= */
+
+/* bpf.CreateMap: returns handle > 0 or -errno.  key/value sizes are the
+ * byte sizes of the reference C structs (bpf/lib/common.h). */
+int gf_map_create(uint32_t map_type, uint32_t key_size, uint32_t value_size,
+                  uint32_t max_entries, uint32_t map_flags);
+/* bpf.UpdateElement: flags GF_ANY/GF_NOEXIST/GF_EXIST.  -E2BIG when a
+ * hash map is full, -ENOSPC for a full LPM trie, -EEXIST/-ENOENT under
+ * NOEXIST/EXIST, -EINVAL for bad flags or an LPM prefixlen > max. */
+int gf_map_update_elem(int map, const void *key, const void *value, uint64_t flags);
+/* bpf.LookupElement: copies the value; -ENOENT if absent.  LPM tries use
+ * longest-prefix semantics on key->prefixlen (kernel trie_lookup_elem). */
+int gf_map_lookup_elem(int map, const void *key, void *value);
+/* bpf.DeleteElement: -ENOENT if absent. */
+int gf_map_delete_elem(int map, const void *key);
+/* bpf.GetNextKey: key == NULL or an absent key -> first key; -ENOENT at end. */
+int gf_map_get_next_key(int map, const void *key, void *next_key);
+/* Batched update (same semantics as n sequential gf_map_update_elem calls;
+ * stops at the first error and returns it, *n_done = entries applied). */
+int gf_map_update_batch(int map, const void *keys, const void *values,
+                        uint32_t n, uint64_t flags, uint32_t *n_done);
+
+typedef struct gf_map_info {
+    uint32_t map_type, key_size, value_size, max_entries, map_flags;
+    uint32_t n_entries;        /* current element count */
+    uint64_t device_bytes;     /* HBM bytes of the replica (0 if never synced) */
+} gf_map_info;
+int gf_map_get_info(int map, gf_map_info *info);
+
+/* bpf.ObjPin / ObjGet / ObjClose.  Pin paths are names in a process-wide
+ * registry that stands in for /sys/fs/bpf (pkg/bpf/bpffs.go:35-38). */
+int gf_obj_pin(int handle, const char *path);
+int gf_obj_get(const char *path);          /* new handle referring to the object */
+int gf_obj_close(int handle);
+int gf_obj_unpin(const char *path);        /* os.Remove(path) of a pinned map */
+
+/* CLOCK_MONOTONIC seconds, the clock bpf_ktime_get_sec() reads. */
+uint32_t gf_now_sec(void);
+
+/* ======================= 2. Programs ======================= */
+
+/* Parsed header columns.  One element per packet; all DEVICE pointers.
+ * Produced from raw frames by gf_parse_frames (or by a NIC/ingest stage
+ * with the same rules).  "be16"/"be32" fields hold the raw network-order
+ * bytes of the frame loaded little-endian, exactly what the BPF programs
+ * hold in their registers after skb_load_bytes(). */
+typedef struct gf_pkt_cols {
+    uint32_t n;
+    const uint32_t *len;        /* skb->len (linear == data_end - data) */
+    const uint16_t *ethertype;  /* host order: 0x0800 / 0x86DD / other; 0 if len < 14 */
+    const uint32_t *saddr4;     /* iphdr.saddr (raw be32), v4 only */
+    const uint32_t *daddr4;     /* iphdr.daddr (raw be32), v4 only */
+    const uint8_t  *proto;      /* v4: protocol; v6: nexthdr after ipv6_hdrlen() (unchanged on error) */
+    const int16_t  *l4_off;     /* v4: 14 + ihl*4; v6: 14 + ipv6_hdrlen() (negative DROP_* on error) */
+    const uint32_t *l4w0;       /* frame bytes [l4_off, l4_off+4) (0-filled past len) */
+    const uint16_t *l4w3;       /* frame bytes [l4_off+12, l4_off+14) (TCP flags word) */
+    const uint8_t  *saddr6;     /* 16 B per packet, v6 (may be NULL if no IPv6 in batch) */
+    const uint8_t  *daddr6;     /* 16 B per packet, v6 */
+    /* skb metadata the calling programs provide */
+    const uint32_t *src_identity; /* cb[CB_SRC_LABEL] (bpf/lib/l3.h:160) */
+    const uint32_t *ifindex;      /* cb[CB_IFINDEX]  (bpf/lib/l3.h:161) */
+    const uint16_t *lxc_id;       /* tail-call slot into cilium_policy (bpf/lib/l3.h:163) */
+    const uint8_t  *tc_index;     /* skb->tc_index (TC_INDEX_F_SKIP_PROXY = bit 0) */
+    const uint32_t *flow_hash;    /* get_hash_recalc(skb) (bpf/lib/lb.h:109-121) */
+} gf_pkt_cols;
+
+/* Raw frames: snap_stride bytes per packet starting at the Ethernet header. */
+typedef struct gf_frames {
+    uint32_t n;
+    uint32_t snap_stride;       /* >= all header bytes the programs read */
+    const uint8_t  *snap;       /* n * snap_stride bytes */
+    const uint32_t *len;        /* wire length of each frame */
+} gf_frames;
+
+/* Writable column storage for gf_parse_frames (DEVICE pointers, n elements;
+ * saddr6/daddr6 16*n bytes, may be NULL to skip IPv6 address extraction). */
+typedef struct gf_pkt_cols_out {
+    uint16_t *ethertype; uint32_t *saddr4; uint32_t *daddr4; uint8_t *proto;
+    int16_t *l4_off; uint32_t *l4w0; uint16_t *l4w3; uint8_t *saddr6; uint8_t *daddr6;
+} gf_pkt_cols_out;
+int gf_parse_frames(const gf_frames *frames, gf_pkt_cols_out *out, void *stream);
+
+/* ---- XDP prefilter (bpf/bpf_xdp.c, bpf/filter_config.h) ----
+ * A zero handle means the corresponding #define is absent. */
+typedef struct gf_xdp_cfg {
+    int cidr4_hmap;   /* CIDR4_FILTER + CIDR4_HMAP_NAME (v4_fix, HASH, key lpm_v4_key) */
+    int cidr4_lmap;   /* CIDR4_LPM_PREFILTER + CIDR4_LMAP_NAME (v4_dyn, LPM_TRIE) */
+    int cidr6_hmap;   /* CIDR6_FILTER + v6_fix */
+    int cidr6_lmap;   /* CIDR6_LPM_PREFILTER + v6_dyn */
+    int lxc_map;      /* cilium_lxc (bpf/lib/maps.h:27-33) */
+} gf_xdp_cfg;
+int gf_xdp_prog_load(const gf_xdp_cfg *cfg);
+/* verdict[i] = GF_XDP_DROP / GF_XDP_PASS. */
+int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *stream);
+
+/* ---- standalone LB (bpf/bpf_lb.c, bpf/netdev_config.h) ---- */
+#define GF_LB_F_L3       (1u << 0)   /* LB_L3 */
+#define GF_LB_F_L4       (1u << 1)   /* LB_L4 */
+#define GF_LB_F_REDIRECT (1u << 2)   /* LB_REDIRECT defined */
+#define GF_LB_F_NO_IPV4  (1u << 3)   /* LB_DISABLE_IPV4 */
+#define GF_LB_F_NO_IPV6  (1u << 4)   /* LB_DISABLE_IPV6 */
+typedef struct gf_lb_cfg {
+    int lb4_services;  /* cilium_lb4_services (key lb4_key 8 B, value lb4_service 12 B) */
+    int lb6_services;  /* cilium_lb6_services (key lb6_key 20 B, value lb6_service 24 B) */
+    uint32_t flags;
+    uint32_t redirect_ifindex; /* LB_REDIRECT */
+} gf_lb_cfg;
+int gf_lb_prog_load(const gf_lb_cfg *cfg);
+/* Output record per packet (12 B). */
+typedef struct gf_lb_out {
+    uint8_t  action;     /* GF_TC_ACT_OK / SHOT / REDIRECT */
+    uint8_t  reason;     /* -DROP_* (or errno for helper failures) when SHOT, else 0 */
+    uint16_t slave;      /* selected slave index (0 = not load balanced) */
+    uint16_t new_dport;  /* raw be16 destination port after lb*_xlate */
+    uint16_t rev_nat;    /* slave's rev_nat_index (raw) */
+    uint32_t new_daddr4; /* raw be32 (v4) */
+} gf_lb_out;
+/* new_daddr6 (16 B per packet, may be NULL) receives the v6 translated address. */
+int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out,
+                   uint8_t *new_daddr6, void *stream);
+
+/* ---- endpoint ingress policy (bpf/bpf_lxc.c handle_policy) ---- */
+#define GF_LXC_F_DROP_ALL        (1u << 0)  /* DROP_ALL */
+#define GF_LXC_F_POLICY_INGRESS  (1u << 1)  /* POLICY_INGRESS */
+#define GF_LXC_F_HAVE_L4_POLICY  (1u << 2)  /* HAVE_L4_POLICY */
+#define GF_LXC_F_CT_ACCOUNTING   (1u << 3)  /* CONNTRACK_ACCOUNTING */
+#define GF_LXC_F_LXC_IPV4        (1u << 4)  /* LXC_IPV4 */
+#define GF_MAX_L4_INGRESS 64
+typedef struct gf_l4_allow {   /* struct l4_allow, bpf/lib/l4.h:126-136 */
+    uint16_t port;             /* raw be16 */
+    uint16_t proxy;            /* raw be16 */
+    uint8_t  nexthdr;
+    uint8_t  pad[3];
+} gf_l4_allow;
+typedef struct gf_lxc_cfg {
+    uint32_t lxc_id;           /* LXC_ID */
+    uint32_t seclabel;         /* SECLABEL */
+    int policy_map;            /* POLICY_MAP (key policy_key 8 B, value policy_entry 24 B) */
+    int ct_map4;               /* CT_MAP4 (key ipv4_ct_tuple 14 B, value ct_entry 48 B) */
+    int ct_map6;               /* CT_MAP6 (key ipv6_ct_tuple 40 B, value ct_entry 48 B) */
+    int cidr4_ingress_map;     /* CIDR4_INGRESS_MAP (LPM_TRIE), 0 = undefined */
+    int cidr6_ingress_map;     /* CIDR6_INGRESS_MAP (LPM_TRIE), 0 = undefined */
+    int revnat4_map;           /* cilium_lb4_reverse_nat (key u16, value 6 B) */
+    int revnat6_map;           /* cilium_lb6_reverse_nat (key u16, value 18 B) */
+    uint32_t flags;            /* GF_LXC_F_* */
+    uint32_t n_l4_ingress;     /* CFG_L3L4_INGRESS entries */
+    gf_l4_allow l4_ingress[GF_MAX_L4_INGRESS];
+} gf_lxc_cfg;
+int gf_lxc_prog_load(const gf_lxc_cfg *cfg);
+
+/* The cilium_policy prog array (bpf/lib/maps.h:36-43): slot lxc_id -> program. */
+int gf_policy_array_create(void);
+int gf_policy_array_update(int array, uint32_t lxc_id, int prog);  /* prog 0 = delete */
+
+typedef struct gf_node_cfg {   /* node_config.h values used on the path */
+    uint32_t host_ifindex;     /* HOST_IFINDEX */
+} gf_node_cfg;
+int gf_node_config(const gf_node_cfg *cfg);
+
+/* Output record per packet (8 B). */
+typedef struct gf_ingress_out {
+    uint8_t  action;      /* TC_ACT_OK / SHOT / REDIRECT (handle_policy return) */
+    uint8_t  reason;      /* cb[2] = -ret when SHOT (bpf/lib/drop.h:92-107) */
+    uint8_t  ct_ret;      /* forwarding_reason: CT_NEW/ESTABLISHED/REPLY/RELATED */
+    uint8_t  flags;       /* bit0: redirected to proxy, bit1: CT entry created */
+    uint16_t proxy_port;  /* raw be16 policy verdict > 0 */
+    uint16_t ifindex_lo;  /* low 16 bits of the redirect ifindex */
+} gf_ingress_out;
+#define GF_INGRESS_F_PROXY    1
+#define GF_INGRESS_F_CREATED  2
+
+/* Runs handle_policy over the batch, in batch order per flow group
+ * (unordered address pair): packets of one group see each other's CT
+ * updates in batch order, as on one CPU of the reference.  now_sec
+ * replaces bpf_ktime_get_sec() for the whole batch. */
+int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
+                               uint32_t now_sec, gf_ingress_out *out, void *stream);
+
+/* ---- per-call statistics (device counter block) ---- */
+#define GF_STATS_WORDS 512
+/* Adds the counters of the next classify calls into `dev_counters`
+ * (GF_STATS_WORDS u64 in DEVICE memory; NULL disables). Layout:
+ * [0..255] drop-reason histogram, [256..263] action counts,
+ * [264..267] CT ret counts, [268] packets, [269] bytes. */
+int gf_set_stats_sink(uint64_t *dev_counters);
+
+/* ---- device memory helpers for hosts without a GPU runtime binding ---- */
+void *gf_dev_alloc(size_t bytes);
+int   gf_dev_free(void *p);
+int   gf_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int   gf_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int   gf_stream_sync(void *stream);
+/* Number of visible GPUs; a library built without a device returns 0. */
+int   gf_device_count(void);
+const char *gf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUFLOW_H */

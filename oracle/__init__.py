@@ -1,0 +1,5 @@
+"""CPU restatement of the reference verdict path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this package, and only as the checker / CPU baseline.
+"""

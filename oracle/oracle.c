@@ -1,0 +1,1167 @@
+/*
+ * oracle.c — CPU restatement of the Cilium 1.0.0-rc9 verdict path.
+ * TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline), see oracle.h.
+ *
+ * Byte layouts (little-endian host, as the BPF programs see them):
+ *   struct ipv4_ct_tuple  14 B packed  bpf/lib/common.h:338-346
+ *   struct ipv6_ct_tuple  40 B         bpf/lib/common.h:317-325
+ *   struct ct_entry       48 B         bpf/lib/common.h:359-374
+ *   struct policy_key      8 B         bpf/lib/common.h:184-190
+ *   struct policy_entry   24 B         bpf/lib/common.h:192-197
+ *   struct lb4_key/lb4_service/lb4_reverse_nat 8/12/6 B  common.h:395-412
+ *   struct lb6_key/lb6_service/lb6_reverse_nat 20/24/18 B common.h:376-393
+ *   struct endpoint_key   20 B packed  common.h:150-163
+ *   struct endpoint_info 112 B         common.h:168-177
+ *   struct lpm_v4_key / lpm_v6_key 8/20 B  bpf/lib/xdp.h:23-31
+ */
+#include "oracle.h"
+#include <stdlib.h>
+#include <string.h>
+#include <errno.h>
+#include <pthread.h>
+
+/* ------------------------------------------------------------------ */
+/* kernel-side constants                                               */
+/* ------------------------------------------------------------------ */
+#define ETH_HLEN 14
+#define IPPROTO_ICMP 1
+#define IPPROTO_TCP 6
+#define IPPROTO_UDP 17
+#define IPPROTO_ICMPV6 58
+
+#define TC_ACT_OK 0
+#define TC_ACT_SHOT 2
+#define TC_ACT_REDIRECT 7
+#define XDP_DROP 1
+#define XDP_PASS 2
+
+#define DROP_POLICY -133
+#define DROP_INVALID -134
+#define DROP_CT_INVALID_HDR -135
+#define DROP_CT_UNKNOWN_PROTO -137
+#define DROP_UNKNOWN_L3 -139
+#define DROP_MISSED_TAIL_CALL -140
+#define DROP_WRITE_ERROR -141
+#define DROP_UNKNOWN_L4 -142
+#define DROP_CSUM_L3 -153
+#define DROP_CSUM_L4 -154
+#define DROP_CT_CREATE_FAILED -155
+#define DROP_INVALID_EXTHDR -156
+#define DROP_FRAG_NOSUPPORT -157
+#define DROP_NO_SERVICE -158
+#define DROP_POLICY_L4 -159
+#define DROP_PROXYMAP_CREATE_FAILED -161
+
+#define CT_EGRESS 0
+#define CT_INGRESS 1
+#define CT_NEW 0
+#define CT_ESTABLISHED 1
+#define CT_REPLY 2
+#define CT_RELATED 3
+#define TUPLE_F_OUT 0
+#define TUPLE_F_IN 1
+#define TUPLE_F_RELATED 2
+#define ACTION_UNSPEC 0
+#define ACTION_CREATE 1
+#define ACTION_CLOSE 2
+#define CT_DEFAULT_LIFETIME 43200
+#define CT_SYN_TIMEOUT 300
+#define CT_CLOSE_TIMEOUT 10
+
+/* include/gpuflow.h flag values (kept in sync by tests) */
+#define LB_F_L3 (1u << 0)
+#define LB_F_L4 (1u << 1)
+#define LB_F_REDIRECT (1u << 2)
+#define LB_F_NO_IPV4 (1u << 3)
+#define LB_F_NO_IPV6 (1u << 4)
+#define LXC_F_DROP_ALL (1u << 0)
+#define LXC_F_POLICY_INGRESS (1u << 1)
+#define LXC_F_HAVE_L4_POLICY (1u << 2)
+#define LXC_F_CT_ACCOUNTING (1u << 3)
+#define LXC_F_LXC_IPV4 (1u << 4)
+
+/* IS_ERR, bpf/lib/common.h:221 */
+#define IS_ERR(x) (((x) < 0) || ((x) == TC_ACT_SHOT))
+
+/* ------------------------------------------------------------------ */
+/* maps: exact-match hash (kernel htab) and LPM trie                   */
+/* ------------------------------------------------------------------ */
+typedef struct om_shard {
+    uint8_t *keys, *vals, *state;   /* state: 0 empty, 1 full, 2 deleted */
+    uint64_t cap, used, tomb;
+    pthread_mutex_t mu;
+} om_shard;
+
+struct om_map {
+    uint32_t type, ksz, vsz, max_entries, nshards;
+    uint32_t count;                 /* total elements (atomic across shards) */
+    uint8_t lens_present[129];      /* LPM: prefix lengths present (count) */
+    uint32_t lens_cnt[129];
+    om_shard *sh;
+};
+
+static uint64_t fnv1a(const uint8_t *p, uint32_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+    return h ^ (h >> 29);
+}
+
+static int is_lpm(const om_map *m) { return m->type == OM_LPM_TRIE; }
+static uint32_t lpm_bits(const om_map *m) { return (m->ksz - 4) * 8; }
+
+/* LPM keys are stored normalized: data bits beyond prefixlen cleared. */
+static void lpm_normalize(const om_map *m, const uint8_t *key, uint8_t *out) {
+    uint32_t plen; memcpy(&plen, key, 4);
+    memcpy(out, key, m->ksz);
+    uint32_t nbytes = m->ksz - 4;
+    for (uint32_t i = 0; i < nbytes; i++) {
+        int keep = (int)plen - (int)(i * 8);
+        uint8_t mask = keep >= 8 ? 0xff : keep <= 0 ? 0 : (uint8_t)(0xff << (8 - keep));
+        out[4 + i] &= mask;
+    }
+}
+
+static uint32_t shard_of(const om_map *m, const uint8_t *key);
+
+om_map *om_create(uint32_t type, uint32_t key_size, uint32_t value_size,
+                  uint32_t max_entries, uint32_t shards) {
+    if (!key_size || !value_size || !max_entries) return NULL;
+    if (type == OM_LPM_TRIE && (key_size < 5 || key_size > 4 + 16)) return NULL;
+    om_map *m = (om_map *)calloc(1, sizeof(*m));
+    m->type = type; m->ksz = key_size; m->vsz = value_size; m->max_entries = max_entries;
+    m->nshards = shards ? shards : 1;
+    m->sh = (om_shard *)calloc(m->nshards, sizeof(om_shard));
+    for (uint32_t s = 0; s < m->nshards; s++) {
+        om_shard *h = &m->sh[s];
+        h->cap = 64;
+        h->keys = (uint8_t *)calloc(h->cap, key_size);
+        h->vals = (uint8_t *)calloc(h->cap, value_size);
+        h->state = (uint8_t *)calloc(h->cap, 1);
+        pthread_mutex_init(&h->mu, NULL);
+    }
+    return m;
+}
+
+void om_destroy(om_map *m) {
+    if (!m) return;
+    for (uint32_t s = 0; s < m->nshards; s++) {
+        free(m->sh[s].keys); free(m->sh[s].vals); free(m->sh[s].state);
+        pthread_mutex_destroy(&m->sh[s].mu);
+    }
+    free(m->sh); free(m);
+}
+
+static int64_t sh_find(const om_map *m, const om_shard *h, const uint8_t *key) {
+    uint64_t mask = h->cap - 1, i = fnv1a(key, m->ksz) & mask;
+    for (;;) {
+        uint8_t st = h->state[i];
+        if (st == 0) return -1;
+        if (st == 1 && memcmp(h->keys + i * m->ksz, key, m->ksz) == 0) return (int64_t)i;
+        i = (i + 1) & mask;
+    }
+}
+
+static void sh_grow(const om_map *m, om_shard *h) {
+    uint64_t ncap = h->cap;
+    while ((h->used + 1) * 2 > ncap) ncap *= 2;
+    uint8_t *ok = h->keys, *ov = h->vals, *os = h->state; uint64_t ocap = h->cap;
+    h->cap = ncap;
+    h->keys = (uint8_t *)calloc(ncap, m->ksz);
+    h->vals = (uint8_t *)calloc(ncap, m->vsz);
+    h->state = (uint8_t *)calloc(ncap, 1);
+    h->tomb = 0;
+    for (uint64_t j = 0; j < ocap; j++) {
+        if (os[j] != 1) continue;
+        uint64_t i = fnv1a(ok + j * m->ksz, m->ksz) & (ncap - 1);
+        while (h->state[i]) i = (i + 1) & (ncap - 1);
+        h->state[i] = 1;
+        memcpy(h->keys + i * m->ksz, ok + j * m->ksz, m->ksz);
+        memcpy(h->vals + i * m->vsz, ov + j * m->vsz, m->vsz);
+    }
+    free(ok); free(ov); free(os);
+}
+
+/* Element lookup returning a pointer into the shard (NULL if absent). For
+ * LPM maps: exact (normalized) match — used by update/delete. */
+static uint8_t *om_ptr_exact(om_map *m, const uint8_t *key) {
+    uint8_t nk[64];
+    const uint8_t *k = key;
+    if (is_lpm(m)) { lpm_normalize(m, key, nk); k = nk; }
+    om_shard *h = &m->sh[shard_of(m, k)];
+    int64_t i = sh_find(m, h, k);
+    return i < 0 ? NULL : h->vals + (uint64_t)i * m->vsz;
+}
+
+/* kernel trie_lookup_elem: longest stored prefix with len <= key.prefixlen
+ * whose bits match the key data (kernel/bpf/lpm_trie.c). */
+static uint8_t *om_lpm_lookup_ptr(om_map *m, const uint8_t *key) {
+    uint32_t plen; memcpy(&plen, key, 4);
+    uint32_t maxb = lpm_bits(m);
+    if (plen > maxb) plen = maxb;
+    uint8_t probe[64];
+    for (int l = (int)plen; l >= 0; l--) {
+        if (!m->lens_cnt[l]) continue;
+        uint32_t ul = (uint32_t)l;
+        memcpy(probe, key, m->ksz);
+        memcpy(probe, &ul, 4);
+        uint8_t *v = om_ptr_exact(m, probe);
+        if (v) return v;
+    }
+    return NULL;
+}
+
+/* datapath map_lookup_elem() */
+static uint8_t *om_lookup_ptr(om_map *m, const void *key) {
+    if (!m) return NULL;
+    if (is_lpm(m)) return om_lpm_lookup_ptr(m, (const uint8_t *)key);
+    om_shard *h = &m->sh[shard_of(m, (const uint8_t *)key)];
+    int64_t i = sh_find(m, h, (const uint8_t *)key);
+    return i < 0 ? NULL : h->vals + (uint64_t)i * m->vsz;
+}
+
+int om_lookup(om_map *m, const void *key, void *value_out) {
+    uint8_t *v = om_lookup_ptr(m, key);
+    if (!v) return -ENOENT;
+    if (value_out) memcpy(value_out, v, m->vsz);
+    return 0;
+}
+
+/* map_update_elem(): kernel htab_map_update_elem / trie_update_elem. */
+int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
+    if (flags > 2) return -EINVAL;
+    uint8_t nk[64];
+    const uint8_t *key = (const uint8_t *)key_;
+    if (is_lpm(m)) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        if (plen > lpm_bits(m)) return -EINVAL;
+        lpm_normalize(m, key, nk); key = nk;
+    }
+    om_shard *h = &m->sh[shard_of(m, key)];
+    int64_t i = sh_find(m, h, key);
+    if (i >= 0) {
+        if (flags == 1) return -EEXIST;
+        memcpy(h->vals + (uint64_t)i * m->vsz, value, m->vsz);
+        return 0;
+    }
+    if (flags == 2) return -ENOENT;
+    uint32_t c = __atomic_add_fetch(&m->count, 1, __ATOMIC_RELAXED);
+    if (c > m->max_entries) {
+        __atomic_sub_fetch(&m->count, 1, __ATOMIC_RELAXED);
+        return is_lpm(m) ? -ENOSPC : -E2BIG;
+    }
+    if ((h->used + h->tomb + 1) * 2 > h->cap) sh_grow(m, h);
+    uint64_t mask = h->cap - 1, j = fnv1a(key, m->ksz) & mask;
+    while (h->state[j] == 1) j = (j + 1) & mask;
+    if (h->state[j] == 2) h->tomb--;
+    h->state[j] = 1;
+    memcpy(h->keys + j * m->ksz, key, m->ksz);
+    memcpy(h->vals + j * m->vsz, value, m->vsz);
+    h->used++;
+    if (is_lpm(m)) { uint32_t plen; memcpy(&plen, key, 4); m->lens_cnt[plen]++; }
+    return 0;
+}
+
+int om_delete(om_map *m, const void *key_) {
+    uint8_t nk[64];
+    const uint8_t *key = (const uint8_t *)key_;
+    if (is_lpm(m)) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        if (plen > lpm_bits(m)) return -EINVAL;
+        lpm_normalize(m, key, nk); key = nk;
+    }
+    om_shard *h = &m->sh[shard_of(m, key)];
+    int64_t i = sh_find(m, h, key);
+    if (i < 0) return -ENOENT;
+    h->state[i] = 2; h->used--; h->tomb++;
+    __atomic_sub_fetch(&m->count, 1, __ATOMIC_RELAXED);
+    if (is_lpm(m)) { uint32_t plen; memcpy(&plen, key, 4); m->lens_cnt[plen]--; }
+    return 0;
+}
+
+uint32_t om_count(om_map *m) { return m->count; }
+
+uint32_t om_foreach(om_map *m, om_visit_fn fn, void *ctx) {
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < m->nshards; s++) {
+        om_shard *h = &m->sh[s];
+        for (uint64_t i = 0; i < h->cap; i++)
+            if (h->state[i] == 1) { fn(h->keys + i * m->ksz, h->vals + i * m->vsz, ctx); n++; }
+    }
+    return n;
+}
+
+typedef struct dump_ctx { om_map *m; uint8_t *k, *v; uint32_t cap, n; } dump_ctx;
+static void dump_visit(const void *k, const void *v, void *c_) {
+    dump_ctx *c = (dump_ctx *)c_;
+    if (c->n < c->cap) {
+        memcpy(c->k + (size_t)c->n * c->m->ksz, k, c->m->ksz);
+        memcpy(c->v + (size_t)c->n * c->m->vsz, v, c->m->vsz);
+    }
+    c->n++;
+}
+uint32_t om_dump(om_map *m, void *keys, void *values, uint32_t capacity) {
+    dump_ctx c = { m, (uint8_t *)keys, (uint8_t *)values, capacity, 0 };
+    om_foreach(m, dump_visit, &c);
+    return c.n;
+}
+
+/* CT shard selection: unordered address pair of the tuple. */
+uint32_t o_ct_pair_hash4(uint32_t a, uint32_t b) {
+    uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    uint64_t x = ((uint64_t)hi << 32) | lo;
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return (uint32_t)x;
+}
+uint32_t o_ct_pair_hash6(const uint8_t *a, const uint8_t *b) {
+    const uint8_t *lo = memcmp(a, b, 16) <= 0 ? a : b, *hi = lo == a ? b : a;
+    uint8_t buf[32]; memcpy(buf, lo, 16); memcpy(buf + 16, hi, 16);
+    return (uint32_t)fnv1a(buf, 32);
+}
+static uint32_t shard_of(const om_map *m, const uint8_t *key) {
+    if (m->nshards <= 1) return 0;
+    if (m->ksz == 14) { uint32_t a, b; memcpy(&a, key, 4); memcpy(&b, key + 4, 4);
+        return o_ct_pair_hash4(a, b) % m->nshards; }
+    if (m->ksz == 40) return o_ct_pair_hash6(key, key + 16) % m->nshards;
+    return (uint32_t)(fnv1a(key, m->ksz) % m->nshards);
+}
+
+/* ------------------------------------------------------------------ */
+/* skb access emulation                                                */
+/* ------------------------------------------------------------------ */
+typedef struct skb {
+    const uint8_t *data; uint32_t len, cap;   /* cap = snap bytes present */
+    uint32_t cb[5];
+    uint32_t tc_index, hash;
+    uint16_t protocol;                        /* host order ethertype */
+} skb_t;
+
+static inline uint8_t skb_byte(const skb_t *s, uint32_t off) { return off < s->cap ? s->data[off] : 0; }
+
+/* bpf_skb_load_bytes(): offset > 0xffff (incl. negative) or past len -> -EFAULT */
+static int skb_load_bytes(const skb_t *s, int32_t off, void *to, uint32_t n) {
+    uint8_t *d = (uint8_t *)to;
+    if ((uint32_t)off > 0xffff || (uint64_t)(uint32_t)off + n > s->len) {
+        memset(d, 0, n);
+        return -EFAULT;
+    }
+    for (uint32_t i = 0; i < n; i++) d[i] = skb_byte(s, (uint32_t)off + i);
+    return 0;
+}
+/* bpf_skb_store_bytes()/bpf_l{3,4}_csum_replace() writability checks:
+ * offset > 0xffff -> -EFAULT; offset + n past len -> -EFAULT. */
+static int skb_writable(const skb_t *s, int32_t off, uint32_t n) {
+    if ((uint32_t)off > 0xffff || (uint64_t)(uint32_t)off + n > s->len) return -EFAULT;
+    return 0;
+}
+static int l4_csum_replace_chk(const skb_t *s, int32_t off) {
+    if ((uint32_t)off > 0xffff || (off & 1)) return -EFAULT;
+    return skb_writable(s, off, 2);
+}
+static inline uint16_t rd16(const skb_t *s, uint32_t off) {
+    return (uint16_t)(skb_byte(s, off) | (skb_byte(s, off + 1) << 8));
+}
+static inline uint32_t rd32(const skb_t *s, uint32_t off) {
+    return (uint32_t)rd16(s, off) | ((uint32_t)rd16(s, off + 2) << 16);
+}
+static inline uint16_t bswap16(uint16_t x) { return (uint16_t)((x >> 8) | (x << 8)); }
+
+/* csum_l4_offset_and_flags, bpf/lib/csum.h:45-67 (offset part) */
+static uint16_t csum_l4_offset(uint8_t nexthdr) {
+    switch (nexthdr) {
+    case IPPROTO_TCP: return 16;
+    case IPPROTO_UDP: return 6;
+    case IPPROTO_ICMPV6: return 2;
+    default: return 0;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* KAT helpers, bpf/lib/ipv6.h:136-150, bpf/lib/maps.h:147-160          */
+/* ------------------------------------------------------------------ */
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+uint32_t o_get_prefix(int prefix) {
+    uint32_t v = prefix <= 0 ? 0 : prefix < 32 ? ((1u << prefix) - 1) << (32 - prefix) : 0xFFFFFFFFu;
+    return bswap32(v);   /* bpf_htonl */
+}
+void o_ipv6_addr_clear_suffix(uint8_t addr[16], int prefix) {
+    for (int w = 0; w < 4; w++) {
+        uint32_t p; memcpy(&p, addr + 4 * w, 4);
+        p &= o_get_prefix(prefix);
+        memcpy(addr + 4 * w, &p, 4);
+        prefix -= 32;
+    }
+}
+int o_lpm4_iter_lookup(uint32_t stored_net, const int *prefixes, int n, uint32_t addr) {
+    for (int i = 0; i < n; i++)
+        if ((addr & o_get_prefix(prefixes[i])) == stored_net) return 1;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* header parse (the rules gf_parse_frames implements)                 */
+/* ------------------------------------------------------------------ */
+
+/* ipv6_hdrlen, bpf/lib/ipv6.h:61-98.  NB: the AUTH length formula is chosen
+ * by the NEXT header value (nh is reassigned before the test), reproduced. */
+static int ipv6_hdrlen(const skb_t *s, int l3_off, uint8_t *nexthdr) {
+    int len = 40;
+    uint8_t nh = *nexthdr;
+    for (int i = 0; i < 4; i++) {
+        switch (nh) {
+        case 59: return DROP_INVALID_EXTHDR;      /* NEXTHDR_NONE */
+        case 44: return DROP_FRAG_NOSUPPORT;      /* NEXTHDR_FRAGMENT */
+        case 0: case 43: case 51: case 60: {      /* HOP, ROUTING, AUTH, DEST */
+            uint8_t opt[2];
+            if (skb_load_bytes(s, l3_off + len, opt, 2) < 0) return DROP_INVALID;
+            nh = opt[0];
+            if (nh == 51) len += (opt[1] + 2) << 2;   /* ipv6_authlen */
+            else len += (opt[1] + 1) << 3;            /* ipv6_optlen */
+            break;
+        }
+        default:
+            *nexthdr = nh;
+            return len;
+        }
+    }
+    return DROP_INVALID_EXTHDR;
+}
+
+static void skb_init(skb_t *s, const o_batch *b, uint32_t i) {
+    memset(s, 0, sizeof(*s));
+    s->data = b->snap + (size_t)i * b->snap_stride;
+    s->len = b->len[i];
+    s->cap = b->snap_stride < s->len ? b->snap_stride : s->len;
+    s->protocol = s->len >= 14 ? (uint16_t)((s->data[12] << 8) | s->data[13]) : 0;
+    if (b->tc_index) s->tc_index = b->tc_index[i];
+    if (b->flow_hash) s->hash = b->flow_hash[i];
+}
+
+static void l4_bytes(const skb_t *s, int l4_off, uint32_t *w0, uint16_t *w3) {
+    uint8_t b[4] = {0, 0, 0, 0}, c[2] = {0, 0};
+    for (int k = 0; k < 4; k++) {
+        int64_t o = (int64_t)l4_off + k;
+        if (o >= 0 && o < s->len) b[k] = skb_byte(s, (uint32_t)o);
+    }
+    for (int k = 0; k < 2; k++) {
+        int64_t o = (int64_t)l4_off + 12 + k;
+        if (o >= 0 && o < s->len) c[k] = skb_byte(s, (uint32_t)o);
+    }
+    memcpy(w0, b, 4); memcpy(w3, c, 2);
+}
+
+void o_parse_batch(const o_batch *b, o_cols *o) {
+    for (uint32_t i = 0; i < b->n; i++) {
+        skb_t s; skb_init(&s, b, i);
+        uint16_t et = s.protocol;
+        uint32_t sa = 0, da = 0, w0 = 0; uint16_t w3 = 0; uint8_t proto = 0; int l4 = 0;
+        uint8_t s6[16] = {0}, d6[16] = {0};
+        if (et == 0x0800 && s.len >= 34) {
+            sa = rd32(&s, 26); da = rd32(&s, 30); proto = skb_byte(&s, 23);
+            l4 = ETH_HLEN + (skb_byte(&s, 14) & 0xf) * 4;
+            l4_bytes(&s, l4, &w0, &w3);
+        } else if (et == 0x86DD && s.len >= 54) {
+            for (int k = 0; k < 16; k++) { s6[k] = skb_byte(&s, 22 + k); d6[k] = skb_byte(&s, 38 + k); }
+            proto = skb_byte(&s, 20);
+            l4 = ETH_HLEN + ipv6_hdrlen(&s, ETH_HLEN, &proto);
+            l4_bytes(&s, l4, &w0, &w3);
+        }
+        o->ethertype[i] = et; o->saddr4[i] = sa; o->daddr4[i] = da; o->proto[i] = proto;
+        o->l4_off[i] = (int16_t)l4; o->l4w0[i] = w0; o->l4w3[i] = w3;
+        if (o->saddr6) memcpy(o->saddr6 + 16 * (size_t)i, s6, 16);
+        if (o->daddr6) memcpy(o->daddr6 + 16 * (size_t)i, d6, 16);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* XDP prefilter, bpf/bpf_xdp.c:88-184                                 */
+/* ------------------------------------------------------------------ */
+/* lookup_ip4_endpoint / lookup_ip6_endpoint, bpf/lib/eps.h:26-46 */
+static int lookup_ip4_endpoint(om_map *lxc, uint32_t daddr) {
+    uint8_t key[20] = {0};
+    memcpy(key, &daddr, 4); key[16] = 1;   /* ENDPOINT_KEY_IPV4 */
+    return om_lookup_ptr(lxc, key) != NULL;
+}
+static int lookup_ip6_endpoint(om_map *lxc, const uint8_t *daddr) {
+    uint8_t key[20] = {0};
+    memcpy(key, daddr, 16); key[16] = 2;   /* ENDPOINT_KEY_IPV6 */
+    return om_lookup_ptr(lxc, key) != NULL;
+}
+
+static int xdp_check_v4(const o_xdp_cfg *c, const skb_t *s) {
+    if (s->len < ETH_HLEN + 20) return XDP_DROP;          /* xdp_no_room */
+    uint32_t saddr = rd32(s, 26), daddr = rd32(s, 30);
+    if (c->cidr4_hmap) {                                   /* CIDR4_FILTER */
+        uint8_t pfx[8]; uint32_t pl = 32;
+        memcpy(pfx, &pl, 4); memcpy(pfx + 4, &saddr, 4);
+        if (c->cidr4_lmap && om_lookup_ptr(c->cidr4_lmap, pfx)) return XDP_DROP;
+        return om_lookup_ptr(c->cidr4_hmap, pfx) ? XDP_DROP
+               : (lookup_ip4_endpoint(c->lxc_map, daddr) ? XDP_PASS : XDP_DROP);
+    }
+    return lookup_ip4_endpoint(c->lxc_map, daddr) ? XDP_PASS : XDP_DROP;
+}
+static int xdp_check_v6(const o_xdp_cfg *c, const skb_t *s) {
+    if (s->len < ETH_HLEN + 40) return XDP_DROP;
+    uint8_t saddr[16], daddr[16];
+    for (int k = 0; k < 16; k++) { saddr[k] = skb_byte(s, 22 + k); daddr[k] = skb_byte(s, 38 + k); }
+    if (c->cidr6_hmap) {                                   /* CIDR6_FILTER */
+        uint8_t pfx[20]; uint32_t pl = 128;
+        memcpy(pfx, &pl, 4); memcpy(pfx + 4, saddr, 16);
+        if (c->cidr6_lmap && om_lookup_ptr(c->cidr6_lmap, pfx)) return XDP_DROP;
+        return om_lookup_ptr(c->cidr6_hmap, pfx) ? XDP_DROP
+               : (lookup_ip6_endpoint(c->lxc_map, daddr) ? XDP_PASS : XDP_DROP);
+    }
+    return lookup_ip6_endpoint(c->lxc_map, daddr) ? XDP_PASS : XDP_DROP;
+}
+static int xdp_start(const o_xdp_cfg *c, const skb_t *s) {
+    if (s->len < ETH_HLEN) return XDP_DROP;
+    if (s->protocol == 0x0800) return xdp_check_v4(c, s);
+    if (s->protocol == 0x86DD) return xdp_check_v6(c, s);
+    return XDP_PASS;
+}
+
+void o_xdp_batch(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict) {
+    for (uint32_t i = 0; i < b->n; i++) { skb_t s; skb_init(&s, b, i); verdict[i] = (uint8_t)xdp_start(cfg, &s); }
+}
+
+/* ------------------------------------------------------------------ */
+/* Standalone LB, bpf/bpf_lb.c:58-212 + bpf/lib/lb.h                   */
+/* ------------------------------------------------------------------ */
+typedef struct lb_res { uint16_t slave, new_dport, rev_nat; uint32_t new_daddr4; uint8_t nd6[16]; } lb_res;
+
+/* extract_l4_port, bpf/lib/lb.h:191-215 */
+static int extract_l4_port(const skb_t *s, uint8_t nexthdr, int l4_off, uint16_t *port) {
+    switch (nexthdr) {
+    case IPPROTO_TCP: case IPPROTO_UDP: {
+        int ret = skb_load_bytes(s, l4_off + 2, port, 2);   /* l4_load_port, TCP_DPORT_OFF */
+        if (IS_ERR(ret)) return ret;
+        break;
+    }
+    case IPPROTO_ICMPV6: case IPPROTO_ICMP: break;
+    default: return DROP_UNKNOWN_L4;
+    }
+    return 0;
+}
+
+/* lb4_lookup_service, bpf/lib/lb.h:566-597 ; key = {be32 address, be16 dport, u16 slave} */
+static uint8_t *lb4_lookup_service(const o_lb_cfg *c, uint8_t *key) {
+    uint16_t dport; memcpy(&dport, key + 4, 2);
+    if ((c->flags & LB_F_L4) && dport) {
+        uint8_t *svc = om_lookup_ptr(c->lb4_services, key);
+        if (svc) { uint16_t cnt; memcpy(&cnt, svc + 6, 2); if (cnt) return svc; }
+        memset(key + 4, 0, 2);                                 /* key->dport = 0 */
+    }
+    if (c->flags & LB_F_L3) {
+        uint8_t *svc = om_lookup_ptr(c->lb4_services, key);
+        if (svc) { uint16_t cnt; memcpy(&cnt, svc + 6, 2); if (cnt) return svc; }
+    }
+    return NULL;
+}
+/* lb6_lookup_service, bpf/lib/lb.h:350-379 ; lb6_key = {addr[16], be16 dport, u16 slave} */
+static uint8_t *lb6_lookup_service(const o_lb_cfg *c, uint8_t *key) {
+    uint16_t dport; memcpy(&dport, key + 16, 2);
+    if ((c->flags & LB_F_L4) && dport) {
+        uint8_t *svc = om_lookup_ptr(c->lb6_services, key);
+        if (svc) { uint16_t cnt; memcpy(&cnt, svc + 18, 2); if (cnt) return svc; }
+        memset(key + 16, 0, 2);
+    }
+    if (c->flags & LB_F_L3) {
+        uint8_t *svc = om_lookup_ptr(c->lb6_services, key);
+        if (svc) { uint16_t cnt; memcpy(&cnt, svc + 18, 2); if (cnt) return svc; }
+    }
+    return NULL;
+}
+
+/* shared tail of lb4_xlate / lb6_xlate (bpf/lib/lb.h:615-659, 397-423):
+ * verdict-affecting checks of the checksum/port rewrites. */
+static int lb_xlate_checks(const o_lb_cfg *c, const skb_t *s, uint8_t nexthdr, int l4_off,
+                           uint16_t key_dport, uint16_t svc_port, int v6, uint16_t *new_dport) {
+    uint16_t csum_off = csum_l4_offset(nexthdr);
+    if ((csum_off || v6) && l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+    if ((c->flags & LB_F_L4) && svc_port && key_dport != svc_port &&
+        (nexthdr == IPPROTO_TCP || nexthdr == IPPROTO_UDP)) {
+        /* l4_modify_port: csum_l4_replace then skb_store_bytes(l4_off+2) */
+        if (l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+        if (skb_writable(s, l4_off + 2, 2) < 0) return DROP_WRITE_ERROR;
+        *new_dport = svc_port;
+    }
+    return TC_ACT_OK;
+}
+
+static int lb_handle_ipv4(const o_lb_cfg *c, const skb_t *s, lb_res *r) {
+    if (s->len < ETH_HLEN + 20) return DROP_INVALID;             /* revalidate_data */
+    uint8_t nexthdr = skb_byte(s, 23);
+    uint8_t key[8] = {0};
+    uint32_t daddr = rd32(s, 30);
+    memcpy(key, &daddr, 4);
+    int l4_off = ETH_HLEN + (skb_byte(s, 14) & 0xf) * 4;        /* ipv4_hdrlen */
+    int ret;
+    if (c->flags & LB_F_L4) {
+        ret = extract_l4_port(s, nexthdr, l4_off, (uint16_t *)(key + 4));
+        if (IS_ERR(ret)) return ret == DROP_UNKNOWN_L4 ? TC_ACT_OK : ret;
+    }
+    uint8_t *svc = lb4_lookup_service(c, key);
+    if (!svc) return TC_ACT_OK;
+    uint16_t count; memcpy(&count, svc + 6, 2);
+    uint16_t slave = (uint16_t)((s->hash % count) + 1);           /* lb4_select_slave */
+    memcpy(key + 6, &slave, 2);                                  /* lb4_lookup_slave */
+    svc = om_lookup_ptr(c->lb4_services, key);
+    if (!svc) return DROP_NO_SERVICE;
+    uint16_t key_dport, svc_port; memcpy(&key_dport, key + 4, 2); memcpy(&svc_port, svc + 4, 2);
+    ret = lb_xlate_checks(c, s, nexthdr, l4_off, key_dport, svc_port, 0, &r->new_dport);
+    if (IS_ERR(ret)) return ret;
+    r->slave = slave;
+    memcpy(&r->new_daddr4, svc, 4);
+    memcpy(&r->rev_nat, svc + 8, 2);
+    return TC_ACT_REDIRECT;
+}
+
+static int lb_handle_ipv6(const o_lb_cfg *c, const skb_t *s, lb_res *r) {
+    if (s->len < ETH_HLEN + 40) return DROP_INVALID;
+    uint8_t nexthdr = skb_byte(s, 20);
+    uint8_t key[20] = {0};
+    for (int k = 0; k < 16; k++) key[k] = skb_byte(s, 38 + k);
+    int l4_off = ETH_HLEN + ipv6_hdrlen(s, ETH_HLEN, &nexthdr);
+    int ret;
+    if (c->flags & LB_F_L4) {
+        ret = extract_l4_port(s, nexthdr, l4_off, (uint16_t *)(key + 16));
+        if (IS_ERR(ret)) return ret == DROP_UNKNOWN_L4 ? TC_ACT_OK : ret;
+    }
+    uint8_t *svc = lb6_lookup_service(c, key);
+    if (!svc) return TC_ACT_OK;
+    uint16_t count; memcpy(&count, svc + 18, 2);
+    uint16_t slave = (uint16_t)((s->hash % count) + 1);
+    memcpy(key + 18, &slave, 2);
+    svc = om_lookup_ptr(c->lb6_services, key);
+    if (!svc) return DROP_NO_SERVICE;
+    uint8_t nd[16]; memcpy(nd, svc, 16);
+    uint16_t rn; memcpy(&rn, svc + 20, 2);
+    if (rn) { uint32_t p4; memcpy(&p4, nd + 12, 4); p4 |= rn; memcpy(nd + 12, &p4, 4); }
+    uint16_t key_dport, svc_port; memcpy(&key_dport, key + 16, 2); memcpy(&svc_port, svc + 16, 2);
+    ret = lb_xlate_checks(c, s, nexthdr, l4_off, key_dport, svc_port, 1, &r->new_dport);
+    if (IS_ERR(ret)) return ret;
+    r->slave = slave; r->rev_nat = rn;
+    memcpy(r->nd6, nd, 16);
+    return TC_ACT_REDIRECT;
+}
+
+/* from_netdev, bpf/bpf_lb.c:169-212.  The output reports what the
+ * translation changed: slave/new_daddr/rev_nat when lb*_xlate ran, new_dport
+ * when the L4 port was rewritten; zero otherwise. */
+static void lb_one(const o_lb_cfg *c, const skb_t *s, o_lb_out *o, uint8_t *nd6) {
+    lb_res r; memset(&r, 0, sizeof(r));
+    memset(o, 0, sizeof *o);
+    if (nd6) memset(nd6, 0, 16);
+    int ret, v6 = 0;
+    switch (s->protocol) {
+    case 0x86DD:
+        if (c->flags & LB_F_NO_IPV6) return;
+        v6 = 1; ret = lb_handle_ipv6(c, s, &r); break;
+    case 0x0800:
+        if (c->flags & LB_F_NO_IPV4) return;
+        ret = lb_handle_ipv4(c, s, &r); break;
+    default:
+        return;                                           /* TC_ACT_OK */
+    }
+    if (IS_ERR(ret)) {                                    /* send_drop_notify_error */
+        o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret);
+        return;
+    }
+    o->action = ((c->flags & LB_F_REDIRECT) && ret == TC_ACT_REDIRECT) ? TC_ACT_REDIRECT : TC_ACT_OK;
+    if (ret == TC_ACT_REDIRECT) {
+        o->slave = r.slave; o->new_dport = r.new_dport; o->rev_nat = r.rev_nat;
+        if (v6) { if (nd6) memcpy(nd6, r.nd6, 16); }
+        else o->new_daddr4 = r.new_daddr4;
+    }
+}
+
+void o_lb_batch(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t *nd6) {
+    for (uint32_t i = 0; i < b->n; i++) {
+        skb_t s; skb_init(&s, b, i);
+        lb_one(cfg, &s, &out[i], nd6 ? nd6 + 16 * (size_t)i : NULL);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Conntrack, bpf/lib/conntrack.h:47-580                               */
+/* ------------------------------------------------------------------ */
+/* ct_entry byte offsets */
+#define CTE_RX_PKTS 0
+#define CTE_RX_BYTES 8
+#define CTE_TX_PKTS 16
+#define CTE_TX_BYTES 24
+#define CTE_LIFETIME 32
+#define CTE_FLAGS 36
+#define CTE_REVNAT 38
+#define CTE_SRCSEC 44
+#define CTF_RX_CLOSING 1u
+#define CTF_TX_CLOSING 2u
+#define CTF_LB_LOOPBACK 8u
+#define CTF_SEEN_NON_SYN 16u
+
+typedef struct ct_state { uint16_t rev_nat_index; uint8_t loopback; uint16_t orig_dport;
+                          uint32_t addr, svc_addr, src_sec_id; } ct_state_t;
+
+static inline uint16_t ge16(const uint8_t *p, int o) { uint16_t v; memcpy(&v, p + o, 2); return v; }
+static inline void se16(uint8_t *p, int o, uint16_t v) { memcpy(p + o, &v, 2); }
+static inline uint32_t ge32(const uint8_t *p, int o) { uint32_t v; memcpy(&v, p + o, 4); return v; }
+static inline void se32(uint8_t *p, int o, uint32_t v) { memcpy(p + o, &v, 4); }
+static inline uint64_t ge64(const uint8_t *p, int o) { uint64_t v; memcpy(&v, p + o, 8); return v; }
+static inline void se64(uint8_t *p, int o, uint64_t v) { memcpy(p + o, &v, 8); }
+
+/* ct_update_timeout / __ct_update_timeout (NEEDS_TIMEOUT), conntrack.h:47-62 */
+static void ct_update_timeout(uint8_t *e, int syn, uint32_t now) {
+    uint16_t f = ge16(e, CTE_FLAGS);
+    if (!syn) f |= CTF_SEEN_NON_SYN;
+    se16(e, CTE_FLAGS, f);
+    se32(e, CTE_LIFETIME, now + ((f & CTF_SEEN_NON_SYN) ? CT_DEFAULT_LIFETIME : CT_SYN_TIMEOUT));
+}
+static int ct_entry_alive(const uint8_t *e) {
+    uint16_t f = ge16(e, CTE_FLAGS);
+    return !(f & CTF_RX_CLOSING) || !(f & CTF_TX_CLOSING);
+}
+
+typedef struct ctx {
+    uint32_t now;
+    const o_lxc_cfg *lxc;
+} ctx_t;
+
+/* __ct_lookup, conntrack.h:75-135 */
+static int __ct_lookup(om_map *map, const skb_t *s, const void *tuple, int action, int dir,
+                       ct_state_t *st, int syn, uint32_t now, int accounting) {
+    uint8_t *e = om_lookup_ptr(map, tuple);
+    if (!e) return CT_NEW;
+    if (ct_entry_alive(e)) ct_update_timeout(e, syn, now);
+    if (st) {
+        st->rev_nat_index = ge16(e, CTE_REVNAT);
+        st->loopback = (ge16(e, CTE_FLAGS) & CTF_LB_LOOPBACK) ? 1 : 0;
+    }
+    if (accounting) {
+        if (dir == CT_INGRESS) {
+            se64(e, CTE_RX_PKTS, ge64(e, CTE_RX_PKTS) + 1);
+            se64(e, CTE_RX_BYTES, ge64(e, CTE_RX_BYTES) + s->len);
+        } else {
+            se64(e, CTE_TX_PKTS, ge64(e, CTE_TX_PKTS) + 1);
+            se64(e, CTE_TX_BYTES, ge64(e, CTE_TX_BYTES) + s->len);
+        }
+    }
+    uint16_t f = ge16(e, CTE_FLAGS);
+    switch (action) {
+    case ACTION_CREATE:
+        if (((f & CTF_RX_CLOSING) ? 1 : 0) + ((f & CTF_TX_CLOSING) ? 1 : 0) >= 1) {
+            se16(e, CTE_FLAGS, (uint16_t)(f & ~(CTF_RX_CLOSING | CTF_TX_CLOSING)));
+            ct_update_timeout(e, syn, now);
+        }
+        break;
+    case ACTION_CLOSE:
+        f |= (dir == CT_INGRESS) ? CTF_RX_CLOSING : CTF_TX_CLOSING;
+        se16(e, CTE_FLAGS, f);
+        if (ct_entry_alive(e)) break;
+        se32(e, CTE_LIFETIME, now + CT_CLOSE_TIMEOUT);
+        break;
+    }
+    return CT_ESTABLISHED;
+}
+
+/* tuple4 offsets: daddr 0, saddr 4, dport 8, sport 10, nexthdr 12, flags 13 */
+static void ipv4_ct_tuple_reverse(uint8_t *t) {                 /* conntrack.h:291-308 */
+    uint8_t tmp[4]; memcpy(tmp, t + 4, 4); memcpy(t + 4, t, 4); memcpy(t, tmp, 4);
+    uint16_t sp = ge16(t, 10), dp = ge16(t, 8); se16(t, 10, dp); se16(t, 8, sp);
+    t[13] = (t[13] & TUPLE_F_IN) ? (uint8_t)(t[13] & ~TUPLE_F_IN) : (uint8_t)(t[13] | TUPLE_F_IN);
+}
+/* tuple6 offsets: daddr 0, saddr 16, dport 32, sport 34, nexthdr 36, flags 37 */
+static void ipv6_ct_tuple_reverse(uint8_t *t) {                 /* conntrack.h:147-167 */
+    uint8_t tmp[16]; memcpy(tmp, t + 16, 16); memcpy(t + 16, t, 16); memcpy(t, tmp, 16);
+    uint16_t sp = ge16(t, 34), dp = ge16(t, 32); se16(t, 34, dp); se16(t, 32, sp);
+    t[37] = (t[37] & TUPLE_F_IN) ? (uint8_t)(t[37] & ~TUPLE_F_IN) : (uint8_t)(t[37] | TUPLE_F_IN);
+}
+
+/* ct_lookup4 / ct_lookup6 (conntrack.h:170-289, 319-435).  v6 selects the
+ * tuple layout and the ICMPv6 type table. */
+static int ct_lookup(om_map *map, uint8_t *t, const skb_t *s, int off, int dir,
+                     ct_state_t *st, int v6, uint32_t now, int accounting) {
+    int action = ACTION_UNSPEC, syn = 0, ret;
+    int o_dport = v6 ? 32 : 8, o_sport = v6 ? 34 : 10, o_nh = v6 ? 36 : 12, o_fl = v6 ? 37 : 13;
+    t[o_fl] = dir == CT_INGRESS ? TUPLE_F_OUT : TUPLE_F_IN;
+    uint8_t nh = t[o_nh];
+    if ((!v6 && nh == IPPROTO_ICMP) || (v6 && nh == IPPROTO_ICMPV6)) {
+        uint8_t type;
+        if (skb_load_bytes(s, off, &type, 1) < 0) return DROP_CT_INVALID_HDR;
+        se16(t, o_sport, 0); se16(t, o_dport, 0);
+        if (!v6) {
+            switch (type) {
+            case 3: case 11: case 12: t[o_fl] |= TUPLE_F_RELATED; break;   /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
+            case 0: se16(t, o_dport, 8); break;                             /* ECHOREPLY -> dport = ICMP_ECHO */
+            case 8: se16(t, o_sport, type); /* fallthrough */               /* ECHO */
+            default: action = ACTION_CREATE; break;
+            }
+        } else {
+            switch (type) {
+            case 1: case 2: case 3: case 4: t[o_fl] |= TUPLE_F_RELATED; break;
+            case 129: se16(t, o_dport, 128); break;                         /* ECHO_REPLY */
+            case 128: se16(t, o_sport, type); /* fallthrough */
+            default: action = ACTION_CREATE; break;
+            }
+        }
+    } else if (nh == IPPROTO_TCP) {
+        uint16_t fl;
+        if (skb_load_bytes(s, off + 12, &fl, 2) < 0) return DROP_CT_INVALID_HDR;
+        int fin = (fl >> 8) & 1, sy = (fl >> 9) & 1, rst = (fl >> 10) & 1;   /* struct tcp_flags, LE bitfield */
+        action = (rst || fin) ? ACTION_CLOSE : ACTION_CREATE;
+        syn = sy;
+        if (skb_load_bytes(s, off, t + o_dport, 4) < 0) return DROP_CT_INVALID_HDR;
+    } else if (nh == IPPROTO_UDP) {
+        if (skb_load_bytes(s, off, t + o_dport, 4) < 0) return DROP_CT_INVALID_HDR;
+        action = ACTION_CREATE;
+    } else {
+        return DROP_CT_UNKNOWN_PROTO;
+    }
+    ret = __ct_lookup(map, s, t, action, dir, st, syn, now, accounting);
+    if (ret != CT_NEW) {
+        if (ret == CT_ESTABLISHED) ret = (t[o_fl] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+        return ret;
+    }
+    if (v6) ipv6_ct_tuple_reverse(t); else ipv4_ct_tuple_reverse(t);
+    return __ct_lookup(map, s, t, action, dir, st, syn, now, accounting);
+}
+
+/* ct_create4 (conntrack.h:503-580) / ct_create6 (:446-493), ingress use
+ * (ct_state->addr == 0, so the loopback branch is not taken). */
+static int ct_create(om_map *map, uint8_t *t, const skb_t *s, int dir, const ct_state_t *st,
+                     int v6, uint32_t now) {
+    uint8_t e[48]; memset(e, 0, sizeof e);
+    int o_nh = v6 ? 36 : 12, o_fl = v6 ? 37 : 13, ksz = v6 ? 40 : 14;
+    se16(e, CTE_REVNAT, st->rev_nat_index);
+    if (st->loopback) se16(e, CTE_FLAGS, CTF_LB_LOOPBACK);
+    ct_update_timeout(e, t[o_nh] == IPPROTO_TCP, now);
+    if (dir == CT_INGRESS) { se64(e, CTE_RX_PKTS, 1); se64(e, CTE_RX_BYTES, s->len); }
+    else { se64(e, CTE_TX_PKTS, 1); se64(e, CTE_TX_BYTES, s->len); }
+    se32(e, CTE_SRCSEC, st->src_sec_id);
+    if (om_update(map, t, e, 0) < 0) return DROP_CT_CREATE_FAILED;
+    uint8_t it[40]; memset(it, 0, sizeof it);
+    if (v6) { memcpy(it, t, 32); it[36] = IPPROTO_ICMPV6; }
+    else { memcpy(it, t, 8); it[12] = IPPROTO_ICMP; }
+    it[o_fl] = t[o_fl] | TUPLE_F_RELATED;
+    se16(e, CTE_FLAGS, (uint16_t)(ge16(e, CTE_FLAGS) | CTF_SEEN_NON_SYN));
+    if (om_update(map, it, e, 0) < 0) return DROP_CT_CREATE_FAILED;
+    (void)ksz;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Policy, bpf/lib/policy.h:42-168 + bpf/lib/l4.h:151-217              */
+/* ------------------------------------------------------------------ */
+/* l4_ingress_proxy_lookup via BPF_L4_MAP/F (bpf/lib/common.h:105-127) */
+static int l4_ingress_proxy_lookup(const o_lxc_cfg *c, uint16_t dport, uint8_t nexthdr) {
+    if (!c->n_l4_ingress) return 0;                 /* CFG_L3L4_INGRESS undefined */
+    int allowed = DROP_POLICY_L4;
+    for (uint32_t i = 0; i < c->n_l4_ingress; i++) {
+        const o_l4_allow *a = &c->l4_ingress[i];
+        allowed = allowed > -1 ? allowed
+                : ((a->port && a->port == dport) ? ((a->nexthdr && a->nexthdr == nexthdr) ? (int)a->proxy
+                                                                                     : DROP_POLICY_L4)
+                                                  : DROP_POLICY_L4);
+    }
+    return allowed > 0 ? allowed : 0;
+}
+static int l4_proxy_lookup(const o_lxc_cfg *c, uint8_t nh, uint16_t dport) {   /* dir = INGRESS */
+    int proxy_port = 0;
+    if (nh == IPPROTO_UDP || nh == IPPROTO_TCP) {
+        proxy_port = l4_ingress_proxy_lookup(c, dport, nh);
+        if (proxy_port < 0) return proxy_port;
+    }
+    return proxy_port;
+}
+
+static void policy_count(uint8_t *p, uint32_t len) {            /* __sync_fetch_and_add x2 */
+    __atomic_fetch_add((uint64_t *)(p + 8), 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add((uint64_t *)(p + 16), (uint64_t)len, __ATOMIC_RELAXED);
+}
+
+/* __policy_can_access, policy.h:42-113 (dir = CT_INGRESS) */
+static int __policy_can_access(const o_lxc_cfg *c, const skb_t *s, uint32_t identity,
+                               uint16_t dport, uint8_t proto) {
+    if (c->flags & LXC_F_DROP_ALL) return DROP_POLICY;
+    uint8_t key[8];
+    se32(key, 0, identity); se16(key, 4, dport); key[6] = proto; key[7] = 0;   /* egress = !dir = 0 */
+    uint8_t *p;
+    if (c->flags & LXC_F_HAVE_L4_POLICY) {
+        p = om_lookup_ptr(c->policy_map, key);
+        if (p) { policy_count(p, s->len); goto get_proxy_port; }
+    }
+    se16(key, 4, 0); key[6] = 0;
+    p = om_lookup_ptr(c->policy_map, key);
+    if (p) { policy_count(p, s->len); return TC_ACT_OK; }
+    if (c->flags & LXC_F_HAVE_L4_POLICY) {
+        se32(key, 0, 0); se16(key, 4, dport); key[6] = proto;
+        p = om_lookup_ptr(c->policy_map, key);
+        if (p) { policy_count(p, s->len); goto get_proxy_port; }
+    }
+    if (s->cb[2]) return TC_ACT_OK;                   /* cb[CB_POLICY], cleared by policy_clear_mark */
+    return DROP_POLICY;
+get_proxy_port: {
+        uint16_t pp = ge16(p, 0);
+        if (pp) return pp;
+        return l4_proxy_lookup(c, proto, dport);
+    }
+}
+
+/* policy_can_access_ingress, policy.h:133-168 */
+static int policy_can_access_ingress(const o_lxc_cfg *c, const skb_t *s, uint32_t src_identity,
+                                     uint16_t dport, uint8_t proto, int v6, const uint8_t *cidr_addr) {
+    if (c->flags & LXC_F_DROP_ALL) return DROP_POLICY;
+    if (!(c->flags & LXC_F_POLICY_INGRESS)) return TC_ACT_OK;
+    int ret = __policy_can_access(c, s, src_identity, dport, proto);
+    if (ret >= TC_ACT_OK) return ret;
+    if (src_identity < 256) {                          /* identity_is_reserved */
+        if (v6 && c->cidr6_ingress_map) {
+            uint8_t k[20]; uint32_t pl = 128; memcpy(k, &pl, 4); memcpy(k + 4, cidr_addr, 16);
+            if (om_lookup_ptr(c->cidr6_ingress_map, k)) return TC_ACT_OK;
+        }
+        if (!v6 && c->cidr4_ingress_map) {
+            uint8_t k[8]; uint32_t pl = 32; memcpy(k, &pl, 4); memcpy(k + 4, cidr_addr, 4);
+            if (om_lookup_ptr(c->cidr4_ingress_map, k)) return TC_ACT_OK;
+        }
+    }
+    return DROP_POLICY;
+}
+
+/* __lb4_rev_nat / __lb6_rev_nat verdict-affecting steps (lb.h:447-512,
+ * 253-293): reverse_map_l4_port + checksum writability. */
+static int lb_rev_nat_checks(const skb_t *s, int l4_off, uint8_t nexthdr, uint16_t nat_port, int v6) {
+    uint16_t csum_off = csum_l4_offset(nexthdr);
+    if (nat_port) {
+        switch (nexthdr) {                             /* reverse_map_l4_port, lb.h:217-251 */
+        case IPPROTO_TCP: case IPPROTO_UDP: {
+            uint16_t old;
+            int ret = skb_load_bytes(s, l4_off, &old, 2);   /* TCP_SPORT_OFF */
+            if (IS_ERR(ret)) return ret;
+            if (nat_port != old) {
+                if (l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+                if (skb_writable(s, l4_off, 2) < 0) return DROP_WRITE_ERROR;
+            }
+            break;
+        }
+        case IPPROTO_ICMPV6: case IPPROTO_ICMP: break;
+        default: return DROP_UNKNOWN_L4;
+        }
+    }
+    if (v6) {
+        if (l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+    } else {
+        if (csum_off && l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+    }
+    return 0;
+}
+
+/* ipv4_redirect_to_host_port / ipv6_... verdict-affecting steps (lib/lxc.h:96-205) */
+static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t nexthdr) {
+    uint16_t csum_off = csum_l4_offset(nexthdr);
+    if (l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_WRITE_ERROR;  /* l4_modify_port */
+    if (skb_writable(s, l4_off + 2, 2) < 0) return DROP_WRITE_ERROR;
+    return 0;                                          /* cilium_proxy{4,6} update: §8(f) */
+}
+
+static uint32_t g_host_ifindex = 1;                    /* HOST_IFINDEX, bpf/node_config.h */
+void o_set_node(const o_node_cfg *node) { g_host_ifindex = node->host_ifindex; }
+
+/* ipv4_policy, bpf/bpf_lxc.c:865-970 */
+static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags, uint16_t *proxy) {
+    if (s->len < ETH_HLEN + 20) return DROP_INVALID;
+    s->cb[2] = 0;                                      /* policy_clear_mark */
+    uint8_t t[14]; memset(t, 0, sizeof t);
+    t[12] = skb_byte(s, 23);
+    int skip_proxy = s->tc_index & 1;
+    uint32_t daddr = rd32(s, 30), saddr = rd32(s, 26);
+    se32(t, 0, daddr); se32(t, 4, saddr);
+    uint32_t orig_sip = saddr;
+    int l4_off = ETH_HLEN + (skb_byte(s, 14) & 0xf) * 4;
+    ct_state_t st; memset(&st, 0, sizeof st);
+    int acct = (c->flags & LXC_F_CT_ACCOUNTING) != 0;
+    int ret = ct_lookup(c->ct_map4, t, s, l4_off, CT_INGRESS, &st, 0, now, acct);
+    if (ret < 0) return ret;
+    *fwd = ret;
+    if (ret == CT_REPLY && st.rev_nat_index && !st.loopback) {
+        uint8_t *nat = om_lookup_ptr(c->revnat4_map, &st.rev_nat_index);
+        if (nat) {
+            int r2 = lb_rev_nat_checks(s, l4_off, t[12], ge16(nat, 4), 0);
+            if (IS_ERR(r2)) return r2;
+            memcpy(t + 4, nat, 4);                     /* tuple->saddr = nat->address */
+        }
+    }
+    int verdict = policy_can_access_ingress(c, s, src_label, ge16(t, 8), t[12], 0, (const uint8_t *)&orig_sip);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) om_delete(c->ct_map4, t);   /* ct_delete4 */
+        return DROP_POLICY;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == CT_NEW) {
+        ct_state_t sn; memset(&sn, 0, sizeof sn);
+        sn.orig_dport = ge16(t, 8); sn.src_sec_id = src_label;
+        ret = ct_create(c->ct_map4, t, s, CT_INGRESS, &sn, 0, now);
+        if (IS_ERR(ret)) return ret;
+        *oflags |= 2;
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        ret = redirect_to_host_port_checks(s, l4_off, t[12]);
+        if (IS_ERR(ret)) return ret;
+        s->cb[1] = g_host_ifindex;
+        *oflags |= 1;
+        *proxy = (uint16_t)verdict;
+    }
+    return 0;
+}
+
+/* ipv6_policy, bpf/bpf_lxc.c:745-862 */
+static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags, uint16_t *proxy) {
+    if (s->len < ETH_HLEN + 40) return DROP_INVALID;
+    s->cb[2] = 0;
+    uint8_t t[40]; memset(t, 0, sizeof t);
+    t[36] = skb_byte(s, 20);
+    for (int k = 0; k < 16; k++) { t[k] = skb_byte(s, 38 + k); t[16 + k] = skb_byte(s, 22 + k); }
+    int skip_proxy = s->tc_index & 1;
+    int l4_off = ETH_HLEN + ipv6_hdrlen(s, ETH_HLEN, &t[36]);
+    uint16_t csum_off = csum_l4_offset(t[36]);
+    ct_state_t st, sn; memset(&st, 0, sizeof st); memset(&sn, 0, sizeof sn);
+    uint32_t p4 = ge32(t, 12);                         /* ip6->daddr.s6_addr32[3] */
+    sn.rev_nat_index = (uint16_t)(p4 & 0xFFFF);
+    if (sn.rev_nat_index) {
+        if (csum_off && l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+    }
+    int acct = (c->flags & LXC_F_CT_ACCOUNTING) != 0;
+    int ret = ct_lookup(c->ct_map6, t, s, l4_off, CT_INGRESS, &st, 1, now, acct);
+    if (ret < 0) return ret;
+    *fwd = ret;
+    if (st.rev_nat_index) {
+        uint8_t *nat = om_lookup_ptr(c->revnat6_map, &st.rev_nat_index);
+        if (nat) {
+            int r2 = lb_rev_nat_checks(s, l4_off, t[36], ge16(nat, 16), 1);
+            if (IS_ERR(r2)) return r2;
+        }
+    }
+    int verdict = policy_can_access_ingress(c, s, src_label, ge16(t, 32), t[36], 1, t + 16);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) om_delete(c->ct_map6, t);
+        return DROP_POLICY;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == CT_NEW) {
+        sn.orig_dport = ge16(t, 32); sn.src_sec_id = src_label;
+        ret = ct_create(c->ct_map6, t, s, CT_INGRESS, &sn, 1, now);
+        if (IS_ERR(ret)) return ret;
+        *oflags |= 2;
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        ret = redirect_to_host_port_checks(s, l4_off, t[36]);
+        if (IS_ERR(ret)) return ret;
+        s->cb[1] = g_host_ifindex;
+        *oflags |= 1;
+        *proxy = (uint16_t)verdict;
+    }
+    return 0;
+}
+
+/* handle_policy, bpf/bpf_lxc.c:980-1024 */
+static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o) {
+    skb_t s; skb_init(&s, b, i);
+    s.cb[0] = b->src_identity ? b->src_identity[i] : 0;
+    s.cb[1] = b->ifindex ? b->ifindex[i] : 0;
+    uint32_t lxc_id = b->lxc_id ? b->lxc_id[i] : 0;
+    memset(o, 0, sizeof *o);
+    const o_lxc_cfg *c = a->slot[lxc_id & 0xffff];
+    if (!c) {                                          /* tail_call miss -> caller's DROP_MISSED_TAIL_CALL */
+        o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL);
+        return;
+    }
+    uint32_t src_label = s.cb[0];
+    int fwd = 0, ret;
+    uint8_t fl = 0;
+    uint16_t proxy = 0;
+    if (c->flags & LXC_F_DROP_ALL) ret = DROP_POLICY;
+    else if (s.protocol == 0x86DD) ret = ipv6_policy(c, &s, src_label, &fwd, now, &fl, &proxy);
+    else if (s.protocol == 0x0800 && (c->flags & LXC_F_LXC_IPV4)) ret = ipv4_policy(c, &s, src_label, &fwd, now, &fl, &proxy);
+    else ret = DROP_UNKNOWN_L3;
+    o->ct_ret = (uint8_t)fwd;
+    o->flags = fl;
+    if (ret < 0 || ret == TC_ACT_SHOT) {                /* IS_ERR */
+        o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret); o->flags = fl & 2;
+        return;
+    }
+    o->proxy_port = proxy;
+    uint32_t ifindex = s.cb[1];
+    o->ifindex_lo = (uint16_t)ifindex;
+    o->action = ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+}
+
+o_prog_array *o_prog_array_create(void) { return (o_prog_array *)calloc(1, sizeof(o_prog_array)); }
+void o_prog_array_destroy(o_prog_array *a) { free(a); }
+void o_prog_array_set(o_prog_array *a, uint32_t lxc_id, const o_lxc_cfg *cfg) { a->slot[lxc_id & 0xffff] = cfg; }
+
+void o_ingress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out) {
+    for (uint32_t i = 0; i < b->n; i++) handle_policy(a, b, i, now, &out[i]);
+}
+
+/* ------------------------------------------------------------------ */
+/* multi-threaded drivers (CPU baseline)                               */
+/* ------------------------------------------------------------------ */
+typedef struct mt_arg {
+    const o_prog_array *a; const o_batch *b; uint32_t now; o_ingress_out *out;
+    const o_xdp_cfg *xc; uint8_t *verdict; const o_lb_cfg *lc; o_lb_out *lo; uint8_t *nd6;
+    uint32_t tid, nthreads; int kind;
+} mt_arg;
+
+static uint32_t pkt_group(const o_batch *b, uint32_t i) {
+    const uint8_t *d = b->snap + (size_t)i * b->snap_stride;
+    uint32_t len = b->len[i], cap = b->snap_stride < len ? b->snap_stride : len;
+    if (cap >= 34 && d[12] == 0x08 && d[13] == 0x00) {
+        uint32_t sa, da; memcpy(&sa, d + 26, 4); memcpy(&da, d + 30, 4);
+        return o_ct_pair_hash4(sa, da);
+    }
+    if (cap >= 54 && d[12] == 0x86 && d[13] == 0xDD) return o_ct_pair_hash6(d + 22, d + 38);
+    return 0;
+}
+
+static void *mt_worker(void *p) {
+    mt_arg *m = (mt_arg *)p;
+    const o_batch *b = m->b;
+    if (m->kind == 0) {
+        for (uint32_t i = 0; i < b->n; i++)
+            if (pkt_group(b, i) % m->nthreads == m->tid) handle_policy(m->a, b, i, m->now, &m->out[i]);
+    } else {
+        uint32_t lo = (uint32_t)((uint64_t)b->n * m->tid / m->nthreads);
+        uint32_t hi = (uint32_t)((uint64_t)b->n * (m->tid + 1) / m->nthreads);
+        for (uint32_t i = lo; i < hi; i++) {
+            skb_t s; skb_init(&s, b, i);
+            if (m->kind == 1) m->verdict[i] = (uint8_t)xdp_start(m->xc, &s);
+            else lb_one(m->lc, &s, &m->lo[i], m->nd6 ? m->nd6 + 16 * (size_t)i : NULL);
+        }
+    }
+    return NULL;
+}
+
+static void run_mt(mt_arg *tmpl, uint32_t threads) {
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+    mt_arg *args = (mt_arg *)calloc(threads, sizeof(mt_arg));
+    for (uint32_t t = 0; t < threads; t++) {
+        args[t] = *tmpl; args[t].tid = t; args[t].nthreads = threads;
+        pthread_create(&th[t], NULL, mt_worker, &args[t]);
+    }
+    for (uint32_t t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th); free(args);
+}
+
+void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
+    mt_arg m; memset(&m, 0, sizeof m);
+    m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0;
+    run_mt(&m, threads);
+}
+void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads) {
+    mt_arg m; memset(&m, 0, sizeof m);
+    m.b = b; m.xc = cfg; m.verdict = verdict; m.kind = 1;
+    run_mt(&m, threads);
+}
+void o_lb_batch_mt(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t *nd6, uint32_t threads) {
+    mt_arg m; memset(&m, 0, sizeof m);
+    m.b = b; m.lc = cfg; m.lo = out; m.nd6 = nd6; m.kind = 2;
+    run_mt(&m, threads);
+}

@@ -1,0 +1,195 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY (see oracle.h)."""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PATH = os.path.join(_HERE, "liboracle.so")
+if not os.path.exists(_PATH):
+    raise ImportError(f"{_PATH} missing: run `make -C oracle`")
+lib = C.CDLL(_PATH)
+VP = C.c_void_p
+
+
+class o_l4_allow(C.Structure):
+    _fields_ = [("port", C.c_uint16), ("proxy", C.c_uint16), ("nexthdr", C.c_uint8), ("pad", C.c_uint8 * 3)]
+
+
+class o_xdp_cfg(C.Structure):
+    _fields_ = [("cidr4_hmap", VP), ("cidr4_lmap", VP), ("cidr6_hmap", VP), ("cidr6_lmap", VP), ("lxc_map", VP)]
+
+
+class o_lb_cfg(C.Structure):
+    _fields_ = [("lb4_services", VP), ("lb6_services", VP), ("flags", C.c_uint32), ("redirect_ifindex", C.c_uint32)]
+
+
+class o_lxc_cfg(C.Structure):
+    _fields_ = [("lxc_id", C.c_uint32), ("seclabel", C.c_uint32), ("policy_map", VP), ("ct_map4", VP),
+                ("ct_map6", VP), ("cidr4_ingress_map", VP), ("cidr6_ingress_map", VP), ("revnat4_map", VP),
+                ("revnat6_map", VP), ("flags", C.c_uint32), ("n_l4_ingress", C.c_uint32),
+                ("l4_ingress", o_l4_allow * 64)]
+
+
+class o_node_cfg(C.Structure):
+    _fields_ = [("host_ifindex", C.c_uint32)]
+
+
+class o_batch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("snap_stride", C.c_uint32), ("snap", VP), ("len", VP),
+                ("src_identity", VP), ("ifindex", VP), ("flow_hash", VP), ("lxc_id", VP), ("tc_index", VP)]
+
+
+class o_cols(C.Structure):
+    _fields_ = [("ethertype", VP), ("saddr4", VP), ("daddr4", VP), ("proto", VP), ("l4_off", VP),
+                ("l4w0", VP), ("l4w3", VP), ("saddr6", VP), ("daddr6", VP)]
+
+
+def _s(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+
+
+_s("om_create", VP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
+_s("om_destroy", None, VP)
+_s("om_update", C.c_int, VP, VP, VP, C.c_uint64)
+_s("om_lookup", C.c_int, VP, VP, VP)
+_s("om_delete", C.c_int, VP, VP)
+_s("om_count", C.c_uint32, VP)
+_s("om_dump", C.c_uint32, VP, VP, VP, C.c_uint32)
+_s("o_parse_batch", None, C.POINTER(o_batch), C.POINTER(o_cols))
+_s("o_xdp_batch", None, C.POINTER(o_xdp_cfg), C.POINTER(o_batch), VP)
+_s("o_xdp_batch_mt", None, C.POINTER(o_xdp_cfg), C.POINTER(o_batch), VP, C.c_uint32)
+_s("o_lb_batch", None, C.POINTER(o_lb_cfg), C.POINTER(o_batch), VP, VP)
+_s("o_lb_batch_mt", None, C.POINTER(o_lb_cfg), C.POINTER(o_batch), VP, VP, C.c_uint32)
+_s("o_prog_array_create", VP)
+_s("o_prog_array_destroy", None, VP)
+_s("o_prog_array_set", None, VP, C.c_uint32, C.POINTER(o_lxc_cfg))
+_s("o_set_node", None, C.POINTER(o_node_cfg))
+_s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
+_s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
+_s("o_get_prefix", C.c_uint32, C.c_int)
+_s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
+_s("o_lpm4_iter_lookup", C.c_int, C.c_uint32, VP, C.c_int, C.c_uint32)
+_s("o_ct_pair_hash4", C.c_uint32, C.c_uint32, C.c_uint32)
+
+LB_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("slave", "<u2"), ("new_dport", "<u2"),
+                   ("rev_nat", "<u2"), ("new_daddr4", "<u4")])
+ING_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
+                    ("proxy_port", "<u2"), ("ifindex_lo", "<u2")])
+
+
+class OMap:
+    """One oracle map (kernel htab / LPM trie semantics)."""
+
+    def __init__(self, typ, ksz, vsz, max_entries, shards=1):
+        self.ptr = lib.om_create(typ, ksz, vsz, max_entries, shards)
+        if not self.ptr:
+            raise ValueError("om_create failed")
+        self.ksz, self.vsz = ksz, vsz
+
+    def update(self, key, value, flags=0):
+        return lib.om_update(self.ptr, key, value, flags)
+
+    def update_many(self, keys, values, flags=0):
+        kb, vb = bytes(keys), bytes(values)
+        n = len(kb) // self.ksz
+        kbuf = C.create_string_buffer(kb, len(kb))
+        vbuf = C.create_string_buffer(vb, len(vb))
+        ka, va = C.addressof(kbuf), C.addressof(vbuf)
+        for i in range(n):
+            rc = lib.om_update(self.ptr, ka + i * self.ksz, va + i * self.vsz, flags)
+            if rc:
+                raise OSError(-rc, "om_update")
+
+    def lookup(self, key):
+        v = C.create_string_buffer(self.vsz)
+        rc = lib.om_lookup(self.ptr, key, v)
+        return None if rc else v.raw
+
+    def delete(self, key):
+        return lib.om_delete(self.ptr, key)
+
+    def count(self):
+        return lib.om_count(self.ptr)
+
+    def dump(self):
+        n = self.count()
+        kb = C.create_string_buffer(max(1, n * self.ksz))
+        vb = C.create_string_buffer(max(1, n * self.vsz))
+        m = lib.om_dump(self.ptr, kb, vb, n)
+        return {kb.raw[i * self.ksz:(i + 1) * self.ksz]: vb.raw[i * self.vsz:(i + 1) * self.vsz] for i in range(m)}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib.om_destroy(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def make_batch(frames, lens, src_identity=None, ifindex=None, lxc_id=None, tc_index=None, flow_hash=None):
+    """Builds an o_batch over numpy arrays (kept alive on the returned object)."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    keep = [frames]
+    b = o_batch()
+    b.n = frames.shape[0]
+    b.snap_stride = frames.shape[1]
+    b.snap = frames.ctypes.data
+
+    def arr(x, dt):
+        if x is None:
+            return None
+        a = np.ascontiguousarray(x, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data
+
+    b.len = arr(lens, np.uint32)
+    b.src_identity = arr(src_identity, np.uint32)
+    b.ifindex = arr(ifindex, np.uint32)
+    b.lxc_id = arr(lxc_id, np.uint16)
+    b.tc_index = arr(tc_index, np.uint8)
+    b.flow_hash = arr(flow_hash, np.uint32)
+    b._keep = keep
+    return b
+
+
+def parse(b):
+    n = b.n
+    out = {"ethertype": np.zeros(n, np.uint16), "saddr4": np.zeros(n, np.uint32), "daddr4": np.zeros(n, np.uint32),
+           "proto": np.zeros(n, np.uint8), "l4_off": np.zeros(n, np.int16), "l4w0": np.zeros(n, np.uint32),
+           "l4w3": np.zeros(n, np.uint16), "saddr6": np.zeros((n, 16), np.uint8), "daddr6": np.zeros((n, 16), np.uint8)}
+    c = o_cols(*[out[k].ctypes.data for k in ("ethertype", "saddr4", "daddr4", "proto", "l4_off", "l4w0", "l4w3",
+                                               "saddr6", "daddr6")])
+    lib.o_parse_batch(C.byref(b), C.byref(c))
+    return out
+
+
+def xdp(cfg, b, threads=1):
+    v = np.zeros(b.n, np.uint8)
+    if threads > 1:
+        lib.o_xdp_batch_mt(C.byref(cfg), C.byref(b), v.ctypes.data, threads)
+    else:
+        lib.o_xdp_batch(C.byref(cfg), C.byref(b), v.ctypes.data)
+    return v
+
+
+def lb(cfg, b, threads=1):
+    out = np.zeros(b.n, LB_OUT)
+    nd6 = np.zeros((b.n, 16), np.uint8)
+    if threads > 1:
+        lib.o_lb_batch_mt(C.byref(cfg), C.byref(b), out.ctypes.data, nd6.ctypes.data, threads)
+    else:
+        lib.o_lb_batch(C.byref(cfg), C.byref(b), out.ctypes.data, nd6.ctypes.data)
+    return out, nd6
+
+
+def ingress(prog_array, b, now, threads=1):
+    out = np.zeros(b.n, ING_OUT)
+    if threads > 1:
+        lib.o_ingress_batch_mt(prog_array, C.byref(b), now, out.ctypes.data, threads)
+    else:
+        lib.o_ingress_batch(prog_array, C.byref(b), now, out.ctypes.data)
+    return out
