@@ -1,0 +1,241 @@
+"""Benchmark: BASELINE config 2 — bpf_lxc ingress (ct_lookup4 + policy_can_access)
+over a steady-state stream of 16M-packet batches (4M new flows per step, each
+flow spans 4 steps), 2^20 address pairs, 4,352 identities, 256 endpoints.
+
+One step = gf_policy_ingress_classify over one batch resident in HBM (flow-group
+grouping + CT + policy + output).  N GPUs: one process per GPU, flow groups
+(unordered address pairs) sharded across ranks, tables replicated, CT
+partitioned; the only collective is the RCCL all-reduce of the counter block
+(and the timing max).
+
+Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpps classified (whole node) + % HBM roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--flows-per-step", type=int, default=4 << 20)
+    ap.add_argument("--pairs", type=int, default=1 << 20)
+    ap.add_argument("--ct-max", type=int, default=64_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from cilium_amd import synth, stream
+    from cilium_amd._lib import lib, gf_prof_rec
+    from cilium_amd.datapath import Datapath
+    import ctypes as C
+
+    W, K = max(args.warmup, 3), args.steps
+    t0 = time.time()
+    sc, P, _ = synth.config2_tables(n_pairs=args.pairs, ct_max=args.ct_max)
+    st = stream.Stream(P, rank=rank, world=world, flows_per_step=args.flows_per_step, device=dev)
+    rk, rv = st.reply_ct_entries(W + K)
+    sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
+    log(f"rank {rank}: tables {sum(m.n() for m in sc.maps.values())} entries, {len(rk)} pre-inserted CT, "
+        f"{len(st.own)} owned pairs ({time.time() - t0:.1f}s)")
+    dp = Datapath(sc, pin_prefix=None)
+    steps = []
+    for s in range(W + K):
+        cols, _, n = st.step(s)
+        steps.append((cols, n))
+    torch.cuda.synchronize()
+    log(f"rank {rank}: generated {W + K} steps ({time.time() - t0:.1f}s)")
+
+    class B:
+        pass
+
+    def batch(cols, n):
+        b = B()
+        b.n, b.device = n, dev
+        for k, v in cols.items():
+            setattr(b, k, v)
+        b.saddr6 = b.daddr6 = b.flow_hash = None
+        from cilium_amd.datapath import DeviceBatch
+        b.cols = lambda: DeviceBatch.cols(b)
+        return b
+
+    batches = [batch(c, n) for c, n in steps]
+    out = torch.empty((max(n for _, n in steps), 8), dtype=torch.uint8, device=dev)
+    now = sc.now
+    for s in range(W):
+        dp.ingress(batches[s], now + s, out=out[: batches[s].n])
+    torch.cuda.synchronize()
+    counters = torch.zeros(512, dtype=torch.int64, device=dev)
+    lib.gf_set_stats_sink(C.c_void_p(counters.data_ptr()))
+    lib.gf_prof_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for s in range(W, W + K):
+        dp.ingress(batches[s], now + s, out=out[: batches[s].n])
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    lib.gf_set_stats_sink(None)
+    recs = (gf_prof_rec * 16)()
+    nrec = lib.gf_prof_read(recs, 16)
+    lib.gf_prof_enable(0)
+    kern = {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
+    elapsed = t_end - t_start
+    local_pkts = sum(batches[s].n for s in range(W, W + K))
+    local_counters = counters.clone()
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)        # RCCL over xGMI: verdict counter block
+    elapsed = float(tt.item())
+    c = counters.cpu().numpy()
+    lc = local_counters.cpu().numpy()
+    total_pkts = int(c[268])
+    if world == 1:
+        assert total_pkts == local_pkts, (total_pkts, local_pkts)
+
+    # ---- roofline of the dominant kernel (k_ing_run), this rank ----
+    ki = kern.get("ing_levels", (0, 0.0))
+    avg_ms = ki[1] / max(ki[0], 1)
+    ab_per_launch = float(lc[270]) / max(K, 1)
+    achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    traffic_src = None
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    if pmc:
+        try:
+            j = json.load(open(pmc[-1]))
+            traffic = j.get("k_ing_run_hbm_bytes_per_launch_per_16M")
+            if traffic is not None:
+                traffic = traffic * (batches[W].n / 16_777_216.0)
+                traffic_src = os.path.relpath(pmc[-1], ROOT)
+        except Exception:
+            traffic = None
+
+    # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1 only) ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(sc, st, W, K, args.cpu_seconds)
+
+    res = {
+        "metric": METRIC,
+        "value": round(total_pkts / elapsed / 1e6, 3),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded config-2 stream generated on device; tables from cilium_amd.synth)",
+        "config": {
+            "workload": "config2: bpf_lxc ingress handle_policy (ct_lookup4 + policy_can_access), steady-state "
+                        "stream, 4M new flows/step (16M active), 256 endpoints, 4352 identities",
+            "packets_per_step_per_gpu": int(batches[W].n),
+            "address_pairs": int(args.pairs),
+            "ct_capacity": int(args.ct_max),
+            "parallelism": f"dp{world} (flow-group sharded, tables replicated, CT partitioned)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_ing_level+k_ing_tail (CT+policy stage, per step)",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": ab_per_launch,
+            "avg_launch_ms": round(avg_ms, 4),
+        },
+        "kernels_ms_per_step": {k: round(v[1] / max(v[0], 1), 4) for k, v in kern.items()},
+        "verdicts": {
+            "pass": int(c[256]), "drop": int(c[258]), "redirect": int(c[263]),
+            "ct_new": int(c[264]), "ct_established": int(c[265]), "ct_reply": int(c[266]), "ct_related": int(c[267]),
+            "drop_reasons": {str(r): int(c[r]) for r in range(1, 256) if c[r]},
+            "wire_bytes": int(c[269]),
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sc, st, W, K, seconds):
+    """Times the CPU restatement (oracle, multi-threaded, RSS-style partition by
+    flow group) on a bounded sample of the same stream: the flows of 1/8 of the
+    rank's address pairs, warmed over the same W steps, then timed step by step
+    until `seconds` of CPU wall time."""
+    import torch
+    from cilium_amd import stream
+    from oracle.scenario import OracleDP
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    ref = OracleDP(sc, shards=threads)
+    keep = None
+
+    def sample(s):
+        cols, p, n = st.step(s)
+        m = (p % 8) == 0
+        c = {k: v[m].cpu().numpy() for k, v in cols.items()}
+        to_u = {np.dtype(np.int32): np.uint32, np.dtype(np.int16): np.uint16}
+        c = {k: (v.view(to_u[v.dtype]) if v.dtype in to_u else v) for k, v in c.items()}
+        f, lens = stream.to_frames(c)
+        from cilium_amd.synth import Packets
+        return Packets(f, lens, c["src_identity"], c["ifindex"], c["lxc_id"], c["tc_index"])
+
+    for s in range(W):
+        ref.ingress(sample(s), sc.now + s, threads=threads)
+    done, tt = 0, 0.0
+    for s in range(W, W + K):
+        pk = sample(s)
+        a = time.perf_counter()
+        ref.ingress(pk, sc.now + s, threads=threads)
+        tt += time.perf_counter() - a
+        done += pk.n
+        if tt >= seconds:
+            break
+    log(f"cpu baseline: {done} packets in {tt:.2f}s on {threads} threads (setup {time.time() - t0:.1f}s)")
+    del keep
+    return {"value": round(done / tt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
+            "sample": f"{done} packets of the same config-2 stream (flows of 1/8 of the address pairs, "
+                      f"after the same {W} warm-up steps), oracle restatement, RSS-style flow-group partition"}
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,10 @@ class gf_lxc_cfg(C.Structure):
                 ("l4_ingress", gf_l4_allow * GF_MAX_L4_INGRESS)]
 
 
+class gf_prof_rec(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("count", C.c_uint32), ("pad", C.c_uint32), ("total_ms", C.c_double)]
+
+
 class gf_node_cfg(C.Structure):
     _fields_ = [("host_ifindex", C.c_uint32)]
 
@@ -102,6 +106,8 @@ _sig("gf_policy_array_update", C.c_int, C.c_int, C.c_uint32, C.c_int)
 _sig("gf_node_config", C.c_int, C.POINTER(gf_node_cfg))
 _sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c_uint32, VP, VP)
 _sig("gf_set_stats_sink", C.c_int, VP)
+_sig("gf_prof_enable", C.c_int, C.c_int)
+_sig("gf_prof_read", C.c_int, C.POINTER(gf_prof_rec), C.c_int)
 _sig("gf_dev_alloc", VP, C.c_size_t)
 _sig("gf_dev_free", C.c_int, VP)
 _sig("gf_memcpy_h2d", C.c_int, VP, VP, C.c_size_t, VP)
@@ -117,6 +123,6 @@ EXPORTED = [
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_set_stats_sink", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
 ]

@@ -5,8 +5,10 @@
 //   k_lb        bpf/bpf_lb.c:58-212 + lib/lb.h      one packet per lane
 //   k_ing_pack  columns -> 32-B records + flow-group key (unordered addr pair)
 //   (rocPRIM stable radix sort of (group, index) + exclusive scan)
-//   k_ing_run   bpf/bpf_lxc.c:745-1024 handle_policy: one flow-group queue per
-//               lane, packets of a queue in batch order (CT ordering rule)
+//   k_bucket_*  bucket-size histogram + count-descending bucket order
+//   k_ing_level bpf/bpf_lxc.c:745-1024 handle_policy, level-synchronous: launch k
+//               runs the k-th packet of every flow-group bucket (CT ordering rule)
+//   k_ing_tail  the remaining ranks of the few deepest buckets, sequentially
 #include "gf_internal.h"
 #include "gf_device.h"
 #include <rocprim/device/device_radix_sort.hpp>
@@ -41,6 +43,11 @@ struct Stats {
         __syncthreads();
     }
     __device__ void add(uint32_t bin) { atomicAdd(&lds[bin], 1u); }
+    __device__ void add_n(uint32_t bin, uint32_t v) { if (v) atomicAdd(&lds[bin], v); }
+    // one packet: reason/action bins + packets, wire bytes, algorithmic bytes
+    __device__ void pkt(uint32_t reason, uint32_t action, uint32_t len, uint32_t ab) {
+        add(reason); add(256 + action); add(268); add_n(269, len); add_n(270, ab);
+    }
     __device__ void flush(unsigned long long *g) {
         __syncthreads();
         for (int k = threadIdx.x; k < 272; k += blockDim.x)
@@ -138,16 +145,20 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
         uint32_t len = c.len[i];
         uint32_t et = c.ethertype[i];
         uint8_t v;
+        uint32_t ab = 1;                                  // output record
         if (len < 14) v = XDP_DROP_;
         else if (et == 0x0800) {
             if (len < 34) v = XDP_DROP_;
             else {
                 uint32_t sa = c.saddr4[i];
                 bool drop = false;
+                ab += 10;
                 if (x.has_h4) {
+                    ab += 9;
                     if (trie_lookup(x.l4, &sa)) drop = true;
-                    else { uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
+                    else { ab += 9; uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
                 }
+                if (!drop) ab += 20;
                 v = drop ? XDP_DROP_ : (lxc_has4(x.lxc, c.daddr4[i]) ? XDP_PASS_ : XDP_DROP_);
             }
         } else if (et == 0x86DD) {
@@ -156,12 +167,15 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
                 uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
                 uint32_t sw[4] = {s.x, s.y, s.z, s.w};
                 bool drop = false;
+                ab += 34;
                 if (x.has_h6) {
+                    ab += 21;
                     if (trie_lookup(x.l6, sw)) drop = true;
-                    else { uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
+                    else { ab += 21; uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
                 }
                 if (drop) v = XDP_DROP_;
                 else {
+                    ab += 20;
                     uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
                     uint32_t dw[4] = {d.x, d.y, d.z, d.w};
                     v = lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
@@ -169,7 +183,7 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
             }
         } else v = XDP_PASS_;
         verdict[i] = v;
-        if (stats) st.add(256 + v);
+        if (stats) st.pkt(v == XDP_DROP_ ? 1u : 0u, v, len, ab);
     }
     if (stats) st.flush(stats);
 }
@@ -193,7 +207,7 @@ __device__ __forceinline__ int lb_checks(const LbDev &L, uint32_t len, int l4_of
 }
 
 // returns program result (TC_OK pass / TC_REDIRECT translated / negative error)
-__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o) {
+__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t &ab) {
     if (len < 34) return D_INVALID;
     uint32_t nh = c.proto[i], daddr = c.daddr4[i];
     int l4_off = c.l4_off[i];
@@ -208,12 +222,14 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     if ((L.flags & GF_LB_F_L4) && dport) {
         uint32_t kw[2] = {daddr, dport};
         int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+        ab += 20;
         if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
         if (!svc) dport = 0;
     }
     if (!svc && (L.flags & GF_LB_F_L3)) {
         uint32_t kw[2] = {daddr, dport};
         int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+        ab += 20;
         if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
     }
     if (!svc) return TC_OK;
@@ -221,6 +237,7 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
     uint32_t kw[2] = {daddr, dport | (slave << 16)};
     int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
+    ab += 20;
     if (f < 0) return D_NO_SERVICE;
     const uint8_t *be = ht_val(L.s4, f);
     uint32_t target = *reinterpret_cast<const uint32_t *>(be);
@@ -233,7 +250,8 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     return TC_REDIRECT;
 }
 
-__device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t *nd6) {
+__device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t *nd6,
+                     uint32_t &ab) {
     if (len < 54 || !c.daddr6) return D_INVALID;
     uint32_t nh = c.proto[i];
     int l4_off = c.l4_off[i];
@@ -249,12 +267,14 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     if ((L.flags & GF_LB_F_L4) && dport) {
         uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
         int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+        ab += 44;
         if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
         if (!svc) dport = 0;
     }
     if (!svc && (L.flags & GF_LB_F_L3)) {
         uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
         int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+        ab += 44;
         if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
     }
     if (!svc) return TC_OK;
@@ -262,6 +282,7 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
     uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport | (slave << 16)};
     int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
+    ab += 44;
     if (f < 0) return D_NO_SERVICE;
     const uint8_t *be = ht_val(L.s6, f);
     uint32_t t[4];
@@ -288,8 +309,9 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         uint32_t len = c.len[i], et = c.ethertype[i];
         int ret = TC_OK;
         bool v6 = false;
-        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ret = lb_v6(L, c, i, len, o, n6); } }
-        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o); }
+        uint32_t ab = 12 + 12;                            // header columns + output record
+        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(L, c, i, len, o, n6, ab); } }
+        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o, ab); }
         if (ret < 0 || ret == TC_SHOT) {
             o = gf_lb_out{};
             o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -300,7 +322,7 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         out[i] = o;
         if (nd6 && v6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
         else if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(0, 0, 0, 0);
-        if (stats) { st.add(o.reason); st.add(256 + o.action); }
+        if (stats) st.pkt(o.reason, o.action, len, ab);
     }
     if (stats) st.flush(stats);
 }
@@ -319,9 +341,11 @@ struct CtState { uint32_t rev_nat, loopback; };
 // __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS)
 template <int KSZ>
 __device__ __forceinline__ int ct_probe(const gf_htab_desc &d, const uint32_t *kw, int action, bool syn,
-                                        uint32_t len, uint32_t now, bool acct, CtState &st) {
+                                        uint32_t len, uint32_t now, bool acct, CtState &st, uint32_t &ab) {
     int64_t f = ht_find<KSZ>(d, kw, key_hash<KSZ>(kw));
+    ab += KSZ;
     if (f < 0) return CT_NEW;
+    ab += 96;                                           // entry RMW: 48 B read + 48 B written
     uint8_t *e = ht_val(d, (uint64_t)f);
     uint4 c = *reinterpret_cast<uint4 *>(e + 32);       // lifetime, flags|rev_nat, unused, src_sec_id
     uint32_t life = c.x, fl = c.y & 0xffffu, rn = c.y >> 16;
@@ -355,8 +379,9 @@ __device__ __forceinline__ int ct_probe(const gf_htab_desc &d, const uint32_t *k
 // ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0)
 template <int KSZ, int TW>
 __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
-                                         uint32_t len, uint32_t now, bool strict, int *added) {
-    constexpr int NHW = TW - 1;                        // word holding nexthdr | flags << 8
+                                         uint32_t len, uint32_t now, bool strict, int *added, uint32_t &ab) {
+    constexpr int NHW = TW - 1;
+    ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written                        // word holding nexthdr | flags << 8
     uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
     uint32_t fl = (nh == 6) ? 0u : F_SEEN_NON_SYN;      // ct_update_timeout(syn = nexthdr == TCP)
     uint32_t life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
@@ -394,7 +419,7 @@ __device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, u
 
 // __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168)
 __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t identity, uint32_t dport,
-                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr) {
+                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab) {
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
     const gf_htab_desc pd = c->policy;
@@ -402,20 +427,24 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
     if (flags & GF_LXC_F_HAVE_L4_POLICY) {
         uint32_t kw[2] = {identity, dport | (proto << 16)};
         f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        ab += 8;
         if (f >= 0) goto proxy;
     }
     {
         uint32_t kw[2] = {identity, 0u};
         f = ht_find<8>(pd, kw, key_hash<8>(kw));
-        if (f >= 0) { policy_count(pd, f, len); return TC_OK; }
+        ab += 8;
+        if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
     }
     if (flags & GF_LXC_F_HAVE_L4_POLICY) {
         uint32_t kw[2] = {0u, dport | (proto << 16)};
         f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        ab += 8;
         if (f >= 0) goto proxy;
     }
     goto deny;
 proxy: {
+        ab += 40;                                       // entry read + counters written
         policy_count(pd, f, len);
         uint32_t pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
@@ -423,8 +452,8 @@ proxy: {
     }
 deny:
     if (identity < 256) {                               // identity_is_reserved
-        if (v6) { if (trie_lookup(c->cidr6, cidr_addr)) return TC_OK; }
-        else { if (trie_lookup(c->cidr4, cidr_addr)) return TC_OK; }
+        if (v6) { if (c->cidr6.root_bits) ab += 21; if (trie_lookup(c->cidr6, cidr_addr)) return TC_OK; }
+        else { if (c->cidr4.root_bits) ab += 9; if (trie_lookup(c->cidr4, cidr_addr)) return TC_OK; }
     }
     return D_POLICY;
 }
@@ -497,7 +526,7 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, int &fwd,
-                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added) {
+                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
     uint32_t nh = r.proto;
@@ -510,7 +539,7 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     const gf_htab_desc ct = c->ct4;
     CtState st{0, 0};
-    int ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st);
+    int ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st, ab);
     if (ret != CT_NEW) {
         ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
     } else {
@@ -518,13 +547,14 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
         t[2] = (t[2] >> 16) | (t[2] << 16);
         tfl ^= 1u;
         t[3] = nh | (tfl << 8);
-        ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st);
+        ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st, ab);
     }
     fwd = ret;
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
         const gf_htab_desc rn = c->revnat4;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
+        ab += 8;
         if (f >= 0) {
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 4), r.l4w0, false);
@@ -533,14 +563,14 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
         }
     }
     uint32_t orig_sip = r.saddr;
-    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip);
+    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) ht_delete<14>(ct, t, X.strict & 1, added);
+        if (ret == CT_ESTABLISHED) { ab += 14; ht_delete<14>(ct, t, X.strict & 1, added); }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;                         // skip_proxy
     if (ret == CT_NEW) {
-        ret = ct_create<14, 4>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, added);
+        ret = ct_create<14, 4>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, added, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -556,7 +586,7 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
 
 // ipv6_policy, bpf/bpf_lxc.c:745-862
 __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, uint32_t i,
-                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added) {
+                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab) {
     uint32_t len = r.len;
     if (len < 54) return D_INVALID;
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
@@ -575,7 +605,7 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     const gf_htab_desc ct = c->ct6;
     CtState st{0, 0};
-    int ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st);
+    int ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st, ab);
     if (ret != CT_NEW) {
         ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
     } else {
@@ -583,27 +613,28 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
         t[8] = (t[8] >> 16) | (t[8] << 16);
         tfl ^= 1u;
         t[9] = nh | (tfl << 8);
-        ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st);
+        ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st, ab);
     }
     fwd = ret;
     if (st.rev_nat) {
         const gf_htab_desc rn = c->revnat6;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
+        ab += 20;
         if (f >= 0) {
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 16), r.l4w0, true);
             if (r2 < 0) return r2;
         }
     }
-    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4);
+    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) ht_delete<40>(ct, t, X.strict & 1, added);
+        if (ret == CT_ESTABLISHED) { ab += 40; ht_delete<40>(ct, t, X.strict & 1, added); }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;
     if (ret == CT_NEW) {
-        ret = ct_create<40, 10>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, added);
+        ret = ct_create<40, 10>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, added, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -618,7 +649,8 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
 }
 
 // handle_policy, bpf/bpf_lxc.c:980-1024
-__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, int *added) {
+__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, int *added,
+                                                       uint32_t &ab) {
     gf_ingress_out o{};
     uint32_t sl = X.slot_of[r.lxc_id];
     if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }
@@ -630,8 +662,8 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     uint32_t ifindex = r.ifindex;
     uint32_t cls = r.cls & 3u;
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
-    else if (cls == 2) ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added);
-    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added);
+    else if (cls == 2) { ab += 47; ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added, ab); }
+    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) { ab += 23; ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added, ab); }
     else ret = D_UNKNOWN_L3;
     o.ct_ret = (uint8_t)fwd;
     if (ret < 0 || ret == TC_SHOT) {
@@ -663,7 +695,12 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmas
     if (c.tc_index && (c.tc_index[i] & 1)) cls |= 4u;
     r.cls = (uint8_t)cls;
     uint32_t h;
-    if ((cls & 3) == 2 && c.saddr6) {
+    // Only packets that can reach conntrack (an IP header is present) are bound to
+    // their flow group; the rest carry no ordering constraint and are spread out.
+    bool ct_ok = ((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6);
+    if (!ct_ok) {
+        h = gf_hash_words(&i, 1, 4);
+    } else if ((cls & 3) == 2) {
         uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
         uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
         uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
@@ -678,37 +715,147 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmas
     atomicAdd(&cnt[q], 1u);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ing_run(IngCtx X, uint32_t nq, const uint32_t *off, const uint32_t *cnt,
-                                                   const uint32_t *perm, const gf_rec *rec, gf_ingress_out *out,
-                                                   uint32_t *ct4_count, uint32_t *ct6_count,
-                                                   unsigned long long *stats) {
+// Level-synchronous schedule over flow-group buckets: launch k processes the
+// k-th packet (batch order) of every bucket with more than k packets, one
+// packet per lane.  Buckets are ordered by packet count (descending), so the
+// active buckets of level k are order[0 .. A_k).  Packets of one bucket are
+// therefore handled in batch order, and different buckets (disjoint CT keys)
+// run concurrently — the CT ordering rule of DESIGN.md.
+__device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec *rec, gf_ingress_out *out,
+                                        Stats &st, bool stats, int &added) {
+    gf_rec r = rec[i];
+    uint32_t ab = 8;                                    // output record
+    gf_ingress_out o = handle_policy(X, r, i, &added, ab);
+    out[i] = o;
+    if (stats) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
+}
+
+__device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t *ct_count, uint32_t *lds_added) {
+    if (X.strict & 1) return;
+    if (added) atomicAdd(lds_added, (uint32_t)added);
+    __syncthreads();
+    if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ing_level(IngCtx X, uint32_t level, uint32_t active, const uint32_t *order,
+                                                     const uint32_t *off, const uint32_t *perm, const gf_rec *rec,
+                                                     gf_ingress_out *out, uint32_t *ct_count,
+                                                     unsigned long long *stats) {
     __shared__ uint32_t sl[272];
+    __shared__ uint32_t sadd;
     Stats st{sl};
-    if (stats) st.init();
-    uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (threadIdx.x == 0) sadd = 0;
+    if (stats) st.init(); else __syncthreads();
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     int added = 0;
-    if (q < nq) {
-        uint32_t b = off[q], e = b + cnt[q];
-        for (uint32_t j = b; j < e; j++) {
-            uint32_t i = perm[j];
-            gf_rec r = rec[i];
-            gf_ingress_out o = handle_policy(X, r, i, &added);
-            out[i] = o;
-            if (stats) { st.add(o.reason); st.add(256 + o.action); st.add(264 + (o.ct_ret & 3)); }
-        }
-    }
-    // Net CT element-count change (non-strict mode); CT maps of one batch share the
-    // counter of the map the packets used (ct4 for v4, ct6 for v6 are accounted together
-    // when they are the same map; see gf_policy_ingress_classify).
-    if (!(X.strict & 1) && added && ct4_count) atomicAdd(ct4_count, (uint32_t)added);
+    if (t < active) ing_one(X, perm[off[order[t]] + level], rec, out, st, stats != nullptr, added);
+    flush_added(X, added, ct_count, &sadd);
     if (stats) st.flush(stats);
+}
+
+// Remaining ranks [level, cnt) of the few deep buckets: one bucket per lane.
+__global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, uint32_t active, const uint32_t *order,
+                                                    const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
+                                                    const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
+                                                    unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    __shared__ uint32_t sadd;
+    Stats st{sl};
+    if (threadIdx.x == 0) sadd = 0;
+    if (stats) st.init(); else __syncthreads();
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    int added = 0;
+    if (t < active) {
+        uint32_t q = order[t], b = off[q], e = b + cnt[q];
+        for (uint32_t j = b + level; j < e; j++) ing_one(X, perm[j], rec, out, st, stats != nullptr, added);
+    }
+    flush_added(X, added, ct_count, &sadd);
+    if (stats) st.flush(stats);
+}
+
+#define GF_LCAP 1024u
+// Bucket-size histogram: block-local LDS bins, one global add per non-empty bin.
+#define GF_SCHED_ITEMS 4096
+__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, uint32_t nq, uint32_t *hist) {
+    __shared__ uint32_t h[GF_LCAP + 1];
+    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
+        uint32_t c = cnt[q];
+        if (c) atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+// order[] = non-empty buckets sorted by count, descending (ties in any order):
+// block-local counts per bin, one global reservation per (block, bin).
+__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, uint32_t nq, const uint32_t *base,
+                                                        uint32_t *cursor, uint32_t *order) {
+    __shared__ uint32_t h[GF_LCAP + 1];
+    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
+        uint32_t c = cnt[q];
+        if (c) atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x)
+        if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
+    __syncthreads();
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
+        uint32_t c = cnt[q];
+        if (c) order[atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u)] = q;
+    }
 }
 
 // ================================================================ host: programs
 namespace {
 
+// ---- launch profiler: HIP events on the launch stream around each kernel ----
+struct ProfEntry { std::string name; hipEvent_t a, b; };
+struct Prof {
+    bool on = false;
+    std::vector<ProfEntry> pending;
+    std::map<std::string, std::pair<uint32_t, double>> acc;
+};
+Prof &prof() { static Prof p; return p; }
+struct ProfScope {
+    ProfEntry e{};
+    bool on;
+    hipStream_t s;
+    ProfScope(const char *n, hipStream_t s_) : on(prof().on), s(s_) {
+        if (!on) return;
+        e.name = n;
+        (void)hipEventCreate(&e.a);
+        (void)hipEventCreate(&e.b);
+        (void)hipEventRecord(e.a, s);
+    }
+    ~ProfScope() {
+        if (!on) return;
+        (void)hipEventRecord(e.b, s);
+        prof().pending.push_back(e);
+    }
+};
+void prof_drain() {
+    for (auto &e : prof().pending) {
+        float ms = 0;
+        if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+            auto &a = prof().acc[e.name];
+            a.first++;
+            a.second += ms;
+        }
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    prof().pending.clear();
+}
+
 struct Workspace {
-    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp;
+    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp, hist, base, order;
 };
 Workspace &ws() { static Workspace w; return w; }
 
@@ -738,6 +885,7 @@ int gf_parse_frames(const gf_frames *fr, gf_pkt_cols_out *o, void *stream) {
         !o->l4w0 || !o->l4w3)
         return -EFAULT;
     if (fr->snap_stride < 14) return -EINVAL;
+    ProfScope ps("k_parse", (hipStream_t)stream);
     hipLaunchKernelGGL(k_parse, dim3(grid_for(fr->n)), dim3(BLOCK), 0, (hipStream_t)stream, *fr, *o);
     return hip_ok(hipGetLastError(), "k_parse");
 }
@@ -784,6 +932,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     if (p->m4l) x.l4 = p->m4l->tdesc();
     if (p->m6l) x.l6 = p->m6l->tdesc();
     x.lxc = p->lxc->hdesc();
+    ProfScope ps("k_xdp", s);
     hipLaunchKernelGGL(k_xdp, dim3(grid_for(pkts->n)), dim3(BLOCK), 0, s, *pkts, x, verdict,
                        (unsigned long long *)stats_sink());
     return hip_ok(hipGetLastError(), "k_xdp");
@@ -822,6 +971,7 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
     if (p->lb4) L.s4 = p->lb4->hdesc();
     if (p->lb6) L.s6 = p->lb6->hdesc();
     L.flags = p->cfg.flags;
+    ProfScope ps("k_lb", s);
     hipLaunchKernelGGL(k_lb, dim3(grid_for(pkts->n)), dim3(BLOCK), 0, s, *pkts, L, out, nd6,
                        (unsigned long long *)stats_sink());
     return hip_ok(hipGetLastError(), "k_lb");
@@ -850,6 +1000,30 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
     if (p->ct4) p->ct4->make_fixed_capacity();
     if (p->ct6) p->ct6->make_fixed_capacity();
     return new_handle(p);
+}
+
+int gf_prof_enable(int on) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    prof_drain();
+    prof().acc.clear();
+    prof().on = on != 0;
+    return 0;
+}
+
+int gf_prof_read(gf_prof_rec *out, int max) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (max < 0 || (max > 0 && !out)) return -EFAULT;
+    prof_drain();
+    int k = 0;
+    for (auto &kv : prof().acc) {
+        if (k >= max) break;
+        memset(&out[k], 0, sizeof out[k]);
+        strncpy(out[k].name, kv.first.c_str(), sizeof(out[k].name) - 1);
+        out[k].count = kv.second.first;
+        out[k].total_ms = kv.second.second;
+        k++;
+    }
+    return k;
 }
 
 int gf_policy_array_create(void) {
@@ -928,7 +1102,10 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
         if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
     }
     if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
-    // strict (exact max_entries accounting) only when a batch could fill a CT map
+    // Strict (exact, atomic per insert) element accounting only when this batch could
+    // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
+    // fail in the kernel (they evict); here they keep entries past max_entries until
+    // GC and are bounded only by the slot array (7/8 load), see DESIGN.md.
     uint32_t strict = 0;
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
@@ -938,7 +1115,12 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
             if (hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count")) return -EIO;
             upper = dc;
         }
-        if (upper + 2ull * pkts->n > m->max_entries) strict = 1;
+        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
+        if (upper + 2ull * pkts->n > limit) strict = 1;
+        if (m->type == GF_MAP_TYPE_LRU_HASH) {
+            if (m == ct4m) { for (auto &d : cfgs) d.ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
+            else { for (auto &d : cfgs) d.ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
+        }
     }
     if (a->dirty || a->d_cfgs.bytes != cfgs.size() * sizeof(gf_lxc_dev) || true) {
         if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
@@ -951,14 +1133,17 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     }
     // 2. group by flow group (stable radix sort of (group, index))
     uint32_t n = pkts->n;
+    // ~4 buckets per expected flow group keeps bucket collisions (two groups in one
+    // bucket => serialized) rare; 2^22 buckets cover 2^20 address pairs.
     uint32_t qbits = 10;
-    while (qbits < 22 && (1u << qbits) * 48u < n) qbits++;
+    while (qbits < 22 && (1u << qbits) * 4u < n) qbits++;
     uint32_t nq = 1u << qbits;
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
         (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
-        (r = grow(w.cnt, (size_t)nq * 4)) || (r = grow(w.off, (size_t)nq * 4)))
+        (r = grow(w.cnt, (size_t)nq * 4)) || (r = grow(w.off, (size_t)nq * 4)) || (r = grow(w.order, (size_t)nq * 4)) ||
+        (r = grow(w.hist, (GF_LCAP + 1) * 8)) || (r = grow(w.base, (GF_LCAP + 1) * 4)))
         return r;
     (void)any_v6;   // IPv6 packets in a batch without v6 columns are dropped (DROP_INVALID)
     size_t sort_bytes = 0, scan_bytes = 0;
@@ -968,17 +1153,26 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
                             rocprim::plus<uint32_t>(), s);
     if ((r = grow(w.tmp, std::max(sort_bytes, scan_bytes) + 256))) return r;
     if (hip_ok(hipMemsetAsync(w.cnt.p, 0, (size_t)nq * 4, s), "memset cnt")) return -EIO;
-    hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, nq - 1,
-                       (gf_rec *)w.rec.p, (uint32_t *)w.keys.p, (uint32_t *)w.vals.p, (uint32_t *)w.cnt.p);
+    {
+        ProfScope ps("k_ing_pack", s);
+        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, nq - 1,
+                           (gf_rec *)w.rec.p, (uint32_t *)w.keys.p, (uint32_t *)w.vals.p, (uint32_t *)w.cnt.p);
+    }
     if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     size_t tb = w.tmp.bytes;
-    if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
-                                         (uint32_t *)w.perm.p, n, 0, qbits, s), "radix_sort_pairs"))
-        return -EIO;
+    {
+        ProfScope ps("rocprim_radix_sort", s);
+        if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
+                                             (uint32_t *)w.perm.p, n, 0, qbits, s), "radix_sort_pairs"))
+            return -EIO;
+    }
     tb = w.tmp.bytes;
-    if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
-                                       rocprim::plus<uint32_t>(), s), "exclusive_scan"))
-        return -EIO;
+    {
+        ProfScope ps("rocprim_exclusive_scan", s);
+        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
+                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
+            return -EIO;
+    }
     // 3. run handle_policy per flow-group queue
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
@@ -989,11 +1183,49 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     // Non-strict mode accounts the net element change per map; with both families
     // present each lane's `added` mixes them, so v6 batches use strict mode.
     if (ct4m && ct6m) X.strict = 1;
-    uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : (ct6m ? (uint32_t *)ct6m->d_count.p : nullptr);
-    hipLaunchKernelGGL(k_ing_run, dim3((nq + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, nq, (const uint32_t *)w.off.p,
-                       (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cnt4,
-                       (uint32_t *)nullptr, (unsigned long long *)stats_sink());
-    if ((r = hip_ok(hipGetLastError(), "k_ing_run"))) return r;
+    uint32_t *cntp = ct4m ? (uint32_t *)ct4m->d_count.p : (ct6m ? (uint32_t *)ct6m->d_count.p : nullptr);
+    unsigned long long *sink = (unsigned long long *)stats_sink();
+    // 4. bucket schedule: histogram of bucket sizes -> per-level active counts
+    {
+        ProfScope ps("k_bucket_sched", s);
+        if (hip_ok(hipMemsetAsync(w.hist.p, 0, (GF_LCAP + 1) * 8, s), "memset hist")) return -EIO;
+        hipLaunchKernelGGL(k_bucket_hist, dim3((nq + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
+                           nq, (uint32_t *)w.hist.p);
+    }
+    std::vector<uint32_t> hist(GF_LCAP + 1), base(GF_LCAP + 1), active(GF_LCAP + 1);
+    if (hip_ok(hipMemcpyAsync(hist.data(), w.hist.p, (GF_LCAP + 1) * 4, hipMemcpyDeviceToHost, s), "hist d2h") ||
+        hip_ok(hipStreamSynchronize(s), "hist sync"))
+        return -EIO;
+    uint32_t acc = 0, maxc = 0;
+    for (int c = (int)GF_LCAP; c >= 1; c--) { base[c] = acc; acc += hist[c]; if (hist[c] && !maxc) maxc = (uint32_t)c; }
+    {   // active[k] = buckets with count > k
+        uint32_t a = 0;
+        for (int c = (int)GF_LCAP; c >= 1; c--) { a += hist[c]; active[c - 1] = a; }
+    }
+    if (hip_ok(hipMemcpyAsync(w.base.p, base.data(), (GF_LCAP + 1) * 4, hipMemcpyHostToDevice, s), "base h2d") ||
+        hip_ok(hipMemsetAsync((uint8_t *)w.hist.p + (GF_LCAP + 1) * 4, 0, (GF_LCAP + 1) * 4, s), "cursor"))
+        return -EIO;
+    {
+        ProfScope ps("k_bucket_sched", s);
+        hipLaunchKernelGGL(k_bucket_order, dim3((nq + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
+                           nq, (const uint32_t *)w.base.p, (uint32_t *)w.hist.p + (GF_LCAP + 1), (uint32_t *)w.order.p);
+    }
+    if ((r = hip_ok(hipGetLastError(), "k_bucket_order"))) return r;
+    // 5. levels while there is enough parallelism, then one sequential tail launch
+    const uint32_t tail_below = 16384;
+    uint32_t k = 0;
+    {
+        ProfScope ps("ing_levels", s);
+        for (; k < maxc && k < GF_LCAP && active[k] >= tail_below; k++)
+            hipLaunchKernelGGL(k_ing_level, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k],
+                               (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.perm.p,
+                               (const gf_rec *)w.rec.p, out, cntp, sink);
+        if (k < maxc)
+            hipLaunchKernelGGL(k_ing_tail, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k],
+                               (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
+                               (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cntp, sink);
+    }
+    if ((r = hip_ok(hipGetLastError(), "k_ing_level"))) return r;
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }

@@ -500,10 +500,11 @@ def _interleave(rng, n_flows, k, start_spread):
     return np.argsort(key, kind="stable")
 
 
-def config2(n_flows=16_777_216, n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000, n_l4=4000, n_wc=32, n_cidr=128,
-            pkts_per_flow=4, warm_frac=0.5, seed=0xC1D40002, stride=64, ct_max=48_000_000, proxy_frac=0.10,
-            reply_frac=0.05, related_frac=0.01, unk_frac=0.005, trunc_frac=0.005, now=100_000):
-    """BASELINE config 2 / SURVEY §8(d): bpf_lxc ingress, ct_lookup4 + policy."""
+def config2_tables(n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000, n_l4=4000, n_wc=32, n_cidr=128,
+                   seed=0xC1D40002, ct_max=48_000_000, proxy_frac=0.10, now=100_000):
+    """Tables of BASELINE config 2 (256 endpoints, 4k identities, per-endpoint
+    policy/CIDR maps, global CT) and the address-pair population.  Returns
+    (scenario, pairs, rng)."""
     rng = np.random.default_rng(seed)
     sc = Scenario("config2_ingress", now=now)
     ep_ip = (ip4("10.1.0.0") + 1 + np.arange(n_ep)).astype(np.uint32)
@@ -569,6 +570,19 @@ def config2(n_flows=16_777_216, n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000
         sc.lxc.append({"lxc_id": int(lxc_id[e]), "seclabel": 256 + e, "policy": pname, "ct4": "cilium_ct4_global",
                        "ct6": None, "cidr4": cname, "cidr6": None, "revnat4": "cilium_lb4_reverse_nat",
                        "revnat6": None, "flags": LXC_PRODUCTION, "l4": l4cfg})
+    pairs = dict(pe=pe, cls=cls, pid=pid, port1=port1, port2=port2, raddr=raddr, ep_ip=ep_ip, lxc_id=lxc_id,
+                 ifidx=ifidx)
+    return sc, pairs, rng
+
+
+def config2(n_flows=16_777_216, n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000, n_l4=4000, n_wc=32, n_cidr=128,
+            pkts_per_flow=4, warm_frac=0.5, seed=0xC1D40002, stride=64, ct_max=48_000_000, proxy_frac=0.10,
+            reply_frac=0.05, related_frac=0.01, unk_frac=0.005, trunc_frac=0.005, now=100_000):
+    """BASELINE config 2 / SURVEY §8(d): bpf_lxc ingress, ct_lookup4 + policy.
+    Host-generated frames (parity tests); the bench uses cilium_amd.stream."""
+    sc, P, rng = config2_tables(n_pairs, n_ep, n_ids, n_l3, n_l4, n_wc, n_cidr, seed, ct_max, proxy_frac, now)
+    pe, cls, pid, port1, port2, raddr = P["pe"], P["cls"], P["pid"], P["port1"], P["port2"], P["raddr"]
+    ep_ip, lxc_id, ifidx = P["ep_ip"], P["lxc_id"], P["ifidx"]
     # ---- flows
     fp = rng.integers(0, n_pairs, n_flows)
     fe = pe[fp]

@@ -283,9 +283,20 @@ int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
 #define GF_STATS_WORDS 512
 /* Adds the counters of the next classify calls into `dev_counters`
  * (GF_STATS_WORDS u64 in DEVICE memory; NULL disables). Layout:
- * [0..255] drop-reason histogram, [256..263] action counts,
- * [264..267] CT ret counts, [268] packets, [269] bytes. */
+ * [0..255] drop-reason histogram (reason 0 = not dropped), [256..263]
+ * action counts, [264..267] CT ret counts, [268] packets, [269] wire bytes,
+ * [270] algorithmic bytes touched (per-probe costs of SURVEY.md §8(d)). */
 int gf_set_stats_sink(uint64_t *dev_counters);
+
+/* ---- launch profiler (HIP events recorded on the launch stream) ---- */
+typedef struct gf_prof_rec {
+    char     name[32];     /* kernel / primitive name */
+    uint32_t count;        /* launches since gf_prof_enable */
+    uint32_t pad;
+    double   total_ms;     /* summed event-measured duration */
+} gf_prof_rec;
+int gf_prof_enable(int on);                       /* clears accumulators */
+int gf_prof_read(gf_prof_rec *out, int max);      /* returns records written */
 
 /* ---- device memory helpers for hosts without a GPU runtime binding ---- */
 void *gf_dev_alloc(size_t bytes);

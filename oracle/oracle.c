@@ -1107,6 +1107,9 @@ typedef struct mt_arg {
     const o_prog_array *a; const o_batch *b; uint32_t now; o_ingress_out *out;
     const o_xdp_cfg *xc; uint8_t *verdict; const o_lb_cfg *lc; o_lb_out *lo; uint8_t *nd6;
     uint32_t tid, nthreads; int kind;
+    /* ingress partition (RSS-style): owner[], per-slice counts, per-owner lists */
+    uint32_t *owner, *cnt, *list, *start;
+    int phase;
 } mt_arg;
 
 static uint32_t pkt_group(const o_batch *b, uint32_t i) {
@@ -1117,18 +1120,27 @@ static uint32_t pkt_group(const o_batch *b, uint32_t i) {
         return o_ct_pair_hash4(sa, da);
     }
     if (cap >= 54 && d[12] == 0x86 && d[13] == 0xDD) return o_ct_pair_hash6(d + 22, d + 38);
-    return 0;
+    return i * 2654435761u;              /* no CT access: no ordering constraint */
 }
 
 static void *mt_worker(void *p) {
     mt_arg *m = (mt_arg *)p;
     const o_batch *b = m->b;
+    uint32_t T = m->nthreads, t = m->tid;
+    uint32_t lo = (uint32_t)((uint64_t)b->n * t / T), hi = (uint32_t)((uint64_t)b->n * (t + 1) / T);
     if (m->kind == 0) {
-        for (uint32_t i = 0; i < b->n; i++)
-            if (pkt_group(b, i) % m->nthreads == m->tid) handle_policy(m->a, b, i, m->now, &m->out[i]);
+        if (m->phase == 0) {                 /* group -> owner thread, counts per (slice, owner) */
+            uint32_t *c = m->cnt + (size_t)t * T;
+            for (uint32_t i = lo; i < hi; i++) { uint32_t o = pkt_group(b, i) % T; m->owner[i] = o; c[o]++; }
+        } else if (m->phase == 1) {          /* stable scatter into per-owner lists */
+            uint32_t pos[1024];
+            for (uint32_t u = 0; u < T; u++) pos[u] = m->start[(size_t)t * T + u];
+            for (uint32_t i = lo; i < hi; i++) m->list[pos[m->owner[i]]++] = i;
+        } else {                             /* each owner runs its flow groups in batch order */
+            uint32_t a0 = m->start[t], a1 = m->start[T * T + t];
+            for (uint32_t k = a0; k < a1; k++) handle_policy(m->a, b, m->list[k], m->now, &m->out[m->list[k]]);
+        }
     } else {
-        uint32_t lo = (uint32_t)((uint64_t)b->n * m->tid / m->nthreads);
-        uint32_t hi = (uint32_t)((uint64_t)b->n * (m->tid + 1) / m->nthreads);
         for (uint32_t i = lo; i < hi; i++) {
             skb_t s; skb_init(&s, b, i);
             if (m->kind == 1) m->verdict[i] = (uint8_t)xdp_start(m->xc, &s);
@@ -1151,9 +1163,29 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
 }
 
 void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 1024) threads = 1024;
+    uint32_t T = threads;
     mt_arg m; memset(&m, 0, sizeof m);
     m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0;
-    run_mt(&m, threads);
+    m.owner = (uint32_t *)malloc((size_t)b->n * 4 + 4);
+    m.list = (uint32_t *)malloc((size_t)b->n * 4 + 4);
+    m.cnt = (uint32_t *)calloc((size_t)T * T, 4);
+    /* start: [slice t][owner u] write offsets, then row T*T.. : owner begin/end */
+    m.start = (uint32_t *)calloc((size_t)T * T + T + 1, 4);
+    m.phase = 0; run_mt(&m, T);
+    uint32_t acc = 0;
+    for (uint32_t u = 0; u < T; u++) {
+        for (uint32_t t = 0; t < T; t++) { m.start[(size_t)t * T + u] = acc; acc += m.cnt[(size_t)t * T + u]; }
+    }
+    /* owner ranges: begin = start[0*T+u] (slice 0 offset), end = begin of owner u+1 */
+    uint32_t *beg = (uint32_t *)malloc((T + 1) * 4);
+    for (uint32_t u = 0; u < T; u++) beg[u] = m.start[u];
+    beg[T] = acc;
+    m.phase = 1; run_mt(&m, T);
+    for (uint32_t u = 0; u < T; u++) { m.start[u] = beg[u]; m.start[(size_t)T * T + u] = beg[u + 1]; }
+    m.phase = 2; run_mt(&m, T);
+    free(beg); free(m.owner); free(m.list); free(m.cnt); free(m.start);
 }
 void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads) {
     mt_arg m; memset(&m, 0, sizeof m);
