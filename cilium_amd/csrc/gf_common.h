@@ -34,7 +34,7 @@
 enum : uint8_t { GF_SLOT_EMPTY = 0, GF_SLOT_FULL = 1, GF_SLOT_TOMB = 2, GF_SLOT_BUSY = 3 };
 
 struct gf_htab_desc {
-    uint8_t  *slots;       // nslots * slot_size
+    uint8_t  *slots;       // nslots * slot_size (hash mode: see gf_key_hash)
     uint8_t  *vals;        // split layout only (nslots * vsz), else nullptr
     uint32_t *count;       // device element counter (inserts / deletes)
     uint64_t  mask;        // nslots - 1 (0 with slots == nullptr => empty map)
@@ -65,6 +65,48 @@ GF_HD uint32_t gf_hash_words(const uint32_t *w, int nw, uint32_t nbytes) {
     }
     h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
     return h;
+}
+
+// Hash modes: a map's role picks how its keys are hashed (host and device agree).
+//  PLAIN  : all key words.
+//  CT     : the canonical tuple (unordered addresses, unordered ports, flags
+//           without TUPLE_F_IN), so a tuple and its reverse share a home line —
+//           ct_lookup's reverse-then-forward probe touches one line.
+//  POLICY : identity only for identity != 0, so an identity's L3 and L4 entries
+//           share a home line (the L4 miss -> L3 hit sequence of
+//           __policy_can_access touches one line); identity 0 (L4 wildcard)
+//           hashes the full key.
+enum { GF_HASH_PLAIN = 0, GF_HASH_CT = 1, GF_HASH_POLICY = 2 };
+
+GF_HD uint32_t gf_key_hash(const uint32_t *w, uint32_t ksz, uint32_t mode) {
+    if (mode == GF_HASH_CT && ksz == 14) {
+        uint32_t a = w[0], b = w[1];
+        uint32_t p0 = w[2] & 0xffffu, p1 = w[2] >> 16;
+        uint32_t c[4] = {a < b ? a : b, a < b ? b : a,
+                         (p0 < p1 ? p0 : p1) | ((p0 < p1 ? p1 : p0) << 16),
+                         (w[3] & 0xffu) | (((w[3] >> 8) & 0xfeu) << 8)};
+        return gf_hash_words(c, 4, 14);
+    }
+    if (mode == GF_HASH_CT && ksz == 40) {
+        int less = 0;
+        for (int i = 0; i < 4; i++)
+            if (w[i] != w[4 + i]) { less = w[i] < w[4 + i]; break; }
+        const uint32_t *lo = less ? w : w + 4, *hi = less ? w + 4 : w;
+        uint32_t p0 = w[8] & 0xffffu, p1 = w[8] >> 16;
+        uint32_t c[10] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3],
+                          (p0 < p1 ? p0 : p1) | ((p0 < p1 ? p1 : p0) << 16),
+                          (w[9] & 0xffu) | (((w[9] >> 8) & 0xfeu) << 8)};
+        return gf_hash_words(c, 10, 40);
+    }
+    if (mode == GF_HASH_POLICY && ksz == 8 && w[0] != 0) return gf_hash_words(w, 1, 4);
+    return gf_hash_words(w, (int)((ksz + 3) / 4), ksz);
+}
+
+// First slot probed: the first slot of the home 128-B line (lines hold
+// 128/slot_size slots), then linear.
+GF_HD uint64_t gf_home_slot(uint32_t h, uint64_t mask, uint32_t slot_size) {
+    uint64_t spl = slot_size >= 128 ? 1 : 128 / slot_size;
+    return ((uint64_t)h & mask) & ~(spl - 1);
 }
 
 // Layout rule (host decides, device reads from the descriptor).

@@ -26,33 +26,87 @@ __device__ __forceinline__ void load_words(const uint8_t *p, uint32_t (&w)[NW]) 
     if (NW - k == 1) w[k] = *reinterpret_cast<const uint32_t *>(p + 4 * k);
 }
 
-template <int KSZ>
+template <int KSZ, int MODE = GF_HASH_PLAIN>
 __device__ __forceinline__ uint32_t key_hash(const uint32_t *kw) {
-    return gf_hash_words(kw, (KSZ + 3) / 4, KSZ);
+    return gf_key_hash(kw, KSZ, MODE);
 }
 
-// Exact-match probe; returns slot index or -1.
+// Slot header = key words + the word holding the state byte, loaded as whole
+// dwordx4s (every slot is >= 16 B and a pow2 >= the header, so the rounded-up
+// header never leaves the slot).
 template <int KSZ>
+struct Hdr {
+    static constexpr int SW = KSZ / 4, SB = KSZ % 4, NW = (SW + 1 + 3) / 4 * 4;
+    uint32_t w[NW];
+    __device__ __forceinline__ void load(const uint8_t *s) {
+#pragma unroll
+        for (int k = 0; k < NW; k += 4) {
+            uint4 v = *reinterpret_cast<const uint4 *>(s + 4 * k);
+            w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+        }
+    }
+    __device__ __forceinline__ uint32_t state() const { return (w[SW] >> (8 * SB)) & 0xffu; }
+    __device__ __forceinline__ bool eq(const uint32_t *kw) const {
+        bool e = true;
+#pragma unroll
+        for (int k = 0; k < SW; k++) e &= (w[k] == kw[k]);
+        if (SB) e &= ((w[SW] & ((1u << (8 * SB)) - 1u)) == kw[SW]);
+        return e;
+    }
+};
+
+// Exact-match probe; returns slot index or -1.  U slot headers are loaded
+// together per step (U = slots per 128-B line for the map's layout), so a
+// probe that resolves inside its home line costs one memory round trip.
+template <int KSZ, int U = 1>
 __device__ __forceinline__ int64_t ht_find(const gf_htab_desc &d, const uint32_t *kw, uint32_t h) {
     if (!d.slots) return -1;
-    constexpr int SW = KSZ / 4, SB = KSZ % 4, NW = SW + 1;
-    uint64_t i = h & d.mask;
-    for (uint64_t p = 0; p <= d.mask; p++) {
-        const uint8_t *s = d.slots + i * d.slot_size;
-        uint32_t w[NW];
-        load_words<NW>(s, w);
-        uint32_t st = (w[SW] >> (8 * SB)) & 0xff;
-        if (st == GF_SLOT_EMPTY) return -1;
-        if (st == GF_SLOT_FULL) {
-            bool eq = true;
+    uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
+    for (uint64_t p = 0; p <= d.mask; p += U) {
+        Hdr<KSZ> hd[U];
 #pragma unroll
-            for (int k = 0; k < SW; k++) eq &= (w[k] == kw[k]);
-            if (SB) eq &= ((w[SW] & ((1u << (8 * SB)) - 1u)) == kw[SW]);
-            if (eq) return (int64_t)i;
+        for (int u = 0; u < U; u++) hd[u].load(d.slots + ((i + u) & d.mask) * d.slot_size);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t st = hd[u].state();
+            if (st == GF_SLOT_EMPTY) return -1;
+            if (st == GF_SLOT_FULL && hd[u].eq(kw)) return (int64_t)((i + u) & d.mask);
         }
-        i = (i + 1) & d.mask;
+        i = (i + U) & d.mask;
     }
     return -1;
+}
+
+// Two keys with the same hash (hence the same probe sequence): the CT reverse
+// and forward tuples under GF_HASH_CT, the L4 and L3 policy keys of one
+// identity under GF_HASH_POLICY.  Key A has priority: returns A's slot if A is
+// present, else B's slot (*is_b = true), else -1 — exactly the outcome of
+// probing A and then B, with the home line fetched once.
+template <int KSZ, int U = 1>
+__device__ __forceinline__ int64_t ht_find2(const gf_htab_desc &d, const uint32_t *ka, const uint32_t *kb, uint32_t h,
+                                            bool *is_b) {
+    *is_b = false;
+    if (!d.slots) return -1;
+    int64_t fb = -1;
+    uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
+    for (uint64_t p = 0; p <= d.mask; p += U) {
+        Hdr<KSZ> hd[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) hd[u].load(d.slots + ((i + u) & d.mask) * d.slot_size);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t st = hd[u].state();
+            if (st == GF_SLOT_EMPTY) goto done;
+            if (st == GF_SLOT_FULL) {
+                if (hd[u].eq(ka)) return (int64_t)((i + u) & d.mask);
+                if (fb < 0 && hd[u].eq(kb)) fb = (int64_t)((i + u) & d.mask);
+            }
+        }
+        i = (i + U) & d.mask;
+    }
+done:
+    *is_b = fb >= 0;
+    return fb;
 }
 
 __device__ __forceinline__ uint8_t *ht_val(const gf_htab_desc &d, uint64_t i) {
@@ -63,12 +117,12 @@ __device__ __forceinline__ uint8_t *ht_val(const gf_htab_desc &d, uint64_t i) {
 // lane (flow-group exclusivity).  VW = value words.  Returns 0,
 // or -E2BIG (7) when a new key would exceed max_entries (strict mode) or no
 // empty slot is left.  *added is incremented for a new key.
-template <int KSZ, int VW>
+template <int KSZ, int VW, int MODE, int U = 1>
 __device__ __forceinline__ int ht_upsert(const gf_htab_desc &d, const uint32_t *kw, const uint32_t *vw,
-                                         bool strict, int *added) {
+                                         bool strict, int *added, bool known_absent = false) {
     constexpr int SW = KSZ / 4, SB = KSZ % 4;
-    uint32_t h = key_hash<KSZ>(kw);
-    int64_t f = ht_find<KSZ>(d, kw, h);
+    uint32_t h = key_hash<KSZ, MODE>(kw);
+    int64_t f = known_absent ? -1 : ht_find<KSZ, U>(d, kw, h);
     if (f >= 0) {
         uint32_t *v = reinterpret_cast<uint32_t *>(ht_val(d, (uint64_t)f));
 #pragma unroll
@@ -79,7 +133,7 @@ __device__ __forceinline__ int ht_upsert(const gf_htab_desc &d, const uint32_t *
         uint32_t old = atomicAdd(d.count, 1u);
         if (old >= d.max_entries) { atomicSub(d.count, 1u); return -7; }
     }
-    uint64_t i = h & d.mask;
+    uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
     for (uint64_t p = 0; p <= d.mask; p++) {
         uint8_t *s = d.slots + i * d.slot_size;
         uint32_t *sw = reinterpret_cast<uint32_t *>(s + 4 * SW);
@@ -109,10 +163,10 @@ __device__ __forceinline__ int ht_upsert(const gf_htab_desc &d, const uint32_t *
     return -7;
 }
 
-template <int KSZ>
+template <int KSZ, int MODE, int U = 1>
 __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t *kw, bool strict, int *added) {
     constexpr int SW = KSZ / 4, SB = KSZ % 4;
-    int64_t f = ht_find<KSZ>(d, kw, key_hash<KSZ>(kw));
+    int64_t f = ht_find<KSZ, U>(d, kw, key_hash<KSZ, MODE>(kw));
     if (f < 0) return;
     uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + (uint64_t)f * d.slot_size + 4 * SW);
     uint32_t cur = *sw;

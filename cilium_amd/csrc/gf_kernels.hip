@@ -13,6 +13,8 @@
 #include "gf_device.h"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_run_length_encode.hpp>
+#include <rocprim/iterator/discard_iterator.hpp>
 #include <errno.h>
 #include <string.h>
 
@@ -338,13 +340,17 @@ struct IngCtx {
 
 struct CtState { uint32_t rev_nat, loopback; };
 
-// __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS)
-template <int KSZ>
-__device__ __forceinline__ int ct_probe(const gf_htab_desc &d, const uint32_t *kw, int action, bool syn,
-                                        uint32_t len, uint32_t now, bool acct, CtState &st, uint32_t &ab) {
-    int64_t f = ht_find<KSZ>(d, kw, key_hash<KSZ>(kw));
-    ab += KSZ;
-    if (f < 0) return CT_NEW;
+// Slots per 128-B line of the fixed map layouts (gf_htab_layout): CT4 entry
+// 14+48 B -> 64-B slots, CT6 40+48 B -> 128-B slots, policy 8+24 B -> 64-B slots.
+// Only the number of headers fetched together depends on these; results do not.
+#define GF_CT4_U 2
+#define GF_CT6_U 1
+#define GF_POL_U 2
+
+// __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part: the
+// entry at slot f is updated in place.
+__device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, int action, bool syn, uint32_t len,
+                                       uint32_t now, bool acct, CtState &st, uint32_t &ab) {
     ab += 96;                                           // entry RMW: 48 B read + 48 B written
     uint8_t *e = ht_val(d, (uint64_t)f);
     uint4 c = *reinterpret_cast<uint4 *>(e + 32);       // lifetime, flags|rev_nat, unused, src_sec_id
@@ -373,27 +379,59 @@ __device__ __forceinline__ int ct_probe(const gf_htab_desc &d, const uint32_t *k
     c.x = life;
     c.y = (c.y & 0xffff0000u) | fl;
     *reinterpret_cast<uint2 *>(e + 32) = make_uint2(c.x, c.y);
+}
+
+// ct_lookup4/6 (conntrack.h:310-437, dir = CT_INGRESS): reverse-direction
+// probe of t, then forward probe of the reversed tuple tf.  Both share a home
+// line (GF_HASH_CT), so one ht_find2 walk answers both probes.  On return t
+// holds the tuple the reference leaves in *tuple (tf unless the first probe
+// hit), *tfl its flags.  Returns CT_NEW / CT_ESTABLISHED / CT_REPLY / CT_RELATED.
+template <int KSZ, int TW, int U>
+__device__ __forceinline__ int ct_lookup(const gf_htab_desc &d, uint32_t *t, uint32_t nh, uint32_t &tfl, int action,
+                                         bool syn, uint32_t len, uint32_t now, bool acct, CtState &st,
+                                         bool &fwd_absent, uint32_t &ab) {
+    constexpr int AW = (TW - 2) / 2;                   // address words per side
+    uint32_t tf[TW];
+#pragma unroll
+    for (int k = 0; k < AW; k++) { tf[k] = t[AW + k]; tf[AW + k] = t[k]; }
+    tf[TW - 2] = (t[TW - 2] >> 16) | (t[TW - 2] << 16);
+    tf[TW - 1] = nh | ((tfl ^ 1u) << 8);
+    bool is_b;
+    int64_t f = ht_find2<KSZ, U>(d, t, tf, key_hash<KSZ, GF_HASH_CT>(t), &is_b);
+    ab += KSZ;
+    fwd_absent = false;
+    if (f >= 0 && !is_b) {
+        ct_hit(d, f, action, syn, len, now, acct, st, ab);
+        return (tfl & 2u) ? CT_RELATED : CT_REPLY;
+    }
+    ab += KSZ;
+#pragma unroll
+    for (int k = 0; k < TW; k++) t[k] = tf[k];
+    tfl ^= 1u;
+    if (f < 0) { fwd_absent = true; return CT_NEW; }
+    ct_hit(d, f, action, syn, len, now, acct, st, ab);
     return CT_ESTABLISHED;
 }
 
 // ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0)
-template <int KSZ, int TW>
+template <int KSZ, int TW, int U>
 __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
-                                         uint32_t len, uint32_t now, bool strict, int *added, uint32_t &ab) {
+                                         uint32_t len, uint32_t now, bool strict, bool absent, int *added,
+                                         uint32_t &ab) {
     constexpr int NHW = TW - 1;
     ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written                        // word holding nexthdr | flags << 8
     uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
     uint32_t fl = (nh == 6) ? 0u : F_SEEN_NON_SYN;      // ct_update_timeout(syn = nexthdr == TCP)
     uint32_t life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
     uint32_t v[12] = {1u, 0u, len, 0u, 0u, 0u, 0u, 0u, life, fl | (rev_nat << 16), 0u, src_sec};
-    if (ht_upsert<KSZ, 12>(d, t, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+    if (ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, t, v, strict, added, absent) < 0) return D_CT_CREATE_FAILED;
     uint32_t it[TW];
 #pragma unroll
     for (int k = 0; k < TW; k++) it[k] = t[k];
     it[NHW - 1] = 0;                                    // sport = dport = 0
     it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
     v[9] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
-    if (ht_upsert<KSZ, 12>(d, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+    if (ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
     return 0;
 }
 
@@ -424,21 +462,30 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
     if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
     const gf_htab_desc pd = c->policy;
     int64_t f;
-    if (flags & GF_LXC_F_HAVE_L4_POLICY) {
-        uint32_t kw[2] = {identity, dport | (proto << 16)};
-        f = ht_find<8>(pd, kw, key_hash<8>(kw));
-        ab += 8;
-        if (f >= 0) goto proxy;
-    }
     {
-        uint32_t kw[2] = {identity, 0u};
-        f = ht_find<8>(pd, kw, key_hash<8>(kw));
-        ab += 8;
-        if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
+        uint32_t k4[2] = {identity, dport | (proto << 16)}, k3[2] = {identity, 0u};
+        if ((flags & GF_LXC_F_HAVE_L4_POLICY) && identity) {
+            // L4 then L3 key of one identity share a home line (GF_HASH_POLICY)
+            bool l3;
+            f = ht_find2<8, GF_POL_U>(pd, k4, k3, key_hash<8, GF_HASH_POLICY>(k4), &l3);
+            ab += 8;
+            if (f >= 0 && !l3) goto proxy;
+            ab += 8;
+            if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
+        } else {
+            if (flags & GF_LXC_F_HAVE_L4_POLICY) {
+                f = ht_find<8, GF_POL_U>(pd, k4, key_hash<8, GF_HASH_POLICY>(k4));
+                ab += 8;
+                if (f >= 0) goto proxy;
+            }
+            f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
+            ab += 8;
+            if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
+        }
     }
     if (flags & GF_LXC_F_HAVE_L4_POLICY) {
         uint32_t kw[2] = {0u, dport | (proto << 16)};
-        f = ht_find<8>(pd, kw, key_hash<8>(kw));
+        f = ht_find<8, GF_POL_U>(pd, kw, key_hash<8, GF_HASH_POLICY>(kw));
         ab += 8;
         if (f >= 0) goto proxy;
     }
@@ -539,16 +586,8 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     const gf_htab_desc ct = c->ct4;
     CtState st{0, 0};
-    int ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st, ab);
-    if (ret != CT_NEW) {
-        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
-    } else {
-        uint32_t tmp = t[0]; t[0] = t[1]; t[1] = tmp;  // ipv4_ct_tuple_reverse
-        t[2] = (t[2] >> 16) | (t[2] << 16);
-        tfl ^= 1u;
-        t[3] = nh | (tfl << 8);
-        ret = ct_probe<14>(ct, t, action, syn, len, X.now, acct, st, ab);
-    }
+    bool absent;
+    int ret = ct_lookup<14, 4, GF_CT4_U>(ct, t, nh, tfl, action, syn, len, X.now, acct, st, absent, ab);
     fwd = ret;
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
         const gf_htab_desc rn = c->revnat4;
@@ -565,12 +604,12 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     uint32_t orig_sip = r.saddr;
     int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { ab += 14; ht_delete<14>(ct, t, X.strict & 1, added); }
+        if (ret == CT_ESTABLISHED) { ab += 14; ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added); }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;                         // skip_proxy
     if (ret == CT_NEW) {
-        ret = ct_create<14, 4>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, added, ab);
+        ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, absent, added, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -605,16 +644,8 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     const gf_htab_desc ct = c->ct6;
     CtState st{0, 0};
-    int ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st, ab);
-    if (ret != CT_NEW) {
-        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
-    } else {
-        for (int k = 0; k < 4; k++) { uint32_t tmp = t[k]; t[k] = t[4 + k]; t[4 + k] = tmp; }
-        t[8] = (t[8] >> 16) | (t[8] << 16);
-        tfl ^= 1u;
-        t[9] = nh | (tfl << 8);
-        ret = ct_probe<40>(ct, t, action, syn, len, X.now, acct, st, ab);
-    }
+    bool absent;
+    int ret = ct_lookup<40, 10, GF_CT6_U>(ct, t, nh, tfl, action, syn, len, X.now, acct, st, absent, ab);
     fwd = ret;
     if (st.rev_nat) {
         const gf_htab_desc rn = c->revnat6;
@@ -629,12 +660,12 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     }
     int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { ab += 40; ht_delete<40>(ct, t, X.strict & 1, added); }
+        if (ret == CT_ESTABLISHED) { ab += 40; ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added); }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;
     if (ret == CT_NEW) {
-        ret = ct_create<40, 10>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, added, ab);
+        ret = ct_create<40, 10, GF_CT6_U>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, absent, added, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -677,8 +708,7 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     return o;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmask, gf_rec *rec, uint32_t *keys,
-                                                    uint32_t *vals, uint32_t *cnt) {
+__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, uint32_t *keys, uint32_t *vals) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c.n) return;
     gf_rec r;
@@ -697,6 +727,8 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmas
     uint32_t h;
     // Only packets that can reach conntrack (an IP header is present) are bound to
     // their flow group; the rest carry no ordering constraint and are spread out.
+    // The full 32-bit group hash is the sort key: two groups share a bucket only on
+    // a 32-bit hash collision (always safe: a bucket is serialized as a whole).
     bool ct_ok = ((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6);
     if (!ct_ok) {
         h = gf_hash_words(&i, 1, 4);
@@ -708,22 +740,21 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, uint32_t qmas
     } else {
         h = gf_pair_hash4(r.saddr, r.daddr);
     }
-    uint32_t q = h & qmask;
     rec[i] = r;
-    keys[i] = q;
+    keys[i] = h;
     vals[i] = i;
-    atomicAdd(&cnt[q], 1u);
 }
 
-// Level-synchronous schedule over flow-group buckets: launch k processes the
-// k-th packet (batch order) of every bucket with more than k packets, one
-// packet per lane.  Buckets are ordered by packet count (descending), so the
-// active buckets of level k are order[0 .. A_k).  Packets of one bucket are
-// therefore handled in batch order, and different buckets (disjoint CT keys)
-// run concurrently — the CT ordering rule of DESIGN.md.
-__device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec *rec, gf_ingress_out *out,
+// Level-synchronous schedule over flow-group buckets (runs of equal group hash in
+// the stably sorted batch): launch k processes the k-th packet (batch order) of
+// every bucket with more than k packets, one packet per lane.  Buckets are
+// ordered by packet count (descending), so the active buckets of level k are
+// order[0 .. A_k), and k_level_gather lays level k out contiguously at
+// [L_k, L_k + A_k) — level launches read their records coalesced.  Packets of one
+// bucket are therefore handled in batch order, and different buckets (disjoint
+// CT keys) run concurrently — the CT ordering rule of DESIGN.md.
+__device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
                                         Stats &st, bool stats, int &added) {
-    gf_rec r = rec[i];
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy(X, r, i, &added, ab);
     out[i] = o;
@@ -737,9 +768,27 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t
     if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ing_level(IngCtx X, uint32_t level, uint32_t active, const uint32_t *order,
-                                                     const uint32_t *off, const uint32_t *perm, const gf_rec *rec,
-                                                     gf_ingress_out *out, uint32_t *ct_count,
+// Level-major layout: lane t (bucket order[t]) copies its first min(cnt, KL)
+// packets to position L[k] + t of level k.  For a fixed k the lanes of a wave
+// write consecutive positions.
+__global__ __launch_bounds__(BLOCK) void k_level_gather(uint32_t nb, uint32_t KL, const uint32_t *order,
+                                                        const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
+                                                        const uint32_t *L, const gf_rec *rec, gf_rec *lrec,
+                                                        uint32_t *lidx) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb) return;
+    uint32_t b = order[t], o = off[b], c = cnt[b];
+    if (c > KL) c = KL;
+    for (uint32_t k = 0; k < c; k++) {
+        uint32_t i = perm[o + k];
+        uint32_t j = L[k] + t;
+        lrec[j] = rec[i];
+        lidx[j] = i;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ing_level(IngCtx X, uint32_t lbase, uint32_t active, const gf_rec *lrec,
+                                                     const uint32_t *lidx, gf_ingress_out *out, uint32_t *ct_count,
                                                      unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
@@ -748,16 +797,22 @@ __global__ __launch_bounds__(BLOCK) void k_ing_level(IngCtx X, uint32_t level, u
     if (stats) st.init(); else __syncthreads();
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     int added = 0;
-    if (t < active) ing_one(X, perm[off[order[t]] + level], rec, out, st, stats != nullptr, added);
+    if (t < active) {
+        uint32_t j = lbase + t;
+        gf_rec r = lrec[j];
+        ing_one(X, lidx[j], r, out, st, stats != nullptr, added);
+    }
     flush_added(X, added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }
 
 // Remaining ranks [level, cnt) of the few deep buckets: one bucket per lane.
-__global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, uint32_t active, const uint32_t *order,
-                                                    const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
-                                                    const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
-                                                    unsigned long long *stats) {
+// Ranks below KL come from the level-major copy, deeper ones from the sort.
+__global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, uint32_t active, uint32_t KL,
+                                                    const uint32_t *L, const gf_rec *lrec, const uint32_t *lidx,
+                                                    const uint32_t *order, const uint32_t *off, const uint32_t *cnt,
+                                                    const uint32_t *perm, const gf_rec *rec, gf_ingress_out *out,
+                                                    uint32_t *ct_count, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     Stats st{sl};
@@ -766,8 +821,14 @@ __global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, ui
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     int added = 0;
     if (t < active) {
-        uint32_t q = order[t], b = off[q], e = b + cnt[q];
-        for (uint32_t j = b + level; j < e; j++) ing_one(X, perm[j], rec, out, st, stats != nullptr, added);
+        uint32_t q = order[t], b = off[q], c = cnt[q];
+        for (uint32_t k = level; k < c; k++) {
+            uint32_t i;
+            gf_rec r;
+            if (k < KL) { uint32_t j = L[k] + t; i = lidx[j]; r = lrec[j]; }
+            else { i = perm[b + k]; r = rec[i]; }
+            ing_one(X, i, r, out, st, stats != nullptr, added);
+        }
     }
     flush_added(X, added, ct_count, &sadd);
     if (stats) st.flush(stats);
@@ -776,10 +837,11 @@ __global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, ui
 #define GF_LCAP 1024u
 // Bucket-size histogram: block-local LDS bins, one global add per non-empty bin.
 #define GF_SCHED_ITEMS 4096
-__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, uint32_t nq, uint32_t *hist) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, const uint32_t *nruns, uint32_t *hist) {
     __shared__ uint32_t h[GF_LCAP + 1];
     for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
     __syncthreads();
+    uint32_t nq = *nruns;
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         uint32_t c = cnt[q];
@@ -855,7 +917,7 @@ void prof_drain() {
 }
 
 struct Workspace {
-    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp, hist, base, order;
+    DevBuf rec, lrec, keys, vals, skeys, perm, lidx, cnt, off, tmp, hist, base, order;
 };
 Workspace &ws() { static Workspace w; return w; }
 
@@ -997,8 +1059,9 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         if (m->ksz != b.k || m->is_lpm() != b.lpm || (!b.lpm && m->vsz != b.v)) return -EINVAL;
         *b.out = m;
     }
-    if (p->ct4) p->ct4->make_fixed_capacity();
-    if (p->ct6) p->ct6->make_fixed_capacity();
+    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->make_fixed_capacity(); }
+    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->make_fixed_capacity(); }
+    if (p->policy) p->policy->set_hash_mode(GF_HASH_POLICY);
     return new_handle(p);
 }
 
@@ -1131,49 +1194,49 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
             return -EIO;
         a->dirty = false;
     }
-    // 2. group by flow group (stable radix sort of (group, index))
+    // 2. group by flow group: stable radix sort of (32-bit group hash, index), then
+    //    run-length encoding of the sorted hashes (one bucket per run)
     uint32_t n = pkts->n;
-    // ~4 buckets per expected flow group keeps bucket collisions (two groups in one
-    // bucket => serialized) rare; 2^22 buckets cover 2^20 address pairs.
-    uint32_t qbits = 10;
-    while (qbits < 22 && (1u << qbits) * 4u < n) qbits++;
-    uint32_t nq = 1u << qbits;
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-    if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
-        (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
-        (r = grow(w.cnt, (size_t)nq * 4)) || (r = grow(w.off, (size_t)nq * 4)) || (r = grow(w.order, (size_t)nq * 4)) ||
-        (r = grow(w.hist, (GF_LCAP + 1) * 8)) || (r = grow(w.base, (GF_LCAP + 1) * 4)))
+    if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.lrec, (size_t)n * sizeof(gf_rec))) ||
+        (r = grow(w.keys, (size_t)n * 4)) || (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) ||
+        (r = grow(w.perm, (size_t)n * 4)) || (r = grow(w.lidx, (size_t)n * 4)) || (r = grow(w.cnt, (size_t)n * 4)) ||
+        (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
+        (r = grow(w.hist, (2 * (GF_LCAP + 1) + 1) * 4)) || (r = grow(w.base, 2 * (GF_LCAP + 1) * 4)))
         return r;
     (void)any_v6;   // IPv6 packets in a batch without v6 columns are dropped (DROP_INVALID)
-    size_t sort_bytes = 0, scan_bytes = 0;
+    uint32_t *d_hist = (uint32_t *)w.hist.p, *d_cursor = d_hist + (GF_LCAP + 1), *d_nruns = d_cursor + (GF_LCAP + 1);
+    uint32_t *d_base = (uint32_t *)w.base.p, *d_L = d_base + (GF_LCAP + 1);
+    size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
-                              (uint32_t *)w.perm.p, n, 0, qbits, s);
-    (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
-                            rocprim::plus<uint32_t>(), s);
-    if ((r = grow(w.tmp, std::max(sort_bytes, scan_bytes) + 256))) return r;
-    if (hip_ok(hipMemsetAsync(w.cnt.p, 0, (size_t)nq * 4, s), "memset cnt")) return -EIO;
+                                    (uint32_t *)w.perm.p, n, 0, 32, s);
+    (void)rocprim::run_length_encode(nullptr, rle_bytes, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
+                                     (uint32_t *)w.cnt.p, d_nruns, s);
+    (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
+                                  rocprim::plus<uint32_t>(), s);
+    if ((r = grow(w.tmp, std::max(std::max(sort_bytes, scan_bytes), rle_bytes) + 256))) return r;
     {
         ProfScope ps("k_ing_pack", s);
-        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, nq - 1,
-                           (gf_rec *)w.rec.p, (uint32_t *)w.keys.p, (uint32_t *)w.vals.p, (uint32_t *)w.cnt.p);
+        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, (gf_rec *)w.rec.p,
+                           (uint32_t *)w.keys.p, (uint32_t *)w.vals.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
         if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
-                                             (uint32_t *)w.perm.p, n, 0, qbits, s), "radix_sort_pairs"))
+                                             (uint32_t *)w.perm.p, n, 0, 32, s), "radix_sort_pairs"))
             return -EIO;
     }
     tb = w.tmp.bytes;
     {
-        ProfScope ps("rocprim_exclusive_scan", s);
-        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nq,
-                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
+        ProfScope ps("rocprim_rle", s);
+        if (hip_ok(rocprim::run_length_encode(w.tmp.p, tb, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
+                                              (uint32_t *)w.cnt.p, d_nruns, s), "run_length_encode"))
             return -EIO;
     }
-    // 3. run handle_policy per flow-group queue
+    // 3. run handle_policy per flow-group bucket
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
     X.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
@@ -1188,40 +1251,61 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     // 4. bucket schedule: histogram of bucket sizes -> per-level active counts
     {
         ProfScope ps("k_bucket_sched", s);
-        if (hip_ok(hipMemsetAsync(w.hist.p, 0, (GF_LCAP + 1) * 8, s), "memset hist")) return -EIO;
-        hipLaunchKernelGGL(k_bucket_hist, dim3((nq + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           nq, (uint32_t *)w.hist.p);
+        if (hip_ok(hipMemsetAsync(d_hist, 0, (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
+        hipLaunchKernelGGL(k_bucket_hist, dim3((n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s,
+                           (const uint32_t *)w.cnt.p, (const uint32_t *)d_nruns, d_hist);
     }
-    std::vector<uint32_t> hist(GF_LCAP + 1), base(GF_LCAP + 1), active(GF_LCAP + 1);
-    if (hip_ok(hipMemcpyAsync(hist.data(), w.hist.p, (GF_LCAP + 1) * 4, hipMemcpyDeviceToHost, s), "hist d2h") ||
+    std::vector<uint32_t> hist(GF_LCAP + 2), hb(2 * (GF_LCAP + 1)), active(GF_LCAP + 1);
+    if (hip_ok(hipMemcpyAsync(hist.data(), d_hist, (GF_LCAP + 1) * 4, hipMemcpyDeviceToHost, s), "hist d2h") ||
+        hip_ok(hipMemcpyAsync(&hist[GF_LCAP + 1], d_nruns, 4, hipMemcpyDeviceToHost, s), "runs d2h") ||
         hip_ok(hipStreamSynchronize(s), "hist sync"))
         return -EIO;
+    uint32_t nb = hist[GF_LCAP + 1];
     uint32_t acc = 0, maxc = 0;
+    uint32_t *base = hb.data(), *L = hb.data() + (GF_LCAP + 1);
     for (int c = (int)GF_LCAP; c >= 1; c--) { base[c] = acc; acc += hist[c]; if (hist[c] && !maxc) maxc = (uint32_t)c; }
-    {   // active[k] = buckets with count > k
-        uint32_t a = 0;
-        for (int c = (int)GF_LCAP; c >= 1; c--) { a += hist[c]; active[c - 1] = a; }
+    {   // active[k] = buckets with count > k;  L[k] = start of level k in the level-major copy
+        uint32_t av = 0;
+        for (int c = (int)GF_LCAP; c >= 1; c--) { av += hist[c]; active[c - 1] = av; }
+        uint32_t l = 0;
+        for (uint32_t k = 0; k <= GF_LCAP; k++) { L[k] = l; if (k < GF_LCAP) l += active[k]; }
     }
-    if (hip_ok(hipMemcpyAsync(w.base.p, base.data(), (GF_LCAP + 1) * 4, hipMemcpyHostToDevice, s), "base h2d") ||
-        hip_ok(hipMemsetAsync((uint8_t *)w.hist.p + (GF_LCAP + 1) * 4, 0, (GF_LCAP + 1) * 4, s), "cursor"))
+    uint32_t KL = maxc;                                 // levels held in the level-major copy (<= GF_LCAP)
+    if (hip_ok(hipMemcpyAsync(d_base, hb.data(), 2 * (GF_LCAP + 1) * 4, hipMemcpyHostToDevice, s), "base h2d") ||
+        hip_ok(hipMemsetAsync(d_cursor, 0, (GF_LCAP + 1) * 4, s), "cursor"))
         return -EIO;
+    tb = w.tmp.bytes;
+    {
+        ProfScope ps("rocprim_exclusive_scan", s);
+        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nb,
+                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
+            return -EIO;
+    }
     {
         ProfScope ps("k_bucket_sched", s);
-        hipLaunchKernelGGL(k_bucket_order, dim3((nq + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           nq, (const uint32_t *)w.base.p, (uint32_t *)w.hist.p + (GF_LCAP + 1), (uint32_t *)w.order.p);
+        hipLaunchKernelGGL(k_bucket_order, dim3((nb + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s,
+                           (const uint32_t *)w.cnt.p, nb, (const uint32_t *)d_base, d_cursor, (uint32_t *)w.order.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_bucket_order"))) return r;
+    {
+        ProfScope ps("k_level_gather", s);
+        hipLaunchKernelGGL(k_level_gather, dim3((nb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, nb, KL,
+                           (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
+                           (const uint32_t *)w.perm.p, (const uint32_t *)d_L, (const gf_rec *)w.rec.p,
+                           (gf_rec *)w.lrec.p, (uint32_t *)w.lidx.p);
+    }
+    if ((r = hip_ok(hipGetLastError(), "k_level_gather"))) return r;
     // 5. levels while there is enough parallelism, then one sequential tail launch
     const uint32_t tail_below = 16384;
     uint32_t k = 0;
     {
         ProfScope ps("ing_levels", s);
-        for (; k < maxc && k < GF_LCAP && active[k] >= tail_below; k++)
-            hipLaunchKernelGGL(k_ing_level, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k],
-                               (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.perm.p,
-                               (const gf_rec *)w.rec.p, out, cntp, sink);
+        for (; k < maxc && active[k] >= tail_below; k++)
+            hipLaunchKernelGGL(k_ing_level, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, L[k], active[k],
+                               (const gf_rec *)w.lrec.p, (const uint32_t *)w.lidx.p, out, cntp, sink);
         if (k < maxc)
-            hipLaunchKernelGGL(k_ing_tail, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k],
+            hipLaunchKernelGGL(k_ing_tail, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k], KL,
+                               (const uint32_t *)d_L, (const gf_rec *)w.lrec.p, (const uint32_t *)w.lidx.p,
                                (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
                                (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cntp, sink);
     }

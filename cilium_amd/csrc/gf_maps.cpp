@@ -61,12 +61,12 @@ void HTab::init(uint32_t k, uint32_t v, uint64_t n) {
 uint32_t HTab::hash(const uint8_t *key) const {
     uint32_t w[16] = {0};
     memcpy(w, key, ksz);
-    return gf_hash_words(w, (int)((ksz + 3) / 4), ksz);
+    return gf_key_hash(w, ksz, mode);
 }
 
 int64_t HTab::find(const uint8_t *key) const {
     if (!nslots) return -1;
-    uint64_t mask = nslots - 1, i = hash(key) & mask;
+    uint64_t mask = nslots - 1, i = gf_home_slot(hash(key), mask, slot_size);
     for (uint64_t p = 0; p < nslots; p++) {
         uint8_t st = state(i);
         if (st == GF_SLOT_EMPTY) return -1;
@@ -77,7 +77,7 @@ int64_t HTab::find(const uint8_t *key) const {
 }
 
 int64_t HTab::insert_new(const uint8_t *key, const uint8_t *value) {
-    uint64_t mask = nslots - 1, i = hash(key) & mask;
+    uint64_t mask = nslots - 1, i = gf_home_slot(hash(key), mask, slot_size);
     for (uint64_t p = 0; p < nslots; p++) {
         uint8_t st = state(i);
         if (st == GF_SLOT_EMPTY || st == GF_SLOT_TOMB) {
@@ -101,11 +101,13 @@ void HTab::erase(uint64_t i) {
 }
 
 void HTab::rehash(uint64_t n) {
+    if (slots.empty()) { nslots = n; count = 0; tombs = 0; return; }   // not materialised: stays all-empty
     std::vector<uint8_t> os, ov;
     os.swap(slots); ov.swap(vals);
     uint64_t on = nslots;
-    uint32_t oss = slot_size;
+    uint32_t oss = slot_size, md = mode;
     init(ksz, vsz, n);
+    mode = md;
     for (uint64_t i = 0; i < on; i++) {
         if (os[i * oss + ksz] != GF_SLOT_FULL) continue;
         const uint8_t *v = split ? &ov[i * vsz] : &os[i * oss + voff];
@@ -147,6 +149,14 @@ static void materialize(HTab &h) {
         h.slots.assign(h.nslots * h.slot_size, 0);
         if (h.split) h.vals.assign(h.nslots * h.vsz, 0);
     }
+}
+
+void Map::set_hash_mode(uint32_t m) {
+    if (is_lpm() || ht.mode == m) return;
+    pull();
+    ht.mode = m;
+    if (!ht.slots.empty()) ht.rehash(ht.nslots);
+    dev_valid = false;
 }
 
 void Map::make_fixed_capacity() {
