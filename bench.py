@@ -127,8 +127,8 @@ def main():
     if world == 1 and not args.no_stats:
         assert total_pkts == local_pkts, (total_pkts, local_pkts)
 
-    # ---- roofline of the dominant kernel (k_ing_run), this rank ----
-    ki = kern.get("ing_levels", (0, 0.0))
+    # ---- roofline of the dominant kernel (k_ing_groups), this rank ----
+    ki = kern.get("k_ing_groups", (0, 0.0))
     avg_ms = ki[1] / max(ki[0], 1)
     ab_per_launch = float(lc[270]) / max(K, 1)
     achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -138,7 +138,7 @@ def main():
     if pmc:
         try:
             j = json.load(open(pmc[-1]))
-            traffic = j.get("k_ing_run_hbm_bytes_per_launch_per_16M")
+            traffic = j.get("k_ing_groups_hbm_bytes_per_launch_per_16M")
             if traffic is not None:
                 traffic = traffic * (batches[W].n / 16_777_216.0)
                 traffic_src = os.path.relpath(pmc[-1], ROOT)
@@ -173,7 +173,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_ing_level+k_ing_tail (CT+policy stage, per step)",
+            "kernel": "k_ing_groups (CT+policy stage: handle_policy over every packet of the step)",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -64,6 +64,7 @@ struct Map : Obj {
     bool host_valid = true;     // host shadow up to date
     bool dev_valid = false;     // HBM replica up to date
     bool fixed_capacity = false; // device inserts into this map (CT): nslots sized by max_entries
+    uint64_t dev_count_hi = 0;  // upper bound of the device element count (classify bookkeeping)
     DevBuf d_slots, d_vals, d_count;
     // LPM
     std::map<std::string, std::string, LpmKeyLess> lpm;   // orig key bytes -> value
@@ -114,6 +115,8 @@ struct PolicyArray : Obj {
     // device image
     DevBuf d_slot_of_lxc;      // uint16[65536]: 0 = empty, else cfg index + 1
     DevBuf d_cfgs;             // gf_lxc_dev[]
+    std::vector<uint8_t> h_cfgs;       // last uploaded program table (change detection)
+    std::vector<uint16_t> h_slot_of;
     bool dirty = true;
     PolicyArray() : Obj(ObjKind::PolicyArray) {}
 };

@@ -449,15 +449,33 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
     return 0;
 }
 
-__device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, uint32_t len) {
-    unsigned long long *p = reinterpret_cast<unsigned long long *>(ht_val(d, (uint64_t)f) + 8);
-    atomicAdd(&p[0], 1ull);
-    atomicAdd(&p[1], (unsigned long long)len);
+// policy_entry packets/bytes counters (policy.h:67-68,79-80,91-92).  The
+// reference adds them per packet; nothing reads them inside a batch (the host
+// sees them after classify returns), so a lane sums the increments of its
+// consecutive packets that hit the same entry in registers and applies them
+// with one pair of atomics when the entry changes and at the end — the same
+// totals with a fraction of the memory-side atomics.
+struct PolAcc {
+    unsigned long long *p = nullptr;
+    unsigned long long pk = 0, by = 0;
+    __device__ __forceinline__ void flush() {
+        if (p) { atomicAdd(&p[0], pk); atomicAdd(&p[1], by); }
+        p = nullptr; pk = 0; by = 0;
+    }
+    __device__ __forceinline__ void add(unsigned long long *q, uint32_t len) {
+        if (q != p) { flush(); p = q; }
+        pk += 1ull; by += (unsigned long long)len;
+    }
+};
+
+__device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, uint32_t len, PolAcc &acc) {
+    acc.add(reinterpret_cast<unsigned long long *>(ht_val(d, (uint64_t)f) + 8), len);
 }
 
 // __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168)
 __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t identity, uint32_t dport,
-                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab) {
+                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab,
+                              PolAcc &acc) {
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
     const gf_htab_desc pd = c->policy;
@@ -471,7 +489,7 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
             ab += 8;
             if (f >= 0 && !l3) goto proxy;
             ab += 8;
-            if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
+            if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
         } else {
             if (flags & GF_LXC_F_HAVE_L4_POLICY) {
                 f = ht_find<8, GF_POL_U>(pd, k4, key_hash<8, GF_HASH_POLICY>(k4));
@@ -480,7 +498,7 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
             }
             f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
             ab += 8;
-            if (f >= 0) { ab += 40; policy_count(pd, f, len); return TC_OK; }
+            if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
         }
     }
     if (flags & GF_LXC_F_HAVE_L4_POLICY) {
@@ -492,7 +510,7 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
     goto deny;
 proxy: {
         ab += 40;                                       // entry read + counters written
-        policy_count(pd, f, len);
+        policy_count(pd, f, len, acc);
         uint32_t pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
         return l4_proxy_lookup(c, proto, dport);
@@ -573,7 +591,7 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, int &fwd,
-                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab) {
+                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
     uint32_t nh = r.proto;
@@ -602,7 +620,7 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
         }
     }
     uint32_t orig_sip = r.saddr;
-    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab);
+    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab, acc);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { ab += 14; ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added); }
         return D_POLICY;
@@ -625,7 +643,8 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
 
 // ipv6_policy, bpf/bpf_lxc.c:745-862
 __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, uint32_t i,
-                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab) {
+                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab,
+                           PolAcc &acc) {
     uint32_t len = r.len;
     if (len < 54) return D_INVALID;
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
@@ -658,7 +677,7 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
             if (r2 < 0) return r2;
         }
     }
-    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab);
+    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { ab += 40; ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added); }
         return D_POLICY;
@@ -681,7 +700,7 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
 
 // handle_policy, bpf/bpf_lxc.c:980-1024
 __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, int *added,
-                                                       uint32_t &ab) {
+                                                       uint32_t &ab, PolAcc &acc) {
     gf_ingress_out o{};
     uint32_t sl = X.slot_of[r.lxc_id];
     if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }
@@ -693,8 +712,8 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     uint32_t ifindex = r.ifindex;
     uint32_t cls = r.cls & 3u;
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
-    else if (cls == 2) { ab += 47; ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added, ab); }
-    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) { ab += 23; ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added, ab); }
+    else if (cls == 2) { ab += 47; ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added, ab, acc); }
+    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) { ab += 23; ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added, ab, acc); }
     else ret = D_UNKNOWN_L3;
     o.ct_ret = (uint8_t)fwd;
     if (ret < 0 || ret == TC_SHOT) {
@@ -745,18 +764,18 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, 
     vals[i] = i;
 }
 
-// Level-synchronous schedule over flow-group buckets (runs of equal group hash in
-// the stably sorted batch): launch k processes the k-th packet (batch order) of
-// every bucket with more than k packets, one packet per lane.  Buckets are
-// ordered by packet count (descending), so the active buckets of level k are
-// order[0 .. A_k), and k_level_gather lays level k out contiguously at
-// [L_k, L_k + A_k) — level launches read their records coalesced.  Packets of one
-// bucket are therefore handled in batch order, and different buckets (disjoint
-// CT keys) run concurrently — the CT ordering rule of DESIGN.md.
+// Flow-group schedule.  A bucket is a run of equal 32-bit group hash in the
+// stably sorted batch, so it holds whole flow groups with their packets in batch
+// order.  One lane runs one bucket to completion, packet after packet — the
+// order BPF would see them on one CPU — while different buckets (disjoint CT
+// keys) run concurrently.  Buckets are handed out longest first
+// (LPT): k_bucket_order lists them by packet count, descending, and waves take
+// the next 64 entries of that list from a device queue, so the lanes of a wave
+// carry equal work and the deepest buckets start first.
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
-                                        Stats &st, bool stats, int &added) {
+                                        Stats &st, bool stats, int &added, PolAcc &acc) {
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy(X, r, i, &added, ab);
+    gf_ingress_out o = handle_policy(X, r, i, &added, ab, acc);
     out[i] = o;
     if (stats) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
 }
@@ -768,68 +787,40 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t
     if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
 }
 
-// Level-major layout: lane t (bucket order[t]) copies its first min(cnt, KL)
-// packets to position L[k] + t of level k.  For a fixed k the lanes of a wave
-// write consecutive positions.
-__global__ __launch_bounds__(BLOCK) void k_level_gather(uint32_t nb, uint32_t KL, const uint32_t *order,
-                                                        const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
-                                                        const uint32_t *L, const gf_rec *rec, gf_rec *lrec,
-                                                        uint32_t *lidx) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nb) return;
-    uint32_t b = order[t], o = off[b], c = cnt[b];
-    if (c > KL) c = KL;
-    for (uint32_t k = 0; k < c; k++) {
-        uint32_t i = perm[o + k];
-        uint32_t j = L[k] + t;
-        lrec[j] = rec[i];
-        lidx[j] = i;
-    }
-}
-
-__global__ __launch_bounds__(BLOCK) void k_ing_level(IngCtx X, uint32_t lbase, uint32_t active, const gf_rec *lrec,
-                                                     const uint32_t *lidx, gf_ingress_out *out, uint32_t *ct_count,
-                                                     unsigned long long *stats) {
+__global__ __launch_bounds__(BLOCK) void k_ing_groups(IngCtx X, const uint32_t *nruns, const uint32_t *order,
+                                                      const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
+                                                      const gf_rec *rec, gf_ingress_out *out, uint32_t *queue,
+                                                      uint32_t *ct_count, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nb = *nruns, lane = threadIdx.x & 63u;
     int added = 0;
-    if (t < active) {
-        uint32_t j = lbase + t;
-        gf_rec r = lrec[j];
-        ing_one(X, lidx[j], r, out, st, stats != nullptr, added);
-    }
-    flush_added(X, added, ct_count, &sadd);
-    if (stats) st.flush(stats);
-}
-
-// Remaining ranks [level, cnt) of the few deep buckets: one bucket per lane.
-// Ranks below KL come from the level-major copy, deeper ones from the sort.
-__global__ __launch_bounds__(BLOCK) void k_ing_tail(IngCtx X, uint32_t level, uint32_t active, uint32_t KL,
-                                                    const uint32_t *L, const gf_rec *lrec, const uint32_t *lidx,
-                                                    const uint32_t *order, const uint32_t *off, const uint32_t *cnt,
-                                                    const uint32_t *perm, const gf_rec *rec, gf_ingress_out *out,
-                                                    uint32_t *ct_count, unsigned long long *stats) {
-    __shared__ uint32_t sl[272];
-    __shared__ uint32_t sadd;
-    Stats st{sl};
-    if (threadIdx.x == 0) sadd = 0;
-    if (stats) st.init(); else __syncthreads();
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    int added = 0;
-    if (t < active) {
+    PolAcc acc;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(queue, 64u);
+        base = __shfl(base, 0);
+        if (base >= nb) break;
+        uint32_t t = base + lane;
+        if (t >= nb) continue;
         uint32_t q = order[t], b = off[q], c = cnt[q];
-        for (uint32_t k = level; k < c; k++) {
-            uint32_t i;
-            gf_rec r;
-            if (k < KL) { uint32_t j = L[k] + t; i = lidx[j]; r = lrec[j]; }
-            else { i = perm[b + k]; r = rec[i]; }
-            ing_one(X, i, r, out, st, stats != nullptr, added);
+        uint32_t i = perm[b];
+        uint32_t inx = c > 1 ? perm[b + 1] : 0u;
+        gf_rec r = rec[i];
+        for (uint32_t k = 0; k < c; k++) {
+            // next record and the index after it are in flight while packet k runs
+            gf_rec rn;
+            uint32_t in2 = 0;
+            if (k + 1 < c) rn = rec[inx];
+            if (k + 2 < c) in2 = perm[b + k + 2];
+            ing_one(X, i, r, out, st, stats != nullptr, added, acc);
+            i = inx; inx = in2; r = rn;
         }
     }
+    acc.flush();
     flush_added(X, added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }
@@ -852,13 +843,34 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, cons
         if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
+// base[c] = number of buckets with count > c (start of bin c in the descending
+// order), one block of GF_LCAP threads: thread k owns bin c = GF_LCAP - k.  Also
+// clears the order cursors and the work queue.
+__global__ __launch_bounds__(GF_LCAP) void k_bucket_base(const uint32_t *hist, uint32_t *base, uint32_t *cursor,
+                                                          uint32_t *queue) {
+    __shared__ uint32_t s[GF_LCAP];
+    const uint32_t k = threadIdx.x, c = GF_LCAP - k;
+    s[k] = hist[c];
+    __syncthreads();
+    for (uint32_t d = 1; d < GF_LCAP; d <<= 1) {      // inclusive scan over bins GF_LCAP .. 1
+        uint32_t v = k >= d ? s[k - d] : 0u;
+        __syncthreads();
+        s[k] += v;
+        __syncthreads();
+    }
+    base[c] = s[k] - hist[c];
+    cursor[c] = 0;
+    if (k == 0) { base[0] = 0; cursor[0] = 0; *queue = 0; }
+}
+
 // order[] = non-empty buckets sorted by count, descending (ties in any order):
 // block-local counts per bin, one global reservation per (block, bin).
-__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, uint32_t nq, const uint32_t *base,
+__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, const uint32_t *nruns, const uint32_t *base,
                                                         uint32_t *cursor, uint32_t *order) {
     __shared__ uint32_t h[GF_LCAP + 1];
     for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
     __syncthreads();
+    uint32_t nq = *nruns;
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         uint32_t c = cnt[q];
@@ -917,7 +929,7 @@ void prof_drain() {
 }
 
 struct Workspace {
-    DevBuf rec, lrec, keys, vals, skeys, perm, lidx, cnt, off, tmp, hist, base, order;
+    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp, sched, order;
 };
 Workspace &ws() { static Workspace w; return w; }
 
@@ -935,6 +947,18 @@ uint32_t grid_for(uint32_t n) {
 }
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
+
+// blocks of BLOCK threads that fill the device at `per_cu` blocks per CU
+uint32_t resident_blocks(uint32_t per_cu) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return (uint32_t)cus * per_cu;
+}
 
 }  // namespace
 
@@ -1169,45 +1193,62 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
     // fail in the kernel (they evict); here they keep entries past max_entries until
     // GC and are bounded only by the slot array (7/8 load), see DESIGN.md.
+    // The decision uses a host-side upper bound of the device element count (each
+    // packet inserts at most 2 entries), read back from the device only when the
+    // bound gets near the limit — steady-state batches never wait on the GPU here.
     uint32_t strict = 0;
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
-        uint64_t upper = m->ht.count;  // host view (exact after pull/push)
-        if (!m->host_valid) {
-            uint32_t dc = 0;
-            if (hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count")) return -EIO;
-            upper = dc;
-        }
         uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
-        if (upper + 2ull * pkts->n > limit) strict = 1;
+        if (m->host_valid) m->dev_count_hi = m->ht.count;
+        if (m->dev_count_hi + 2ull * pkts->n > limit && !m->host_valid) {
+            uint32_t dc = 0;
+            if (hip_ok(hipStreamSynchronize(s), "ct count sync") ||
+                hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
+                return -EIO;
+            m->dev_count_hi = dc;
+        }
+        if (m->dev_count_hi + 2ull * pkts->n > limit) strict = 1;
+        m->dev_count_hi += 2ull * pkts->n;
         if (m->type == GF_MAP_TYPE_LRU_HASH) {
             if (m == ct4m) { for (auto &d : cfgs) d.ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
             else { for (auto &d : cfgs) d.ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
         }
     }
-    if (a->dirty || a->d_cfgs.bytes != cfgs.size() * sizeof(gf_lxc_dev) || true) {
-        if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
-        if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cfgs.size()) * sizeof(gf_lxc_dev)))) return r;
-        if (hip_ok(hipMemcpy(a->d_slot_of_lxc.p, slot_of.data(), 65536 * 2, hipMemcpyHostToDevice), "slots")) return -EIO;
-        if (!cfgs.empty() &&
-            hip_ok(hipMemcpy(a->d_cfgs.p, cfgs.data(), cfgs.size() * sizeof(gf_lxc_dev), hipMemcpyHostToDevice), "cfgs"))
-            return -EIO;
-        a->dirty = false;
+    // device program table: uploaded only when it changed (programs, bindings,
+    // or a map's device storage moved)
+    {
+        size_t cb = cfgs.size() * sizeof(gf_lxc_dev);
+        bool changed = a->dirty || a->h_cfgs.size() != cb || a->h_slot_of.size() != slot_of.size() ||
+                       (cb && memcmp(a->h_cfgs.data(), cfgs.data(), cb)) ||
+                       memcmp(a->h_slot_of.data(), slot_of.data(), slot_of.size() * 2);
+        if (changed) {
+            if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
+            if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cb)))) return r;
+            a->h_cfgs.assign((const uint8_t *)cfgs.data(), (const uint8_t *)cfgs.data() + cb);
+            a->h_slot_of = slot_of;
+            if (hip_ok(hipMemcpyAsync(a->d_slot_of_lxc.p, a->h_slot_of.data(), 65536 * 2, hipMemcpyHostToDevice, s), "slots"))
+                return -EIO;
+            if (cb && hip_ok(hipMemcpyAsync(a->d_cfgs.p, a->h_cfgs.data(), cb, hipMemcpyHostToDevice, s), "cfgs"))
+                return -EIO;
+            if (hip_ok(hipStreamSynchronize(s), "cfg sync")) return -EIO;
+            a->dirty = false;
+        }
     }
     // 2. group by flow group: stable radix sort of (32-bit group hash, index), then
     //    run-length encoding of the sorted hashes (one bucket per run)
     uint32_t n = pkts->n;
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-    if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.lrec, (size_t)n * sizeof(gf_rec))) ||
-        (r = grow(w.keys, (size_t)n * 4)) || (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) ||
-        (r = grow(w.perm, (size_t)n * 4)) || (r = grow(w.lidx, (size_t)n * 4)) || (r = grow(w.cnt, (size_t)n * 4)) ||
-        (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
-        (r = grow(w.hist, (2 * (GF_LCAP + 1) + 1) * 4)) || (r = grow(w.base, 2 * (GF_LCAP + 1) * 4)))
+    const size_t SCHED_WORDS = 3 * (GF_LCAP + 1) + 2;   // hist | base | cursor | nruns | queue
+    if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
+        (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
+        (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
+        (r = grow(w.sched, SCHED_WORDS * 4)))
         return r;
     (void)any_v6;   // IPv6 packets in a batch without v6 columns are dropped (DROP_INVALID)
-    uint32_t *d_hist = (uint32_t *)w.hist.p, *d_cursor = d_hist + (GF_LCAP + 1), *d_nruns = d_cursor + (GF_LCAP + 1);
-    uint32_t *d_base = (uint32_t *)w.base.p, *d_L = d_base + (GF_LCAP + 1);
+    uint32_t *d_hist = (uint32_t *)w.sched.p, *d_base = d_hist + (GF_LCAP + 1), *d_cursor = d_base + (GF_LCAP + 1);
+    uint32_t *d_nruns = d_cursor + (GF_LCAP + 1), *d_queue = d_nruns + 1;
     size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
                                     (uint32_t *)w.perm.p, n, 0, 32, s);
@@ -1229,14 +1270,33 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
                                              (uint32_t *)w.perm.p, n, 0, 32, s), "radix_sort_pairs"))
             return -EIO;
     }
-    tb = w.tmp.bytes;
     {
-        ProfScope ps("rocprim_rle", s);
+        ProfScope ps("bucket_runs", s);
+        // counts past the last run stay 0 so the offset scan can run over n
+        if (hip_ok(hipMemsetAsync(w.cnt.p, 0, (size_t)n * 4, s), "memset cnt")) return -EIO;
+        tb = w.tmp.bytes;
         if (hip_ok(rocprim::run_length_encode(w.tmp.p, tb, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
                                               (uint32_t *)w.cnt.p, d_nruns, s), "run_length_encode"))
             return -EIO;
+        tb = w.tmp.bytes;
+        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
+                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
+            return -EIO;
     }
-    // 3. run handle_policy per flow-group bucket
+    // 3. longest-first bucket order, built on the device (no host round trip)
+    {
+        ProfScope ps("k_bucket_sched", s);
+        if (hip_ok(hipMemsetAsync(d_hist, 0, (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
+        uint32_t g = (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS;
+        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
+                           (const uint32_t *)d_nruns, d_hist);
+        hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, (const uint32_t *)d_hist, d_base, d_cursor,
+                           d_queue);
+        hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
+                           (const uint32_t *)d_nruns, (const uint32_t *)d_base, d_cursor, (uint32_t *)w.order.p);
+    }
+    if ((r = hip_ok(hipGetLastError(), "k_bucket_sched"))) return r;
+    // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
     X.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
@@ -1248,68 +1308,17 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (ct4m && ct6m) X.strict = 1;
     uint32_t *cntp = ct4m ? (uint32_t *)ct4m->d_count.p : (ct6m ? (uint32_t *)ct6m->d_count.p : nullptr);
     unsigned long long *sink = (unsigned long long *)stats_sink();
-    // 4. bucket schedule: histogram of bucket sizes -> per-level active counts
     {
-        ProfScope ps("k_bucket_sched", s);
-        if (hip_ok(hipMemsetAsync(d_hist, 0, (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
-        hipLaunchKernelGGL(k_bucket_hist, dim3((n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s,
-                           (const uint32_t *)w.cnt.p, (const uint32_t *)d_nruns, d_hist);
-    }
-    std::vector<uint32_t> hist(GF_LCAP + 2), hb(2 * (GF_LCAP + 1)), active(GF_LCAP + 1);
-    if (hip_ok(hipMemcpyAsync(hist.data(), d_hist, (GF_LCAP + 1) * 4, hipMemcpyDeviceToHost, s), "hist d2h") ||
-        hip_ok(hipMemcpyAsync(&hist[GF_LCAP + 1], d_nruns, 4, hipMemcpyDeviceToHost, s), "runs d2h") ||
-        hip_ok(hipStreamSynchronize(s), "hist sync"))
-        return -EIO;
-    uint32_t nb = hist[GF_LCAP + 1];
-    uint32_t acc = 0, maxc = 0;
-    uint32_t *base = hb.data(), *L = hb.data() + (GF_LCAP + 1);
-    for (int c = (int)GF_LCAP; c >= 1; c--) { base[c] = acc; acc += hist[c]; if (hist[c] && !maxc) maxc = (uint32_t)c; }
-    {   // active[k] = buckets with count > k;  L[k] = start of level k in the level-major copy
-        uint32_t av = 0;
-        for (int c = (int)GF_LCAP; c >= 1; c--) { av += hist[c]; active[c - 1] = av; }
-        uint32_t l = 0;
-        for (uint32_t k = 0; k <= GF_LCAP; k++) { L[k] = l; if (k < GF_LCAP) l += active[k]; }
-    }
-    uint32_t KL = maxc;                                 // levels held in the level-major copy (<= GF_LCAP)
-    if (hip_ok(hipMemcpyAsync(d_base, hb.data(), 2 * (GF_LCAP + 1) * 4, hipMemcpyHostToDevice, s), "base h2d") ||
-        hip_ok(hipMemsetAsync(d_cursor, 0, (GF_LCAP + 1) * 4, s), "cursor"))
-        return -EIO;
-    tb = w.tmp.bytes;
-    {
-        ProfScope ps("rocprim_exclusive_scan", s);
-        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, nb,
-                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
-            return -EIO;
-    }
-    {
-        ProfScope ps("k_bucket_sched", s);
-        hipLaunchKernelGGL(k_bucket_order, dim3((nb + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS), dim3(BLOCK), 0, s,
-                           (const uint32_t *)w.cnt.p, nb, (const uint32_t *)d_base, d_cursor, (uint32_t *)w.order.p);
-    }
-    if ((r = hip_ok(hipGetLastError(), "k_bucket_order"))) return r;
-    {
-        ProfScope ps("k_level_gather", s);
-        hipLaunchKernelGGL(k_level_gather, dim3((nb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, nb, KL,
+        // resident-grid launch: every wave loops on the queue until it is drained
+        uint32_t grid = resident_blocks(8);
+        uint32_t need = (n + BLOCK - 1) / BLOCK;
+        if (grid > need) grid = need;
+        ProfScope ps("k_ing_groups", s);
+        hipLaunchKernelGGL(k_ing_groups, dim3(grid), dim3(BLOCK), 0, s, X, (const uint32_t *)d_nruns,
                            (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)w.perm.p, (const uint32_t *)d_L, (const gf_rec *)w.rec.p,
-                           (gf_rec *)w.lrec.p, (uint32_t *)w.lidx.p);
+                           (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, d_queue, cntp, sink);
     }
-    if ((r = hip_ok(hipGetLastError(), "k_level_gather"))) return r;
-    // 5. levels while there is enough parallelism, then one sequential tail launch
-    const uint32_t tail_below = 16384;
-    uint32_t k = 0;
-    {
-        ProfScope ps("ing_levels", s);
-        for (; k < maxc && active[k] >= tail_below; k++)
-            hipLaunchKernelGGL(k_ing_level, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, L[k], active[k],
-                               (const gf_rec *)w.lrec.p, (const uint32_t *)w.lidx.p, out, cntp, sink);
-        if (k < maxc)
-            hipLaunchKernelGGL(k_ing_tail, dim3((active[k] + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, k, active[k], KL,
-                               (const uint32_t *)d_L, (const gf_rec *)w.lrec.p, (const uint32_t *)w.lidx.p,
-                               (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
-                               (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cntp, sink);
-    }
-    if ((r = hip_ok(hipGetLastError(), "k_ing_level"))) return r;
+    if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }

@@ -21,7 +21,7 @@ def load(path):
 
 
 def group(name):
-    for g in ("k_ing_level", "k_ing_tail", "k_ing_pack", "k_bucket", "radix_sort", "exclusive_scan", "scan_impl",
+    for g in ("k_ing_groups", "k_ing_pack", "k_bucket", "radix_sort", "exclusive_scan", "scan_impl",
               "k_xdp", "k_lb", "k_parse"):
         if g in name:
             return {"radix_sort": "rocprim_sort", "scan_impl": "rocprim_scan", "exclusive_scan": "rocprim_scan"}.get(g, g)
@@ -54,7 +54,7 @@ def main():
     for f in glob.glob(os.path.join(a.dir, "*", "run_counter_collection.csv")):
         for c, gs in per_step(load(f), a.steps).items():
             res.setdefault(c, {}).update(gs)
-    stage = ("k_ing_level", "k_ing_tail")
+    stage = ("k_ing_groups",)
     out = {"per_step_counters": res, "steps_averaged": a.steps, "packets_per_step": a.packets_per_step}
     fs = sum(res.get("FETCH_SIZE", {}).get(k, 0) for k in stage)
     ws = sum(res.get("WRITE_SIZE", {}).get(k, 0) for k in stage)
@@ -69,7 +69,7 @@ def main():
         "ea_wrreq": sum(res.get("TCC_EA0_WRREQ_sum", {}).get(k, 0) for k in stage),
         "ea_atomic": sum(res.get("TCC_EA0_ATOMIC_sum", {}).get(k, 0) for k in stage),
     }
-    out["k_ing_run_hbm_bytes_per_launch_per_16M"] = out["ct_stage"]["hbm_bytes_per_step"] * 16777216 / a.packets_per_step
+    out["k_ing_groups_hbm_bytes_per_launch_per_16M"] = out["ct_stage"]["hbm_bytes_per_step"] * 16777216 / a.packets_per_step
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out["ct_stage"], indent=1))
 
