@@ -9,6 +9,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpuflow.so")
+# diagnostic ablation builds only (tools/diag.sh); never set in tests, smoke or bench runs
+if os.environ.get("GPUFLOW_DIAG_LIB"):
+    LIB_PATH = os.environ["GPUFLOW_DIAG_LIB"]
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

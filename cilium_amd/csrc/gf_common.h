@@ -109,6 +109,32 @@ GF_HD uint64_t gf_home_slot(uint32_t h, uint64_t mask, uint32_t slot_size) {
     return ((uint64_t)h & mask) & ~(spl - 1);
 }
 
+// Value codecs: how a map's value bytes are laid out in its slots (host shadow
+// and HBM replica alike).  The ABI always sees the reference layout.
+//  IDENT : the reference struct as is.
+//  CT    : struct ct_entry (bpf/lib/common.h:359-374) reordered so that what an
+//          ingress hit reads and writes sits in the 16 B right after the key,
+//          i.e. in the key's own 32-B sector:
+//            +0 lifetime  +4 flags u16 | rev_nat_index u16  +8 rx_packets lo32
+//            +12 rx_bytes lo32  +16 rx_packets hi32  +20 rx_bytes hi32
+//            +24 tx_packets  +32 tx_bytes  +40 unused, pad  +44 src_sec_id
+//          (reference offsets: rx_packets 0, rx_bytes 8, tx_packets 16,
+//          tx_bytes 24, lifetime 32, flags 36, rev_nat_index 38, 40.., 44).
+enum { GF_VCODEC_IDENT = 0, GF_VCODEC_CT = 1 };
+#define GF_CT_VSZ 48u
+GF_HD void gf_ct_encode(const uint8_t *ext, uint8_t *in) {
+    const int map[12] = {8, 9, 0, 2, 1, 3, 4, 5, 6, 7, 10, 11};   // internal word k <- reference word map[k]
+    uint32_t w[12];
+    for (int k = 0; k < 12; k++) { uint32_t v; __builtin_memcpy(&v, ext + 4 * map[k], 4); w[k] = v; }
+    __builtin_memcpy(in, w, 48);
+}
+GF_HD void gf_ct_decode(const uint8_t *in, uint8_t *ext) {
+    const int map[12] = {8, 9, 0, 2, 1, 3, 4, 5, 6, 7, 10, 11};
+    uint32_t w[12];
+    __builtin_memcpy(w, in, 48);
+    for (int k = 0; k < 12; k++) __builtin_memcpy(ext + 4 * map[k], &w[k], 4);
+}
+
 // Layout rule (host decides, device reads from the descriptor).
 GF_HD uint32_t gf_pow2ceil32(uint32_t x) {
     uint32_t p = 1;
@@ -157,7 +183,7 @@ GF_HD uint32_t gf_pair_hash6(const uint32_t *a, const uint32_t *b) {
 // bit 2 TC_INDEX_F_SKIP_PROXY.
 struct __attribute__((aligned(16))) gf_rec {
     uint32_t saddr, daddr, len, l4w0, src_identity, ifindex;
-    uint16_t lxc_id;
+    uint16_t ep;           // cilium_policy slot of the packet's lxc_id: program index + 1, 0 = empty
     int16_t  l4_off;
     uint16_t l4w3;
     uint8_t  proto, cls;

@@ -33,10 +33,11 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t *kw) {
 
 // Slot header = key words + the word holding the state byte, loaded as whole
 // dwordx4s (every slot is >= 16 B and a pow2 >= the header, so the rounded-up
-// header never leaves the slot).
-template <int KSZ>
+// header never leaves the slot).  XW extra words (a multiple of 4) load the
+// start of the value with the header (e.g. the policy proxy_port).
+template <int KSZ, int XW = 0>
 struct Hdr {
-    static constexpr int SW = KSZ / 4, SB = KSZ % 4, NW = (SW + 1 + 3) / 4 * 4;
+    static constexpr int SW = KSZ / 4, SB = KSZ % 4, NW = (SW + 1 + 3) / 4 * 4 + XW;
     uint32_t w[NW];
     __device__ __forceinline__ void load(const uint8_t *s) {
 #pragma unroll
@@ -109,52 +110,131 @@ done:
     return fb;
 }
 
+// The home line of a key, loaded ahead of its use so that probes of different
+// tables (CT and policy) are in flight together: U slot headers from the
+// first slot of the home line.
+template <int KSZ, int U, int XW = 0>
+struct ProbeLine {
+    Hdr<KSZ, XW> hd[U];
+    uint64_t i;
+    __device__ __forceinline__ void load(const gf_htab_desc &d, uint32_t h) {
+        i = gf_home_slot(h, d.mask, d.slot_size);
+        if (!d.slots) return;
+#pragma unroll
+        for (int u = 0; u < U; u++) hd[u].load(d.slots + ((i + u) & d.mask) * d.slot_size);
+    }
+};
+
+// Outcome of a probe walk: the slot of key A, else of key B (is_b), else -1;
+// plus the EMPTY slot that ended the walk — where an absent key is inserted —
+// and the header word holding its state byte as it was observed.
+struct ProbeRes {
+    int64_t f, empty;
+    uint32_t empty_word;
+    bool is_b;
+    int u;                 // index of the found slot in L.hd (headers still loaded), or -1
+};
+
+// ht_find2 continuing from a preloaded home line (key B only when has_b).  The
+// walk ends at the first EMPTY slot, as in ht_find2.
+template <int KSZ, int U, int XW>
+__device__ __forceinline__ ProbeRes probe2(const gf_htab_desc &d, const uint32_t *ka, const uint32_t *kb,
+                                           ProbeLine<KSZ, U, XW> &L, bool has_b = true) {
+    constexpr int SW = Hdr<KSZ, XW>::SW;
+    ProbeRes r{-1, -1, 0u, false, -1};
+    if (!d.slots) return r;
+    int64_t fb = -1;
+    int ub = -1;
+    uint64_t i = L.i;
+    for (uint64_t p = 0; p <= d.mask; p += U) {
+        if (p) {
+            ub = -1;                                   // headers of B's line are replaced
+#pragma unroll
+            for (int u = 0; u < U; u++) L.hd[u].load(d.slots + ((i + u) & d.mask) * d.slot_size);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t st = L.hd[u].state();
+            int64_t slot = (int64_t)((i + u) & d.mask);
+            if (st == GF_SLOT_EMPTY) { r.empty = slot; r.empty_word = L.hd[u].w[SW]; goto done; }
+            if (st == GF_SLOT_FULL) {
+                if (L.hd[u].eq(ka)) { r.f = slot; r.u = u; return r; }
+                if (has_b && fb < 0 && L.hd[u].eq(kb)) { fb = slot; ub = u; }
+            }
+        }
+        i = (i + U) & d.mask;
+    }
+done:
+    r.f = fb;
+    r.is_b = fb >= 0;
+    r.u = ub;
+    return r;
+}
+
+// VW value words to p (16-B aligned for every device-written layout: CT values
+// sit at voff 16 / 48).
+template <int VW>
+__device__ __forceinline__ void store_words(uint8_t *p, const uint32_t *v) {
+    if ((VW % 4) == 0 && ((uintptr_t)p & 15u) == 0) {
+#pragma unroll
+        for (int k = 0; k < VW; k += 4)
+            *reinterpret_cast<uint4 *>(p + 4 * k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < VW; k++) reinterpret_cast<uint32_t *>(p)[k] = v[k];
+    }
+}
+
 __device__ __forceinline__ uint8_t *ht_val(const gf_htab_desc &d, uint64_t i) {
     return d.split ? d.vals + i * d.vsz : d.slots + i * d.slot_size + d.voff;
 }
 
 // Insert-or-replace (map_update_elem BPF_ANY) for keys owned by the calling
-// lane (flow-group exclusivity).  VW = value words.  Returns 0,
-// or -E2BIG (7) when a new key would exceed max_entries (strict mode) or no
-// empty slot is left.  *added is incremented for a new key.
+// lane (flow-group exclusivity).  VW = value words.  Returns the
+// slot written, or -7 (E2BIG) when a new key would exceed max_entries (strict
+// mode) or no empty slot is left.  *added is incremented for a new key.
+// hint/hint_word: an EMPTY slot observed by this lane's lookup walk of the same
+// home (and the header word seen there), tried first with one CAS.
 template <int KSZ, int VW, int MODE, int U = 1>
-__device__ __forceinline__ int ht_upsert(const gf_htab_desc &d, const uint32_t *kw, const uint32_t *vw,
-                                         bool strict, int *added, bool known_absent = false) {
+__device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32_t *kw, const uint32_t *vw,
+                                             bool strict, int *added, bool known_absent = false,
+                                             int64_t hint = -1, uint32_t hint_word = 0) {
     constexpr int SW = KSZ / 4, SB = KSZ % 4;
+    if (!d.slots) return -7;
     uint32_t h = key_hash<KSZ, MODE>(kw);
     int64_t f = known_absent ? -1 : ht_find<KSZ, U>(d, kw, h);
     if (f >= 0) {
-        uint32_t *v = reinterpret_cast<uint32_t *>(ht_val(d, (uint64_t)f));
-#pragma unroll
-        for (int k = 0; k < VW; k++) v[k] = vw[k];
-        return 0;
+        store_words<VW>(ht_val(d, (uint64_t)f), vw);
+        return f;
     }
     if (strict) {
         uint32_t old = atomicAdd(d.count, 1u);
         if (old >= d.max_entries) { atomicSub(d.count, 1u); return -7; }
     }
+    const uint32_t keep = SB ? (kw[SW] & ((1u << (8 * SB)) - 1u)) : 0u;
+    const uint32_t busy = keep | ((uint32_t)GF_SLOT_BUSY << (8 * SB));
+    auto fill = [&](uint64_t i) {
+        uint8_t *s = d.slots + i * d.slot_size;
+        uint32_t *ks = reinterpret_cast<uint32_t *>(s);
+#pragma unroll
+        for (int k = 0; k < SW; k++) ks[k] = kw[k];
+        store_words<VW>(ht_val(d, i), vw);
+        __atomic_store_n(reinterpret_cast<uint32_t *>(s + 4 * SW), keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)),
+                         __ATOMIC_RELAXED);
+        if (!strict) (*added)++;
+    };
+    if (hint >= 0 && ((hint_word >> (8 * SB)) & 0xffu) == GF_SLOT_EMPTY) {
+        uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + (uint64_t)hint * d.slot_size + 4 * SW);
+        if (atomicCAS(sw, hint_word, busy) == hint_word) { fill((uint64_t)hint); return hint; }
+    }
     uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
     for (uint64_t p = 0; p <= d.mask; p++) {
-        uint8_t *s = d.slots + i * d.slot_size;
-        uint32_t *sw = reinterpret_cast<uint32_t *>(s + 4 * SW);
+        uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + i * d.slot_size + 4 * SW);
         uint32_t cur = *reinterpret_cast<volatile uint32_t *>(sw);
         for (;;) {
-            uint32_t st = (cur >> (8 * SB)) & 0xff;
-            if (st != GF_SLOT_EMPTY) break;
-            uint32_t keep = SB ? (kw[SW] & ((1u << (8 * SB)) - 1u)) : 0u;
-            uint32_t want = keep | ((uint32_t)GF_SLOT_BUSY << (8 * SB));
-            uint32_t seen = atomicCAS(sw, cur, want);
-            if (seen == cur) {
-                uint32_t *ks = reinterpret_cast<uint32_t *>(s);
-#pragma unroll
-                for (int k = 0; k < SW; k++) ks[k] = kw[k];
-                uint32_t *v = reinterpret_cast<uint32_t *>(ht_val(d, i));
-#pragma unroll
-                for (int k = 0; k < VW; k++) v[k] = vw[k];
-                __atomic_store_n(sw, keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)), __ATOMIC_RELAXED);
-                if (!strict) (*added)++;
-                return 0;
-            }
+            if (((cur >> (8 * SB)) & 0xffu) != GF_SLOT_EMPTY) break;
+            uint32_t seen = atomicCAS(sw, cur, busy);
+            if (seen == cur) { fill(i); return (int64_t)i; }
             cur = seen;
         }
         i = (i + 1) & d.mask;

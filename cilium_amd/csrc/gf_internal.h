@@ -34,6 +34,7 @@ struct LpmKeyLess {
 // ---- exact-match hash table (host shadow, same layout as the device) ----
 struct HTab {
     uint32_t ksz = 0, vsz = 0, slot_size = 0, voff = 0, split = 0, mode = GF_HASH_PLAIN;
+    uint32_t codec = GF_VCODEC_IDENT;   // value layout in the slots (gf_common.h)
     uint64_t nslots = 0;
     std::vector<uint8_t> slots, vals;
     uint64_t count = 0, tombs = 0;
@@ -90,6 +91,7 @@ struct Map : Obj {
     void device_modified() { host_valid = false; }
     void make_fixed_capacity();
     void set_hash_mode(uint32_t mode);   // role-specific hashing (gf_key_hash), rehashes
+    void set_value_codec(uint32_t codec); // role-specific value layout, converts stored values
     gf_htab_desc hdesc();             // requires push() done
     gf_trie_desc tdesc();             // requires push() done
     uint64_t device_bytes() const { return d_slots.bytes + d_vals.bytes + d_root.bytes + d_nodes.bytes; }

@@ -22,6 +22,16 @@ using namespace gf;
 using namespace gfd;
 
 #define BLOCK 256
+#ifndef GF_DIAG
+#define GF_DIAG 0      // diagnostic ablations (tools/diag.sh); 0 in the product build
+#endif
+// Tuning knobs of the flow-group kernel (tools/variants.sh sweeps them).
+#ifndef GF_PREFETCH_REC
+#define GF_PREFETCH_REC 1   // load the lane's next packet record while the current one runs
+#endif
+#ifndef GF_ING_MINW
+#define GF_ING_MINW 1       // __launch_bounds__ min waves per SIMD (register budget)
+#endif
 
 // ---------------------------------------------------------------- constants
 enum {
@@ -330,10 +340,15 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
 }
 
 // ================================================================ ingress (handle_policy)
+// Device-only program flags (high bits of gf_lxc_dev.flags): the program binds
+// the CT map of that family (all programs share one per family, X.ct4 / X.ct6).
+#define GF_LXC_DEV_HAS_CT4 (1u << 30)
+#define GF_LXC_DEV_HAS_CT6 (1u << 31)
+
 struct IngCtx {
     const gf_lxc_dev *cfgs;
-    const uint16_t *slot_of;
     const uint8_t *saddr6, *daddr6;
+    gf_htab_desc ct4, ct6;   // cilium_ct4_global / cilium_ct6_global (shared by every program)
     uint32_t now, host_ifindex;
     uint32_t strict;   // bit0: CT inserts check max_entries with atomics
 };
@@ -346,25 +361,65 @@ struct CtState { uint32_t rev_nat, loopback; };
 #define GF_CT4_U 2
 #define GF_CT6_U 1
 #define GF_POL_U 2
+#define GF_POL_SLOT 64u    // gf_htab_layout(8, 24)
+#define GF_POL_VOFF 16u
 
-// __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part: the
-// entry at slot f is updated in place.
-__device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, int action, bool syn, uint32_t len,
-                                       uint32_t now, bool acct, CtState &st, uint32_t &ab) {
-    ab += 96;                                           // entry RMW: 48 B read + 48 B written
+// The endpoint program of the lane's current packet, kept in registers while
+// consecutive packets of the lane's bucket target the same endpoint.
+struct Ep {
+    uint32_t sl = 0;                 // program slot + 1 (0: none loaded)
+    uint32_t flags = 0;
+    const gf_lxc_dev *c = nullptr;
+    uint8_t *pol = nullptr;          // policy map slots / mask
+    uint64_t pol_mask = 0;
+    __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
+        if (s == sl) return;
+        sl = s;
+        c = X.cfgs + (s - 1);
+        flags = c->flags;
+        pol = c->policy.slots;
+        pol_mask = c->policy.mask;
+    }
+    __device__ __forceinline__ gf_htab_desc pdesc() const {
+        gf_htab_desc d{};
+        d.slots = pol; d.mask = pol_mask; d.ksz = 8; d.vsz = 24;
+        d.slot_size = GF_POL_SLOT; d.voff = GF_POL_VOFF;
+        return d;
+    }
+};
+
+// The ICMP-related entry ct_create writes for every new flow of a group
+// (conntrack.h:563-577) is the same key for the whole group: a lane keeps
+// where it lives.  Only this lane changes keys of its group; a delete by the
+// lane clears the cache.
+template <int TW>
+struct RelCache {
+    uint32_t k[TW];
+    int64_t slot = -1;
+};
+
+// __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part.  CT
+// values use the GF_VCODEC_CT layout: `hot` = the entry's first 16 B
+// (lifetime, flags | rev_nat_index, rx_packets lo32, rx_bytes lo32), loaded
+// with the key; the update is one 16-B store into the key's sector (the high
+// halves of the rx counters are touched only on a 32-bit carry).
+__device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 hot, int action, bool syn,
+                                       uint32_t len, uint32_t now, bool acct, CtState &st, uint32_t &ab) {
+    ab += 96;                                           // entry RMW: 48 B read + 48 B written (SURVEY §8(d))
     uint8_t *e = ht_val(d, (uint64_t)f);
-    uint4 c = *reinterpret_cast<uint4 *>(e + 32);       // lifetime, flags|rev_nat, unused, src_sec_id
-    uint32_t life = c.x, fl = c.y & 0xffffu, rn = c.y >> 16;
+    uint32_t life = hot.x, fl = hot.y & 0xffffu, rn = hot.y >> 16;
     if (!(fl & F_RX_CLOSING) || !(fl & F_TX_CLOSING)) {  // ct_entry_alive -> ct_update_timeout
         if (!syn) fl |= F_SEEN_NON_SYN;
         life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
     }
     st.rev_nat = rn;
     st.loopback = (fl >> 3) & 1u;
-    if (acct) {                                         // rx_packets/rx_bytes (exclusive lane)
-        unsigned long long *rx = reinterpret_cast<unsigned long long *>(e);
-        rx[0] += 1ull;
-        rx[1] += (unsigned long long)len;
+    if (acct) {                                         // rx_packets += 1, rx_bytes += len (exclusive lane)
+        uint32_t pk = hot.z + 1u, by = hot.w + len;
+        uint32_t *hi = reinterpret_cast<uint32_t *>(e + 16);
+        if (pk == 0u) hi[0] += 1u;
+        if (by < hot.w) hi[1] += 1u;
+        hot.z = pk; hot.w = by;
     }
     if (action == ACT_CREATE) {
         if (fl & (F_RX_CLOSING | F_TX_CLOSING)) {
@@ -376,62 +431,87 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, int act
         fl |= F_RX_CLOSING;
         if ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) life = now + 10u;
     }
-    c.x = life;
-    c.y = (c.y & 0xffff0000u) | fl;
-    *reinterpret_cast<uint2 *>(e + 32) = make_uint2(c.x, c.y);
+    hot.x = life;
+    hot.y = (hot.y & 0xffff0000u) | fl;
+    *reinterpret_cast<uint4 *>(e) = hot;
 }
 
-// ct_lookup4/6 (conntrack.h:310-437, dir = CT_INGRESS): reverse-direction
-// probe of t, then forward probe of the reversed tuple tf.  Both share a home
-// line (GF_HASH_CT), so one ht_find2 walk answers both probes.  On return t
-// holds the tuple the reference leaves in *tuple (tf unless the first probe
-// hit), *tfl its flags.  Returns CT_NEW / CT_ESTABLISHED / CT_REPLY / CT_RELATED.
+// ct_lookup4/6 (conntrack.h:310-437, dir = CT_INGRESS), resolve part: the home
+// line of t (shared by the reverse-direction tuple t and the forward tuple tf
+// under GF_HASH_CT) was loaded by the caller.  Reverse probe of t, then forward
+// probe of tf, answered by one walk.  On return t holds the tuple the reference
+// leaves in *tuple (tf unless the first probe hit), *tfl its flags, and pr the
+// walk (its EMPTY slot is where ct_create inserts).
 template <int KSZ, int TW, int U>
-__device__ __forceinline__ int ct_lookup(const gf_htab_desc &d, uint32_t *t, uint32_t nh, uint32_t &tfl, int action,
-                                         bool syn, uint32_t len, uint32_t now, bool acct, CtState &st,
-                                         bool &fwd_absent, uint32_t &ab) {
+__device__ __forceinline__ int ct_lookup(const gf_htab_desc &d, ProbeLine<KSZ, U, 4> &L, uint32_t *t, uint32_t nh,
+                                         uint32_t &tfl, int action, bool syn, uint32_t len, uint32_t now, bool acct,
+                                         CtState &st, ProbeRes &pr, uint32_t &ab) {
     constexpr int AW = (TW - 2) / 2;                   // address words per side
     uint32_t tf[TW];
 #pragma unroll
     for (int k = 0; k < AW; k++) { tf[k] = t[AW + k]; tf[AW + k] = t[k]; }
     tf[TW - 2] = (t[TW - 2] >> 16) | (t[TW - 2] << 16);
     tf[TW - 1] = nh | ((tfl ^ 1u) << 8);
-    bool is_b;
-    int64_t f = ht_find2<KSZ, U>(d, t, tf, key_hash<KSZ, GF_HASH_CT>(t), &is_b);
+    pr = probe2<KSZ, U, 4>(d, t, tf, L);
     ab += KSZ;
-    fwd_absent = false;
-    if (f >= 0 && !is_b) {
-        ct_hit(d, f, action, syn, len, now, acct, st, ab);
+    uint4 hot = make_uint4(0, 0, 0, 0);
+    if (pr.f >= 0) {
+        constexpr int NW = Hdr<KSZ, 4>::NW;
+        if (pr.u >= 0) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (u == pr.u) hot = make_uint4(L.hd[u].w[NW - 4], L.hd[u].w[NW - 3], L.hd[u].w[NW - 2], L.hd[u].w[NW - 1]);
+        } else {
+            hot = *reinterpret_cast<const uint4 *>(ht_val(d, (uint64_t)pr.f));
+        }
+    }
+    if (pr.f >= 0 && !pr.is_b) {
+        ct_hit(d, pr.f, hot, action, syn, len, now, acct, st, ab);
         return (tfl & 2u) ? CT_RELATED : CT_REPLY;
     }
     ab += KSZ;
 #pragma unroll
     for (int k = 0; k < TW; k++) t[k] = tf[k];
     tfl ^= 1u;
-    if (f < 0) { fwd_absent = true; return CT_NEW; }
-    ct_hit(d, f, action, syn, len, now, acct, st, ab);
+    if (pr.f < 0) return CT_NEW;
+    ct_hit(d, pr.f, hot, action, syn, len, now, acct, st, ab);
     return CT_ESTABLISHED;
 }
 
-// ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0)
+// ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0).  The
+// tuple goes to the EMPTY slot the lookup walk ended on (one CAS), the related
+// entry to its cached slot when this lane wrote it before.
 template <int KSZ, int TW, int U>
 __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
-                                         uint32_t len, uint32_t now, bool strict, bool absent, int *added,
-                                         uint32_t &ab) {
-    constexpr int NHW = TW - 1;
-    ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written                        // word holding nexthdr | flags << 8
+                                         uint32_t len, uint32_t now, bool strict, const ProbeRes &pr, int *added,
+                                         RelCache<TW> &rc, uint32_t &ab) {
+    constexpr int NHW = TW - 1;                         // word holding nexthdr | flags << 8
+    ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written
     uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
     uint32_t fl = (nh == 6) ? 0u : F_SEEN_NON_SYN;      // ct_update_timeout(syn = nexthdr == TCP)
     uint32_t life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
-    uint32_t v[12] = {1u, 0u, len, 0u, 0u, 0u, 0u, 0u, life, fl | (rev_nat << 16), 0u, src_sec};
-    if (ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, t, v, strict, added, absent) < 0) return D_CT_CREATE_FAILED;
+    // GF_VCODEC_CT: lifetime, flags|rev_nat, rx_packets/bytes lo, hi, tx, unused, src_sec_id
+    uint32_t v[12] = {life, fl | (rev_nat << 16), 1u, len, 0u, 0u, 0u, 0u, 0u, 0u, 0u, src_sec};
+    if (ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, t, v, strict, added, true, pr.empty, pr.empty_word) < 0)
+        return D_CT_CREATE_FAILED;
     uint32_t it[TW];
 #pragma unroll
     for (int k = 0; k < TW; k++) it[k] = t[k];
     it[NHW - 1] = 0;                                    // sport = dport = 0
     it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
-    v[9] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
-    if (ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+    v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
+    bool same = rc.slot >= 0;
+#pragma unroll
+    for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
+    if (same) {                                         // BPF_ANY over the entry this lane wrote
+        store_words<12>(ht_val(d, (uint64_t)rc.slot), v);
+        return 0;
+    }
+    int64_t s = ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added);
+    if (s < 0) return D_CT_CREATE_FAILED;
+#pragma unroll
+    for (int k = 0; k < TW; k++) rc.k[k] = it[k];
+    rc.slot = s;
     return 0;
 }
 
@@ -472,31 +552,48 @@ __device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, u
     acc.add(reinterpret_cast<unsigned long long *>(ht_val(d, (uint64_t)f) + 8), len);
 }
 
-// __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168)
-__device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t identity, uint32_t dport,
-                              uint32_t proto, uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab,
-                              PolAcc &acc) {
+// Policy slots are probed with the first 16 B of the value (proxy_port) so an
+// L4 hit needs no second load.
+typedef ProbeLine<8, GF_POL_U, 4> PolLine;
+
+__device__ __forceinline__ uint32_t pol_home(uint32_t identity, uint32_t dport, uint32_t proto) {
+    uint32_t kw[2] = {identity, dport | (proto << 16)};
+    return key_hash<8, GF_HASH_POLICY>(kw);
+}
+
+// __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168).
+// pl: the home line of (identity, *) loaded by the caller (identity != 0 hashes
+// by identity only, so the L4 and the L3 key of the identity share it).
+__device__ int policy_ingress(const Ep &ep, PolLine &pl, uint32_t identity, uint32_t dport, uint32_t proto,
+                              uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc) {
+    const uint32_t flags = ep.flags;
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
-    const gf_htab_desc pd = c->policy;
+    const gf_htab_desc pd = ep.pdesc();
     int64_t f;
+    uint32_t pp = 0;
     {
         uint32_t k4[2] = {identity, dport | (proto << 16)}, k3[2] = {identity, 0u};
-        if ((flags & GF_LXC_F_HAVE_L4_POLICY) && identity) {
-            // L4 then L3 key of one identity share a home line (GF_HASH_POLICY)
-            bool l3;
-            f = ht_find2<8, GF_POL_U>(pd, k4, k3, key_hash<8, GF_HASH_POLICY>(k4), &l3);
+        if (identity == 0) pl.load(pd, pol_home(0u, dport, proto));   // full-key hash: not preloaded
+        if (flags & GF_LXC_F_HAVE_L4_POLICY) {
+            ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k4, k3, pl, identity != 0);
             ab += 8;
-            if (f >= 0 && !l3) goto proxy;
+            if (r.f >= 0 && !r.is_b) {
+                pp = 0xffffffffu;
+#pragma unroll
+                for (int u = 0; u < GF_POL_U; u++)
+                    if (u == r.u) pp = pl.hd[u].w[4] & 0xffffu;
+                f = r.f;
+                goto proxy;
+            }
             ab += 8;
+            if (!identity) {                                // L3 key {0,0,0}: its own home line
+                f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
+            } else f = r.f;
             if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
         } else {
-            if (flags & GF_LXC_F_HAVE_L4_POLICY) {
-                f = ht_find<8, GF_POL_U>(pd, k4, key_hash<8, GF_HASH_POLICY>(k4));
-                ab += 8;
-                if (f >= 0) goto proxy;
-            }
-            f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
+            if (identity) { ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k3, k3, pl, false); f = r.f; }
+            else f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
             ab += 8;
             if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
         }
@@ -505,20 +602,21 @@ __device__ int policy_ingress(const gf_lxc_dev *c, uint32_t flags, uint32_t iden
         uint32_t kw[2] = {0u, dport | (proto << 16)};
         f = ht_find<8, GF_POL_U>(pd, kw, key_hash<8, GF_HASH_POLICY>(kw));
         ab += 8;
-        if (f >= 0) goto proxy;
+        if (f >= 0) { pp = 0xffffffffu; goto proxy; }
     }
     goto deny;
 proxy: {
         ab += 40;                                       // entry read + counters written
         policy_count(pd, f, len, acc);
-        uint32_t pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
+        if (pp == 0xffffffffu) pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
-        return l4_proxy_lookup(c, proto, dport);
+        return l4_proxy_lookup(ep.c, proto, dport);
     }
 deny:
     if (identity < 256) {                               // identity_is_reserved
-        if (v6) { if (c->cidr6.root_bits) ab += 21; if (trie_lookup(c->cidr6, cidr_addr)) return TC_OK; }
-        else { if (c->cidr4.root_bits) ab += 9; if (trie_lookup(c->cidr4, cidr_addr)) return TC_OK; }
+        const gf_lxc_dev *c = ep.c;
+        if (v6) { const gf_trie_desc tr = c->cidr6; if (tr.root_bits) ab += 21; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
+        else { const gf_trie_desc tr = c->cidr4; if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
     }
     return D_POLICY;
 }
@@ -590,10 +688,11 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
-__device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, int &fwd,
-                           uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc) {
+__device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &fwd, uint8_t &ofl, uint16_t &proxy,
+                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
+    const uint32_t flags = ep.flags;
     uint32_t nh = r.proto;
     uint32_t t[4] = {r.daddr, r.saddr, 0u, nh};
     uint32_t tfl = 0;                                   // TUPLE_F_OUT (ingress)
@@ -601,14 +700,20 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     int e = ct_l4(nh, false, r, t[2], tfl, action, syn);
     if (e < 0) return e;
     t[3] = nh | (tfl << 8);
+    const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT4) ? X.ct4 : gf_htab_desc{};
+    // the CT home line and the policy home line of the source identity go out together
+    ProbeLine<14, GF_CT4_U, 4> cl;
+    cl.load(ct, key_hash<14, GF_HASH_CT>(t));
+    PolLine pl;
+    if (r.src_identity && (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS)
+        pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
-    const gf_htab_desc ct = c->ct4;
     CtState st{0, 0};
-    bool absent;
-    int ret = ct_lookup<14, 4, GF_CT4_U>(ct, t, nh, tfl, action, syn, len, X.now, acct, st, absent, ab);
+    ProbeRes pr;
+    int ret = ct_lookup<14, 4, GF_CT4_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
-        const gf_htab_desc rn = c->revnat4;
+        const gf_htab_desc rn = ep.c->revnat4;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 8;
@@ -620,14 +725,18 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
         }
     }
     uint32_t orig_sip = r.saddr;
-    int verdict = policy_ingress(c, flags, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab, acc);
+    int verdict = (GF_DIAG & 4) ? 0 : policy_ingress(ep, pl, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab, acc);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { ab += 14; ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added); }
+        if (ret == CT_ESTABLISHED) {
+            ab += 14;
+            ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added);
+            rc.slot = -1;
+        }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;                         // skip_proxy
-    if (ret == CT_NEW) {
-        ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, absent, added, ab);
+    if (ret == CT_NEW && !(GF_DIAG & 8)) {
+        ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -642,12 +751,13 @@ __device__ int ipv4_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
 }
 
 // ipv6_policy, bpf/bpf_lxc.c:745-862
-__device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags, const gf_rec &r, uint32_t i,
-                           int &fwd, uint8_t &ofl, uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab,
-                           PolAcc &acc) {
+__device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
+                           uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc,
+                           RelCache<10> &rc) {
     uint32_t len = r.len;
     if (len < 54) return D_INVALID;
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
+    const uint32_t flags = ep.flags;
     uint32_t nh = r.proto;
     uint4 d = reinterpret_cast<const uint4 *>(X.daddr6)[i];
     uint4 s = reinterpret_cast<const uint4 *>(X.saddr6)[i];
@@ -660,14 +770,19 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     int e = ct_l4(nh, true, r, t[8], tfl, action, syn);
     if (e < 0) return e;
     t[9] = nh | (tfl << 8);
+    const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT6) ? X.ct6 : gf_htab_desc{};
+    ProbeLine<40, GF_CT6_U, 4> cl;
+    cl.load(ct, key_hash<40, GF_HASH_CT>(t));
+    PolLine pl;
+    if (r.src_identity && (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS)
+        pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
-    const gf_htab_desc ct = c->ct6;
     CtState st{0, 0};
-    bool absent;
-    int ret = ct_lookup<40, 10, GF_CT6_U>(ct, t, nh, tfl, action, syn, len, X.now, acct, st, absent, ab);
+    ProbeRes pr;
+    int ret = ct_lookup<40, 10, GF_CT6_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
     if (st.rev_nat) {
-        const gf_htab_desc rn = c->revnat6;
+        const gf_htab_desc rn = ep.c->revnat6;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 20;
@@ -677,14 +792,18 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
             if (r2 < 0) return r2;
         }
     }
-    int verdict = policy_ingress(c, flags, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc);
+    int verdict = policy_ingress(ep, pl, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { ab += 40; ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added); }
+        if (ret == CT_ESTABLISHED) {
+            ab += 40;
+            ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added);
+            rc.slot = -1;
+        }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;
     if (ret == CT_NEW) {
-        ret = ct_create<40, 10, GF_CT6_U>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, absent, added, ab);
+        ret = ct_create<40, 10, GF_CT6_U>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -698,22 +817,44 @@ __device__ int ipv6_policy(const IngCtx &X, const gf_lxc_dev *c, uint32_t flags,
     return 0;
 }
 
-// handle_policy, bpf/bpf_lxc.c:980-1024
-__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, int *added,
-                                                       uint32_t &ab, PolAcc &acc) {
+// Per-lane state carried across the packets of the lane's buckets.
+struct Lane {
+    Ep ep;
+    PolAcc acc;
+    RelCache<4> rc4;
+    RelCache<10> rc6;
+    int added = 0;
+};
+// (the unused cache of the other family is dead code in each specialization)
+
+// handle_policy, bpf/bpf_lxc.c:980-1024.  FAM selects the CT path compiled in:
+// 4 = the IPv4 path plus every packet that cannot reach conntrack (no IP
+// header: their early returns need no CT code), 6 = IPv6 packets that reach
+// conntrack.  The sort key keeps the two sets in different buckets.
+template <int FAM>
+__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane &ln,
+                                                       uint32_t &ab) {
     gf_ingress_out o{};
-    uint32_t sl = X.slot_of[r.lxc_id];
-    if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }
-    const gf_lxc_dev *c = X.cfgs + (sl - 1);
-    uint32_t flags = c->flags;
+    uint32_t sl = r.ep;
+    if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }   // missed tail call (DROP_MISSED_TAIL_CALL)
+    ln.ep.use(X, sl);
+    uint32_t flags = ln.ep.flags;
     int fwd = 0, ret;
     uint8_t fl = 0;
     uint16_t proxy = 0;
     uint32_t ifindex = r.ifindex;
     uint32_t cls = r.cls & 3u;
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
-    else if (cls == 2) { ab += 47; ret = ipv6_policy(X, c, flags, r, i, fwd, fl, proxy, ifindex, added, ab, acc); }
-    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) { ab += 23; ret = ipv4_policy(X, c, flags, r, fwd, fl, proxy, ifindex, added, ab, acc); }
+    else if (cls == 2) {
+        ab += 47;
+        if (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc6);
+        else ret = D_INVALID;                       // ipv6_policy: short frame or batch without v6 columns
+    }
+    else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
+        ab += 23;
+        if (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc4);
+        else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
+    }
     else ret = D_UNKNOWN_L3;
     o.ct_ret = (uint8_t)fwd;
     if (ret < 0 || ret == TC_SHOT) {
@@ -727,7 +868,8 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     return o;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, uint32_t *keys, uint32_t *vals) {
+__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
+                                                    uint32_t *keys, uint32_t *vals) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c.n) return;
     gf_rec r;
@@ -737,7 +879,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, 
     r.l4w0 = c.l4w0[i]; r.l4w3 = c.l4w3[i];
     r.src_identity = c.src_identity ? c.src_identity[i] : 0u;
     r.ifindex = c.ifindex ? c.ifindex[i] : 0u;
-    r.lxc_id = c.lxc_id ? c.lxc_id[i] : 0;
+    r.ep = slot_of[c.lxc_id ? c.lxc_id[i] : 0];        // tail_call(cilium_policy, lxc_id) target
     r.l4_off = c.l4_off[i];
     r.proto = c.proto[i];
     uint32_t cls = et == 0x0800 ? 1u : et == 0x86DD ? 2u : 0u;
@@ -746,18 +888,19 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, 
     uint32_t h;
     // Only packets that can reach conntrack (an IP header is present) are bound to
     // their flow group; the rest carry no ordering constraint and are spread out.
-    // The full 32-bit group hash is the sort key: two groups share a bucket only on
-    // a 32-bit hash collision (always safe: a bucket is serialized as a whole).
+    // The group hash is the sort key: two groups share a bucket only on a 31-bit
+    // hash collision (always safe: a bucket is serialized as a whole).
     bool ct_ok = ((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6);
+    // Bit 31 of the key is the family of the CT path (1: IPv6 reaching conntrack).
     if (!ct_ok) {
-        h = gf_hash_words(&i, 1, 4);
+        h = gf_hash_words(&i, 1, 4) & 0x7fffffffu;
     } else if ((cls & 3) == 2) {
         uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
         uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
         uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
-        h = gf_pair_hash6(sw, dw);
+        h = gf_pair_hash6(sw, dw) | 0x80000000u;
     } else {
-        h = gf_pair_hash4(r.saddr, r.daddr);
+        h = gf_pair_hash4(r.saddr, r.daddr) & 0x7fffffffu;
     }
     rec[i] = r;
     keys[i] = h;
@@ -772,12 +915,13 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, gf_rec *rec, 
 // (LPT): k_bucket_order lists them by packet count, descending, and waves take
 // the next 64 entries of that list from a device queue, so the lanes of a wave
 // carry equal work and the deepest buckets start first.
+template <int FAM>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
-                                        Stats &st, bool stats, int &added, PolAcc &acc) {
+                                        Stats &st, bool stats, Lane &ln) {
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy(X, r, i, &added, ab, acc);
-    out[i] = o;
-    if (stats) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
+    gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
+    if (!(GF_DIAG & 1)) out[i] = o;
+    if (stats && !(GF_DIAG & 2)) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
 }
 
 __device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t *ct_count, uint32_t *lds_added) {
@@ -787,18 +931,33 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t
     if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ing_groups(IngCtx X, const uint32_t *nruns, const uint32_t *order,
+// Schedule words (device): hist[2][GF_LCAP+1] | base[2][..] | cursor[2][..] |
+// nruns | queue[2] | nfam[2] (buckets per family; family 1's order follows 0's).
+#define GF_LCAP 1024u
+#define GF_SCHED_HIST(p) (p)
+#define GF_SCHED_BASE(p) ((p) + 2 * (GF_LCAP + 1))
+#define GF_SCHED_CURSOR(p) ((p) + 4 * (GF_LCAP + 1))
+#define GF_SCHED_NRUNS(p) ((p) + 6 * (GF_LCAP + 1))
+#define GF_SCHED_QUEUE(p) ((p) + 6 * (GF_LCAP + 1) + 1)
+#define GF_SCHED_NFAM(p) ((p) + 6 * (GF_LCAP + 1) + 3)
+#define GF_SCHED_WORDS (6 * (GF_LCAP + 1) + 5)
+
+template <int FAM>
+__global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint32_t *order,
                                                       const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
-                                                      const gf_rec *rec, gf_ingress_out *out, uint32_t *queue,
-                                                      uint32_t *ct_count, unsigned long long *stats) {
+                                                      const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
+                                                      unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    const uint32_t nb = *nruns, lane = threadIdx.x & 63u;
-    int added = 0;
-    PolAcc acc;
+    constexpr int F = FAM == 6 ? 1 : 0;
+    const uint32_t *nfam = GF_SCHED_NFAM(sched);
+    uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
+    const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
+    if (F) order += nfam[0];
+    Lane ln;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -810,79 +969,105 @@ __global__ __launch_bounds__(BLOCK) void k_ing_groups(IngCtx X, const uint32_t *
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = rec[i];
+        ln.rc4.slot = -1;                               // a new bucket: new flow groups
+        ln.rc6.slot = -1;
         for (uint32_t k = 0; k < c; k++) {
-            // next record and the index after it are in flight while packet k runs
-            gf_rec rn;
+            // the next record and the index after it are in flight while packet k runs
             uint32_t in2 = 0;
-            if (k + 1 < c) rn = rec[inx];
             if (k + 2 < c) in2 = perm[b + k + 2];
-            ing_one(X, i, r, out, st, stats != nullptr, added, acc);
+#if GF_PREFETCH_REC
+            gf_rec rn;
+            if (k + 1 < c) rn = rec[inx];
+            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
             i = inx; inx = in2; r = rn;
+#else
+            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
+            i = inx; inx = in2;
+            if (k + 1 < c) r = rec[i];
+#endif
         }
     }
-    acc.flush();
-    flush_added(X, added, ct_count, &sadd);
+    ln.acc.flush();
+    flush_added(X, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }
 
 #define GF_LCAP 1024u
-// Bucket-size histogram: block-local LDS bins, one global add per non-empty bin.
+// Bucket-size histogram per family (bit 31 of the bucket's sorted key):
+// block-local LDS bins, one global add per non-empty bin.
 #define GF_SCHED_ITEMS 4096
-__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, const uint32_t *nruns, uint32_t *hist) {
-    __shared__ uint32_t h[GF_LCAP + 1];
-    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
+__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, const uint32_t *off, const uint32_t *skeys,
+                                                       uint32_t *sched) {
+    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
-    uint32_t nq = *nruns;
+    uint32_t nq = *GF_SCHED_NRUNS(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q];
-        if (c) atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u);
+        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x)
+    uint32_t *hist = GF_SCHED_HIST(sched);
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
         if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-// base[c] = number of buckets with count > c (start of bin c in the descending
-// order), one block of GF_LCAP threads: thread k owns bin c = GF_LCAP - k.  Also
-// clears the order cursors and the work queue.
-__global__ __launch_bounds__(GF_LCAP) void k_bucket_base(const uint32_t *hist, uint32_t *base, uint32_t *cursor,
-                                                          uint32_t *queue) {
+// base[f][c] = start of (family f, count c) in the order list: family 0 first,
+// each family by count descending.  One block of GF_LCAP threads (thread k owns
+// bin c = GF_LCAP - k); also clears the cursors and the work queues.
+__global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
     __shared__ uint32_t s[GF_LCAP];
+    __shared__ uint32_t tot0;
     const uint32_t k = threadIdx.x, c = GF_LCAP - k;
-    s[k] = hist[c];
-    __syncthreads();
-    for (uint32_t d = 1; d < GF_LCAP; d <<= 1) {      // inclusive scan over bins GF_LCAP .. 1
-        uint32_t v = k >= d ? s[k - d] : 0u;
+    const uint32_t *hist = GF_SCHED_HIST(sched);
+    uint32_t *base = GF_SCHED_BASE(sched), *cursor = GF_SCHED_CURSOR(sched);
+    for (uint32_t f = 0; f < 2; f++) {
+        const uint32_t *hf = hist + f * (GF_LCAP + 1);
+        s[k] = hf[c];
         __syncthreads();
-        s[k] += v;
+        for (uint32_t d = 1; d < GF_LCAP; d <<= 1) {    // inclusive scan over bins GF_LCAP .. 1
+            uint32_t v = k >= d ? s[k - d] : 0u;
+            __syncthreads();
+            s[k] += v;
+            __syncthreads();
+        }
+        uint32_t add = f ? tot0 : 0u;
+        base[f * (GF_LCAP + 1) + c] = add + s[k] - hf[c];
+        cursor[f * (GF_LCAP + 1) + c] = 0;
+        if (k == 0) { base[f * (GF_LCAP + 1)] = 0; cursor[f * (GF_LCAP + 1)] = 0; }
+        __syncthreads();
+        if (k == GF_LCAP - 1) {
+            GF_SCHED_NFAM(sched)[f] = s[k];
+            if (!f) tot0 = s[k];
+            GF_SCHED_QUEUE(sched)[f] = 0;
+        }
         __syncthreads();
     }
-    base[c] = s[k] - hist[c];
-    cursor[c] = 0;
-    if (k == 0) { base[0] = 0; cursor[0] = 0; *queue = 0; }
 }
 
-// order[] = non-empty buckets sorted by count, descending (ties in any order):
-// block-local counts per bin, one global reservation per (block, bin).
-__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, const uint32_t *nruns, const uint32_t *base,
-                                                        uint32_t *cursor, uint32_t *order) {
-    __shared__ uint32_t h[GF_LCAP + 1];
-    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x) h[k] = 0;
+// order[] = non-empty buckets, family 0 then 1, each by count descending (ties in
+// any order): block-local counts per bin, one global reservation per (block, bin).
+__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, const uint32_t *off, const uint32_t *skeys,
+                                                        uint32_t *sched, uint32_t *order) {
+    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
-    uint32_t nq = *nruns;
+    uint32_t nq = *GF_SCHED_NRUNS(sched);
+    const uint32_t *base = GF_SCHED_BASE(sched);
+    uint32_t *cursor = GF_SCHED_CURSOR(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q];
-        if (c) atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u);
+        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k <= GF_LCAP; k += blockDim.x)
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
         if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q];
-        if (c) order[atomicAdd(&h[c < GF_LCAP ? c : GF_LCAP], 1u)] = q;
+        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = q;
     }
 }
 
@@ -1083,8 +1268,8 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         if (m->ksz != b.k || m->is_lpm() != b.lpm || (!b.lpm && m->vsz != b.v)) return -EINVAL;
         *b.out = m;
     }
-    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->make_fixed_capacity(); }
-    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->make_fixed_capacity(); }
+    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(); }
+    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(); }
     if (p->policy) p->policy->set_hash_mode(GF_HASH_POLICY);
     return new_handle(p);
 }
@@ -1174,8 +1359,8 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
             d.l4[j].nexthdr = p->cfg.l4_ingress[j].nexthdr;
         }
         if (p->policy) d.policy = p->policy->hdesc();
-        if (p->ct4) { d.ct4 = p->ct4->hdesc(); ctmaps.push_back(p->ct4); }
-        if (p->ct6) { d.ct6 = p->ct6->hdesc(); ctmaps.push_back(p->ct6); any_v6 = true; }
+        if (p->ct4) { d.ct4 = p->ct4->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT4; ctmaps.push_back(p->ct4); }
+        if (p->ct6) { d.ct6 = p->ct6->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT6; ctmaps.push_back(p->ct6); any_v6 = true; }
         if (p->cidr4) d.cidr4 = p->cidr4->tdesc();
         if (p->cidr6) d.cidr6 = p->cidr6->tdesc();
         if (p->revnat4) d.revnat4 = p->revnat4->hdesc();
@@ -1197,6 +1382,9 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     // packet inserts at most 2 entries), read back from the device only when the
     // bound gets near the limit — steady-state batches never wait on the GPU here.
     uint32_t strict = 0;
+    gf_htab_desc cfg_ct4{}, cfg_ct6{};
+    if (ct4m) cfg_ct4 = ct4m->hdesc();
+    if (ct6m) cfg_ct6 = ct6m->hdesc();
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
         uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
@@ -1211,8 +1399,8 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
         if (m->dev_count_hi + 2ull * pkts->n > limit) strict = 1;
         m->dev_count_hi += 2ull * pkts->n;
         if (m->type == GF_MAP_TYPE_LRU_HASH) {
-            if (m == ct4m) { for (auto &d : cfgs) d.ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
-            else { for (auto &d : cfgs) d.ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu); }
+            if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
+            else cfg_ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
         }
     }
     // device program table: uploaded only when it changed (programs, bindings,
@@ -1240,15 +1428,12 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     uint32_t n = pkts->n;
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-    const size_t SCHED_WORDS = 3 * (GF_LCAP + 1) + 2;   // hist | base | cursor | nruns | queue
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
         (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
         (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
-        (r = grow(w.sched, SCHED_WORDS * 4)))
+        (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
-    (void)any_v6;   // IPv6 packets in a batch without v6 columns are dropped (DROP_INVALID)
-    uint32_t *d_hist = (uint32_t *)w.sched.p, *d_base = d_hist + (GF_LCAP + 1), *d_cursor = d_base + (GF_LCAP + 1);
-    uint32_t *d_nruns = d_cursor + (GF_LCAP + 1), *d_queue = d_nruns + 1;
+    uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
     size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
                                     (uint32_t *)w.perm.p, n, 0, 32, s);
@@ -1259,7 +1444,8 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if ((r = grow(w.tmp, std::max(std::max(sort_bytes, scan_bytes), rle_bytes) + 256))) return r;
     {
         ProfScope ps("k_ing_pack", s);
-        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts, (gf_rec *)w.rec.p,
+        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
+                           (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
                            (uint32_t *)w.keys.p, (uint32_t *)w.vals.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
@@ -1283,40 +1469,46 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
                                            rocprim::plus<uint32_t>(), s), "exclusive_scan"))
             return -EIO;
     }
-    // 3. longest-first bucket order, built on the device (no host round trip)
+    // 3. longest-first bucket order per family, built on the device (no host round trip)
     {
         ProfScope ps("k_bucket_sched", s);
-        if (hip_ok(hipMemsetAsync(d_hist, 0, (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
+        if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
         uint32_t g = (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS;
         hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)d_nruns, d_hist);
-        hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, (const uint32_t *)d_hist, d_base, d_cursor,
-                           d_queue);
+                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched);
+        hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
         hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)d_nruns, (const uint32_t *)d_base, d_cursor, (uint32_t *)w.order.p);
+                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched, (uint32_t *)w.order.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_bucket_sched"))) return r;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
-    X.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
     X.saddr6 = pkts->saddr6; X.daddr6 = pkts->daddr6;
+    if (ct4m) X.ct4 = cfg_ct4;
+    if (ct6m) X.ct6 = cfg_ct6;
     X.now = now_sec; X.host_ifindex = host_ifindex();
     X.strict = strict;
-    // Non-strict mode accounts the net element change per map; with both families
-    // present each lane's `added` mixes them, so v6 batches use strict mode.
-    if (ct4m && ct6m) X.strict = 1;
-    uint32_t *cntp = ct4m ? (uint32_t *)ct4m->d_count.p : (ct6m ? (uint32_t *)ct6m->d_count.p : nullptr);
+    // Non-strict mode accounts each kernel's net element change into its family's map.
+    uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
     {
-        // resident-grid launch: every wave loops on the queue until it is drained
+        // resident-grid launches: every wave loops on its family's queue until it is drained
         uint32_t grid = resident_blocks(8);
         uint32_t need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
-        ProfScope ps("k_ing_groups", s);
-        hipLaunchKernelGGL(k_ing_groups, dim3(grid), dim3(BLOCK), 0, s, X, (const uint32_t *)d_nruns,
-                           (const uint32_t *)w.order.p, (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, d_queue, cntp, sink);
+        {
+            ProfScope ps("k_ing_groups", s);
+            hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint32_t *)w.order.p,
+                               (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p,
+                               (const gf_rec *)w.rec.p, out, cnt4, sink);
+        }
+        if (pkts->saddr6) {    // IPv6 packets reach conntrack only with v6 columns
+            ProfScope ps("k_ing_groups6", s);
+            hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint32_t *)w.order.p,
+                               (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p,
+                               (const gf_rec *)w.rec.p, out, cnt6, sink);
+        }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
     for (auto &p : progs) {

@@ -151,6 +151,21 @@ static void materialize(HTab &h) {
     }
 }
 
+void Map::set_value_codec(uint32_t c) {
+    if (is_lpm() || ht.codec == c) return;
+    if (c == GF_VCODEC_CT && vsz != GF_CT_VSZ) return;
+    pull();
+    uint8_t tmp[GF_CT_VSZ];
+    for (uint64_t i = 0; i < (ht.slots.empty() ? 0 : ht.nslots); i++) {
+        if (ht.state(i) != GF_SLOT_FULL) continue;
+        uint8_t *v = ht.val(i);
+        if (ht.codec == GF_VCODEC_CT) { gf_ct_decode(v, tmp); memcpy(v, tmp, vsz); }
+        if (c == GF_VCODEC_CT) { gf_ct_encode(v, tmp); memcpy(v, tmp, vsz); }
+    }
+    ht.codec = c;
+    dev_valid = false;
+}
+
 void Map::set_hash_mode(uint32_t m) {
     if (is_lpm() || ht.mode == m) return;
     pull();
@@ -262,6 +277,8 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
     }
     int r = pull(); if (r) return r;
     materialize(ht);
+    uint8_t enc[GF_CT_VSZ];
+    if (ht.codec == GF_VCODEC_CT) { gf_ct_encode(value, enc); value = enc; }
     int64_t i = ht.find(key);
     if (i >= 0) {
         if (fl == GF_NOEXIST) return -EEXIST;
@@ -299,7 +316,8 @@ int Map::lookup(const uint8_t *key, uint8_t *value) {
     if (ht.slots.empty()) return -ENOENT;
     int64_t i = ht.find(key);
     if (i < 0) return -ENOENT;
-    memcpy(value, ht.val((uint64_t)i), vsz);
+    if (ht.codec == GF_VCODEC_CT) gf_ct_decode(ht.val((uint64_t)i), value);
+    else memcpy(value, ht.val((uint64_t)i), vsz);
     return 0;
 }
 
