@@ -27,10 +27,10 @@ using namespace gfd;
 #endif
 // Tuning knobs of the flow-group kernel (tools/variants.sh sweeps them).
 #ifndef GF_PREFETCH_REC
-#define GF_PREFETCH_REC 1   // load the lane's next packet record while the current one runs
+#define GF_PREFETCH_REC 0   // load the lane's next packet record while the current one runs
 #endif
 #ifndef GF_ING_MINW
-#define GF_ING_MINW 1       // __launch_bounds__ min waves per SIMD (register budget)
+#define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
 #endif
 
 // ---------------------------------------------------------------- constants
@@ -358,9 +358,13 @@ struct CtState { uint32_t rev_nat, loopback; };
 // Slots per 128-B line of the fixed map layouts (gf_htab_layout): CT4 entry
 // 14+48 B -> 64-B slots, CT6 40+48 B -> 128-B slots, policy 8+24 B -> 64-B slots.
 // Only the number of headers fetched together depends on these; results do not.
+#ifndef GF_CT4_U
 #define GF_CT4_U 2
+#endif
 #define GF_CT6_U 1
+#ifndef GF_POL_U
 #define GF_POL_U 2
+#endif
 #define GF_POL_SLOT 64u    // gf_htab_layout(8, 24)
 #define GF_POL_VOFF 16u
 
@@ -561,12 +565,30 @@ __device__ __forceinline__ uint32_t pol_home(uint32_t identity, uint32_t dport, 
     return key_hash<8, GF_HASH_POLICY>(kw);
 }
 
-// __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168).
-// pl: the home line of (identity, *) loaded by the caller (identity != 0 hashes
-// by identity only, so the L4 and the L3 key of the identity share it).
-__device__ int policy_ingress(const Ep &ep, PolLine &pl, uint32_t identity, uint32_t dport, uint32_t proto,
-                              uint32_t len, bool v6, const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc) {
+// The lane's last policy decision.  __policy_can_access + the reserved-identity
+// CIDR check are a pure function of (program, identity, dport, proto, source
+// address for reserved identities) while a batch runs: the device never changes
+// policy keys, proxy ports, CIDR tries or L4 lists, only the entry counters —
+// which stay per packet.  Consecutive packets of a lane's flow group mostly ask
+// the same question, so the answer (and the entry to count) is kept.
+struct PolMemo {
+    uint32_t sl = 0, id = 0, pk = 0, sip = 0;
+    int verdict = 0;
+    int64_t f = -1;          // policy slot counted by the decision, -1: none
+    uint32_t ab = 0;         // algorithmic bytes the decision touches
+    __device__ __forceinline__ bool hit(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
+        return sl == s && id == identity && pk == k && (identity >= 256 || sip == a);
+    }
+};
+
+// __policy_can_access (policy.h:42-113) + policy_can_access_ingress (:133-168),
+// without the counter update: *fc = the entry the reference counts (or -1).
+// pl: the home line of (identity, *) if pl_loaded (identity != 0 hashes by
+// identity only, so the L4 and the L3 key of the identity share it).
+__device__ int policy_lookup(const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity, uint32_t dport,
+                             uint32_t proto, bool v6, const uint32_t *cidr_addr, uint32_t &ab, int64_t &fc) {
     const uint32_t flags = ep.flags;
+    fc = -1;
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_INGRESS)) return TC_OK;
     const gf_htab_desc pd = ep.pdesc();
@@ -574,7 +596,7 @@ __device__ int policy_ingress(const Ep &ep, PolLine &pl, uint32_t identity, uint
     uint32_t pp = 0;
     {
         uint32_t k4[2] = {identity, dport | (proto << 16)}, k3[2] = {identity, 0u};
-        if (identity == 0) pl.load(pd, pol_home(0u, dport, proto));   // full-key hash: not preloaded
+        if (!pl_loaded) pl.load(pd, identity ? pol_home(identity, 0u, 0u) : pol_home(0u, dport, proto));
         if (flags & GF_LXC_F_HAVE_L4_POLICY) {
             ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k4, k3, pl, identity != 0);
             ab += 8;
@@ -590,12 +612,12 @@ __device__ int policy_ingress(const Ep &ep, PolLine &pl, uint32_t identity, uint
             if (!identity) {                                // L3 key {0,0,0}: its own home line
                 f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
             } else f = r.f;
-            if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
+            if (f >= 0) { ab += 40; fc = f; return TC_OK; }
         } else {
             if (identity) { ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k3, k3, pl, false); f = r.f; }
             else f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
             ab += 8;
-            if (f >= 0) { ab += 40; policy_count(pd, f, len, acc); return TC_OK; }
+            if (f >= 0) { ab += 40; fc = f; return TC_OK; }
         }
     }
     if (flags & GF_LXC_F_HAVE_L4_POLICY) {
@@ -607,7 +629,7 @@ __device__ int policy_ingress(const Ep &ep, PolLine &pl, uint32_t identity, uint
     goto deny;
 proxy: {
         ab += 40;                                       // entry read + counters written
-        policy_count(pd, f, len, acc);
+        fc = f;
         if (pp == 0xffffffffu) pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
         return l4_proxy_lookup(ep.c, proto, dport);
@@ -619,6 +641,26 @@ deny:
         else { const gf_trie_desc tr = c->cidr4; if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
     }
     return D_POLICY;
+}
+
+// policy_can_access_ingress with the counter update (policy.h:67-92), through the
+// lane's decision memo (IPv4, or any non-reserved identity).
+__device__ __forceinline__ int policy_ingress(const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
+                                              uint32_t dport, uint32_t proto, uint32_t len, bool v6,
+                                              const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo &m) {
+    const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
+    const bool memo_ok = !v6 || identity >= 256;
+    if (memo_ok && m.hit(ep.sl, identity, pk, sip)) {
+        ab += m.ab;
+        if (m.f >= 0) policy_count(ep.pdesc(), m.f, len, acc);
+        return m.verdict;
+    }
+    uint32_t ab0 = ab;
+    int64_t fc;
+    int v = policy_lookup(ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
+    if (fc >= 0) policy_count(ep.pdesc(), fc, len, acc);
+    if (memo_ok) { m.sl = ep.sl; m.id = identity; m.pk = pk; m.sip = sip; m.verdict = v; m.f = fc; m.ab = ab - ab0; }
+    return v;
 }
 
 // __lb{4,6}_rev_nat verdict-affecting checks (lb.h:217-293, 447-512)
@@ -689,7 +731,7 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &fwd, uint8_t &ofl, uint16_t &proxy,
-                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc) {
+                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo &pm) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
     const uint32_t flags = ep.flags;
@@ -704,9 +746,12 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
     // the CT home line and the policy home line of the source identity go out together
     ProbeLine<14, GF_CT4_U, 4> cl;
     cl.load(ct, key_hash<14, GF_HASH_CT>(t));
+    // (unless the lane's policy memo already answers the NEW/ESTABLISHED question)
     PolLine pl;
-    if (r.src_identity && (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS)
-        pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
+    const bool pre = r.src_identity &&
+                     (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS &&
+                     !pm.hit(ep.sl, r.src_identity, (t[2] >> 16) | (nh << 16), r.saddr);
+    if (pre) pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     CtState st{0, 0};
     ProbeRes pr;
@@ -725,7 +770,8 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
         }
     }
     uint32_t orig_sip = r.saddr;
-    int verdict = (GF_DIAG & 4) ? 0 : policy_ingress(ep, pl, r.src_identity, t[2] & 0xffffu, nh, len, false, &orig_sip, ab, acc);
+    int verdict = (GF_DIAG & 4) ? 0 : policy_ingress(ep, pl, pre, r.src_identity, t[2] & 0xffffu, nh, len, false,
+                                                     &orig_sip, ab, acc, pm);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ab += 14;
@@ -753,7 +799,7 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
 // ipv6_policy, bpf/bpf_lxc.c:745-862
 __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
                            uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc,
-                           RelCache<10> &rc) {
+                           RelCache<10> &rc, PolMemo &pm) {
     uint32_t len = r.len;
     if (len < 54) return D_INVALID;
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
@@ -774,8 +820,10 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
     ProbeLine<40, GF_CT6_U, 4> cl;
     cl.load(ct, key_hash<40, GF_HASH_CT>(t));
     PolLine pl;
-    if (r.src_identity && (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS)
-        pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
+    const bool pre = r.src_identity &&
+                     (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS &&
+                     !(r.src_identity >= 256 && pm.hit(ep.sl, r.src_identity, (t[8] >> 16) | (nh << 16), 0u));
+    if (pre) pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     CtState st{0, 0};
     ProbeRes pr;
@@ -792,7 +840,7 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
             if (r2 < 0) return r2;
         }
     }
-    int verdict = policy_ingress(ep, pl, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc);
+    int verdict = policy_ingress(ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ab += 40;
@@ -821,6 +869,7 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
 struct Lane {
     Ep ep;
     PolAcc acc;
+    PolMemo pm;
     RelCache<4> rc4;
     RelCache<10> rc6;
     int added = 0;
@@ -847,12 +896,12 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
     else if (cls == 2) {
         ab += 47;
-        if (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc6);
+        if (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc6, ln.pm);
         else ret = D_INVALID;                       // ipv6_policy: short frame or batch without v6 columns
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc4);
+        if (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc4, ln.pm);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
     else ret = D_UNKNOWN_L3;
