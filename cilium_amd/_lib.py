@@ -17,6 +17,15 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"libgpuflow.so not found at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; g.build()'`")
 
+# One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64
+# (SONAME libamdhip64.so.7).  Loading torch first lets that copy satisfy
+# libgpuflow's libamdhip64.so.7 dependency; loading libgpuflow first would map
+# /opt/rocm's runtime as a second, separate HIP/HSA runtime next to torch's.
+try:
+    import torch  # noqa: F401
+except ImportError:   # hosts without torch (e.g. a cgo agent) use /opt/rocm's runtime
+    pass
+
 lib = C.CDLL(LIB_PATH)
 
 GF_MAX_L4_INGRESS = 64

@@ -15,7 +15,9 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 #include <rocprim/iterator/discard_iterator.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
+#include <new>
 #include <string.h>
 
 using namespace gf;
@@ -29,6 +31,11 @@ using namespace gfd;
 #ifndef GF_PREFETCH_REC
 #define GF_PREFETCH_REC 0   // load the lane's next packet record while the current one runs
 #endif
+#ifndef GF_KEY_BITS
+#define GF_KEY_BITS 32      // bucket key: family bit + (GF_KEY_BITS-1) bits of the group hash
+#endif
+#define GF_KEY_FAM (1u << (GF_KEY_BITS - 1))
+#define GF_KEY_HASH (GF_KEY_FAM - 1u)
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
 #endif
@@ -359,7 +366,7 @@ struct CtState { uint32_t rev_nat, loopback; };
 // 14+48 B -> 64-B slots, CT6 40+48 B -> 128-B slots, policy 8+24 B -> 64-B slots.
 // Only the number of headers fetched together depends on these; results do not.
 #ifndef GF_CT4_U
-#define GF_CT4_U 2
+#define GF_CT4_U 1
 #endif
 #define GF_CT6_U 1
 #ifndef GF_POL_U
@@ -373,17 +380,17 @@ struct CtState { uint32_t rev_nat, loopback; };
 struct Ep {
     uint32_t sl = 0;                 // program slot + 1 (0: none loaded)
     uint32_t flags = 0;
-    const gf_lxc_dev *c = nullptr;
     uint8_t *pol = nullptr;          // policy map slots / mask
     uint64_t pol_mask = 0;
     __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
         if (s == sl) return;
         sl = s;
-        c = X.cfgs + (s - 1);
+        const gf_lxc_dev *c = X.cfgs + (s - 1);
         flags = c->flags;
         pol = c->policy.slots;
         pol_mask = c->policy.mask;
     }
+    __device__ __forceinline__ const gf_lxc_dev *cfg(const IngCtx &X) const { return X.cfgs + (sl - 1); }
     __device__ __forceinline__ gf_htab_desc pdesc() const {
         gf_htab_desc d{};
         d.slots = pol; d.mask = pol_mask; d.ksz = 8; d.vsz = 24;
@@ -541,14 +548,15 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // totals with a fraction of the memory-side atomics.
 struct PolAcc {
     unsigned long long *p = nullptr;
-    unsigned long long pk = 0, by = 0;
+    unsigned long long by = 0;
+    uint32_t pk = 0;                 // a lane runs < 2^32 packets per launch
     __device__ __forceinline__ void flush() {
-        if (p) { atomicAdd(&p[0], pk); atomicAdd(&p[1], by); }
+        if (p) { atomicAdd(&p[0], (unsigned long long)pk); atomicAdd(&p[1], by); }
         p = nullptr; pk = 0; by = 0;
     }
     __device__ __forceinline__ void add(unsigned long long *q, uint32_t len) {
         if (q != p) { flush(); p = q; }
-        pk += 1ull; by += (unsigned long long)len;
+        pk += 1u; by += (unsigned long long)len;
     }
 };
 
@@ -585,7 +593,7 @@ struct PolMemo {
 // without the counter update: *fc = the entry the reference counts (or -1).
 // pl: the home line of (identity, *) if pl_loaded (identity != 0 hashes by
 // identity only, so the L4 and the L3 key of the identity share it).
-__device__ int policy_lookup(const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity, uint32_t dport,
+__device__ int policy_lookup(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity, uint32_t dport,
                              uint32_t proto, bool v6, const uint32_t *cidr_addr, uint32_t &ab, int64_t &fc) {
     const uint32_t flags = ep.flags;
     fc = -1;
@@ -632,11 +640,11 @@ proxy: {
         fc = f;
         if (pp == 0xffffffffu) pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
-        return l4_proxy_lookup(ep.c, proto, dport);
+        return l4_proxy_lookup(ep.cfg(X), proto, dport);
     }
 deny:
     if (identity < 256) {                               // identity_is_reserved
-        const gf_lxc_dev *c = ep.c;
+        const gf_lxc_dev *c = ep.cfg(X);
         if (v6) { const gf_trie_desc tr = c->cidr6; if (tr.root_bits) ab += 21; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
         else { const gf_trie_desc tr = c->cidr4; if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
     }
@@ -645,7 +653,7 @@ deny:
 
 // policy_can_access_ingress with the counter update (policy.h:67-92), through the
 // lane's decision memo (IPv4, or any non-reserved identity).
-__device__ __forceinline__ int policy_ingress(const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
+__device__ __forceinline__ int policy_ingress(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
                                               uint32_t dport, uint32_t proto, uint32_t len, bool v6,
                                               const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo &m) {
     const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
@@ -657,7 +665,7 @@ __device__ __forceinline__ int policy_ingress(const Ep &ep, PolLine &pl, bool pl
     }
     uint32_t ab0 = ab;
     int64_t fc;
-    int v = policy_lookup(ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
+    int v = policy_lookup(X, ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
     if (fc >= 0) policy_count(ep.pdesc(), fc, len, acc);
     if (memo_ok) { m.sl = ep.sl; m.id = identity; m.pk = pk; m.sip = sip; m.verdict = v; m.f = fc; m.ab = ab - ab0; }
     return v;
@@ -758,7 +766,7 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
     int ret = ct_lookup<14, 4, GF_CT4_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
-        const gf_htab_desc rn = ep.c->revnat4;
+        const gf_htab_desc rn = ep.cfg(X)->revnat4;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 8;
@@ -770,7 +778,7 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
         }
     }
     uint32_t orig_sip = r.saddr;
-    int verdict = (GF_DIAG & 4) ? 0 : policy_ingress(ep, pl, pre, r.src_identity, t[2] & 0xffffu, nh, len, false,
+    int verdict = (GF_DIAG & 4) ? 0 : policy_ingress(X, ep, pl, pre, r.src_identity, t[2] & 0xffffu, nh, len, false,
                                                      &orig_sip, ab, acc, pm);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
@@ -830,7 +838,7 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
     int ret = ct_lookup<40, 10, GF_CT6_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
     if (st.rev_nat) {
-        const gf_htab_desc rn = ep.c->revnat6;
+        const gf_htab_desc rn = ep.cfg(X)->revnat6;
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 20;
@@ -840,7 +848,7 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
             if (r2 < 0) return r2;
         }
     }
-    int verdict = policy_ingress(ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
+    int verdict = policy_ingress(X, ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ab += 40;
@@ -865,23 +873,25 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
     return 0;
 }
 
-// Per-lane state carried across the packets of the lane's buckets.
+// Per-lane state carried across the packets of the lane's buckets.  It lives in
+// LDS (one record per thread, k_ing_groups) so that registers hold only the
+// state of the packet in flight: the register budget is what bounds waves per
+// SIMD, and waves in flight are what hide the probes' memory latency.
+template <int FAM>
 struct Lane {
     Ep ep;
     PolAcc acc;
     PolMemo pm;
-    RelCache<4> rc4;
-    RelCache<10> rc6;
+    RelCache<FAM == 6 ? 10 : 4> rc;
     int added = 0;
 };
-// (the unused cache of the other family is dead code in each specialization)
 
 // handle_policy, bpf/bpf_lxc.c:980-1024.  FAM selects the CT path compiled in:
 // 4 = the IPv4 path plus every packet that cannot reach conntrack (no IP
 // header: their early returns need no CT code), 6 = IPv6 packets that reach
 // conntrack.  The sort key keeps the two sets in different buckets.
 template <int FAM>
-__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane &ln,
+__device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane<FAM> &ln,
                                                        uint32_t &ab) {
     gf_ingress_out o{};
     uint32_t sl = r.ep;
@@ -896,12 +906,12 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
     else if (cls == 2) {
         ab += 47;
-        if (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc6, ln.pm);
+        if constexpr (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
         else ret = D_INVALID;                       // ipv6_policy: short frame or batch without v6 columns
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc4, ln.pm);
+        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
     else ret = D_UNKNOWN_L3;
@@ -918,7 +928,7 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
 }
 
 __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
-                                                    uint32_t *keys, uint32_t *vals) {
+                                                    uint32_t *keys) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c.n) return;
     gf_rec r;
@@ -937,23 +947,23 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
     uint32_t h;
     // Only packets that can reach conntrack (an IP header is present) are bound to
     // their flow group; the rest carry no ordering constraint and are spread out.
-    // The group hash is the sort key: two groups share a bucket only on a 31-bit
-    // hash collision (always safe: a bucket is serialized as a whole).
+    // GF_KEY_BITS-1 bits of the group hash are the sort key: groups that collide
+    // share a bucket (always safe: a bucket is serialized as a whole), and a
+    // shorter key is one radix pass less.
     bool ct_ok = ((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6);
-    // Bit 31 of the key is the family of the CT path (1: IPv6 reaching conntrack).
+    // The top key bit is the family of the CT path (1: IPv6 reaching conntrack).
     if (!ct_ok) {
-        h = gf_hash_words(&i, 1, 4) & 0x7fffffffu;
+        h = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
     } else if ((cls & 3) == 2) {
         uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
         uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
         uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
-        h = gf_pair_hash6(sw, dw) | 0x80000000u;
+        h = (gf_pair_hash6(sw, dw) & GF_KEY_HASH) | GF_KEY_FAM;
     } else {
-        h = gf_pair_hash4(r.saddr, r.daddr) & 0x7fffffffu;
+        h = gf_pair_hash4(r.saddr, r.daddr) & GF_KEY_HASH;
     }
     rec[i] = r;
     keys[i] = h;
-    vals[i] = i;
 }
 
 // Flow-group schedule.  A bucket is a run of equal 32-bit group hash in the
@@ -966,7 +976,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 // carry equal work and the deepest buckets start first.
 template <int FAM>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
-                                        Stats &st, bool stats, Lane &ln) {
+                                        Stats &st, bool stats, Lane<FAM> &ln) {
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
     if (!(GF_DIAG & 1)) out[i] = o;
@@ -1006,7 +1016,8 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
     uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
     const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
     if (F) order += nfam[0];
-    Lane ln;
+    __shared__ __attribute__((aligned(16))) char lane_mem[BLOCK * sizeof(Lane<FAM>)];
+    Lane<FAM> &ln = *new (lane_mem + threadIdx.x * sizeof(Lane<FAM>)) Lane<FAM>();
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -1018,8 +1029,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = rec[i];
-        ln.rc4.slot = -1;                               // a new bucket: new flow groups
-        ln.rc6.slot = -1;
+        ln.rc.slot = -1;                                // a new bucket: new flow groups
         for (uint32_t k = 0; k < c; k++) {
             // the next record and the index after it are in flight while packet k runs
             uint32_t in2 = 0;
@@ -1053,7 +1063,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, cons
     uint32_t nq = *GF_SCHED_NRUNS(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
@@ -1107,7 +1117,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
     uint32_t *cursor = GF_SCHED_CURSOR(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
@@ -1115,7 +1125,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
         if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> 31;
+        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = q;
     }
 }
@@ -1163,7 +1173,7 @@ void prof_drain() {
 }
 
 struct Workspace {
-    DevBuf rec, keys, vals, skeys, perm, cnt, off, tmp, sched, order;
+    DevBuf rec, keys, skeys, perm, cnt, off, tmp, sched, order;
 };
 Workspace &ws() { static Workspace w; return w; }
 
@@ -1478,14 +1488,14 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
-        (r = grow(w.vals, (size_t)n * 4)) || (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
+        (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
         (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
         (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
     uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
     size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
-                                    (uint32_t *)w.perm.p, n, 0, 32, s);
+    (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
+                                    rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0, GF_KEY_BITS, s);
     (void)rocprim::run_length_encode(nullptr, rle_bytes, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
                                      (uint32_t *)w.cnt.p, d_nruns, s);
     (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
@@ -1495,14 +1505,15 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
         ProfScope ps("k_ing_pack", s);
         hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
                            (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
-                           (uint32_t *)w.keys.p, (uint32_t *)w.vals.p);
+                           (uint32_t *)w.keys.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
-        if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p, (uint32_t *)w.vals.p,
-                                             (uint32_t *)w.perm.p, n, 0, 32, s), "radix_sort_pairs"))
+        if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
+                                             rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0,
+                                             GF_KEY_BITS, s), "radix_sort_pairs"))
             return -EIO;
     }
     {

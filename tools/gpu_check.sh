@@ -5,7 +5,7 @@ set -e
 T=${1:-dev}
 O=$(pwd)/gpurun_out/$T
 mkdir -p "$O"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > "$O/par.log" 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/par.log" 2>&1
 echo "parity ok"
 timeout -k 10 300 python -u bench.py > "$O/bench.json" 2> "$O/bench.err"
 echo "bench ok"
