@@ -380,15 +380,15 @@ struct CtState { uint32_t rev_nat, loopback; };
 struct Ep {
     uint32_t sl = 0;                 // program slot + 1 (0: none loaded)
     uint32_t flags = 0;
-    uint8_t *pol = nullptr;          // policy map slots / mask
-    uint64_t pol_mask = 0;
+    uint8_t *pol = nullptr;          // policy map slots / mask (policy maps hold < 2^32 slots)
+    uint32_t pol_mask = 0;
     __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
         if (s == sl) return;
         sl = s;
         const gf_lxc_dev *c = X.cfgs + (s - 1);
         flags = c->flags;
         pol = c->policy.slots;
-        pol_mask = c->policy.mask;
+        pol_mask = (uint32_t)c->policy.mask;
     }
     __device__ __forceinline__ const gf_lxc_dev *cfg(const IngCtx &X) const { return X.cfgs + (sl - 1); }
     __device__ __forceinline__ gf_htab_desc pdesc() const {
@@ -547,16 +547,19 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // with one pair of atomics when the entry changes and at the end — the same
 // totals with a fraction of the memory-side atomics.
 struct PolAcc {
-    unsigned long long *p = nullptr;
-    unsigned long long by = 0;
-    uint32_t pk = 0;                 // a lane runs < 2^32 packets per launch
-    __device__ __forceinline__ void flush() {
-        if (p) { atomicAdd(&p[0], (unsigned long long)pk); atomicAdd(&p[1], by); }
-        p = nullptr; pk = 0; by = 0;
+    unsigned long long *p[2] = {nullptr, nullptr};
+    uint32_t pk[2] = {0, 0}, by[2] = {0, 0};   // flushed before a 32-bit sum could wrap
+    uint32_t next = 0;
+    __device__ __forceinline__ void flush_one(int j) {
+        if (p[j]) { atomicAdd(&p[j][0], (unsigned long long)pk[j]); atomicAdd(&p[j][1], (unsigned long long)by[j]); }
+        p[j] = nullptr; pk[j] = 0; by[j] = 0;
     }
+    __device__ __forceinline__ void flush() { flush_one(0); flush_one(1); }
     __device__ __forceinline__ void add(unsigned long long *q, uint32_t len) {
-        if (q != p) { flush(); p = q; }
-        pk += 1u; by += (unsigned long long)len;
+        int j = q == p[0] ? 0 : (q == p[1] ? 1 : -1);
+        if (j < 0) { j = (int)next; next ^= 1u; flush_one(j); p[j] = q; }
+        else if (by[j] + len < by[j] || pk[j] == 0xffffffffu) { flush_one(j); p[j] = q; }
+        pk[j] += 1u; by[j] += len;
     }
 };
 
@@ -579,13 +582,24 @@ __device__ __forceinline__ uint32_t pol_home(uint32_t identity, uint32_t dport, 
 // policy keys, proxy ports, CIDR tries or L4 lists, only the entry counters —
 // which stay per packet.  Consecutive packets of a lane's flow group mostly ask
 // the same question, so the answer (and the entry to count) is kept.
-struct PolMemo {
-    uint32_t sl = 0, id = 0, pk = 0, sip = 0;
+struct PolDecision {          // 24 B (kept in LDS with the rest of the lane state)
+    uint32_t id = 0, sip = 0, pk = 0;
+    uint32_t slab = 0;       // program slot + 1 | algorithmic bytes of the decision << 16
+    uint32_t f = ~0u;        // policy slot counted by the decision, ~0u: none
     int verdict = 0;
-    int64_t f = -1;          // policy slot counted by the decision, -1: none
-    uint32_t ab = 0;         // algorithmic bytes the decision touches
+};
+struct PolMemo {             // two decisions (a group's flows use a couple of ports)
+    PolDecision d[2];
+    uint32_t next = 0;
+    __device__ __forceinline__ int find(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+            if ((d[j].slab & 0xffffu) == s && d[j].id == identity && d[j].pk == k && (identity >= 256 || d[j].sip == a))
+                return j;
+        return -1;
+    }
     __device__ __forceinline__ bool hit(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
-        return sl == s && id == identity && pk == k && (identity >= 256 || sip == a);
+        return find(s, identity, k, a) >= 0;
     }
 };
 
@@ -658,16 +672,24 @@ __device__ __forceinline__ int policy_ingress(const IngCtx &X, const Ep &ep, Pol
                                               const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo &m) {
     const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
     const bool memo_ok = !v6 || identity >= 256;
-    if (memo_ok && m.hit(ep.sl, identity, pk, sip)) {
-        ab += m.ab;
-        if (m.f >= 0) policy_count(ep.pdesc(), m.f, len, acc);
-        return m.verdict;
+    const int j = memo_ok ? m.find(ep.sl, identity, pk, sip) : -1;
+    if (j >= 0) {
+        const PolDecision &d = m.d[j];
+        ab += d.slab >> 16;
+        if (d.f != ~0u) policy_count(ep.pdesc(), (int64_t)d.f, len, acc);
+        return d.verdict;
     }
     uint32_t ab0 = ab;
     int64_t fc;
     int v = policy_lookup(X, ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
     if (fc >= 0) policy_count(ep.pdesc(), fc, len, acc);
-    if (memo_ok) { m.sl = ep.sl; m.id = identity; m.pk = pk; m.sip = sip; m.verdict = v; m.f = fc; m.ab = ab - ab0; }
+    if (memo_ok) {
+        PolDecision &d = m.d[m.next];
+        d.id = identity; d.pk = pk; d.sip = sip; d.verdict = v;
+        d.f = fc >= 0 ? (uint32_t)fc : ~0u;    // policy maps hold < 2^32 slots (max_entries is u32)
+        d.slab = ep.sl | ((ab - ab0) << 16);
+        m.next ^= 1u;
+    }
     return v;
 }
 
