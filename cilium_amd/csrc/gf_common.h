@@ -8,6 +8,11 @@
 //     [ key (ksz B) | state (1 B) | pad | value (vsz B) at voff | pad ]
 //   split layout (key+value > 128 B, e.g. endpoint_info 112 B):
 //     slots: [ key | state | pad ]  (pow2 stride)   vals: vsz B per slot
+//   hot-split layout (CT maps, value codec GF_VCODEC_CT): the first 16 value
+//     bytes (what an ingress hit reads and writes) stay in the slot, the other
+//     32 go to vals, so a CT4 slot is 32 B — one memory sector — and a probe
+//     step of 2 slots is one 64-B request:
+//     slots: [ key | state | pad | hot 16 B at voff ]   vals: 32 B per slot
 //
 // state: 0 empty, 1 full, 2 deleted (tombstone), 3 busy (device insert in
 // flight).  Device inserts only ever claim EMPTY slots; tombstones are reused
@@ -40,6 +45,8 @@ struct gf_htab_desc {
     uint64_t  mask;        // nslots - 1 (0 with slots == nullptr => empty map)
     uint32_t  ksz, vsz, slot_size, voff;
     uint32_t  split, max_entries;
+    uint32_t  vin;         // value bytes inline in the slot (at voff); the rest is in vals
+    uint32_t  sstride;     // bytes per slot in vals (0: no side array)
 };
 
 struct gf_trie_desc {

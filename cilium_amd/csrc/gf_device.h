@@ -185,8 +185,26 @@ __device__ __forceinline__ void store_words(uint8_t *p, const uint32_t *v) {
     }
 }
 
+// Value bytes of slot i held in the slot (all of them for inline maps, the hot
+// 16 B for hot-split CT maps), or the side-array value of a full-split map.
 __device__ __forceinline__ uint8_t *ht_val(const gf_htab_desc &d, uint64_t i) {
-    return d.split ? d.vals + i * d.vsz : d.slots + i * d.slot_size + d.voff;
+    return d.vin ? d.slots + i * d.slot_size + d.voff : d.vals + i * d.vsz;
+}
+// The side-array part of a hot-split value (value bytes vin..vsz).
+__device__ __forceinline__ uint8_t *ht_side(const gf_htab_desc &d, uint64_t i) {
+    return d.vals + i * d.sstride;
+}
+
+// A whole value of VW words into slot i in the map's layout.
+template <int VW>
+__device__ __forceinline__ void store_value(const gf_htab_desc &d, uint64_t i, const uint32_t *vw) {
+    if (!d.sstride) { store_words<VW>(ht_val(d, i), vw); return; }
+    if (d.vin == 16 && VW > 4) {                        // hot-split: 4 words inline, the rest aside
+        store_words<4>(d.slots + i * d.slot_size + d.voff, vw);
+        store_words<VW - 4>(ht_side(d, i), vw + 4);
+        return;
+    }
+    store_words<VW>(d.vals + i * d.vsz, vw);            // full split
 }
 
 // Insert-or-replace (map_update_elem BPF_ANY) for keys owned by the calling
@@ -204,7 +222,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
     uint32_t h = key_hash<KSZ, MODE>(kw);
     int64_t f = known_absent ? -1 : ht_find<KSZ, U>(d, kw, h);
     if (f >= 0) {
-        store_words<VW>(ht_val(d, (uint64_t)f), vw);
+        store_value<VW>(d, (uint64_t)f, vw);
         return f;
     }
     if (strict) {
@@ -218,7 +236,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         uint32_t *ks = reinterpret_cast<uint32_t *>(s);
 #pragma unroll
         for (int k = 0; k < SW; k++) ks[k] = kw[k];
-        store_words<VW>(ht_val(d, i), vw);
+        store_value<VW>(d, i, vw);
         __atomic_store_n(reinterpret_cast<uint32_t *>(s + 4 * SW), keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)),
                          __ATOMIC_RELAXED);
         if (!strict) (*added)++;

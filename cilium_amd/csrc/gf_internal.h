@@ -35,13 +35,17 @@ struct LpmKeyLess {
 struct HTab {
     uint32_t ksz = 0, vsz = 0, slot_size = 0, voff = 0, split = 0, mode = GF_HASH_PLAIN;
     uint32_t codec = GF_VCODEC_IDENT;   // value layout in the slots (gf_common.h)
+    uint32_t hot_split = 0;             // 1: hot-split layout (CT maps, gf_common.h)
+    uint32_t vin = 0, sstride = 0;      // inline value bytes / side-array bytes per slot
     uint64_t nslots = 0;
     std::vector<uint8_t> slots, vals;
     uint64_t count = 0, tombs = 0;
     void init(uint32_t k, uint32_t v, uint64_t n);
     uint32_t hash(const uint8_t *key) const;
     int64_t find(const uint8_t *key) const;
-    uint8_t *val(uint64_t i) { return split ? &vals[i * vsz] : &slots[i * slot_size + voff]; }
+    void relayout();                    // slot_size/voff/split/vin/sstride from ksz, vsz, hot_split
+    void get_val(uint64_t i, uint8_t *out) const;
+    void put_val(uint64_t i, const uint8_t *in);
     const uint8_t *key(uint64_t i) const { return &slots[i * slot_size]; }
     uint8_t state(uint64_t i) const { return slots[i * slot_size + ksz]; }
     void set_state(uint64_t i, uint8_t s) { slots[i * slot_size + ksz] = s; }

@@ -362,11 +362,11 @@ struct IngCtx {
 
 struct CtState { uint32_t rev_nat, loopback; };
 
-// Slots per 128-B line of the fixed map layouts (gf_htab_layout): CT4 entry
-// 14+48 B -> 64-B slots, CT6 40+48 B -> 128-B slots, policy 8+24 B -> 64-B slots.
-// Only the number of headers fetched together depends on these; results do not.
+// Slot headers fetched per probe step.  CT maps use the hot-split layout
+// (gf_common.h): CT4 slots are 32 B (2 per step = one 64-B request), CT6 64 B;
+// policy 8+24 B -> 64-B slots.  Results do not depend on these.
 #ifndef GF_CT4_U
-#define GF_CT4_U 1
+#define GF_CT4_U 2
 #endif
 #define GF_CT6_U 1
 #ifndef GF_POL_U
@@ -394,7 +394,7 @@ struct Ep {
     __device__ __forceinline__ gf_htab_desc pdesc() const {
         gf_htab_desc d{};
         d.slots = pol; d.mask = pol_mask; d.ksz = 8; d.vsz = 24;
-        d.slot_size = GF_POL_SLOT; d.voff = GF_POL_VOFF;
+        d.slot_size = GF_POL_SLOT; d.voff = GF_POL_VOFF; d.vin = 24;
         return d;
     }
 };
@@ -427,7 +427,7 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     st.loopback = (fl >> 3) & 1u;
     if (acct) {                                         // rx_packets += 1, rx_bytes += len (exclusive lane)
         uint32_t pk = hot.z + 1u, by = hot.w + len;
-        uint32_t *hi = reinterpret_cast<uint32_t *>(e + 16);
+        uint32_t *hi = reinterpret_cast<uint32_t *>(d.sstride ? ht_side(d, (uint64_t)f) : e + 16);
         if (pk == 0u) hi[0] += 1u;
         if (by < hot.w) hi[1] += 1u;
         hot.z = pk; hot.w = by;
@@ -515,7 +515,7 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
 #pragma unroll
     for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
     if (same) {                                         // BPF_ANY over the entry this lane wrote
-        store_words<12>(ht_val(d, (uint64_t)rc.slot), v);
+        store_value<12>(d, (uint64_t)rc.slot, v);
         return 0;
     }
     int64_t s = ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added);

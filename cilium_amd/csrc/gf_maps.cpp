@@ -49,13 +49,37 @@ int DevBuf::ensure(size_t n) {
 }
 
 // ------------------------------------------------------------------ HTab
+void HTab::relayout() {
+    if (hot_split) {
+        voff = (ksz + 1 + 15) / 16 * 16;
+        vin = 16;
+        slot_size = std::max<uint32_t>(16, gf_pow2ceil32(voff + vin));
+        split = 1;
+        sstride = vsz - vin;
+        return;
+    }
+    gf_htab_layout(ksz, vsz, &slot_size, &voff, &split);
+    vin = split ? 0 : vsz;
+    sstride = split ? vsz : 0;
+}
+
 void HTab::init(uint32_t k, uint32_t v, uint64_t n) {
     ksz = k; vsz = v;
-    gf_htab_layout(k, v, &slot_size, &voff, &split);
+    relayout();
     nslots = n;
     slots.assign(nslots * slot_size, 0);
-    if (split) vals.assign(nslots * vsz, 0); else vals.clear();
+    if (sstride) vals.assign(nslots * sstride, 0); else vals.clear();
     count = 0; tombs = 0;
+}
+
+void HTab::get_val(uint64_t i, uint8_t *out) const {
+    if (vin) memcpy(out, &slots[i * slot_size + voff], vin);
+    if (vin < vsz) memcpy(out + vin, &vals[i * sstride], vsz - vin);
+}
+
+void HTab::put_val(uint64_t i, const uint8_t *in) {
+    if (vin) memcpy(&slots[i * slot_size + voff], in, vin);
+    if (vin < vsz) memcpy(&vals[i * sstride], in + vin, vsz - vin);
 }
 
 uint32_t HTab::hash(const uint8_t *key) const {
@@ -86,7 +110,7 @@ int64_t HTab::insert_new(const uint8_t *key, const uint8_t *value) {
             memset(s, 0, slot_size);
             memcpy(s, key, ksz);
             s[ksz] = GF_SLOT_FULL;
-            memcpy(val(i), value, vsz);
+            put_val(i, value);
             count++;
             return (int64_t)i;
         }
@@ -101,17 +125,17 @@ void HTab::erase(uint64_t i) {
 }
 
 void HTab::rehash(uint64_t n) {
-    if (slots.empty()) { nslots = n; count = 0; tombs = 0; return; }   // not materialised: stays all-empty
-    std::vector<uint8_t> os, ov;
-    os.swap(slots); ov.swap(vals);
-    uint64_t on = nslots;
-    uint32_t oss = slot_size, md = mode;
+    if (slots.empty()) { relayout(); nslots = n; count = 0; tombs = 0; return; }   // not materialised: all-empty
+    HTab old;
+    old.ksz = ksz; old.vsz = vsz; old.slot_size = slot_size; old.voff = voff; old.vin = vin;
+    old.sstride = sstride; old.nslots = nslots;
+    old.slots.swap(slots); old.vals.swap(vals);
     init(ksz, vsz, n);
-    mode = md;
-    for (uint64_t i = 0; i < on; i++) {
-        if (os[i * oss + ksz] != GF_SLOT_FULL) continue;
-        const uint8_t *v = split ? &ov[i * vsz] : &os[i * oss + voff];
-        insert_new(&os[i * oss], v);
+    std::vector<uint8_t> v(vsz);
+    for (uint64_t i = 0; i < old.nslots; i++) {
+        if (old.state(i) != GF_SLOT_FULL) continue;
+        old.get_val(i, v.data());
+        insert_new(old.key(i), v.data());
     }
 }
 
@@ -147,7 +171,7 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
 static void materialize(HTab &h) {
     if (h.slots.empty() && h.nslots) {
         h.slots.assign(h.nslots * h.slot_size, 0);
-        if (h.split) h.vals.assign(h.nslots * h.vsz, 0);
+        if (h.sstride) h.vals.assign(h.nslots * h.sstride, 0);
     }
 }
 
@@ -155,14 +179,17 @@ void Map::set_value_codec(uint32_t c) {
     if (is_lpm() || ht.codec == c) return;
     if (c == GF_VCODEC_CT && vsz != GF_CT_VSZ) return;
     pull();
-    uint8_t tmp[GF_CT_VSZ];
+    uint8_t v[GF_CT_VSZ], tmp[GF_CT_VSZ];
     for (uint64_t i = 0; i < (ht.slots.empty() ? 0 : ht.nslots); i++) {
         if (ht.state(i) != GF_SLOT_FULL) continue;
-        uint8_t *v = ht.val(i);
+        ht.get_val(i, v);
         if (ht.codec == GF_VCODEC_CT) { gf_ct_decode(v, tmp); memcpy(v, tmp, vsz); }
         if (c == GF_VCODEC_CT) { gf_ct_encode(v, tmp); memcpy(v, tmp, vsz); }
+        ht.put_val(i, v);
     }
     ht.codec = c;
+    uint32_t hs = c == GF_VCODEC_CT ? 1u : 0u;
+    if (hs != ht.hot_split) { ht.hot_split = hs; ht.rehash(ht.nslots); }
     dev_valid = false;
 }
 
@@ -188,7 +215,7 @@ int Map::pull() {
     materialize(ht);
     if (hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize")) return -EIO;
     if (d_slots.p && hip_ok(hipMemcpy(ht.slots.data(), d_slots.p, ht.slots.size(), hipMemcpyDeviceToHost), "pull slots")) return -EIO;
-    if (ht.split && d_vals.p && hip_ok(hipMemcpy(ht.vals.data(), d_vals.p, ht.vals.size(), hipMemcpyDeviceToHost), "pull vals")) return -EIO;
+    if (ht.sstride && d_vals.p && hip_ok(hipMemcpy(ht.vals.data(), d_vals.p, ht.vals.size(), hipMemcpyDeviceToHost), "pull vals")) return -EIO;
     // recount (device inserts/deletes)
     uint64_t c = 0, t = 0;
     for (uint64_t i = 0; i < ht.nslots; i++) {
@@ -218,14 +245,14 @@ int Map::push(hipStream_t s) {
     if (dev_valid) return 0;
     int r;
     if ((r = d_slots.ensure(ht.nslots * ht.slot_size))) return r;
-    if (ht.split && (r = d_vals.ensure(ht.nslots * ht.vsz))) return r;
+    if (ht.sstride && (r = d_vals.ensure(ht.nslots * ht.sstride))) return r;
     if ((r = d_count.ensure(8))) return r;
     if (ht.slots.empty()) {
         if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
-        if (ht.split && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
+        if (ht.sstride && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
     } else {
         if (hip_ok(hipMemcpyAsync(d_slots.p, ht.slots.data(), ht.slots.size(), hipMemcpyHostToDevice, s), "push slots")) return -EIO;
-        if (ht.split && hip_ok(hipMemcpyAsync(d_vals.p, ht.vals.data(), ht.vals.size(), hipMemcpyHostToDevice, s), "push vals")) return -EIO;
+        if (ht.sstride && hip_ok(hipMemcpyAsync(d_vals.p, ht.vals.data(), ht.vals.size(), hipMemcpyHostToDevice, s), "push vals")) return -EIO;
     }
     uint32_t cnt[2] = {(uint32_t)ht.count, 0};
     if (hip_ok(hipMemcpyAsync(d_count.p, cnt, 8, hipMemcpyHostToDevice, s), "push count")) return -EIO;
@@ -242,6 +269,7 @@ gf_htab_desc Map::hdesc() {
     d.mask = ht.nslots ? ht.nslots - 1 : 0;
     d.ksz = ksz; d.vsz = vsz; d.slot_size = ht.slot_size; d.voff = ht.voff;
     d.split = ht.split; d.max_entries = max_entries;
+    d.vin = ht.vin; d.sstride = ht.sstride;
     return d;
 }
 
@@ -282,7 +310,7 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
     int64_t i = ht.find(key);
     if (i >= 0) {
         if (fl == GF_NOEXIST) return -EEXIST;
-        memcpy(ht.val((uint64_t)i), value, vsz);
+        ht.put_val((uint64_t)i, value);
         dev_valid = false;
         return 0;
     }
@@ -316,8 +344,8 @@ int Map::lookup(const uint8_t *key, uint8_t *value) {
     if (ht.slots.empty()) return -ENOENT;
     int64_t i = ht.find(key);
     if (i < 0) return -ENOENT;
-    if (ht.codec == GF_VCODEC_CT) gf_ct_decode(ht.val((uint64_t)i), value);
-    else memcpy(value, ht.val((uint64_t)i), vsz);
+    if (ht.codec == GF_VCODEC_CT) { uint8_t v[GF_CT_VSZ]; ht.get_val((uint64_t)i, v); gf_ct_decode(v, value); }
+    else ht.get_val((uint64_t)i, value);
     return 0;
 }
 
