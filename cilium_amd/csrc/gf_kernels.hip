@@ -360,7 +360,7 @@ struct IngCtx {
     uint32_t strict;   // bit0: CT inserts check max_entries with atomics
 };
 
-struct CtState { uint32_t rev_nat, loopback; };
+struct CtState { uint32_t rev_nat, loopback, carry; };
 
 // Slot headers fetched per probe step.  CT maps use the hot-split layout
 // (gf_common.h): CT4 slots are 32 B (2 per step = one 64-B request), CT6 64 B;
@@ -382,6 +382,7 @@ struct Ep {
     uint32_t flags = 0;
     uint8_t *pol = nullptr;          // policy map slots / mask (policy maps hold < 2^32 slots)
     uint32_t pol_mask = 0;
+    uint32_t next = 0;               // round-robin bits: bit0 counter sums (PolAcc), bit1 decisions (PolMemo)
     __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
         if (s == sl) return;
         sl = s;
@@ -406,7 +407,8 @@ struct Ep {
 template <int TW>
 struct RelCache {
     uint32_t k[TW];
-    int64_t slot = -1;
+    uint32_t slot = ~0u;     // ~0u: none (tables of >= 2^32 slots are not cached)
+    uint32_t sec = 0;        // src_sec_id of the cold value part this lane wrote there
 };
 
 // __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part.  CT
@@ -428,8 +430,8 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     if (acct) {                                         // rx_packets += 1, rx_bytes += len (exclusive lane)
         uint32_t pk = hot.z + 1u, by = hot.w + len;
         uint32_t *hi = reinterpret_cast<uint32_t *>(d.sstride ? ht_side(d, (uint64_t)f) : e + 16);
-        if (pk == 0u) hi[0] += 1u;
-        if (by < hot.w) hi[1] += 1u;
+        if (pk == 0u) { hi[0] += 1u; st.carry = 1; }
+        if (by < hot.w) { hi[1] += 1u; st.carry = 1; }
         hot.z = pk; hot.w = by;
     }
     if (action == ACT_CREATE) {
@@ -511,18 +513,23 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     it[NHW - 1] = 0;                                    // sport = dport = 0
     it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
     v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
-    bool same = rc.slot >= 0;
+    bool same = rc.slot != ~0u;
 #pragma unroll
     for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
     if (same) {                                         // BPF_ANY over the entry this lane wrote
-        store_value<12>(d, (uint64_t)rc.slot, v);
+        if (d.vin == 16 && rc.sec == src_sec)           // cold part (rx hi, tx, src_sec_id) unchanged
+            store_words<4>(d.slots + (uint64_t)rc.slot * d.slot_size + d.voff, v);
+        else
+            store_value<12>(d, (uint64_t)rc.slot, v);
+        rc.sec = src_sec;
         return 0;
     }
     int64_t s = ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added);
     if (s < 0) return D_CT_CREATE_FAILED;
 #pragma unroll
     for (int k = 0; k < TW; k++) rc.k[k] = it[k];
-    rc.slot = s;
+    rc.slot = (uint64_t)s < 0xffffffffull ? (uint32_t)s : ~0u;
+    rc.sec = src_sec;
     return 0;
 }
 
@@ -547,24 +554,32 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // with one pair of atomics when the entry changes and at the end — the same
 // totals with a fraction of the memory-side atomics.
 struct PolAcc {
-    unsigned long long *p[2] = {nullptr, nullptr};
-    uint32_t pk[2] = {0, 0}, by[2] = {0, 0};   // flushed before a 32-bit sum could wrap
-    uint32_t next = 0;
-    __device__ __forceinline__ void flush_one(int j) {
-        if (p[j]) { atomicAdd(&p[j][0], (unsigned long long)pk[j]); atomicAdd(&p[j][1], (unsigned long long)by[j]); }
-        p[j] = nullptr; pk[j] = 0; by[j] = 0;
+    uint32_t f[2] = {0, 0};                  // policy slots of the open sums
+    uint16_t sl[2] = {0, 0};                 // their program slot + 1 (0: sum not open)
+    uint32_t pk[2] = {0, 0}, by[2] = {0, 0}; // flushed before a 32-bit sum could wrap
+    __device__ __forceinline__ void flush_one(const IngCtx &X, int j) {
+        if (sl[j]) {
+            uint8_t *slots = X.cfgs[sl[j] - 1].policy.slots;
+            unsigned long long *c = reinterpret_cast<unsigned long long *>(
+                slots + (uint64_t)f[j] * GF_POL_SLOT + GF_POL_VOFF + 8);
+            atomicAdd(&c[0], (unsigned long long)pk[j]);
+            atomicAdd(&c[1], (unsigned long long)by[j]);
+        }
+        sl[j] = 0; pk[j] = 0; by[j] = 0;
     }
-    __device__ __forceinline__ void flush() { flush_one(0); flush_one(1); }
-    __device__ __forceinline__ void add(unsigned long long *q, uint32_t len) {
-        int j = q == p[0] ? 0 : (q == p[1] ? 1 : -1);
-        if (j < 0) { j = (int)next; next ^= 1u; flush_one(j); p[j] = q; }
-        else if (by[j] + len < by[j] || pk[j] == 0xffffffffu) { flush_one(j); p[j] = q; }
+    __device__ __forceinline__ void flush(const IngCtx &X) { flush_one(X, 0); flush_one(X, 1); }
+    __device__ __forceinline__ void add(const IngCtx &X, uint32_t s, uint32_t slot, uint32_t len, uint32_t &next) {
+        int j = (sl[0] == s && f[0] == slot) ? 0 : ((sl[1] == s && f[1] == slot) ? 1 : -1);
+        if (j < 0) { j = (int)(next & 1u); next ^= 1u; flush_one(X, j); sl[j] = (uint16_t)s; f[j] = slot; }
+        else if (by[j] + len < by[j] || pk[j] == 0xffffffffu) { flush_one(X, j); sl[j] = (uint16_t)s; f[j] = slot; }
         pk[j] += 1u; by[j] += len;
     }
 };
 
-__device__ __forceinline__ void policy_count(const gf_htab_desc &d, int64_t f, uint32_t len, PolAcc &acc) {
-    acc.add(reinterpret_cast<unsigned long long *>(ht_val(d, (uint64_t)f) + 8), len);
+// policy_entry packets/bytes of slot f of the program's policy map (policy maps
+// hold < 2^32 slots: max_entries is u32 and the load is <= 1/2)
+__device__ __forceinline__ void policy_count(const IngCtx &X, Ep &ep, int64_t f, uint32_t len, PolAcc &acc) {
+    acc.add(X, ep.sl, (uint32_t)f, len, ep.next);
 }
 
 // Policy slots are probed with the first 16 B of the value (proxy_port) so an
@@ -590,7 +605,6 @@ struct PolDecision {          // 24 B (kept in LDS with the rest of the lane sta
 };
 struct PolMemo {             // two decisions (a group's flows use a couple of ports)
     PolDecision d[2];
-    uint32_t next = 0;
     __device__ __forceinline__ int find(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
 #pragma unroll
         for (int j = 0; j < 2; j++)
@@ -667,7 +681,7 @@ deny:
 
 // policy_can_access_ingress with the counter update (policy.h:67-92), through the
 // lane's decision memo (IPv4, or any non-reserved identity).
-__device__ __forceinline__ int policy_ingress(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
+__device__ __forceinline__ int policy_ingress(const IngCtx &X, Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
                                               uint32_t dport, uint32_t proto, uint32_t len, bool v6,
                                               const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo &m) {
     const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
@@ -676,19 +690,19 @@ __device__ __forceinline__ int policy_ingress(const IngCtx &X, const Ep &ep, Pol
     if (j >= 0) {
         const PolDecision &d = m.d[j];
         ab += d.slab >> 16;
-        if (d.f != ~0u) policy_count(ep.pdesc(), (int64_t)d.f, len, acc);
+        if (d.f != ~0u) policy_count(X, ep, (int64_t)d.f, len, acc);
         return d.verdict;
     }
     uint32_t ab0 = ab;
     int64_t fc;
     int v = policy_lookup(X, ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
-    if (fc >= 0) policy_count(ep.pdesc(), fc, len, acc);
+    if (fc >= 0) policy_count(X, ep, fc, len, acc);
     if (memo_ok) {
-        PolDecision &d = m.d[m.next];
+        PolDecision &d = m.d[(ep.next >> 1) & 1u];
         d.id = identity; d.pk = pk; d.sip = sip; d.verdict = v;
         d.f = fc >= 0 ? (uint32_t)fc : ~0u;    // policy maps hold < 2^32 slots (max_entries is u32)
         d.slab = ep.sl | ((ab - ab0) << 16);
-        m.next ^= 1u;
+        ep.next ^= 2u;
     }
     return v;
 }
@@ -760,7 +774,7 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
-__device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &fwd, uint8_t &ofl, uint16_t &proxy,
+__device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, int &fwd, uint8_t &ofl, uint16_t &proxy,
                            uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo &pm) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
@@ -783,10 +797,11 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
                      !pm.hit(ep.sl, r.src_identity, (t[2] >> 16) | (nh << 16), r.saddr);
     if (pre) pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
-    CtState st{0, 0};
+    CtState st{0, 0, 0};
     ProbeRes pr;
     int ret = ct_lookup<14, 4, GF_CT4_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
+    if (st.carry) rc.slot = ~0u;                         // a counter carry touched a cold value part
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
         const gf_htab_desc rn = ep.cfg(X)->revnat4;
         uint32_t kw[1] = {st.rev_nat};
@@ -806,7 +821,7 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
         if (ret == CT_ESTABLISHED) {
             ab += 14;
             ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added);
-            rc.slot = -1;
+            rc.slot = ~0u;
         }
         return D_POLICY;
     }
@@ -827,7 +842,7 @@ __device__ int ipv4_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, int &
 }
 
 // ipv6_policy, bpf/bpf_lxc.c:745-862
-__device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
+__device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
                            uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc,
                            RelCache<10> &rc, PolMemo &pm) {
     uint32_t len = r.len;
@@ -855,10 +870,11 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
                      !(r.src_identity >= 256 && pm.hit(ep.sl, r.src_identity, (t[8] >> 16) | (nh << 16), 0u));
     if (pre) pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
-    CtState st{0, 0};
+    CtState st{0, 0, 0};
     ProbeRes pr;
     int ret = ct_lookup<40, 10, GF_CT6_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
+    if (st.carry) rc.slot = ~0u;
     if (st.rev_nat) {
         const gf_htab_desc rn = ep.cfg(X)->revnat6;
         uint32_t kw[1] = {st.rev_nat};
@@ -875,7 +891,7 @@ __device__ int ipv6_policy(const IngCtx &X, const Ep &ep, const gf_rec &r, uint3
         if (ret == CT_ESTABLISHED) {
             ab += 40;
             ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added);
-            rc.slot = -1;
+            rc.slot = ~0u;
         }
         return D_POLICY;
     }
@@ -1024,8 +1040,8 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t
 #define GF_SCHED_WORDS (6 * (GF_LCAP + 1) + 5)
 
 template <int FAM>
-__global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint32_t *order,
-                                                      const uint32_t *off, const uint32_t *cnt, const uint32_t *perm,
+__global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
+                                                      const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
                                                       unsigned long long *stats) {
     __shared__ uint32_t sl[272];
@@ -1047,11 +1063,12 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         if (base >= nb) break;
         uint32_t t = base + lane;
         if (t >= nb) continue;
-        uint32_t q = order[t], b = off[q], c = cnt[q];
+        const uint2 oc = order[t];
+        const uint32_t b = oc.x, c = oc.y;
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = rec[i];
-        ln.rc.slot = -1;                                // a new bucket: new flow groups
+        ln.rc.slot = ~0u;                                // a new bucket: new flow groups
         for (uint32_t k = 0; k < c; k++) {
             // the next record and the index after it are in flight while packet k runs
             uint32_t in2 = 0;
@@ -1068,7 +1085,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 #endif
         }
     }
-    ln.acc.flush();
+    ln.acc.flush(X);
     flush_added(X, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }
@@ -1127,10 +1144,11 @@ __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
     }
 }
 
-// order[] = non-empty buckets, family 0 then 1, each by count descending (ties in
-// any order): block-local counts per bin, one global reservation per (block, bin).
+// order[] = {first sorted position, packet count} of the non-empty buckets,
+// family 0 then 1, each by count descending (ties in any order): block-local
+// counts per bin, one global reservation per (block, bin).
 __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, const uint32_t *off, const uint32_t *skeys,
-                                                        uint32_t *sched, uint32_t *order) {
+                                                        uint32_t *sched, uint2 *order) {
     __shared__ uint32_t h[2 * (GF_LCAP + 1)];
     for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
@@ -1148,7 +1166,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
-        if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = q;
+        if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = make_uint2(off[q], c);
     }
 }
 
@@ -1511,7 +1529,7 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
         (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
-        (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 4)) ||
+        (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 8)) ||
         (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
     uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
@@ -1560,7 +1578,7 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
                            (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched);
         hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
         hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched, (uint32_t *)w.order.p);
+                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched, (uint2 *)w.order.p);
     }
     if ((r = hip_ok(hipGetLastError(), "k_bucket_sched"))) return r;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
@@ -1581,14 +1599,14 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
         if (grid > need) grid = need;
         {
             ProfScope ps("k_ing_groups", s);
-            hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint32_t *)w.order.p,
-                               (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p,
+            hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
+                               (const uint32_t *)w.perm.p,
                                (const gf_rec *)w.rec.p, out, cnt4, sink);
         }
         if (pkts->saddr6) {    // IPv6 packets reach conntrack only with v6 columns
             ProfScope ps("k_ing_groups6", s);
-            hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint32_t *)w.order.p,
-                               (const uint32_t *)w.off.p, (const uint32_t *)w.cnt.p, (const uint32_t *)w.perm.p,
+            hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
+                               (const uint32_t *)w.perm.p,
                                (const gf_rec *)w.rec.p, out, cnt6, sink);
         }
     }

@@ -103,3 +103,42 @@ def test_ingress_large_batch_properties():
     o = outs[-1]
     assert np.all(np.isin(o["action"], [0, 2, 7]))
     assert np.all((o["reason"] == 0) == (o["action"] != 2))
+
+
+def test_ct_counter_carry_and_codec():
+    """CT values live on the device in the GF_VCODEC_CT hot-split layout with the
+    rx counters' low halves next to the key: entries whose rx_packets/rx_bytes sit
+    at a 32-bit boundary must carry into the high halves exactly like the
+    reference's u64 adds (conntrack.h:99-108), and lookups through the map API
+    must decode to the reference ct_entry layout."""
+    import struct
+    from cilium_amd.synth import ip4, raw16, TCP
+    E, R, NOW = ip4("10.1.0.5"), ip4("100.64.1.9"), 7000
+    htonl = lambda x: struct.unpack("<I", struct.pack(">I", x))[0]
+    sc = synth.Scenario("carry", now=NOW)
+    # forward tuples (reversed at ingress: daddr=R, saddr=E... as ct_lookup4 leaves them), TUPLE_F_IN
+    keys, vals = [], []
+    for j, (rx, rxb) in enumerate([(0xffffffff, 100), (5, 0xfffffff0), (0xffffffff, 0xffffffff), (2**40 + 7, 2**33)]):
+        k = struct.pack("<IIHHBB", htonl(R), htonl(E), raw16(8080 + j), raw16(40000), TCP, 1)
+        v = struct.pack("<QQQQIHHHHI", rx, rxb, 11, 22, NOW + 100, 16, 0, 0, 0, 300)
+        keys.append(np.frombuffer(k, np.uint8)); vals.append(np.frombuffer(v, np.uint8))
+    sc.add_map(synth.MapSpec("ct4", synth.LRU_HASH, 14, 48, 1000, 0, np.stack(keys), np.stack(vals)))
+    sc.add_map(synth.MapSpec("pol", synth.HASH, 8, 24, 16384, 0, synth.policy_keys([300], [0], [0]),
+                             synth.policy_vals([0])))
+    sc.lxc.append({"lxc_id": 7, "seclabel": 500, "policy": "pol", "ct4": "ct4", "ct6": None, "cidr4": None,
+                   "cidr6": None, "revnat4": None, "revnat6": None, "flags": synth.LXC_PRODUCTION, "l4": []})
+    n = 4
+    f, l = synth.frames_v4(n, 64, [R] * n, [E] * n, [TCP] * n, [40000] * n, [8080 + j for j in range(n)],
+                           [synth.F_ACK] * n, [8] * n, payload=10)
+    l = np.array([40, 0x20, 0x30, 60], np.uint32) + 54
+    pk = synth.Packets(f, l, np.full(n, 300, np.uint32), np.full(n, 42, np.uint32), np.full(n, 7, np.uint16),
+                       np.zeros(n, np.uint8))
+    sc.batches.append(pk)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    io = dp.ingress(DeviceBatch(pk), NOW)
+    torch.cuda.synchronize()
+    _cmp_struct(to_numpy(io, ING_OUT), ref.ingress(pk, NOW), "ingress")
+    got, want = dp.dump_map("ct4"), ref.dump("ct4")
+    assert got == want
+    rx = sorted(struct.unpack("<QQ", v[:16]) for v in got.values())
+    assert (0x100000000, 100 + 94) in rx and (6, 0xfffffff0 + 0x20 + 54) in rx
