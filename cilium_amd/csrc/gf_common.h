@@ -13,6 +13,10 @@
 //     32 go to vals, so a CT4 slot is 32 B — one memory sector — and a probe
 //     step of 2 slots is one 64-B request:
 //     slots: [ key | state | pad | hot 16 B at voff ]   vals: 32 B per slot
+//   policy layout (policy maps, codec GF_VCODEC_POL): 16-B slots
+//     [ key 8 | state | pad | proxy_port 2 at voff 10 | pad 4 ], so one 64-B
+//     request reads the 4 slots an identity's L3/L4 keys cluster in;
+//     vals: 24 B per slot (packets, bytes, the reference's pad bytes)
 //
 // state: 0 empty, 1 full, 2 deleted (tombstone), 3 busy (device insert in
 // flight).  Device inserts only ever claim EMPTY slots; tombstones are reused
@@ -127,7 +131,22 @@ GF_HD uint64_t gf_home_slot(uint32_t h, uint64_t mask, uint32_t slot_size) {
 //            +24 tx_packets  +32 tx_bytes  +40 unused, pad  +44 src_sec_id
 //          (reference offsets: rx_packets 0, rx_bytes 8, tx_packets 16,
 //          tx_bytes 24, lifetime 32, flags 36, rev_nat_index 38, 40.., 44).
-enum { GF_VCODEC_IDENT = 0, GF_VCODEC_CT = 1 };
+//  POL   : struct policy_entry (common.h:192-197: proxy_port, pad[3], packets,
+//          bytes) reordered as proxy_port | packets | bytes | pad: proxy_port
+//          stays in a 16-B slot with the key, the counters start the side
+//          array entry 8-aligned for the device's 64-bit atomics.
+enum { GF_VCODEC_IDENT = 0, GF_VCODEC_CT = 1, GF_VCODEC_POL = 2 };
+#define GF_POL_VSZ 24u
+GF_HD void gf_pol_encode(const uint8_t *ext, uint8_t *in) {
+    __builtin_memcpy(in, ext, 2);
+    __builtin_memcpy(in + 2, ext + 8, 16);
+    __builtin_memcpy(in + 18, ext + 2, 6);
+}
+GF_HD void gf_pol_decode(const uint8_t *in, uint8_t *ext) {
+    __builtin_memcpy(ext, in, 2);
+    __builtin_memcpy(ext + 8, in + 2, 16);
+    __builtin_memcpy(ext + 2, in + 18, 6);
+}
 #define GF_CT_VSZ 48u
 GF_HD void gf_ct_encode(const uint8_t *ext, uint8_t *in) {
     const int map[12] = {8, 9, 0, 2, 1, 3, 4, 5, 6, 7, 10, 11};   // internal word k <- reference word map[k]

@@ -364,23 +364,26 @@ struct CtState { uint32_t rev_nat, loopback, carry; };
 
 // Slot headers fetched per probe step.  CT maps use the hot-split layout
 // (gf_common.h): CT4 slots are 32 B (2 per step = one 64-B request), CT6 64 B;
-// policy 8+24 B -> 64-B slots.  Results do not depend on these.
+// policy maps the 16-B policy layout (4 per step = one 64-B request).
+// Results do not depend on these.
 #ifndef GF_CT4_U
 #define GF_CT4_U 2
 #endif
 #define GF_CT6_U 1
 #ifndef GF_POL_U
-#define GF_POL_U 2
+#define GF_POL_U 4
 #endif
-#define GF_POL_SLOT 64u    // gf_htab_layout(8, 24)
-#define GF_POL_VOFF 16u
+#define GF_POL_SLOT 16u    // policy layout (GF_VCODEC_POL, gf_common.h): key | state | pad | proxy_port
+#define GF_POL_VOFF 10u
+#define GF_POL_SIDE 24u    // side array: packets, bytes, pad
 
 // The endpoint program of the lane's current packet, kept in registers while
 // consecutive packets of the lane's bucket target the same endpoint.
 struct Ep {
     uint32_t sl = 0;                 // program slot + 1 (0: none loaded)
     uint32_t flags = 0;
-    uint8_t *pol = nullptr;          // policy map slots / mask (policy maps hold < 2^32 slots)
+    uint8_t *pol = nullptr;          // policy map slots / side array / mask (< 2^32 slots)
+    uint8_t *pol_side = nullptr;
     uint32_t pol_mask = 0;
     uint32_t next = 0;               // round-robin bits: bit0 counter sums (PolAcc), bit1 decisions (PolMemo)
     __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
@@ -389,13 +392,14 @@ struct Ep {
         const gf_lxc_dev *c = X.cfgs + (s - 1);
         flags = c->flags;
         pol = c->policy.slots;
+        pol_side = c->policy.vals;
         pol_mask = (uint32_t)c->policy.mask;
     }
     __device__ __forceinline__ const gf_lxc_dev *cfg(const IngCtx &X) const { return X.cfgs + (sl - 1); }
     __device__ __forceinline__ gf_htab_desc pdesc() const {
         gf_htab_desc d{};
-        d.slots = pol; d.mask = pol_mask; d.ksz = 8; d.vsz = 24;
-        d.slot_size = GF_POL_SLOT; d.voff = GF_POL_VOFF; d.vin = 24;
+        d.slots = pol; d.vals = pol_side; d.mask = pol_mask; d.ksz = 8; d.vsz = 24;
+        d.slot_size = GF_POL_SLOT; d.voff = GF_POL_VOFF; d.vin = 2; d.split = 1; d.sstride = GF_POL_SIDE;
         return d;
     }
 };
@@ -559,9 +563,8 @@ struct PolAcc {
     uint32_t pk[2] = {0, 0}, by[2] = {0, 0}; // flushed before a 32-bit sum could wrap
     __device__ __forceinline__ void flush_one(const IngCtx &X, int j) {
         if (sl[j]) {
-            uint8_t *slots = X.cfgs[sl[j] - 1].policy.slots;
-            unsigned long long *c = reinterpret_cast<unsigned long long *>(
-                slots + (uint64_t)f[j] * GF_POL_SLOT + GF_POL_VOFF + 8);
+            uint8_t *side = X.cfgs[sl[j] - 1].policy.vals;
+            unsigned long long *c = reinterpret_cast<unsigned long long *>(side + (uint64_t)f[j] * GF_POL_SIDE);
             atomicAdd(&c[0], (unsigned long long)pk[j]);
             atomicAdd(&c[1], (unsigned long long)by[j]);
         }
@@ -582,9 +585,8 @@ __device__ __forceinline__ void policy_count(const IngCtx &X, Ep &ep, int64_t f,
     acc.add(X, ep.sl, (uint32_t)f, len, ep.next);
 }
 
-// Policy slots are probed with the first 16 B of the value (proxy_port) so an
-// L4 hit needs no second load.
-typedef ProbeLine<8, GF_POL_U, 4> PolLine;
+// A policy slot is 16 B with proxy_port inside, so an L4 hit needs no second load.
+typedef ProbeLine<8, GF_POL_U, 0> PolLine;
 
 __device__ __forceinline__ uint32_t pol_home(uint32_t identity, uint32_t dport, uint32_t proto) {
     uint32_t kw[2] = {identity, dport | (proto << 16)};
@@ -634,13 +636,13 @@ __device__ int policy_lookup(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl
         uint32_t k4[2] = {identity, dport | (proto << 16)}, k3[2] = {identity, 0u};
         if (!pl_loaded) pl.load(pd, identity ? pol_home(identity, 0u, 0u) : pol_home(0u, dport, proto));
         if (flags & GF_LXC_F_HAVE_L4_POLICY) {
-            ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k4, k3, pl, identity != 0);
+            ProbeRes r = probe2<8, GF_POL_U, 0>(pd, k4, k3, pl, identity != 0);
             ab += 8;
             if (r.f >= 0 && !r.is_b) {
                 pp = 0xffffffffu;
 #pragma unroll
                 for (int u = 0; u < GF_POL_U; u++)
-                    if (u == r.u) pp = pl.hd[u].w[4] & 0xffffu;
+                    if (u == r.u) pp = pl.hd[u].w[2] >> 16;          // proxy_port at slot byte 10
                 f = r.f;
                 goto proxy;
             }
@@ -650,7 +652,7 @@ __device__ int policy_lookup(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl
             } else f = r.f;
             if (f >= 0) { ab += 40; fc = f; return TC_OK; }
         } else {
-            if (identity) { ProbeRes r = probe2<8, GF_POL_U, 4>(pd, k3, k3, pl, false); f = r.f; }
+            if (identity) { ProbeRes r = probe2<8, GF_POL_U, 0>(pd, k3, k3, pl, false); f = r.f; }
             else f = ht_find<8, GF_POL_U>(pd, k3, key_hash<8, GF_HASH_POLICY>(k3));
             ab += 8;
             if (f >= 0) { ab += 40; fc = f; return TC_OK; }
@@ -1369,7 +1371,7 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
     }
     if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(); }
     if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(); }
-    if (p->policy) p->policy->set_hash_mode(GF_HASH_POLICY);
+    if (p->policy) { p->policy->set_hash_mode(GF_HASH_POLICY); p->policy->set_value_codec(GF_VCODEC_POL); }
     return new_handle(p);
 }
 

@@ -50,6 +50,14 @@ int DevBuf::ensure(size_t n) {
 
 // ------------------------------------------------------------------ HTab
 void HTab::relayout() {
+    if (hot_split == 2) {                       // policy layout (gf_common.h)
+        vin = 2;
+        voff = ksz + 2;
+        slot_size = std::max<uint32_t>(16, gf_pow2ceil32(voff + vin));
+        split = 1;
+        sstride = (vsz - vin + 7) / 8 * 8;
+        return;
+    }
     if (hot_split) {
         voff = (ksz + 1 + 15) / 16 * 16;
         vin = 16;
@@ -175,20 +183,30 @@ static void materialize(HTab &h) {
     }
 }
 
+static void codec_encode(uint32_t c, const uint8_t *ext, uint8_t *in) {
+    if (c == GF_VCODEC_CT) gf_ct_encode(ext, in);
+    else gf_pol_encode(ext, in);
+}
+static void codec_decode(uint32_t c, const uint8_t *in, uint8_t *ext) {
+    if (c == GF_VCODEC_CT) gf_ct_decode(in, ext);
+    else gf_pol_decode(in, ext);
+}
+
 void Map::set_value_codec(uint32_t c) {
     if (is_lpm() || ht.codec == c) return;
     if (c == GF_VCODEC_CT && vsz != GF_CT_VSZ) return;
+    if (c == GF_VCODEC_POL && (vsz != GF_POL_VSZ || ksz != 8)) return;
     pull();
     uint8_t v[GF_CT_VSZ], tmp[GF_CT_VSZ];
     for (uint64_t i = 0; i < (ht.slots.empty() ? 0 : ht.nslots); i++) {
         if (ht.state(i) != GF_SLOT_FULL) continue;
         ht.get_val(i, v);
-        if (ht.codec == GF_VCODEC_CT) { gf_ct_decode(v, tmp); memcpy(v, tmp, vsz); }
-        if (c == GF_VCODEC_CT) { gf_ct_encode(v, tmp); memcpy(v, tmp, vsz); }
+        if (ht.codec != GF_VCODEC_IDENT) { codec_decode(ht.codec, v, tmp); memcpy(v, tmp, vsz); }
+        if (c != GF_VCODEC_IDENT) { codec_encode(c, v, tmp); memcpy(v, tmp, vsz); }
         ht.put_val(i, v);
     }
     ht.codec = c;
-    uint32_t hs = c == GF_VCODEC_CT ? 1u : 0u;
+    uint32_t hs = c == GF_VCODEC_CT ? 1u : (c == GF_VCODEC_POL ? 2u : 0u);
     if (hs != ht.hot_split) { ht.hot_split = hs; ht.rehash(ht.nslots); }
     dev_valid = false;
 }
@@ -306,7 +324,7 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
     int r = pull(); if (r) return r;
     materialize(ht);
     uint8_t enc[GF_CT_VSZ];
-    if (ht.codec == GF_VCODEC_CT) { gf_ct_encode(value, enc); value = enc; }
+    if (ht.codec != GF_VCODEC_IDENT) { codec_encode(ht.codec, value, enc); value = enc; }
     int64_t i = ht.find(key);
     if (i >= 0) {
         if (fl == GF_NOEXIST) return -EEXIST;
@@ -344,7 +362,7 @@ int Map::lookup(const uint8_t *key, uint8_t *value) {
     if (ht.slots.empty()) return -ENOENT;
     int64_t i = ht.find(key);
     if (i < 0) return -ENOENT;
-    if (ht.codec == GF_VCODEC_CT) { uint8_t v[GF_CT_VSZ]; ht.get_val((uint64_t)i, v); gf_ct_decode(v, value); }
+    if (ht.codec != GF_VCODEC_IDENT) { uint8_t v[GF_CT_VSZ]; ht.get_val((uint64_t)i, v); codec_decode(ht.codec, v, value); }
     else ht.get_val((uint64_t)i, value);
     return 0;
 }

@@ -1,12 +1,18 @@
-"""Summarise rocprofv3 --pmc passes (profiles/collect_pmc.sh) into per-step
-numbers for the bench's kernels.  Steps are delimited by k_ing_pack dispatches;
-the last `--steps` windows (steady state) are averaged.
+"""Summarise rocprofv3 --pmc passes over bench.py (tools/profile_round.sh) into
+per-launch numbers for the dominant kernel, k_ing_groups.
 
-FETCH_SIZE / WRITE_SIZE are in KB.  Per the MI355X guide (HBM/rocprofv3
-section) FETCH_SIZE reads exactly 1/2 of the bytes of wide coalesced streaming
-reads on gfx950, so the read side is doubled; other access widths are
-uncalibrated (our probes are 16-64 B random reads), so the raw values are kept
-next to the corrected ones."""
+Steady-state launches only: the bench's first W launches run on a stream that
+is still filling (1/4, 2/4, 3/4 of the flows), so the last `--steps` launches
+of each pass are averaged.
+
+Byte counters (KB in rocprofv3's CSV):
+  * FETCH_SIZE = 64 B per memory-side read request (TCC_EA0_RDREQ x 64 B).
+    The MI355X guide's 2x correction is for wide streaming reads; every read
+    of this kernel is a random 16-32 B access, for which tools/primbench.hip
+    calibrates FETCH_SIZE at exactly one 64-B request per load
+    (profiles/r1_pmc_calibration.json), so FETCH_SIZE is used as is.
+  * WRITE_SIZE = 32 B per write request / atomic (same calibration).
+"""
 import argparse
 import collections
 import csv
@@ -14,64 +20,58 @@ import glob
 import json
 import os
 
+KERNEL = "k_ing_groups"
 
-def load(path):
+
+def per_launch(path, nsteps):
     rows = list(csv.DictReader(open(path)))
-    return rows
-
-
-def group(name):
-    for g in ("k_ing_groups", "k_ing_pack", "k_bucket", "radix_sort", "exclusive_scan", "scan_impl",
-              "k_xdp", "k_lb", "k_parse"):
-        if g in name:
-            return {"radix_sort": "rocprim_sort", "scan_impl": "rocprim_scan", "exclusive_scan": "rocprim_scan"}.get(g, g)
-    return None
-
-
-def per_step(rows, nsteps):
-    packs = sorted(int(r["Dispatch_Id"]) for r in rows if "k_ing_pack" in r["Kernel_Name"])
-    packs = sorted(set(packs))
-    bounds = packs[-nsteps:] + [10 ** 18]
-    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in rows:
-        d = int(r["Dispatch_Id"])
-        if d < bounds[0]:
-            continue
-        g = group(r["Kernel_Name"])
-        if g:
-            acc[r["Counter_Name"]][g] += float(r["Counter_Value"])
-    return {c: {g: v / nsteps for g, v in gs.items()} for c, gs in acc.items()}
+        name = r["Kernel_Name"]
+        if KERNEL in name and "ILi6E" not in name and "<6>" not in name:
+            per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    ds = sorted(per)[-nsteps:]
+    out = collections.defaultdict(float)
+    for d in ds:
+        for c, v in per[d].items():
+            out[c] += v / len(ds)
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--packets", type=int, default=16777216, help="packets per launch (bench config 2)")
     ap.add_argument("--out", required=True)
-    ap.add_argument("--packets-per-step", type=int, default=16777216)
     a = ap.parse_args()
-    res = {}
+    c = {}
     for f in glob.glob(os.path.join(a.dir, "*", "run_counter_collection.csv")):
-        for c, gs in per_step(load(f), a.steps).items():
-            res.setdefault(c, {}).update(gs)
-    stage = ("k_ing_groups",)
-    out = {"per_step_counters": res, "steps_averaged": a.steps, "packets_per_step": a.packets_per_step}
-    fs = sum(res.get("FETCH_SIZE", {}).get(k, 0) for k in stage)
-    ws = sum(res.get("WRITE_SIZE", {}).get(k, 0) for k in stage)
-    hit = sum(res.get("TCC_HIT_sum", {}).get(k, 0) for k in stage)
-    miss = sum(res.get("TCC_MISS_sum", {}).get(k, 0) for k in stage)
-    out["ct_stage"] = {
-        "fetch_bytes_raw": fs * 1024, "fetch_bytes_corrected_x2": fs * 2048, "write_bytes": ws * 1024,
-        "hbm_bytes_per_step": fs * 2048 + ws * 1024,
-        "hbm_bytes_per_packet": (fs * 2048 + ws * 1024) / a.packets_per_step,
-        "tcc_hit_rate": hit / (hit + miss) if hit + miss else None,
-        "ea_rdreq": sum(res.get("TCC_EA0_RDREQ_sum", {}).get(k, 0) for k in stage),
-        "ea_wrreq": sum(res.get("TCC_EA0_WRREQ_sum", {}).get(k, 0) for k in stage),
-        "ea_atomic": sum(res.get("TCC_EA0_ATOMIC_sum", {}).get(k, 0) for k in stage),
+        c.update(per_launch(f, a.steps))
+    n = a.packets
+    fetch = c.get("FETCH_SIZE", 0.0) * 1024
+    write = c.get("WRITE_SIZE", 0.0) * 1024
+    hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+    res = {
+        "kernel": KERNEL,
+        "packets_per_launch": n,
+        "launches_averaged": a.steps,
+        "counters_per_launch": {k: round(v, 1) for k, v in sorted(c.items())},
+        "fetch_bytes_per_launch": fetch,
+        "write_bytes_per_launch": write,
+        "traffic_bytes_per_launch": fetch + write,
+        "traffic_bytes_per_packet": (fetch + write) / n,
+        "ea_requests_per_packet": {
+            "read": c.get("TCC_EA0_RDREQ_sum", 0.0) / n,
+            "write_incl_atomics": c.get("TCC_EA0_WRREQ_sum", 0.0) / n,
+            "atomic": c.get("TCC_EA0_ATOMIC_sum", 0.0) / n,
+        },
+        "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None,
+        "calibration": "FETCH_SIZE used raw: random 16-32 B loads are one 64-B request each "
+                       "(tools/primbench.hip under --pmc; profiles/r1_pmc_calibration.json)",
     }
-    out["k_ing_groups_hbm_bytes_per_launch_per_16M"] = out["ct_stage"]["hbm_bytes_per_step"] * 16777216 / a.packets_per_step
-    json.dump(out, open(a.out, "w"), indent=1)
-    print(json.dumps(out["ct_stage"], indent=1))
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}, indent=1))
 
 
 if __name__ == "__main__":
