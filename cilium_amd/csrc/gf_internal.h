@@ -93,7 +93,7 @@ struct Map : Obj {
     int pull();                       // device -> host if !host_valid
     int push(hipStream_t s);          // host -> device if !dev_valid / trie dirty
     void device_modified() { host_valid = false; }
-    void make_fixed_capacity();
+    void make_fixed_capacity(uint32_t factor = 2);
     void set_hash_mode(uint32_t mode);   // role-specific hashing (gf_key_hash), rehashes
     void set_value_codec(uint32_t codec); // role-specific value layout, converts stored values
     gf_htab_desc hdesc();             // requires push() done

@@ -31,6 +31,9 @@ using namespace gfd;
 #ifndef GF_PREFETCH_REC
 #define GF_PREFETCH_REC 0   // load the lane's next packet record while the current one runs
 #endif
+#ifndef GF_CT_SLOT_FACTOR
+#define GF_CT_SLOT_FACTOR 4 // CT slots per max_entries (a 1/4-loaded table; HBM is plentiful)
+#endif
 #ifndef GF_KEY_BITS
 #define GF_KEY_BITS 32      // bucket key: family bit + (GF_KEY_BITS-1) bits of the group hash
 #endif
@@ -1369,8 +1372,8 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         if (m->ksz != b.k || m->is_lpm() != b.lpm || (!b.lpm && m->vsz != b.v)) return -EINVAL;
         *b.out = m;
     }
-    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(); }
-    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(); }
+    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
+    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
     if (p->policy) { p->policy->set_hash_mode(GF_HASH_POLICY); p->policy->set_value_codec(GF_VCODEC_POL); }
     return new_handle(p);
 }
@@ -1488,7 +1491,10 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (ct6m) cfg_ct6 = ct6m->hdesc();
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
-        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
+        // LRU: no eviction in classify; bounded at 2 x max_entries (and 7/8 of the slots)
+        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH
+                             ? std::min<uint64_t>(m->ht.nslots / 8 * 7, 2ull * m->max_entries)
+                             : m->max_entries;
         if (m->host_valid) m->dev_count_hi = m->ht.count;
         if (m->dev_count_hi + 2ull * pkts->n > limit && !m->host_valid) {
             uint32_t dc = 0;

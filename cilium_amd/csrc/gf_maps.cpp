@@ -219,10 +219,20 @@ void Map::set_hash_mode(uint32_t m) {
     dev_valid = false;
 }
 
-void Map::make_fixed_capacity() {
-    if (is_lpm() || fixed_capacity) return;
+static uint64_t pow2ceil64(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Maps the device inserts into (CT) get a slot array sized from max_entries
+// once, never rehashed by the device.  `factor` slots per entry: 4 for CT maps
+// (HBM is plentiful on MI355X; a 1/4-loaded table resolves almost every probe
+// in the home 64-B request).
+void Map::make_fixed_capacity(uint32_t factor) {
+    if (is_lpm()) return;
     pull();
-    uint64_t want = gf_pow2ceil32(std::max<uint32_t>(64, 2 * max_entries));
+    uint64_t want = pow2ceil64(std::max<uint64_t>(64, (uint64_t)factor * max_entries));
     fixed_capacity = true;
     if (want != ht.nslots) ht.rehash(want);
     dev_valid = false;
