@@ -10,6 +10,78 @@
 
 namespace gfd {
 
+// Table pointers reach the kernels inside descriptor structs (kernel arguments
+// passed by value, or loaded from the program table), where the compiler can no
+// longer see that they point to global memory and would emit flat_* accesses.
+// Flat accesses count against both vmcnt and lgkmcnt, so every wait on one also
+// drains the LDS traffic of the lane state (and vice versa).  All table accesses
+// go through these global-address-space views instead.
+#define GF_GLOBAL __attribute__((address_space(1)))
+typedef unsigned int gf_u32x4 __attribute__((ext_vector_type(4)));
+// Scalars load/store directly; aggregates (uint4, descriptors) move as words.
+template <class T>
+__device__ __forceinline__ T gload(const void *p) {
+    if constexpr (__is_scalar(T)) {
+        return *(const GF_GLOBAL T *)p;
+    } else if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+        gf_u32x4 w[sizeof(T) / 16];
+#pragma unroll
+        for (unsigned k = 0; k < sizeof(T) / 16; k++) w[k] = ((const GF_GLOBAL gf_u32x4 *)p)[k];
+        T v;
+        __builtin_memcpy(&v, w, sizeof(T));
+        return v;
+    } else if constexpr (sizeof(T) % 8 == 0 && alignof(T) >= 8) {
+        unsigned long long w[sizeof(T) / 8];
+#pragma unroll
+        for (unsigned k = 0; k < sizeof(T) / 8; k++) w[k] = ((const GF_GLOBAL unsigned long long *)p)[k];
+        T v;
+        __builtin_memcpy(&v, w, sizeof(T));
+        return v;
+    } else if constexpr (sizeof(T) % 4 == 0 && alignof(T) >= 4) {
+        unsigned w[sizeof(T) / 4];
+#pragma unroll
+        for (unsigned k = 0; k < sizeof(T) / 4; k++) w[k] = ((const GF_GLOBAL unsigned *)p)[k];
+        T v;
+        __builtin_memcpy(&v, w, sizeof(T));
+        return v;
+    } else {
+        static_assert(sizeof(T) % 2 == 0 && alignof(T) >= 2, "gload: half-word aggregates at least");
+        unsigned short w[sizeof(T) / 2];
+#pragma unroll
+        for (unsigned k = 0; k < sizeof(T) / 2; k++) w[k] = ((const GF_GLOBAL unsigned short *)p)[k];
+        T v;
+        __builtin_memcpy(&v, w, sizeof(T));
+        return v;
+    }
+}
+template <class T>
+__device__ __forceinline__ void gstore(void *p, T v) {
+    if constexpr (__is_scalar(T)) {
+        *(GF_GLOBAL T *)p = v;
+    } else {
+        static_assert(sizeof(T) == 16 && alignof(T) >= 16, "gstore: 16-B aggregates only");
+        gf_u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        *(GF_GLOBAL gf_u32x4 *)p = w;
+    }
+}
+__device__ __forceinline__ uint32_t gcas(void *p, uint32_t expect, uint32_t want) {
+    __hip_atomic_compare_exchange_strong((GF_GLOBAL uint32_t *)p, &expect, want, __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return expect;                                   // the value seen (== expect on success)
+}
+__device__ __forceinline__ uint32_t gadd32(void *p, uint32_t v) {
+    return __hip_atomic_fetch_add((GF_GLOBAL uint32_t *)p, v, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gadd64(void *p, unsigned long long v) {
+    (void)__hip_atomic_fetch_add((GF_GLOBAL unsigned long long *)p, v, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore_relaxed(void *p, uint32_t v) {
+    __hip_atomic_store((GF_GLOBAL uint32_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NW>
 __device__ __forceinline__ void load_words(const uint8_t *p, uint32_t (&w)[NW]) {
     int k = 0;
@@ -42,7 +114,7 @@ struct Hdr {
     __device__ __forceinline__ void load(const uint8_t *s) {
 #pragma unroll
         for (int k = 0; k < NW; k += 4) {
-            uint4 v = *reinterpret_cast<const uint4 *>(s + 4 * k);
+            uint4 v = gload<uint4>(s + 4 * k);
             w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
         }
     }
@@ -177,11 +249,10 @@ template <int VW>
 __device__ __forceinline__ void store_words(uint8_t *p, const uint32_t *v) {
     if ((VW % 4) == 0 && ((uintptr_t)p & 15u) == 0) {
 #pragma unroll
-        for (int k = 0; k < VW; k += 4)
-            *reinterpret_cast<uint4 *>(p + 4 * k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+        for (int k = 0; k < VW; k += 4) gstore<uint4>(p + 4 * k, make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]));
     } else {
 #pragma unroll
-        for (int k = 0; k < VW; k++) reinterpret_cast<uint32_t *>(p)[k] = v[k];
+        for (int k = 0; k < VW; k++) gstore<uint32_t>(p + 4 * k, v[k]);
     }
 }
 
@@ -226,38 +297,36 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         return f;
     }
     if (strict) {
-        uint32_t old = atomicAdd(d.count, 1u);
-        if (old >= d.max_entries) { atomicSub(d.count, 1u); return -7; }
+        uint32_t old = gadd32(d.count, 1u);
+        if (old >= d.max_entries) { gadd32(d.count, ~0u); return -7; }
     }
     const uint32_t keep = SB ? (kw[SW] & ((1u << (8 * SB)) - 1u)) : 0u;
     const uint32_t busy = keep | ((uint32_t)GF_SLOT_BUSY << (8 * SB));
     auto fill = [&](uint64_t i) {
         uint8_t *s = d.slots + i * d.slot_size;
-        uint32_t *ks = reinterpret_cast<uint32_t *>(s);
 #pragma unroll
-        for (int k = 0; k < SW; k++) ks[k] = kw[k];
+        for (int k = 0; k < SW; k++) gstore<uint32_t>(s + 4 * k, kw[k]);
         store_value<VW>(d, i, vw);
-        __atomic_store_n(reinterpret_cast<uint32_t *>(s + 4 * SW), keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)),
-                         __ATOMIC_RELAXED);
+        gstore_relaxed(s + 4 * SW, keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)));
         if (!strict) (*added)++;
     };
     if (hint >= 0 && ((hint_word >> (8 * SB)) & 0xffu) == GF_SLOT_EMPTY) {
-        uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + (uint64_t)hint * d.slot_size + 4 * SW);
-        if (atomicCAS(sw, hint_word, busy) == hint_word) { fill((uint64_t)hint); return hint; }
+        uint8_t *sw = d.slots + (uint64_t)hint * d.slot_size + 4 * SW;
+        if (gcas(sw, hint_word, busy) == hint_word) { fill((uint64_t)hint); return hint; }
     }
     uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
     for (uint64_t p = 0; p <= d.mask; p++) {
-        uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + i * d.slot_size + 4 * SW);
-        uint32_t cur = *reinterpret_cast<volatile uint32_t *>(sw);
+        uint8_t *sw = d.slots + i * d.slot_size + 4 * SW;
+        uint32_t cur = *(volatile GF_GLOBAL uint32_t *)sw;
         for (;;) {
             if (((cur >> (8 * SB)) & 0xffu) != GF_SLOT_EMPTY) break;
-            uint32_t seen = atomicCAS(sw, cur, busy);
+            uint32_t seen = gcas(sw, cur, busy);
             if (seen == cur) { fill(i); return (int64_t)i; }
             cur = seen;
         }
         i = (i + 1) & d.mask;
     }
-    if (strict) atomicSub(d.count, 1u);
+    if (strict) gadd32(d.count, ~0u);
     return -7;
 }
 
@@ -266,11 +335,11 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
     constexpr int SW = KSZ / 4, SB = KSZ % 4;
     int64_t f = ht_find<KSZ, U>(d, kw, key_hash<KSZ, MODE>(kw));
     if (f < 0) return;
-    uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + (uint64_t)f * d.slot_size + 4 * SW);
-    uint32_t cur = *sw;
+    uint8_t *sw = d.slots + (uint64_t)f * d.slot_size + 4 * SW;
+    uint32_t cur = gload<uint32_t>(sw);
     uint32_t nv = (cur & ~(0xffu << (8 * SB))) | ((uint32_t)GF_SLOT_TOMB << (8 * SB));
-    __atomic_store_n(sw, nv, __ATOMIC_RELAXED);
-    if (strict) atomicSub(d.count, 1u);
+    gstore_relaxed(sw, nv);
+    if (strict) gadd32(d.count, ~0u);
     else (*added)--;
 }
 
@@ -279,20 +348,20 @@ __device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_
     if (!t.root_bits) return false;
     auto byte_at = [&](uint32_t k) -> uint32_t { return (aw[k >> 2] >> (8 * (k & 3))) & 0xffu; };
     uint32_t idx = t.root_bits == 16 ? ((byte_at(0) << 8) | byte_at(1)) : byte_at(0);
-    uint32_t e = t.root[idx];
+    uint32_t e = gload<uint32_t>(t.root + idx);
     if (e == 0) return false;
     if (e == GF_TRIE_FULL) return true;
     uint32_t node = e - 1;
     for (uint32_t k = t.root_bits / 8; k < t.addr_bytes; k++) {
         uint32_t b = byte_at(k);
-        const uint64_t *nd = reinterpret_cast<const uint64_t *>(t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES);
+        const uint8_t *nd = t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES;
         uint32_t w = b >> 6, bit = b & 63;
-        if ((nd[w] >> bit) & 1ull) return true;
-        uint64_t cw = nd[4 + w];
+        if ((gload<uint64_t>(nd + 8 * w) >> bit) & 1ull) return true;
+        uint64_t cw = gload<uint64_t>(nd + 32 + 8 * w);
         if (!((cw >> bit) & 1ull)) return false;
         uint32_t rank = __popcll(cw & ((1ull << bit) - 1ull));
-        for (uint32_t j = 0; j < w; j++) rank += __popcll(nd[4 + j]);
-        node = reinterpret_cast<const uint32_t *>(nd)[16] + rank;
+        for (uint32_t j = 0; j < w; j++) rank += __popcll(gload<uint64_t>(nd + 32 + 8 * j));
+        node = gload<uint32_t>(nd + 64) + rank;
     }
     return false;
 }

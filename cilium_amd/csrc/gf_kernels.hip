@@ -17,7 +17,6 @@
 #include <rocprim/iterator/discard_iterator.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
-#include <new>
 #include <string.h>
 
 using namespace gf;
@@ -198,7 +197,7 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
                 if (drop) v = XDP_DROP_;
                 else {
                     ab += 20;
-                    uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+                    uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
                     uint32_t dw[4] = {d.x, d.y, d.z, d.w};
                     v = lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
                 }
@@ -245,26 +244,26 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
         uint32_t kw[2] = {daddr, dport};
         int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
         ab += 20;
-        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
+        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (gload<uint16_t>(v + 6)) svc = v; }
         if (!svc) dport = 0;
     }
     if (!svc && (L.flags & GF_LB_F_L3)) {
         uint32_t kw[2] = {daddr, dport};
         int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
         ab += 20;
-        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (*reinterpret_cast<const uint16_t *>(v + 6)) svc = v; }
+        if (f >= 0) { const uint8_t *v = ht_val(L.s4, f); if (gload<uint16_t>(v + 6)) svc = v; }
     }
     if (!svc) return TC_OK;
-    uint32_t count = *reinterpret_cast<const uint16_t *>(svc + 6);
+    uint32_t count = gload<uint16_t>(svc + 6);
     uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
     uint32_t kw[2] = {daddr, dport | (slave << 16)};
     int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
     ab += 20;
     if (f < 0) return D_NO_SERVICE;
     const uint8_t *be = ht_val(L.s4, f);
-    uint32_t target = *reinterpret_cast<const uint32_t *>(be);
-    uint32_t port = *reinterpret_cast<const uint16_t *>(be + 4);
-    uint32_t rn = *reinterpret_cast<const uint16_t *>(be + 8);
+    uint32_t target = gload<uint32_t>(be);
+    uint32_t port = gload<uint16_t>(be + 4);
+    uint32_t rn = gload<uint16_t>(be + 8);
     uint16_t nd = 0;
     int r = lb_checks(L, len, l4_off, nh, dport, port, false, &nd);
     if (r < 0) return r;
@@ -277,7 +276,7 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     if (len < 54 || !c.daddr6) return D_INVALID;
     uint32_t nh = c.proto[i];
     int l4_off = c.l4_off[i];
-    uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+    uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
     uint32_t dport = 0;
     if (L.flags & GF_LB_F_L4) {
         if (nh == 6 || nh == 17) {
@@ -290,17 +289,17 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
         uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
         int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
         ab += 44;
-        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
+        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (gload<uint16_t>(v + 18)) svc = v; }
         if (!svc) dport = 0;
     }
     if (!svc && (L.flags & GF_LB_F_L3)) {
         uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport};
         int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
         ab += 44;
-        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (*reinterpret_cast<const uint16_t *>(v + 18)) svc = v; }
+        if (f >= 0) { const uint8_t *v = ht_val(L.s6, f); if (gload<uint16_t>(v + 18)) svc = v; }
     }
     if (!svc) return TC_OK;
-    uint32_t count = *reinterpret_cast<const uint16_t *>(svc + 18);
+    uint32_t count = gload<uint16_t>(svc + 18);
     uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
     uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport | (slave << 16)};
     int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
@@ -308,9 +307,9 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     if (f < 0) return D_NO_SERVICE;
     const uint8_t *be = ht_val(L.s6, f);
     uint32_t t[4];
-    for (int k = 0; k < 4; k++) t[k] = *reinterpret_cast<const uint32_t *>(be + 4 * k);
-    uint32_t port = *reinterpret_cast<const uint16_t *>(be + 16);
-    uint32_t rn = *reinterpret_cast<const uint16_t *>(be + 20);
+    for (int k = 0; k < 4; k++) t[k] = gload<uint32_t>(be + 4 * k);
+    uint32_t port = gload<uint16_t>(be + 16);
+    uint32_t rn = gload<uint16_t>(be + 20);
     if (rn) t[3] |= rn;
     uint16_t ndp = 0;
     int r = lb_checks(L, len, l4_off, nh, dport, port, true, &ndp);
@@ -383,20 +382,21 @@ struct CtState { uint32_t rev_nat, loopback, carry; };
 // The endpoint program of the lane's current packet, kept in registers while
 // consecutive packets of the lane's bucket target the same endpoint.
 struct Ep {
-    uint32_t sl = 0;                 // program slot + 1 (0: none loaded)
-    uint32_t flags = 0;
-    uint8_t *pol = nullptr;          // policy map slots / side array / mask (< 2^32 slots)
-    uint8_t *pol_side = nullptr;
-    uint32_t pol_mask = 0;
-    uint32_t next = 0;               // round-robin bits: bit0 counter sums (PolAcc), bit1 decisions (PolMemo)
+    uint32_t sl;                     // program slot + 1 (0: none loaded)
+    uint32_t flags;
+    uint8_t *pol;                    // policy map slots / side array / mask (< 2^32 slots)
+    uint8_t *pol_side;
+    uint32_t pol_mask;
+    uint32_t next;                   // round-robin bits: bit0 counter sums (PolAcc), bit1 decisions (PolMemo)
+    __device__ __forceinline__ void init() { sl = 0; flags = 0; pol = pol_side = nullptr; pol_mask = 0; next = 0; }
     __device__ __forceinline__ void use(const IngCtx &X, uint32_t s) {
         if (s == sl) return;
         sl = s;
         const gf_lxc_dev *c = X.cfgs + (s - 1);
-        flags = c->flags;
-        pol = c->policy.slots;
-        pol_side = c->policy.vals;
-        pol_mask = (uint32_t)c->policy.mask;
+        flags = gload<uint32_t>(&c->flags);
+        pol = gload<uint8_t *>(&c->policy.slots);
+        pol_side = gload<uint8_t *>(&c->policy.vals);
+        pol_mask = (uint32_t)gload<uint64_t>(&c->policy.mask);
     }
     __device__ __forceinline__ const gf_lxc_dev *cfg(const IngCtx &X) const { return X.cfgs + (sl - 1); }
     __device__ __forceinline__ gf_htab_desc pdesc() const {
@@ -414,8 +414,9 @@ struct Ep {
 template <int TW>
 struct RelCache {
     uint32_t k[TW];
-    uint32_t slot = ~0u;     // ~0u: none (tables of >= 2^32 slots are not cached)
-    uint32_t sec = 0;        // src_sec_id of the cold value part this lane wrote there
+    uint32_t slot;           // ~0u: none (tables of >= 2^32 slots are not cached)
+    uint32_t sec;            // src_sec_id of the cold value part this lane wrote there
+    __device__ __forceinline__ void init() { slot = ~0u; sec = 0; }
 };
 
 // __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part.  CT
@@ -436,9 +437,9 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     st.loopback = (fl >> 3) & 1u;
     if (acct) {                                         // rx_packets += 1, rx_bytes += len (exclusive lane)
         uint32_t pk = hot.z + 1u, by = hot.w + len;
-        uint32_t *hi = reinterpret_cast<uint32_t *>(d.sstride ? ht_side(d, (uint64_t)f) : e + 16);
-        if (pk == 0u) { hi[0] += 1u; st.carry = 1; }
-        if (by < hot.w) { hi[1] += 1u; st.carry = 1; }
+        uint8_t *hi = d.sstride ? ht_side(d, (uint64_t)f) : e + 16;
+        if (pk == 0u) { gstore<uint32_t>(hi, gload<uint32_t>(hi) + 1u); st.carry = 1; }
+        if (by < hot.w) { gstore<uint32_t>(hi + 4, gload<uint32_t>(hi + 4) + 1u); st.carry = 1; }
         hot.z = pk; hot.w = by;
     }
     if (action == ACT_CREATE) {
@@ -453,7 +454,7 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     }
     hot.x = life;
     hot.y = (hot.y & 0xffff0000u) | fl;
-    *reinterpret_cast<uint4 *>(e) = hot;
+    gstore<uint4>(e, hot);
 }
 
 // ct_lookup4/6 (conntrack.h:310-437, dir = CT_INGRESS), resolve part: the home
@@ -482,7 +483,7 @@ __device__ __forceinline__ int ct_lookup(const gf_htab_desc &d, ProbeLine<KSZ, U
             for (int u = 0; u < U; u++)
                 if (u == pr.u) hot = make_uint4(L.hd[u].w[NW - 4], L.hd[u].w[NW - 3], L.hd[u].w[NW - 2], L.hd[u].w[NW - 1]);
         } else {
-            hot = *reinterpret_cast<const uint4 *>(ht_val(d, (uint64_t)pr.f));
+            hot = gload<uint4>(ht_val(d, (uint64_t)pr.f));
         }
     }
     if (pr.f >= 0 && !pr.is_b) {
@@ -543,10 +544,10 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
 // l4_proxy_lookup (ingress) + BPF_L4_MAP semantics, bpf/lib/l4.h:151-217, common.h:105-127
 __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh, uint32_t dport) {
     if (nh != 6 && nh != 17) return 0;
-    uint32_t n = c->n_l4;
+    uint32_t n = gload<uint32_t>(&c->n_l4);
     if (!n) return 0;
     for (uint32_t k = 0; k < n; k++) {
-        gf_l4_allow_dev a = c->l4[k];
+        gf_l4_allow_dev a = gload<gf_l4_allow_dev>(&c->l4[k]);
         if (a.port && a.port == dport) {
             if (a.nexthdr && a.nexthdr == nh) return a.proxy;   // first match decides
         }
@@ -561,15 +562,18 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // with one pair of atomics when the entry changes and at the end — the same
 // totals with a fraction of the memory-side atomics.
 struct PolAcc {
-    uint32_t f[2] = {0, 0};                  // policy slots of the open sums
-    uint16_t sl[2] = {0, 0};                 // their program slot + 1 (0: sum not open)
-    uint32_t pk[2] = {0, 0}, by[2] = {0, 0}; // flushed before a 32-bit sum could wrap
+    uint32_t f[2];                           // policy slots of the open sums
+    uint16_t sl[2];                          // their program slot + 1 (0: sum not open)
+    uint32_t pk[2], by[2];                   // flushed before a 32-bit sum could wrap
+    __device__ __forceinline__ void init() {
+        for (int j = 0; j < 2; j++) { f[j] = 0; sl[j] = 0; pk[j] = 0; by[j] = 0; }
+    }
     __device__ __forceinline__ void flush_one(const IngCtx &X, int j) {
         if (sl[j]) {
-            uint8_t *side = X.cfgs[sl[j] - 1].policy.vals;
-            unsigned long long *c = reinterpret_cast<unsigned long long *>(side + (uint64_t)f[j] * GF_POL_SIDE);
-            atomicAdd(&c[0], (unsigned long long)pk[j]);
-            atomicAdd(&c[1], (unsigned long long)by[j]);
+            uint8_t *side = gload<uint8_t *>(&X.cfgs[sl[j] - 1].policy.vals);
+            uint8_t *c = side + (uint64_t)f[j] * GF_POL_SIDE;
+            gadd64(c, (unsigned long long)pk[j]);
+            gadd64(c + 8, (unsigned long long)by[j]);
         }
         sl[j] = 0; pk[j] = 0; by[j] = 0;
     }
@@ -603,13 +607,14 @@ __device__ __forceinline__ uint32_t pol_home(uint32_t identity, uint32_t dport, 
 // which stay per packet.  Consecutive packets of a lane's flow group mostly ask
 // the same question, so the answer (and the entry to count) is kept.
 struct PolDecision {          // 24 B (kept in LDS with the rest of the lane state)
-    uint32_t id = 0, sip = 0, pk = 0;
-    uint32_t slab = 0;       // program slot + 1 | algorithmic bytes of the decision << 16
-    uint32_t f = ~0u;        // policy slot counted by the decision, ~0u: none
-    int verdict = 0;
+    uint32_t id, sip, pk;
+    uint32_t slab;           // program slot + 1 | algorithmic bytes of the decision << 16 (0: empty)
+    uint32_t f;              // policy slot counted by the decision, ~0u: none
+    int verdict;
 };
 struct PolMemo {             // two decisions (a group's flows use a couple of ports)
     PolDecision d[2];
+    __device__ __forceinline__ void init() { d[0].slab = d[1].slab = 0; }
     __device__ __forceinline__ int find(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
 #pragma unroll
         for (int j = 0; j < 2; j++)
@@ -671,15 +676,15 @@ __device__ int policy_lookup(const IngCtx &X, const Ep &ep, PolLine &pl, bool pl
 proxy: {
         ab += 40;                                       // entry read + counters written
         fc = f;
-        if (pp == 0xffffffffu) pp = *reinterpret_cast<const uint16_t *>(ht_val(pd, (uint64_t)f));
+        if (pp == 0xffffffffu) pp = gload<uint16_t>(ht_val(pd, (uint64_t)f));
         if (pp) return (int)pp;
         return l4_proxy_lookup(ep.cfg(X), proto, dport);
     }
 deny:
     if (identity < 256) {                               // identity_is_reserved
         const gf_lxc_dev *c = ep.cfg(X);
-        if (v6) { const gf_trie_desc tr = c->cidr6; if (tr.root_bits) ab += 21; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
-        else { const gf_trie_desc tr = c->cidr4; if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
+        if (v6) { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr6); if (tr.root_bits) ab += 21; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
+        else { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr4); if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
     }
     return D_POLICY;
 }
@@ -808,15 +813,15 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, int &fwd, u
     fwd = ret;
     if (st.carry) rc.slot = ~0u;                         // a counter carry touched a cold value part
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
-        const gf_htab_desc rn = ep.cfg(X)->revnat4;
+        const gf_htab_desc rn = gload<gf_htab_desc>(&ep.cfg(X)->revnat4);
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 8;
         if (f >= 0) {
             const uint8_t *nat = ht_val(rn, f);
-            int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 4), r.l4w0, false);
+            int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 4), r.l4w0, false);
             if (r2 < 0) return r2;
-            t[1] = *reinterpret_cast<const uint32_t *>(nat);   // tuple->saddr = nat->address
+            t[1] = gload<uint32_t>(nat);                       // tuple->saddr = nat->address
         }
     }
     uint32_t orig_sip = r.saddr;
@@ -855,8 +860,8 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
     const uint32_t flags = ep.flags;
     uint32_t nh = r.proto;
-    uint4 d = reinterpret_cast<const uint4 *>(X.daddr6)[i];
-    uint4 s = reinterpret_cast<const uint4 *>(X.saddr6)[i];
+    uint4 d = gload<uint4>(X.daddr6 + 16 * (size_t)i);
+    uint4 s = gload<uint4>(X.saddr6 + 16 * (size_t)i);
     uint32_t t[10] = {d.x, d.y, d.z, d.w, s.x, s.y, s.z, s.w, 0u, nh};
     uint32_t co = csum_l4_offset(nh);
     uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
@@ -881,13 +886,13 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     fwd = ret;
     if (st.carry) rc.slot = ~0u;
     if (st.rev_nat) {
-        const gf_htab_desc rn = ep.cfg(X)->revnat6;
+        const gf_htab_desc rn = gload<gf_htab_desc>(&ep.cfg(X)->revnat6);
         uint32_t kw[1] = {st.rev_nat};
         int64_t f = ht_find<2>(rn, kw, key_hash<2>(kw));
         ab += 20;
         if (f >= 0) {
             const uint8_t *nat = ht_val(rn, f);
-            int r2 = rev_nat_checks(len, r.l4_off, nh, *reinterpret_cast<const uint16_t *>(nat + 16), r.l4w0, true);
+            int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 16), r.l4w0, true);
             if (r2 < 0) return r2;
         }
     }
@@ -926,7 +931,8 @@ struct Lane {
     PolAcc acc;
     PolMemo pm;
     RelCache<FAM == 6 ? 10 : 4> rc;
-    int added = 0;
+    int added;
+    __device__ __forceinline__ void init() { ep.init(); acc.init(); pm.init(); rc.init(); added = 0; }
 };
 
 // handle_policy, bpf/bpf_lxc.c:980-1024.  FAM selects the CT path compiled in:
@@ -999,7 +1005,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
         h = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
     } else if ((cls & 3) == 2) {
         uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
-        uint4 d = reinterpret_cast<const uint4 *>(c.daddr6)[i];
+        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
         uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
         h = (gf_pair_hash6(sw, dw) & GF_KEY_HASH) | GF_KEY_FAM;
     } else {
@@ -1059,8 +1065,9 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
     uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
     const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
     if (F) order += nfam[0];
-    __shared__ __attribute__((aligned(16))) char lane_mem[BLOCK * sizeof(Lane<FAM>)];
-    Lane<FAM> &ln = *new (lane_mem + threadIdx.x * sizeof(Lane<FAM>)) Lane<FAM>();
+    __shared__ Lane<FAM> lanes[BLOCK];
+    Lane<FAM> &ln = lanes[threadIdx.x];
+    ln.init();
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
