@@ -65,9 +65,12 @@ __device__ __forceinline__ void gstore(void *p, T v) {
         *(GF_GLOBAL gf_u32x4 *)p = w;
     }
 }
+#ifndef GF_CAS_SCOPE
+#define GF_CAS_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#endif
 __device__ __forceinline__ uint32_t gcas(void *p, uint32_t expect, uint32_t want) {
     __hip_atomic_compare_exchange_strong((GF_GLOBAL uint32_t *)p, &expect, want, __ATOMIC_RELAXED,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                         __ATOMIC_RELAXED, GF_CAS_SCOPE);
     return expect;                                   // the value seen (== expect on success)
 }
 __device__ __forceinline__ uint32_t gadd32(void *p, uint32_t v) {
@@ -302,12 +305,26 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
     }
     const uint32_t keep = SB ? (kw[SW] & ((1u << (8 * SB)) - 1u)) : 0u;
     const uint32_t busy = keep | ((uint32_t)GF_SLOT_BUSY << (8 * SB));
+    // The claimed (BUSY) slot is this lane's: key, state FULL and value are plain
+    // stores (other lanes only ever test the slot for EMPTY, and their claims go
+    // through the CAS; the host reads after the kernel).  The header goes out as
+    // whole 16-B words when the value starts after the padded header.
     auto fill = [&](uint64_t i) {
         uint8_t *s = d.slots + i * d.slot_size;
+        constexpr int NW = Hdr<KSZ>::NW;
+        if (d.voff >= 4u * NW) {
+            uint32_t h[NW];
 #pragma unroll
-        for (int k = 0; k < SW; k++) gstore<uint32_t>(s + 4 * k, kw[k]);
+            for (int k = 0; k < NW; k++) h[k] = k < SW ? kw[k] : 0u;
+            h[SW] = keep | ((uint32_t)GF_SLOT_FULL << (8 * SB));
+#pragma unroll
+            for (int k = 0; k < NW; k += 4) gstore<uint4>(s + 4 * k, make_uint4(h[k], h[k + 1], h[k + 2], h[k + 3]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < SW; k++) gstore<uint32_t>(s + 4 * k, kw[k]);
+            gstore<uint32_t>(s + 4 * SW, keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)));
+        }
         store_value<VW>(d, i, vw);
-        gstore_relaxed(s + 4 * SW, keep | ((uint32_t)GF_SLOT_FULL << (8 * SB)));
         if (!strict) (*added)++;
     };
     if (hint >= 0 && ((hint_word >> (8 * SB)) & 0xffu) == GF_SLOT_EMPTY) {
@@ -338,7 +355,7 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
     uint8_t *sw = d.slots + (uint64_t)f * d.slot_size + 4 * SW;
     uint32_t cur = gload<uint32_t>(sw);
     uint32_t nv = (cur & ~(0xffu << (8 * SB))) | ((uint32_t)GF_SLOT_TOMB << (8 * SB));
-    gstore_relaxed(sw, nv);
+    gstore<uint32_t>(sw, nv);                          // the key is this lane's (group exclusivity)
     if (strict) gadd32(d.count, ~0u);
     else (*added)--;
 }
