@@ -294,7 +294,15 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
     constexpr int SW = KSZ / 4, SB = KSZ % 4;
     if (!d.slots) return -7;
     uint32_t h = key_hash<KSZ, MODE>(kw);
-    int64_t f = known_absent ? -1 : ht_find<KSZ, U>(d, kw, h);
+    int64_t f = -1;
+    if (!known_absent) {                               // lookup walk; its EMPTY slot is the insert hint
+        ProbeLine<KSZ, U> L;
+        L.load(d, h);
+        ProbeRes r = probe2<KSZ, U, 0>(d, kw, kw, L, false);
+        f = r.f;
+        hint = r.empty;
+        hint_word = r.empty_word;
+    }
     if (f >= 0) {
         store_value<VW>(d, (uint64_t)f, vw);
         return f;
@@ -334,7 +342,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
     uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
     for (uint64_t p = 0; p <= d.mask; p++) {
         uint8_t *sw = d.slots + i * d.slot_size + 4 * SW;
-        uint32_t cur = *(volatile GF_GLOBAL uint32_t *)sw;
+        uint32_t cur = gload<uint32_t>(sw);            // a stale view only makes the CAS fail and retry
         for (;;) {
             if (((cur >> (8 * SB)) & 0xffu) != GF_SLOT_EMPTY) break;
             uint32_t seen = gcas(sw, cur, busy);
