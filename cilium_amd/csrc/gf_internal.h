@@ -54,7 +54,7 @@ struct HTab {
     void rehash(uint64_t new_nslots);
 };
 
-enum class ObjKind { Map, ProgXdp, ProgLb, ProgLxc, PolicyArray };
+enum class ObjKind { Map, ProgXdp, ProgLb, ProgLxc, PolicyArray, ProgPipe };
 
 struct Obj {
     ObjKind kind;
@@ -125,6 +125,15 @@ struct PolicyArray : Obj {
     std::vector<uint16_t> h_slot_of;
     bool dirty = true;
     PolicyArray() : Obj(ObjKind::PolicyArray) {}
+};
+
+struct ProgPipe : Obj {
+    gf_pipeline_cfg cfg{};
+    std::shared_ptr<ProgXdp> xdp;
+    std::shared_ptr<ProgLb> lb;
+    std::shared_ptr<Map> lxc;
+    std::shared_ptr<PolicyArray> policy;
+    ProgPipe() : Obj(ObjKind::ProgPipe) {}
 };
 
 std::shared_ptr<Obj> get_obj(int handle);

@@ -157,6 +157,45 @@ __device__ __forceinline__ bool lxc_has6(const gf_htab_desc &lxc, const uint32_t
     return ht_find<20>(lxc, kw, key_hash<20>(kw)) >= 0;
 }
 
+// xdp_start -> check_filters -> check_v4 / check_v6 (bpf/bpf_xdp.c:97-184) for
+// packet i; ab accumulates the algorithmic bytes.
+__device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const gf_pkt_cols &c, uint32_t i, uint32_t len,
+                                               uint32_t et, uint32_t &ab) {
+    if (len < 14) return XDP_DROP_;
+    if (et == 0x0800) {
+        if (len < 34) return XDP_DROP_;
+        uint32_t sa = c.saddr4[i];
+        bool drop = false;
+        ab += 10;
+        if (x.has_h4) {
+            ab += 9;
+            if (trie_lookup(x.l4, &sa)) drop = true;
+            else { ab += 9; uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
+        }
+        if (drop) return XDP_DROP_;
+        ab += 20;
+        return lxc_has4(x.lxc, c.daddr4[i]) ? XDP_PASS_ : XDP_DROP_;
+    }
+    if (et == 0x86DD) {
+        if (len < 54 || !c.saddr6 || !c.daddr6) return XDP_DROP_;
+        uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
+        uint32_t sw[4] = {s.x, s.y, s.z, s.w};
+        bool drop = false;
+        ab += 34;
+        if (x.has_h6) {
+            ab += 21;
+            if (trie_lookup(x.l6, sw)) drop = true;
+            else { ab += 21; uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
+        }
+        if (drop) return XDP_DROP_;
+        ab += 20;
+        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
+        uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+        return lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
+    }
+    return XDP_PASS_;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t *verdict,
                                                unsigned long long *stats) {
     __shared__ uint32_t sl[272];
@@ -164,45 +203,8 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
     if (stats) st.init();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += gridDim.x * blockDim.x) {
         uint32_t len = c.len[i];
-        uint32_t et = c.ethertype[i];
-        uint8_t v;
         uint32_t ab = 1;                                  // output record
-        if (len < 14) v = XDP_DROP_;
-        else if (et == 0x0800) {
-            if (len < 34) v = XDP_DROP_;
-            else {
-                uint32_t sa = c.saddr4[i];
-                bool drop = false;
-                ab += 10;
-                if (x.has_h4) {
-                    ab += 9;
-                    if (trie_lookup(x.l4, &sa)) drop = true;
-                    else { ab += 9; uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
-                }
-                if (!drop) ab += 20;
-                v = drop ? XDP_DROP_ : (lxc_has4(x.lxc, c.daddr4[i]) ? XDP_PASS_ : XDP_DROP_);
-            }
-        } else if (et == 0x86DD) {
-            if (len < 54 || !c.saddr6 || !c.daddr6) v = XDP_DROP_;
-            else {
-                uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
-                uint32_t sw[4] = {s.x, s.y, s.z, s.w};
-                bool drop = false;
-                ab += 34;
-                if (x.has_h6) {
-                    ab += 21;
-                    if (trie_lookup(x.l6, sw)) drop = true;
-                    else { ab += 21; uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
-                }
-                if (drop) v = XDP_DROP_;
-                else {
-                    ab += 20;
-                    uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
-                    uint32_t dw[4] = {d.x, d.y, d.z, d.w};
-                    v = lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
-                }
-            }
-        } else v = XDP_PASS_;
+        uint8_t v = xdp_verdict(x, c, i, len, c.ethertype[i], ab);
         verdict[i] = v;
         if (stats) st.pkt(v == XDP_DROP_ ? 1u : 0u, v, len, ab);
     }
@@ -228,7 +230,8 @@ __device__ __forceinline__ int lb_checks(const LbDev &L, uint32_t len, int l4_of
 }
 
 // returns program result (TC_OK pass / TC_REDIRECT translated / negative error)
-__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t &ab) {
+__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t &ab,
+                     uint32_t &key_dport) {
     if (len < 34) return D_INVALID;
     uint32_t nh = c.proto[i], daddr = c.daddr4[i];
     int l4_off = c.l4_off[i];
@@ -267,12 +270,13 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     uint16_t nd = 0;
     int r = lb_checks(L, len, l4_off, nh, dport, port, false, &nd);
     if (r < 0) return r;
+    key_dport = dport;
     o.slave = (uint16_t)slave; o.new_dport = nd; o.rev_nat = (uint16_t)rn; o.new_daddr4 = target;
     return TC_REDIRECT;
 }
 
 __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t *nd6,
-                     uint32_t &ab) {
+                     uint32_t &ab, uint32_t &key_dport) {
     if (len < 54 || !c.daddr6) return D_INVALID;
     uint32_t nh = c.proto[i];
     int l4_off = c.l4_off[i];
@@ -314,6 +318,7 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     uint16_t ndp = 0;
     int r = lb_checks(L, len, l4_off, nh, dport, port, true, &ndp);
     if (r < 0) return r;
+    key_dport = dport;
     o.slave = (uint16_t)slave; o.new_dport = ndp; o.rev_nat = (uint16_t)rn;
     for (int k = 0; k < 4; k++) nd6[k] = t[k];
     return TC_REDIRECT;
@@ -331,8 +336,9 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         int ret = TC_OK;
         bool v6 = false;
         uint32_t ab = 12 + 12;                            // header columns + output record
-        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(L, c, i, len, o, n6, ab); } }
-        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o, ab); }
+        uint32_t kd = 0;
+        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(L, c, i, len, o, n6, ab, kd); } }
+        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o, ab, kd); }
         if (ret < 0 || ret == TC_SHOT) {
             o = gf_lb_out{};
             o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -976,8 +982,10 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     return o;
 }
 
+// skip (may be null): packets of a pipeline batch that end before the
+// cilium_policy tail call; they are marked (cls bit 3) and left untouched.
 __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
-                                                    uint32_t *keys) {
+                                                    uint32_t *keys, const uint8_t *skip) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c.n) return;
     gf_rec r;
@@ -992,6 +1000,8 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
     r.proto = c.proto[i];
     uint32_t cls = et == 0x0800 ? 1u : et == 0x86DD ? 2u : 0u;
     if (c.tc_index && (c.tc_index[i] & 1)) cls |= 4u;
+    const bool skipped = skip && skip[i];
+    if (skipped) cls |= 8u;
     r.cls = (uint8_t)cls;
     uint32_t h;
     // Only packets that can reach conntrack (an IP header is present) are bound to
@@ -999,7 +1009,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
     // GF_KEY_BITS-1 bits of the group hash are the sort key: groups that collide
     // share a bucket (always safe: a bucket is serialized as a whole), and a
     // shorter key is one radix pass less.
-    bool ct_ok = ((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6);
+    bool ct_ok = !skipped && (((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6));
     // The top key bit is the family of the CT path (1: IPv6 reaching conntrack).
     if (!ct_ok) {
         h = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
@@ -1026,6 +1036,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 template <int FAM>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
                                         Stats &st, bool stats, Lane<FAM> &ln) {
+    if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
     if (!(GF_DIAG & 1)) out[i] = o;
@@ -1182,6 +1193,293 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
     }
 }
 
+// ================================================================ pipeline (config 4)
+// bpf_xdp -> bpf_lb from-netdev -> bpf_netdev from-netdev -> cilium_policy tail
+// call, each program seeing the frame as the previous one rewrote it.
+// k_pipe_front runs the first three on one packet per lane over a copy of the
+// frame (the rewrites and their checksum updates are applied to that copy),
+// k_parse re-derives the header columns of the rewritten frames, the ingress
+// machinery runs handle_policy on the packets that reached the tail call, and
+// k_pipe_merge folds its records into the pipeline records.
+struct NetdevDev {
+    gf_htab_desc lxc;
+    uint32_t flags, fixed_secctx;
+    uint32_t router6[2];           // first 8 bytes of ROUTER_IP (LE words)
+};
+struct PipeDev {
+    XdpDev x;
+    LbDev L;
+    NetdevDev nd;
+    uint32_t has_xdp, has_lb, lb_redirect_ifindex, vec_copy;
+};
+struct PipeMeta {
+    uint32_t *src_identity, *ifindex;
+    uint16_t *lxc_id;
+    uint8_t *skip;
+};
+
+// The lane's frame copy.  Reads past the snap (or len) are 0, writes past the
+// snap are dropped (the snap holds every header byte the programs touch).
+struct Row {
+    uint8_t *p;
+    uint32_t cap;
+    __device__ __forceinline__ uint32_t b(uint32_t off) const { return off < cap ? (uint32_t)p[off] : 0u; }
+    __device__ __forceinline__ uint32_t r16(uint32_t off) const { return b(off) | (b(off + 1) << 8); }
+    __device__ __forceinline__ uint32_t r32(uint32_t off) const { return r16(off) | (r16(off + 2) << 16); }
+    __device__ __forceinline__ void w8(uint32_t off, uint32_t v) { if (off < cap) p[off] = (uint8_t)v; }
+    __device__ __forceinline__ void w16(uint32_t off, uint32_t v) { w8(off, v & 0xffu); w8(off + 1, (v >> 8) & 0xffu); }
+    __device__ __forceinline__ void w32(uint32_t off, uint32_t v) { w16(off, v & 0xffffu); w16(off + 2, v >> 16); }
+};
+
+// Checksum arithmetic of bpf_l3_csum_replace / bpf_l4_csum_replace /
+// bpf_csum_diff (Linux net/core/filter.c over include/net/checksum.h; the skb is
+// a received frame, not CHECKSUM_PARTIAL).  Operands are raw LE loads of the
+// network-order bytes, as the programs pass them.
+#define GF_F_PSEUDO_HDR (1u << 4)
+#define GF_F_MANGLED_0 (1u << 5)
+__device__ __forceinline__ uint32_t ck_add(uint32_t a, uint32_t b) { uint32_t r = a + b; return r + (r < b ? 1u : 0u); }
+__device__ __forceinline__ uint32_t ck_fold(uint32_t x) {
+    x = (x & 0xffffu) + (x >> 16);
+    x = (x & 0xffffu) + (x >> 16);
+    return ~x & 0xffffu;
+}
+__device__ __forceinline__ uint32_t ck16_add(uint32_t a, uint32_t b) {
+    uint32_t r = (a + b) & 0xffffu;
+    return (r + (r < b ? 1u : 0u)) & 0xffffu;
+}
+// bpf_l3_csum_replace: size 0 = by diff, 2 = csum_replace2, 4 = csum_replace4
+__device__ int l3_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t size) {
+    if (!l4csum_ok(off, len)) return -GF_EFAULT;
+    uint32_t sum = w.r16((uint32_t)off);
+    if (size == 0) sum = ck_fold(ck_add(to, ~sum));
+    else if (size == 2) sum = ~ck16_add(ck16_add(~sum & 0xffffu, ~from & 0xffffu), to & 0xffffu) & 0xffffu;
+    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
+    w.w16((uint32_t)off, sum);
+    return 0;
+}
+// bpf_l4_csum_replace (inet_proto_csum_replace4 / _by_diff, BPF_F_MARK_MANGLED_0)
+__device__ int l4_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t flags) {
+    if (!l4csum_ok(off, len)) return -GF_EFAULT;
+    uint32_t sum = w.r16((uint32_t)off);
+    const bool mmzero = (flags & GF_F_MANGLED_0) != 0;
+    if (mmzero && !sum) return 0;
+    if ((flags & 0xfu) == 0) sum = ck_fold(ck_add(to, ~sum));
+    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
+    if (mmzero && !sum) sum = 0xffffu;                  // CSUM_MANGLED_0
+    w.w16((uint32_t)off, sum);
+    return 0;
+}
+
+// lb4_xlate / lb6_xlate writes (bpf/lib/lb.h:615-659, 397-423) of a translation
+// lb_v4/lb_v6 accepted (their checks passed, so every helper succeeds).
+__device__ void pipe_lb_rewrite(Row &w, uint32_t len, const gf_pkt_cols &c, uint32_t i, bool v6, const gf_lb_out &o,
+                                const uint32_t *n6, uint32_t key_dport, uint32_t &ab) {
+    const uint32_t nh = c.proto[i];
+    const int l4_off = c.l4_off[i];
+    uint32_t sum = 0;
+    if (!v6) {
+        const uint32_t old = c.daddr4[i], nw = o.new_daddr4;
+        w.w32(30, nw);
+        sum = ck_add(ck_add(0u, ~old), nw);             // csum_diff(&key->address, 4, new_daddr, 4, 0)
+        l3_csum(w, len, 24, 0, sum, 0);
+        ab += 4 + 2;
+    } else {
+        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
+        const uint32_t od[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            w.w32(38 + 4 * k, n6[k]);                   // ipv6_store_daddr
+            sum = ck_add(ck_add(sum, ~od[k]), n6[k]);
+        }
+        ab += 16;
+    }
+    const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+    if (co || v6) { l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl); ab += 2; }
+    if (o.new_dport) {                                  // l4_modify_port, bpf/lib/l4.h:50-60
+        l4_csum(w, len, l4_off + (int)co, key_dport, o.new_dport, 2u | fl);
+        w.w16((uint32_t)(l4_off + 2), o.new_dport);
+        ab += 4;
+    }
+}
+
+enum { ND_TAILCALL = 1000, ND_ICMP6_TE = 1001 };
+
+// The common tail of ipv{4,6}_local_delivery (bpf/lib/l3.h:106-168): MACs,
+// map_lxc_in (l3.h:71-104 + l4_port_map_in, bpf/lib/l4.h:62-88: every portmap
+// entry is compared with the dport loaded once), cb[], tail call.
+__device__ int delivery_tail(Row &w, uint32_t len, int l4_off, uint32_t nh, const uint8_t *ep, uint32_t &ifx,
+                             uint32_t &lxc, uint32_t &mapped, uint32_t &ndport, uint32_t &ab) {
+    const uint32_t m0 = gload<uint32_t>(ep + 16), m1 = gload<uint32_t>(ep + 20);
+    const uint32_t r0 = gload<uint32_t>(ep + 24), r1 = gload<uint32_t>(ep + 28);
+    w.w32(6, r0); w.w16(10, r1 & 0xffffu);              // eth_store_saddr(node_mac)
+    w.w32(0, m0); w.w16(4, m1 & 0xffffu);               // eth_store_daddr(mac)
+    ab += 16 + 12;
+    const uint32_t pm0 = gload<uint32_t>(ep + 48);
+    ab += 4;
+    if ((pm0 >> 16) && (nh == 6 || nh == 17)) {
+        if (!skb_ok(l4_off + 2, 2, len)) return D_INVALID;
+        const uint32_t dport = w.r16((uint32_t)(l4_off + 2));
+        const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+        for (int k = 0; k < 16; k++) {                  // PORTMAP_MAX
+            const uint32_t pm = k ? gload<uint32_t>(ep + 48 + 4 * k) : pm0;
+            const uint32_t from = pm & 0xffffu, to = pm >> 16;
+            if (k) ab += 4;
+            if (!to || !from) break;
+            if (from != dport) continue;
+            if (l4_csum(w, len, l4_off + (int)co, dport, to, 2u | fl) < 0) return D_CSUM_L4;
+            if (!skb_ok(l4_off + 2, 2, len)) return D_WRITE_ERROR;
+            w.w16((uint32_t)(l4_off + 2), to);
+            mapped = 1; ndport = to;
+            ab += 4;
+        }
+    }
+    ifx = gload<uint32_t>(ep);                          // cb[CB_IFINDEX] = ep->ifindex
+    lxc = gload<uint16_t>(ep + 6);                      // tail_call(cilium_policy, ep->lxc_id)
+    return ND_TAILCALL;
+}
+
+// from_netdev of bpf/bpf_netdev.c:395-460 -> handle_ipv4 (:326-393) / handle_ipv6
+// (:160-247), without FROM_HOST, ENCAP_IFINDEX or HANDLE_NS.
+__device__ int pipe_netdev(const NetdevDev &N, Row &w, const gf_pkt_cols &c, uint32_t i, uint32_t et, uint32_t len,
+                           uint32_t &sec, uint32_t &ifx, uint32_t &lxc, uint32_t &mapped, uint32_t &ndport,
+                           uint32_t &ab) {
+    if (et == 0x0800) {
+        if (len < 34) return D_INVALID;                 // revalidate_data
+        sec = (N.flags & GF_NETDEV_F_FIXED_SECCTX) ? N.fixed_secctx : 2u;   // derive_ipv4_sec_ctx: WORLD_ID
+        uint32_t kw[5] = {w.r32(30), 0, 0, 0, 1u};      // lookup_ip4_endpoint (post-LB daddr)
+        const int64_t f = ht_find<20>(N.lxc, kw, key_hash<20>(kw));
+        ab += 20;
+        if (f < 0) return TC_OK;
+        const uint8_t *ep = ht_val(N.lxc, f);
+        ab += 8;
+        if (gload<uint32_t>(ep + 8) & 1u) return TC_OK; // ENDPOINT_F_HOST
+        const uint32_t ttl = w.b(22);                   // ipv4_dec_ttl, bpf/lib/ipv4.h:30-43
+        if (ttl <= 1) return D_INVALID;
+        l3_csum(w, len, 24, ttl, ttl - 1, 2);
+        w.w8(22, ttl - 1);
+        ab += 3;
+        return delivery_tail(w, len, c.l4_off[i], c.proto[i], ep, ifx, lxc, mapped, ndport, ab);
+    }
+    if (et == 0x86DD) {
+        if (len < 54) return D_INVALID;
+        sec = 2u;                                       // derive_sec_ctx (bpf_netdev.c:50-64)
+        if (N.flags & GF_NETDEV_F_FIXED_SECCTX) sec = N.fixed_secctx;
+        else if (w.r32(22) == N.router6[0] && w.r32(26) == N.router6[1])
+            sec = __builtin_bswap32(w.r32(14) & __builtin_bswap32(0x000FFFFFu));
+        uint32_t kw[5] = {w.r32(38), w.r32(42), w.r32(46), w.r32(50), 2u};
+        const int64_t f = ht_find<20>(N.lxc, kw, key_hash<20>(kw));
+        ab += 20 + 8;
+        if (f < 0) return TC_OK;
+        const uint8_t *ep = ht_val(N.lxc, f);
+        ab += 8;
+        if (gload<uint32_t>(ep + 8) & 1u) return TC_OK;
+        const uint32_t hl = w.b(21);                    // ipv6_dec_hoplimit, bpf/lib/ipv6.h:178-193
+        if (hl <= 1) return ND_ICMP6_TE;
+        w.w8(21, hl - 1);
+        ab += 1;
+        return delivery_tail(w, len, c.l4_off[i], c.proto[i], ep, ifx, lxc, mapped, ndport, ab);
+    }
+    return TC_OK;                                       // unknown traffic to the stack
+}
+
+__global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols c, PipeDev P, uint8_t *snap2,
+                                                      gf_pipeline_out *out, uint8_t *nd6, PipeMeta M,
+                                                      unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    // this block's frames, copied coalesced; each lane then rewrites its own row
+    const uint32_t S = fr.snap_stride, b0 = blockIdx.x * BLOCK;
+    const uint32_t nb = fr.n - b0 < BLOCK ? fr.n - b0 : BLOCK;
+    {
+        const uint8_t *src = fr.snap + (size_t)b0 * S;
+        uint8_t *dst = snap2 + (size_t)b0 * S;
+        const size_t bytes = (size_t)nb * S;
+        size_t k0 = 0;
+        if (P.vec_copy) {
+            const size_t nv = bytes / 16;
+            for (size_t k = threadIdx.x; k < nv; k += BLOCK)
+                reinterpret_cast<uint4 *>(dst)[k] = reinterpret_cast<const uint4 *>(src)[k];
+            k0 = nv * 16;
+        }
+        for (size_t k = k0 + threadIdx.x; k < bytes; k += BLOCK) dst[k] = src[k];
+    }
+    if (stats) st.init(); else __syncthreads();
+    const uint32_t i = b0 + threadIdx.x;
+    if (i < fr.n) {
+        const uint32_t len = c.len[i], et = c.ethertype[i];
+        Row w{snap2 + (size_t)i * S, S < len ? S : len};
+        gf_pipeline_out o{};
+        uint32_t n6[4] = {0, 0, 0, 0};
+        uint32_t sec = 0, ifx = 0, lxc = 0, mapped = 0, ndport = 0;
+        uint32_t ab = 24;                               // output record
+        bool tail = false;
+        do {
+            if (P.has_xdp && xdp_verdict(P.x, c, i, len, et, ab) == XDP_DROP_) {
+                o.stage = GF_STAGE_XDP; o.action = XDP_DROP_;
+                break;
+            }
+            if (P.has_lb) {
+                gf_lb_out lo{};
+                uint32_t kd = 0;
+                int ret = TC_OK;
+                bool v6 = false;
+                ab += 12;
+                if (et == 0x86DD) {
+                    if (!(P.L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(P.L, c, i, len, lo, n6, ab, kd); }
+                } else if (et == 0x0800) {
+                    if (!(P.L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(P.L, c, i, len, lo, ab, kd);
+                }
+                if (ret < 0 || ret == TC_SHOT) {
+                    o.stage = GF_STAGE_LB; o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
+                    n6[0] = n6[1] = n6[2] = n6[3] = 0;
+                    break;
+                }
+                if (ret == TC_REDIRECT) {
+                    pipe_lb_rewrite(w, len, c, i, v6, lo, n6, kd, ab);
+                    o.slave = lo.slave; o.rev_nat = lo.rev_nat; o.dport = lo.new_dport;
+                    o.daddr4 = v6 ? 0u : lo.new_daddr4;
+                    o.flags |= GF_PIPE_F_LB;
+                    if (P.L.flags & GF_LB_F_REDIRECT) {
+                        o.stage = GF_STAGE_LB; o.action = TC_REDIRECT; o.ifindex_lo = (uint16_t)P.lb_redirect_ifindex;
+                        break;
+                    }
+                } else {
+                    n6[0] = n6[1] = n6[2] = n6[3] = 0;
+                }
+            }
+            const int r = pipe_netdev(P.nd, w, c, i, et, len, sec, ifx, lxc, mapped, ndport, ab);
+            if (mapped) { o.flags |= GF_PIPE_F_PORTMAP; o.dport = (uint16_t)ndport; }
+            o.stage = GF_STAGE_NETDEV;
+            if (r == ND_TAILCALL) { o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; tail = true; }
+            else if (r == ND_ICMP6_TE) { o.action = TC_REDIRECT; o.flags |= GF_PIPE_F_ICMP6_TE; }
+            else if (r < 0 || r == TC_SHOT) { o.action = TC_SHOT; o.reason = (uint8_t)(-r); }
+            else o.action = (uint8_t)r;
+        } while (0);
+        out[i] = o;
+        if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
+        M.skip[i] = tail ? 0 : 1;
+        M.src_identity[i] = tail ? sec : 0u;
+        M.ifindex[i] = tail ? ifx : 0u;
+        M.lxc_id[i] = (uint16_t)(tail ? lxc : 0u);
+        if (stats) {
+            if (tail) st.add_n(270, ab);                // handle_policy counts the packet itself
+            else st.pkt(o.reason, o.action, len, ab);
+        }
+    }
+    if (stats) st.flush(stats);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_pipe_merge(uint32_t n, const uint8_t *skip, const gf_ingress_out *ing,
+                                                      gf_pipeline_out *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || skip[i]) return;
+    const gf_ingress_out g = ing[i];
+    gf_pipeline_out o = out[i];
+    o.action = g.action; o.reason = g.reason; o.ct_ret = g.ct_ret; o.flags |= g.flags;
+    o.proxy_port = g.proxy_port; o.ifindex_lo = g.ifindex_lo;
+    out[i] = o;
+}
+
 // ================================================================ host: programs
 namespace {
 
@@ -1228,6 +1526,11 @@ struct Workspace {
     DevBuf rec, keys, skeys, perm, cnt, off, tmp, sched, order;
 };
 Workspace &ws() { static Workspace w; return w; }
+struct PipeWs {
+    DevBuf et[2], sa[2], da[2], proto[2], l4off[2], w0[2], w3[2], s6[2], d6[2];   // [0] original, [1] rewritten
+    DevBuf sid, ifx, lxc, skip, ing, snap;
+};
+PipeWs &pipe_ws() { static PipeWs w; return w; }
 
 int check_cols(const gf_pkt_cols *p) {
     if (!p) return -EFAULT;
@@ -1428,17 +1731,12 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
     return 0;
 }
 
-int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
-                               void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
-    auto o = get_obj(array);
-    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
-    auto a = std::static_pointer_cast<PolicyArray>(o);
-    int c = check_cols(pkts);
-    if (c <= 0) return c;
-    if (!out) return -EFAULT;
-    if (pkts->n > (1u << 30)) return -E2BIG;
-    hipStream_t s = (hipStream_t)stream;
+}  // extern "C"
+
+// handle_policy over a batch (caller holds big_lock and checked the columns).
+// skip (DEVICE, may be null): packets a pipeline ended before the tail call.
+static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
+                       gf_ingress_out *out, hipStream_t s, const uint8_t *skip) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -1560,7 +1858,7 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
         ProfScope ps("k_ing_pack", s);
         hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
                            (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
-                           (uint32_t *)w.keys.p);
+                           (uint32_t *)w.keys.p, skip);
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     size_t tb = w.tmp.bytes;
@@ -1632,6 +1930,154 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
     return 0;
+}
+
+extern "C" {
+
+int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
+                               void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    int c = check_cols(pkts);
+    if (c <= 0) return c;
+    if (!out) return -EFAULT;
+    if (pkts->n > (1u << 30)) return -E2BIG;
+    return ingress_run(a, pkts, now_sec, out, (hipStream_t)stream, nullptr);
+}
+
+// ---- full pipeline ----
+int gf_pipeline_load(const gf_pipeline_cfg *cfg) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!cfg) return -EFAULT;
+    auto p = std::make_shared<ProgPipe>();
+    p->cfg = *cfg;
+    if (cfg->xdp_prog) {
+        auto o = get_obj(cfg->xdp_prog);
+        if (!o || o->kind != ObjKind::ProgXdp) return -EBADF;
+        p->xdp = std::static_pointer_cast<ProgXdp>(o);
+    }
+    if (cfg->lb_prog) {
+        auto o = get_obj(cfg->lb_prog);
+        if (!o || o->kind != ObjKind::ProgLb) return -EBADF;
+        p->lb = std::static_pointer_cast<ProgLb>(o);
+    }
+    auto m = get_map(cfg->netdev.lxc_map);
+    if (!m) return -EBADF;
+    if (m->ksz != 20 || m->vsz != 112 || m->is_lpm()) return -EINVAL;
+    p->lxc = m;
+    auto a = get_obj(cfg->policy_array);
+    if (!a || a->kind != ObjKind::PolicyArray) return -EBADF;
+    p->policy = std::static_pointer_cast<PolicyArray>(a);
+    return new_handle(p);
+}
+
+int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_pipeline_out *out,
+                         uint8_t *nd6, uint8_t *snap_out, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(pipe);
+    if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
+    auto p = std::static_pointer_cast<ProgPipe>(o);
+    if (!b) return -EFAULT;
+    const gf_frames &fr = b->frames;
+    if (fr.n == 0) return 0;
+    if (!fr.snap || !fr.len || !out) return -EFAULT;
+    if (fr.snap_stride < 14) return -EINVAL;
+    if (fr.n > (1u << 30)) return -E2BIG;
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    const uint32_t n = fr.n;
+    PipeDev P{};
+    if (p->xdp) {
+        auto &x = *p->xdp;
+        if ((r = push_map(x.m4h, s)) || (r = push_map(x.m4l, s)) || (r = push_map(x.m6h, s)) ||
+            (r = push_map(x.m6l, s)) || (r = push_map(x.lxc, s)))
+            return r;
+        if (x.m4h) { P.x.h4 = x.m4h->hdesc(); P.x.has_h4 = 1; }
+        if (x.m6h) { P.x.h6 = x.m6h->hdesc(); P.x.has_h6 = 1; }
+        if (x.m4l) P.x.l4 = x.m4l->tdesc();
+        if (x.m6l) P.x.l6 = x.m6l->tdesc();
+        P.x.lxc = x.lxc->hdesc();
+        P.has_xdp = 1;
+    }
+    if (p->lb) {
+        if ((r = push_map(p->lb->lb4, s)) || (r = push_map(p->lb->lb6, s))) return r;
+        if (p->lb->lb4) P.L.s4 = p->lb->lb4->hdesc();
+        if (p->lb->lb6) P.L.s6 = p->lb->lb6->hdesc();
+        P.L.flags = p->lb->cfg.flags;
+        P.lb_redirect_ifindex = p->lb->cfg.redirect_ifindex;
+        P.has_lb = 1;
+    }
+    if ((r = push_map(p->lxc, s))) return r;
+    P.nd.lxc = p->lxc->hdesc();
+    P.nd.flags = p->cfg.netdev.flags;
+    P.nd.fixed_secctx = p->cfg.netdev.fixed_secctx;
+    memcpy(P.nd.router6, p->cfg.netdev.router_ip6, 8);
+    // workspace: original and rewritten columns, the rewritten frames, tail-call metadata
+    PipeWs &w = pipe_ws();
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    const size_t S = fr.snap_stride;
+    for (int k = 0; k < 2; k++) {
+        if ((r = grow(w.et[k], (size_t)n * 2)) || (r = grow(w.sa[k], (size_t)n * 4)) || (r = grow(w.da[k], (size_t)n * 4)) ||
+            (r = grow(w.proto[k], n)) || (r = grow(w.l4off[k], (size_t)n * 2)) || (r = grow(w.w0[k], (size_t)n * 4)) ||
+            (r = grow(w.w3[k], (size_t)n * 2)) || (r = grow(w.s6[k], (size_t)n * 16)) || (r = grow(w.d6[k], (size_t)n * 16)))
+            return r;
+    }
+    if ((r = grow(w.sid, (size_t)n * 4)) || (r = grow(w.ifx, (size_t)n * 4)) || (r = grow(w.lxc, (size_t)n * 2)) ||
+        (r = grow(w.skip, n)) || (r = grow(w.ing, (size_t)n * sizeof(gf_ingress_out))) ||
+        (!snap_out && (r = grow(w.snap, (size_t)n * S))))
+        return r;
+    uint8_t *snap2 = snap_out ? snap_out : (uint8_t *)w.snap.p;
+    auto cols_out = [&](int k) {
+        gf_pkt_cols_out co{};
+        co.ethertype = (uint16_t *)w.et[k].p; co.saddr4 = (uint32_t *)w.sa[k].p; co.daddr4 = (uint32_t *)w.da[k].p;
+        co.proto = (uint8_t *)w.proto[k].p; co.l4_off = (int16_t *)w.l4off[k].p; co.l4w0 = (uint32_t *)w.w0[k].p;
+        co.l4w3 = (uint16_t *)w.w3[k].p; co.saddr6 = (uint8_t *)w.s6[k].p; co.daddr6 = (uint8_t *)w.d6[k].p;
+        return co;
+    };
+    auto cols_in = [&](int k) {
+        gf_pkt_cols c{};
+        c.n = n; c.len = fr.len;
+        c.ethertype = (const uint16_t *)w.et[k].p; c.saddr4 = (const uint32_t *)w.sa[k].p;
+        c.daddr4 = (const uint32_t *)w.da[k].p; c.proto = (const uint8_t *)w.proto[k].p;
+        c.l4_off = (const int16_t *)w.l4off[k].p; c.l4w0 = (const uint32_t *)w.w0[k].p;
+        c.l4w3 = (const uint16_t *)w.w3[k].p; c.saddr6 = (const uint8_t *)w.s6[k].p; c.daddr6 = (const uint8_t *)w.d6[k].p;
+        c.tc_index = b->tc_index;
+        return c;
+    };
+    PipeMeta M{(uint32_t *)w.sid.p, (uint32_t *)w.ifx.p, (uint16_t *)w.lxc.p, (uint8_t *)w.skip.p};
+    P.vec_copy = (((uintptr_t)fr.snap | (uintptr_t)snap2) & 15u) == 0;
+    unsigned long long *sink = (unsigned long long *)stats_sink();
+    const uint32_t grid = (n + BLOCK - 1) / BLOCK;
+    {
+        ProfScope ps("k_parse", s);
+        gf_pkt_cols_out co = cols_out(0);
+        hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(BLOCK), 0, s, fr, co);
+    }
+    {
+        ProfScope ps("k_pipe_front", s);
+        gf_pkt_cols c0 = cols_in(0);
+        c0.flow_hash = b->flow_hash;
+        hipLaunchKernelGGL(k_pipe_front, dim3(grid), dim3(BLOCK), 0, s, fr, c0, P, snap2, out, nd6, M, sink);
+    }
+    if ((r = hip_ok(hipGetLastError(), "k_pipe_front"))) return r;
+    gf_frames fr2 = fr;
+    fr2.snap = snap2;
+    {
+        ProfScope ps("k_parse", s);
+        gf_pkt_cols_out co = cols_out(1);
+        hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(BLOCK), 0, s, fr2, co);
+    }
+    gf_pkt_cols c2 = cols_in(1);
+    c2.src_identity = M.src_identity; c2.ifindex = M.ifindex; c2.lxc_id = M.lxc_id;
+    if ((r = ingress_run(p->policy, &c2, now_sec, (gf_ingress_out *)w.ing.p, s, M.skip))) return r;
+    {
+        ProfScope ps("k_pipe_merge", s);
+        hipLaunchKernelGGL(k_pipe_merge, dim3(grid), dim3(BLOCK), 0, s, n, (const uint8_t *)M.skip,
+                           (const gf_ingress_out *)w.ing.p, out);
+    }
+    return hip_ok(hipGetLastError(), "k_pipe_merge");
 }
 
 }  // extern "C"

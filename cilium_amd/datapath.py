@@ -16,12 +16,15 @@ import numpy as np
 
 from . import bpf
 from ._lib import (lib, gf_frames, gf_pkt_cols, gf_pkt_cols_out, gf_xdp_cfg, gf_lb_cfg, gf_lxc_cfg,
-                   gf_node_cfg)
+                   gf_node_cfg, gf_netdev_cfg, gf_pipeline_cfg, gf_pipe_batch)
 
 LB_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("slave", "<u2"), ("new_dport", "<u2"),
                    ("rev_nat", "<u2"), ("new_daddr4", "<u4")])
 ING_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
                     ("proxy_port", "<u2"), ("ifindex_lo", "<u2")])
+PIPE_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
+                     ("pad0", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
+                     ("rev_nat", "<u2"), ("dport", "<u2"), ("daddr4", "<u4"), ("lxc_id", "<u2"), ("pad1", "<u2")])
 
 
 def _torch():
@@ -156,6 +159,14 @@ class Datapath:
                 self.lxc_progs.append(p)
                 _check(lib.gf_policy_array_update(self.policy_array, e["lxc_id"], p), "gf_policy_array_update")
 
+        self.pipe = None
+        if sc.netdev and self.policy_array:
+            nd = sc.netdev
+            ncfg = gf_netdev_cfg(h(nd["lxc_map"]), nd.get("flags", 0), nd.get("fixed_secctx", 0),
+                                 (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
+            pcfg = gf_pipeline_cfg(self.xdp_prog or 0, self.lb_prog or 0, ncfg, self.policy_array)
+            self.pipe = _check(lib.gf_pipeline_load(C.byref(pcfg)), "gf_pipeline_load")
+
     # ---- classify calls -------------------------------------------------
     def xdp(self, b):
         torch = _torch()
@@ -180,6 +191,20 @@ class Datapath:
         _check(lib.gf_policy_ingress_classify(self.policy_array, C.byref(c), now, _ptr(out), _stream()),
                "gf_policy_ingress_classify")
         return out
+
+    def pipeline(self, b, now, out=None, snap_out=True):
+        """Full pipeline over the batch's frames: returns (records [n,24] u8,
+        new_daddr6 [n,16] u8, rewritten snaps [n,stride] u8 or None)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty((b.n, 24), dtype=torch.uint8, device=b.device)
+        nd6 = torch.empty((b.n, 16), dtype=torch.uint8, device=b.device)
+        snap = torch.empty_like(b.frames) if snap_out else None
+        stride = b.frames.shape[1] if b.n else 64
+        pb = gf_pipe_batch(gf_frames(b.n, stride, _ptr(b.frames), _ptr(b.len)), _ptr(b.tc_index), _ptr(b.flow_hash))
+        _check(lib.gf_pipeline_classify(self.pipe, C.byref(pb), now, _ptr(out), _ptr(nd6), _ptr(snap), _stream()),
+               "gf_pipeline_classify")
+        return out, nd6, snap
 
     # ---- map readback ----------------------------------------------------
     def dump_map(self, name):

@@ -66,6 +66,7 @@ class Scenario:
     xdp: dict = None             # role -> map name
     lb: dict = None              # {'lb4','lb6','flags','redirect_ifindex'}
     lxc: list = field(default_factory=list)   # endpoint program configs
+    netdev: dict = None          # bpf_netdev config of the full pipeline (gf_netdev_cfg)
     host_ifindex: int = 1
     batches: list = field(default_factory=list)   # list of Packets, processed in order
     now: int = 1000
@@ -851,4 +852,75 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
         tci = (rng.random(n) < 0.1).astype(np.uint8)
         fh = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
         sc.batches.append(Packets(f, lens, sid, ifx, lid, tci, fh))
+    return sc
+
+
+def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed_secctx=None):
+    """The fuzz scenario run through the whole pipeline (bpf_xdp -> bpf_lb ->
+    bpf_netdev -> handle_policy): endpoint MACs and port maps (duplicated and
+    unterminated entries), host endpoints, VIPs present in cilium_lxc as host
+    entries (so the prefilter passes them), TTL / hop-limit 0..1, random IPv4
+    and L4 checksums (UDP 0 = no checksum), sources inside ROUTER_IP/64.
+    256-B snaps hold every header byte the programs touch."""
+    sc = fuzz(seed, n_packets, n_batches, stride=256)
+    sc.name = f"pipe{seed}"
+    rng = np.random.default_rng(seed ^ 0x5151)
+    lxc = sc.maps["cilium_lxc"]
+    n = lxc.n()
+    v = lxc.vals.copy()
+    v[:, 16:22] = rng.integers(0, 256, (n, 6))
+    v[:, 24:30] = rng.integers(0, 256, (n, 6))
+    ports = np.array([80, 443, 53, 8080, 1000, 2000], np.uint32)
+    for e in range(n):
+        if e % 3 == 1:
+            k = int(rng.integers(1, 6))
+            frm = ports[rng.integers(0, len(ports), k)]
+            to = rng.integers(1, 65536, k)
+            if e % 2:
+                frm[-1] = frm[0]                        # two entries for one port: both apply
+            pm = np.stack([raw16(frm), raw16(to)], axis=1).astype("<u2").view(np.uint8).reshape(-1)
+            v[e, 48:48 + 4 * k] = pm
+            if e == 4:
+                v[e, 48 + 4 * k:48 + 4 * k + 2] = 1     # a 'from' without 'to' ends the list
+    v[3, 8:12] = 1                                      # ENDPOINT_F_HOST (v4)
+    v[15, 8:12] = 1                                     # ENDPOINT_F_HOST (v6)
+    # VIPs as host entries (half of them), so bpf_xdp's endpoint check passes them
+    vip4 = (ip4("10.96.0.1") + np.arange(8)).astype(np.uint32)[::2]
+    hk = endpoint_keys4(vip4)
+    hv = endpoint_infos(np.full(len(vip4), 1), np.zeros(len(vip4)), np.zeros(len(vip4)), np.ones(len(vip4)))
+    lb6 = sc.maps["lb6_svc"]
+    vip6 = np.unique(lb6.keys[:, :16], axis=0)[::2]
+    hk6 = endpoint_keys6(vip6)
+    hv6 = endpoint_infos(np.full(len(vip6), 1), np.zeros(len(vip6)), np.zeros(len(vip6)), np.ones(len(vip6)))
+    lxc.keys, lxc.vals = dedup(np.concatenate([lxc.keys, hk, hk6]), np.concatenate([v, hv, hv6]))
+    router = np.zeros(16, np.uint8)
+    router[:8] = (0x20, 0x01, 0x0d, 0xb8, 0xaa, 0xbb, 0, 0)
+    for pk in sc.batches:
+        f = pk.frames
+        m = pk.n
+        et = (f[:, 12].astype(np.uint32) << 8) | f[:, 13]
+        ttl = np.where(rng.random(m) < 0.06, rng.integers(0, 2, m), rng.integers(2, 256, m)).astype(np.uint8)
+        v4 = et == 0x0800
+        v6 = et == 0x86DD
+        f[v4, 22] = ttl[v4]
+        f[v6, 21] = ttl[v6]
+        f[v4, 24:26] = rng.integers(0, 256, (int(v4.sum()), 2))
+        # L4 checksum fields (TCP +16, UDP +6 after an IHL-derived offset), 10% zero
+        l4 = 14 + (f[:, 14] & 0xf).astype(np.int64) * 4
+        pr = f[:, 23]
+        off = np.where(pr == 6, l4 + 16, np.where(pr == 17, l4 + 6, -1))
+        ck = rng.integers(0, 65536, m)
+        ck[rng.random(m) < 0.1] = 0
+        ok = v4 & (off >= 0) & (off + 1 < f.shape[1])
+        rows = np.nonzero(ok)[0]
+        f[rows, off[ok]] = (ck[ok] >> 8).astype(np.uint8)
+        f[rows, off[ok] + 1] = (ck[ok] & 0xff).astype(np.uint8)
+        # IPv6 sources inside ROUTER_IP/64 (derive_sec_ctx takes the flow label)
+        r6 = np.nonzero(v6 & (rng.random(m) < 0.2))[0]
+        f[r6, 22:30] = router[:8]
+        f[r6, 15:18] = rng.integers(0, 256, (len(r6), 3))
+    if not lb_redirect:
+        sc.lb = dict(sc.lb, flags=LB_L3 | LB_L4)
+    sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0 if fixed_secctx is None else 1,
+                 "fixed_secctx": fixed_secctx or 0, "router_ip6": bytes(router)}
     return sc

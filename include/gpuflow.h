@@ -279,6 +279,69 @@ typedef struct gf_ingress_out {
 int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
                                uint32_t now_sec, gf_ingress_out *out, void *stream);
 
+/* ---- full pipeline (BASELINE config 4) ----
+ * One frame through the programs a node attaches in order, each seeing the
+ * frame as the previous one rewrote it:
+ *   bpf_xdp (prefilter)          bpf/bpf_xdp.c:158-184
+ *   bpf_lb  from-netdev          bpf/bpf_lb.c:169-212 (lb4_xlate/lb6_xlate rewrites + checksums)
+ *   bpf_netdev from-netdev       bpf/bpf_netdev.c:160-247, 326-393 (endpoint lookup,
+ *                                ipv{4,6}_local_delivery: TTL/hop limit, MACs, port map)
+ *   cilium_policy[ep->lxc_id]    bpf/bpf_lxc.c:980-1024 handle_policy (as gf_policy_ingress_classify)
+ * The pipeline replaces the per-program entry points of a node for traffic
+ * arriving on the netdev; it has no equivalent call in the reference (the
+ * kernel chains the programs), see DESIGN.md. */
+#define GF_NETDEV_F_FIXED_SECCTX (1u << 0)  /* FIXED_SRC_SECCTX defined */
+typedef struct gf_netdev_cfg {
+    int lxc_map;               /* cilium_lxc (endpoint_key 20 B -> endpoint_info 112 B) */
+    uint32_t flags;            /* GF_NETDEV_F_* */
+    uint32_t fixed_secctx;     /* FIXED_SRC_SECCTX */
+    uint8_t  router_ip6[16];   /* ROUTER_IP (node_config.h), derive_sec_ctx() */
+} gf_netdev_cfg;
+typedef struct gf_pipeline_cfg {
+    int xdp_prog;              /* gf_xdp_prog_load handle, 0 = no XDP program attached */
+    int lb_prog;               /* gf_lb_prog_load handle, 0 = no LB program attached */
+    gf_netdev_cfg netdev;
+    int policy_array;          /* cilium_policy prog array */
+} gf_pipeline_cfg;
+int gf_pipeline_load(const gf_pipeline_cfg *cfg);
+
+typedef struct gf_pipe_batch {
+    gf_frames frames;          /* DEVICE frames; snap_stride must hold every header byte the
+                                  programs read or write (>= l4_off + 18) */
+    const uint8_t  *tc_index;  /* skb->tc_index (DEVICE, may be NULL) */
+    const uint32_t *flow_hash; /* get_hash_recalc(skb) (DEVICE, may be NULL) */
+} gf_pipe_batch;
+
+#define GF_STAGE_XDP    1      /* dropped by bpf_xdp (action = XDP_DROP) */
+#define GF_STAGE_LB     2      /* bpf_lb verdict is final (SHOT, or REDIRECT with LB_REDIRECT) */
+#define GF_STAGE_NETDEV 3      /* bpf_netdev verdict is final (to the stack, SHOT, ICMPv6 reply) */
+#define GF_STAGE_POLICY 4      /* tail-called into cilium_policy: handle_policy's verdict */
+#define GF_PIPE_F_ICMP6_TE  0x20  /* hop limit reached: icmp6_send_time_exceeded (bpf/lib/icmp6.h:313-322);
+                                     action REDIRECT, the reply frame itself is not built */
+#define GF_PIPE_F_LB        0x40  /* translated by lb*_xlate */
+#define GF_PIPE_F_PORTMAP   0x80  /* dport rewritten by map_lxc_in */
+typedef struct gf_pipeline_out {   /* 24 B */
+    uint8_t  stage;       /* GF_STAGE_* */
+    uint8_t  action;      /* XDP_DROP at stage XDP, else TC_ACT_* */
+    uint8_t  reason;      /* drop reason (cb[2]) when SHOT */
+    uint8_t  ct_ret;      /* stage POLICY: CT_NEW/ESTABLISHED/REPLY/RELATED */
+    uint8_t  flags;       /* gf_ingress_out.flags | GF_PIPE_F_* */
+    uint8_t  pad0;
+    uint16_t proxy_port;  /* stage POLICY: raw be16 */
+    uint16_t ifindex_lo;  /* redirect target (LB_REDIRECT ifindex, or handle_policy's) */
+    uint16_t slave;       /* LB: selected slave */
+    uint16_t rev_nat;     /* LB: slave's rev_nat_index */
+    uint16_t dport;       /* raw be16 dport written by lb*_xlate / map_lxc_in (0 = unchanged) */
+    uint32_t daddr4;      /* raw be32 daddr written by lb4_xlate (0 = unchanged) */
+    uint16_t lxc_id;      /* stage POLICY: endpoint tail-called into */
+    uint16_t pad1;
+} gf_pipeline_out;
+/* new_daddr6 (16 B per packet, may be NULL): lb6_xlate's address.  snap_out
+ * (n * snap_stride, may be NULL): every frame as rewritten before handle_policy
+ * (MACs, TTL/hop limit, daddr, dport, IPv4 + L4 checksums). */
+int gf_pipeline_classify(int pipe, const gf_pipe_batch *batch, uint32_t now_sec, gf_pipeline_out *out,
+                         uint8_t *new_daddr6, uint8_t *snap_out, void *stream);
+
 /* ---- per-call statistics (device counter block) ---- */
 #define GF_STATS_WORDS 512
 /* Adds the counters of the next classify calls into `dev_counters`

@@ -526,7 +526,7 @@ void o_xdp_batch(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict) {
 /* ------------------------------------------------------------------ */
 /* Standalone LB, bpf/bpf_lb.c:58-212 + bpf/lib/lb.h                   */
 /* ------------------------------------------------------------------ */
-typedef struct lb_res { uint16_t slave, new_dport, rev_nat; uint32_t new_daddr4; uint8_t nd6[16]; } lb_res;
+typedef struct lb_res { uint16_t slave, new_dport, rev_nat, key_dport; uint32_t new_daddr4; uint8_t nd6[16]; } lb_res;
 
 /* extract_l4_port, bpf/lib/lb.h:191-215 */
 static int extract_l4_port(const skb_t *s, uint8_t nexthdr, int l4_off, uint16_t *port) {
@@ -609,7 +609,7 @@ static int lb_handle_ipv4(const o_lb_cfg *c, const skb_t *s, lb_res *r) {
     uint16_t key_dport, svc_port; memcpy(&key_dport, key + 4, 2); memcpy(&svc_port, svc + 4, 2);
     ret = lb_xlate_checks(c, s, nexthdr, l4_off, key_dport, svc_port, 0, &r->new_dport);
     if (IS_ERR(ret)) return ret;
-    r->slave = slave;
+    r->slave = slave; r->key_dport = key_dport;
     memcpy(&r->new_daddr4, svc, 4);
     memcpy(&r->rev_nat, svc + 8, 2);
     return TC_ACT_REDIRECT;
@@ -639,7 +639,7 @@ static int lb_handle_ipv6(const o_lb_cfg *c, const skb_t *s, lb_res *r) {
     uint16_t key_dport, svc_port; memcpy(&key_dport, key + 16, 2); memcpy(&svc_port, svc + 16, 2);
     ret = lb_xlate_checks(c, s, nexthdr, l4_off, key_dport, svc_port, 1, &r->new_dport);
     if (IS_ERR(ret)) return ret;
-    r->slave = slave; r->rev_nat = rn;
+    r->slave = slave; r->rev_nat = rn; r->key_dport = key_dport;
     memcpy(r->nd6, nd, 16);
     return TC_ACT_REDIRECT;
 }
@@ -647,8 +647,9 @@ static int lb_handle_ipv6(const o_lb_cfg *c, const skb_t *s, lb_res *r) {
 /* from_netdev, bpf/bpf_lb.c:169-212.  The output reports what the
  * translation changed: slave/new_daddr/rev_nat when lb*_xlate ran, new_dport
  * when the L4 port was rewritten; zero otherwise. */
-static void lb_one(const o_lb_cfg *c, const skb_t *s, o_lb_out *o, uint8_t *nd6) {
+static void lb_one_res(const o_lb_cfg *c, const skb_t *s, o_lb_out *o, uint8_t *nd6, lb_res *rout) {
     lb_res r; memset(&r, 0, sizeof(r));
+    if (rout) memset(rout, 0, sizeof *rout);
     memset(o, 0, sizeof *o);
     if (nd6) memset(nd6, 0, 16);
     int ret, v6 = 0;
@@ -671,8 +672,10 @@ static void lb_one(const o_lb_cfg *c, const skb_t *s, o_lb_out *o, uint8_t *nd6)
         o->slave = r.slave; o->new_dport = r.new_dport; o->rev_nat = r.rev_nat;
         if (v6) { if (nd6) memcpy(nd6, r.nd6, 16); }
         else o->new_daddr4 = r.new_daddr4;
+        if (rout) *rout = r;
     }
 }
+static void lb_one(const o_lb_cfg *c, const skb_t *s, o_lb_out *o, uint8_t *nd6) { lb_one_res(c, s, o, nd6, NULL); }
 
 void o_lb_batch(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t *nd6) {
     for (uint32_t i = 0; i < b->n; i++) {
@@ -1061,11 +1064,7 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
 }
 
 /* handle_policy, bpf/bpf_lxc.c:980-1024 */
-static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o) {
-    skb_t s; skb_init(&s, b, i);
-    s.cb[0] = b->src_identity ? b->src_identity[i] : 0;
-    s.cb[1] = b->ifindex ? b->ifindex[i] : 0;
-    uint32_t lxc_id = b->lxc_id ? b->lxc_id[i] : 0;
+static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, uint32_t now, o_ingress_out *o) {
     memset(o, 0, sizeof *o);
     const o_lxc_cfg *c = a->slot[lxc_id & 0xffff];
     if (!c) {                                          /* tail_call miss -> caller's DROP_MISSED_TAIL_CALL */
@@ -1091,6 +1090,12 @@ static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, u
     o->ifindex_lo = (uint16_t)ifindex;
     o->action = ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 }
+static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o) {
+    skb_t s; skb_init(&s, b, i);
+    s.cb[0] = b->src_identity ? b->src_identity[i] : 0;
+    s.cb[1] = b->ifindex ? b->ifindex[i] : 0;
+    handle_policy_skb(a, s, b->lxc_id ? b->lxc_id[i] : 0, now, o);
+}
 
 o_prog_array *o_prog_array_create(void) { return (o_prog_array *)calloc(1, sizeof(o_prog_array)); }
 void o_prog_array_destroy(o_prog_array *a) { free(a); }
@@ -1110,7 +1115,14 @@ typedef struct mt_arg {
     /* ingress partition (RSS-style): owner[], per-slice counts, per-owner lists */
     uint32_t *owner, *cnt, *list, *start;
     int phase;
+    const uint8_t *skip;                /* pipeline: packets that never reach handle_policy */
+    /* pipeline front pass (kind 3) */
+    const o_pipeline_cfg *pc; o_pipeline_out *po; uint8_t *snap_out, *skip_w;
+    uint32_t *secctx, *ifx; uint16_t *lxcid;
 } mt_arg;
+
+static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i, uint8_t *row, o_pipeline_out *o,
+                           uint8_t *nd6, uint32_t *secctx, uint32_t *ifx, uint16_t *lxcid, uint8_t *skip);
 
 static uint32_t pkt_group(const o_batch *b, uint32_t i) {
     const uint8_t *d = b->snap + (size_t)i * b->snap_stride;
@@ -1138,8 +1150,17 @@ static void *mt_worker(void *p) {
             for (uint32_t i = lo; i < hi; i++) m->list[pos[m->owner[i]]++] = i;
         } else {                             /* each owner runs its flow groups in batch order */
             uint32_t a0 = m->start[t], a1 = m->start[T * T + t];
-            for (uint32_t k = a0; k < a1; k++) handle_policy(m->a, b, m->list[k], m->now, &m->out[m->list[k]]);
+            for (uint32_t k = a0; k < a1; k++) {
+                uint32_t i = m->list[k];
+                if (m->skip && m->skip[i]) continue;
+                handle_policy(m->a, b, i, m->now, &m->out[i]);
+            }
         }
+    } else if (m->kind == 3) {
+        for (uint32_t i = lo; i < hi; i++)
+            pipeline_front(m->pc, b, i, m->snap_out + (size_t)i * b->snap_stride, &m->po[i],
+                           m->nd6 ? m->nd6 + 16 * (size_t)i : NULL, &m->secctx[i], &m->ifx[i], &m->lxcid[i],
+                           &m->skip_w[i]);
     } else {
         for (uint32_t i = lo; i < hi; i++) {
             skb_t s; skb_init(&s, b, i);
@@ -1162,12 +1183,13 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
     free(th); free(args);
 }
 
-void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
+static void ingress_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads,
+                       const uint8_t *skip) {
     if (threads < 1) threads = 1;
     if (threads > 1024) threads = 1024;
     uint32_t T = threads;
     mt_arg m; memset(&m, 0, sizeof m);
-    m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0;
+    m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0; m.skip = skip;
     m.owner = (uint32_t *)malloc((size_t)b->n * 4 + 4);
     m.list = (uint32_t *)malloc((size_t)b->n * 4 + 4);
     m.cnt = (uint32_t *)calloc((size_t)T * T, 4);
@@ -1187,6 +1209,9 @@ void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o
     m.phase = 2; run_mt(&m, T);
     free(beg); free(m.owner); free(m.list); free(m.cnt); free(m.start);
 }
+void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
+    ingress_mt(a, b, now, out, threads, NULL);
+}
 void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads) {
     mt_arg m; memset(&m, 0, sizeof m);
     m.b = b; m.xc = cfg; m.verdict = verdict; m.kind = 1;
@@ -1196,4 +1221,292 @@ void o_lb_batch_mt(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t
     mt_arg m; memset(&m, 0, sizeof m);
     m.b = b; m.lc = cfg; m.lo = out; m.nd6 = nd6; m.kind = 2;
     run_mt(&m, threads);
+}
+
+/* ------------------------------------------------------------------ */
+/* Checksum arithmetic of the helpers the header rewrites call: Linux   */
+/* net/core/filter.c bpf_l3_csum_replace / bpf_l4_csum_replace /        */
+/* bpf_csum_diff over include/net/checksum.h (generic forms; not in     */
+/* /root/reference).  Operands are the raw little-endian loads of the   */
+/* network-order bytes, exactly what the BPF programs pass.  The skb is */
+/* taken as not CHECKSUM_PARTIAL (a received frame).                    */
+/* ------------------------------------------------------------------ */
+#define BPF_F_PSEUDO_HDR (1u << 4)
+#define BPF_F_MARK_MANGLED_0 (1u << 5)
+#define ENDPOINT_F_HOST 1u
+#define WORLD_ID 2u
+#define O_NETDEV_TAILCALL 1000
+#define O_NETDEV_ICMP6_TE 1001
+#define O_PIPE_F_ICMP6_TE 0x20
+#define O_PIPE_F_LB 0x40
+#define O_PIPE_F_PORTMAP 0x80
+
+static inline uint32_t ck_add(uint32_t a, uint32_t b) { uint32_t r = a + b; return r + (r < b); }   /* csum_add */
+static inline uint32_t ck_sub(uint32_t a, uint32_t b) { return ck_add(a, ~b); }                   /* csum_sub */
+static inline uint16_t ck_fold(uint32_t x) {                                                      /* csum_fold */
+    x = (x & 0xffff) + (x >> 16); x = (x & 0xffff) + (x >> 16); return (uint16_t)~x;
+}
+static inline uint16_t ck16_add(uint16_t a, uint16_t b) { uint16_t r = (uint16_t)(a + b); return (uint16_t)(r + (r < b)); }
+/* bpf_csum_diff(from, n, to, n, 0): ones' complement sum of ~from and to words */
+static uint32_t ck_diff(const uint8_t *from, const uint8_t *to, int n) {
+    uint32_t x = 0;
+    for (int k = 0; k < n; k += 4) {
+        uint32_t f, t; memcpy(&f, from + k, 4); memcpy(&t, to + k, 4);
+        x = ck_add(x, ~f); x = ck_add(x, t);
+    }
+    return x;
+}
+static uint32_t csum_l4_flags(uint8_t nexthdr) { return nexthdr == IPPROTO_UDP ? BPF_F_MARK_MANGLED_0 : 0; }  /* csum.h:52-55 */
+
+/* writes into the frame copy w (bytes past the snap are not kept) */
+static void wbytes(const skb_t *s, uint8_t *w, uint32_t off, const void *from, uint32_t n) {
+    for (uint32_t k = 0; k < n; k++) if (off + k < s->cap) w[off + k] = ((const uint8_t *)from)[k];
+}
+/* bpf_skb_store_bytes */
+static int skb_store_bytes(const skb_t *s, uint8_t *w, int32_t off, const void *from, uint32_t n) {
+    if (skb_writable(s, off, n) < 0) return -EFAULT;
+    wbytes(s, w, (uint32_t)off, from, n);
+    return 0;
+}
+/* bpf_l3_csum_replace */
+static int l3_csum_replace(const skb_t *s, uint8_t *w, int32_t off, uint32_t from, uint32_t to, uint32_t flags) {
+    if (l4_csum_replace_chk(s, off) < 0) return -EFAULT;      /* offset > 0xffff || odd || past len */
+    uint16_t sum = rd16(s, (uint32_t)off);
+    switch (flags & 0xf) {
+    case 0: if (from) return -EINVAL; sum = ck_fold(ck_add(to, ~(uint32_t)sum)); break;          /* csum_replace_by_diff */
+    case 2: sum = (uint16_t)~ck16_add(ck16_add((uint16_t)~sum, (uint16_t)~(uint16_t)from), (uint16_t)to); break; /* csum_replace2 */
+    case 4: sum = ck_fold(ck_add(ck_sub(~(uint32_t)sum, from), to)); break;                     /* csum_replace4 */
+    default: return -EINVAL;
+    }
+    wbytes(s, w, (uint32_t)off, &sum, 2);
+    return 0;
+}
+/* bpf_l4_csum_replace (inet_proto_csum_replace{4,2,_by_diff}) */
+static int l4_csum_replace(const skb_t *s, uint8_t *w, int32_t off, uint32_t from, uint32_t to, uint32_t flags) {
+    if (l4_csum_replace_chk(s, off) < 0) return -EFAULT;
+    uint16_t sum = rd16(s, (uint32_t)off);
+    int mmzero = (flags & BPF_F_MARK_MANGLED_0) != 0;
+    if (mmzero && !sum) return 0;
+    switch (flags & 0xf) {
+    case 0: if (from) return -EINVAL; sum = ck_fold(ck_add(to, ~(uint32_t)sum)); break;
+    case 2: case 4: sum = ck_fold(ck_add(ck_sub(~(uint32_t)sum, from), to)); break;
+    default: return -EINVAL;
+    }
+    if (mmzero && !sum) sum = 0xffff;                         /* CSUM_MANGLED_0 */
+    wbytes(s, w, (uint32_t)off, &sum, 2);
+    return 0;
+}
+
+/* lb4_xlate / lb6_xlate writes (bpf/lib/lb.h:615-659, 397-423) for a
+ * translation lb_one_res accepted (its checks already passed, so every
+ * helper below succeeds). */
+static void lb_rewrite(const skb_t *s, uint8_t *w, const lb_res *r, int v6) {
+    uint8_t nexthdr;
+    int l4_off;
+    uint8_t old[16], nw[16];
+    uint32_t sum;
+    if (!v6) {
+        nexthdr = skb_byte(s, 23);
+        l4_off = ETH_HLEN + (skb_byte(s, 14) & 0xf) * 4;
+        for (int k = 0; k < 4; k++) old[k] = skb_byte(s, 30 + k);
+        memcpy(nw, &r->new_daddr4, 4);
+        wbytes(s, w, 30, nw, 4);                                        /* daddr */
+        sum = ck_diff(old, nw, 4);
+        l3_csum_replace(s, w, ETH_HLEN + 10, 0, sum, 0);
+    } else {
+        nexthdr = skb_byte(s, 20);
+        l4_off = ETH_HLEN + ipv6_hdrlen(s, ETH_HLEN, &nexthdr);
+        for (int k = 0; k < 16; k++) old[k] = skb_byte(s, 38 + k);
+        memcpy(nw, r->nd6, 16);
+        wbytes(s, w, 38, nw, 16);                                       /* ipv6_store_daddr */
+        sum = ck_diff(old, nw, 16);
+    }
+    uint16_t co = csum_l4_offset(nexthdr);
+    uint32_t fl = csum_l4_flags(nexthdr);
+    if (co || v6) l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl);
+    if (r->new_dport) {                                                 /* l4_modify_port, bpf/lib/l4.h:50-60 */
+        l4_csum_replace(s, w, l4_off + co, r->key_dport, r->new_dport, 2 | fl);
+        wbytes(s, w, (uint32_t)l4_off + 2, &r->new_dport, 2);
+    }
+}
+
+/* map_lxc_in, bpf/lib/l3.h:71-104, with l4_port_map_in (bpf/lib/l4.h:62-88):
+ * every entry is compared against the dport loaded once at the start. */
+static int map_lxc_in(const skb_t *s, uint8_t *w, int l4_off, const uint8_t *ep, uint8_t nexthdr, int *mapped,
+                      uint16_t *new_dport) {
+    uint16_t to0; memcpy(&to0, ep + 48 + 2, 2);
+    if (!to0) return 0;
+    if (nexthdr != IPPROTO_TCP && nexthdr != IPPROTO_UDP) return 0;
+    uint16_t dport;
+    if (skb_load_bytes(s, l4_off + 2, &dport, 2) < 0) return DROP_INVALID;
+    uint16_t co = csum_l4_offset(nexthdr);
+    uint32_t fl = csum_l4_flags(nexthdr);
+    for (int i = 0; i < 16; i++) {                                      /* PORTMAP_MAX */
+        uint16_t from, to;
+        memcpy(&from, ep + 48 + 4 * i, 2); memcpy(&to, ep + 48 + 4 * i + 2, 2);
+        if (!to || !from) break;
+        if (from != dport) continue;
+        if (l4_csum_replace(s, w, l4_off + co, dport, to, 2 | fl) < 0) return DROP_CSUM_L4;
+        if (skb_store_bytes(s, w, l4_off + 2, &to, 2) < 0) return DROP_WRITE_ERROR;
+        *mapped = 1; *new_dport = to;
+    }
+    return 0;
+}
+
+static const uint8_t *endpoint_val4(om_map *lxc, uint32_t daddr) {
+    uint8_t key[20] = {0};
+    memcpy(key, &daddr, 4); key[16] = 1;
+    return om_lookup_ptr(lxc, key);
+}
+static const uint8_t *endpoint_val6(om_map *lxc, const uint8_t *daddr) {
+    uint8_t key[20] = {0};
+    memcpy(key, daddr, 16); key[16] = 2;
+    return om_lookup_ptr(lxc, key);
+}
+
+typedef struct nd_res { uint32_t secctx, ifindex; uint16_t lxc_id, new_dport; int mapped; } nd_res;
+
+/* the common tail of ipv{4,6}_local_delivery, bpf/lib/l3.h:106-168: MACs, port map, cb[], tail call */
+static int local_delivery_tail(const skb_t *s, uint8_t *w, int l4_off, const uint8_t *ep, uint8_t nexthdr,
+                               uint32_t seclabel, nd_res *r) {
+    if (skb_store_bytes(s, w, 6, ep + 24, 6) < 0) return DROP_WRITE_ERROR;   /* eth_store_saddr(node_mac) */
+    if (skb_store_bytes(s, w, 0, ep + 16, 6) < 0) return DROP_WRITE_ERROR;   /* eth_store_daddr(mac) */
+    int ret = map_lxc_in(s, w, l4_off, ep, nexthdr, &r->mapped, &r->new_dport);
+    if (IS_ERR(ret)) return ret;
+    r->secctx = seclabel;                                                   /* cb[CB_SRC_LABEL] */
+    memcpy(&r->ifindex, ep, 4);                                             /* cb[CB_IFINDEX] */
+    memcpy(&r->lxc_id, ep + 6, 2);                                          /* tail_call(cilium_policy, lxc_id) */
+    return O_NETDEV_TAILCALL;
+}
+
+/* handle_ipv4 of bpf/bpf_netdev.c:326-393 (no FROM_HOST, no ENCAP_IFINDEX)
+ * + ipv4_local_delivery (bpf/lib/l3.h:136-168) + ipv4_l3 / ipv4_dec_ttl
+ * (l3.h:54-70, bpf/lib/ipv4.h:30-43) */
+static int netdev_ipv4(const o_netdev_cfg *c, const skb_t *s, uint8_t *w, nd_res *r) {
+    if (s->len < ETH_HLEN + 20) return DROP_INVALID;
+    int l4_off = ETH_HLEN + (skb_byte(s, 14) & 0xf) * 4;
+    uint32_t secctx = (c->flags & O_NETDEV_F_FIXED_SECCTX) ? c->fixed_secctx : WORLD_ID;  /* derive_ipv4_sec_ctx */
+    uint8_t nexthdr = skb_byte(s, 23);
+    const uint8_t *ep = endpoint_val4(c->lxc_map, rd32(s, 30));
+    if (!ep) return TC_ACT_OK;
+    uint32_t epf; memcpy(&epf, ep + 8, 4);
+    if (epf & ENDPOINT_F_HOST) return TC_ACT_OK;
+    uint8_t ttl = skb_byte(s, 22);
+    if (ttl <= 1) return DROP_INVALID;
+    uint8_t nt = (uint8_t)(ttl - 1);
+    l3_csum_replace(s, w, ETH_HLEN + 10, ttl, nt, 2);
+    skb_store_bytes(s, w, ETH_HLEN + 8, &nt, 1);
+    return local_delivery_tail(s, w, l4_off, ep, nexthdr, secctx, r);
+}
+
+/* handle_ipv6 of bpf/bpf_netdev.c:160-247 (no HANDLE_NS, FROM_HOST,
+ * ENCAP_IFINDEX) + derive_sec_ctx (:50-64) + ipv6_local_delivery
+ * (bpf/lib/l3.h:106-134) + ipv6_l3 / ipv6_dec_hoplimit (l3.h:31-52,
+ * bpf/lib/ipv6.h:178-193) */
+static int netdev_ipv6(const o_netdev_cfg *c, const skb_t *s, uint8_t *w, nd_res *r) {
+    if (s->len < ETH_HLEN + 40) return DROP_INVALID;
+    uint8_t nexthdr = skb_byte(s, 20);
+    int l4_off = ETH_HLEN + ipv6_hdrlen(s, ETH_HLEN, &nexthdr);
+    uint32_t fl = WORLD_ID;
+    if (c->flags & O_NETDEV_F_FIXED_SECCTX) fl = c->fixed_secctx;
+    else {
+        int match = 1;
+        for (int k = 0; k < 8; k++) if (skb_byte(s, 22 + k) != c->router_ip6[k]) match = 0;  /* ipv6_match_prefix_64 */
+        if (match) fl = bswap32(rd32(s, 14) & bswap32(0x000FFFFFu));                           /* flow label */
+    }
+    uint8_t d6[16];
+    for (int k = 0; k < 16; k++) d6[k] = skb_byte(s, 38 + k);
+    const uint8_t *ep = endpoint_val6(c->lxc_map, d6);
+    if (!ep) return TC_ACT_OK;
+    uint32_t epf; memcpy(&epf, ep + 8, 4);
+    if (epf & ENDPOINT_F_HOST) return TC_ACT_OK;
+    uint8_t hl = skb_byte(s, ETH_HLEN + 7);
+    if (hl <= 1) return O_NETDEV_ICMP6_TE;              /* icmp6_send_time_exceeded, bpf/lib/icmp6.h:313-322 */
+    uint8_t nh = (uint8_t)(hl - 1);
+    if (skb_store_bytes(s, w, ETH_HLEN + 7, &nh, 1) < 0) return DROP_WRITE_ERROR;
+    return local_delivery_tail(s, w, l4_off, ep, nexthdr, fl, r);
+}
+
+/* One packet through bpf_xdp -> bpf_lb from-netdev -> bpf_netdev from-netdev
+ * up to the cilium_policy tail call.  row receives the frame as rewritten. */
+static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i, uint8_t *row, o_pipeline_out *o,
+                           uint8_t *nd6, uint32_t *secctx, uint32_t *ifx, uint16_t *lxcid, uint8_t *skip) {
+    skb_t s; skb_init(&s, b, i);
+    memcpy(row, s.data, b->snap_stride);
+    s.data = row;
+    memset(o, 0, sizeof *o);
+    if (nd6) memset(nd6, 0, 16);
+    *skip = 1; *secctx = 0; *ifx = 0; *lxcid = 0;
+    if (c->xdp && xdp_start(c->xdp, &s) == XDP_DROP) { o->stage = 1; o->action = XDP_DROP; return; }
+    if (c->lb) {
+        o_lb_out lo; lb_res r; uint8_t n6[16];
+        lb_one_res(c->lb, &s, &lo, n6, &r);
+        if (lo.action == TC_ACT_SHOT) { o->stage = 2; o->action = TC_ACT_SHOT; o->reason = lo.reason; return; }
+        if (lo.slave) {
+            int v6 = s.protocol == 0x86DD;
+            lb_rewrite(&s, row, &r, v6);
+            o->slave = lo.slave; o->rev_nat = lo.rev_nat; o->dport = lo.new_dport; o->daddr4 = lo.new_daddr4;
+            o->flags |= O_PIPE_F_LB;
+            if (v6 && nd6) memcpy(nd6, n6, 16);
+        }
+        if (lo.action == TC_ACT_REDIRECT) {
+            o->stage = 2; o->action = TC_ACT_REDIRECT; o->ifindex_lo = (uint16_t)c->lb->redirect_ifindex;
+            return;
+        }
+    }
+    nd_res nr; memset(&nr, 0, sizeof nr);
+    int ret;
+    if (s.protocol == 0x86DD) ret = netdev_ipv6(c->netdev, &s, row, &nr);
+    else if (s.protocol == 0x0800) ret = netdev_ipv4(c->netdev, &s, row, &nr);   /* tail_handle_ipv4 */
+    else ret = TC_ACT_OK;
+    if (nr.mapped) { o->flags |= O_PIPE_F_PORTMAP; o->dport = nr.new_dport; }
+    o->stage = 3;
+    if (ret == O_NETDEV_TAILCALL) {
+        o->stage = 4; o->lxc_id = nr.lxc_id;
+        *skip = 0; *secctx = nr.secctx; *ifx = nr.ifindex; *lxcid = nr.lxc_id;
+    } else if (ret == O_NETDEV_ICMP6_TE) {              /* the reply goes back out: redirect */
+        o->action = TC_ACT_REDIRECT; o->flags |= O_PIPE_F_ICMP6_TE;
+    } else if (IS_ERR(ret)) {
+        o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret);
+    } else {
+        o->action = (uint8_t)ret;
+    }
+}
+
+void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now, o_pipeline_out *out,
+                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads) {
+    if (threads < 1) threads = 1;
+    uint32_t n = b->n;
+    uint8_t *snap = snap_out ? snap_out : (uint8_t *)malloc((size_t)n * b->snap_stride + 1);
+    uint8_t *skip = (uint8_t *)malloc((size_t)n + 1);
+    uint32_t *secctx = (uint32_t *)malloc((size_t)n * 4 + 4), *ifx = (uint32_t *)malloc((size_t)n * 4 + 4);
+    uint16_t *lxcid = (uint16_t *)malloc((size_t)n * 2 + 2);
+    o_ingress_out *ing = (o_ingress_out *)calloc((size_t)n + 1, sizeof(o_ingress_out));
+    mt_arg m; memset(&m, 0, sizeof m);
+    m.b = b; m.kind = 3; m.pc = c; m.po = out; m.nd6 = nd6; m.snap_out = snap; m.skip_w = skip;
+    m.secctx = secctx; m.ifx = ifx; m.lxcid = lxcid;
+    run_mt(&m, threads);
+    if (c->policy) {
+        /* handle_policy over the rewritten frames, flow groups of the rewritten addresses */
+        o_batch b2 = *b;
+        b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+        if (threads == 1) {
+            for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(c->policy, &b2, i, now, &ing[i]);
+        } else {
+            ingress_mt(c->policy, &b2, now, ing, threads, skip);
+        }
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        if (skip[i]) continue;
+        o_pipeline_out *o = &out[i];
+        if (!c->policy) { o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL); continue; }
+        o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
+        o->flags |= ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
+    }
+    if (!snap_out) free(snap);
+    free(skip); free(secctx); free(ifx); free(lxcid); free(ing);
+}
+void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now, o_pipeline_out *out,
+                      uint8_t *nd6, uint8_t *snap_out) {
+    o_pipeline_batch_mt(c, b, now, out, nd6, snap_out, 1);
 }

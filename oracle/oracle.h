@@ -115,6 +115,35 @@ void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now_se
 void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads);
 void o_lb_batch_mt(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t *nd6, uint32_t threads);
 
+/* ---------------- full pipeline (BASELINE config 4) ----------------
+ * bpf_xdp -> bpf_lb from-netdev -> bpf_netdev from-netdev (endpoint
+ * delivery) -> cilium_policy tail call (handle_policy), each stage on the
+ * frame as the previous one rewrote it (== gf_pipeline_classify). */
+#define O_NETDEV_F_FIXED_SECCTX 1u
+typedef struct o_netdev_cfg {
+    om_map *lxc_map;
+    uint32_t flags, fixed_secctx;
+    uint8_t router_ip6[16];
+} o_netdev_cfg;
+typedef struct o_pipeline_cfg {
+    const o_xdp_cfg *xdp;           /* NULL: no XDP stage */
+    const o_lb_cfg *lb;             /* NULL: no LB stage */
+    const o_netdev_cfg *netdev;
+    const o_prog_array *policy;
+} o_pipeline_cfg;
+typedef struct o_pipeline_out {     /* == gf_pipeline_out (24 B) */
+    uint8_t stage, action, reason, ct_ret, flags, pad0;
+    uint16_t proxy_port, ifindex_lo, slave, rev_nat, dport;
+    uint32_t daddr4;
+    uint16_t lxc_id, pad1;
+} o_pipeline_out;
+/* snap_out (n * snap_stride, may be NULL) receives each frame as rewritten
+ * before handle_policy; nd6 (16 B per packet, may be NULL) the LB v6 address. */
+void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_sec, o_pipeline_out *out,
+                      uint8_t *nd6, uint8_t *snap_out);
+void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_sec, o_pipeline_out *out,
+                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads);
+
 /* Shard of a CT key (unordered address pair), exposed for pre-population. */
 uint32_t o_ct_pair_hash4(uint32_t a, uint32_t b);
 uint32_t o_ct_pair_hash6(const uint8_t *a, const uint8_t *b);

@@ -45,6 +45,15 @@ class o_cols(C.Structure):
                 ("l4w0", VP), ("l4w3", VP), ("saddr6", VP), ("daddr6", VP)]
 
 
+class o_netdev_cfg(C.Structure):
+    _fields_ = [("lxc_map", VP), ("flags", C.c_uint32), ("fixed_secctx", C.c_uint32), ("router_ip6", C.c_uint8 * 16)]
+
+
+class o_pipeline_cfg(C.Structure):
+    _fields_ = [("xdp", C.POINTER(o_xdp_cfg)), ("lb", C.POINTER(o_lb_cfg)), ("netdev", C.POINTER(o_netdev_cfg)),
+                ("policy", VP)]
+
+
 def _s(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -69,6 +78,7 @@ _s("o_prog_array_set", None, VP, C.c_uint32, C.POINTER(o_lxc_cfg))
 _s("o_set_node", None, C.POINTER(o_node_cfg))
 _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
+_s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
 _s("o_lpm4_iter_lookup", C.c_int, C.c_uint32, VP, C.c_int, C.c_uint32)
@@ -78,6 +88,9 @@ LB_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("slave", "<u2"), ("new_d
                    ("rev_nat", "<u2"), ("new_daddr4", "<u4")])
 ING_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
                     ("proxy_port", "<u2"), ("ifindex_lo", "<u2")])
+PIPE_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
+                     ("pad0", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
+                     ("rev_nat", "<u2"), ("dport", "<u2"), ("daddr4", "<u4"), ("lxc_id", "<u2"), ("pad1", "<u2")])
 
 
 class OMap:
@@ -193,3 +206,13 @@ def ingress(prog_array, b, now, threads=1):
     else:
         lib.o_ingress_batch(prog_array, C.byref(b), now, out.ctypes.data)
     return out
+
+
+def pipeline(cfg, b, now, threads=1):
+    """o_pipeline_batch_mt: returns (records, new_daddr6, rewritten snaps)."""
+    out = np.zeros(b.n, PIPE_OUT)
+    nd6 = np.zeros((b.n, 16), np.uint8)
+    snap = np.zeros((b.n, b.snap_stride), np.uint8)
+    lib.o_pipeline_batch_mt(C.byref(cfg), C.byref(b), now, out.ctypes.data, nd6.ctypes.data, snap.ctypes.data,
+                            max(1, threads))
+    return out, nd6, snap

@@ -27,6 +27,7 @@ class OracleDP:
             self.lb_cfg = O.o_lb_cfg(p(sc.lb.get("lb4")), p(sc.lb.get("lb6")), sc.lb["flags"],
                                      sc.lb.get("redirect_ifindex", 0))
         self.arr = None
+        self._pipe = None
         self.cfgs = []
         if sc.lxc:
             self.arr = O.lib.o_prog_array_create()
@@ -61,6 +62,16 @@ class OracleDP:
 
     def ingress(self, pk, now, threads=1):
         return O.ingress(self.arr, self.batch(pk), now, threads)
+
+    def pipeline(self, pk, now, threads=1):
+        if self._pipe is None:
+            nd = self.sc.netdev
+            self._nd = O.o_netdev_cfg(self.m[nd["lxc_map"]].ptr, nd.get("flags", 0), nd.get("fixed_secctx", 0),
+                                      (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
+            self._pipe = O.o_pipeline_cfg(C.pointer(self.xdp_cfg) if self.xdp_cfg is not None else None,
+                                          C.pointer(self.lb_cfg) if self.lb_cfg is not None else None,
+                                          C.pointer(self._nd), self.arr)
+        return O.pipeline(self._pipe, self.batch(pk), now, threads)
 
     def dump(self, name):
         return self.m[name].dump()
