@@ -46,7 +46,8 @@ def pair_rank(raddr, ep_ip, world):
 
 class Stream:
     def __init__(self, pairs, rank=0, world=1, flows_per_step=4 << 20, device="cuda", seed=0xC1D40002,
-                 reply_frac=0.05, related_frac=0.20, unk_frac=0.005, trunc_frac=0.005, skip_proxy_frac=0.01):
+                 reply_frac=0.05, related_frac=0.20, unk_frac=0.005, trunc_frac=0.005, skip_proxy_frac=0.01,
+                 vip_ip=None, vip_frac=0.3):
         import torch
         self.torch = torch
         self.device = device
@@ -64,6 +65,12 @@ class Stream:
         self.p_port1 = T(pairs["port1"][own], np.int64)
         self.p_port2 = T(pairs["port2"][own], np.int64)
         self.np_ = len(own)
+        # config 4: pairs whose flows address the endpoint's service VIP (bpf_lb translates it back)
+        self.p_vip = None
+        if vip_ip is not None:
+            self.p_vip = T(_bswap32(np.asarray(vip_ip)[pe].astype(np.int64)), np.int64)
+            self.p_usevip = T((synth.mix32(own.astype(np.uint64) * np.uint64(2654435761)) % 1000) < int(vip_frac * 1000),
+                              np.bool_)
         self.fr = (int(reply_frac * 1000), int(related_frac * 1000), int(unk_frac * 10000), int(trunc_frac * 10000),
                    int(skip_proxy_frac * 1000))
 
@@ -137,12 +144,15 @@ class Stream:
         l4w0 = torch.where(length >= 34 + 4, l4w0, torch.where(length >= 35, l4w0 & ((1 << (8 * (length - 34).clamp(0, 4))) - 1), 0))
         l4w3 = torch.where(length >= 48, l4w3, torch.where(length == 47, l4w3 & 0xff, 0))
         hdr_ok = length >= 34
+        daddr = self.p_daddr[p]
+        if self.p_vip is not None:
+            daddr = torch.where(self.p_usevip[p] & is_tu, self.p_vip[p], daddr)
         i32 = lambda x: x.to(torch.int64).where(x < (1 << 31), x - (1 << 32)).to(torch.int32)
         cols = {
             "len": length.to(torch.int32),
             "ethertype": torch.where(length >= 14, 0x0800, 0).to(torch.int16),
             "saddr4": i32(torch.where(hdr_ok, self.p_saddr[p], 0)),
-            "daddr4": i32(torch.where(hdr_ok, self.p_daddr[p], 0)),
+            "daddr4": i32(torch.where(hdr_ok, daddr, 0)),
             "proto": torch.where(hdr_ok, proto, 0).to(torch.uint8),
             "l4_off": torch.where(hdr_ok, 34, 0).to(torch.int16),
             "l4w0": i32(torch.where(hdr_ok, l4w0, 0)),
@@ -167,4 +177,88 @@ def to_frames(cols_np, stride=64):
     f[:, 30:34] = cols_np["daddr4"].astype(np.uint32).view(np.uint8).reshape(n, 4)
     f[:, 34:38] = cols_np["l4w0"].astype(np.uint32).view(np.uint8).reshape(n, 4)
     f[:, 46:48] = cols_np["l4w3"].astype(np.uint16).view(np.uint8).reshape(n, 2)
+    return f, lens
+
+
+def device_frames(cols, stride=64, ttl=64):
+    """Raw Ethernet/IPv4 frames on the device whose parse yields exactly these
+    columns (torch twin of to_frames, TTL set): the input of the full pipeline."""
+    import torch
+    n = cols["len"].shape[0]
+    f = torch.zeros((n, stride // 4), dtype=torch.int32, device=cols["len"].device)
+    u = lambda t: t.to(torch.int64) & 0xFFFFFFFF
+    i32 = lambda x: torch.where(x >= (1 << 31), x - (1 << 32), x).to(torch.int32)
+    sa, da, w0 = u(cols["saddr4"]), u(cols["daddr4"]), u(cols["l4w0"])
+    w3 = cols["l4w3"].to(torch.int64) & 0xFFFF
+    pr = cols["proto"].to(torch.int64)
+    f[:, 3] = 0x00450008                                           # ethertype 0x0800, ver/IHL 0x45
+    f[:, 5] = i32((ttl << 16) | (pr << 24))                        # TTL, protocol
+    f[:, 6] = i32((sa & 0xFFFF) << 16)                             # saddr bytes 26..27
+    f[:, 7] = i32((sa >> 16) | ((da & 0xFFFF) << 16))
+    f[:, 8] = i32((da >> 16) | ((w0 & 0xFFFF) << 16))
+    f[:, 9] = i32(w0 >> 16)
+    f[:, 11] = i32(w3 << 16)                                       # TCP flags word (bytes 46..47)
+    return f.view(torch.uint8).reshape(n, stride), cols["len"]
+
+
+class Stream6(Stream):
+    """Config 5: the same flow model over IPv6 (remote 2001:db8::<v4 remote>,
+    endpoints f00d::<v4 endpoint>; ICMP flows are ICMPv6 echo / DEST_UNREACH),
+    no pre-inserted reply entries."""
+
+    def __init__(self, pairs, **kw):
+        kw.setdefault("reply_frac", 0.0)
+        super().__init__(pairs, **kw)
+
+    def step(self, s):
+        torch = self.torch
+        cols, p, n = super().step(s)
+        length = cols["len"].to(torch.int64) + 20                     # 40-B header instead of 20
+        proto = cols["proto"].to(torch.int64)
+        w0 = cols["l4w0"].to(torch.int64) & 0xFFFFFFFF
+        icmp = proto == ICMP
+        # ICMP echo (8) -> ICMPv6 echo request (128), DEST_UNREACH (3) -> ICMPv6 DEST_UNREACH (1)
+        w0 = torch.where(icmp, torch.where((w0 & 0xff) == 3, 1, 128), w0)
+        proto = torch.where(icmp, 58, proto)
+        hdr_ok = length >= 54
+        avail = (length - 54).clamp(0, 4)                             # the parser zero-fills past len
+        w0 = torch.where(hdr_ok, w0 & ((1 << (8 * avail)) - 1), 0)
+        w3 = cols["l4w3"].to(torch.int64) & 0xFFFF
+        w3 = torch.where(length >= 68, w3, torch.where(length == 67, w3 & 0xff, 0))
+        s6 = torch.zeros((n, 4), dtype=torch.int32, device=self.device)
+        d6 = torch.zeros((n, 4), dtype=torch.int32, device=self.device)
+        s6[:, 0] = 0xb80d0120 - (1 << 32)                            # 2001:db8::
+        s6[:, 3] = self.p_saddr[p].to(torch.int64).where(self.p_saddr[p] < (1 << 31), self.p_saddr[p] - (1 << 32)).to(torch.int32)
+        d6[:, 0] = 0x00000df0                                        # f00d::
+        d6[:, 3] = self.p_daddr[p].to(torch.int64).where(self.p_daddr[p] < (1 << 31), self.p_daddr[p] - (1 << 32)).to(torch.int32)
+        z = lambda t: torch.where(hdr_ok[:, None], t, 0)
+        i32 = lambda x: torch.where(x >= (1 << 31), x - (1 << 32), x).to(torch.int32)
+        cols.update({
+            "len": length.to(torch.int32),
+            "ethertype": torch.where(length >= 14, 0x86DD - (1 << 16), 0).to(torch.int16),
+            "saddr4": torch.zeros(n, dtype=torch.int32, device=self.device),
+            "daddr4": torch.zeros(n, dtype=torch.int32, device=self.device),
+            "proto": torch.where(hdr_ok, proto, 0).to(torch.uint8),
+            "l4_off": torch.where(hdr_ok, 54, 0).to(torch.int16),
+            "l4w0": i32(w0),
+            "l4w3": torch.where(w3 >= (1 << 15), w3 - (1 << 16), w3).to(torch.int16),
+            "saddr6": z(s6).view(torch.uint8).reshape(n, 16),
+            "daddr6": z(d6).view(torch.uint8).reshape(n, 16),
+        })
+        return cols, p, n
+
+
+def to_frames6(cols_np, stride=96):
+    """Raw Ethernet/IPv6 frames whose parse yields exactly these Stream6 columns."""
+    n = len(cols_np["len"])
+    lens = cols_np["len"].astype(np.uint32)
+    f = np.zeros((n, stride), np.uint8)
+    f[:, 12], f[:, 13] = 0x86, 0xDD
+    f[:, 14] = 0x60
+    f[:, 20] = cols_np["proto"]
+    f[:, 21] = 64
+    f[:, 22:38] = cols_np["saddr6"]
+    f[:, 38:54] = cols_np["daddr6"]
+    f[:, 54:58] = cols_np["l4w0"].astype(np.uint32).view(np.uint8).reshape(n, 4)
+    f[:, 66:68] = cols_np["l4w3"].astype(np.uint16).view(np.uint8).reshape(n, 2)
     return f, lens

@@ -502,7 +502,7 @@ def _interleave(rng, n_flows, k, start_spread):
 
 
 def config2_tables(n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000, n_l4=4000, n_wc=32, n_cidr=128,
-                   seed=0xC1D40002, ct_max=48_000_000, proxy_frac=0.10, now=100_000):
+                   seed=0xC1D40002, ct_max=48_000_000, proxy_frac=0.10, now=100_000, cls_p=(0.45, 0.30, 0.15, 0.10)):
     """Tables of BASELINE config 2 (256 endpoints, 4k identities, per-endpoint
     policy/CIDR maps, global CT) and the address-pair population.  Returns
     (scenario, pairs, rng)."""
@@ -514,7 +514,7 @@ def config2_tables(n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000, n_l4=4000, 
     user_ids = 256 + np.arange(n_ids)
     # ---- pairs
     pe = rng.integers(0, n_ep, n_pairs)
-    cls = rng.choice(4, n_pairs, p=[0.45, 0.30, 0.15, 0.10])          # A: L3, B: L4, W: world/CIDR, D: deny
+    cls = rng.choice(4, n_pairs, p=list(cls_p))                        # A: L3, B: L4, W: world/CIDR, D: deny
     pid = user_ids[rng.integers(0, n_ids, n_pairs)].astype(np.uint32)
     pid[cls == 2] = 2                                                   # WORLD_ID
     port1 = SERVICE_PORTS[rng.integers(0, len(SERVICE_PORTS), n_pairs)]
@@ -924,3 +924,58 @@ def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed
     sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0 if fixed_secctx is None else 1,
                  "fixed_secctx": fixed_secctx or 0, "router_ip6": bytes(router)}
     return sc
+
+
+# ------------------------------------------------------------------ config 4: full pipeline tables
+def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000, seed=0xC1D40004, **kw):
+    """BASELINE config 4 / SURVEY §8(d): the tables of configs 1-3 on one node,
+    composed as bpf_xdp -> bpf_lb -> bpf_netdev -> handle_policy.  Config 2's
+    endpoints/policies/CT; config 1's prefilter (10k LPM prefixes + 2k /32s);
+    a service VIP per endpoint for each of SERVICE_PORTS (one backend: the
+    endpoint itself, 30% on another port), present in cilium_lxc as host
+    entries so the prefilter's endpoint check passes them.  Returns
+    (scenario, pairs, vip_ip[n_ep])."""
+    # traffic arriving on the netdev carries WORLD_ID (derive_ipv4_sec_ctx, bpf_netdev.c:249-261):
+    # most pairs are world peers, admitted by the endpoints' CIDR / L4-wildcard rules
+    kw.setdefault("cls_p", (0.05, 0.10, 0.75, 0.10))
+    sc, P, rng = config2_tables(n_pairs=n_pairs, ct_max=ct_max, **kw)
+    rng4 = np.random.default_rng(seed)
+    n_ep = len(P["ep_ip"])
+    # prefilter: prefixes outside the pair populations' ranges except for a few
+    u = rng4.random(n_lpm)
+    plen = np.where(u < 0.55, 24, np.where(u < 0.85, rng4.integers(16, 24, n_lpm), rng4.integers(25, 32, n_lpm)))
+    net = (ip4("20.0.0.0") + rng4.integers(0, 1 << 28, n_lpm)).astype(np.uint32)
+    hit = rng4.random(n_lpm) < 0.02                     # ~2% of prefixes cover pair addresses
+    net = np.where(hit, P["raddr"][rng4.integers(0, n_pairs, n_lpm)], net).astype(np.uint32)
+    mask = ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF).astype(np.uint32)
+    k, v = lpm_dedup(lpm4_keys(plen, net & mask), np.ones((n_lpm, 1), np.uint8), 32)
+    sc.add_map(MapSpec("cilium_cidr_v4_dyn", LPM, 8, 1, 65536, NO_PREALLOC, k, v))
+    fix = np.concatenate([(ip4("20.0.0.0") + rng4.integers(0, 1 << 28, n_fix - 64)).astype(np.uint32),
+                          P["raddr"][rng4.integers(0, n_pairs, 64)]])
+    k, v = dedup(lpm4_keys(np.full(n_fix, 32), fix), np.ones((n_fix, 1), np.uint8))
+    sc.add_map(MapSpec("cilium_cidr_v4_fix", HASH, 8, 1, 20971520, NO_PREALLOC, k, v))
+    vip = (ip4("10.96.0.0") + 1 + np.arange(n_ep)).astype(np.uint32)
+    keys = np.concatenate([endpoint_keys4(P["ep_ip"]), endpoint_keys4(vip)])
+    vals = endpoint_infos(np.concatenate([P["ifidx"], np.zeros(n_ep)]),
+                          np.concatenate([256 + np.arange(n_ep), np.ones(n_ep)]),
+                          np.concatenate([P["lxc_id"], np.zeros(n_ep)]),
+                          np.concatenate([np.zeros(n_ep), np.ones(n_ep)]).astype(np.uint32))
+    vals[:n_ep, 16:22] = rng4.integers(0, 256, (n_ep, 6))
+    vals[:n_ep, 24:30] = rng4.integers(0, 256, (n_ep, 6))
+    sc.add_map(MapSpec("cilium_lxc", HASH, 20, 112, 65535, 0, keys, vals))
+    sp = SERVICE_PORTS
+    ns = n_ep * len(sp)
+    sv_vip = np.repeat(vip, len(sp))
+    sv_port = np.tile(sp, n_ep)
+    sv_ep = np.repeat(P["ep_ip"], len(sp))
+    be_port = np.where(rng4.random(ns) < 0.3, np.roll(sv_port, 1), sv_port).astype(np.uint32)
+    keys = np.concatenate([lb4_keys(sv_vip, sv_port, np.zeros(ns)), lb4_keys(sv_vip, sv_port, np.ones(ns))])
+    vals = np.concatenate([lb4_vals(np.zeros(ns), np.zeros(ns), np.ones(ns), np.zeros(ns)),
+                           lb4_vals(sv_ep, be_port, np.zeros(ns), (np.arange(ns) % 256) + 1)])
+    sc.add_map(MapSpec("cilium_lb4_services", HASH, 8, 12, 65536, 0, keys, vals))
+    sc.xdp = {"cidr4_hmap": "cilium_cidr_v4_fix", "cidr4_lmap": "cilium_cidr_v4_dyn", "cidr6_hmap": None,
+              "cidr6_lmap": None, "lxc_map": "cilium_lxc"}
+    sc.lb = {"lb4": "cilium_lb4_services", "lb6": None, "flags": LB_L3 | LB_L4, "redirect_ifindex": 0}
+    sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0}
+    sc.name = "config4_pipeline"
+    return sc, P, vip
