@@ -17,6 +17,7 @@
 #include <rocprim/iterator/discard_iterator.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
+#include <functional>
 #include <string.h>
 
 using namespace gf;
@@ -81,65 +82,108 @@ __device__ __forceinline__ uint32_t fbyte(const uint8_t *f, uint32_t cap, uint32
     return off < cap ? f[off] : 0u;
 }
 
+// Header values of one frame, as the BPF programs hold them after their loads
+// (the rules of gf_parse_frames; oracle.c o_parse_batch).
+struct PktHdr {
+    uint32_t et, sa, da, w0, w3, proto;
+    int l4;
+    uint32_t s6[4], d6[4];
+};
+__device__ __forceinline__ void parse_row(const uint8_t *f, uint32_t cap, uint32_t len, PktHdr &h) {
+    h.et = len >= 14 ? ((fbyte(f, cap, 12) << 8) | fbyte(f, cap, 13)) : 0u;
+    h.sa = h.da = h.w0 = h.w3 = h.proto = 0;
+    h.l4 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) h.s6[k] = h.d6[k] = 0;
+    bool have = false;
+    if (h.et == 0x0800 && len >= 34) {
+        for (int k = 0; k < 4; k++) { h.sa |= fbyte(f, cap, 26 + k) << (8 * k); h.da |= fbyte(f, cap, 30 + k) << (8 * k); }
+        h.proto = fbyte(f, cap, 23);
+        h.l4 = 14 + (int)(fbyte(f, cap, 14) & 0xf) * 4;
+        have = true;
+    } else if (h.et == 0x86DD && len >= 54) {
+        for (int k = 0; k < 16; k++) {
+            h.s6[k >> 2] |= fbyte(f, cap, 22 + k) << (8 * (k & 3));
+            h.d6[k >> 2] |= fbyte(f, cap, 38 + k) << (8 * (k & 3));
+        }
+        // ipv6_hdrlen, bpf/lib/ipv6.h:61-98 (AUTH length chosen by the NEXT header, as written)
+        uint32_t nh = fbyte(f, cap, 20);
+        int hl = 40, res = -156;
+        for (int it = 0; it < 4; it++) {
+            if (nh == 59) { res = -156; goto done; }
+            if (nh == 44) { res = -157; goto done; }
+            if (nh == 0 || nh == 43 || nh == 51 || nh == 60) {
+                int off = 14 + hl;
+                if (!skb_ok(off, 2, len)) { res = -134; goto done; }
+                uint32_t onh = fbyte(f, cap, off), ohl = fbyte(f, cap, off + 1);
+                nh = onh;
+                if (nh == 51) hl += (int)(ohl + 2) << 2; else hl += (int)(ohl + 1) << 3;
+                continue;
+            }
+            res = hl;
+            h.proto = nh;
+            goto done;
+        }
+        res = -156;
+    done:
+        if (res < 0) h.proto = fbyte(f, cap, 20);
+        h.l4 = 14 + res;
+        have = true;
+    }
+    if (have) {
+        for (int k = 0; k < 4; k++) {
+            int64_t off = (int64_t)h.l4 + k;
+            if (off >= 0 && off < (int64_t)len) h.w0 |= fbyte(f, cap, (uint32_t)off) << (8 * k);
+        }
+        for (int k = 0; k < 2; k++) {
+            int64_t off = (int64_t)h.l4 + 12 + k;
+            if (off >= 0 && off < (int64_t)len) h.w3 |= fbyte(f, cap, (uint32_t)off) << (8 * k);
+        }
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_parse(gf_frames fr, gf_pkt_cols_out o) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < fr.n; i += gridDim.x * blockDim.x) {
         const uint8_t *f = fr.snap + (size_t)i * fr.snap_stride;
         uint32_t len = fr.len[i];
         uint32_t cap = fr.snap_stride < len ? fr.snap_stride : len;
-        uint16_t et = len >= 14 ? (uint16_t)((fbyte(f, cap, 12) << 8) | fbyte(f, cap, 13)) : 0;
-        uint32_t sa = 0, da = 0, w0 = 0; uint16_t w3 = 0; uint8_t proto = 0; int l4 = 0;
-        uint32_t s6[4] = {0, 0, 0, 0}, d6[4] = {0, 0, 0, 0};
-        bool have = false;
-        if (et == 0x0800 && len >= 34) {
-            for (int k = 0; k < 4; k++) { sa |= fbyte(f, cap, 26 + k) << (8 * k); da |= fbyte(f, cap, 30 + k) << (8 * k); }
-            proto = (uint8_t)fbyte(f, cap, 23);
-            l4 = 14 + (fbyte(f, cap, 14) & 0xf) * 4;
-            have = true;
-        } else if (et == 0x86DD && len >= 54) {
-            for (int k = 0; k < 16; k++) {
-                s6[k >> 2] |= fbyte(f, cap, 22 + k) << (8 * (k & 3));
-                d6[k >> 2] |= fbyte(f, cap, 38 + k) << (8 * (k & 3));
-            }
-            // ipv6_hdrlen, bpf/lib/ipv6.h:61-98 (AUTH length chosen by the NEXT header, as written)
-            uint8_t nh = (uint8_t)fbyte(f, cap, 20);
-            int hl = 40, res = -156;
-            for (int it = 0; it < 4; it++) {
-                if (nh == 59) { res = -156; goto done; }
-                if (nh == 44) { res = -157; goto done; }
-                if (nh == 0 || nh == 43 || nh == 51 || nh == 60) {
-                    int off = 14 + hl;
-                    if (!skb_ok(off, 2, len)) { res = -134; goto done; }
-                    uint32_t onh = fbyte(f, cap, off), ohl = fbyte(f, cap, off + 1);
-                    nh = (uint8_t)onh;
-                    if (nh == 51) hl += (int)(ohl + 2) << 2; else hl += (int)(ohl + 1) << 3;
-                    continue;
-                }
-                res = hl;
-                proto = nh;
-                goto done;
-            }
-            res = -156;
-        done:
-            if (res < 0) proto = (uint8_t)fbyte(f, cap, 20);
-            l4 = 14 + res;
-            have = true;
-        }
-        if (have) {
-            for (int k = 0; k < 4; k++) {
-                int64_t off = (int64_t)l4 + k;
-                if (off >= 0 && off < (int64_t)len) w0 |= fbyte(f, cap, (uint32_t)off) << (8 * k);
-            }
-            for (int k = 0; k < 2; k++) {
-                int64_t off = (int64_t)l4 + 12 + k;
-                if (off >= 0 && off < (int64_t)len) w3 |= (uint16_t)(fbyte(f, cap, (uint32_t)off) << (8 * k));
-            }
-        }
-        o.ethertype[i] = et; o.saddr4[i] = sa; o.daddr4[i] = da; o.proto[i] = proto;
-        o.l4_off[i] = (int16_t)l4; o.l4w0[i] = w0; o.l4w3[i] = w3;
-        if (o.saddr6) reinterpret_cast<uint4 *>(o.saddr6)[i] = make_uint4(s6[0], s6[1], s6[2], s6[3]);
-        if (o.daddr6) reinterpret_cast<uint4 *>(o.daddr6)[i] = make_uint4(d6[0], d6[1], d6[2], d6[3]);
+        PktHdr h;
+        parse_row(f, cap, len, h);
+        o.ethertype[i] = (uint16_t)h.et; o.saddr4[i] = h.sa; o.daddr4[i] = h.da; o.proto[i] = (uint8_t)h.proto;
+        o.l4_off[i] = (int16_t)h.l4; o.l4w0[i] = h.w0; o.l4w3[i] = (uint16_t)h.w3;
+        if (o.saddr6) reinterpret_cast<uint4 *>(o.saddr6)[i] = make_uint4(h.s6[0], h.s6[1], h.s6[2], h.s6[3]);
+        if (o.daddr6) reinterpret_cast<uint4 *>(o.daddr6)[i] = make_uint4(h.d6[0], h.d6[1], h.d6[2], h.d6[3]);
     }
 }
+
+// Header access for the per-packet programs: packet i of a column batch, or
+// the values a lane parsed itself (the fused pipeline front).
+struct ColA {
+    const gf_pkt_cols &c;
+    uint32_t i;
+    __device__ __forceinline__ uint32_t saddr4() const { return c.saddr4[i]; }
+    __device__ __forceinline__ uint32_t daddr4() const { return c.daddr4[i]; }
+    __device__ __forceinline__ uint32_t proto() const { return c.proto[i]; }
+    __device__ __forceinline__ int l4_off() const { return c.l4_off[i]; }
+    __device__ __forceinline__ uint32_t l4w0() const { return c.l4w0[i]; }
+    __device__ __forceinline__ uint32_t fhash() const { return c.flow_hash ? c.flow_hash[i] : 0u; }
+    __device__ __forceinline__ bool has6() const { return c.saddr6 && c.daddr6; }
+    __device__ __forceinline__ uint4 saddr6() const { return reinterpret_cast<const uint4 *>(c.saddr6)[i]; }
+    __device__ __forceinline__ uint4 daddr6() const { return gload<uint4>(c.daddr6 + 16 * (size_t)i); }
+};
+struct PktHdrA {
+    const PktHdr &h;
+    uint32_t fh;
+    __device__ __forceinline__ uint32_t saddr4() const { return h.sa; }
+    __device__ __forceinline__ uint32_t daddr4() const { return h.da; }
+    __device__ __forceinline__ uint32_t proto() const { return h.proto; }
+    __device__ __forceinline__ int l4_off() const { return h.l4; }
+    __device__ __forceinline__ uint32_t l4w0() const { return h.w0; }
+    __device__ __forceinline__ uint32_t fhash() const { return fh; }
+    __device__ __forceinline__ bool has6() const { return true; }
+    __device__ __forceinline__ uint4 saddr6() const { return make_uint4(h.s6[0], h.s6[1], h.s6[2], h.s6[3]); }
+    __device__ __forceinline__ uint4 daddr6() const { return make_uint4(h.d6[0], h.d6[1], h.d6[2], h.d6[3]); }
+};
 
 // ================================================================ XDP
 struct XdpDev {
@@ -159,12 +203,12 @@ __device__ __forceinline__ bool lxc_has6(const gf_htab_desc &lxc, const uint32_t
 
 // xdp_start -> check_filters -> check_v4 / check_v6 (bpf/bpf_xdp.c:97-184) for
 // packet i; ab accumulates the algorithmic bytes.
-__device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const gf_pkt_cols &c, uint32_t i, uint32_t len,
-                                               uint32_t et, uint32_t &ab) {
+template <class A>
+__device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint32_t len, uint32_t et, uint32_t &ab) {
     if (len < 14) return XDP_DROP_;
     if (et == 0x0800) {
         if (len < 34) return XDP_DROP_;
-        uint32_t sa = c.saddr4[i];
+        uint32_t sa = a.saddr4();
         bool drop = false;
         ab += 10;
         if (x.has_h4) {
@@ -174,11 +218,11 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const gf_pkt_col
         }
         if (drop) return XDP_DROP_;
         ab += 20;
-        return lxc_has4(x.lxc, c.daddr4[i]) ? XDP_PASS_ : XDP_DROP_;
+        return lxc_has4(x.lxc, a.daddr4()) ? XDP_PASS_ : XDP_DROP_;
     }
     if (et == 0x86DD) {
-        if (len < 54 || !c.saddr6 || !c.daddr6) return XDP_DROP_;
-        uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
+        if (len < 54 || !a.has6()) return XDP_DROP_;
+        uint4 s = a.saddr6();
         uint32_t sw[4] = {s.x, s.y, s.z, s.w};
         bool drop = false;
         ab += 34;
@@ -189,7 +233,7 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const gf_pkt_col
         }
         if (drop) return XDP_DROP_;
         ab += 20;
-        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
+        uint4 d = a.daddr6();
         uint32_t dw[4] = {d.x, d.y, d.z, d.w};
         return lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
     }
@@ -204,7 +248,7 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += gridDim.x * blockDim.x) {
         uint32_t len = c.len[i];
         uint32_t ab = 1;                                  // output record
-        uint8_t v = xdp_verdict(x, c, i, len, c.ethertype[i], ab);
+        uint8_t v = xdp_verdict(x, ColA{c, i}, len, c.ethertype[i], ab);
         verdict[i] = v;
         if (stats) st.pkt(v == XDP_DROP_ ? 1u : 0u, v, len, ab);
     }
@@ -230,16 +274,16 @@ __device__ __forceinline__ int lb_checks(const LbDev &L, uint32_t len, int l4_of
 }
 
 // returns program result (TC_OK pass / TC_REDIRECT translated / negative error)
-__device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t &ab,
-                     uint32_t &key_dport) {
+template <class A>
+__device__ int lb_v4(const LbDev &L, const A &a, uint32_t len, gf_lb_out &o, uint32_t &ab, uint32_t &key_dport) {
     if (len < 34) return D_INVALID;
-    uint32_t nh = c.proto[i], daddr = c.daddr4[i];
-    int l4_off = c.l4_off[i];
+    uint32_t nh = a.proto(), daddr = a.daddr4();
+    int l4_off = a.l4_off();
     uint32_t dport = 0;
     if (L.flags & GF_LB_F_L4) {
         if (nh == 6 || nh == 17) {
             if (!skb_ok(l4_off + 2, 2, len)) return -GF_EFAULT;
-            dport = c.l4w0[i] >> 16;
+            dport = a.l4w0() >> 16;
         } else if (nh != 1 && nh != 58) return TC_OK;     // DROP_UNKNOWN_L4 -> pass
     }
     const uint8_t *svc = nullptr;
@@ -258,7 +302,7 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     }
     if (!svc) return TC_OK;
     uint32_t count = gload<uint16_t>(svc + 6);
-    uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
+    uint32_t slave = (a.fhash() % count + 1u) & 0xffffu;
     uint32_t kw[2] = {daddr, dport | (slave << 16)};
     int64_t f = ht_find<8>(L.s4, kw, key_hash<8>(kw));
     ab += 20;
@@ -275,17 +319,18 @@ __device__ int lb_v4(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     return TC_REDIRECT;
 }
 
-__device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t len, gf_lb_out &o, uint32_t *nd6,
-                     uint32_t &ab, uint32_t &key_dport) {
-    if (len < 54 || !c.daddr6) return D_INVALID;
-    uint32_t nh = c.proto[i];
-    int l4_off = c.l4_off[i];
-    uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
+template <class A>
+__device__ int lb_v6(const LbDev &L, const A &a, uint32_t len, gf_lb_out &o, uint32_t *nd6, uint32_t &ab,
+                     uint32_t &key_dport) {
+    if (len < 54 || !a.has6()) return D_INVALID;
+    uint32_t nh = a.proto();
+    int l4_off = a.l4_off();
+    uint4 d = a.daddr6();
     uint32_t dport = 0;
     if (L.flags & GF_LB_F_L4) {
         if (nh == 6 || nh == 17) {
             if (!skb_ok(l4_off + 2, 2, len)) return -GF_EFAULT;
-            dport = c.l4w0[i] >> 16;
+            dport = a.l4w0() >> 16;
         } else if (nh != 1 && nh != 58) return TC_OK;
     }
     const uint8_t *svc = nullptr;
@@ -304,7 +349,7 @@ __device__ int lb_v6(const LbDev &L, const gf_pkt_cols &c, uint32_t i, uint32_t 
     }
     if (!svc) return TC_OK;
     uint32_t count = gload<uint16_t>(svc + 18);
-    uint32_t slave = ((c.flow_hash ? c.flow_hash[i] : 0u) % count + 1u) & 0xffffu;
+    uint32_t slave = (a.fhash() % count + 1u) & 0xffffu;
     uint32_t kw[5] = {d.x, d.y, d.z, d.w, dport | (slave << 16)};
     int64_t f = ht_find<20>(L.s6, kw, key_hash<20>(kw));
     ab += 44;
@@ -337,8 +382,8 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         bool v6 = false;
         uint32_t ab = 12 + 12;                            // header columns + output record
         uint32_t kd = 0;
-        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(L, c, i, len, o, n6, ab, kd); } }
-        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, c, i, len, o, ab, kd); }
+        if (et == 0x86DD) { if (!(L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(L, ColA{c, i}, len, o, n6, ab, kd); } }
+        else if (et == 0x0800) { if (!(L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(L, ColA{c, i}, len, o, ab, kd); }
         if (ret < 0 || ret == TC_SHOT) {
             o = gf_lb_out{};
             o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -366,6 +411,7 @@ struct IngCtx {
     gf_htab_desc ct4, ct6;   // cilium_ct4_global / cilium_ct6_global (shared by every program)
     uint32_t now, host_ifindex;
     uint32_t strict;   // bit0: CT inserts check max_entries with atomics
+    uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
 };
 
 struct CtState { uint32_t rev_nat, loopback, carry; };
@@ -982,47 +1028,54 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     return o;
 }
 
-// skip (may be null): packets of a pipeline batch that end before the
-// cilium_policy tail call; they are marked (cls bit 3) and left untouched.
-__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
-                                                    uint32_t *keys, const uint8_t *skip) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= c.n) return;
-    gf_rec r;
-    uint32_t et = c.ethertype[i];
-    r.len = c.len[i];
-    r.saddr = c.saddr4[i]; r.daddr = c.daddr4[i];
-    r.l4w0 = c.l4w0[i]; r.l4w3 = c.l4w3[i];
-    r.src_identity = c.src_identity ? c.src_identity[i] : 0u;
-    r.ifindex = c.ifindex ? c.ifindex[i] : 0u;
-    r.ep = slot_of[c.lxc_id ? c.lxc_id[i] : 0];        // tail_call(cilium_policy, lxc_id) target
-    r.l4_off = c.l4_off[i];
-    r.proto = c.proto[i];
+// The 32-B record handle_policy reads and the packet's flow-group bucket key.
+// Only packets that can reach conntrack (an IP header is present) are bound to
+// their flow group; the rest carry no ordering constraint and are spread out.
+// GF_KEY_BITS-1 bits of the group hash are the sort key: groups that collide
+// share a bucket (always safe: a bucket is serialized as a whole), and a
+// shorter key is one radix pass less.  The top key bit is the family of the CT
+// path (1: IPv6 reaching conntrack).  skipped: a pipeline packet that ended
+// before the cilium_policy tail call (cls bit 3; left untouched).
+__device__ __forceinline__ uint32_t pack_rec(uint32_t i, uint32_t et, uint32_t len, uint32_t sa, uint32_t da,
+                                             uint32_t w0, uint32_t w3, int l4, uint32_t proto, uint32_t sid,
+                                             uint32_t ifx, uint16_t ep, uint32_t tci, bool skipped, bool have6,
+                                             const uint32_t *s6, const uint32_t *d6, gf_rec &r) {
+    r.len = len;
+    r.saddr = sa; r.daddr = da;
+    r.l4w0 = w0; r.l4w3 = (uint16_t)w3;
+    r.src_identity = sid;
+    r.ifindex = ifx;
+    r.ep = ep;                                          // tail_call(cilium_policy, lxc_id) target
+    r.l4_off = (int16_t)l4;
+    r.proto = (uint8_t)proto;
     uint32_t cls = et == 0x0800 ? 1u : et == 0x86DD ? 2u : 0u;
-    if (c.tc_index && (c.tc_index[i] & 1)) cls |= 4u;
-    const bool skipped = skip && skip[i];
+    if (tci & 1) cls |= 4u;
     if (skipped) cls |= 8u;
     r.cls = (uint8_t)cls;
-    uint32_t h;
-    // Only packets that can reach conntrack (an IP header is present) are bound to
-    // their flow group; the rest carry no ordering constraint and are spread out.
-    // GF_KEY_BITS-1 bits of the group hash are the sort key: groups that collide
-    // share a bucket (always safe: a bucket is serialized as a whole), and a
-    // shorter key is one radix pass less.
-    bool ct_ok = !skipped && (((cls & 3) == 1 && r.len >= 34) || ((cls & 3) == 2 && r.len >= 54 && c.saddr6));
-    // The top key bit is the family of the CT path (1: IPv6 reaching conntrack).
-    if (!ct_ok) {
-        h = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
-    } else if ((cls & 3) == 2) {
-        uint4 s = reinterpret_cast<const uint4 *>(c.saddr6)[i];
-        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
-        uint32_t sw[4] = {s.x, s.y, s.z, s.w}, dw[4] = {d.x, d.y, d.z, d.w};
-        h = (gf_pair_hash6(sw, dw) & GF_KEY_HASH) | GF_KEY_FAM;
-    } else {
-        h = gf_pair_hash4(r.saddr, r.daddr) & GF_KEY_HASH;
+    const bool ct_ok = !skipped && (((cls & 3) == 1 && len >= 34) || ((cls & 3) == 2 && len >= 54 && have6));
+    if (!ct_ok) return gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
+    if ((cls & 3) == 2) return (gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;
+    return gf_pair_hash4(sa, da) & GF_KEY_HASH;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
+                                                    uint32_t *keys) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c.n) return;
+    const uint32_t et = c.ethertype[i], len = c.len[i];
+    uint32_t s6[4] = {0, 0, 0, 0}, d6[4] = {0, 0, 0, 0};
+    if (et == 0x86DD && len >= 54 && c.saddr6) {
+        uint4 sv = reinterpret_cast<const uint4 *>(c.saddr6)[i];
+        uint4 dv = gload<uint4>(c.daddr6 + 16 * (size_t)i);
+        s6[0] = sv.x; s6[1] = sv.y; s6[2] = sv.z; s6[3] = sv.w;
+        d6[0] = dv.x; d6[1] = dv.y; d6[2] = dv.z; d6[3] = dv.w;
     }
+    gf_rec r;
+    keys[i] = pack_rec(i, et, len, c.saddr4[i], c.daddr4[i], c.l4w0[i], c.l4w3[i], c.l4_off[i], c.proto[i],
+                       c.src_identity ? c.src_identity[i] : 0u, c.ifindex ? c.ifindex[i] : 0u,
+                       slot_of[c.lxc_id ? c.lxc_id[i] : 0], c.tc_index ? c.tc_index[i] : 0u, false,
+                       c.saddr6 != nullptr, s6, d6, r);
     rec[i] = r;
-    keys[i] = h;
 }
 
 // Flow-group schedule.  A bucket is a run of equal 32-bit group hash in the
@@ -1039,7 +1092,17 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
-    if (!(GF_DIAG & 1)) out[i] = o;
+    if (X.pout) {                                       // complete the pipeline record
+        uint8_t *q = X.pout + 24 * (size_t)i;
+        uint2 a = *reinterpret_cast<const uint2 *>(q), b = *reinterpret_cast<const uint2 *>(q + 8);
+        a.x = (a.x & 0xffu) | ((uint32_t)o.action << 8) | ((uint32_t)o.reason << 16) | ((uint32_t)o.ct_ret << 24);
+        a.y = ((a.y & 0xffu) | o.flags) | (a.y & 0xff00u) | ((uint32_t)o.proxy_port << 16);
+        b.x = (b.x & 0xffff0000u) | o.ifindex_lo;
+        *reinterpret_cast<uint2 *>(q) = a;
+        *reinterpret_cast<uint2 *>(q + 8) = b;
+    } else if (!(GF_DIAG & 1)) {
+        out[i] = o;
+    }
     if (stats && !(GF_DIAG & 2)) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
 }
 
@@ -1196,11 +1259,12 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
 // ================================================================ pipeline (config 4)
 // bpf_xdp -> bpf_lb from-netdev -> bpf_netdev from-netdev -> cilium_policy tail
 // call, each program seeing the frame as the previous one rewrote it.
-// k_pipe_front runs the first three on one packet per lane over a copy of the
-// frame (the rewrites and their checksum updates are applied to that copy),
-// k_parse re-derives the header columns of the rewritten frames, the ingress
-// machinery runs handle_policy on the packets that reached the tail call, and
-// k_pipe_merge folds its records into the pipeline records.
+// k_pipe_front stages a block's frames in LDS and runs the first three on one
+// packet per lane over its frame there (the rewrites and their checksum updates
+// are applied to that copy), re-parses the rewritten header and writes the
+// packet's handle_policy record and flow-group key directly (k_ing_pack fused);
+// the ingress machinery then runs handle_policy on the packets that reached the
+// tail call and completes their pipeline records in place.
 struct NetdevDev {
     gf_htab_desc lxc;
     uint32_t flags, fixed_secctx;
@@ -1212,12 +1276,6 @@ struct PipeDev {
     NetdevDev nd;
     uint32_t has_xdp, has_lb, lb_redirect_ifindex, vec_copy;
 };
-struct PipeMeta {
-    uint32_t *src_identity, *ifindex;
-    uint16_t *lxc_id;
-    uint8_t *skip;
-};
-
 // The lane's frame copy.  Reads past the snap (or len) are 0, writes past the
 // snap are dropped (the snap holds every header byte the programs touch).
 struct Row {
@@ -1272,20 +1330,19 @@ __device__ int l4_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_
 
 // lb4_xlate / lb6_xlate writes (bpf/lib/lb.h:615-659, 397-423) of a translation
 // lb_v4/lb_v6 accepted (their checks passed, so every helper succeeds).
-__device__ void pipe_lb_rewrite(Row &w, uint32_t len, const gf_pkt_cols &c, uint32_t i, bool v6, const gf_lb_out &o,
+__device__ void pipe_lb_rewrite(Row &w, uint32_t len, const PktHdr &h, bool v6, const gf_lb_out &o,
                                 const uint32_t *n6, uint32_t key_dport, uint32_t &ab) {
-    const uint32_t nh = c.proto[i];
-    const int l4_off = c.l4_off[i];
+    const uint32_t nh = h.proto;
+    const int l4_off = h.l4;
     uint32_t sum = 0;
     if (!v6) {
-        const uint32_t old = c.daddr4[i], nw = o.new_daddr4;
+        const uint32_t old = h.da, nw = o.new_daddr4;
         w.w32(30, nw);
         sum = ck_add(ck_add(0u, ~old), nw);             // csum_diff(&key->address, 4, new_daddr, 4, 0)
         l3_csum(w, len, 24, 0, sum, 0);
         ab += 4 + 2;
     } else {
-        uint4 d = gload<uint4>(c.daddr6 + 16 * (size_t)i);
-        const uint32_t od[4] = {d.x, d.y, d.z, d.w};
+        const uint32_t *od = h.d6;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             w.w32(38 + 4 * k, n6[k]);                   // ipv6_store_daddr
@@ -1340,7 +1397,7 @@ __device__ int delivery_tail(Row &w, uint32_t len, int l4_off, uint32_t nh, cons
 
 // from_netdev of bpf/bpf_netdev.c:395-460 -> handle_ipv4 (:326-393) / handle_ipv6
 // (:160-247), without FROM_HOST, ENCAP_IFINDEX or HANDLE_NS.
-__device__ int pipe_netdev(const NetdevDev &N, Row &w, const gf_pkt_cols &c, uint32_t i, uint32_t et, uint32_t len,
+__device__ int pipe_netdev(const NetdevDev &N, Row &w, const PktHdr &h, uint32_t et, uint32_t len,
                            uint32_t &sec, uint32_t &ifx, uint32_t &lxc, uint32_t &mapped, uint32_t &ndport,
                            uint32_t &ab) {
     if (et == 0x0800) {
@@ -1358,7 +1415,7 @@ __device__ int pipe_netdev(const NetdevDev &N, Row &w, const gf_pkt_cols &c, uin
         l3_csum(w, len, 24, ttl, ttl - 1, 2);
         w.w8(22, ttl - 1);
         ab += 3;
-        return delivery_tail(w, len, c.l4_off[i], c.proto[i], ep, ifx, lxc, mapped, ndport, ab);
+        return delivery_tail(w, len, h.l4, h.proto, ep, ifx, lxc, mapped, ndport, ab);
     }
     if (et == 0x86DD) {
         if (len < 54) return D_INVALID;
@@ -1377,44 +1434,53 @@ __device__ int pipe_netdev(const NetdevDev &N, Row &w, const gf_pkt_cols &c, uin
         if (hl <= 1) return ND_ICMP6_TE;
         w.w8(21, hl - 1);
         ab += 1;
-        return delivery_tail(w, len, c.l4_off[i], c.proto[i], ep, ifx, lxc, mapped, ndport, ab);
+        return delivery_tail(w, len, h.l4, h.proto, ep, ifx, lxc, mapped, ndport, ab);
     }
     return TC_OK;                                       // unknown traffic to the stack
 }
 
-__global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols c, PipeDev P, uint8_t *snap2,
-                                                      gf_pipeline_out *out, uint8_t *nd6, PipeMeta M,
-                                                      unsigned long long *stats) {
+// One packet per lane; the block's frames are staged in LDS (BLOCK * snap_stride
+// bytes of dynamic shared memory) and copied back out only when the caller
+// asked for the rewritten frames.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *tc_index, const uint32_t *flow_hash,
+                                                      PipeDev P, const uint16_t *slot_of, gf_rec *rec, uint32_t *keys,
+                                                      uint8_t *s6out, uint8_t *d6out, gf_pipeline_out *out,
+                                                      uint8_t *nd6, uint8_t *snap_out, unsigned long long *stats) {
+    extern __shared__ uint4 lds_rows[];
+    uint8_t *rows = reinterpret_cast<uint8_t *>(lds_rows);
     __shared__ uint32_t sl[272];
     Stats st{sl};
-    // this block's frames, copied coalesced; each lane then rewrites its own row
-    const uint32_t S = fr.snap_stride, b0 = blockIdx.x * BLOCK;
-    const uint32_t nb = fr.n - b0 < BLOCK ? fr.n - b0 : BLOCK;
+    const uint32_t S = fr.snap_stride, b0 = blockIdx.x * NT;
+    const uint32_t nb = fr.n - b0 < NT ? fr.n - b0 : NT;
+    const size_t bytes = (size_t)nb * S;
     {
         const uint8_t *src = fr.snap + (size_t)b0 * S;
-        uint8_t *dst = snap2 + (size_t)b0 * S;
-        const size_t bytes = (size_t)nb * S;
         size_t k0 = 0;
         if (P.vec_copy) {
             const size_t nv = bytes / 16;
-            for (size_t k = threadIdx.x; k < nv; k += BLOCK)
-                reinterpret_cast<uint4 *>(dst)[k] = reinterpret_cast<const uint4 *>(src)[k];
+            for (size_t k = threadIdx.x; k < nv; k += NT) lds_rows[k] = reinterpret_cast<const uint4 *>(src)[k];
             k0 = nv * 16;
         }
-        for (size_t k = k0 + threadIdx.x; k < bytes; k += BLOCK) dst[k] = src[k];
+        for (size_t k = k0 + threadIdx.x; k < bytes; k += NT) rows[k] = src[k];
     }
     if (stats) st.init(); else __syncthreads();
     const uint32_t i = b0 + threadIdx.x;
     if (i < fr.n) {
-        const uint32_t len = c.len[i], et = c.ethertype[i];
-        Row w{snap2 + (size_t)i * S, S < len ? S : len};
+        const uint32_t len = fr.len[i];
+        const uint32_t cap = S < len ? S : len;
+        Row w{rows + (size_t)threadIdx.x * S, cap};
+        PktHdr h;
+        parse_row(w.p, cap, len, h);
+        const uint32_t et = h.et;
+        const PktHdrA ha{h, flow_hash ? flow_hash[i] : 0u};
         gf_pipeline_out o{};
         uint32_t n6[4] = {0, 0, 0, 0};
         uint32_t sec = 0, ifx = 0, lxc = 0, mapped = 0, ndport = 0;
-        uint32_t ab = 24;                               // output record
+        uint32_t ab = 24 + 34;                          // output record, header bytes parsed
         bool tail = false;
         do {
-            if (P.has_xdp && xdp_verdict(P.x, c, i, len, et, ab) == XDP_DROP_) {
+            if (P.has_xdp && xdp_verdict(P.x, ha, len, et, ab) == XDP_DROP_) {
                 o.stage = GF_STAGE_XDP; o.action = XDP_DROP_;
                 break;
             }
@@ -1425,9 +1491,9 @@ __global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols 
                 bool v6 = false;
                 ab += 12;
                 if (et == 0x86DD) {
-                    if (!(P.L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(P.L, c, i, len, lo, n6, ab, kd); }
+                    if (!(P.L.flags & GF_LB_F_NO_IPV6)) { v6 = true; ab += 28; ret = lb_v6(P.L, ha, len, lo, n6, ab, kd); }
                 } else if (et == 0x0800) {
-                    if (!(P.L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(P.L, c, i, len, lo, ab, kd);
+                    if (!(P.L.flags & GF_LB_F_NO_IPV4)) ret = lb_v4(P.L, ha, len, lo, ab, kd);
                 }
                 if (ret < 0 || ret == TC_SHOT) {
                     o.stage = GF_STAGE_LB; o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -1435,7 +1501,7 @@ __global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols 
                     break;
                 }
                 if (ret == TC_REDIRECT) {
-                    pipe_lb_rewrite(w, len, c, i, v6, lo, n6, kd, ab);
+                    pipe_lb_rewrite(w, len, h, v6, lo, n6, kd, ab);
                     o.slave = lo.slave; o.rev_nat = lo.rev_nat; o.dport = lo.new_dport;
                     o.daddr4 = v6 ? 0u : lo.new_daddr4;
                     o.flags |= GF_PIPE_F_LB;
@@ -1447,7 +1513,7 @@ __global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols 
                     n6[0] = n6[1] = n6[2] = n6[3] = 0;
                 }
             }
-            const int r = pipe_netdev(P.nd, w, c, i, et, len, sec, ifx, lxc, mapped, ndport, ab);
+            const int r = pipe_netdev(P.nd, w, h, et, len, sec, ifx, lxc, mapped, ndport, ab);
             if (mapped) { o.flags |= GF_PIPE_F_PORTMAP; o.dport = (uint16_t)ndport; }
             o.stage = GF_STAGE_NETDEV;
             if (r == ND_TAILCALL) { o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; tail = true; }
@@ -1455,29 +1521,43 @@ __global__ __launch_bounds__(BLOCK) void k_pipe_front(gf_frames fr, gf_pkt_cols 
             else if (r < 0 || r == TC_SHOT) { o.action = TC_SHOT; o.reason = (uint8_t)(-r); }
             else o.action = (uint8_t)r;
         } while (0);
+        // handle_policy's input: the rewritten header, re-parsed (k_ing_pack fused)
+        gf_rec rr;
+        uint32_t key;
+        const uint32_t tci = tc_index ? tc_index[i] : 0u;
+        if (tail) {
+            PktHdr h2;
+            parse_row(w.p, cap, len, h2);
+            key = pack_rec(i, h2.et, len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto, sec, ifx, slot_of[lxc & 0xffffu],
+                           tci, false, true, h2.s6, h2.d6, rr);
+            if (h2.et == 0x86DD) {
+                reinterpret_cast<uint4 *>(s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
+                reinterpret_cast<uint4 *>(d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
+            }
+        } else {
+            key = pack_rec(i, et, len, 0, 0, 0, 0, 0, 0, 0, 0, 0, tci, true, true, h.s6, h.d6, rr);
+        }
+        rec[i] = rr;
+        keys[i] = key;
         out[i] = o;
         if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
-        M.skip[i] = tail ? 0 : 1;
-        M.src_identity[i] = tail ? sec : 0u;
-        M.ifindex[i] = tail ? ifx : 0u;
-        M.lxc_id[i] = (uint16_t)(tail ? lxc : 0u);
         if (stats) {
             if (tail) st.add_n(270, ab);                // handle_policy counts the packet itself
             else st.pkt(o.reason, o.action, len, ab);
         }
     }
+    if (snap_out) {
+        __syncthreads();
+        uint8_t *dst = snap_out + (size_t)b0 * S;
+        size_t k0 = 0;
+        if (P.vec_copy) {
+            const size_t nv = bytes / 16;
+            for (size_t k = threadIdx.x; k < nv; k += NT) reinterpret_cast<uint4 *>(dst)[k] = lds_rows[k];
+            k0 = nv * 16;
+        }
+        for (size_t k = k0 + threadIdx.x; k < bytes; k += NT) dst[k] = rows[k];
+    }
     if (stats) st.flush(stats);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_pipe_merge(uint32_t n, const uint8_t *skip, const gf_ingress_out *ing,
-                                                      gf_pipeline_out *out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || skip[i]) return;
-    const gf_ingress_out g = ing[i];
-    gf_pipeline_out o = out[i];
-    o.action = g.action; o.reason = g.reason; o.ct_ret = g.ct_ret; o.flags |= g.flags;
-    o.proxy_port = g.proxy_port; o.ifindex_lo = g.ifindex_lo;
-    out[i] = o;
 }
 
 // ================================================================ host: programs
@@ -1527,8 +1607,7 @@ struct Workspace {
 };
 Workspace &ws() { static Workspace w; return w; }
 struct PipeWs {
-    DevBuf et[2], sa[2], da[2], proto[2], l4off[2], w0[2], w3[2], s6[2], d6[2];   // [0] original, [1] rewritten
-    DevBuf sid, ifx, lxc, skip, ing, snap;
+    DevBuf s6, d6;             // IPv6 addresses of the rewritten frames (read by handle_policy)
 };
 PipeWs &pipe_ws() { static PipeWs w; return w; }
 
@@ -1735,8 +1814,11 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 
 // handle_policy over a batch (caller holds big_lock and checked the columns).
 // skip (DEVICE, may be null): packets a pipeline ended before the tail call.
+// pack (may be empty): fills the records and bucket keys itself (the fused
+// pipeline front) instead of k_ing_pack; pout: pipeline records to complete.
+using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
-                       gf_ingress_out *out, hipStream_t s, const uint8_t *skip) {
+                       gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -1796,10 +1878,9 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     if (ct6m) cfg_ct6 = ct6m->hdesc();
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
-        // LRU: no eviction in classify; bounded at 2 x max_entries (and 7/8 of the slots)
-        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH
-                             ? std::min<uint64_t>(m->ht.nslots / 8 * 7, 2ull * m->max_entries)
-                             : m->max_entries;
+        // LRU: never fails in the kernel (it evicts); here no eviction in classify, the
+        // entries stay until GC, bounded by the slot array (7/8 load = 3.5 x max_entries)
+        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
         if (m->host_valid) m->dev_count_hi = m->ht.count;
         if (m->dev_count_hi + 2ull * pkts->n > limit && !m->host_valid) {
             uint32_t dc = 0;
@@ -1854,13 +1935,15 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
                                   rocprim::plus<uint32_t>(), s);
     if ((r = grow(w.tmp, std::max(std::max(sort_bytes, scan_bytes), rle_bytes) + 256))) return r;
-    {
+    if (pack) {
+        if ((r = pack((const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p))) return r;
+    } else {
         ProfScope ps("k_ing_pack", s);
         hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
                            (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
-                           (uint32_t *)w.keys.p, skip);
+                           (uint32_t *)w.keys.p);
+        if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
-    if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
@@ -1902,6 +1985,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     if (ct6m) X.ct6 = cfg_ct6;
     X.now = now_sec; X.host_ifindex = host_ifindex();
     X.strict = strict;
+    X.pout = pout;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
@@ -1944,7 +2028,7 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (c <= 0) return c;
     if (!out) return -EFAULT;
     if (pkts->n > (1u << 30)) return -E2BIG;
-    return ingress_run(a, pkts, now_sec, out, (hipStream_t)stream, nullptr);
+    return ingress_run(a, pkts, now_sec, out, (hipStream_t)stream);
 }
 
 // ---- full pipeline ----
@@ -2014,70 +2098,31 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     P.nd.flags = p->cfg.netdev.flags;
     P.nd.fixed_secctx = p->cfg.netdev.fixed_secctx;
     memcpy(P.nd.router6, p->cfg.netdev.router_ip6, 8);
-    // workspace: original and rewritten columns, the rewritten frames, tail-call metadata
+    // LDS staging of the block's frames (one row per lane)
+    // (256 lanes per block up to 128-B snaps, 128 lanes up to 256 B: <= 32 KiB)
+    if (fr.snap_stride > 256) return -EINVAL;          // not a header snap
+    const uint32_t nt = fr.snap_stride <= 128 ? 256u : 128u;
+    const size_t lds = (size_t)nt * fr.snap_stride;
     PipeWs &w = pipe_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
-    const size_t S = fr.snap_stride;
-    for (int k = 0; k < 2; k++) {
-        if ((r = grow(w.et[k], (size_t)n * 2)) || (r = grow(w.sa[k], (size_t)n * 4)) || (r = grow(w.da[k], (size_t)n * 4)) ||
-            (r = grow(w.proto[k], n)) || (r = grow(w.l4off[k], (size_t)n * 2)) || (r = grow(w.w0[k], (size_t)n * 4)) ||
-            (r = grow(w.w3[k], (size_t)n * 2)) || (r = grow(w.s6[k], (size_t)n * 16)) || (r = grow(w.d6[k], (size_t)n * 16)))
-            return r;
-    }
-    if ((r = grow(w.sid, (size_t)n * 4)) || (r = grow(w.ifx, (size_t)n * 4)) || (r = grow(w.lxc, (size_t)n * 2)) ||
-        (r = grow(w.skip, n)) || (r = grow(w.ing, (size_t)n * sizeof(gf_ingress_out))) ||
-        (!snap_out && (r = grow(w.snap, (size_t)n * S))))
-        return r;
-    uint8_t *snap2 = snap_out ? snap_out : (uint8_t *)w.snap.p;
-    auto cols_out = [&](int k) {
-        gf_pkt_cols_out co{};
-        co.ethertype = (uint16_t *)w.et[k].p; co.saddr4 = (uint32_t *)w.sa[k].p; co.daddr4 = (uint32_t *)w.da[k].p;
-        co.proto = (uint8_t *)w.proto[k].p; co.l4_off = (int16_t *)w.l4off[k].p; co.l4w0 = (uint32_t *)w.w0[k].p;
-        co.l4w3 = (uint16_t *)w.w3[k].p; co.saddr6 = (uint8_t *)w.s6[k].p; co.daddr6 = (uint8_t *)w.d6[k].p;
-        return co;
-    };
-    auto cols_in = [&](int k) {
-        gf_pkt_cols c{};
-        c.n = n; c.len = fr.len;
-        c.ethertype = (const uint16_t *)w.et[k].p; c.saddr4 = (const uint32_t *)w.sa[k].p;
-        c.daddr4 = (const uint32_t *)w.da[k].p; c.proto = (const uint8_t *)w.proto[k].p;
-        c.l4_off = (const int16_t *)w.l4off[k].p; c.l4w0 = (const uint32_t *)w.w0[k].p;
-        c.l4w3 = (const uint16_t *)w.w3[k].p; c.saddr6 = (const uint8_t *)w.s6[k].p; c.daddr6 = (const uint8_t *)w.d6[k].p;
-        c.tc_index = b->tc_index;
-        return c;
-    };
-    PipeMeta M{(uint32_t *)w.sid.p, (uint32_t *)w.ifx.p, (uint16_t *)w.lxc.p, (uint8_t *)w.skip.p};
-    P.vec_copy = (((uintptr_t)fr.snap | (uintptr_t)snap2) & 15u) == 0;
+    if ((r = grow(w.s6, (size_t)n * 16)) || (r = grow(w.d6, (size_t)n * 16))) return r;
+    P.vec_copy = (fr.snap_stride % 16 == 0) && (((uintptr_t)fr.snap | (uintptr_t)snap_out) & 15u) == 0;
     unsigned long long *sink = (unsigned long long *)stats_sink();
-    const uint32_t grid = (n + BLOCK - 1) / BLOCK;
-    {
-        ProfScope ps("k_parse", s);
-        gf_pkt_cols_out co = cols_out(0);
-        hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(BLOCK), 0, s, fr, co);
-    }
-    {
+    const uint32_t grid = (n + nt - 1) / nt;
+    gf_pkt_cols c2{};
+    c2.n = n;
+    c2.saddr6 = (const uint8_t *)w.s6.p; c2.daddr6 = (const uint8_t *)w.d6.p;
+    auto front = [&](const uint16_t *slot_of, gf_rec *rec, uint32_t *keys) -> int {
         ProfScope ps("k_pipe_front", s);
-        gf_pkt_cols c0 = cols_in(0);
-        c0.flow_hash = b->flow_hash;
-        hipLaunchKernelGGL(k_pipe_front, dim3(grid), dim3(BLOCK), 0, s, fr, c0, P, snap2, out, nd6, M, sink);
-    }
-    if ((r = hip_ok(hipGetLastError(), "k_pipe_front"))) return r;
-    gf_frames fr2 = fr;
-    fr2.snap = snap2;
-    {
-        ProfScope ps("k_parse", s);
-        gf_pkt_cols_out co = cols_out(1);
-        hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(BLOCK), 0, s, fr2, co);
-    }
-    gf_pkt_cols c2 = cols_in(1);
-    c2.src_identity = M.src_identity; c2.ifindex = M.ifindex; c2.lxc_id = M.lxc_id;
-    if ((r = ingress_run(p->policy, &c2, now_sec, (gf_ingress_out *)w.ing.p, s, M.skip))) return r;
-    {
-        ProfScope ps("k_pipe_merge", s);
-        hipLaunchKernelGGL(k_pipe_merge, dim3(grid), dim3(BLOCK), 0, s, n, (const uint8_t *)M.skip,
-                           (const gf_ingress_out *)w.ing.p, out);
-    }
-    return hip_ok(hipGetLastError(), "k_pipe_merge");
+        if (nt == 256)
+            hipLaunchKernelGGL(k_pipe_front<256>, dim3(grid), dim3(256), lds, s, fr, b->tc_index, b->flow_hash, P,
+                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.d6.p, out, nd6, snap_out, sink);
+        else
+            hipLaunchKernelGGL(k_pipe_front<128>, dim3(grid), dim3(128), lds, s, fr, b->tc_index, b->flow_hash, P,
+                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.d6.p, out, nd6, snap_out, sink);
+        return hip_ok(hipGetLastError(), "k_pipe_front");
+    };
+    return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out);
 }
 
 }  // extern "C"
