@@ -410,7 +410,7 @@ struct IngCtx {
     const uint8_t *saddr6, *daddr6;
     gf_htab_desc ct4, ct6;   // cilium_ct4_global / cilium_ct6_global (shared by every program)
     uint32_t now, host_ifindex;
-    uint32_t strict;   // bit0: CT inserts check max_entries with atomics
+    uint32_t strict;   // bit0 / bit1: CT4 / CT6 inserts check max_entries with atomics
     uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
 };
 
@@ -952,14 +952,14 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ab += 40;
-            ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, X.strict & 1, added);
+            ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, (X.strict & 2) != 0, added);
             rc.slot = ~0u;
         }
         return D_POLICY;
     }
     if (r.cls & 4) verdict = 0;
     if (ret == CT_NEW) {
-        ret = ct_create<40, 10, GF_CT6_U>(ct, t, rn_new, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab);
+        ret = ct_create<40, 10, GF_CT6_U>(ct, t, rn_new, r.src_identity, len, X.now, (X.strict & 2) != 0, pr, added, rc, ab);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -1106,8 +1106,9 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     if (stats && !(GF_DIAG & 2)) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
 }
 
-__device__ __forceinline__ void flush_added(const IngCtx &X, int added, uint32_t *ct_count, uint32_t *lds_added) {
-    if (X.strict & 1) return;
+__device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, int added, uint32_t *ct_count,
+                                            uint32_t *lds_added) {
+    if (X.strict & fam_bit) return;
     if (added) atomicAdd(lds_added, (uint32_t)added);
     __syncthreads();
     if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
@@ -1172,7 +1173,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         }
     }
     ln.acc.flush(X);
-    flush_added(X, ln.added, ct_count, &sadd);
+    flush_added(X, F ? 2u : 1u, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }
 
@@ -1560,6 +1561,89 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
     if (stats) st.flush(stats);
 }
 
+// ================================================================ CT garbage collection
+// ctmap.GC / Flush (pkg/maps/ctmap/ctmap.go:277-368, GCFilterByTime): delete every
+// entry with lifetime < filter_time.  On the device the sweep also compacts each
+// probe cluster (a maximal run of non-EMPTY slots) in place, so deleted entries
+// and the tombstones of ct_delete leave EMPTY slots behind: k_gc_starts marks
+// the cluster starts (a non-EMPTY slot after an EMPTY one) on the unmodified
+// table, then k_gc_clusters walks each cluster with one lane, dropping expired
+// entries and tombstones and moving every live entry to the first EMPTY slot at
+// or after its home — the invariant lookups rely on (no EMPTY slot between a
+// key's home and the key) holds after the move.
+__global__ __launch_bounds__(BLOCK) void k_gc_starts(gf_htab_desc d, uint32_t *bits) {
+    const uint64_t nw = (d.mask + 1 + 31) / 32;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t m = 0;
+        uint64_t i0 = w * 32;
+        uint32_t prev = d.slots[((i0 - 1) & d.mask) * d.slot_size + d.ksz];
+        for (int k = 0; k < 32; k++) {
+            uint64_t i = i0 + k;
+            if (i > d.mask) break;
+            uint32_t st = d.slots[i * d.slot_size + d.ksz];
+            if (st != GF_SLOT_EMPTY && prev == GF_SLOT_EMPTY) m |= 1u << k;
+            prev = st;
+        }
+        bits[w] = m;
+    }
+}
+
+__device__ __forceinline__ void gc_move(const gf_htab_desc &d, uint64_t from, uint64_t to, uint32_t vstride) {
+    uint8_t *a = d.slots + from * d.slot_size, *b = d.slots + to * d.slot_size;
+    for (uint32_t k = 0; k < d.slot_size; k += 16) *reinterpret_cast<uint4 *>(b + k) = *reinterpret_cast<const uint4 *>(a + k);
+    if (vstride) {
+        uint8_t *va = d.vals + from * vstride, *vb = d.vals + to * vstride;
+        for (uint32_t k = 0; k < vstride; k += 4) *reinterpret_cast<uint32_t *>(vb + k) = *reinterpret_cast<const uint32_t *>(va + k);
+    }
+    a[d.ksz] = GF_SLOT_EMPTY;
+}
+
+// lt_off: byte offset of ct_entry.lifetime within the value bytes ht_val points at
+// (0 in the CT codec's hot block, 32 in the reference layout).  res[0] += deleted
+// entries, res[1] += tombstones cleared.
+__global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
+                                                       const uint32_t *bits, unsigned long long *res) {
+    const uint64_t nw = (d.mask + 1 + 31) / 32;
+    const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
+    uint32_t dead = 0, tombs = 0;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t m = bits[w];
+        while (m) {
+            const int k = __builtin_ctz(m);
+            m &= m - 1;
+            uint64_t j = w * 32 + k;
+            for (;;) {
+                uint8_t *sl = d.slots + j * d.slot_size;
+                const uint32_t st = sl[d.ksz];
+                if (st == GF_SLOT_EMPTY) break;
+                if (st == GF_SLOT_TOMB) {
+                    sl[d.ksz] = GF_SLOT_EMPTY;
+                    tombs++;
+                } else {
+                    const uint32_t lt = *reinterpret_cast<const uint32_t *>(ht_val(d, j) + lt_off);
+                    if (lt < now) {
+                        sl[d.ksz] = GF_SLOT_EMPTY;
+                        dead++;
+                    } else {
+                        uint32_t kw[10];
+                        const uint32_t nkw = (d.ksz + 3) / 4;
+                        for (uint32_t q = 0; q < 10; q++) kw[q] = 0;
+                        for (uint32_t q = 0; q < d.ksz; q++) kw[q >> 2] |= (uint32_t)sl[q] << (8 * (q & 3));
+                        (void)nkw;
+                        const uint64_t home = gf_home_slot(gf_key_hash(kw, d.ksz, mode), d.mask, d.slot_size);
+                        for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
+                            if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) { gc_move(d, j, p, vstride); break; }
+                        }
+                    }
+                }
+                j = (j + 1) & d.mask;
+            }
+        }
+    }
+    if (dead) atomicAdd(&res[0], (unsigned long long)dead);
+    if (tombs) atomicAdd(&res[1], (unsigned long long)tombs);
+}
+
 // ================================================================ host: programs
 namespace {
 
@@ -1889,7 +1973,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                 return -EIO;
             m->dev_count_hi = dc;
         }
-        if (m->dev_count_hi + 2ull * pkts->n > limit) strict = 1;
+        if (m->dev_count_hi + 2ull * pkts->n > limit) strict |= m == ct4m ? 1u : 2u;
         m->dev_count_hi += 2ull * pkts->n;
         if (m->type == GF_MAP_TYPE_LRU_HASH) {
             if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
@@ -2123,6 +2207,57 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
         return hip_ok(hipGetLastError(), "k_pipe_front");
     };
     return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out);
+}
+
+// ---- conntrack GC ----
+int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto m = get_map(map);
+    if (!m) return -EBADF;
+    if (m->is_lpm() || (m->ksz != 14 && m->ksz != 40) || m->vsz != 48) return -EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
+    if (m->host_valid || !m->dev_valid || !m->d_slots.p) {
+        // host shadow authoritative: delete there, the replica is rebuilt on the next push
+        uint64_t dead = 0;
+        std::vector<std::string> keys;
+        uint8_t v[GF_CT_VSZ];
+        for (uint64_t i = 0; i < m->ht.nslots; i++) {
+            if (m->ht.state(i) != GF_SLOT_FULL) continue;
+            m->ht.get_val(i, v);
+            uint32_t lt;
+            memcpy(&lt, v + lt_off, 4);
+            if (lt < filter_time) keys.emplace_back((const char *)m->ht.key(i), m->ksz);
+        }
+        for (auto &k : keys) if (m->erase((const uint8_t *)k.data()) == 0) dead++;
+        return (int)std::min<uint64_t>(dead, 0x7fffffff);
+    }
+    gf_htab_desc d = m->hdesc();
+    const uint64_t nslots = d.mask + 1, nw = (nslots + 31) / 32;
+    static DevBuf bits, res;
+    if (bits.bytes < nw * 4 && bits.ensure(nw * 4)) return -ENOMEM;
+    if (res.bytes < 16 && res.ensure(16)) return -ENOMEM;
+    if (hip_ok(hipMemsetAsync(res.p, 0, 16, s), "gc res")) return -EIO;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, 65535u * 8);
+    {
+        ProfScope ps("k_gc", s);
+        hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, (uint32_t *)bits.p);
+        hipLaunchKernelGGL(k_gc_clusters, dim3(grid), dim3(BLOCK), 0, s, d, m->ht.mode, lt_off, filter_time,
+                           (const uint32_t *)bits.p, (unsigned long long *)res.p);
+    }
+    if (hip_ok(hipGetLastError(), "k_gc")) return -EIO;
+    unsigned long long r[2] = {0, 0};
+    if (hip_ok(hipMemcpyAsync(r, res.p, 16, hipMemcpyDeviceToHost, s), "gc result") ||
+        hip_ok(hipStreamSynchronize(s), "gc sync"))
+        return -EIO;
+    // device element count: entries are deleted, tombstones were already uncounted
+    uint32_t cnt = 0;
+    if (hip_ok(hipMemcpy(&cnt, m->d_count.p, 4, hipMemcpyDeviceToHost), "gc count")) return -EIO;
+    cnt = cnt >= r[0] ? cnt - (uint32_t)r[0] : 0u;
+    if (hip_ok(hipMemcpy(m->d_count.p, &cnt, 4, hipMemcpyHostToDevice), "gc count")) return -EIO;
+    m->dev_count_hi = cnt;
+    m->device_modified();
+    return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
 
 }  // extern "C"

@@ -4,8 +4,9 @@ CtKey4Global = struct ipv4_ct_tuple (14 B, packed): daddr, saddr, dport(be), spo
 CtKey6Global = struct ipv6_ct_tuple (40 B)
 CtEntry (48 B): rx_packets, rx_bytes, tx_packets, tx_bytes, lifetime u32, flags u16,
                 revnat u16 (network order), unused u16, pad u16, src_sec_id u32
-GC (ctmap.go:277-352) deletes entries whose lifetime < now.  It walks the map
-through the C ABI here; a device-side GC kernel is SURVEY §8(f) row 3.
+GC (ctmap.go:277-352) deletes entries whose lifetime < now; Flush (:354-368)
+deletes every entry.  Both go to gf_ct_gc: a device sweep of the HBM replica
+(with probe-cluster compaction) when the datapath owns the map.
 """
 import errno
 import struct
@@ -62,9 +63,19 @@ def Dump(fd, v6=False):
         key = nk
 
 
+MaxTime = 0xFFFFFFFF
+
+
 def GC(fd, now_sec, v6=False):
-    """doGC4/doGC6 + doFiltering (GCFilterByTime): delete lifetime < now."""
-    dead = [k for k, e in Dump(fd, v6) if e.lifetime < now_sec]
-    for k in dead:
-        bpf.DeleteElement(fd, k)
-    return len(dead)
+    """doGC4/doGC6 + doFiltering (GCFilterByTime): delete lifetime < now; returns
+    the number of entries deleted."""
+    from .._lib import lib
+    rc = lib.gf_ct_gc(fd, now_sec & 0xFFFFFFFF, None)
+    if rc < 0:
+        raise bpf.BPFError(-rc, "Unable to garbage collect CT map")
+    return rc
+
+
+def Flush(fd, v6=False):
+    """ctmap.Flush: GC with filter time MaxTime (every entry)."""
+    return GC(fd, MaxTime, v6)

@@ -342,6 +342,15 @@ typedef struct gf_pipeline_out {   /* 24 B */
 int gf_pipeline_classify(int pipe, const gf_pipe_batch *batch, uint32_t now_sec, gf_pipeline_out *out,
                          uint8_t *new_daddr6, uint8_t *snap_out, void *stream);
 
+/* ---- conntrack garbage collection ----
+ * ctmap.GC(m, name, GCFilterByTime) / ctmap.Flush (pkg/maps/ctmap/ctmap.go:277-368):
+ * deletes every entry of a CT map (key ipv4_ct_tuple 14 B or ipv6_ct_tuple 40 B,
+ * value ct_entry 48 B) whose lifetime < filter_time (Flush: 0xFFFFFFFF) and
+ * returns how many were deleted (or -errno).  Runs on the device replica when the
+ * datapath owns the map (compacting probe clusters in the same sweep), else on the
+ * host shadow.  Synchronous on `stream`. */
+int gf_ct_gc(int map, uint32_t filter_time, void *stream);
+
 /* ---- per-call statistics (device counter block) ---- */
 #define GF_STATS_WORDS 512
 /* Adds the counters of the next classify calls into `dev_counters`

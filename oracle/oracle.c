@@ -1510,3 +1510,25 @@ void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now, o
                       uint8_t *nd6, uint8_t *snap_out) {
     o_pipeline_batch_mt(c, b, now, out, nd6, snap_out, 1);
 }
+
+/* ------------------------------------------------------------------ */
+/* ctmap.GC / Flush, pkg/maps/ctmap/ctmap.go:277-368 (GCFilterByTime): */
+/* delete every entry whose ct_entry.lifetime (offset 32) < t.          */
+/* ------------------------------------------------------------------ */
+typedef struct gc_ctx { uint32_t t, n, cap, ksz; uint8_t *keys; } gc_ctx;
+static void gc_visit(const void *k, const void *v, void *c_) {
+    gc_ctx *c = (gc_ctx *)c_;
+    uint32_t lt; memcpy(&lt, (const uint8_t *)v + 32, 4);
+    if (lt >= c->t) return;
+    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 1024; c->keys = (uint8_t *)realloc(c->keys, (size_t)c->cap * c->ksz); }
+    memcpy(c->keys + (size_t)c->n * c->ksz, k, c->ksz);
+    c->n++;
+}
+uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
+    gc_ctx c = {filter_time, 0, 0, m->ksz, NULL};
+    om_foreach(m, gc_visit, &c);
+    uint32_t dead = 0;
+    for (uint32_t i = 0; i < c.n; i++) if (om_delete(m, c.keys + (size_t)i * c.ksz) == 0) dead++;
+    free(c.keys);
+    return dead;
+}

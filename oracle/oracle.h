@@ -144,6 +144,9 @@ void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_se
 void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_sec, o_pipeline_out *out,
                          uint8_t *nd6, uint8_t *snap_out, uint32_t threads);
 
+/* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
+uint32_t o_ct_gc(om_map *m, uint32_t filter_time);
+
 /* Shard of a CT key (unordered address pair), exposed for pre-population. */
 uint32_t o_ct_pair_hash4(uint32_t a, uint32_t b);
 uint32_t o_ct_pair_hash6(const uint8_t *a, const uint8_t *b);

@@ -79,6 +79,7 @@ _s("o_set_node", None, C.POINTER(o_node_cfg))
 _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
 _s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32)
+_s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
 _s("o_lpm4_iter_lookup", C.c_int, C.c_uint32, VP, C.c_int, C.c_uint32)
@@ -126,6 +127,9 @@ class OMap:
 
     def count(self):
         return lib.om_count(self.ptr)
+
+    def ct_gc(self, filter_time):
+        return lib.o_ct_gc(self.ptr, filter_time)
 
     def dump(self):
         n = self.count()

@@ -73,6 +73,9 @@ class OracleDP:
                                           C.pointer(self._nd), self.arr)
         return O.pipeline(self._pipe, self.batch(pk), now, threads)
 
+    def ct_gc(self, name, filter_time):
+        return self.m[name].ct_gc(filter_time)
+
     def dump(self, name):
         return self.m[name].dump()
 

@@ -180,3 +180,36 @@ def test_pipeline_checksum_rewrites():
     ro, rn6, rs = ref.pipeline(pk, sc.now)
     _cmp_struct(to_numpy(out, PIPE_OUT), ro, "pipeline")
     assert np.array_equal(snap.cpu().numpy(), rs)
+
+
+def test_ct_gc_device_sweep_then_traffic():
+    """ctmap.GC on the device replica (expired entries and ct_delete tombstones
+    removed, probe clusters compacted) equals the oracle's doGC4/doGC6, and the
+    traffic after it still sees exactly the reference's CT state."""
+    import ctypes as C
+    from cilium_amd._lib import lib
+    sc = synth.fuzz(seed=5, n_packets=20000, n_batches=4)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run(bi, now):
+        pk = sc.batches[bi]
+        io = dp.ingress(DeviceBatch(pk), now)
+        torch.cuda.synchronize()
+        _cmp_struct(to_numpy(io, ING_OUT), ref.ingress(pk, now), f"ingress b{bi}")
+
+    run(0, sc.now)
+    run(1, sc.now + 1)
+    for name in ("ct4", "ct6"):
+        got = lib.gf_ct_gc(dp.fd[name], sc.now + 11, st)
+        assert got == ref.ct_gc(name, sc.now + 11) and got > 0, name
+        assert dp.dump_map(name) == ref.dump(name), name
+    run(2, sc.now + 200)
+    for name in ("ct4", "ct6"):
+        got = lib.gf_ct_gc(dp.fd[name], sc.now + 301, st)
+        assert got == ref.ct_gc(name, sc.now + 301), name
+    run(3, sc.now + 400)
+    for name in ("ct4", "ct6"):
+        assert dp.dump_map(name) == ref.dump(name), name
+    assert lib.gf_ct_gc(dp.fd["ct4"], 0xFFFFFFFF, st) == ref.ct_gc("ct4", 0xFFFFFFFF)
+    assert dp.dump_map("ct4") == {} == ref.dump("ct4")

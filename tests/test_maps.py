@@ -177,3 +177,30 @@ def test_batch_update_matches_sequential():
     ma, mb = bpf.Map("a", 1, 14, 48, 1000), bpf.Map("b", 1, 14, 48, 1000)
     ma.fd, mb.fd = a, b
     assert ma.Dump() == mb.Dump()
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_ctmap_gc_and_flush_host_shadow(v6):
+    """ctmap.GC (GCFilterByTime: lifetime < now) and Flush through gf_ct_gc on a
+    host-authoritative map, against the oracle's restatement of doGC4/doGC6."""
+    rng = random.Random(7 + v6)
+    fd, _ = ctmap.OpenMap(bpf.MapPath(f"test_gc_{int(v6)}"), v6=v6, max_entries=5000)
+    om = O.OMap(9, 40 if v6 else 14, 48, 5000)
+    for i in range(3000):
+        if v6:
+            k = ctmap.ct_key6(rng.randbytes(16), rng.randbytes(16), rng.getrandbits(16), rng.getrandbits(16), 6, i & 1)
+        else:
+            k = ctmap.ct_key4(rng.getrandbits(32), rng.getrandbits(32), rng.getrandbits(16), rng.getrandbits(16), 6,
+                              i & 3)
+        v = ctmap.ct_entry(rx_packets=i, lifetime=rng.choice([0, 5, 99, 100, 101, 43300]), flags=16)
+        bpf.UpdateElement(fd, k, v)
+        assert om.update(k, v) == 0
+    want = O.lib.o_ct_gc(om.ptr, 100)
+    got = ctmap.GC(fd, 100, v6=v6)
+    assert got == want > 0
+    left = dict(ctmap.Dump(fd, v6))
+    assert set(left) == set(om.dump())
+    assert all(e.lifetime >= 100 for e in left.values())
+    assert ctmap.Flush(fd, v6=v6) == len(left)
+    assert ctmap.Dump(fd, v6) == []
+    bpf.ObjClose(fd)
