@@ -140,7 +140,7 @@ def bench_config2(args, dev, rank, world):
     ab_per_launch = float(lc[270]) / max(K, 1)
     achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = traffic_src = None
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary*.json")))
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
     if pmc:
         try:
             j = json.load(open(pmc[-1]))
@@ -264,16 +264,20 @@ def bench_config1(args, dev):
     W, K = 5, 50
     el, c, _, kern = timed(step, W, K, dev)
     threads = min(16, os.cpu_count() or 1)
-    ref = OracleDP(sc)
-    bt = ref.batch(pk)
-    from oracle import oracle as O
-    done, tt = cpu_loop(lambda: (O.xdp(ref.xdp_cfg, bt, threads), pk.n)[1], args.cpu_seconds / 4)
+    cpu = None
+    if not args.no_cpu:
+        ref = OracleDP(sc)
+        bt = ref.batch(pk)
+        from oracle import oracle as O
+        done, tt = cpu_loop(lambda: (O.xdp(ref.xdp_cfg, bt, threads), pk.n)[1], args.cpu_seconds / 4)
+        cpu = {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
+               "sample": f"{done} packets (the same 1M-packet batch, repeated)"}
     return {"workload": "config1: bpf_xdp CIDR prefilter (10k LPM prefixes + 2k /32, 1025 endpoints), 1M packets/step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "packets_per_step": int(c[268]) // K, "warmup": W,
             "roofline": roofline(kern, ["k_xdp"], float(c[270]) / K, "k_xdp"), "kernels_ms_per_step": kms(kern),
             "verdicts": {"pass": int(c[258]), "drop": int(c[257])},
-            "cpu_baseline": {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-                             "sample": f"{done} packets (the same 1M-packet batch, repeated)"}}
+            "cpu_baseline": cpu}
 
 
 def bench_config3(args, dev):
@@ -296,18 +300,22 @@ def bench_config3(args, dev):
     W, K = 3, 10
     el, c, _, kern = timed(step, W, K, dev)
     threads = min(16, os.cpu_count() or 1)
-    ref = OracleDP(sc)
-    sub = pk.slice(0, 2_000_000)
-    bt = ref.batch(sub)
-    from oracle import oracle as O
-    done, tt = cpu_loop(lambda: (O.lb(ref.lb_cfg, bt, threads), sub.n)[1], args.cpu_seconds / 4)
+    cpu = None
+    if not args.no_cpu:
+        ref = OracleDP(sc)
+        sub = pk.slice(0, 2_000_000)
+        bt = ref.batch(sub)
+        from oracle import oracle as O
+        done, tt = cpu_loop(lambda: (O.lb(ref.lb_cfg, bt, threads), sub.n)[1], args.cpu_seconds / 4)
+        cpu = {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
+               "sample": f"{done} packets (the first 2M packets of the batch, repeated)"}
     return {"workload": "config3: bpf_lb lb4_lookup_service + slave select, 100k services / ~1M backends, "
                         "16M packets/step (Zipf 1.1)",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "packets_per_step": int(c[268]) // K, "warmup": W,
             "roofline": roofline(kern, ["k_lb"], float(c[270]) / K, "k_lb"), "kernels_ms_per_step": kms(kern),
             "verdicts": verdicts(c),
-            "cpu_baseline": {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-                             "sample": f"{done} packets (the first 2M packets of the batch, repeated)"}}
+            "cpu_baseline": cpu}
 
 
 # ----------------------------------------------------------------------------- config 4 (full pipeline)
@@ -345,7 +353,19 @@ def bench_config4(args, dev):
     el, c, _, kern = timed(lambda s: dp.pipeline(fbs[s], sc.now + s, out=out[: fbs[s].n], snap_out=False),
                            W, K, dev)
     names = [k for k in kern]
-    # CPU: the oracle pipeline on the flows of 1/8 of the address pairs, after the same warm-up
+    cpu = None if args.no_cpu else cpu_config4(args, sc, frames, W, K)
+    return {"workload": "config4: bpf_xdp -> bpf_lb -> bpf_netdev delivery -> handle_policy over raw 64-B frames "
+                        "(config-2 stream, 30% of pairs via service VIPs; 10k-prefix prefilter), 16.8M packets/step",
+            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "packets_per_step": int(c[268]) // K, "warmup": W,
+            "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)"),
+            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu}
+
+
+def cpu_config4(args, sc, frames, W, K):
+    """The oracle pipeline on the flows of 1/8 of the address pairs, after the same warm-up."""
+    from cilium_amd.synth import Packets
+    from oracle.scenario import OracleDP
     threads = min(16, os.cpu_count() or 1)
     ref = OracleDP(sc, shards=threads)
 
@@ -366,13 +386,8 @@ def bench_config4(args, dev):
         done += pk.n
         if tt >= args.cpu_seconds / 2:
             break
-    return {"workload": "config4: bpf_xdp -> bpf_lb -> bpf_netdev delivery -> handle_policy over raw 64-B frames "
-                        "(config-2 stream, 30% of pairs via service VIPs; 10k-prefix prefilter), 16.8M packets/step",
-            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
-            "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)"),
-            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c),
-            "cpu_baseline": {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-                             "sample": f"{done} packets (flows of 1/8 of the address pairs, same warm-up)"}}
+    return {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
+            "sample": f"{done} packets (flows of 1/8 of the address pairs, same warm-up)"}
 
 
 # ----------------------------------------------------------------------------- config 5 (IPv6 ingress)
@@ -395,6 +410,21 @@ def bench_config5(args, dev):
     out = torch.empty((max(b.n for b in batches), 8), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     el, c, _, kern = timed(lambda s: dp.ingress(batches[s], sc.now + s, out=out[: batches[s].n]), W, K, dev)
+    cpu = None if args.no_cpu else cpu_config5(sc, st, W, K, S0)
+    return {"workload": "config5: bpf_lxc ingress over IPv6 (ct_lookup6 + policy), 1M new flows/step "
+                        "(4.2M packets/step), CT capacity 10,485,760 (LRU)",
+            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "packets_per_step": int(c[268]) // K, "warmup": W,
+            "roofline": roofline(kern, ["k_ing_groups6", "k_ing_groups"], float(c[270]) / K,
+                                 "k_ing_groups<6> (+ <4> for packets without an IPv6 header)"),
+            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu}
+
+
+def cpu_config5(sc, st, W, K, S0):
+    """The oracle on the IPv6 flows of 1/8 of the address pairs, after the same warm-up."""
+    from cilium_amd import stream
+    from cilium_amd.synth import Packets
+    from oracle.scenario import OracleDP
     threads = min(16, os.cpu_count() or 1)
     ref = OracleDP(sc, shards=threads)
 
@@ -416,17 +446,29 @@ def bench_config5(args, dev):
         ref.ingress(pk, sc.now + s, threads=threads)
         tt += time.perf_counter() - a
         done += pk.n
-    return {"workload": "config5: bpf_lxc ingress over IPv6 (ct_lookup6 + policy), 1M new flows/step "
-                        "(4.2M packets/step), CT capacity 10,485,760 (LRU)",
-            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
-            "roofline": roofline(kern, ["k_ing_groups6", "k_ing_groups"], float(c[270]) / K,
-                                 "k_ing_groups<6> (+ <4> for packets without an IPv6 header)"),
-            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c),
-            "cpu_baseline": {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-                             "sample": f"{done} packets (flows of 1/8 of the address pairs, same warm-up)"}}
+    return {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": threads, "kind": "port",
+            "sample": f"{done} packets (flows of 1/8 of the address pairs, same warm-up)"}
 
 
 EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_config5}
+
+
+def add_traffic(cfg, r):
+    """roofline.traffic of configuration `cfg` from its committed PMC summary
+    (profiles/*pmc_summary_c<cfg>.json: FETCH_SIZE + WRITE_SIZE per launch of the
+    roofline kernels, tools/pmc_summary.py), scaled per packet to this run."""
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_summary_c{cfg}.json")))
+    if not pmc or "roofline" not in r:
+        return r
+    try:
+        j = json.load(open(pmc[-1]))
+        ppl = float(j["packets_per_launch"])
+        if ppl > 0 and j.get("traffic_bytes_per_launch"):
+            r["roofline"]["traffic"] = j["traffic_bytes_per_launch"] * (r["packets_per_step"] / ppl)
+            r["roofline"]["traffic_source"] = os.path.relpath(pmc[-1], ROOT)
+    except Exception:
+        pass
+    return r
 
 
 def main():
@@ -462,7 +504,7 @@ def main():
             for k, fn in EXTRA.items():
                 t0 = time.time()
                 try:
-                    res["configs"][k] = fn(args, dev)
+                    res["configs"][k] = add_traffic(k, fn(args, dev))
                 except Exception as e:                       # reported, never silently dropped
                     res["configs"][k] = {"error": f"{type(e).__name__}: {e}"}
                 log(f"config {k}: {res['configs'][k].get('mpps')} Mpps ({time.time() - t0:.1f}s)")
@@ -470,10 +512,11 @@ def main():
     else:
         if world > 1:
             raise SystemExit("--config other than 2 runs on one GPU")
-        r = EXTRA[args.config](args, dev)
+        r = add_traffic(args.config, EXTRA[args.config](args, dev))
         res = {"metric": METRIC, "value": r["mpps"], "unit": "Mpps", "n_gpus": 1, "steps": r["steps"],
-               "warmup": None, "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "u32", "data": "synthetic", "config": {"workload": r["workload"]},
+               "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+               "config": {"workload": r["workload"], "packets_per_step": r["packets_per_step"]},
                "roofline": r["roofline"], "kernels_ms_per_step": r["kernels_ms_per_step"],
                "cpu_baseline": r["cpu_baseline"]}
     if rank == 0:

@@ -38,16 +38,40 @@ def per_launch(path, nsteps):
     return out
 
 
+def per_step(path, names, nsteps):
+    """Counters summed over every dispatch of the kernels matching `names`
+    (substrings; "gpuflow" = every libgpuflow kernel: k_* and its rocPRIM
+    instantiations), divided by the number of bench steps the process ran."""
+    out = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"]
+        short = name.split("(")[0]
+        ok = any((n == "gpuflow" and (" k_" in " " + short.replace("void ", "") or "ROCPRIM_400200" in name))
+                 or (n != "gpuflow" and n in short) for n in names)
+        if ok:
+            out[r["Counter_Name"]] += float(r["Counter_Value"]) / nsteps
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--packets", type=int, default=16777216, help="packets per launch (bench config 2)")
+    ap.add_argument("--kernels", default=None,
+                    help="per-step mode: comma list of kernel-name substrings summed over all their dispatches")
+    ap.add_argument("--nsteps", type=int, default=0, help="per-step mode: bench steps run (warm-up + timed)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
+    global KERNEL
     c = {}
     for f in glob.glob(os.path.join(a.dir, "*", "run_counter_collection.csv")):
-        c.update(per_launch(f, a.steps))
+        if a.kernels:
+            c.update(per_step(f, a.kernels.split(","), a.nsteps))
+        else:
+            c.update(per_launch(f, a.steps))
+    if a.kernels:
+        KERNEL = a.kernels
     n = a.packets
     fetch = c.get("FETCH_SIZE", 0.0) * 1024
     write = c.get("WRITE_SIZE", 0.0) * 1024

@@ -1,34 +1,42 @@
 #!/bin/bash
-# Round profile of the bench workload (run from the repo root on the GPU box):
-#   1. rocprofv3 --kernel-trace --stats over bench.py (per-kernel durations)
+# Round profile of the bench workloads (run from the repo root on the GPU box):
+#   1. rocprofv3 --kernel-trace --stats, one process per BASELINE configuration
+#      (config 2 = the headline line; 1, 3, 4, 5 = the "configs" entries)
 #   2. --pmc passes, one counter group per run (MI355X guide: FETCH_SIZE and
-#      WRITE_SIZE in separate passes), for the k_ing_groups byte/request mix
-#   3. primbench under FETCH_SIZE / WRITE_SIZE / EA requests (calibration)
+#      WRITE_SIZE in separate passes): the k_ing_groups request mix of config 2,
+#      FETCH/WRITE of the roofline kernels of configs 1, 3, 4, 5
 #   tools/profile_round.sh <tag>      -> gpurun_out/prof_<tag>/
 set -e
 T=${1:-r1}
 R=$(pwd)
 O=$R/gpurun_out/prof_$T
-mkdir -p "$O" "$O/pmc" "$O/cal"
+mkdir -p "$O" "$O/pmc"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks" -o run -- \
-    python "$R/bench.py" --no-cpu --steps 4 > "$O/ks_bench.json" 2> "$O/ks_bench.err"
-echo "kernel stats done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks2" -o run -- \
+    python "$R/bench.py" --no-cpu --no-extra > "$O/ks2.json" 2> "$O/ks2.err"
+echo "kernel stats config 2 done"
+for C in 1 3 4 5; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks$C" -o run -- \
+      python "$R/bench.py" --no-cpu --config $C > "$O/ks$C.json" 2> "$O/ks$C.err"
+  echo "kernel stats config $C done"
+done
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "TCC_EA0_ATOMIC_sum" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d "$O/pmc/p$i" -o run -- \
-      python "$R/bench.py" --no-cpu --steps 2 --warmup 3 > "$O/pmc/p$i.json" 2> "$O/pmc/p$i.err"
-  echo "pmc pass $i done"
+  timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d "$O/pmc/c2/p$i" -o run -- \
+      python "$R/bench.py" --no-cpu --no-extra --steps 2 --warmup 3 > "$O/pmc/c2p$i.json" 2> "$O/pmc/c2p$i.err"
+  echo "config 2 pmc pass $i done"
 done
-i=0
-for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
-  i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d "$O/cal/p$i" -o run -- "$R/tools/_bin/primbench" \
-      > "$O/cal/p$i.txt" 2>&1
-  echo "calibration pass $i done"
+for C in 1 3 4 5; do
+  i=0
+  for P in "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    timeout -s KILL 200 rocprofv3 --pmc $P --output-format csv -d "$O/pmc/c$C/p$i" -o run -- \
+        python "$R/bench.py" --no-cpu --config $C > "$O/pmc/c${C}p$i.json" 2> "$O/pmc/c${C}p$i.err"
+    echo "config $C pmc pass $i done"
+  done
 done
 cd "$R"
-python tools/pmc_summary.py "$O/pmc" --steps 2 --out "$O/pmc_summary.json" > /dev/null
-python tools/kstats.py "$O/ks/run_kernel_stats.csv" 8 > "$O/kstats.txt"
+python tools/pmc_summary.py "$O/pmc/c2" --steps 2 --out "$O/pmc_summary.json" > /dev/null
+python tools/kstats.py "$O/ks2/run_kernel_stats.csv" 12 > "$O/kstats.txt"
 echo "summaries done"
