@@ -100,6 +100,13 @@ class gf_pipe_batch(C.Structure):
     _fields_ = [("frames", gf_frames), ("tc_index", C.c_void_p), ("flow_hash", C.c_void_p)]
 
 
+class gf_event_ring(C.Structure):
+    _fields_ = [("records", C.c_void_p), ("capacity", C.c_uint32), ("count", C.c_void_p)]
+
+
+GF_EVENT_RECORD = 160
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -133,6 +140,7 @@ _sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c
 _sig("gf_pipeline_load", C.c_int, C.POINTER(gf_pipeline_cfg))
 _sig("gf_pipeline_classify", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, VP, VP, VP, VP)
 _sig("gf_ct_gc", C.c_int, C.c_int, C.c_uint32, VP)
+_sig("gf_set_event_ring", C.c_int, C.POINTER(gf_event_ring))
 _sig("gf_set_stats_sink", C.c_int, VP)
 _sig("gf_prof_enable", C.c_int, C.c_int)
 _sig("gf_prof_read", C.c_int, C.POINTER(gf_prof_rec), C.c_int)
@@ -151,6 +159,6 @@ EXPORTED = [
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_ct_gc", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_ct_gc", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
 ]

@@ -1644,6 +1644,81 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
     if (tombs) atomicAdd(&res[1], (unsigned long long)tombs);
 }
 
+// ================================================================ drop notifications
+// send_drop_notify / __send_drop_notify (bpf/lib/drop.h:47-107, DROP_NOTIFY): one
+// struct drop_notify (32 B, pkg/monitor DropNotify) + up to TRACE_PAYLOAD_LEN
+// captured bytes per dropped packet, appended to the event ring in batch order
+// (per-block counts, an exclusive scan, then a block-local scan for the slots).
+struct EvSrc {
+    const uint8_t *recs;      // per-packet verdict records
+    uint32_t stride, act_off; // record stride, offset of action (reason follows)
+    int32_t stage_off;        // pipeline: offset of the stage byte (-1: ingress records)
+    const gf_rec *prec;       // handle_policy inputs (src_identity, ifindex, program slot)
+    const gf_lxc_dev *cfgs;   // endpoint programs (LXC_ID, SECLABEL)
+    const uint32_t *len, *flow_hash;
+    const uint8_t *snap;      // frames to capture from (may be null)
+    uint32_t snap_stride, n;
+};
+__device__ __forceinline__ bool ev_dropped(const EvSrc &E, uint32_t i) {
+    const uint8_t *r = E.recs + (size_t)i * E.stride;
+    return r[E.act_off] == TC_SHOT && (E.stage_off < 0 || r[E.stage_off] != GF_STAGE_XDP);
+}
+__global__ __launch_bounds__(BLOCK) void k_ev_count(EvSrc E, uint32_t *blk) {
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < E.n && ev_dropped(E, i)) atomicAdd(&c, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) blk[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(BLOCK) void k_ev_write(EvSrc E, const uint32_t *boff, gf_event_ring R) {
+    __shared__ uint32_t sc[BLOCK];
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool d = i < E.n && ev_dropped(E, i);
+    sc[threadIdx.x] = d ? 1u : 0u;
+    __syncthreads();
+    for (uint32_t o = 1; o < BLOCK; o <<= 1) {          // inclusive scan
+        uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
+        __syncthreads();
+        sc[threadIdx.x] += v;
+        __syncthreads();
+    }
+    if (!d) return;
+    const uint64_t pos = (uint64_t)*R.count + boff[blockIdx.x] + sc[threadIdx.x] - 1;
+    if (pos >= R.capacity) return;                      // ring full: the record is lost
+    const uint8_t *r = E.recs + (size_t)i * E.stride;
+    const uint32_t reason = r[E.act_off + 1];
+    uint32_t src = 0, dst = 0, dst_id = 0, ifx = 0, source = 0;
+    const bool policy = E.stage_off < 0 || r[E.stage_off] == GF_STAGE_POLICY;
+    if (policy) {
+        const gf_rec pr = E.prec[i];
+        if (pr.ep) {                                    // handle_policy: send_drop_notify(src_label, SECLABEL, LXC_ID, ifindex)
+            const gf_lxc_dev &cf = E.cfgs[pr.ep - 1];
+            src = pr.src_identity & 0xffffu; dst = cf.seclabel & 0xffffu;
+            dst_id = cf.lxc_id; ifx = pr.ifindex; source = cf.lxc_id & 0xffffu;
+        }                                               // else the caller's send_drop_notify_error: zeros
+    }
+    const uint32_t len = E.len[i];
+    const uint32_t cap = len < GF_TRACE_PAYLOAD_LEN ? len : GF_TRACE_PAYLOAD_LEN;
+    uint32_t *w = reinterpret_cast<uint32_t *>(R.records + pos * GF_EVENT_RECORD);
+    w[0] = 1u /* CILIUM_NOTIFY_DROP */ | (reason << 8) | (source << 16);
+    w[1] = E.flow_hash ? E.flow_hash[i] : 0u;             // get_hash_recalc(skb)
+    w[2] = len; w[3] = cap; w[4] = src; w[5] = dst; w[6] = dst_id; w[7] = ifx;
+    const uint8_t *f = E.snap ? E.snap + (size_t)i * E.snap_stride : nullptr;
+    for (uint32_t k = 0; k < GF_TRACE_PAYLOAD_LEN / 4; k++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; b++) {
+            const uint32_t off = 4 * k + b;
+            if (f && off < cap && off < E.snap_stride) v |= (uint32_t)f[off] << (8 * b);
+        }
+        w[8 + k] = v;
+    }
+}
+__global__ void k_ev_commit(const uint32_t *boff, const uint32_t *blk, uint32_t nb, gf_event_ring R) {
+    *R.count += boff[nb - 1] + blk[nb - 1];
+}
+
 // ================================================================ host: programs
 namespace {
 
@@ -1690,6 +1765,7 @@ struct Workspace {
     DevBuf rec, keys, skeys, perm, cnt, off, tmp, sched, order;
 };
 Workspace &ws() { static Workspace w; return w; }
+gf_event_ring &event_ring() { static gf_event_ring r{}; return r; }
 struct PipeWs {
     DevBuf s6, d6;             // IPv6 addresses of the rewritten frames (read by handle_policy)
 };
@@ -1851,6 +1927,14 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
     return new_handle(p);
 }
 
+int gf_set_event_ring(const gf_event_ring *ring) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    if (!ring) { event_ring() = gf_event_ring{}; return 0; }
+    if (!ring->records || !ring->count) return -EFAULT;
+    event_ring() = *ring;
+    return 0;
+}
+
 int gf_prof_enable(int on) {
     std::lock_guard<std::recursive_mutex> g(big_lock());
     prof_drain();
@@ -1898,11 +1982,35 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 
 // handle_policy over a batch (caller holds big_lock and checked the columns).
 // skip (DEVICE, may be null): packets a pipeline ended before the tail call.
+// Drop notifications of one classify call (no-op without an event ring).
+static int emit_drop_events(EvSrc E, hipStream_t s) {
+    gf_event_ring R = event_ring();
+    if (!R.records || !R.count || !R.capacity || E.n == 0) return 0;
+    static DevBuf blk, boff, tmp;
+    const uint32_t nb = (E.n + BLOCK - 1) / BLOCK;
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    int r;
+    if ((r = grow(blk, (size_t)nb * 4)) || (r = grow(boff, (size_t)nb * 4))) return r;
+    size_t tb = 0;
+    (void)rocprim::exclusive_scan(nullptr, tb, (uint32_t *)blk.p, (uint32_t *)boff.p, 0u, nb, rocprim::plus<uint32_t>(), s);
+    if ((r = grow(tmp, tb + 256))) return r;
+    ProfScope ps("k_drop_events", s);
+    hipLaunchKernelGGL(k_ev_count, dim3(nb), dim3(BLOCK), 0, s, E, (uint32_t *)blk.p);
+    tb = tmp.bytes;
+    if (hip_ok(rocprim::exclusive_scan(tmp.p, tb, (uint32_t *)blk.p, (uint32_t *)boff.p, 0u, nb,
+                                       rocprim::plus<uint32_t>(), s), "event scan"))
+        return -EIO;
+    hipLaunchKernelGGL(k_ev_write, dim3(nb), dim3(BLOCK), 0, s, E, (const uint32_t *)boff.p, R);
+    hipLaunchKernelGGL(k_ev_commit, dim3(1), dim3(1), 0, s, (const uint32_t *)boff.p, (const uint32_t *)blk.p, nb, R);
+    return hip_ok(hipGetLastError(), "k_drop_events");
+}
+
 // pack (may be empty): fills the records and bucket keys itself (the fused
 // pipeline front) instead of k_ing_pack; pout: pipeline records to complete.
 using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
-                       gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr) {
+                       gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
+                       const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -2092,6 +2200,15 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
+    {
+        EvSrc E{};
+        E.recs = pout ? pout : (const uint8_t *)out;
+        E.stride = pout ? 24u : 8u; E.act_off = pout ? 1u : 0u; E.stage_off = pout ? 0 : -1;
+        E.prec = (const gf_rec *)w.rec.p; E.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
+        E.len = ev_len ? ev_len : pkts->len; E.flow_hash = pkts->flow_hash; E.n = n;
+        E.snap = ev_snap; E.snap_stride = ev_stride;
+        if ((r = emit_drop_events(E, s))) return r;
+    }
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
@@ -2206,7 +2323,9 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
                                slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.d6.p, out, nd6, snap_out, sink);
         return hip_ok(hipGetLastError(), "k_pipe_front");
     };
-    return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out);
+    c2.flow_hash = b->flow_hash;
+    return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out, fr.len,
+                       snap_out ? snap_out : fr.snap, fr.snap_stride);
 }
 
 // ---- conntrack GC ----

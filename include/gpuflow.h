@@ -351,6 +351,25 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *batch, uint32_t now_sec,
  * host shadow.  Synchronous on `stream`. */
 int gf_ct_gc(int map, uint32_t filter_time, void *stream);
 
+/* ---- drop notifications (bpf/lib/drop.h:38-107, DROP_NOTIFY) ----
+ * With a ring set, gf_policy_ingress_classify and gf_pipeline_classify append
+ * one record per dropped packet (TC_ACT_SHOT; XDP drops send none), in batch
+ * order: struct drop_notify (32 B: type CILIUM_NOTIFY_DROP=1, subtype = drop
+ * reason, source = EVENT_SOURCE, hash, len_orig, len_cap, src_label, dst_label,
+ * dst_id, ifindex — the layout pkg/monitor/datapath_drop.go DropNotify decodes)
+ * followed by GF_TRACE_PAYLOAD_LEN bytes holding the first len_cap bytes of the
+ * frame (the pipeline's frames; zeros for column batches, which carry none).
+ * *count accumulates across calls; records past `capacity` are lost (a perf ring
+ * overrun). */
+#define GF_TRACE_PAYLOAD_LEN 128u   /* TRACE_PAYLOAD_LEN, bpf/lib/common.h:213-215 */
+#define GF_EVENT_RECORD 160u
+typedef struct gf_event_ring {
+    uint8_t  *records;         /* DEVICE, capacity * GF_EVENT_RECORD bytes */
+    uint32_t  capacity;        /* records */
+    uint32_t *count;           /* DEVICE u32: records appended so far */
+} gf_event_ring;
+int gf_set_event_ring(const gf_event_ring *ring);   /* NULL disables */
+
 /* ---- per-call statistics (device counter block) ---- */
 #define GF_STATS_WORDS 512
 /* Adds the counters of the next classify calls into `dev_counters`

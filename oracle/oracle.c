@@ -1124,6 +1124,25 @@ typedef struct mt_arg {
 static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i, uint8_t *row, o_pipeline_out *o,
                            uint8_t *nd6, uint32_t *secctx, uint32_t *ifx, uint16_t *lxcid, uint8_t *skip);
 
+/* send_drop_notify + __send_drop_notify, bpf/lib/drop.h:47-107: the 32-B struct
+ * drop_notify followed by the first len_cap (<= TRACE_PAYLOAD_LEN) frame bytes. */
+#define O_EVENT_RECORD 160
+static void drop_event(uint8_t *ev, int reason, uint32_t source, uint32_t hash, uint32_t len, uint32_t src,
+                       uint32_t dst, uint32_t dst_id, uint32_t ifindex, const uint8_t *frame, uint32_t frame_bytes) {
+    memset(ev, 0, O_EVENT_RECORD);
+    uint32_t cb1 = (src << 16) | (dst & 0xFFFF);        /* skb->cb[1] */
+    uint32_t cap = len < 128 ? len : 128;                /* min(TRACE_PAYLOAD_LEN, skb->len) */
+    int error = reason < 0 ? -reason : reason;
+    uint16_t src16 = (uint16_t)source;
+    uint32_t f[6] = {len, cap, cb1 >> 16, cb1 & 0xFFFF, dst_id, ifindex};
+    ev[0] = 1;                                           /* CILIUM_NOTIFY_DROP */
+    ev[1] = (uint8_t)error;
+    memcpy(ev + 2, &src16, 2);
+    memcpy(ev + 4, &hash, 4);
+    memcpy(ev + 8, f, 24);
+    if (frame) memcpy(ev + 32, frame, cap < frame_bytes ? cap : frame_bytes);
+}
+
 static uint32_t pkt_group(const o_batch *b, uint32_t i) {
     const uint8_t *d = b->snap + (size_t)i * b->snap_stride;
     uint32_t len = b->len[i], cap = b->snap_stride < len ? b->snap_stride : len;
@@ -1474,7 +1493,7 @@ static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i
 }
 
 void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now, o_pipeline_out *out,
-                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads) {
+                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads, uint8_t *events) {
     if (threads < 1) threads = 1;
     uint32_t n = b->n;
     uint8_t *snap = snap_out ? snap_out : (uint8_t *)malloc((size_t)n * b->snap_stride + 1);
@@ -1497,18 +1516,31 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
         }
     }
     for (uint32_t i = 0; i < n; i++) {
-        if (skip[i]) continue;
         o_pipeline_out *o = &out[i];
-        if (!c->policy) { o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL); continue; }
-        o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
-        o->flags |= ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
+        if (!skip[i]) {
+            if (!c->policy) { o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL); }
+            else {
+                o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
+                o->flags |= ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
+            }
+        }
+        if (!events) continue;
+        uint8_t *e = events + (size_t)i * O_EVENT_RECORD;
+        memset(e, 0, O_EVENT_RECORD);
+        if (o->action != TC_ACT_SHOT || o->stage == 1) continue;
+        const uint8_t *row = snap + (size_t)i * b->snap_stride;
+        uint32_t hash = b->flow_hash ? b->flow_hash[i] : 0, len = b->len[i];
+        const o_lxc_cfg *lc = (o->stage == 4 && c->policy) ? c->policy->slot[lxcid[i]] : NULL;
+        if (lc) drop_event(e, o->reason, lc->lxc_id, hash, len, secctx[i], lc->seclabel, lc->lxc_id, ifx[i], row,
+                           b->snap_stride);
+        else drop_event(e, o->reason, 0, hash, len, 0, 0, 0, 0, row, b->snap_stride);
     }
     if (!snap_out) free(snap);
     free(skip); free(secctx); free(ifx); free(lxcid); free(ing);
 }
 void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now, o_pipeline_out *out,
                       uint8_t *nd6, uint8_t *snap_out) {
-    o_pipeline_batch_mt(c, b, now, out, nd6, snap_out, 1);
+    o_pipeline_batch_mt(c, b, now, out, nd6, snap_out, 1, NULL);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1531,4 +1563,20 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
     for (uint32_t i = 0; i < c.n; i++) if (om_delete(m, c.keys + (size_t)i * c.ksz) == 0) dead++;
     free(c.keys);
     return dead;
+}
+
+/* Drop notifications of an ingress batch: one record per dropped packet, in
+ * the packet's slot (ev: n * O_EVENT_RECORD, zero for the others).  Column
+ * batches carry no frame bytes to capture. */
+void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_out *out, uint8_t *ev) {
+    for (uint32_t i = 0; i < b->n; i++) {
+        uint8_t *e = ev + (size_t)i * O_EVENT_RECORD;
+        memset(e, 0, O_EVENT_RECORD);
+        if (out[i].action != TC_ACT_SHOT) continue;
+        uint32_t hash = b->flow_hash ? b->flow_hash[i] : 0, len = b->len[i];
+        const o_lxc_cfg *c = a->slot[(b->lxc_id ? b->lxc_id[i] : 0) & 0xffff];
+        if (c) drop_event(e, out[i].reason, c->lxc_id, hash, len, b->src_identity ? b->src_identity[i] : 0,
+                          c->seclabel, c->lxc_id, b->ifindex ? b->ifindex[i] : 0, NULL, 0);
+        else drop_event(e, out[i].reason, 0, hash, len, 0, 0, 0, 0, NULL, 0);   /* caller's send_drop_notify_error */
+    }
 }

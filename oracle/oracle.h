@@ -142,7 +142,11 @@ typedef struct o_pipeline_out {     /* == gf_pipeline_out (24 B) */
 void o_pipeline_batch(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_sec, o_pipeline_out *out,
                       uint8_t *nd6, uint8_t *snap_out);
 void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now_sec, o_pipeline_out *out,
-                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads);
+                         uint8_t *nd6, uint8_t *snap_out, uint32_t threads, uint8_t *events);
+/* Drop notifications (bpf/lib/drop.h:47-107): events holds n records of 160 B
+ * (struct drop_notify + up to 128 captured bytes), a packet's record in its
+ * slot, zero where the packet was not dropped. */
+void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_out *out, uint8_t *events);
 
 /* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time);

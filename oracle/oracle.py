@@ -78,7 +78,8 @@ _s("o_prog_array_set", None, VP, C.c_uint32, C.POINTER(o_lxc_cfg))
 _s("o_set_node", None, C.POINTER(o_node_cfg))
 _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
-_s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32)
+_s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32, VP)
+_s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
@@ -212,11 +213,21 @@ def ingress(prog_array, b, now, threads=1):
     return out
 
 
-def pipeline(cfg, b, now, threads=1):
-    """o_pipeline_batch_mt: returns (records, new_daddr6, rewritten snaps)."""
+def pipeline(cfg, b, now, threads=1, events=False):
+    """o_pipeline_batch_mt: returns (records, new_daddr6, rewritten snaps[, drop events in batch order])."""
     out = np.zeros(b.n, PIPE_OUT)
     nd6 = np.zeros((b.n, 16), np.uint8)
     snap = np.zeros((b.n, b.snap_stride), np.uint8)
+    ev = np.zeros((b.n, 160), np.uint8) if events else None
     lib.o_pipeline_batch_mt(C.byref(cfg), C.byref(b), now, out.ctypes.data, nd6.ctypes.data, snap.ctypes.data,
-                            max(1, threads))
+                            max(1, threads), None if ev is None else ev.ctypes.data)
+    if events:
+        return out, nd6, snap, ev[ev[:, 0] == 1]
     return out, nd6, snap
+
+
+def ingress_events(prog_array, b, out):
+    """Drop notifications of an ingress batch, in batch order ([k, 160] u8)."""
+    ev = np.zeros((b.n, 160), np.uint8)
+    lib.o_ingress_events(prog_array, C.byref(b), out.ctypes.data, ev.ctypes.data)
+    return ev[ev[:, 0] == 1]

@@ -63,7 +63,10 @@ class OracleDP:
     def ingress(self, pk, now, threads=1):
         return O.ingress(self.arr, self.batch(pk), now, threads)
 
-    def pipeline(self, pk, now, threads=1):
+    def ingress_events(self, pk, out):
+        return O.ingress_events(self.arr, self.batch(pk), out)
+
+    def pipeline(self, pk, now, threads=1, events=False):
         if self._pipe is None:
             nd = self.sc.netdev
             self._nd = O.o_netdev_cfg(self.m[nd["lxc_map"]].ptr, nd.get("flags", 0), nd.get("fixed_secctx", 0),
@@ -71,7 +74,7 @@ class OracleDP:
             self._pipe = O.o_pipeline_cfg(C.pointer(self.xdp_cfg) if self.xdp_cfg is not None else None,
                                           C.pointer(self.lb_cfg) if self.lb_cfg is not None else None,
                                           C.pointer(self._nd), self.arr)
-        return O.pipeline(self._pipe, self.batch(pk), now, threads)
+        return O.pipeline(self._pipe, self.batch(pk), now, threads, events)
 
     def ct_gc(self, name, filter_time):
         return self.m[name].ct_gc(filter_time)

@@ -213,3 +213,48 @@ def test_ct_gc_device_sweep_then_traffic():
         assert dp.dump_map(name) == ref.dump(name), name
     assert lib.gf_ct_gc(dp.fd["ct4"], 0xFFFFFFFF, st) == ref.ct_gc("ct4", 0xFFFFFFFF)
     assert dp.dump_map("ct4") == {} == ref.dump("ct4")
+
+
+def test_drop_notify_events():
+    """send_drop_notify records (bpf/lib/drop.h:47-107) appended to the device
+    event ring in batch order, for the ingress program and the full pipeline,
+    equal the oracle's, capture bytes included."""
+    import ctypes as C
+    from cilium_amd._lib import lib, gf_event_ring
+    cap = 200000
+    recs = torch.zeros((cap, 160), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ring = gf_event_ring(recs.data_ptr(), cap, cnt.data_ptr())
+    assert lib.gf_set_event_ring(C.byref(ring)) == 0
+    try:
+        sc = synth.fuzz(seed=2, n_packets=20000, n_batches=2)
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        exp = []
+        for bi, pk in enumerate(sc.batches):
+            io = dp.ingress(DeviceBatch(pk), sc.now + bi)
+            ro = ref.ingress(pk, sc.now + bi)
+            torch.cuda.synchronize()
+            _cmp_struct(to_numpy(io, ING_OUT), ro, f"ingress b{bi}")
+            exp.append(ref.ingress_events(pk, ro))
+        e = np.concatenate(exp)
+        n = int(cnt.item())
+        assert n == len(e) > 100
+        assert np.array_equal(recs[:n].cpu().numpy(), e)
+        cnt.zero_()
+        sc = synth.pipeline_fuzz(seed=3, n_packets=20000, n_batches=2)
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        exp = []
+        for bi, pk in enumerate(sc.batches):
+            out, nd6, snap = dp.pipeline(DeviceBatch(pk, parse=False), sc.now + bi)
+            ro, rn6, rs, ev = ref.pipeline(pk, sc.now + bi, events=True)
+            torch.cuda.synchronize()
+            _cmp_struct(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
+            exp.append(ev)
+        e = np.concatenate(exp)
+        n = int(cnt.item())
+        assert n == len(e) > 100
+        got = recs[:n].cpu().numpy()
+        bad = np.nonzero((got != e).any(axis=1))[0]
+        assert len(bad) == 0, f"{len(bad)} event records differ, first {bad[:1]}: {got[bad[0]][:32]} vs {e[bad[0]][:32]}"
+    finally:
+        lib.gf_set_event_ring(None)
