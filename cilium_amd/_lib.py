@@ -84,7 +84,9 @@ class gf_prof_rec(C.Structure):
 
 
 class gf_node_cfg(C.Structure):
-    _fields_ = [("host_ifindex", C.c_uint32)]
+    _fields_ = [("host_ifindex", C.c_uint32), ("proxy4_map", C.c_int), ("proxy6_map", C.c_int),
+                ("ipv4_gateway", C.c_uint32), ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6),
+                ("node_mac", C.c_uint8 * 6)]
 
 
 class gf_netdev_cfg(C.Structure):

@@ -140,6 +140,8 @@ std::shared_ptr<Obj> get_obj(int handle);
 std::shared_ptr<Map> get_map(int handle);
 int new_handle(std::shared_ptr<Obj> o);
 uint32_t host_ifindex();
+const gf_node_cfg &node_cfg();
+std::shared_ptr<Map> proxy_map(int fam);   // cilium_proxy4 (4) / cilium_proxy6 (6), may be null
 uint64_t *stats_sink();
 
 // trie builder (host)

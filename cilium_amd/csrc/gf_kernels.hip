@@ -185,6 +185,58 @@ struct PktHdrA {
     __device__ __forceinline__ uint4 daddr6() const { return make_uint4(h.d6[0], h.d6[1], h.d6[2], h.d6[3]); }
 };
 
+// The lane's frame copy.  Reads past the snap (or len) are 0, writes past the
+// snap are dropped (the snap holds every header byte the programs touch).
+struct Row {
+    uint8_t *p;
+    uint32_t cap;
+    __device__ __forceinline__ uint32_t b(uint32_t off) const { return off < cap ? (uint32_t)p[off] : 0u; }
+    __device__ __forceinline__ uint32_t r16(uint32_t off) const { return b(off) | (b(off + 1) << 8); }
+    __device__ __forceinline__ uint32_t r32(uint32_t off) const { return r16(off) | (r16(off + 2) << 16); }
+    __device__ __forceinline__ void w8(uint32_t off, uint32_t v) { if (off < cap) p[off] = (uint8_t)v; }
+    __device__ __forceinline__ void w16(uint32_t off, uint32_t v) { w8(off, v & 0xffu); w8(off + 1, (v >> 8) & 0xffu); }
+    __device__ __forceinline__ void w32(uint32_t off, uint32_t v) { w16(off, v & 0xffffu); w16(off + 2, v >> 16); }
+};
+
+// Checksum arithmetic of bpf_l3_csum_replace / bpf_l4_csum_replace /
+// bpf_csum_diff (Linux net/core/filter.c over include/net/checksum.h; the skb is
+// a received frame, not CHECKSUM_PARTIAL).  Operands are raw LE loads of the
+// network-order bytes, as the programs pass them.
+#define GF_F_PSEUDO_HDR (1u << 4)
+#define GF_F_MANGLED_0 (1u << 5)
+__device__ __forceinline__ uint32_t ck_add(uint32_t a, uint32_t b) { uint32_t r = a + b; return r + (r < b ? 1u : 0u); }
+__device__ __forceinline__ uint32_t ck_fold(uint32_t x) {
+    x = (x & 0xffffu) + (x >> 16);
+    x = (x & 0xffffu) + (x >> 16);
+    return ~x & 0xffffu;
+}
+__device__ __forceinline__ uint32_t ck16_add(uint32_t a, uint32_t b) {
+    uint32_t r = (a + b) & 0xffffu;
+    return (r + (r < b ? 1u : 0u)) & 0xffffu;
+}
+// bpf_l3_csum_replace: size 0 = by diff, 2 = csum_replace2, 4 = csum_replace4
+__device__ int l3_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t size) {
+    if (!l4csum_ok(off, len)) return -GF_EFAULT;
+    uint32_t sum = w.r16((uint32_t)off);
+    if (size == 0) sum = ck_fold(ck_add(to, ~sum));
+    else if (size == 2) sum = ~ck16_add(ck16_add(~sum & 0xffffu, ~from & 0xffffu), to & 0xffffu) & 0xffffu;
+    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
+    w.w16((uint32_t)off, sum);
+    return 0;
+}
+// bpf_l4_csum_replace (inet_proto_csum_replace4 / _by_diff, BPF_F_MARK_MANGLED_0)
+__device__ int l4_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t flags) {
+    if (!l4csum_ok(off, len)) return -GF_EFAULT;
+    uint32_t sum = w.r16((uint32_t)off);
+    const bool mmzero = (flags & GF_F_MANGLED_0) != 0;
+    if (mmzero && !sum) return 0;
+    if ((flags & 0xfu) == 0) sum = ck_fold(ck_add(to, ~sum));
+    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
+    if (mmzero && !sum) sum = 0xffffu;                  // CSUM_MANGLED_0
+    w.w16((uint32_t)off, sum);
+    return 0;
+}
+
 // ================================================================ XDP
 struct XdpDev {
     gf_htab_desc h4, h6, lxc;
@@ -412,7 +464,99 @@ struct IngCtx {
     uint32_t now, host_ifindex;
     uint32_t strict;   // bit0 / bit1: CT4 / CT6 inserts check max_entries with atomics
     uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
+    uint8_t *snap;     // pipeline: the frames as rewritten so far (handle_policy's writes land here)
+    uint32_t snap_stride;
+    uint32_t *plog, *plog_n;   // cilium_proxy{4,6} update log (16 words per redirect) and its length
+    uint32_t gw, host6[4];     // IPV4_GATEWAY, HOST_IP (node_config.h)
 };
+
+// ---- handle_policy's own header writes (kept out of line: cold paths of the
+// hot kernel) and the proxy-map log ----
+__device__ __forceinline__ Row pol_row(const IngCtx &X, uint32_t i, uint32_t len) {
+    return Row{X.snap + (size_t)i * X.snap_stride, X.snap_stride < len ? X.snap_stride : len};
+}
+// reverse_map_l4_port (bpf/lib/lb.h:217-251) + __lb4_rev_nat / __lb6_rev_nat
+// (lb.h:253-293, 447-512; v4 with REV_NAT_F_TUPLE_SADDR: the old address is the
+// tuple's, v6 with flags 0: the frame's)
+__device__ __attribute__((noinline)) void pol_rev_nat_write(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                            uint32_t nh, const uint8_t *nat, bool v6,
+                                                            uint32_t old_sip4) {
+    Row w = pol_row(X, i, len);
+    const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+    const uint32_t port = gload<uint16_t>(nat + (v6 ? 16 : 4));
+    if (port && (nh == 6 || nh == 17)) {
+        const uint32_t old = w.r16((uint32_t)l4_off);
+        if (port != old) {
+            l4_csum(w, len, l4_off + (int)co, old, port, 2u | fl);
+            w.w16((uint32_t)l4_off, port);
+        }
+    }
+    uint32_t sum = 0;
+    if (!v6) {
+        const uint32_t nw = gload<uint32_t>(nat);
+        w.w32(26, nw);
+        sum = ck_add(ck_add(0u, ~old_sip4), nw);
+        l3_csum(w, len, 24, 0, sum, 0);
+        if (co) l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl);
+    } else {
+        for (int k = 0; k < 4; k++) {
+            const uint32_t od = w.r32(22 + 4 * k), nw = gload<uint32_t>(nat + 4 * k);
+            w.w32(22 + 4 * k, nw);
+            sum = ck_add(ck_add(sum, ~od), nw);
+        }
+        l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl);
+    }
+}
+// ipv6_policy's "derive reverse NAT index and zero it" (bpf_lxc.c:774-790)
+__device__ __attribute__((noinline)) void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                         uint32_t nh, uint32_t rn) {
+    Row w = pol_row(X, i, len);
+    w.w16(38 + 12, 0);
+    const uint32_t co = csum_l4_offset(nh);
+    if (co) l4_csum(w, len, l4_off + (int)co, 0, ck_add(ck_add(0u, ~rn), 0u),
+                    GF_F_PSEUDO_HDR | (nh == 17 ? GF_F_MANGLED_0 : 0u));
+}
+// ipv{4,6}_redirect_to_host_port writes (lib/lxc.h:96-205) after their checks,
+// and the cilium_proxy{4,6} entry, logged for the in-order apply after the launch.
+// t: the CT tuple words as ct_lookup left them; od: the original daddr.
+__device__ __attribute__((noinline)) void pol_redirect(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                       uint32_t nh, const uint32_t *t, bool v6, uint32_t new_port,
+                                                       const uint32_t *od, uint32_t identity) {
+    const uint32_t pw = v6 ? t[8] : t[2];
+    const uint32_t old_port = pw & 0xffffu, sport = pw >> 16;
+    if (X.snap) {
+        Row w = pol_row(X, i, len);
+        const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+        l4_csum(w, len, l4_off + (int)co, old_port, new_port, 2u | fl);     // l4_modify_port
+        w.w16((uint32_t)(l4_off + 2), new_port);
+        if (!v6) {
+            w.w32(30, X.gw);
+            l3_csum(w, len, 24, od[0], X.gw, 4);
+            if (co) l4_csum(w, len, l4_off + (int)co, od[0], X.gw, 4u | GF_F_PSEUDO_HDR | fl);
+        } else {
+            uint32_t sum = 0;
+            for (int k = 0; k < 4; k++) {
+                w.w32(38 + 4 * k, X.host6[k]);
+                sum = ck_add(ck_add(sum, ~od[k]), X.host6[k]);
+            }
+            if (co) l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl);
+        }
+    }
+    if (X.plog) {
+        uint32_t *e = X.plog + 16ull * atomicAdd(X.plog_n, 1u);
+        uint32_t q[16] = {0};
+        q[0] = i; q[1] = v6 ? 6u : 4u;
+        const int a = v6 ? 4 : 1;                       // key: .saddr = tuple->daddr, .dport, .sport, .nexthdr
+        for (int k = 0; k < a; k++) q[2 + k] = t[k];
+        q[2 + a] = new_port | (sport << 16);
+        q[3 + a] = nh;
+        for (int k = 0; k < a; k++) q[8 + k] = od[k];  // value: orig_daddr, orig_dport, identity, lifetime
+        q[8 + a] = old_port;
+        q[9 + a] = identity;
+        q[10 + a] = X.now + 720u;                       // PROXY_DEFAULT_LIFETIME
+        for (int k = 0; k < 16; k += 4) *reinterpret_cast<uint4 *>(e + k) = make_uint4(q[k], q[k + 1], q[k + 2], q[k + 3]);
+    }
+}
 
 struct CtState { uint32_t rev_nat, loopback, carry; };
 
@@ -836,7 +980,7 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
-__device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, int &fwd, uint8_t &ofl, uint16_t &proxy,
+__device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
                            uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo &pm) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
@@ -873,6 +1017,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, int &fwd, u
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 4), r.l4w0, false);
             if (r2 < 0) return r2;
+            if (X.snap) pol_rev_nat_write(X, i, len, r.l4_off, nh, nat, false, t[1]);
             t[1] = gload<uint32_t>(nat);                       // tuple->saddr = nat->address
         }
     }
@@ -896,6 +1041,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, int &fwd, u
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
+        if (X.snap || X.plog) { const uint32_t od[1] = {r.daddr}; pol_redirect(X, i, len, r.l4_off, nh, t, false, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
         ifindex = X.host_ifindex;
         ofl |= GF_INGRESS_F_PROXY;
         proxy = (uint16_t)verdict;
@@ -917,7 +1063,10 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     uint32_t t[10] = {d.x, d.y, d.z, d.w, s.x, s.y, s.z, s.w, 0u, nh};
     uint32_t co = csum_l4_offset(nh);
     uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
-    if (rn_new && co && !l4csum_ok(r.l4_off + (int)co, len)) return D_CSUM_L4;
+    if (rn_new) {
+        if (X.snap) pol_v6_zero_rn(X, i, len, r.l4_off, nh, rn_new);
+        if (co && !l4csum_ok(r.l4_off + (int)co, len)) return D_CSUM_L4;
+    }
     uint32_t tfl = 0;
     int action; bool syn;
     int e = ct_l4(nh, true, r, t[8], tfl, action, syn);
@@ -946,6 +1095,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 16), r.l4w0, true);
             if (r2 < 0) return r2;
+            if (X.snap) pol_rev_nat_write(X, i, len, r.l4_off, nh, nat, true, 0u);
         }
     }
     int verdict = policy_ingress(X, ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
@@ -966,6 +1116,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
+        if (X.snap || X.plog) { const uint32_t od[4] = {d.x, d.y, d.z, d.w}; pol_redirect(X, i, len, r.l4_off, nh, t, true, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
         ifindex = X.host_ifindex;
         ofl |= GF_INGRESS_F_PROXY;
         proxy = (uint16_t)verdict;
@@ -1012,7 +1163,7 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
+        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
     else ret = D_UNKNOWN_L3;
@@ -1277,58 +1428,6 @@ struct PipeDev {
     NetdevDev nd;
     uint32_t has_xdp, has_lb, lb_redirect_ifindex, vec_copy;
 };
-// The lane's frame copy.  Reads past the snap (or len) are 0, writes past the
-// snap are dropped (the snap holds every header byte the programs touch).
-struct Row {
-    uint8_t *p;
-    uint32_t cap;
-    __device__ __forceinline__ uint32_t b(uint32_t off) const { return off < cap ? (uint32_t)p[off] : 0u; }
-    __device__ __forceinline__ uint32_t r16(uint32_t off) const { return b(off) | (b(off + 1) << 8); }
-    __device__ __forceinline__ uint32_t r32(uint32_t off) const { return r16(off) | (r16(off + 2) << 16); }
-    __device__ __forceinline__ void w8(uint32_t off, uint32_t v) { if (off < cap) p[off] = (uint8_t)v; }
-    __device__ __forceinline__ void w16(uint32_t off, uint32_t v) { w8(off, v & 0xffu); w8(off + 1, (v >> 8) & 0xffu); }
-    __device__ __forceinline__ void w32(uint32_t off, uint32_t v) { w16(off, v & 0xffffu); w16(off + 2, v >> 16); }
-};
-
-// Checksum arithmetic of bpf_l3_csum_replace / bpf_l4_csum_replace /
-// bpf_csum_diff (Linux net/core/filter.c over include/net/checksum.h; the skb is
-// a received frame, not CHECKSUM_PARTIAL).  Operands are raw LE loads of the
-// network-order bytes, as the programs pass them.
-#define GF_F_PSEUDO_HDR (1u << 4)
-#define GF_F_MANGLED_0 (1u << 5)
-__device__ __forceinline__ uint32_t ck_add(uint32_t a, uint32_t b) { uint32_t r = a + b; return r + (r < b ? 1u : 0u); }
-__device__ __forceinline__ uint32_t ck_fold(uint32_t x) {
-    x = (x & 0xffffu) + (x >> 16);
-    x = (x & 0xffffu) + (x >> 16);
-    return ~x & 0xffffu;
-}
-__device__ __forceinline__ uint32_t ck16_add(uint32_t a, uint32_t b) {
-    uint32_t r = (a + b) & 0xffffu;
-    return (r + (r < b ? 1u : 0u)) & 0xffffu;
-}
-// bpf_l3_csum_replace: size 0 = by diff, 2 = csum_replace2, 4 = csum_replace4
-__device__ int l3_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t size) {
-    if (!l4csum_ok(off, len)) return -GF_EFAULT;
-    uint32_t sum = w.r16((uint32_t)off);
-    if (size == 0) sum = ck_fold(ck_add(to, ~sum));
-    else if (size == 2) sum = ~ck16_add(ck16_add(~sum & 0xffffu, ~from & 0xffffu), to & 0xffffu) & 0xffffu;
-    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
-    w.w16((uint32_t)off, sum);
-    return 0;
-}
-// bpf_l4_csum_replace (inet_proto_csum_replace4 / _by_diff, BPF_F_MARK_MANGLED_0)
-__device__ int l4_csum(Row &w, uint32_t len, int32_t off, uint32_t from, uint32_t to, uint32_t flags) {
-    if (!l4csum_ok(off, len)) return -GF_EFAULT;
-    uint32_t sum = w.r16((uint32_t)off);
-    const bool mmzero = (flags & GF_F_MANGLED_0) != 0;
-    if (mmzero && !sum) return 0;
-    if ((flags & 0xfu) == 0) sum = ck_fold(ck_add(to, ~sum));
-    else sum = ck_fold(ck_add(ck_add(~sum, ~from), to));
-    if (mmzero && !sum) sum = 0xffffu;                  // CSUM_MANGLED_0
-    w.w16((uint32_t)off, sum);
-    return 0;
-}
-
 // lb4_xlate / lb6_xlate writes (bpf/lib/lb.h:615-659, 397-423) of a translation
 // lb_v4/lb_v6 accepted (their checks passed, so every helper succeeds).
 __device__ void pipe_lb_rewrite(Row &w, uint32_t len, const PktHdr &h, bool v6, const gf_lb_out &o,
@@ -1719,6 +1818,82 @@ __global__ void k_ev_commit(const uint32_t *boff, const uint32_t *blk, uint32_t 
     *R.count += boff[nb - 1] + blk[nb - 1];
 }
 
+// ================================================================ cilium_proxy{4,6} updates
+// The redirects of a launch are logged (pol_redirect) and applied here in batch
+// order.  The proxy maps change only through these updates while a batch runs,
+// so applying them after the launch gives every update the outcome sequential
+// execution gives it.  Parallel path (the maps cannot fill): the log is sorted by
+// (key hash, packet index); an entry is applied only if no later entry of the
+// batch has the same key (the last writer wins, as in order), and distinct keys
+// insert concurrently.  Sequential path (a map could fill): one lane applies the
+// log in packet order with exact max_entries accounting; a failed update turns
+// the packet into DROP_PROXYMAP_CREATE_FAILED (lxc.h:137/199).  Successful
+// redirects get ipv{4,6}_policy's MAC stores (bpf_lxc.c:840-846, 955-961).
+struct PxDev {
+    gf_htab_desc d4, d6;
+    uint8_t *snap;              // writable frames (pipeline) or null
+    const uint32_t *len;
+    uint32_t snap_stride;
+    uint32_t host_mac[2], node_mac[2];
+};
+__device__ __forceinline__ bool px_same(const uint32_t *a, const uint32_t *b) {
+    if (a[1] != b[1]) return false;
+    const int nw = a[1] == 6 ? 6 : 3;
+    for (int k = 0; k < nw; k++) if (a[2 + k] != b[2 + k]) return false;
+    return true;
+}
+__device__ __forceinline__ void px_macs(const PxDev &P, uint32_t i) {
+    if (!P.snap) return;
+    const uint32_t len = P.len[i];
+    Row w{P.snap + (size_t)i * P.snap_stride, P.snap_stride < len ? P.snap_stride : len};
+    w.w32(6, P.node_mac[0]); w.w16(10, P.node_mac[1]);     // eth_store_saddr(NODE_MAC)
+    w.w32(0, P.host_mac[0]); w.w16(4, P.host_mac[1]);      // eth_store_daddr(HOST_IFINDEX_MAC)
+}
+__device__ __forceinline__ int64_t px_upsert(const PxDev &P, const uint32_t *e, bool strict, int *added) {
+    if (e[1] == 6) return P.d6.slots ? ht_upsert<22, 7, GF_HASH_PLAIN>(P.d6, e + 2, e + 8, strict, added) : 0;
+    return P.d4.slots ? ht_upsert<10, 4, GF_HASH_PLAIN>(P.d4, e + 2, e + 8, strict, added) : 0;
+}
+__global__ __launch_bounds__(BLOCK) void k_px_keys(const uint32_t *plog, uint32_t n, bool by_index,
+                                                   unsigned long long *key, uint32_t *val) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t *e = plog + 16ull * j;
+    uint32_t h = 0;
+    if (!by_index) h = e[1] == 6 ? key_hash<22>(e + 2) : key_hash<10>(e + 2);
+    key[j] = ((unsigned long long)h << 32) | e[0];
+    val[j] = j;
+}
+__global__ __launch_bounds__(BLOCK) void k_px_apply(const uint32_t *plog, uint32_t n, const unsigned long long *key,
+                                                    const uint32_t *perm, PxDev P) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t *e = plog + 16ull * perm[p];
+    px_macs(P, e[0]);
+    const uint32_t h = (uint32_t)(key[p] >> 32);
+    for (uint32_t q = p + 1; q < n && (uint32_t)(key[q] >> 32) == h; q++)
+        if (px_same(e, plog + 16ull * perm[q])) return;     // a later update of the same key wins
+    int added = 0;
+    px_upsert(P, e, false, &added);
+    if (added) atomicAdd(e[1] == 6 ? P.d6.count : P.d4.count, (uint32_t)added);
+}
+__global__ void k_px_apply_seq(const uint32_t *plog, uint32_t n, const uint32_t *perm, PxDev P, uint8_t *recs,
+                               uint32_t stride, uint32_t act_off, unsigned long long *stats) {
+    for (uint32_t p = 0; p < n; p++) {
+        const uint32_t *e = plog + 16ull * perm[p];
+        const uint32_t i = e[0];
+        if (px_upsert(P, e, true, nullptr) >= 0) { px_macs(P, i); continue; }
+        uint8_t *r = recs + (size_t)i * stride;             // DROP_PROXYMAP_CREATE_FAILED
+        const uint32_t old_action = r[act_off];
+        r[act_off] = TC_SHOT; r[act_off + 1] = 161;
+        if (stride == 8) { r[3] &= 2; r[4] = r[5] = r[6] = r[7] = 0; }
+        else { r[4] &= ~1u; r[6] = r[7] = r[8] = r[9] = 0; }
+        if (stats) {
+            atomicAdd(&stats[0], ~0ull); atomicAdd(&stats[161], 1ull);
+            atomicAdd(&stats[256 + old_action], ~0ull); atomicAdd(&stats[256 + TC_SHOT], 1ull);
+        }
+    }
+}
+
 // ================================================================ host: programs
 namespace {
 
@@ -2010,7 +2185,8 @@ static int emit_drop_events(EvSrc E, hipStream_t s) {
 using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
-                       const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0) {
+                       const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
+                       uint8_t *wsnap = nullptr) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -2178,6 +2354,20 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.now = now_sec; X.host_ifindex = host_ifindex();
     X.strict = strict;
     X.pout = pout;
+    X.snap = wsnap; X.snap_stride = ev_stride;
+    const gf_node_cfg &node = node_cfg();
+    X.gw = node.ipv4_gateway;
+    memcpy(X.host6, node.host_ip6, 16);
+    auto px4 = proxy_map(4), px6 = proxy_map(6);
+    static DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp;
+    if (px4 || px6) {
+        auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+        if ((r = grow(plog, (size_t)n * 64)) || (r = grow(plog_n, 4))) return r;
+        if (hip_ok(hipMemsetAsync(plog_n.p, 0, 4, s), "plog_n")) return -EIO;
+        for (auto &m : {px4, px6})
+            if (m && (r = push_map(m, s))) return r;
+        X.plog = (uint32_t *)plog.p; X.plog_n = (uint32_t *)plog_n.p;
+    }
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
@@ -2200,6 +2390,51 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
+    if (X.plog) {
+        // cilium_proxy{4,6} updates of this batch, in batch order (see k_px_apply)
+        uint32_t cnt = 0;
+        if (hip_ok(hipMemcpyAsync(&cnt, X.plog_n, 4, hipMemcpyDeviceToHost, s), "plog count") ||
+            hip_ok(hipStreamSynchronize(s), "plog sync"))
+            return -EIO;
+        if (cnt) {
+            PxDev P{};
+            bool seq = false;
+            for (auto &m : {px4, px6}) {
+                if (!m) continue;
+                if (m->host_valid) m->dev_count_hi = m->ht.count;
+                if (m->dev_count_hi + cnt > m->max_entries) seq = true;
+            }
+            if (px4) P.d4 = px4->hdesc();
+            if (px6) P.d6 = px6->hdesc();
+            P.snap = wsnap; P.len = ev_len ? ev_len : pkts->len; P.snap_stride = ev_stride;
+            memcpy(P.host_mac, node.host_mac, 6); memcpy(P.node_mac, node.node_mac, 6);
+            auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+            if ((r = grow(pkey, (size_t)cnt * 8)) || (r = grow(pkey2, (size_t)cnt * 8)) || (r = grow(pval, (size_t)cnt * 4)) ||
+                (r = grow(pperm, (size_t)cnt * 4)))
+                return r;
+            size_t tb = 0;
+            (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)pkey.p, (unsigned long long *)pkey2.p,
+                                            (uint32_t *)pval.p, (uint32_t *)pperm.p, cnt, 0, 64, s);
+            if ((r = grow(ptmp, tb + 256))) return r;
+            ProfScope ps("k_proxy_apply", s);
+            const uint32_t g = (cnt + BLOCK - 1) / BLOCK;
+            hipLaunchKernelGGL(k_px_keys, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)plog.p, cnt, seq,
+                               (unsigned long long *)pkey.p, (uint32_t *)pval.p);
+            tb = ptmp.bytes;
+            if (hip_ok(rocprim::radix_sort_pairs(ptmp.p, tb, (unsigned long long *)pkey.p, (unsigned long long *)pkey2.p,
+                                                 (uint32_t *)pval.p, (uint32_t *)pperm.p, cnt, 0, 64, s), "proxy sort"))
+                return -EIO;
+            if (seq)
+                hipLaunchKernelGGL(k_px_apply_seq, dim3(1), dim3(1), 0, s, (const uint32_t *)plog.p, cnt,
+                                   (const uint32_t *)pperm.p, P, pout ? pout : (uint8_t *)out, pout ? 24u : 8u,
+                                   pout ? 1u : 0u, (unsigned long long *)stats_sink());
+            else
+                hipLaunchKernelGGL(k_px_apply, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)plog.p, cnt,
+                                   (const unsigned long long *)pkey2.p, (const uint32_t *)pperm.p, P);
+            if ((r = hip_ok(hipGetLastError(), "k_proxy_apply"))) return r;
+            for (auto &m : {px4, px6}) if (m) { m->device_modified(); m->dev_count_hi += cnt; }
+        }
+    }
     {
         EvSrc E{};
         E.recs = pout ? pout : (const uint8_t *)out;
@@ -2325,7 +2560,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     };
     c2.flow_hash = b->flow_hash;
     return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out, fr.len,
-                       snap_out ? snap_out : fr.snap, fr.snap_stride);
+                       snap_out ? snap_out : fr.snap, fr.snap_stride, snap_out);
 }
 
 // ---- conntrack GC ----

@@ -512,6 +512,8 @@ struct Registry {
     int next = 3;      // like fds: 0/1/2 are never handed out
     uint32_t host_ifindex = 1;
     uint64_t *stats = nullptr;
+    gf_node_cfg node{1, 0, 0, 0, {0}, {0}, {0}};
+    std::shared_ptr<Map> px4, px6;
 };
 static Registry &reg() { static Registry r; return r; }
 
@@ -532,6 +534,8 @@ int new_handle(std::shared_ptr<Obj> o) {
     return h;
 }
 uint32_t host_ifindex() { return reg().host_ifindex; }
+const gf_node_cfg &node_cfg() { return reg().node; }
+std::shared_ptr<Map> proxy_map(int fam) { return fam == 6 ? reg().px6 : reg().px4; }
 uint64_t *stats_sink() { return reg().stats; }
 
 }  // namespace gf
@@ -666,7 +670,22 @@ uint32_t gf_now_sec(void) {
 int gf_node_config(const gf_node_cfg *cfg) {
     std::lock_guard<std::recursive_mutex> g(big_lock());
     if (!cfg) return -EFAULT;
+    std::shared_ptr<Map> m4, m6;
+    if (cfg->proxy4_map) {
+        m4 = get_map(cfg->proxy4_map);
+        if (!m4) return -EBADF;
+        if (m4->ksz != 10 || m4->vsz != 16 || m4->is_lpm()) return -EINVAL;
+    }
+    if (cfg->proxy6_map) {
+        m6 = get_map(cfg->proxy6_map);
+        if (!m6) return -EBADF;
+        if (m6->ksz != 22 || m6->vsz != 28 || m6->is_lpm()) return -EINVAL;
+    }
+    // the datapath inserts into the proxy maps: fixed slot arrays (1/2 load at max_entries)
+    for (auto &m : {m4, m6}) if (m) m->make_fixed_capacity(2);
     reg().host_ifindex = cfg->host_ifindex;
+    reg().node = *cfg;
+    reg().px4 = m4; reg().px6 = m6;
     return 0;
 }
 

@@ -128,8 +128,12 @@ class Datapath:
                 except OSError:
                     pass
             self.fd[name] = fd
-        _check(lib.gf_node_config(C.byref(gf_node_cfg(sc.host_ifindex))), "gf_node_config")
         h = lambda name: self.fd[name] if name else 0
+        nd = sc.node or {}
+        ncfg = gf_node_cfg(sc.host_ifindex, h(nd.get("proxy4")), h(nd.get("proxy6")), nd.get("ipv4_gateway", 0),
+                           (C.c_uint8 * 16)(*nd.get("host_ip6", bytes(16))), (C.c_uint8 * 6)(*nd.get("host_mac", bytes(6))),
+                           (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))))
+        _check(lib.gf_node_config(C.byref(ncfg)), "gf_node_config")
         self.xdp_prog = self.lb_prog = self.policy_array = None
         if sc.xdp:
             x = sc.xdp

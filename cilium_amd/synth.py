@@ -67,6 +67,7 @@ class Scenario:
     lb: dict = None              # {'lb4','lb6','flags','redirect_ifindex'}
     lxc: list = field(default_factory=list)   # endpoint program configs
     netdev: dict = None          # bpf_netdev config of the full pipeline (gf_netdev_cfg)
+    node: dict = None            # node_config.h values beyond HOST_IFINDEX (gf_node_cfg): proxy maps, ...
     host_ifindex: int = 1
     batches: list = field(default_factory=list)   # list of Packets, processed in order
     now: int = 1000
@@ -855,7 +856,7 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
     return sc
 
 
-def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed_secctx=None):
+def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed_secctx=None, proxy_max=524288):
     """The fuzz scenario run through the whole pipeline (bpf_xdp -> bpf_lb ->
     bpf_netdev -> handle_policy): endpoint MACs and port maps (duplicated and
     unterminated entries), host endpoints, VIPs present in cilium_lxc as host
@@ -923,6 +924,14 @@ def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed
         sc.lb = dict(sc.lb, flags=LB_L3 | LB_L4)
     sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0 if fixed_secctx is None else 1,
                  "fixed_secctx": fixed_secctx or 0, "router_ip6": bytes(router)}
+    # cilium_proxy4/6 (bpf/lib/maps.h:56-71; key 10 / 22 B, value 16 / 28 B) and the
+    # node_config.h addresses of the proxy redirect (IPV4_GATEWAY, HOST_IP, MACs)
+    sc.add_map(MapSpec("cilium_proxy4", HASH, 10, 16, proxy_max, 0))
+    sc.add_map(MapSpec("cilium_proxy6", HASH, 22, 28, proxy_max, 0))
+    sc.node = {"proxy4": "cilium_proxy4", "proxy6": "cilium_proxy6", "ipv4_gateway": 0xfffff50a,
+               "host_ip6": bytes([0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0xa, 0, 0x2, 0xf, 0xff, 0xff]),
+               "host_mac": bytes([0xce, 0x72, 0xa7, 0x03, 0x88, 0x56]),
+               "node_mac": bytes([0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde])}
     return sc
 
 

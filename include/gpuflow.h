@@ -257,6 +257,12 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog);  /* prog 0 = d
 
 typedef struct gf_node_cfg {   /* node_config.h values used on the path */
     uint32_t host_ifindex;     /* HOST_IFINDEX */
+    int      proxy4_map;       /* cilium_proxy4 (proxy4_tbl_key 10 B -> proxy4_tbl_value 16 B), 0 = none */
+    int      proxy6_map;       /* cilium_proxy6 (proxy6_tbl_key 22 B -> proxy6_tbl_value 28 B), 0 = none */
+    uint32_t ipv4_gateway;     /* IPV4_GATEWAY (raw be32), the proxy redirect's new daddr */
+    uint8_t  host_ip6[16];     /* HOST_IP, the IPv6 proxy redirect's new daddr */
+    uint8_t  host_mac[6];      /* HOST_IFINDEX_MAC */
+    uint8_t  node_mac[6];      /* NODE_MAC */
 } gf_node_cfg;
 int gf_node_config(const gf_node_cfg *cfg);
 

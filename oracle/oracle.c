@@ -956,6 +956,47 @@ static int lb_rev_nat_checks(const skb_t *s, int l4_off, uint8_t nexthdr, uint16
     return 0;
 }
 
+/* header-write helpers (defined with the pipeline section below); w == NULL:
+ * the checks only (column batches carry no frame to rewrite) */
+static void wbytes(const skb_t *s, uint8_t *w, uint32_t off, const void *from, uint32_t n);
+static int l3_csum_replace(const skb_t *s, uint8_t *w, int32_t off, uint32_t from, uint32_t to, uint32_t flags);
+static int l4_csum_replace(const skb_t *s, uint8_t *w, int32_t off, uint32_t from, uint32_t to, uint32_t flags);
+static uint32_t ck_diff(const uint8_t *from, const uint8_t *to, int n);
+static uint32_t csum_l4_flags(uint8_t nexthdr);
+#define BPF_F_PSEUDO_HDR (1u << 4)
+#define PROXY_DEFAULT_LIFETIME 720                     /* bpf/lib/common.h:433 */
+#define DROP_PROXYMAP_CREATE_FAILED_ -161
+
+/* The policy-stage context of one packet: the writable frame (pipeline) and
+ * its proxy-map log entry (applied in batch order after the batch, see
+ * proxy_apply).  Log entry: [0] family 4/6, key at +4, value at +28. */
+#define O_PLOG 64
+typedef struct pol_ctx { uint8_t *w; uint8_t *plog; } pol_ctx;
+
+/* reverse_map_l4_port (bpf/lib/lb.h:217-251) + the address part of
+ * __lb4_rev_nat / __lb6_rev_nat (lb.h:253-293, 447-512) */
+static void rev_nat_write(const skb_t *s, uint8_t *w, int l4_off, uint8_t nh, const uint8_t *nat_addr,
+                          uint16_t nat_port, const uint8_t *old_saddr, int v6) {
+    uint16_t co = csum_l4_offset(nh);
+    uint32_t fl = csum_l4_flags(nh);
+    if (nat_port && (nh == IPPROTO_TCP || nh == IPPROTO_UDP)) {
+        uint16_t old = rd16(s, (uint32_t)l4_off);
+        if (nat_port != old) {
+            l4_csum_replace(s, w, l4_off + co, old, nat_port, 2 | fl);
+            wbytes(s, w, (uint32_t)l4_off, &nat_port, 2);
+        }
+    }
+    int n = v6 ? 16 : 4;
+    wbytes(s, w, v6 ? 22 : 26, nat_addr, n);
+    uint32_t sum = ck_diff(old_saddr, nat_addr, n);
+    if (!v6) {
+        l3_csum_replace(s, w, ETH_HLEN + 10, 0, sum, 0);
+        if (co) l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl);
+    } else {
+        l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl);
+    }
+}
+
 /* ipv4_redirect_to_host_port / ipv6_... verdict-affecting steps (lib/lxc.h:96-205) */
 static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t nexthdr) {
     uint16_t csum_off = csum_l4_offset(nexthdr);
@@ -964,11 +1005,77 @@ static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t next
     return 0;                                          /* cilium_proxy{4,6} update: §8(f) */
 }
 
-static uint32_t g_host_ifindex = 1;                    /* HOST_IFINDEX, bpf/node_config.h */
-void o_set_node(const o_node_cfg *node) { g_host_ifindex = node->host_ifindex; }
+static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}};   /* bpf/node_config.h */
+#define g_host_ifindex (g_node.host_ifindex)
+void o_set_node(const o_node_cfg *node) { g_node = *node; }
+
+/* ipv{4,6}_redirect_to_host_port writes (lib/lxc.h:96-205) once its checks
+ * passed, and the cilium_proxy{4,6} entry it creates (logged, see proxy_apply) */
+static void redirect_write(const skb_t *s, pol_ctx *x, int l4_off, const uint8_t *t, int v6, uint16_t new_port,
+                           const uint8_t *orig_dip, uint32_t identity, uint32_t now) {
+    uint8_t nh = v6 ? t[36] : t[12];
+    uint16_t old_port; memcpy(&old_port, t + (v6 ? 32 : 8), 2);
+    uint16_t sport; memcpy(&sport, t + (v6 ? 34 : 10), 2);
+    if (x->w) {
+        uint16_t co = csum_l4_offset(nh);
+        uint32_t fl = csum_l4_flags(nh);
+        uint8_t *w = x->w;
+        l4_csum_replace(s, w, l4_off + co, old_port, new_port, 2 | fl);      /* l4_modify_port */
+        wbytes(s, w, (uint32_t)l4_off + 2, &new_port, 2);
+        if (!v6) {
+            uint32_t gw = g_node.ipv4_gateway, od; memcpy(&od, orig_dip, 4);
+            wbytes(s, w, 30, &gw, 4);
+            l3_csum_replace(s, w, ETH_HLEN + 10, od, gw, 4);
+            if (co) l4_csum_replace(s, w, l4_off + co, od, gw, 4 | BPF_F_PSEUDO_HDR | fl);
+        } else {
+            wbytes(s, w, 38, g_node.host_ip6, 16);                           /* ipv6_store_daddr */
+            if (co) l4_csum_replace(s, w, l4_off + co, 0, ck_diff(orig_dip, g_node.host_ip6, 16), BPF_F_PSEUDO_HDR | fl);
+        }
+    }
+    uint8_t *e = x->plog;
+    if (!e) return;
+    memset(e, 0, O_PLOG);
+    e[0] = v6 ? 6 : 4;
+    uint8_t *k = e + 4, *v = e + 28;
+    int a = v6 ? 16 : 4;
+    memcpy(k, t, a);                                  /* .saddr = tuple->daddr */
+    memcpy(k + a, &new_port, 2);                      /* .dport = new_port */
+    memcpy(k + a + 2, &sport, 2);                     /* .sport = tuple->sport */
+    k[a + 4] = nh;
+    uint32_t lt = now + PROXY_DEFAULT_LIFETIME;       /* proxy{4,6}_update_timeout */
+    memcpy(v, orig_dip, a);
+    memcpy(v + a, &old_port, 2);
+    memcpy(v + a + 4, &identity, 4);
+    memcpy(v + a + 8, &lt, 4);
+}
+
+/* The logged cilium_proxy{4,6} updates of a batch, in batch order: each is the
+ * map_update_elem(BPF_ANY) of lxc.h:137/:199.  The maps change only through
+ * these updates while a batch runs, so the outcome of update i (E2BIG ->
+ * DROP_PROXYMAP_CREATE_FAILED) is the one sequential execution gives.  A failed
+ * packet's verdict is patched; a successful one gets the MAC stores of
+ * ipv{4,6}_policy that follow the redirect (bpf_lxc.c:840-846, 955-961). */
+static void proxy_apply(const o_batch *b, const uint8_t *plog, o_ingress_out *out, uint8_t *wsnap) {
+    for (uint32_t i = 0; i < b->n; i++) {
+        const uint8_t *e = plog + (size_t)i * O_PLOG;
+        if (!e[0]) continue;
+        om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
+        int r = m ? om_update(m, e + 4, e + 28, 0) : 0;
+        if (r < 0) {
+            out[i].action = TC_ACT_SHOT; out[i].reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
+            out[i].flags &= 2; out[i].proxy_port = 0; out[i].ifindex_lo = 0;
+        } else if (wsnap) {
+            skb_t s; skb_init(&s, b, i);
+            uint8_t *w = wsnap + (size_t)i * b->snap_stride;
+            wbytes(&s, w, 6, g_node.node_mac, 6);      /* eth_store_saddr(NODE_MAC) */
+            wbytes(&s, w, 0, g_node.host_mac, 6);      /* eth_store_daddr(HOST_IFINDEX_MAC) */
+        }
+    }
+}
 
 /* ipv4_policy, bpf/bpf_lxc.c:865-970 */
-static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags, uint16_t *proxy) {
+static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags,
+                       uint16_t *proxy, pol_ctx *x) {
     if (s->len < ETH_HLEN + 20) return DROP_INVALID;
     s->cb[2] = 0;                                      /* policy_clear_mark */
     uint8_t t[14]; memset(t, 0, sizeof t);
@@ -988,6 +1095,7 @@ static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
         if (nat) {
             int r2 = lb_rev_nat_checks(s, l4_off, t[12], ge16(nat, 4), 0);
             if (IS_ERR(r2)) return r2;
+            if (x->w) rev_nat_write(s, x->w, l4_off, t[12], nat, ge16(nat, 4), t + 4, 0);
             memcpy(t + 4, nat, 4);                     /* tuple->saddr = nat->address */
         }
     }
@@ -1007,6 +1115,7 @@ static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         ret = redirect_to_host_port_checks(s, l4_off, t[12]);
         if (IS_ERR(ret)) return ret;
+        redirect_write(s, x, l4_off, t, 0, (uint16_t)verdict, (const uint8_t *)&daddr, src_label, now);
         s->cb[1] = g_host_ifindex;
         *oflags |= 1;
         *proxy = (uint16_t)verdict;
@@ -1015,7 +1124,8 @@ static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
 }
 
 /* ipv6_policy, bpf/bpf_lxc.c:745-862 */
-static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags, uint16_t *proxy) {
+static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags,
+                       uint16_t *proxy, pol_ctx *x) {
     if (s->len < ETH_HLEN + 40) return DROP_INVALID;
     s->cb[2] = 0;
     uint8_t t[40]; memset(t, 0, sizeof t);
@@ -1027,8 +1137,16 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
     ct_state_t st, sn; memset(&st, 0, sizeof st); memset(&sn, 0, sizeof sn);
     uint32_t p4 = ge32(t, 12);                         /* ip6->daddr.s6_addr32[3] */
     sn.rev_nat_index = (uint16_t)(p4 & 0xFFFF);
-    if (sn.rev_nat_index) {
+    uint8_t orig_dip[16]; memcpy(orig_dip, t, 16);
+    if (sn.rev_nat_index) {                            /* dip.p4 &= ~0xFFFF; ipv6_store_daddr */
+        static const uint8_t z2[2] = {0, 0};
+        wbytes(s, x->w, 38 + 12, z2, 2);
         if (csum_off && l4_csum_replace_chk(s, l4_off + csum_off) < 0) return DROP_CSUM_L4;
+        if (csum_off) {                                /* csum_diff(&rev_nat_index, 4, &zero_nat, 4) */
+            uint32_t rn = sn.rev_nat_index, zero = 0;
+            l4_csum_replace(s, x->w, l4_off + csum_off, 0, ck_diff((const uint8_t *)&rn, (const uint8_t *)&zero, 4),
+                            BPF_F_PSEUDO_HDR | csum_l4_flags(t[36]));
+        }
     }
     int acct = (c->flags & LXC_F_CT_ACCOUNTING) != 0;
     int ret = ct_lookup(c->ct_map6, t, s, l4_off, CT_INGRESS, &st, 1, now, acct);
@@ -1039,6 +1157,11 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
         if (nat) {
             int r2 = lb_rev_nat_checks(s, l4_off, t[36], ge16(nat, 16), 1);
             if (IS_ERR(r2)) return r2;
+            if (x->w) {                                /* flags 0: the old saddr is the frame's */
+                uint8_t os[16];
+                for (int k = 0; k < 16; k++) os[k] = skb_byte(s, 22 + k);
+                rev_nat_write(s, x->w, l4_off, t[36], nat, ge16(nat, 16), os, 1);
+            }
         }
     }
     int verdict = policy_can_access_ingress(c, s, src_label, ge16(t, 32), t[36], 1, t + 16);
@@ -1056,6 +1179,7 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         ret = redirect_to_host_port_checks(s, l4_off, t[36]);
         if (IS_ERR(ret)) return ret;
+        redirect_write(s, x, l4_off, t, 1, (uint16_t)verdict, orig_dip, src_label, now);
         s->cb[1] = g_host_ifindex;
         *oflags |= 1;
         *proxy = (uint16_t)verdict;
@@ -1064,7 +1188,8 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
 }
 
 /* handle_policy, bpf/bpf_lxc.c:980-1024 */
-static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, uint32_t now, o_ingress_out *o) {
+static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, uint32_t now, o_ingress_out *o,
+                              pol_ctx *x) {
     memset(o, 0, sizeof *o);
     const o_lxc_cfg *c = a->slot[lxc_id & 0xffff];
     if (!c) {                                          /* tail_call miss -> caller's DROP_MISSED_TAIL_CALL */
@@ -1076,13 +1201,14 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
     uint8_t fl = 0;
     uint16_t proxy = 0;
     if (c->flags & LXC_F_DROP_ALL) ret = DROP_POLICY;
-    else if (s.protocol == 0x86DD) ret = ipv6_policy(c, &s, src_label, &fwd, now, &fl, &proxy);
-    else if (s.protocol == 0x0800 && (c->flags & LXC_F_LXC_IPV4)) ret = ipv4_policy(c, &s, src_label, &fwd, now, &fl, &proxy);
+    else if (s.protocol == 0x86DD) ret = ipv6_policy(c, &s, src_label, &fwd, now, &fl, &proxy, x);
+    else if (s.protocol == 0x0800 && (c->flags & LXC_F_LXC_IPV4)) ret = ipv4_policy(c, &s, src_label, &fwd, now, &fl, &proxy, x);
     else ret = DROP_UNKNOWN_L3;
     o->ct_ret = (uint8_t)fwd;
     o->flags = fl;
     if (ret < 0 || ret == TC_ACT_SHOT) {                /* IS_ERR */
         o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret); o->flags = fl & 2;
+        if (x->plog) x->plog[0] = 0;                    /* no proxy entry for a dropped packet */
         return;
     }
     o->proxy_port = proxy;
@@ -1090,11 +1216,15 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
     o->ifindex_lo = (uint16_t)ifindex;
     o->action = ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 }
-static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o) {
+/* plog: the batch's proxy log (n * O_PLOG); wsnap: writable frames (pipeline) */
+static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o,
+                          uint8_t *plog, uint8_t *wsnap) {
     skb_t s; skb_init(&s, b, i);
     s.cb[0] = b->src_identity ? b->src_identity[i] : 0;
     s.cb[1] = b->ifindex ? b->ifindex[i] : 0;
-    handle_policy_skb(a, s, b->lxc_id ? b->lxc_id[i] : 0, now, o);
+    pol_ctx x = {wsnap ? wsnap + (size_t)i * b->snap_stride : NULL, plog + (size_t)i * O_PLOG};
+    x.plog[0] = 0;
+    handle_policy_skb(a, s, b->lxc_id ? b->lxc_id[i] : 0, now, o, &x);
 }
 
 o_prog_array *o_prog_array_create(void) { return (o_prog_array *)calloc(1, sizeof(o_prog_array)); }
@@ -1102,7 +1232,10 @@ void o_prog_array_destroy(o_prog_array *a) { free(a); }
 void o_prog_array_set(o_prog_array *a, uint32_t lxc_id, const o_lxc_cfg *cfg) { a->slot[lxc_id & 0xffff] = cfg; }
 
 void o_ingress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out) {
-    for (uint32_t i = 0; i < b->n; i++) handle_policy(a, b, i, now, &out[i]);
+    uint8_t *plog = (uint8_t *)calloc((size_t)b->n + 1, O_PLOG);
+    for (uint32_t i = 0; i < b->n; i++) handle_policy(a, b, i, now, &out[i], plog, NULL);
+    proxy_apply(b, plog, out, NULL);
+    free(plog);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1116,6 +1249,7 @@ typedef struct mt_arg {
     uint32_t *owner, *cnt, *list, *start;
     int phase;
     const uint8_t *skip;                /* pipeline: packets that never reach handle_policy */
+    uint8_t *plog, *wsnap;              /* proxy log, writable frames (pipeline) */
     /* pipeline front pass (kind 3) */
     const o_pipeline_cfg *pc; o_pipeline_out *po; uint8_t *snap_out, *skip_w;
     uint32_t *secctx, *ifx; uint16_t *lxcid;
@@ -1172,7 +1306,7 @@ static void *mt_worker(void *p) {
             for (uint32_t k = a0; k < a1; k++) {
                 uint32_t i = m->list[k];
                 if (m->skip && m->skip[i]) continue;
-                handle_policy(m->a, b, i, m->now, &m->out[i]);
+                handle_policy(m->a, b, i, m->now, &m->out[i], m->plog, m->wsnap);
             }
         }
     } else if (m->kind == 3) {
@@ -1203,12 +1337,12 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
 }
 
 static void ingress_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads,
-                       const uint8_t *skip) {
+                       const uint8_t *skip, uint8_t *plog, uint8_t *wsnap) {
     if (threads < 1) threads = 1;
     if (threads > 1024) threads = 1024;
     uint32_t T = threads;
     mt_arg m; memset(&m, 0, sizeof m);
-    m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0; m.skip = skip;
+    m.a = a; m.b = b; m.now = now; m.out = out; m.kind = 0; m.skip = skip; m.plog = plog; m.wsnap = wsnap;
     m.owner = (uint32_t *)malloc((size_t)b->n * 4 + 4);
     m.list = (uint32_t *)malloc((size_t)b->n * 4 + 4);
     m.cnt = (uint32_t *)calloc((size_t)T * T, 4);
@@ -1229,7 +1363,10 @@ static void ingress_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_
     free(beg); free(m.owner); free(m.list); free(m.cnt); free(m.start);
 }
 void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
-    ingress_mt(a, b, now, out, threads, NULL);
+    uint8_t *plog = (uint8_t *)calloc((size_t)b->n + 1, O_PLOG);
+    ingress_mt(a, b, now, out, threads, NULL, plog, NULL);
+    proxy_apply(b, plog, out, NULL);
+    free(plog);
 }
 void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads) {
     mt_arg m; memset(&m, 0, sizeof m);
@@ -1250,7 +1387,6 @@ void o_lb_batch_mt(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t
 /* network-order bytes, exactly what the BPF programs pass.  The skb is */
 /* taken as not CHECKSUM_PARTIAL (a received frame).                    */
 /* ------------------------------------------------------------------ */
-#define BPF_F_PSEUDO_HDR (1u << 4)
 #define BPF_F_MARK_MANGLED_0 (1u << 5)
 #define ENDPOINT_F_HOST 1u
 #define WORLD_ID 2u
@@ -1279,6 +1415,7 @@ static uint32_t csum_l4_flags(uint8_t nexthdr) { return nexthdr == IPPROTO_UDP ?
 
 /* writes into the frame copy w (bytes past the snap are not kept) */
 static void wbytes(const skb_t *s, uint8_t *w, uint32_t off, const void *from, uint32_t n) {
+    if (!w) return;
     for (uint32_t k = 0; k < n; k++) if (off + k < s->cap) w[off + k] = ((const uint8_t *)from)[k];
 }
 /* bpf_skb_store_bytes */
@@ -1509,11 +1646,14 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
         /* handle_policy over the rewritten frames, flow groups of the rewritten addresses */
         o_batch b2 = *b;
         b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+        uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
         if (threads == 1) {
-            for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(c->policy, &b2, i, now, &ing[i]);
+            for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(c->policy, &b2, i, now, &ing[i], plog, snap);
         } else {
-            ingress_mt(c->policy, &b2, now, ing, threads, skip);
+            ingress_mt(c->policy, &b2, now, ing, threads, skip, plog, snap);
         }
+        proxy_apply(&b2, plog, ing, snap);
+        free(plog);
     }
     for (uint32_t i = 0; i < n; i++) {
         o_pipeline_out *o = &out[i];

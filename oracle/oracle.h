@@ -68,7 +68,14 @@ typedef struct o_lxc_cfg {
     o_l4_allow l4_ingress[64];
 } o_lxc_cfg;
 
-typedef struct o_node_cfg { uint32_t host_ifindex; } o_node_cfg;
+typedef struct o_node_cfg {       /* == gf_node_cfg (bpf/node_config.h values on the path) */
+    uint32_t host_ifindex;        /* HOST_IFINDEX */
+    om_map *proxy4_map, *proxy6_map;  /* cilium_proxy4 / cilium_proxy6 (NULL: not installed) */
+    uint32_t ipv4_gateway;        /* IPV4_GATEWAY (raw be32) */
+    uint8_t host_ip6[16];         /* HOST_IP */
+    uint8_t host_mac[6];          /* HOST_IFINDEX_MAC */
+    uint8_t node_mac[6];          /* NODE_MAC */
+} o_node_cfg;
 
 /* Per-packet metadata of a batch (host arrays, may be NULL where unused). */
 typedef struct o_batch {

@@ -32,7 +32,8 @@ class o_lxc_cfg(C.Structure):
 
 
 class o_node_cfg(C.Structure):
-    _fields_ = [("host_ifindex", C.c_uint32)]
+    _fields_ = [("host_ifindex", C.c_uint32), ("proxy4_map", VP), ("proxy6_map", VP), ("ipv4_gateway", C.c_uint32),
+                ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6)]
 
 
 class o_batch(C.Structure):

@@ -17,7 +17,12 @@ class OracleDP:
                 om.update_many(np.ascontiguousarray(spec.keys, np.uint8), np.ascontiguousarray(spec.vals, np.uint8))
             self.m[name] = om
         p = lambda name: self.m[name].ptr if name else None
-        O.lib.o_set_node(C.byref(O.o_node_cfg(sc.host_ifindex)))
+        nd = sc.node or {}
+        self._node = O.o_node_cfg(sc.host_ifindex, p(nd.get("proxy4")), p(nd.get("proxy6")), nd.get("ipv4_gateway", 0),
+                                  (C.c_uint8 * 16)(*nd.get("host_ip6", bytes(16))),
+                                  (C.c_uint8 * 6)(*nd.get("host_mac", bytes(6))),
+                                  (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))))
+        O.lib.o_set_node(C.byref(self._node))
         self.xdp_cfg = self.lb_cfg = None
         if sc.xdp:
             x = sc.xdp
@@ -61,12 +66,14 @@ class OracleDP:
         return O.lb(self.lb_cfg, self.batch(pk), threads)
 
     def ingress(self, pk, now, threads=1):
+        O.lib.o_set_node(C.byref(self._node))           # node_config.h is process-global in the restatement
         return O.ingress(self.arr, self.batch(pk), now, threads)
 
     def ingress_events(self, pk, out):
         return O.ingress_events(self.arr, self.batch(pk), out)
 
     def pipeline(self, pk, now, threads=1, events=False):
+        O.lib.o_set_node(C.byref(self._node))
         if self._pipe is None:
             nd = self.sc.netdev
             self._nd = O.o_netdev_cfg(self.m[nd["lxc_map"]].ptr, nd.get("flags", 0), nd.get("fixed_secctx", 0),

@@ -144,7 +144,8 @@ def test_ct_counter_carry_and_codec():
     assert (0x100000000, 100 + 94) in rx and (6, 0xfffffff0 + 0x20 + 54) in rx
 
 
-@pytest.mark.parametrize("seed,kw", [(3, {}), (4, {"fixed_secctx": 300}), (8, {"lb_redirect": True})])
+@pytest.mark.parametrize("seed,kw", [(3, {}), (4, {"fixed_secctx": 300}), (8, {"lb_redirect": True}),
+                                     (9, {"proxy_max": 12})])
 def test_pipeline_fuzz(seed, kw):
     """Config 4 composition: bpf_xdp -> bpf_lb -> bpf_netdev -> handle_policy over
     raw frames; records, LB v6 addresses, the rewritten headers (MACs, TTL, daddr,
@@ -166,6 +167,11 @@ def test_pipeline_fuzz(seed, kw):
     assert dp.dump_map("ct6") == ref.dump("ct6")
     for e in range(16):
         assert dp.dump_map(f"pol{e}") == ref.dump(f"pol{e}"), f"policy counters pol{e}"
+    # cilium_proxy4/6 entries of the proxy redirects (lib/lxc.h:96-205), batch-order semantics
+    p4, p6 = ref.dump("cilium_proxy4"), ref.dump("cilium_proxy6")
+    assert len(p4) > 0
+    assert dp.dump_map("cilium_proxy4") == p4
+    assert dp.dump_map("cilium_proxy6") == p6
 
 
 def test_pipeline_checksum_rewrites():

@@ -20,6 +20,23 @@ def test_pipeline_threads_equal_sequential():
     assert a.dump("ct4") == b.dump("ct4")
     for e in range(16):
         assert a.dump(f"pol{e}") == b.dump(f"pol{e}")
+    assert a.dump("cilium_proxy4") == b.dump("cilium_proxy4") and len(a.dump("cilium_proxy4")) > 0
+
+
+def test_proxy_map_full_is_sequential():
+    """cilium_proxy4 updates in batch order: with a map that fills inside the
+    batch, exactly the redirects past capacity become DROP_PROXYMAP_CREATE_FAILED
+    (-161), sequential and threaded restatements alike."""
+    sc = synth.pipeline_fuzz(seed=9, n_packets=20000, n_batches=2, proxy_max=12)
+    a, b = OracleDP(sc), OracleDP(sc, shards=4)
+    fails = 0
+    for bi, pk in enumerate(sc.batches):
+        o1, _, s1 = a.pipeline(pk, sc.now + bi, threads=1)
+        o2, _, s2 = b.pipeline(pk, sc.now + bi, threads=4)
+        assert np.array_equal(o1, o2) and np.array_equal(s1, s2)
+        fails += int((o1["reason"] == 161).sum())
+    assert fails > 0
+    assert len(a.dump("cilium_proxy4")) == 12
 
 
 def test_pipeline_stage_accounting():
