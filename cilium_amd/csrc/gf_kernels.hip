@@ -478,7 +478,7 @@ __device__ __forceinline__ Row pol_row(const IngCtx &X, uint32_t i, uint32_t len
 // reverse_map_l4_port (bpf/lib/lb.h:217-251) + __lb4_rev_nat / __lb6_rev_nat
 // (lb.h:253-293, 447-512; v4 with REV_NAT_F_TUPLE_SADDR: the old address is the
 // tuple's, v6 with flags 0: the frame's)
-__device__ __attribute__((noinline)) void pol_rev_nat_write(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+__device__ __forceinline__ void pol_rev_nat_write(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
                                                             uint32_t nh, const uint8_t *nat, bool v6,
                                                             uint32_t old_sip4) {
     Row w = pol_row(X, i, len);
@@ -508,7 +508,7 @@ __device__ __attribute__((noinline)) void pol_rev_nat_write(const IngCtx &X, uin
     }
 }
 // ipv6_policy's "derive reverse NAT index and zero it" (bpf_lxc.c:774-790)
-__device__ __attribute__((noinline)) void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+__device__ __forceinline__ void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
                                                          uint32_t nh, uint32_t rn) {
     Row w = pol_row(X, i, len);
     w.w16(38 + 12, 0);
@@ -519,7 +519,7 @@ __device__ __attribute__((noinline)) void pol_v6_zero_rn(const IngCtx &X, uint32
 // ipv{4,6}_redirect_to_host_port writes (lib/lxc.h:96-205) after their checks,
 // and the cilium_proxy{4,6} entry, logged for the in-order apply after the launch.
 // t: the CT tuple words as ct_lookup left them; od: the original daddr.
-__device__ __attribute__((noinline)) void pol_redirect(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+__device__ __forceinline__ void pol_redirect(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
                                                        uint32_t nh, const uint32_t *t, bool v6, uint32_t new_port,
                                                        const uint32_t *od, uint32_t identity) {
     const uint32_t pw = v6 ? t[8] : t[2];
@@ -979,6 +979,22 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
     return D_CT_UNKNOWN_PROTO;
 }
 
+// Out-of-line copies for the IPv6 kernel, whose register budget the inlined
+// cold paths would cut to 2 waves/SIMD (the IPv4 kernel keeps them inline).
+__device__ __attribute__((noinline)) void pol_rev_nat_write_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                               uint32_t nh, const uint8_t *nat) {
+    pol_rev_nat_write(X, i, len, l4_off, nh, nat, true, 0u);
+}
+__device__ __attribute__((noinline)) void pol_v6_zero_rn_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                            uint32_t nh, uint32_t rn) {
+    pol_v6_zero_rn(X, i, len, l4_off, nh, rn);
+}
+__device__ __attribute__((noinline)) void pol_redirect_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+                                                          uint32_t nh, const uint32_t *t, uint32_t new_port,
+                                                          const uint32_t *od, uint32_t identity) {
+    pol_redirect(X, i, len, l4_off, nh, t, true, new_port, od, identity);
+}
+
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
                            uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo &pm) {
@@ -1064,7 +1080,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     uint32_t co = csum_l4_offset(nh);
     uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
     if (rn_new) {
-        if (X.snap) pol_v6_zero_rn(X, i, len, r.l4_off, nh, rn_new);
+        if (X.snap) pol_v6_zero_rn_ol(X, i, len, r.l4_off, nh, rn_new);
         if (co && !l4csum_ok(r.l4_off + (int)co, len)) return D_CSUM_L4;
     }
     uint32_t tfl = 0;
@@ -1095,7 +1111,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 16), r.l4w0, true);
             if (r2 < 0) return r2;
-            if (X.snap) pol_rev_nat_write(X, i, len, r.l4_off, nh, nat, true, 0u);
+            if (X.snap) pol_rev_nat_write_ol(X, i, len, r.l4_off, nh, nat);
         }
     }
     int verdict = policy_ingress(X, ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
@@ -1116,7 +1132,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
-        if (X.snap || X.plog) { const uint32_t od[4] = {d.x, d.y, d.z, d.w}; pol_redirect(X, i, len, r.l4_off, nh, t, true, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
+        if (X.snap || X.plog) { const uint32_t od[4] = {d.x, d.y, d.z, d.w}; pol_redirect_ol(X, i, len, r.l4_off, nh, t, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
         ifindex = X.host_ifindex;
         ofl |= GF_INGRESS_F_PROXY;
         proxy = (uint16_t)verdict;
