@@ -76,7 +76,11 @@ class gf_lxc_cfg(C.Structure):
                 ("ct_map4", C.c_int), ("ct_map6", C.c_int), ("cidr4_ingress_map", C.c_int),
                 ("cidr6_ingress_map", C.c_int), ("revnat4_map", C.c_int), ("revnat6_map", C.c_int),
                 ("flags", C.c_uint32), ("n_l4_ingress", C.c_uint32),
-                ("l4_ingress", gf_l4_allow * GF_MAX_L4_INGRESS)]
+                ("l4_ingress", gf_l4_allow * GF_MAX_L4_INGRESS), ("lxc_mac", C.c_uint8 * 6),
+                ("node_mac", C.c_uint8 * 6), ("lxc_ipv4", C.c_uint32), ("lb4_services", C.c_int),
+                ("ipcache_map", C.c_int), ("cidr4_egress_map", C.c_int), ("n_portmap", C.c_uint32),
+                ("portmap", C.c_uint16 * 32), ("n_l4_egress", C.c_uint32),
+                ("l4_egress", gf_l4_allow * GF_MAX_L4_INGRESS)]
 
 
 class gf_prof_rec(C.Structure):
@@ -86,7 +90,9 @@ class gf_prof_rec(C.Structure):
 class gf_node_cfg(C.Structure):
     _fields_ = [("host_ifindex", C.c_uint32), ("proxy4_map", C.c_int), ("proxy6_map", C.c_int),
                 ("ipv4_gateway", C.c_uint32), ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6),
-                ("node_mac", C.c_uint8 * 6)]
+                ("node_mac", C.c_uint8 * 6), ("lxc_map", C.c_int), ("ipv4_cluster_range", C.c_uint32),
+                ("ipv4_cluster_mask", C.c_uint32), ("ipv4_loopback", C.c_uint32), ("ipv4_mask", C.c_uint32),
+                ("encap_ifindex", C.c_uint32), ("tunnel_map", C.c_int)]
 
 
 class gf_netdev_cfg(C.Structure):
@@ -100,6 +106,10 @@ class gf_pipeline_cfg(C.Structure):
 
 class gf_pipe_batch(C.Structure):
     _fields_ = [("frames", gf_frames), ("tc_index", C.c_void_p), ("flow_hash", C.c_void_p)]
+
+
+class gf_lxc_batch(C.Structure):
+    _fields_ = [("frames", gf_frames), ("lxc_id", C.c_void_p), ("flow_hash", C.c_void_p)]
 
 
 class gf_event_ring(C.Structure):
@@ -142,6 +152,7 @@ _sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c
 _sig("gf_pipeline_load", C.c_int, C.POINTER(gf_pipeline_cfg))
 _sig("gf_pipeline_classify", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, VP, VP, VP, VP)
 _sig("gf_ct_gc", C.c_int, C.c_int, C.c_uint32, VP)
+_sig("gf_lxc_egress_classify", C.c_int, C.c_int, C.POINTER(gf_lxc_batch), C.c_uint32, VP, VP, VP)
 _sig("gf_set_event_ring", C.c_int, C.POINTER(gf_event_ring))
 _sig("gf_set_stats_sink", C.c_int, VP)
 _sig("gf_prof_enable", C.c_int, C.c_int)
@@ -161,6 +172,6 @@ EXPORTED = [
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_ct_gc", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_lxc_egress_classify", "gf_ct_gc", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
 ]

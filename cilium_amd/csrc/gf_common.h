@@ -224,4 +224,11 @@ struct gf_lxc_dev {
     gf_htab_desc policy, ct4, ct6, revnat4, revnat6;
     gf_trie_desc cidr4, cidr6;
     gf_l4_allow_dev l4[GF_MAX_L4];
+    // the from-container section (bpf_lxc.c:427-658)
+    uint32_t lxc_mac[2], node_mac[2];  // 6 B each, LE words (upper half of word 1 zero)
+    uint32_t lxc_ipv4, n_portmap, n_l4e, pad;
+    gf_htab_desc lb4, ipcache;
+    gf_trie_desc cidr4e;
+    uint32_t portmap[16];              // from | to << 16 (raw be16 each)
+    gf_l4_allow_dev l4e[GF_MAX_L4];
 };

@@ -114,6 +114,7 @@ struct ProgLb : Obj {
 struct ProgLxc : Obj {
     gf_lxc_cfg cfg{};
     std::shared_ptr<Map> policy, ct4, ct6, cidr4, cidr6, revnat4, revnat6;
+    std::shared_ptr<Map> lb4, ipcache, cidr4e;   // from-container section
     ProgLxc() : Obj(ObjKind::ProgLxc) {}
 };
 struct PolicyArray : Obj {
@@ -142,6 +143,7 @@ int new_handle(std::shared_ptr<Obj> o);
 uint32_t host_ifindex();
 const gf_node_cfg &node_cfg();
 std::shared_ptr<Map> proxy_map(int fam);   // cilium_proxy4 (4) / cilium_proxy6 (6), may be null
+std::shared_ptr<Map> node_map(int which);  // 1: cilium_lxc, 2: cilium_tunnel_map (gf_node_cfg), may be null
 uint64_t *stats_sink();
 
 // trie builder (host)

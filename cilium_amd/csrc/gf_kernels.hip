@@ -521,7 +521,7 @@ __device__ __forceinline__ void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint
 // t: the CT tuple words as ct_lookup left them; od: the original daddr.
 __device__ __forceinline__ void pol_redirect(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
                                                        uint32_t nh, const uint32_t *t, bool v6, uint32_t new_port,
-                                                       const uint32_t *od, uint32_t identity) {
+                                                       const uint32_t *od, uint32_t identity, uint32_t egress = 0) {
     const uint32_t pw = v6 ? t[8] : t[2];
     const uint32_t old_port = pw & 0xffffu, sport = pw >> 16;
     if (X.snap) {
@@ -554,6 +554,7 @@ __device__ __forceinline__ void pol_redirect(const IngCtx &X, uint32_t i, uint32
         q[8 + a] = old_port;
         q[9 + a] = identity;
         q[10 + a] = X.now + 720u;                       // PROXY_DEFAULT_LIFETIME
+        q[15] = egress;                                 // from-container entry: no handle_policy MAC stores
         for (int k = 0; k < 16; k += 4) *reinterpret_cast<uint4 *>(e + k) = make_uint4(q[k], q[k + 1], q[k + 2], q[k + 3]);
     }
 }
@@ -1806,7 +1807,10 @@ __global__ __launch_bounds__(BLOCK) void k_ev_write(EvSrc E, const uint32_t *bof
     const uint32_t reason = r[E.act_off + 1];
     uint32_t src = 0, dst = 0, dst_id = 0, ifx = 0, source = 0;
     const bool policy = E.stage_off < 0 || r[E.stage_off] == GF_STAGE_POLICY;
-    if (policy) {
+    if (E.stage_off >= 0 && r[E.stage_off] == GF_STAGE_FROM_LXC) {
+        const gf_rec pr = E.prec[i];                    // send_drop_notify(skb, SECLABEL, 0, 0, 0, ret) of the sender
+        if (pr.ep) { const gf_lxc_dev &cf = E.cfgs[pr.ep - 1]; src = cf.seclabel & 0xffffu; source = cf.lxc_id & 0xffffu; }
+    } else if (policy) {
         const gf_rec pr = E.prec[i];
         if (pr.ep) {                                    // handle_policy: send_drop_notify(src_label, SECLABEL, LXC_ID, ifindex)
             const gf_lxc_dev &cf = E.cfgs[pr.ep - 1];
@@ -1884,7 +1888,7 @@ __global__ __launch_bounds__(BLOCK) void k_px_apply(const uint32_t *plog, uint32
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const uint32_t *e = plog + 16ull * perm[p];
-    px_macs(P, e[0]);
+    if (!e[15]) px_macs(P, e[0]);
     const uint32_t h = (uint32_t)(key[p] >> 32);
     for (uint32_t q = p + 1; q < n && (uint32_t)(key[q] >> 32) == h; q++)
         if (px_same(e, plog + 16ull * perm[q])) return;     // a later update of the same key wins
@@ -1897,7 +1901,7 @@ __global__ void k_px_apply_seq(const uint32_t *plog, uint32_t n, const uint32_t 
     for (uint32_t p = 0; p < n; p++) {
         const uint32_t *e = plog + 16ull * perm[p];
         const uint32_t i = e[0];
-        if (px_upsert(P, e, true, nullptr) >= 0) { px_macs(P, i); continue; }
+        if (px_upsert(P, e, true, nullptr) >= 0) { if (!e[15]) px_macs(P, i); continue; }
         uint8_t *r = recs + (size_t)i * stride;             // DROP_PROXYMAP_CREATE_FAILED
         const uint32_t old_action = r[act_off];
         r[act_off] = TC_SHOT; r[act_off + 1] = 161;
@@ -1908,6 +1912,599 @@ __global__ void k_px_apply_seq(const uint32_t *plog, uint32_t n, const uint32_t 
             atomicAdd(&stats[256 + old_action], ~0ull); atomicAdd(&stats[256 + TC_SHOT], 1ull);
         }
     }
+}
+
+// ================================================================ endpoint egress (from-container)
+// handle_ingress (bpf/bpf_lxc.c:685-738) -> tail_handle_ipv4 -> handle_ipv4_from_lxc
+// (:427-658) over frames sent by local endpoints.  k_eg_front runs the stateless
+// part on one packet per lane (checks, lb4_local with its lb4_xlate rewrites,
+// map_lxc_out) and keys the packet by the flow group of its CT tuple; the
+// schedule of the ingress path orders the groups; k_eg_groups runs the CT /
+// policy part of each bucket on one lane in batch order, ending in a verdict or
+// in ipv4_local_delivery, whose handle_policy runs in the ingress pass after it.
+// ct_create4's service entry (conntrack.h:533-561) has the pair {target, target}
+// or {IPV4_LOOPBACK, sender}, outside the packet's group: it is logged and
+// applied after the launch in batch order (last writer wins, as in order).  No
+// packet of the batch reads such a key unless its own tuple has that shape
+// (saddr == daddr, or IPV4_LOOPBACK in it); k_eg_front flags those batches and
+// they run as a single bucket with the entry written inline.
+enum {
+    D_INVALID_SMAC = -130, D_INVALID_DMAC = -131, D_INVALID_SIP = -132, D_NO_LXC = -152, D_CSUM_L3 = -153,
+    D_POLICY_CIDR = -162,
+};
+#define GF_EGR_FINAL 1u                 // EgRec.st: the verdict was written by k_eg_front
+struct __attribute__((aligned(16))) EgRec {   // 32 B: what the CT part needs from the front
+    uint32_t t_daddr, t_saddr;          // CT tuple addresses after lb4_local
+    uint32_t len, orig_dip;             // skb->len; orig_dip (tuple.daddr after lb4_local)
+    uint32_t ct_addr;                   // ct_state_new.addr (0: not load balanced)
+    uint16_t rev_nat, ep;               // ct_state_new.rev_nat_index; program slot + 1
+    int16_t  l4_off;
+    uint8_t  nh, st;
+    uint16_t slave, eflags;             // lb4_local's slave; GF_EG_F_* so far
+};
+static_assert(sizeof(EgRec) == 32, "EgRec must be 32 bytes");
+struct EgDev {
+    const gf_lxc_dev *cfgs;
+    const uint16_t *slot_of;
+    gf_htab_desc ct4, lxc, tunnel;
+    uint8_t *snap;                      // the frames, rewritten in place
+    uint32_t stride, now, host_ifindex, encap_ifindex;
+    uint32_t cluster_range, cluster_mask, loopback, ipv4_mask;
+    uint32_t host_mac[2];
+    uint32_t strict;                    // CT4 inserts check max_entries (forces the single bucket)
+    uint32_t *seq;                      // device word: 1 = single-bucket batch (written by k_eg_front)
+    uint32_t *ctlog, *ctlog_n;          // deferred service entries: {i, key[4], value[12], pad[3]}
+    IngCtx X;                           // redirect writes + cilium_proxy4 log (pol_redirect)
+};
+#define GF_CTLOG_WORDS 20u
+
+__device__ __forceinline__ Row eg_row(const EgDev &E, uint32_t i, uint32_t len) {
+    return Row{E.snap + (size_t)i * E.stride, E.stride < len ? E.stride : len};
+}
+__device__ __forceinline__ bool mac_eq(const Row &w, uint32_t off, const uint32_t *m) {
+    return w.r32(off) == m[0] && w.r16(off + 4) == (m[1] & 0xffffu);
+}
+// ipv4_l3 (bpf/lib/l3.h:54-70) + ipv4_dec_ttl (bpf/lib/ipv4.h:30-43); smac may be null
+__device__ __forceinline__ int eg_ipv4_l3(Row &w, uint32_t len, const uint32_t *smac, const uint32_t *dmac) {
+    const uint32_t ttl = w.b(22);
+    if (ttl <= 1) return D_INVALID;
+    l3_csum(w, len, 24, ttl, ttl - 1, 2);
+    w.w8(22, ttl - 1);
+    if (smac) { w.w32(6, smac[0]); w.w16(10, smac[1] & 0xffffu); }
+    w.w32(0, dmac[0]); w.w16(4, dmac[1] & 0xffffu);
+    return TC_OK;
+}
+
+// handle_ingress + the stateless head of handle_ipv4_from_lxc, one packet per lane
+__global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t *lxc_id, const uint32_t *fhash, EgDev E,
+                                                    EgRec *erec, uint32_t *keys, gf_egress_out *out,
+                                                    unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    if (stats) st.init();
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < fr.n) {
+        const uint32_t len = fr.len[i], S = fr.snap_stride;
+        {   // the frame, rewritten in place from here on
+            const uint8_t *src = fr.snap + (size_t)i * S;
+            uint8_t *dst = E.snap + (size_t)i * S;
+            if (src != dst) for (uint32_t k = 0; k < S; k++) dst[k] = src[k];
+        }
+        Row w = eg_row(E, i, len);
+        gf_egress_out o{};
+        EgRec r{};
+        r.len = len;
+        uint32_t ab = 24 + 34;                            // output record, header bytes parsed
+        const uint32_t sl_ = E.slot_of[lxc_id ? lxc_id[i] : 0];
+        r.ep = (uint16_t)sl_;
+        r.st = GF_EGR_FINAL;
+        int ret = TC_OK;
+        o.stage = GF_STAGE_FROM_LXC;
+        const uint32_t et = len >= 14 ? ((w.b(12) << 8) | w.b(13)) : 0u;
+        do {
+            if (!sl_) { ret = D_MISSED_TAIL_CALL; break; }
+            const gf_lxc_dev *c = E.cfgs + (sl_ - 1);
+            const uint32_t flags = gload<uint32_t>(&c->flags);
+            if (et == 0x0806) { o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_ARP; break; }
+            if (flags & GF_LXC_F_DROP_ALL) { ret = D_POLICY; break; }
+            if (et == 0x86DD) { o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_IPV6; break; }
+            if (et != 0x0800) { ret = D_UNKNOWN_L3; break; }
+            if (len < 34) { ret = D_INVALID; break; }
+            const uint32_t nh = w.b(23);
+            uint32_t m[2];
+            m[0] = gload<uint32_t>(&c->lxc_mac[0]); m[1] = gload<uint32_t>(&c->lxc_mac[1]);
+            if (!mac_eq(w, 6, m)) { ret = D_INVALID_SMAC; break; }
+            m[0] = gload<uint32_t>(&c->node_mac[0]); m[1] = gload<uint32_t>(&c->node_mac[1]);
+            if (!mac_eq(w, 0, m)) { ret = D_INVALID_DMAC; break; }
+            const uint32_t saddr = w.r32(26), daddr = w.r32(30);
+            if (!(flags & GF_LXC_F_LXC_IPV4) || saddr != gload<uint32_t>(&c->lxc_ipv4)) { ret = D_INVALID_SIP; break; }
+            const int l4_off = 14 + (int)(w.b(14) & 0xfu) * 4;
+            const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+            r.t_daddr = daddr; r.t_saddr = saddr; r.nh = (uint8_t)nh; r.l4_off = (int16_t)l4_off;
+            // lb4_extract_key (CT_EGRESS: key.address = daddr) + extract_l4_port (lb.h:191-215, 552-564)
+            bool lb_try = true;
+            uint32_t kport = 0;
+            if (nh == 6 || nh == 17) {
+                if (!skb_ok(l4_off + 2, 2, len)) { ret = -GF_EFAULT; break; }
+                kport = w.r16((uint32_t)(l4_off + 2));
+            } else if (nh != 1 && nh != 58) lb_try = false;     // DROP_UNKNOWN_L4: skip_service_lookup
+            const gf_htab_desc lb = gload<gf_htab_desc>(&c->lb4);
+            if (lb_try && lb.slots) {
+                // lb4_lookup_service (lb.h:566-597), LB_L4 then LB_L3
+                const uint8_t *svc = nullptr;
+                ab += 12;
+                if (kport) {
+                    uint32_t kw[2] = {daddr, kport};
+                    const int64_t f = ht_find<8>(lb, kw, key_hash<8>(kw));
+                    ab += 20;
+                    if (f >= 0) { const uint8_t *v = ht_val(lb, f); if (gload<uint16_t>(v + 6)) svc = v; }
+                    if (!svc) kport = 0;
+                }
+                if (!svc) {
+                    uint32_t kw[2] = {daddr, kport};
+                    const int64_t f = ht_find<8>(lb, kw, key_hash<8>(kw));
+                    ab += 20;
+                    if (f >= 0) { const uint8_t *v = ht_val(lb, f); if (gload<uint16_t>(v + 6)) svc = v; }
+                }
+                if (svc) {                                    // lb4_local, lb.h:662-699
+                    const uint32_t count = gload<uint16_t>(svc + 6);
+                    const uint32_t slave = ((fhash ? fhash[i] : 0u) % count + 1u) & 0xffffu;
+                    uint32_t kw[2] = {daddr, kport | (slave << 16)};
+                    const int64_t f = ht_find<8>(lb, kw, key_hash<8>(kw));
+                    ab += 20;
+                    if (f < 0) { ret = D_NO_SERVICE; break; }
+                    const uint8_t *be = ht_val(lb, f);
+                    const uint32_t target = gload<uint32_t>(be), sport_ = gload<uint16_t>(be + 4);
+                    r.slave = (uint16_t)slave; r.eflags |= GF_EG_F_LB;
+                    r.rev_nat = gload<uint16_t>(be + 8);
+                    r.ct_addr = target;
+                    uint32_t new_saddr = 0;
+                    if (saddr == target) {                    // loopback back to the sender
+                        new_saddr = E.loopback; r.ct_addr = new_saddr; r.eflags |= GF_EG_F_LOOPBACK;
+                    } else r.t_daddr = target;
+                    // lb4_xlate (lb.h:615-659)
+                    w.w32(30, target);
+                    uint32_t sum = ck_add(ck_add(0u, ~daddr), target);
+                    if (new_saddr) {
+                        w.w32(26, new_saddr);
+                        sum = ck_add(sum, ck_add(ck_add(0u, ~saddr), new_saddr));
+                    }
+                    l3_csum(w, len, 24, 0, sum, 0);
+                    if (co && l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl) < 0) { ret = D_CSUM_L4; break; }
+                    if (sport_ && kport != sport_ && (nh == 6 || nh == 17)) {   // l4_modify_port
+                        if (l4_csum(w, len, l4_off + (int)co, kport, sport_, 2u | fl) < 0) { ret = D_CSUM_L4; break; }
+                        if (!skb_ok(l4_off + 2, 2, len)) { ret = D_WRITE_ERROR; break; }
+                        w.w16((uint32_t)(l4_off + 2), sport_);
+                    }
+                    ab += 12;
+                }
+            }
+            r.orig_dip = r.t_daddr;
+            // map_lxc_out (bpf_lxc.c:80-108) + l4_port_map_out (l4.h:107-118)
+            const uint32_t npm = gload<uint32_t>(&c->n_portmap);
+            if (npm && (nh == 6 || nh == 17)) {
+                if (!skb_ok(l4_off, 2, len)) { ret = D_INVALID; break; }
+                const uint32_t sp = w.r16((uint32_t)l4_off);
+                bool bad = false;
+                for (uint32_t k = 0; k < npm && k < 16; k++) {
+                    const uint32_t pm = gload<uint32_t>(&c->portmap[k]);
+                    const uint32_t from = pm & 0xffffu, to = pm >> 16;
+                    if (to != sp) continue;
+                    if (l4_csum(w, len, l4_off + (int)co, sp, from, 2u | fl) < 0) { ret = D_CSUM_L4; bad = true; break; }
+                    if (!skb_ok(l4_off, 2, len)) { ret = D_WRITE_ERROR; bad = true; break; }
+                    w.w16((uint32_t)l4_off, from);
+                    r.eflags |= GF_EG_F_PORTMAP;
+                }
+                if (bad) break;
+            }
+            r.st = 0;                                       // continue in k_eg_groups
+        } while (0);
+        uint32_t key;
+        if (r.st == 0) {
+            key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
+            const uint32_t lo = E.loopback;
+            if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || E.strict) *E.seq = 1u;
+        } else {
+            key = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
+            if (o.stage == GF_STAGE_FROM_LXC) {
+                if (ret < 0 || ret == TC_SHOT) {
+                    o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
+                    o.eg_flags = r.eflags & (GF_EG_F_LB | GF_EG_F_LOOPBACK | GF_EG_F_PORTMAP);
+                    o.slave = r.slave; o.rev_nat = r.rev_nat;
+                } else o.action = (uint8_t)ret;
+            }
+            out[i] = o;
+            if (stats) st.pkt(o.reason, o.action, len, ab);
+        }
+        erec[i] = r;
+        keys[i] = key;
+    }
+    if (stats) st.flush(stats);
+}
+
+// After the front: a flagged batch runs as one bucket (every key equal).
+__global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, uint32_t n, uint32_t *keys) {
+    if (!*seq) return;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] = 0u;
+}
+
+// __ct_lookup hit part for CT_EGRESS (conntrack.h:75-135): tx accounting (the
+// cold part of the value), TX_CLOSING on close.
+__device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int action, bool syn, uint32_t len,
+                                          uint32_t now, bool acct, CtState &st) {
+    uint8_t *e = ht_val(d, (uint64_t)f);
+    uint4 hot = gload<uint4>(e);
+    uint32_t life = hot.x, fl = hot.y & 0xffffu;
+    if (!(fl & F_RX_CLOSING) || !(fl & F_TX_CLOSING)) {
+        if (!syn) fl |= F_SEEN_NON_SYN;
+        life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+    }
+    st.rev_nat = hot.y >> 16;
+    st.loopback = (fl >> 3) & 1u;
+    if (acct) {                                         // tx_packets += 1, tx_bytes += len
+        uint8_t *base = d.sstride ? ht_side(d, (uint64_t)f) - 16 : e;   // internal value word k at base + 4k
+        gstore<unsigned long long>(base + 24, gload<unsigned long long>(base + 24) + 1ull);
+        gstore<unsigned long long>(base + 32, gload<unsigned long long>(base + 32) + (unsigned long long)len);
+    }
+    if (action == ACT_CREATE) {
+        if (fl & (F_RX_CLOSING | F_TX_CLOSING)) {
+            fl &= ~(F_RX_CLOSING | F_TX_CLOSING);
+            if (!syn) fl |= F_SEEN_NON_SYN;
+            life = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+        }
+    } else if (action == ACT_CLOSE) {
+        fl |= F_TX_CLOSING;
+        if ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) life = now + 10u;
+    }
+    hot.x = life;
+    hot.y = (hot.y & 0xffff0000u) | fl;
+    gstore<uint4>(e, hot);
+}
+
+// policy_can_egress4 (policy.h:241-264 with POLICY_EGRESS, else :282-289):
+// ipcache identity, __policy_can_access(dir = CT_EGRESS: key.egress = 1, the
+// CFG_L3L4_EGRESS list), reserved identities through CIDR4_EGRESS_MAP.
+__device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, uint32_t daddr, uint32_t dport,
+                         uint32_t proto, uint32_t len, uint32_t &ab) {
+    if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
+    if (!(flags & GF_LXC_F_POLICY_EGRESS)) return TC_OK;
+    uint32_t identity = dst_id;
+    const gf_htab_desc ic = gload<gf_htab_desc>(&c->ipcache);
+    if (ic.slots) {
+        uint32_t kw[5] = {daddr, 0, 0, 0, 1u};
+        const int64_t f = ht_find<20>(ic, kw, key_hash<20>(kw));
+        ab += 20;
+        if (f >= 0) { identity = gload<uint16_t>(ht_val(ic, f)); ab += 8; }
+    }
+    const gf_htab_desc pd = gload<gf_htab_desc>(&c->policy);
+    int verdict = D_POLICY;
+    int64_t f = -1;
+    bool l4hit = false;
+    if (flags & GF_LXC_F_HAVE_L4_POLICY) {
+        uint32_t kw[2] = {identity, dport | (proto << 16) | (1u << 24)};
+        f = ht_find<8, GF_POL_U>(pd, kw, key_hash<8, GF_HASH_POLICY>(kw));
+        ab += 8;
+        l4hit = f >= 0;
+    }
+    if (f < 0) {
+        uint32_t kw[2] = {identity, 1u << 24};
+        f = ht_find<8, GF_POL_U>(pd, kw, key_hash<8, GF_HASH_POLICY>(kw));
+        ab += 8;
+        if (f >= 0) verdict = TC_OK;
+    }
+    if (f < 0 && (flags & GF_LXC_F_HAVE_L4_POLICY)) {
+        uint32_t kw[2] = {0u, dport | (proto << 16) | (1u << 24)};
+        f = ht_find<8, GF_POL_U>(pd, kw, key_hash<8, GF_HASH_POLICY>(kw));
+        ab += 8;
+        l4hit = f >= 0;
+    }
+    if (f >= 0) {
+        uint8_t *cnt = pd.vals + (uint64_t)f * GF_POL_SIDE;          // packets / bytes (policy.h:67-92)
+        gadd64(cnt, 1ull);
+        gadd64(cnt + 8, (unsigned long long)len);
+        ab += 40;
+        if (l4hit) {
+            const uint32_t pp = gload<uint16_t>(ht_val(pd, (uint64_t)f));
+            verdict = 0;
+            if (pp) verdict = (int)pp;
+            else if (proto == 6 || proto == 17) {         // l4_egress_proxy_lookup (l4.h:178-188)
+                const uint32_t n = gload<uint32_t>(&c->n_l4e);
+                for (uint32_t k = 0; k < n; k++) {
+                    const gf_l4_allow_dev a = gload<gf_l4_allow_dev>(&c->l4e[k]);
+                    if (a.port && a.port == dport) { if (a.nexthdr && a.nexthdr == proto) { verdict = a.proxy; break; } }
+                }
+            }
+        }
+    }
+    if (identity < 256 && verdict < 0) {               // identity_is_reserved -> lpm4_egress_lookup
+        const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr4e);
+        if (tr.root_bits) ab += 9;
+        verdict = trie_lookup(tr, &daddr) ? 0 : D_POLICY_CIDR;
+    }
+    return verdict;
+}
+
+// The CT / policy part of handle_ipv4_from_lxc (bpf_lxc.c:499-658) for packet i.
+// Returns TC_OK / TC_REDIRECT / ND_TAILCALL (local delivery; ifx, lxc, mapped
+// filled) or an error.
+__device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, gf_egress_out &o, uint32_t &ifx, uint32_t &lxc,
+                          int *added, bool seq, uint32_t &ab) {
+    const uint32_t len = r.len, nh = r.nh;
+    const int l4_off = r.l4_off;
+    const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
+    const uint32_t flags = gload<uint32_t>(&c->flags);
+    Row w = eg_row(E, i, len);
+    const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+    // ct_lookup4(CT_EGRESS): the L4 words as the frame holds them now
+    gf_rec hr{};
+    hr.len = len; hr.l4_off = (int16_t)l4_off;
+    for (int k = 0; k < 4; k++) { const int64_t off = (int64_t)l4_off + k; if (off >= 0 && off < (int64_t)len) hr.l4w0 |= w.b((uint32_t)off) << (8 * k); }
+    {
+        uint32_t w3 = 0;
+        for (int k = 0; k < 2; k++) { const int64_t off = (int64_t)l4_off + 12 + k; if (off >= 0 && off < (int64_t)len) w3 |= w.b((uint32_t)off) << (8 * k); }
+        hr.l4w3 = (uint16_t)w3;
+    }
+    uint32_t t[4] = {r.t_daddr, r.t_saddr, 0u, nh};
+    uint32_t tfl = 1u;                                  // TUPLE_F_IN (egress)
+    int action; bool syn;
+    int e = ct_l4(nh, false, hr, t[2], tfl, action, syn);
+    if (e < 0) return e;
+    t[3] = nh | (tfl << 8);
+    const gf_htab_desc &ct = E.ct4;
+    if (!(flags & GF_LXC_DEV_HAS_CT4)) return D_CT_CREATE_FAILED;   // (no CT map bound: never in a valid config)
+    const bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
+    uint32_t tf[4] = {t[1], t[0], (t[2] >> 16) | (t[2] << 16), nh | ((tfl ^ 1u) << 8)};
+    bool isb = false;
+    const int64_t f = ht_find2<14, GF_CT4_U>(ct, t, tf, key_hash<14, GF_HASH_CT>(t), &isb);
+    ab += 14;
+    CtState st{0, 0, 0};
+    int ret;
+    if (f >= 0 && !isb) {
+        ab += 96;
+        ct_hit_eg(ct, f, action, syn, len, E.now, acct, st);
+        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
+    } else {
+        ab += 14;
+        for (int k = 0; k < 4; k++) t[k] = tf[k];
+        tfl ^= 1u;
+        if (f >= 0) { ab += 96; ct_hit_eg(ct, f, action, syn, len, E.now, acct, st); ret = CT_ESTABLISHED; }
+        else ret = CT_NEW;
+    }
+    o.eg_ct_ret = (uint8_t)ret;
+    const uint32_t dst_id = ((r.orig_dip & E.cluster_mask) == E.cluster_range) ? 3u : 2u;   // CLUSTER_ID / WORLD_ID
+    const int verdict = eg_policy(c, flags, dst_id, t[1], t[2] & 0xffffu, nh, len, ab);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) {
+            ab += 14;
+            ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, (E.strict & 1) != 0, added);
+            o.eg_flags |= GF_EG_F_DELETED;
+        }
+        return verdict;
+    }
+    if (ret == CT_NEW) {                                // ct_create4(CT_EGRESS), conntrack.h:503-580
+        ab += 3 * (14 + 48);
+        const uint32_t loop = (r.eflags & GF_EG_F_LOOPBACK) ? 1u : 0u;
+        uint32_t efl = (nh == 6) ? 0u : F_SEEN_NON_SYN;
+        efl |= loop ? F_LB_LOOPBACK : 0u;
+        const uint32_t life = E.now + ((efl & F_SEEN_NON_SYN) ? 43200u : 300u);
+        const uint32_t seclabel = gload<uint32_t>(&c->seclabel);
+        // GF_VCODEC_CT: lifetime, flags|rev_nat, rx lo x2, rx hi x2, tx_packets, tx_bytes, unused, src_sec_id
+        uint32_t v[12] = {life, efl | ((uint32_t)r.rev_nat << 16), 0u, 0u, 0u, 0u, 1u, 0u, len, 0u, 0u, seclabel};
+        const bool strict = (E.strict & 1) != 0;
+        if (ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, t, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+        if (r.ct_addr) {
+            uint32_t t2[4] = {r.ct_addr, t[1], t[2], t[3]};          // dir EGRESS: tuple->daddr = ct_state->addr
+            if (loop) { t2[3] = nh | (1u << 8); t2[1] = r.t_saddr; }  // TUPLE_F_IN, tuple->saddr = svc_addr
+            if (seq) {
+                if (ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, t2, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+            } else {
+                uint32_t *lg = E.ctlog + (size_t)GF_CTLOG_WORDS * atomicAdd(E.ctlog_n, 1u);
+                lg[0] = i;
+                for (int k = 0; k < 4; k++) lg[1 + k] = t2[k];
+                for (int k = 0; k < 12; k++) lg[5 + k] = v[k];
+            }
+        }
+        uint32_t it[4] = {t[0], t[1], 0u, 1u | ((((t[3] >> 8) & 0xffu) | 2u) << 8)};
+        v[1] |= F_SEEN_NON_SYN;
+        if (ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+        o.eg_flags |= GF_EG_F_CREATED;
+    } else if (ret == CT_REPLY || ret == CT_RELATED) {
+        if (st.rev_nat) {                               // lb4_rev_nat(flags 0), lb.h:447-534
+            const gf_htab_desc rn = gload<gf_htab_desc>(&c->revnat4);
+            uint32_t kw[1] = {st.rev_nat};
+            const int64_t fr_ = ht_find<2>(rn, kw, key_hash<2>(kw));
+            ab += 8;
+            if (fr_ >= 0) {
+                const uint8_t *nat = ht_val(rn, fr_);
+                const uint32_t port = gload<uint16_t>(nat + 4);
+                if (port) {                             // reverse_map_l4_port
+                    if (nh == 6 || nh == 17) {
+                        if (!skb_ok(l4_off, 2, len)) return -GF_EFAULT;
+                        const uint32_t old = w.r16((uint32_t)l4_off);
+                        if (port != old) {
+                            if (l4_csum(w, len, l4_off + (int)co, old, port, 2u | fl) < 0) return D_CSUM_L4;
+                            if (!skb_ok(l4_off, 2, len)) return D_WRITE_ERROR;
+                            w.w16((uint32_t)l4_off, port);
+                        }
+                    } else if (nh != 1 && nh != 58) return D_UNKNOWN_L4;
+                }
+                const uint32_t old_sip = w.r32(26), new_sip = gload<uint32_t>(nat);
+                uint32_t sum = 0;
+                if (st.loopback) {
+                    const uint32_t old_dip = w.r32(30);
+                    w.w32(30, old_sip);
+                    sum = ck_add(ck_add(0u, ~old_dip), old_sip);
+                    t[1] = old_sip;
+                }
+                w.w32(26, new_sip);
+                sum = ck_add(sum, ck_add(ck_add(0u, ~old_sip), new_sip));
+                l3_csum(w, len, 24, 0, sum, 0);
+                if (co && l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl) < 0) return D_CSUM_L4;
+                ab += 16;
+            }
+            o.eg_flags |= GF_EG_F_REVNAT;
+        }
+    }
+    uint32_t nm[2] = {gload<uint32_t>(&c->node_mac[0]), gload<uint32_t>(&c->node_mac[1])};
+    if (verdict > 0) {                                  // ipv4_redirect_to_host_port + ipv4_l3 -> HOST_IFINDEX
+        const int r3 = redirect_checks(len, l4_off, nh);
+        if (r3 < 0) return r3;
+        const uint32_t od[1] = {r.orig_dip};
+        pol_redirect(E.X, i, len, l4_off, nh, t, false, (uint32_t)verdict & 0xffffu, od,
+                     gload<uint32_t>(&c->seclabel), 1u);
+        o.eg_flags |= GF_EG_F_PROXY;
+        o.proxy_port = (uint16_t)verdict;
+        const int r4 = eg_ipv4_l3(w, len, nm, E.host_mac);
+        if (r4 != TC_OK) return r4;
+        ifx = E.host_ifindex;
+        return TC_REDIRECT;
+    }
+    const uint32_t dip = w.r32(30);
+    if (E.lxc.slots) {                                  // lookup_ip4_endpoint
+        uint32_t kw[5] = {dip, 0, 0, 0, 1u};
+        const int64_t fe = ht_find<20>(E.lxc, kw, key_hash<20>(kw));
+        ab += 20;
+        if (fe >= 0) {
+            const uint8_t *ep = ht_val(E.lxc, fe);
+            ab += 8;
+            if (gload<uint32_t>(ep + 8) & 1u) {         // ENDPOINT_F_HOST -> to_host
+                if (!E.host_ifindex) return D_NO_LXC;
+                const int r4 = eg_ipv4_l3(w, len, nm, E.host_mac);
+                if (r4 != TC_OK) return r4;
+                o.eg_flags |= GF_EG_F_TO_HOST;
+                ifx = E.host_ifindex;
+                return TC_REDIRECT;
+            }
+            // ipv4_local_delivery (l3.h:136-168): ipv4_l3(node_mac, mac), map_lxc_in, tail call
+            const uint32_t ttl = w.b(22);
+            if (ttl <= 1) return D_INVALID;
+            l3_csum(w, len, 24, ttl, ttl - 1, 2);
+            w.w8(22, ttl - 1);
+            o.eg_flags |= GF_EG_F_LOCAL;
+            uint32_t mapped = 0, ndport = 0;
+            return delivery_tail(w, len, l4_off, nh, ep, ifx, lxc, mapped, ndport, ab);
+        }
+    }
+    if (E.encap_ifindex && E.tunnel.slots) {            // encap_and_redirect (lib/encap.h)
+        uint32_t kw[5] = {dip & E.ipv4_mask, 0, 0, 0, 1u};
+        const int64_t ft = ht_find<20>(E.tunnel, kw, key_hash<20>(kw));
+        ab += 20;
+        if (ft >= 0) {
+            o.tunnel_ip = __builtin_bswap32(gload<uint32_t>(ht_val(E.tunnel, ft)));
+            o.eg_flags |= GF_EG_F_ENCAP;
+            ifx = E.encap_ifindex;
+            ab += 20;
+            return TC_REDIRECT;
+        }
+    }
+    const int r4 = eg_ipv4_l3(w, len, nullptr, nm);    // pass_to_stack
+    if (r4 != TC_OK) return r4;
+    o.eg_flags |= GF_EG_F_TO_STACK;
+    return TC_OK;
+}
+
+// One bucket per lane from the longest-first queue (the ingress schedule), in
+// batch order.  Writes each packet's verdict, and for local deliveries the
+// handle_policy record + flow-group key of the ingress pass (rec2 / key2).
+__global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
+                                                     const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
+                                                     uint32_t *ct_count, unsigned long long *stats) {
+    __shared__ uint32_t sl[272];
+    __shared__ uint32_t sadd;
+    Stats st{sl};
+    if (threadIdx.x == 0) sadd = 0;
+    if (stats) st.init(); else __syncthreads();
+    const uint32_t nb = GF_SCHED_NFAM(sched)[0], lane = threadIdx.x & 63u;
+    uint32_t *queue = GF_SCHED_QUEUE(sched);
+    const bool seq = *E.seq != 0;
+    int added = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(queue, 64u);
+        base = __shfl(base, 0);
+        if (base >= nb) break;
+        const uint32_t tq = base + lane;
+        if (tq >= nb) continue;
+        const uint2 oc = order[tq];
+        for (uint32_t k = 0; k < oc.y; k++) {
+            const uint32_t i = perm[oc.x + k];
+            const EgRec r = erec[i];
+            gf_rec rr;
+            if (r.st) {                                 // final in the front: not part of the ingress pass
+                key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
+                rec2[i] = rr;
+                continue;
+            }
+            gf_egress_out o{};
+            o.stage = GF_STAGE_FROM_LXC;
+            o.slave = r.slave; o.rev_nat = r.rev_nat; o.eg_flags = r.eflags;
+            uint32_t ifx = 0, lxc = 0, ab = 24 + 34 + 32;
+            const int ret = eg_ct_part(E, r, i, o, ifx, lxc, &added, seq, ab);
+            o.ct_ret = o.eg_ct_ret;
+            if (ret == ND_TAILCALL) {                   // handle_policy of the destination, next pass
+                o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; o.ct_ret = 0;
+                PktHdr h2;
+                const Row w = eg_row(E, i, r.len);
+                parse_row(w.p, w.cap, r.len, h2);
+                const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
+                key2[i] = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
+                                   gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, false,
+                                   h2.s6, h2.d6, rr);
+                if (stats) st.add_n(270, ab);
+            } else {
+                if (ret < 0 || ret == TC_SHOT) {
+                    o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
+                    o.eg_flags &= (GF_EG_F_CREATED | GF_EG_F_DELETED | GF_EG_F_LB | GF_EG_F_LOOPBACK | GF_EG_F_PORTMAP |
+                                   GF_EG_F_REVNAT);
+                    o.proxy_port = 0; o.tunnel_ip = 0;
+                } else {
+                    o.action = (uint8_t)ret;
+                    o.ifindex_lo = (uint16_t)ifx;
+                }
+                key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
+                if (stats) st.pkt(o.reason, o.action, r.len, ab);
+            }
+            rec2[i] = rr;
+            out[i] = o;
+        }
+    }
+    if (!(E.strict & 1)) {
+        if (added) atomicAdd(&sadd, (uint32_t)added);
+        __syncthreads();
+        if (threadIdx.x == 0 && sadd && ct_count) atomicAdd(ct_count, sadd);
+    }
+    if (stats) st.flush(stats);
+}
+
+// The deferred service entries of a launch, in batch order (k_px_apply's rule):
+// sorted by (key hash, packet index), an entry is applied only if no later
+// entry of the batch has the same key.
+__global__ __launch_bounds__(BLOCK) void k_ctlog_keys(const uint32_t *lg, const uint32_t *n_, unsigned long long *key,
+                                                      uint32_t *val, uint32_t cap) {
+    const uint32_t n = *n_ < cap ? *n_ : cap;
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= cap) return;
+    if (j >= n) { key[j] = ~0ull; val[j] = j; return; }
+    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
+    key[j] = ((unsigned long long)key_hash<14, GF_HASH_CT>(e + 1) << 32) | e[0];
+    val[j] = j;
+}
+__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, const unsigned long long *key,
+                                                       const uint32_t *perm, gf_htab_desc ct, uint32_t *ct_count) {
+    const uint32_t n = *n_;
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * perm[p];
+    const uint32_t h = (uint32_t)(key[p] >> 32);
+    for (uint32_t q = p + 1; q < n && (uint32_t)(key[q] >> 32) == h; q++) {
+        const uint32_t *g = lg + (size_t)GF_CTLOG_WORDS * perm[q];
+        bool same = true;
+        for (int k = 1; k < 5; k++) same &= (k < 4 ? g[k] == e[k] : (g[4] & 0xffffu) == (e[4] & 0xffffu));
+        if (same) return;                               // a later update of the same key wins
+    }
+    int added = 0;
+    ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
+    if (added && ct_count) atomicAdd(ct_count, (uint32_t)added);
 }
 
 // ================================================================ host: programs
@@ -2095,7 +2692,9 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
 int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
     std::lock_guard<std::recursive_mutex> g(big_lock());
     if (!cfg) return -EFAULT;
-    if (cfg->n_l4_ingress > GF_MAX_L4_INGRESS) return -E2BIG;
+    if (cfg->n_l4_ingress > GF_MAX_L4_INGRESS || cfg->n_l4_egress > GF_MAX_L4_INGRESS ||
+        cfg->n_portmap > GF_MAX_PORTMAP)
+        return -E2BIG;
     auto p = std::make_shared<ProgLxc>();
     p->cfg = *cfg;
     struct B { int h; uint32_t k, v; bool lpm; std::shared_ptr<Map> *out; };
@@ -2104,6 +2703,8 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         {cfg->ct_map6, 40, 48, false, &p->ct6},      {cfg->cidr4_ingress_map, 8, 0, true, &p->cidr4},
         {cfg->cidr6_ingress_map, 20, 0, true, &p->cidr6}, {cfg->revnat4_map, 2, 6, false, &p->revnat4},
         {cfg->revnat6_map, 2, 18, false, &p->revnat6},
+        {cfg->lb4_services, 8, 12, false, &p->lb4},      {cfg->ipcache_map, 20, 8, false, &p->ipcache},
+        {cfg->cidr4_egress_map, 8, 0, true, &p->cidr4e},
     };
     for (auto &b : binds) {
         if (!b.h) continue;
@@ -2196,120 +2797,27 @@ static int emit_drop_events(EvSrc E, hipStream_t s) {
     return hip_ok(hipGetLastError(), "k_drop_events");
 }
 
-// pack (may be empty): fills the records and bucket keys itself (the fused
-// pipeline front) instead of k_ing_pack; pout: pipeline records to complete.
-using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
-static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
-                       gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
-                       const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
-                       uint8_t *wsnap = nullptr) {
-    int r;
-    // 1. sync tables, build the device program table
-    std::vector<std::shared_ptr<ProgLxc>> progs;
-    std::map<ProgLxc *, uint32_t> index;
-    std::vector<uint16_t> slot_of(65536, 0);
-    bool any_v6 = false;
-    for (auto &kv : a->slots) {
-        auto &p = kv.second;
-        auto it = index.find(p.get());
-        if (it == index.end()) {
-            if (progs.size() >= 65535) return -E2BIG;
-            it = index.emplace(p.get(), (uint32_t)progs.size()).first;
-            progs.push_back(p);
-        }
-        slot_of[kv.first] = (uint16_t)(it->second + 1);
-    }
-    std::vector<gf_lxc_dev> cfgs(progs.size());
-    std::vector<std::shared_ptr<Map>> ctmaps;
-    for (size_t k = 0; k < progs.size(); k++) {
-        auto &p = progs[k];
-        for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6})
-            if ((r = push_map(m, s))) return r;
-        gf_lxc_dev &d = cfgs[k];
-        memset(&d, 0, sizeof d);
-        d.flags = p->cfg.flags; d.lxc_id = p->cfg.lxc_id; d.seclabel = p->cfg.seclabel;
-        d.n_l4 = p->cfg.n_l4_ingress;
-        for (uint32_t j = 0; j < d.n_l4; j++) {
-            d.l4[j].port = p->cfg.l4_ingress[j].port; d.l4[j].proxy = p->cfg.l4_ingress[j].proxy;
-            d.l4[j].nexthdr = p->cfg.l4_ingress[j].nexthdr;
-        }
-        if (p->policy) d.policy = p->policy->hdesc();
-        if (p->ct4) { d.ct4 = p->ct4->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT4; ctmaps.push_back(p->ct4); }
-        if (p->ct6) { d.ct6 = p->ct6->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT6; ctmaps.push_back(p->ct6); any_v6 = true; }
-        if (p->cidr4) d.cidr4 = p->cidr4->tdesc();
-        if (p->cidr6) d.cidr6 = p->cidr6->tdesc();
-        if (p->revnat4) d.revnat4 = p->revnat4->hdesc();
-        if (p->revnat6) d.revnat6 = p->revnat6->hdesc();
-    }
-    // CT maps: one counter is tracked in non-strict mode, so all programs must share
-    // one CT map per family (the production layout: cilium_ct4_global / ct6_global).
-    std::shared_ptr<Map> ct4m, ct6m;
-    for (auto &p : progs) {
-        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
-        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
-    }
-    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
-    // Strict (exact, atomic per insert) element accounting only when this batch could
-    // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
-    // fail in the kernel (they evict); here they keep entries past max_entries until
-    // GC and are bounded only by the slot array (7/8 load), see DESIGN.md.
-    // The decision uses a host-side upper bound of the device element count (each
-    // packet inserts at most 2 entries), read back from the device only when the
-    // bound gets near the limit — steady-state batches never wait on the GPU here.
-    uint32_t strict = 0;
-    gf_htab_desc cfg_ct4{}, cfg_ct6{};
-    if (ct4m) cfg_ct4 = ct4m->hdesc();
-    if (ct6m) cfg_ct6 = ct6m->hdesc();
-    for (auto &m : {ct4m, ct6m}) {
-        if (!m) continue;
-        // LRU: never fails in the kernel (it evicts); here no eviction in classify, the
-        // entries stay until GC, bounded by the slot array (7/8 load = 3.5 x max_entries)
-        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
-        if (m->host_valid) m->dev_count_hi = m->ht.count;
-        if (m->dev_count_hi + 2ull * pkts->n > limit && !m->host_valid) {
-            uint32_t dc = 0;
-            if (hip_ok(hipStreamSynchronize(s), "ct count sync") ||
-                hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
-                return -EIO;
-            m->dev_count_hi = dc;
-        }
-        if (m->dev_count_hi + 2ull * pkts->n > limit) strict |= m == ct4m ? 1u : 2u;
-        m->dev_count_hi += 2ull * pkts->n;
-        if (m->type == GF_MAP_TYPE_LRU_HASH) {
-            if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
-            else cfg_ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
-        }
-    }
-    // device program table: uploaded only when it changed (programs, bindings,
-    // or a map's device storage moved)
-    {
-        size_t cb = cfgs.size() * sizeof(gf_lxc_dev);
-        bool changed = a->dirty || a->h_cfgs.size() != cb || a->h_slot_of.size() != slot_of.size() ||
-                       (cb && memcmp(a->h_cfgs.data(), cfgs.data(), cb)) ||
-                       memcmp(a->h_slot_of.data(), slot_of.data(), slot_of.size() * 2);
-        if (changed) {
-            if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
-            if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cb)))) return r;
-            a->h_cfgs.assign((const uint8_t *)cfgs.data(), (const uint8_t *)cfgs.data() + cb);
-            a->h_slot_of = slot_of;
-            if (hip_ok(hipMemcpyAsync(a->d_slot_of_lxc.p, a->h_slot_of.data(), 65536 * 2, hipMemcpyHostToDevice, s), "slots"))
-                return -EIO;
-            if (cb && hip_ok(hipMemcpyAsync(a->d_cfgs.p, a->h_cfgs.data(), cb, hipMemcpyHostToDevice, s), "cfgs"))
-                return -EIO;
-            if (hip_ok(hipStreamSynchronize(s), "cfg sync")) return -EIO;
-            a->dirty = false;
-        }
-    }
-    // 2. group by flow group: stable radix sort of (32-bit group hash, index), then
-    //    run-length encoding of the sorted hashes (one bucket per run)
-    uint32_t n = pkts->n;
+// Per-batch workspace of the flow-group schedule (records, keys, sort, runs, order).
+static int ws_grow(uint32_t n) {
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    int r;
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
         (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
         (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 8)) ||
         (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
+    return 0;
+}
+
+// The flow-group schedule of ws().keys[0..n): stable radix sort of (32-bit group
+// hash, index), run-length encoding of the sorted hashes (one bucket per run),
+// then the longest-first bucket order per family, built on the device (no host
+// round trip): ws().perm / order / sched.
+static int schedule_groups(uint32_t n, hipStream_t s) {
+    Workspace &w = ws();
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    int r;
     uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
     size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
@@ -2319,15 +2827,6 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
                                   rocprim::plus<uint32_t>(), s);
     if ((r = grow(w.tmp, std::max(std::max(sort_bytes, scan_bytes), rle_bytes) + 256))) return r;
-    if (pack) {
-        if ((r = pack((const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p))) return r;
-    } else {
-        ProfScope ps("k_ing_pack", s);
-        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
-                           (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
-                           (uint32_t *)w.keys.p);
-        if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
-    }
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
@@ -2349,7 +2848,6 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                                            rocprim::plus<uint32_t>(), s), "exclusive_scan"))
             return -EIO;
     }
-    // 3. longest-first bucket order per family, built on the device (no host round trip)
     {
         ProfScope ps("k_bucket_sched", s);
         if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
@@ -2360,7 +2858,226 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
                            (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched, (uint2 *)w.order.p);
     }
-    if ((r = hip_ok(hipGetLastError(), "k_bucket_sched"))) return r;
+    return hip_ok(hipGetLastError(), "k_bucket_sched");
+}
+
+// cilium_proxy{4,6} update log of one launch (pol_redirect) and its in-order
+// apply after the launch (see k_px_apply).
+struct PxWs { DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp; };
+static PxWs &px_ws() { static PxWs w; return w; }
+static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X) {
+    auto px4 = proxy_map(4), px6 = proxy_map(6);
+    X.plog = nullptr; X.plog_n = nullptr;
+    if (!px4 && !px6) return 0;
+    PxWs &w = px_ws();
+    int r;
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    if ((r = grow(w.plog, (size_t)n * 64)) || (r = grow(w.plog_n, 4))) return r;
+    if (hip_ok(hipMemsetAsync(w.plog_n.p, 0, 4, s), "plog_n")) return -EIO;
+    for (auto &m : {px4, px6})
+        if (m && (r = push_map(m, s))) return r;
+    X.plog = (uint32_t *)w.plog.p; X.plog_n = (uint32_t *)w.plog_n.p;
+    return 0;
+}
+// recs: the launch's verdict records (24-B pipeline/egress layout when wide, else gf_ingress_out)
+static int px_log_apply(const IngCtx &X, hipStream_t s, uint8_t *wsnap, const uint32_t *len, uint32_t stride,
+                        uint8_t *recs, bool wide) {
+    if (!X.plog) return 0;
+    auto px4 = proxy_map(4), px6 = proxy_map(6);
+    const gf_node_cfg &node = node_cfg();
+    PxWs &w = px_ws();
+    int r;
+    uint32_t cnt = 0;
+    if (hip_ok(hipMemcpyAsync(&cnt, X.plog_n, 4, hipMemcpyDeviceToHost, s), "plog count") ||
+        hip_ok(hipStreamSynchronize(s), "plog sync"))
+        return -EIO;
+    if (!cnt) return 0;
+    PxDev P{};
+    bool seq = false;
+    for (auto &m : {px4, px6}) {
+        if (!m) continue;
+        if (m->host_valid) m->dev_count_hi = m->ht.count;
+        if (m->dev_count_hi + cnt > m->max_entries) seq = true;
+    }
+    if (px4) P.d4 = px4->hdesc();
+    if (px6) P.d6 = px6->hdesc();
+    P.snap = wsnap; P.len = len; P.snap_stride = stride;
+    memcpy(P.host_mac, node.host_mac, 6); memcpy(P.node_mac, node.node_mac, 6);
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    if ((r = grow(w.pkey, (size_t)cnt * 8)) || (r = grow(w.pkey2, (size_t)cnt * 8)) || (r = grow(w.pval, (size_t)cnt * 4)) ||
+        (r = grow(w.pperm, (size_t)cnt * 4)))
+        return r;
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)w.pkey.p, (unsigned long long *)w.pkey2.p,
+                                    (uint32_t *)w.pval.p, (uint32_t *)w.pperm.p, cnt, 0, 64, s);
+    if ((r = grow(w.ptmp, tb + 256))) return r;
+    ProfScope ps("k_proxy_apply", s);
+    const uint32_t g = (cnt + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_px_keys, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.plog.p, cnt, seq,
+                       (unsigned long long *)w.pkey.p, (uint32_t *)w.pval.p);
+    tb = w.ptmp.bytes;
+    if (hip_ok(rocprim::radix_sort_pairs(w.ptmp.p, tb, (unsigned long long *)w.pkey.p, (unsigned long long *)w.pkey2.p,
+                                         (uint32_t *)w.pval.p, (uint32_t *)w.pperm.p, cnt, 0, 64, s), "proxy sort"))
+        return -EIO;
+    if (seq)
+        hipLaunchKernelGGL(k_px_apply_seq, dim3(1), dim3(1), 0, s, (const uint32_t *)w.plog.p, cnt,
+                           (const uint32_t *)w.pperm.p, P, recs, wide ? 24u : 8u, wide ? 1u : 0u,
+                           (unsigned long long *)stats_sink());
+    else
+        hipLaunchKernelGGL(k_px_apply, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.plog.p, cnt,
+                           (const unsigned long long *)w.pkey2.p, (const uint32_t *)w.pperm.p, P);
+    if ((r = hip_ok(hipGetLastError(), "k_proxy_apply"))) return r;
+    for (auto &m : {px4, px6}) if (m) { m->device_modified(); m->dev_count_hi += cnt; }
+    return 0;
+}
+
+// The device program table of a cilium_policy array (every bound map pushed to
+// HBM first); uploaded only when it changed (programs, bindings, or a map's
+// device storage moved).  progs: the distinct programs, slot k+1 = progs[k].
+static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
+                      std::vector<std::shared_ptr<ProgLxc>> &progs) {
+    int r;
+    std::map<ProgLxc *, uint32_t> index;
+    std::vector<uint16_t> slot_of(65536, 0);
+    for (auto &kv : a->slots) {
+        auto &p = kv.second;
+        auto it = index.find(p.get());
+        if (it == index.end()) {
+            if (progs.size() >= 65535) return -E2BIG;
+            it = index.emplace(p.get(), (uint32_t)progs.size()).first;
+            progs.push_back(p);
+        }
+        slot_of[kv.first] = (uint16_t)(it->second + 1);
+    }
+    std::vector<gf_lxc_dev> cfgs(progs.size());
+    for (size_t k = 0; k < progs.size(); k++) {
+        auto &p = progs[k];
+        for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6, p->lb4, p->ipcache,
+                       p->cidr4e})
+            if ((r = push_map(m, s))) return r;
+        gf_lxc_dev &d = cfgs[k];
+        memset(&d, 0, sizeof d);
+        d.flags = p->cfg.flags; d.lxc_id = p->cfg.lxc_id; d.seclabel = p->cfg.seclabel;
+        d.n_l4 = p->cfg.n_l4_ingress;
+        for (uint32_t j = 0; j < d.n_l4; j++) {
+            d.l4[j].port = p->cfg.l4_ingress[j].port; d.l4[j].proxy = p->cfg.l4_ingress[j].proxy;
+            d.l4[j].nexthdr = p->cfg.l4_ingress[j].nexthdr;
+        }
+        if (p->policy) d.policy = p->policy->hdesc();
+        if (p->ct4) { d.ct4 = p->ct4->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT4; }
+        if (p->ct6) { d.ct6 = p->ct6->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT6; }
+        if (p->cidr4) d.cidr4 = p->cidr4->tdesc();
+        if (p->cidr6) d.cidr6 = p->cidr6->tdesc();
+        if (p->revnat4) d.revnat4 = p->revnat4->hdesc();
+        if (p->revnat6) d.revnat6 = p->revnat6->hdesc();
+        memcpy(d.lxc_mac, p->cfg.lxc_mac, 6);
+        memcpy(d.node_mac, p->cfg.node_mac, 6);
+        d.lxc_ipv4 = p->cfg.lxc_ipv4;
+        d.n_portmap = p->cfg.n_portmap;
+        for (uint32_t j = 0; j < d.n_portmap; j++)
+            d.portmap[j] = p->cfg.portmap[j].from | ((uint32_t)p->cfg.portmap[j].to << 16);
+        d.n_l4e = p->cfg.n_l4_egress;
+        for (uint32_t j = 0; j < d.n_l4e; j++) {
+            d.l4e[j].port = p->cfg.l4_egress[j].port; d.l4e[j].proxy = p->cfg.l4_egress[j].proxy;
+            d.l4e[j].nexthdr = p->cfg.l4_egress[j].nexthdr;
+        }
+        if (p->lb4) d.lb4 = p->lb4->hdesc();
+        if (p->ipcache) d.ipcache = p->ipcache->hdesc();
+        if (p->cidr4e) d.cidr4e = p->cidr4e->tdesc();
+    }
+    size_t cb = cfgs.size() * sizeof(gf_lxc_dev);
+    bool changed = a->dirty || a->h_cfgs.size() != cb || a->h_slot_of.size() != slot_of.size() ||
+                   (cb && memcmp(a->h_cfgs.data(), cfgs.data(), cb)) ||
+                   memcmp(a->h_slot_of.data(), slot_of.data(), slot_of.size() * 2);
+    if (changed) {
+        if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
+        if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cb)))) return r;
+        a->h_cfgs.assign((const uint8_t *)cfgs.data(), (const uint8_t *)cfgs.data() + cb);
+        a->h_slot_of = slot_of;
+        if (hip_ok(hipMemcpyAsync(a->d_slot_of_lxc.p, a->h_slot_of.data(), 65536 * 2, hipMemcpyHostToDevice, s), "slots"))
+            return -EIO;
+        if (cb && hip_ok(hipMemcpyAsync(a->d_cfgs.p, a->h_cfgs.data(), cb, hipMemcpyHostToDevice, s), "cfgs"))
+            return -EIO;
+        if (hip_ok(hipStreamSynchronize(s), "cfg sync")) return -EIO;
+        a->dirty = false;
+    }
+    return 0;
+}
+
+// Element accounting mode of the CT maps for a batch of n packets inserting at
+// most per_pkt entries each (see ingress_run); fills the launch descriptors.
+static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map> &ct6m, uint32_t n, uint32_t per_pkt,
+                     hipStream_t s, uint32_t &strict, gf_htab_desc &cfg_ct4, gf_htab_desc &cfg_ct6) {
+    strict = 0;
+    if (ct4m) cfg_ct4 = ct4m->hdesc();
+    if (ct6m) cfg_ct6 = ct6m->hdesc();
+    for (auto &m : {ct4m, ct6m}) {
+        if (!m) continue;
+        // LRU: never fails in the kernel (it evicts); here no eviction in classify, the
+        // entries stay until GC, bounded by the slot array (7/8 load = 3.5 x max_entries)
+        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
+        if (m->host_valid) m->dev_count_hi = m->ht.count;
+        if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && !m->host_valid) {
+            uint32_t dc = 0;
+            if (hip_ok(hipStreamSynchronize(s), "ct count sync") ||
+                hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
+                return -EIO;
+            m->dev_count_hi = dc;
+        }
+        if (m->dev_count_hi + (uint64_t)per_pkt * n > limit) strict |= m == ct4m ? 1u : 2u;
+        m->dev_count_hi += (uint64_t)per_pkt * n;
+        if (m->type == GF_MAP_TYPE_LRU_HASH) {
+            if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
+            else cfg_ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
+        }
+    }
+    return 0;
+}
+
+// pack (may be empty): fills the records and bucket keys itself (the fused
+// pipeline front) instead of k_ing_pack; pout: pipeline records to complete.
+using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
+static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
+                       gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
+                       const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
+                       uint8_t *wsnap = nullptr) {
+    int r;
+    // 1. sync tables, build the device program table
+    std::vector<std::shared_ptr<ProgLxc>> progs;
+    if ((r = prog_table(a, s, progs))) return r;
+    // CT maps: one counter is tracked in non-strict mode, so all programs must share
+    // one CT map per family (the production layout: cilium_ct4_global / ct6_global).
+    std::shared_ptr<Map> ct4m, ct6m;
+    for (auto &p : progs) {
+        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
+        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
+    }
+    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
+    // Strict (exact, atomic per insert) element accounting only when this batch could
+    // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
+    // fail in the kernel (they evict); here they keep entries past max_entries until
+    // GC and are bounded only by the slot array (7/8 load), see DESIGN.md.
+    // The decision uses a host-side upper bound of the device element count (each
+    // packet inserts at most 2 entries), read back from the device only when the
+    // bound gets near the limit — steady-state batches never wait on the GPU here.
+    uint32_t strict = 0;
+    gf_htab_desc cfg_ct4{}, cfg_ct6{};
+    if ((r = ct_limits(ct4m, ct6m, pkts->n, 2, s, strict, cfg_ct4, cfg_ct6))) return r;
+    // 2. group by flow group (records and keys first), 3. longest-first bucket order
+    uint32_t n = pkts->n;
+    Workspace &w = ws();
+    if ((r = ws_grow(n))) return r;
+    if (pack) {
+        if ((r = pack((const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p))) return r;
+    } else {
+        ProfScope ps("k_ing_pack", s);
+        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
+                           (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p,
+                           (uint32_t *)w.keys.p);
+        if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
+    }
+    if ((r = schedule_groups(n, s))) return r;
+    uint32_t *d_sched = (uint32_t *)w.sched.p;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
@@ -2374,16 +3091,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     const gf_node_cfg &node = node_cfg();
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
-    auto px4 = proxy_map(4), px6 = proxy_map(6);
-    static DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp;
-    if (px4 || px6) {
-        auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-        if ((r = grow(plog, (size_t)n * 64)) || (r = grow(plog_n, 4))) return r;
-        if (hip_ok(hipMemsetAsync(plog_n.p, 0, 4, s), "plog_n")) return -EIO;
-        for (auto &m : {px4, px6})
-            if (m && (r = push_map(m, s))) return r;
-        X.plog = (uint32_t *)plog.p; X.plog_n = (uint32_t *)plog_n.p;
-    }
+    if ((r = px_log_begin(n, s, X))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
@@ -2406,51 +3114,9 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
-    if (X.plog) {
-        // cilium_proxy{4,6} updates of this batch, in batch order (see k_px_apply)
-        uint32_t cnt = 0;
-        if (hip_ok(hipMemcpyAsync(&cnt, X.plog_n, 4, hipMemcpyDeviceToHost, s), "plog count") ||
-            hip_ok(hipStreamSynchronize(s), "plog sync"))
-            return -EIO;
-        if (cnt) {
-            PxDev P{};
-            bool seq = false;
-            for (auto &m : {px4, px6}) {
-                if (!m) continue;
-                if (m->host_valid) m->dev_count_hi = m->ht.count;
-                if (m->dev_count_hi + cnt > m->max_entries) seq = true;
-            }
-            if (px4) P.d4 = px4->hdesc();
-            if (px6) P.d6 = px6->hdesc();
-            P.snap = wsnap; P.len = ev_len ? ev_len : pkts->len; P.snap_stride = ev_stride;
-            memcpy(P.host_mac, node.host_mac, 6); memcpy(P.node_mac, node.node_mac, 6);
-            auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-            if ((r = grow(pkey, (size_t)cnt * 8)) || (r = grow(pkey2, (size_t)cnt * 8)) || (r = grow(pval, (size_t)cnt * 4)) ||
-                (r = grow(pperm, (size_t)cnt * 4)))
-                return r;
-            size_t tb = 0;
-            (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)pkey.p, (unsigned long long *)pkey2.p,
-                                            (uint32_t *)pval.p, (uint32_t *)pperm.p, cnt, 0, 64, s);
-            if ((r = grow(ptmp, tb + 256))) return r;
-            ProfScope ps("k_proxy_apply", s);
-            const uint32_t g = (cnt + BLOCK - 1) / BLOCK;
-            hipLaunchKernelGGL(k_px_keys, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)plog.p, cnt, seq,
-                               (unsigned long long *)pkey.p, (uint32_t *)pval.p);
-            tb = ptmp.bytes;
-            if (hip_ok(rocprim::radix_sort_pairs(ptmp.p, tb, (unsigned long long *)pkey.p, (unsigned long long *)pkey2.p,
-                                                 (uint32_t *)pval.p, (uint32_t *)pperm.p, cnt, 0, 64, s), "proxy sort"))
-                return -EIO;
-            if (seq)
-                hipLaunchKernelGGL(k_px_apply_seq, dim3(1), dim3(1), 0, s, (const uint32_t *)plog.p, cnt,
-                                   (const uint32_t *)pperm.p, P, pout ? pout : (uint8_t *)out, pout ? 24u : 8u,
-                                   pout ? 1u : 0u, (unsigned long long *)stats_sink());
-            else
-                hipLaunchKernelGGL(k_px_apply, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)plog.p, cnt,
-                                   (const unsigned long long *)pkey2.p, (const uint32_t *)pperm.p, P);
-            if ((r = hip_ok(hipGetLastError(), "k_proxy_apply"))) return r;
-            for (auto &m : {px4, px6}) if (m) { m->device_modified(); m->dev_count_hi += cnt; }
-        }
-    }
+    if ((r = px_log_apply(X, s, wsnap, ev_len ? ev_len : pkts->len, ev_stride, pout ? pout : (uint8_t *)out,
+                          pout != nullptr)))
+        return r;
     {
         EvSrc E{};
         E.recs = pout ? pout : (const uint8_t *)out;
@@ -2631,3 +3297,130 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
 }
 
 }  // extern "C"
+
+
+// ---- endpoint egress (from-container) ----
+namespace {
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp; };
+EgWs &eg_ws() { static EgWs w; return w; }
+}  // namespace
+
+extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t now_sec, gf_egress_out *out,
+                                      uint8_t *snap_out, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    if (!b) return -EFAULT;
+    const gf_frames &fr = b->frames;
+    if (fr.n == 0) return 0;
+    if (!fr.snap || !fr.len || !out) return -EFAULT;
+    if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
+    if (fr.n > (1u << 30)) return -E2BIG;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t n = fr.n, S = fr.snap_stride;
+    int r;
+    std::vector<std::shared_ptr<ProgLxc>> progs;
+    if ((r = prog_table(a, s, progs))) return r;
+    std::shared_ptr<Map> ct4m;
+    for (auto &p : progs) {
+        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
+    }
+    uint32_t strict = 0;
+    gf_htab_desc cfg_ct4{}, unused6{};
+    if ((r = ct_limits(ct4m, nullptr, n, 3, s, strict, cfg_ct4, unused6))) return r;
+    auto lxc = node_map(1), tun = node_map(2);
+    if ((r = push_map(lxc, s)) || (r = push_map(tun, s))) return r;
+    EgWs &ew = eg_ws();
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
+        (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 4)) || (r = grow(ew.ctlog_n, 4)) ||
+        (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = ws_grow(n)))
+        return r;
+    uint8_t *wsnap = snap_out;
+    if (!wsnap) {
+        if ((r = grow(ew.snap, (size_t)n * S))) return r;
+        wsnap = (uint8_t *)ew.snap.p;
+    }
+    const gf_node_cfg &node = node_cfg();
+    EgDev E{};
+    E.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
+    E.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
+    E.ct4 = cfg_ct4;
+    if (lxc) E.lxc = lxc->hdesc();
+    if (tun) E.tunnel = tun->hdesc();
+    E.snap = wsnap; E.stride = S; E.now = now_sec; E.host_ifindex = host_ifindex();
+    E.encap_ifindex = node.encap_ifindex;
+    E.cluster_range = node.ipv4_cluster_range; E.cluster_mask = node.ipv4_cluster_mask;
+    E.loopback = node.ipv4_loopback; E.ipv4_mask = node.ipv4_mask;
+    memcpy(E.host_mac, node.host_mac, 6);
+    E.strict = strict;
+    E.seq = (uint32_t *)ew.seq.p;
+    E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
+    E.X.snap = wsnap; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;
+    memcpy(E.X.host6, node.host_ip6, 16);
+    if ((r = px_log_begin(n, s, E.X))) return r;
+    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 4, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 4, s), "eg ctlog"))
+        return -EIO;
+    unsigned long long *sink = (unsigned long long *)stats_sink();
+    Workspace &w = ws();
+    {
+        ProfScope ps("k_eg_front", s);
+        hipLaunchKernelGGL(k_eg_front, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash, E,
+                           (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
+        hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p, n,
+                           (uint32_t *)w.keys.p);
+        if ((r = hip_ok(hipGetLastError(), "k_eg_front"))) return r;
+    }
+    if ((r = schedule_groups(n, s))) return r;
+    {
+        uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
+        if (grid > need) grid = need;
+        ProfScope ps("k_eg_groups", s);
+        hipLaunchKernelGGL(k_eg_groups, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p, (const uint2 *)w.order.p,
+                           (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out, (gf_rec *)ew.rec2.p,
+                           (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, sink);
+        if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
+    }
+    // ct_create4's deferred service entries, in batch order
+    uint32_t nlog = 0;
+    if (hip_ok(hipMemcpyAsync(&nlog, ew.ctlog_n.p, 4, hipMemcpyDeviceToHost, s), "ctlog count") ||
+        hip_ok(hipStreamSynchronize(s), "ctlog sync"))
+        return -EIO;
+    if (nlog && ct4m) {
+        if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
+            (r = grow(ew.cval, (size_t)nlog * 4)) || (r = grow(ew.cperm, (size_t)nlog * 4)))
+            return r;
+        size_t tb = 0;
+        (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
+                                        (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s);
+        if ((r = grow(ew.ctmp, tb + 256))) return r;
+        ProfScope ps("k_ctlog_apply", s);
+        const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
+        hipLaunchKernelGGL(k_ctlog_keys, dim3(gl), dim3(BLOCK), 0, s, (const uint32_t *)ew.ctlog.p,
+                           (const uint32_t *)ew.ctlog_n.p, (unsigned long long *)ew.ckey.p, (uint32_t *)ew.cval.p, nlog);
+        tb = ew.ctmp.bytes;
+        if (hip_ok(rocprim::radix_sort_pairs(ew.ctmp.p, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
+                                             (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s), "ctlog sort"))
+            return -EIO;
+        hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, (const uint32_t *)ew.ctlog.p,
+                           (const uint32_t *)ew.ctlog_n.p, (const unsigned long long *)ew.ckey2.p,
+                           (const uint32_t *)ew.cperm.p, cfg_ct4, (uint32_t *)ct4m->d_count.p);
+        if ((r = hip_ok(hipGetLastError(), "k_ctlog_apply"))) return r;
+    }
+    if (ct4m) ct4m->device_modified();
+    // the egress redirects' cilium_proxy4 updates, in batch order
+    if ((r = px_log_apply(E.X, s, wsnap, fr.len, S, (uint8_t *)out, true))) return r;
+    // handle_policy of the local deliveries (the tail calls of ipv4_local_delivery)
+    gf_pkt_cols c2{};
+    c2.n = n;
+    c2.len = fr.len;
+    c2.flow_hash = b->flow_hash;
+    auto pack = [&](const uint16_t *, gf_rec *rec, uint32_t *keys) -> int {
+        if (hip_ok(hipMemcpyAsync(rec, ew.rec2.p, (size_t)n * sizeof(gf_rec), hipMemcpyDeviceToDevice, s), "rec2") ||
+            hip_ok(hipMemcpyAsync(keys, ew.key2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))
+            return -EIO;
+        return 0;
+    };
+    return ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap);
+}

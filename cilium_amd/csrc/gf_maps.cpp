@@ -512,8 +512,8 @@ struct Registry {
     int next = 3;      // like fds: 0/1/2 are never handed out
     uint32_t host_ifindex = 1;
     uint64_t *stats = nullptr;
-    gf_node_cfg node{1, 0, 0, 0, {0}, {0}, {0}};
-    std::shared_ptr<Map> px4, px6;
+    gf_node_cfg node{};
+    std::shared_ptr<Map> px4, px6, lxc, tunnel;
 };
 static Registry &reg() { static Registry r; return r; }
 
@@ -536,6 +536,7 @@ int new_handle(std::shared_ptr<Obj> o) {
 uint32_t host_ifindex() { return reg().host_ifindex; }
 const gf_node_cfg &node_cfg() { return reg().node; }
 std::shared_ptr<Map> proxy_map(int fam) { return fam == 6 ? reg().px6 : reg().px4; }
+std::shared_ptr<Map> node_map(int which) { return which == 1 ? reg().lxc : reg().tunnel; }
 uint64_t *stats_sink() { return reg().stats; }
 
 }  // namespace gf
@@ -681,11 +682,23 @@ int gf_node_config(const gf_node_cfg *cfg) {
         if (!m6) return -EBADF;
         if (m6->ksz != 22 || m6->vsz != 28 || m6->is_lpm()) return -EINVAL;
     }
+    std::shared_ptr<Map> lxc, tun;
+    if (cfg->lxc_map) {
+        lxc = get_map(cfg->lxc_map);
+        if (!lxc) return -EBADF;
+        if (lxc->ksz != 20 || lxc->vsz != 112 || lxc->is_lpm()) return -EINVAL;
+    }
+    if (cfg->tunnel_map) {
+        tun = get_map(cfg->tunnel_map);
+        if (!tun) return -EBADF;
+        if (tun->ksz != 20 || tun->vsz != 20 || tun->is_lpm()) return -EINVAL;
+    }
     // the datapath inserts into the proxy maps: fixed slot arrays (1/2 load at max_entries)
     for (auto &m : {m4, m6}) if (m) m->make_fixed_capacity(2);
     reg().host_ifindex = cfg->host_ifindex;
     reg().node = *cfg;
     reg().px4 = m4; reg().px6 = m6;
+    reg().lxc = lxc; reg().tunnel = tun;
     return 0;
 }
 

@@ -16,7 +16,7 @@ import numpy as np
 
 from . import bpf
 from ._lib import (lib, gf_frames, gf_pkt_cols, gf_pkt_cols_out, gf_xdp_cfg, gf_lb_cfg, gf_lxc_cfg,
-                   gf_node_cfg, gf_netdev_cfg, gf_pipeline_cfg, gf_pipe_batch)
+                   gf_node_cfg, gf_netdev_cfg, gf_pipeline_cfg, gf_pipe_batch, gf_lxc_batch)
 
 LB_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("slave", "<u2"), ("new_dport", "<u2"),
                    ("rev_nat", "<u2"), ("new_daddr4", "<u4")])
@@ -25,6 +25,30 @@ ING_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flag
 PIPE_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
                      ("pad0", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
                      ("rev_nat", "<u2"), ("dport", "<u2"), ("daddr4", "<u4"), ("lxc_id", "<u2"), ("pad1", "<u2")])
+EG_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
+                   ("eg_ct_ret", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
+                   ("rev_nat", "<u2"), ("eg_flags", "<u2"), ("tunnel_ip", "<u4"), ("lxc_id", "<u2"), ("pad", "<u2")])
+
+
+def _be16(x):
+    return ((x & 0xff) << 8) | (x >> 8)
+
+
+def egress_fields(c, e, h):
+    """The from-container section of an endpoint's gf_lxc_cfg (pkg/endpoint/bpf.go:156-330
+    emits these as LXC_MAC, NODE_MAC, LXC_IPV4, LXC_PORT_MAPPINGS, CFG_L3L4_EGRESS)."""
+    c.lxc_mac[:] = list(e.get("lxc_mac", bytes(6)))
+    c.node_mac[:] = list(e.get("node_mac", bytes(6)))
+    c.lxc_ipv4 = e.get("lxc_ipv4", 0)
+    c.lb4_services, c.ipcache_map, c.cidr4_egress_map = h(e.get("lb4")), h(e.get("ipcache")), h(e.get("cidr4e"))
+    pm = e.get("portmap") or []
+    c.n_portmap = len(pm)
+    for i, (frm, to) in enumerate(pm):
+        c.portmap[2 * i], c.portmap[2 * i + 1] = _be16(frm), _be16(to)
+    l4 = e.get("l4e") or []
+    c.n_l4_egress = len(l4)
+    for i, (port, proxy, nh) in enumerate(l4):
+        c.l4_egress[i].port, c.l4_egress[i].proxy, c.l4_egress[i].nexthdr = _be16(port), _be16(proxy), nh
 
 
 def _torch():
@@ -132,7 +156,9 @@ class Datapath:
         nd = sc.node or {}
         ncfg = gf_node_cfg(sc.host_ifindex, h(nd.get("proxy4")), h(nd.get("proxy6")), nd.get("ipv4_gateway", 0),
                            (C.c_uint8 * 16)(*nd.get("host_ip6", bytes(16))), (C.c_uint8 * 6)(*nd.get("host_mac", bytes(6))),
-                           (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))))
+                           (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))), h(nd.get("lxc_map")),
+                           nd.get("ipv4_cluster_range", 0), nd.get("ipv4_cluster_mask", 0), nd.get("ipv4_loopback", 0),
+                           nd.get("ipv4_mask", 0), nd.get("encap_ifindex", 0), h(nd.get("tunnel_map")))
         _check(lib.gf_node_config(C.byref(ncfg)), "gf_node_config")
         self.xdp_prog = self.lb_prog = self.policy_array = None
         if sc.xdp:
@@ -159,6 +185,7 @@ class Datapath:
                     cfg.l4_ingress[i].port = ((port & 0xff) << 8) | (port >> 8)
                     cfg.l4_ingress[i].proxy = ((proxy & 0xff) << 8) | (proxy >> 8)
                     cfg.l4_ingress[i].nexthdr = nh
+                egress_fields(cfg, e, h)
                 p = _check(lib.gf_lxc_prog_load(C.byref(cfg)), "gf_lxc_prog_load")
                 self.lxc_progs.append(p)
                 _check(lib.gf_policy_array_update(self.policy_array, e["lxc_id"], p), "gf_policy_array_update")
@@ -209,6 +236,19 @@ class Datapath:
         _check(lib.gf_pipeline_classify(self.pipe, C.byref(pb), now, _ptr(out), _ptr(nd6), _ptr(snap), _stream()),
                "gf_pipeline_classify")
         return out, nd6, snap
+
+    def egress(self, b, now, out=None, snap_out=True):
+        """The from-container program over the batch's frames (+ handle_policy of the
+        local deliveries): returns (records [n,24] u8, rewritten snaps or None)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty((b.n, 24), dtype=torch.uint8, device=b.device)
+        snap = torch.empty_like(b.frames) if snap_out else None
+        stride = b.frames.shape[1] if b.n else 64
+        eb = gf_lxc_batch(gf_frames(b.n, stride, _ptr(b.frames), _ptr(b.len)), _ptr(b.lxc_id), _ptr(b.flow_hash))
+        _check(lib.gf_lxc_egress_classify(self.policy_array, C.byref(eb), now, _ptr(out), _ptr(snap), _stream()),
+               "gf_lxc_egress_classify")
+        return out, snap
 
     # ---- map readback ----------------------------------------------------
     def dump_map(self, name):

@@ -988,3 +988,163 @@ def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000
     sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0}
     sc.name = "config4_pipeline"
     return sc, P, vip
+
+
+# ------------------------------------------------------------------ endpoint egress (from-container)
+LXC_POLICY_EGRESS = 32
+
+
+def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=True):
+    """Frames sent by the local endpoints through their from-container program
+    (bpf_lxc.c handle_ingress -> handle_ipv4_from_lxc): services whose backends
+    are local endpoints (local delivery after lb4_local, loopback back to the
+    sender), remote peers behind the tunnel map, cluster and world peers, host
+    entries, source-MAC / gateway-MAC / source-IP violations, port maps,
+    POLICY_EGRESS endpoints with ipcache identities and egress CIDR maps,
+    pre-populated reply / related / loopback CT entries (egress rev-NAT), a
+    shared flow pool so that CT state builds up across the batches, and the
+    pipeline's TTL / checksum randomisation.  Local deliveries continue into
+    handle_policy of the destination endpoint.  hazard=False leaves out the
+    tuples that make a batch run as a single bucket (an endpoint sending to
+    itself, IPV4_LOOPBACK as a destination), so the parallel schedule and the
+    deferred service entries are exercised."""
+    sc = pipeline_fuzz(seed, n_packets=8, n_batches=1, proxy_max=proxy_max)
+    sc.name = f"egress{seed}"
+    sc.batches = []
+    rng = np.random.default_rng(seed ^ 0xE6E5)
+    n_ep = 16
+    ep4 = (ip4("10.1.0.1") + np.arange(n_ep)).astype(np.uint32)
+    lxc_id = (2000 + np.arange(n_ep)).astype(np.uint32)
+    vip4 = (ip4("10.96.0.1") + np.arange(8)).astype(np.uint32)
+    rem4 = np.concatenate([ip4("100.64.1.0") + rng.integers(0, 256, 12), ip4("10.128.0.0") + rng.integers(0, 1024, 12),
+                           ip4("10.200.0.0") + rng.integers(0, 256, 8)]).astype(np.uint32)
+    ports = np.array([80, 443, 53, 8080, 1000, 2000], np.uint32)
+    node_mac = bytes([0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde])
+    macs = rng.integers(0, 256, (n_ep, 6)).astype(np.uint8)
+    # ipcache (identities of remote peers), tunnel map (remote node prefixes), egress CIDR maps
+    ic_ip = np.concatenate([rem4[:6], rem4[12:16], ep4[:4]])
+    ic_id = np.concatenate([rng.integers(256, 280, 6), [2, 3, 2, 300], 256 + np.arange(4)]).astype(np.uint32)
+    icv = np.zeros((len(ic_ip), 8), np.uint8)
+    icv[:, 0:2] = le_bytes(ic_id, "<u2")
+    sc.add_map(MapSpec("cilium_ipcache", HASH, 20, 8, 512000, 0, *dedup(endpoint_keys4(ic_ip), icv)))
+    tk = endpoint_keys4(np.array([ip4("10.128.0.0"), ip4("10.200.0.0")], np.uint32))
+    tv = endpoint_keys4(np.array([ip4("192.168.7.2"), ip4("192.168.7.3")], np.uint32))
+    sc.add_map(MapSpec("cilium_tunnel_map", HASH, 20, 20, 65536, 0, tk, tv))
+    # egress policy entries (key.egress = 1) in every endpoint's policy map
+    ids = np.concatenate([[1, 2, 3, 4], 256 + np.arange(24)]).astype(np.uint32)
+    for e in range(n_ep):
+        m = sc.maps[f"pol{e}"]
+        nl3, nl4, nwc = 6, 10, 3
+        l3 = ids[rng.integers(0, len(ids), nl3)]
+        l4i = ids[rng.integers(0, len(ids), nl4)]
+        l4p = ports[rng.integers(0, len(ports), nl4)]
+        l4x = rng.choice([TCP, UDP], nl4)
+        proxy = np.where(rng.random(nl4) < 0.3, rng.integers(1, 65536, nl4), 0)
+        kk = np.concatenate([m.keys, policy_keys(l4i, l4p, l4x, 1), policy_keys(l3, np.zeros(nl3), np.zeros(nl3), 1),
+                             policy_keys(np.zeros(nwc), ports[rng.integers(0, len(ports), nwc)],
+                                         rng.choice([TCP, UDP], nwc), 1)])
+        vv = np.concatenate([m.vals, policy_vals(proxy), policy_vals(np.zeros(nl3)), policy_vals(np.zeros(nwc))])
+        m.keys, m.vals = dedup(kk, vv)
+        if e % 2 == 0:
+            cp = np.array([16, 24, 32], np.uint32)
+            cn = np.array([ip4("100.64.0.0"), rem4[12] & 0xFFFFFF00, rem4[20]], np.uint32)
+            ck, cv = lpm_dedup(lpm4_keys(cp[: 1 + e % 3], cn[: 1 + e % 3]), np.ones((1 + e % 3, 1), np.uint8), 32)
+            sc.add_map(MapSpec(f"cidr4e_{e}", LPM, 8, 1, 1024, NO_PREALLOC, ck, cv))
+    for e, cfg in enumerate(sc.lxc):
+        cfg["lxc_mac"] = bytes(macs[e])
+        cfg["node_mac"] = node_mac if e != 7 else bytes(6)
+        cfg["lxc_ipv4"] = int(be32_bytes([ep4[e]]).view("<u4")[0, 0])
+        cfg["lb4"] = "lb4_svc" if e != 9 else None
+        cfg["ipcache"] = "cilium_ipcache"
+        if e % 4 in (1, 2):
+            cfg["flags"] |= LXC_POLICY_EGRESS
+            cfg["cidr4e"] = f"cidr4e_{e}" if e % 2 == 0 else None
+        if e % 5 == 2:
+            cfg["portmap"] = [(30000 + e, 80), (30100 + e, 53)] + ([(30200, 80)] if e == 2 else [])
+        if e % 3 == 1:
+            cfg["l4e"] = [(80, 17000 + e, TCP), (53, 0, UDP), (443, 18000, TCP)]
+    raw_be = lambda a: int(be32_bytes([a]).view("<u4")[0, 0])
+    sc.node = dict(sc.node, lxc_map="cilium_lxc", ipv4_cluster_range=raw_be(ip4("10.0.0.0")),
+                   ipv4_cluster_mask=raw_be(0xFF000000), ipv4_loopback=raw_be(ip4("10.255.255.245")),
+                   ipv4_mask=raw_be(0xFFFF0000), encap_ifindex=5, tunnel_map="cilium_tunnel_map")
+    # CT entries the egress path meets as replies / related (rev-NAT, loopback) and as established flows
+    ct = sc.maps["ct4"]
+    npre = 48
+    E = ep4[rng.integers(0, n_ep, npre)]
+    R = np.where(rng.random(npre) < 0.5, rem4[rng.integers(0, len(rem4), npre)], ep4[rng.integers(0, n_ep, npre)])
+    if not hazard:
+        R = np.where(R == E, rem4[0], R)
+    a, b = ports[rng.integers(0, len(ports), npre)], ports[rng.integers(0, len(ports), npre)]
+    pr = rng.choice(np.array([TCP, TCP, UDP, ICMP], np.uint8), npre)
+    rk = ct4_keys(R, E, raw16(a), raw16(b), pr, np.ones(npre))                 # egress REPLY probe key
+    relk = ct4_keys(R, E, np.zeros(npre), np.zeros(npre), np.full(npre, ICMP), np.full(npre, 3))
+    estk = ct4_keys(E, R, raw16(b), raw16(a), pr, np.zeros(npre))             # egress forward key
+    fl = rng.choice(np.array([0, 16, 1, 2, 3, 8, 24, 19], np.uint16), npre)
+    rn = np.where(rng.random(npre) < 0.6, raw16(rng.integers(1, 11, npre)), 0).astype(np.uint16)
+    rv = ct_vals(npre, 4000, 0, 0, 300, rx=(2, 200))
+    rv[:, 36:38] = le_bytes(fl, "<u2")
+    rv[:, 38:40] = le_bytes(rn, "<u2")
+    k, v = dedup(np.concatenate([ct.keys, rk, relk, estk]),
+                 np.concatenate([ct.vals, rv, rv, ct_vals(npre, 4000, 16, 0, 256 + np.arange(npre) % 4)]))
+    ct.keys, ct.vals = k, v
+    pool = dict(e=rng.integers(0, n_ep, npre), d=R, sp=a, dp=b, pr=pr)
+    pool["e"] = np.searchsorted(ep4, E)
+    # ---- packets
+    for bi in range(n_batches):
+        n = n_packets
+        kind = rng.random(n)
+        e = rng.integers(0, n_ep, n)
+        peer = rng.integers(0, n_ep, n) if hazard else (e + 1 + rng.integers(0, n_ep - 1, n)) % n_ep
+        lo = np.uint32(ip4("10.255.255.245")) if hazard else rem4[3]
+        d = np.where(kind < 0.30, vip4[rng.integers(0, 8, n)],
+                     np.where(kind < 0.55, ep4[peer],
+                              np.where(kind < 0.85, rem4[rng.integers(0, len(rem4), n)],
+                                       np.where(kind < 0.90, lo,
+                                                rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)))))
+        pr = rng.choice(np.array([TCP, TCP, TCP, UDP, UDP, ICMP, ICMP, 47], np.uint8), n)
+        sp = np.where(rng.random(n) < 0.3, 30000 + rng.integers(0, 20, n), ports[rng.integers(0, len(ports), n)])
+        dp = ports[rng.integers(0, len(ports), n)]
+        use = rng.random(n) < 0.35                     # the pre-populated flows, both directions
+        pi = rng.integers(0, npre, n)
+        e = np.where(use, pool["e"][pi], e)
+        d = np.where(use, pool["d"][pi], d)
+        pr = np.where(use, pool["pr"][pi], pr).astype(np.uint8)
+        sp = np.where(use, pool["sp"][pi], sp)
+        dp = np.where(use, pool["dp"][pi], dp)
+        s = ep4[e].copy()
+        bad_sip = rng.random(n) < 0.02
+        s[bad_sip] = rem4[rng.integers(0, len(rem4), int(bad_sip.sum()))]
+        tf = rng.choice(np.array([F_SYN, F_ACK, F_ACK, F_FIN | F_ACK, F_RST, F_SYN | F_ACK], np.uint8), n)
+        it = rng.choice(np.array([0, 3, 8, 8, 11, 12, 5], np.uint8), n)
+        ihl = np.where(rng.random(n) < 0.05, rng.integers(0, 16, n), 5)
+        f, lens = frames_v4(n, 256, s, d, pr, sp, dp, tf, it, 0, ihl, payload=rng.integers(0, 64, n))
+        f[:, 6:12] = macs[e]
+        f[rng.random(n) < 0.02, 6] ^= 1
+        f[:, 0:6] = np.frombuffer(node_mac, np.uint8)
+        f[rng.random(n) < 0.02, 0] ^= 1
+        ttl = np.where(rng.random(n) < 0.05, rng.integers(0, 2, n), rng.integers(2, 256, n)).astype(np.uint8)
+        f[:, 22] = ttl
+        f[:, 24:26] = rng.integers(0, 256, (n, 2))
+        l4 = 14 + (f[:, 14] & 0xf).astype(np.int64) * 4
+        off = np.where(pr == 6, l4 + 16, np.where(pr == 17, l4 + 6, -1))
+        ck = rng.integers(0, 65536, n)
+        ck[rng.random(n) < 0.1] = 0
+        ok = (off >= 0) & (off + 1 < f.shape[1])
+        rows = np.nonzero(ok)[0]
+        f[rows, off[ok]] = (ck[ok] >> 8).astype(np.uint8)
+        f[rows, off[ok] + 1] = (ck[ok] & 0xff).astype(np.uint8)
+        oth = rng.random(n)
+        i6 = np.nonzero(oth < 0.02)[0]
+        f[i6, 12], f[i6, 13] = 0x86, 0xdd
+        ia = np.nonzero((oth >= 0.02) & (oth < 0.04))[0]
+        f[ia, 12], f[ia, 13] = 0x08, 0x06
+        io = np.nonzero((oth >= 0.04) & (oth < 0.05))[0]
+        f[io, 12], f[io, 13] = 0x88, 0xcc
+        lens = lens.astype(np.int64)
+        tr = rng.random(n) < 0.06
+        lens[tr] = rng.integers(0, np.maximum(lens[tr], 1) + 1)
+        lens = np.minimum(lens, 256 + 400).astype(np.uint32)
+        lid = np.where(rng.random(n) < 0.98, lxc_id[e], 4242).astype(np.uint16)
+        fh = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        sc.batches.append(Packets(f, lens, None, None, lid, None, fh))
+    return sc

@@ -228,7 +228,13 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out,
 #define GF_LXC_F_HAVE_L4_POLICY  (1u << 2)  /* HAVE_L4_POLICY */
 #define GF_LXC_F_CT_ACCOUNTING   (1u << 3)  /* CONNTRACK_ACCOUNTING */
 #define GF_LXC_F_LXC_IPV4        (1u << 4)  /* LXC_IPV4 */
+#define GF_LXC_F_POLICY_EGRESS   (1u << 5)  /* POLICY_EGRESS (the agent does not emit it; lxc_config.h does) */
 #define GF_MAX_L4_INGRESS 64
+#define GF_MAX_PORTMAP 16
+typedef struct gf_portmap {    /* struct portmap (bpf/lib/common.h), LXC_PORT_MAPPINGS entries */
+    uint16_t from;             /* raw be16 */
+    uint16_t to;               /* raw be16 */
+} gf_portmap;
 typedef struct gf_l4_allow {   /* struct l4_allow, bpf/lib/l4.h:126-136 */
     uint16_t port;             /* raw be16 */
     uint16_t proxy;            /* raw be16 */
@@ -248,6 +254,17 @@ typedef struct gf_lxc_cfg {
     uint32_t flags;            /* GF_LXC_F_* */
     uint32_t n_l4_ingress;     /* CFG_L3L4_INGRESS entries */
     gf_l4_allow l4_ingress[GF_MAX_L4_INGRESS];
+    /* ---- the from-container section of the same object (bpf_lxc.c:427-738) ---- */
+    uint8_t  lxc_mac[6];       /* LXC_MAC (is_valid_lxc_src_mac) */
+    uint8_t  node_mac[6];      /* NODE_MAC (is_valid_gw_dst_mac, router MAC of ipv4_l3) */
+    uint32_t lxc_ipv4;         /* LXC_IPV4 value (raw be32, is_valid_lxc_src_ipv4) */
+    int lb4_services;          /* cilium_lb4_services (LB_L3 + LB_L4: lb4_lookup_service / lb4_local), 0 = none */
+    int ipcache_map;           /* cilium_ipcache (endpoint_key 20 B -> remote_endpoint_info 8 B), POLICY_EGRESS */
+    int cidr4_egress_map;      /* CIDR4_EGRESS_MAP (LPM_TRIE), 0 = undefined (deny) */
+    uint32_t n_portmap;        /* LXC_PORT_MAPPINGS entries (map_lxc_out) */
+    gf_portmap portmap[GF_MAX_PORTMAP];
+    uint32_t n_l4_egress;      /* CFG_L3L4_EGRESS entries (l4_egress_proxy_lookup) */
+    gf_l4_allow l4_egress[GF_MAX_L4_INGRESS];
 } gf_lxc_cfg;
 int gf_lxc_prog_load(const gf_lxc_cfg *cfg);
 
@@ -263,6 +280,14 @@ typedef struct gf_node_cfg {   /* node_config.h values used on the path */
     uint8_t  host_ip6[16];     /* HOST_IP, the IPv6 proxy redirect's new daddr */
     uint8_t  host_mac[6];      /* HOST_IFINDEX_MAC */
     uint8_t  node_mac[6];      /* NODE_MAC */
+    /* the from-container path (bpf_lxc.c:427-658) */
+    int      lxc_map;          /* cilium_lxc (lookup_ip4_endpoint of the egress path), 0 = none */
+    uint32_t ipv4_cluster_range; /* IPV4_CLUSTER_RANGE (raw be32) */
+    uint32_t ipv4_cluster_mask;  /* IPV4_CLUSTER_MASK (raw be32) */
+    uint32_t ipv4_loopback;    /* IPV4_LOOPBACK (raw be32), lb4_local's loopback SNAT source */
+    uint32_t ipv4_mask;        /* IPV4_MASK (raw be32), the tunnel map key of encap_and_redirect */
+    uint32_t encap_ifindex;    /* ENCAP_IFINDEX, 0 = undefined (no tunnel) */
+    int      tunnel_map;       /* cilium_tunnel_map (endpoint_key 20 B -> endpoint_key 20 B) */
 } gf_node_cfg;
 int gf_node_config(const gf_node_cfg *cfg);
 
@@ -284,6 +309,57 @@ typedef struct gf_ingress_out {
  * replaces bpf_ktime_get_sec() for the whole batch. */
 int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
                                uint32_t now_sec, gf_ingress_out *out, void *stream);
+
+/* ---- endpoint egress: the from-container program (bpf/bpf_lxc.c:685-738
+ * handle_ingress -> tail_handle_ipv4 -> handle_ipv4_from_lxc :427-658) ----
+ * Frames sent by local endpoints; packet i runs the program of endpoint
+ * lxc_id[i] (its bpf_lxc object = the cilium_policy slot's program).  Local
+ * deliveries (ipv4_local_delivery, bpf/lib/l3.h:136-168) continue into the
+ * destination's handle_policy (tail call into cilium_policy) in a second pass
+ * over the batch, as gf_pipeline_classify does: every from-container effect
+ * of the batch (CT, proxy map) precedes every handle_policy effect of its
+ * deliveries.  IPv6 and ARP frames (the ICMPv6/ARP responders)
+ * are reported as stage GF_STAGE_NONE, not classified. */
+typedef struct gf_lxc_batch {
+    gf_frames frames;          /* DEVICE frames (snap_stride >= every header byte touched, <= 256) */
+    const uint16_t *lxc_id;    /* DEVICE: the sending endpoint (whose from-container program runs) */
+    const uint32_t *flow_hash; /* DEVICE get_hash_recalc(skb) (lb4_select_slave), may be NULL */
+} gf_lxc_batch;
+#define GF_STAGE_NONE     0    /* not classified: IPv6 / ARP from a container (responders) */
+#define GF_STAGE_FROM_LXC 5    /* the from-container verdict is final */
+/* GF_STAGE_POLICY (4): delivered locally, handle_policy of endpoint lxc_id */
+#define GF_EG_F_CREATED   0x0001  /* ct_create4(CT_EGRESS) */
+#define GF_EG_F_PROXY     0x0002  /* ipv4_redirect_to_host_port */
+#define GF_EG_F_LB        0x0004  /* lb4_local translated the destination */
+#define GF_EG_F_LOOPBACK  0x0008  /* ... back to the sender: source SNAT to IPV4_LOOPBACK */
+#define GF_EG_F_REVNAT    0x0010  /* lb4_rev_nat of a reply */
+#define GF_EG_F_PORTMAP   0x0020  /* map_lxc_out rewrote the source port */
+#define GF_EG_F_ENCAP     0x0040  /* encap_and_redirect: tunnel_ip holds the remote node */
+#define GF_EG_F_TO_HOST   0x0080  /* to_host: redirect(HOST_IFINDEX) */
+#define GF_EG_F_TO_STACK  0x0100  /* pass_to_stack: TC_ACT_OK */
+#define GF_EG_F_LOCAL     0x0200  /* ipv4_local_delivery (stage GF_STAGE_POLICY) */
+#define GF_EG_F_DELETED   0x0400  /* ct_delete4 of an ESTABLISHED flow the policy now denies */
+#define GF_EG_F_ARP       0x0800  /* stage NONE: ARP (tail_handle_arp, the responder) */
+#define GF_EG_F_IPV6      0x1000  /* stage NONE: IPv6 (tail_handle_ipv6) */
+typedef struct gf_egress_out {   /* 24 B; bytes 0-9 as gf_pipeline_out */
+    uint8_t  stage;       /* GF_STAGE_FROM_LXC / GF_STAGE_POLICY / GF_STAGE_NONE */
+    uint8_t  action;      /* final TC_ACT_* */
+    uint8_t  reason;      /* drop reason when SHOT */
+    uint8_t  ct_ret;      /* stage FROM_LXC: the egress ct_lookup4 result; POLICY: handle_policy's */
+    uint8_t  flags;       /* stage POLICY: gf_ingress_out.flags */
+    uint8_t  eg_ct_ret;   /* egress ct_lookup4 result (forwarding_reason) */
+    uint16_t proxy_port;  /* raw be16 proxy port of the final redirect */
+    uint16_t ifindex_lo;  /* redirect target (HOST_IFINDEX, ENCAP_IFINDEX, or handle_policy's) */
+    uint16_t slave;       /* lb4_local: selected slave */
+    uint16_t rev_nat;     /* lb4_local: rev_nat_index (raw) */
+    uint16_t eg_flags;    /* GF_EG_F_* */
+    uint32_t tunnel_ip;   /* ENCAP: bpf_tunnel_key.remote_ipv4 */
+    uint16_t lxc_id;      /* stage POLICY: destination endpoint */
+    uint16_t pad;
+} gf_egress_out;
+/* snap_out (n * snap_stride, may be NULL): the frames as the programs left them. */
+int gf_lxc_egress_classify(int policy_array, const gf_lxc_batch *batch, uint32_t now_sec,
+                           gf_egress_out *out, uint8_t *snap_out, void *stream);
 
 /* ---- full pipeline (BASELINE config 4) ----
  * One frame through the programs a node attaches in order, each seeing the

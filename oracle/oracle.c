@@ -827,8 +827,9 @@ static int ct_lookup(om_map *map, uint8_t *t, const skb_t *s, int off, int dir,
     return __ct_lookup(map, s, t, action, dir, st, syn, now, accounting);
 }
 
-/* ct_create4 (conntrack.h:503-580) / ct_create6 (:446-493), ingress use
- * (ct_state->addr == 0, so the loopback branch is not taken). */
+/* ct_create4 (conntrack.h:503-580) / ct_create6 (:446-493).  The second
+ * (service / loopback) entry exists only on the v4 egress path, where
+ * lb4_local sets ct_state->addr. */
 static int ct_create(om_map *map, uint8_t *t, const skb_t *s, int dir, const ct_state_t *st,
                      int v6, uint32_t now) {
     uint8_t e[48]; memset(e, 0, sizeof e);
@@ -840,6 +841,17 @@ static int ct_create(om_map *map, uint8_t *t, const skb_t *s, int dir, const ct_
     else { se64(e, CTE_TX_PKTS, 1); se64(e, CTE_TX_BYTES, s->len); }
     se32(e, CTE_SRCSEC, st->src_sec_id);
     if (om_update(map, t, e, 0) < 0) return DROP_CT_CREATE_FAILED;
+    if (!v6 && st->addr) {                              /* conntrack.h:533-561 (lb4_local set ct_state->addr) */
+        uint8_t sv[14]; memcpy(sv, t, 14);
+        if (dir == CT_INGRESS) se32(t, 4, st->addr); else se32(t, 0, st->addr);
+        if (st->loopback) {
+            t[13] = TUPLE_F_IN;
+            if (dir == CT_INGRESS) se32(t, 0, st->svc_addr); else se32(t, 4, st->svc_addr);
+        }
+        int r = om_update(map, t, e, 0);
+        memcpy(t, sv, 14);
+        if (r < 0) return DROP_CT_CREATE_FAILED;
+    }
     uint8_t it[40]; memset(it, 0, sizeof it);
     if (v6) { memcpy(it, t, 32); it[36] = IPPROTO_ICMPV6; }
     else { memcpy(it, t, 8); it[12] = IPPROTO_ICMP; }
@@ -880,12 +892,27 @@ static void policy_count(uint8_t *p, uint32_t len) {            /* __sync_fetch_
     __atomic_fetch_add((uint64_t *)(p + 16), (uint64_t)len, __ATOMIC_RELAXED);
 }
 
-/* __policy_can_access, policy.h:42-113 (dir = CT_INGRESS) */
-static int __policy_can_access(const o_lxc_cfg *c, const skb_t *s, uint32_t identity,
-                               uint16_t dport, uint8_t proto) {
+/* l4_egress_proxy_lookup via BPF_L4_MAP (bpf/lib/l4.h:178-188, CFG_L3L4_EGRESS) */
+static int l4_egress_proxy_lookup(const o_lxc_cfg *c, uint16_t dport, uint8_t nexthdr) {
+    if (!c->n_l4_egress) return 0;
+    int allowed = DROP_POLICY_L4;
+    for (uint32_t i = 0; i < c->n_l4_egress; i++) {
+        const o_l4_allow *a = &c->l4_egress[i];
+        allowed = allowed > -1 ? allowed
+                : ((a->port && a->port == dport) ? ((a->nexthdr && a->nexthdr == nexthdr) ? (int)a->proxy
+                                                                                     : DROP_POLICY_L4)
+                                                  : DROP_POLICY_L4);
+    }
+    return allowed > 0 ? allowed : 0;
+}
+
+/* __policy_can_access, policy.h:42-113; dir CT_INGRESS (key.egress = 0) or
+ * CT_EGRESS (key.egress = 1, l4_proxy_lookup's egress list, l4.h:192-217) */
+static int __policy_can_access_dir(const o_lxc_cfg *c, const skb_t *s, uint32_t identity,
+                                   uint16_t dport, uint8_t proto, int dir) {
     if (c->flags & LXC_F_DROP_ALL) return DROP_POLICY;
     uint8_t key[8];
-    se32(key, 0, identity); se16(key, 4, dport); key[6] = proto; key[7] = 0;   /* egress = !dir = 0 */
+    se32(key, 0, identity); se16(key, 4, dport); key[6] = proto; key[7] = (uint8_t)!dir;   /* egress = !dir */
     uint8_t *p;
     if (c->flags & LXC_F_HAVE_L4_POLICY) {
         p = om_lookup_ptr(c->policy_map, key);
@@ -904,8 +931,14 @@ static int __policy_can_access(const o_lxc_cfg *c, const skb_t *s, uint32_t iden
 get_proxy_port: {
         uint16_t pp = ge16(p, 0);
         if (pp) return pp;
-        return l4_proxy_lookup(c, proto, dport);
+        if (dir == CT_INGRESS) return l4_proxy_lookup(c, proto, dport);
+        if (proto == IPPROTO_UDP || proto == IPPROTO_TCP) return l4_egress_proxy_lookup(c, dport, proto);
+        return 0;
     }
+}
+static int __policy_can_access(const o_lxc_cfg *c, const skb_t *s, uint32_t identity,
+                               uint16_t dport, uint8_t proto) {
+    return __policy_can_access_dir(c, s, identity, dport, proto, CT_INGRESS);
 }
 
 /* policy_can_access_ingress, policy.h:133-168 */
@@ -1005,7 +1038,7 @@ static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t next
     return 0;                                          /* cilium_proxy{4,6} update: §8(f) */
 }
 
-static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}};   /* bpf/node_config.h */
+static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0, 0, 0, 0, NULL};   /* bpf/node_config.h */
 #define g_host_ifindex (g_node.host_ifindex)
 void o_set_node(const o_node_cfg *node) { g_node = *node; }
 
@@ -1719,4 +1752,350 @@ void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_o
                           c->seclabel, c->lxc_id, b->ifindex ? b->ifindex[i] : 0, NULL, 0);
         else drop_event(e, out[i].reason, 0, hash, len, 0, 0, 0, 0, NULL, 0);   /* caller's send_drop_notify_error */
     }
+}
+
+/* ------------------------------------------------------------------ */
+/* Endpoint egress: the from-container program, bpf/bpf_lxc.c:427-738  */
+/* ------------------------------------------------------------------ */
+#define DROP_INVALID_SMAC -130
+#define DROP_INVALID_DMAC -131
+#define DROP_INVALID_SIP -132
+#define DROP_NO_LXC -152
+#define DROP_POLICY_CIDR -162
+#define CLUSTER_ID 3u
+#define EG_F_CREATED 0x0001
+#define EG_F_PROXY 0x0002
+#define EG_F_LB 0x0004
+#define EG_F_LOOPBACK 0x0008
+#define EG_F_REVNAT 0x0010
+#define EG_F_PORTMAP 0x0020
+#define EG_F_ENCAP 0x0040
+#define EG_F_TO_HOST 0x0080
+#define EG_F_TO_STACK 0x0100
+#define EG_F_LOCAL 0x0200
+#define EG_F_DELETED 0x0400
+#define EG_F_ARP 0x0800
+#define EG_F_IPV6 0x1000
+#define O_STAGE_POLICY 4
+#define O_STAGE_FROM_LXC 5
+#define LXC_F_POLICY_EGRESS (1u << 5)
+
+/* ipv4_l3 (bpf/lib/l3.h:54-70) with ipv4_dec_ttl (bpf/lib/ipv4.h:30-43) */
+static int ipv4_l3(const skb_t *s, uint8_t *w, const uint8_t *smac, const uint8_t *dmac) {
+    uint8_t ttl = skb_byte(s, 22);
+    if (ttl <= 1) return DROP_INVALID;
+    uint8_t nt = (uint8_t)(ttl - 1);
+    l3_csum_replace(s, w, ETH_HLEN + 10, ttl, nt, 2);
+    skb_store_bytes(s, w, ETH_HLEN + 8, &nt, 1);
+    if (smac && skb_store_bytes(s, w, 6, smac, 6) < 0) return DROP_WRITE_ERROR;     /* eth_store_saddr */
+    if (skb_store_bytes(s, w, 0, dmac, 6) < 0) return DROP_WRITE_ERROR;             /* eth_store_daddr */
+    return TC_ACT_OK;
+}
+
+/* policy_can_egress4 (bpf/lib/policy.h:241-264 with POLICY_EGRESS, else
+ * :282-289) + lookup_ip4_remote_endpoint (bpf/lib/eps.h:60-69) +
+ * lpm4_egress_lookup (bpf/lib/maps.h:218-270) */
+static int policy_can_egress4(const o_lxc_cfg *c, const skb_t *s, const uint8_t *t, uint16_t dst_id,
+                              uint32_t daddr) {
+    if (c->flags & LXC_F_DROP_ALL) return DROP_POLICY;
+    if (!(c->flags & LXC_F_POLICY_EGRESS)) return TC_ACT_OK;
+    uint16_t identity = dst_id;
+    if (c->ipcache_map) {
+        uint8_t k[20] = {0}; memcpy(k, &daddr, 4); k[16] = 1;
+        const uint8_t *info = om_lookup_ptr(c->ipcache_map, k);
+        if (info) identity = ge16(info, 0);
+    }
+    int verdict = __policy_can_access_dir(c, s, identity, ge16(t, 8), t[12], CT_EGRESS);
+    if (verdict < 0) verdict = DROP_POLICY;                         /* policy_can_egress */
+    if (identity < 256 && verdict < 0) {                             /* identity_is_reserved */
+        int hit = 0;
+        if (c->cidr4_egress_map) {
+            uint8_t k[8]; uint32_t pl = 32; memcpy(k, &pl, 4); memcpy(k + 4, &daddr, 4);
+            hit = om_lookup_ptr(c->cidr4_egress_map, k) != NULL;
+        }
+        verdict = hit ? 0 : DROP_POLICY_CIDR;
+    }
+    return verdict;
+}
+
+/* lb4_rev_nat / __lb4_rev_nat with flags 0 (bpf/lib/lb.h:447-534): the old
+ * source address is the frame's; a looped-back flow also restores daddr. */
+static int lb4_rev_nat_eg(const o_lxc_cfg *c, const skb_t *s, uint8_t *w, int l4_off, uint8_t *t,
+                          const ct_state_t *st) {
+    const uint8_t *nat = c->revnat4_map ? om_lookup_ptr(c->revnat4_map, &st->rev_nat_index) : NULL;
+    if (!nat) return 0;
+    uint8_t nh = t[12];
+    uint16_t co = csum_l4_offset(nh);
+    uint32_t fl = csum_l4_flags(nh);
+    uint16_t port = ge16(nat, 4);
+    if (port) {                                                   /* reverse_map_l4_port, lb.h:217-251 */
+        switch (nh) {
+        case IPPROTO_TCP: case IPPROTO_UDP: {
+            uint16_t old;
+            int ret = skb_load_bytes(s, l4_off, &old, 2);
+            if (IS_ERR(ret)) return ret;
+            if (port != old) {
+                if (l4_csum_replace(s, w, l4_off + co, old, port, 2 | fl) < 0) return DROP_CSUM_L4;
+                if (skb_store_bytes(s, w, l4_off, &port, 2) < 0) return DROP_WRITE_ERROR;
+            }
+            break;
+        }
+        case IPPROTO_ICMPV6: case IPPROTO_ICMP: break;
+        default: return DROP_UNKNOWN_L4;
+        }
+    }
+    uint32_t old_sip = rd32(s, 26), new_sip = ge32(nat, 0), sum = 0;
+    if (st->loopback) {
+        uint32_t old_dip = rd32(s, 30);
+        if (skb_store_bytes(s, w, 30, &old_sip, 4) < 0) return DROP_WRITE_ERROR;
+        sum = ck_diff((const uint8_t *)&old_dip, (const uint8_t *)&old_sip, 4);
+        se32(t, 4, old_sip);                                      /* tuple->saddr = old_sip */
+    }
+    if (skb_store_bytes(s, w, 26, &new_sip, 4) < 0) return DROP_WRITE_ERROR;
+    sum = ck_add(sum, ck_diff((const uint8_t *)&old_sip, (const uint8_t *)&new_sip, 4));
+    if (l3_csum_replace(s, w, ETH_HLEN + 10, 0, sum, 0) < 0) return DROP_CSUM_L3;
+    if (co && l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl) < 0) return DROP_CSUM_L4;
+    return 0;
+}
+
+typedef struct eg_res { uint32_t ifindex, tunnel_ip; uint16_t proxy, eg_flags, slave, rev_nat; uint8_t ct_ret; } eg_res;
+
+/* handle_ipv4_from_lxc, bpf/bpf_lxc.c:427-658.  w is the frame (s->data == w).
+ * Returns TC_ACT_OK / TC_ACT_REDIRECT / O_NETDEV_TAILCALL (ipv4_local_delivery's
+ * tail call into cilium_policy, nr filled) or an error. */
+static int from_lxc_ipv4(const o_lxc_cfg *c, skb_t *s, uint8_t *w, uint32_t now, eg_res *r, uint8_t *plog,
+                         nd_res *nr) {
+    if (s->len < ETH_HLEN + 20) return DROP_INVALID;                  /* revalidate_data */
+    uint8_t t[14]; memset(t, 0, sizeof t);
+    t[12] = skb_byte(s, 23);
+    for (int k = 0; k < 6; k++) if (skb_byte(s, 6 + k) != c->lxc_mac[k]) return DROP_INVALID_SMAC;
+    for (int k = 0; k < 6; k++) if (skb_byte(s, k) != c->node_mac[k]) return DROP_INVALID_DMAC;
+    uint32_t saddr = rd32(s, 26), daddr = rd32(s, 30);
+    if (!(c->flags & LXC_F_LXC_IPV4) || saddr != c->lxc_ipv4) return DROP_INVALID_SIP;
+    se32(t, 0, daddr); se32(t, 4, saddr);
+    int l4_off = ETH_HLEN + (skb_byte(s, 14) & 0xf) * 4;                /* ipv4_hdrlen */
+    const uint8_t nh = t[12];
+    const uint16_t co = csum_l4_offset(nh);
+    const uint32_t fl = csum_l4_flags(nh);
+    ct_state_t sn; memset(&sn, 0, sizeof sn);
+    uint8_t key[8] = {0}; memcpy(key, &daddr, 4);                      /* lb4_extract_key(CT_EGRESS) */
+    int ret = extract_l4_port(s, nh, l4_off, (uint16_t *)(key + 4));   /* LB_L4 */
+    if (IS_ERR(ret)) {
+        if (ret != DROP_UNKNOWN_L4) return ret;
+        goto skip_service_lookup;
+    }
+    sn.orig_dport = ge16(key, 4);
+    if (c->lb4_services) {
+        o_lb_cfg lc; memset(&lc, 0, sizeof lc);
+        lc.lb4_services = c->lb4_services; lc.flags = LB_F_L3 | LB_F_L4;
+        uint8_t *svc = lb4_lookup_service(&lc, key);
+        if (svc) {                                                      /* lb4_local, lb.h:662-699 */
+            uint16_t count = ge16(svc, 6);
+            uint16_t slave = (uint16_t)((s->hash % count) + 1);
+            se16(key, 6, slave);
+            const uint8_t *be = om_lookup_ptr(c->lb4_services, key);
+            if (!be) return DROP_NO_SERVICE;
+            r->slave = slave; r->eg_flags |= EG_F_LB;
+            sn.rev_nat_index = ge16(be, 8); r->rev_nat = sn.rev_nat_index;
+            uint32_t target = ge32(be, 0), new_saddr = 0;
+            sn.addr = target;
+            if (saddr == target) {                                       /* !DISABLE_LOOPBACK_LB */
+                new_saddr = g_node.ipv4_loopback;
+                sn.loopback = 1; sn.addr = new_saddr; sn.svc_addr = saddr;
+                r->eg_flags |= EG_F_LOOPBACK;
+            }
+            if (!sn.loopback) se32(t, 0, target);
+            /* lb4_xlate, lb.h:615-659 */
+            if (skb_store_bytes(s, w, 30, &target, 4) < 0) return DROP_WRITE_ERROR;
+            uint32_t sum = ck_diff(key, (const uint8_t *)&target, 4);
+            if (new_saddr) {
+                if (skb_store_bytes(s, w, 26, &new_saddr, 4) < 0) return DROP_WRITE_ERROR;
+                sum = ck_add(sum, ck_diff((const uint8_t *)&saddr, (const uint8_t *)&new_saddr, 4));
+            }
+            if (l3_csum_replace(s, w, ETH_HLEN + 10, 0, sum, 0) < 0) return DROP_CSUM_L3;
+            if (co && l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl) < 0) return DROP_CSUM_L4;
+            uint16_t sp = ge16(be, 4), kd = ge16(key, 4);
+            if (sp && kd != sp && (nh == IPPROTO_TCP || nh == IPPROTO_UDP)) {   /* l4_modify_port */
+                if (l4_csum_replace(s, w, l4_off + co, kd, sp, 2 | fl) < 0) return DROP_CSUM_L4;
+                if (skb_store_bytes(s, w, l4_off + 2, &sp, 2) < 0) return DROP_WRITE_ERROR;
+            }
+        }
+    }
+skip_service_lookup: ;
+    uint32_t orig_dip = ge32(t, 0);
+    /* map_lxc_out, bpf_lxc.c:80-108 + l4_port_map_out (bpf/lib/l4.h:107-118) */
+    if (c->n_portmap && (nh == IPPROTO_TCP || nh == IPPROTO_UDP)) {
+        uint16_t sport;
+        if (skb_load_bytes(s, l4_off, &sport, 2) < 0) return DROP_INVALID;
+        for (uint32_t k = 0; k < c->n_portmap && k < 16; k++) {
+            if (c->portmap[k].to != sport) continue;
+            uint16_t from = c->portmap[k].from;
+            if (l4_csum_replace(s, w, l4_off + co, sport, from, 2 | fl) < 0) return DROP_CSUM_L4;
+            if (skb_store_bytes(s, w, l4_off, &from, 2) < 0) return DROP_WRITE_ERROR;
+            r->eg_flags |= EG_F_PORTMAP;
+        }
+    }
+    ct_state_t st; memset(&st, 0, sizeof st);
+    const int acct = (c->flags & LXC_F_CT_ACCOUNTING) != 0;
+    ret = ct_lookup(c->ct_map4, t, s, l4_off, CT_EGRESS, &st, 0, now, acct);
+    if (ret < 0) return ret;
+    const int fwd = ret;
+    r->ct_ret = (uint8_t)fwd;
+    uint16_t dst_id = ((orig_dip & g_node.ipv4_cluster_mask) == g_node.ipv4_cluster_range) ? CLUSTER_ID : WORLD_ID;
+    int verdict = policy_can_egress4(c, s, t, dst_id, ge32(t, 4));   /* ipv4_ct_tuple_get_daddr = tuple->saddr */
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { om_delete(c->ct_map4, t); r->eg_flags |= EG_F_DELETED; }
+        return verdict;
+    }
+    switch (ret) {
+    case CT_NEW:
+        sn.src_sec_id = c->seclabel;
+        ret = ct_create(c->ct_map4, t, s, CT_EGRESS, &sn, 0, now);
+        if (IS_ERR(ret)) return ret;
+        r->eg_flags |= EG_F_CREATED;
+        break;
+    case CT_ESTABLISHED:
+        break;
+    case CT_RELATED: case CT_REPLY:
+        s->cb[2] = 1;                                                    /* policy_mark_skip */
+        if (st.rev_nat_index) {
+            ret = lb4_rev_nat_eg(c, s, w, l4_off, t, &st);
+            if (IS_ERR(ret)) return ret;
+            r->eg_flags |= EG_F_REVNAT;
+        }
+        break;
+    default:
+        return DROP_POLICY;
+    }
+    if (verdict > 0) {                                                   /* redirect_to_proxy */
+        ret = redirect_to_host_port_checks(s, l4_off, nh);
+        if (IS_ERR(ret)) return ret;
+        pol_ctx x = {w, plog};
+        redirect_write(s, &x, l4_off, t, 0, (uint16_t)verdict, (const uint8_t *)&orig_dip, c->seclabel, now);
+        if (plog) plog[1] = 1;                                          /* egress entry: no policy MAC stores */
+        r->eg_flags |= EG_F_PROXY; r->proxy = (uint16_t)verdict;
+        ret = ipv4_l3(s, w, c->node_mac, g_node.host_mac);
+        if (ret != TC_ACT_OK) return ret;
+        r->ifindex = g_node.host_ifindex;
+        return TC_ACT_REDIRECT;
+    }
+    orig_dip = rd32(s, 30);
+    const uint8_t *ep = g_node.lxc_map ? endpoint_val4(g_node.lxc_map, orig_dip) : NULL;
+    if (ep) {
+        uint32_t epf; memcpy(&epf, ep + 8, 4);
+        if (epf & ENDPOINT_F_HOST) {
+            if (!g_node.host_ifindex) return DROP_NO_LXC;
+            goto to_host;
+        }
+        s->cb[2] = 0;                                                    /* policy_clear_mark */
+        ret = ipv4_l3(s, w, ep + 24, ep + 16);                           /* ipv4_local_delivery, l3.h:136-168 */
+        if (ret != TC_ACT_OK) return ret;
+        r->eg_flags |= EG_F_LOCAL;
+        return local_delivery_tail(s, w, l4_off, ep, nh, c->seclabel, nr);
+    }
+    if (g_node.encap_ifindex) {                                          /* encap_and_redirect, lib/encap.h */
+        uint8_t k[20] = {0};
+        uint32_t a = orig_dip & g_node.ipv4_mask;
+        memcpy(k, &a, 4); k[16] = 1;
+        const uint8_t *tun = g_node.tunnel_map ? om_lookup_ptr(g_node.tunnel_map, k) : NULL;
+        if (tun) {
+            r->tunnel_ip = bswap32(ge32(tun, 0));                        /* bpf_htonl(tunnel->ip4) */
+            r->ifindex = g_node.encap_ifindex;
+            r->eg_flags |= EG_F_ENCAP;
+            return TC_ACT_REDIRECT;
+        }
+    }
+    if (dst_id == CLUSTER_ID) s->cb[2] = 1;                              /* policy_mark_skip */
+    ret = ipv4_l3(s, w, NULL, c->node_mac);                              /* pass_to_stack */
+    if (ret != TC_ACT_OK) return ret;
+    r->eg_flags |= EG_F_TO_STACK;
+    return TC_ACT_OK;
+to_host:
+    ret = ipv4_l3(s, w, c->node_mac, g_node.host_mac);
+    if (ret != TC_ACT_OK) return ret;
+    r->eg_flags |= EG_F_TO_HOST;
+    r->ifindex = g_node.host_ifindex;
+    return TC_ACT_REDIRECT;
+}
+
+/* handle_ingress (from-container, bpf_lxc.c:685-738) + tail_handle_ipv4 (:659-668) */
+static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_egress_out *o,
+                           uint8_t *row, uint8_t *plog, uint8_t *skip, uint32_t *secctx, uint32_t *ifx,
+                           uint16_t *lxcid) {
+    skb_t s; skb_init(&s, b, i);
+    memcpy(row, s.data, b->snap_stride);
+    s.data = row;
+    memset(o, 0, sizeof *o);
+    *skip = 1; *secctx = 0; *ifx = 0; *lxcid = 0;
+    if (plog) memset(plog, 0, O_PLOG);
+    const o_lxc_cfg *c = a->slot[(b->lxc_id ? b->lxc_id[i] : 0) & 0xffff];
+    o->stage = O_STAGE_FROM_LXC;
+    if (!c) { o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL); return; }
+    int ret;
+    eg_res r; memset(&r, 0, sizeof r);
+    nd_res nr; memset(&nr, 0, sizeof nr);
+    if (s.protocol == 0x0806) {                  /* tail_handle_arp: the ARP responder (out of scope) */
+        o->stage = 0; o->eg_flags = EG_F_ARP; return;
+    }
+    if (c->flags & LXC_F_DROP_ALL) ret = DROP_POLICY;
+    else if (s.protocol == 0x86DD) { o->stage = 0; o->eg_flags = EG_F_IPV6; return; }
+    else if (s.protocol == 0x0800) ret = from_lxc_ipv4(c, &s, row, now, &r, plog, &nr);
+    else ret = DROP_UNKNOWN_L3;
+    o->eg_ct_ret = r.ct_ret; o->ct_ret = r.ct_ret;
+    o->slave = r.slave; o->rev_nat = r.rev_nat; o->eg_flags = r.eg_flags;
+    if (ret == O_NETDEV_TAILCALL) {
+        o->stage = O_STAGE_POLICY; o->lxc_id = nr.lxc_id; o->ct_ret = 0;
+        *skip = 0; *secctx = nr.secctx; *ifx = nr.ifindex; *lxcid = nr.lxc_id;
+        if (plog) plog[0] = 0;
+        return;
+    }
+    if (IS_ERR(ret)) {                           /* send_drop_notify(SECLABEL, 0, 0, 0, ret, TC_ACT_SHOT) */
+        o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret);
+        /* a cilium_proxy4 entry written by ipv4_redirect_to_host_port stays when
+         * the ipv4_l3 that follows it drops the packet (lxc.h:137 before l3.h:54) */
+        if (plog && !(r.eg_flags & EG_F_PROXY)) plog[0] = 0;
+        o->eg_flags &= (uint16_t)(EG_F_CREATED | EG_F_DELETED | EG_F_LB | EG_F_LOOPBACK | EG_F_PORTMAP | EG_F_REVNAT);
+        return;
+    }
+    o->action = (uint8_t)ret;
+    o->proxy_port = r.proxy; o->ifindex_lo = (uint16_t)r.ifindex; o->tunnel_ip = r.tunnel_ip;
+}
+
+void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egress_out *out, uint8_t *snap_out) {
+    const uint32_t n = b->n;
+    uint8_t *snap = snap_out ? snap_out : (uint8_t *)malloc((size_t)n * b->snap_stride + 1);
+    uint8_t *skip = (uint8_t *)malloc((size_t)n + 1);
+    uint32_t *secctx = (uint32_t *)malloc((size_t)n * 4 + 4), *ifx = (uint32_t *)malloc((size_t)n * 4 + 4);
+    uint16_t *lxcid = (uint16_t *)malloc((size_t)n * 2 + 2);
+    uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
+    for (uint32_t i = 0; i < n; i++)
+        from_container(a, b, i, now, &out[i], snap + (size_t)i * b->snap_stride, plog + (size_t)i * O_PLOG, &skip[i],
+                       &secctx[i], &ifx[i], &lxcid[i]);
+    /* the egress redirects' cilium_proxy4 updates, in batch order (lxc.h:137) */
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *e = plog + (size_t)i * O_PLOG;
+        if (!e[0]) continue;
+        om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
+        if (m && om_update(m, e + 4, e + 28, 0) < 0) {
+            o_egress_out *o = &out[i];
+            o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
+            o->flags &= (uint8_t)~1u; o->proxy_port = 0; o->ifindex_lo = 0;
+        }
+    }
+    /* handle_policy of the local deliveries, over the rewritten frames */
+    o_batch b2 = *b;
+    b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+    uint8_t *plog2 = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
+    o_ingress_out *ing = (o_ingress_out *)calloc((size_t)n + 1, sizeof(o_ingress_out));
+    for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(a, &b2, i, now, &ing[i], plog2, snap);
+    proxy_apply(&b2, plog2, ing, snap);
+    for (uint32_t i = 0; i < n; i++) {
+        if (skip[i]) continue;
+        o_egress_out *o = &out[i];
+        o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
+        o->flags = ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
+    }
+    free(plog2); free(ing); free(plog);
+    if (!snap_out) free(snap);
+    free(skip); free(secctx); free(ifx); free(lxcid);
 }

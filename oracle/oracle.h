@@ -66,6 +66,14 @@ typedef struct o_lxc_cfg {
     uint32_t flags;             /* GF_LXC_F_* */
     uint32_t n_l4_ingress;
     o_l4_allow l4_ingress[64];
+    /* from-container section (== gf_lxc_cfg) */
+    uint8_t lxc_mac[6], node_mac[6];
+    uint32_t lxc_ipv4;
+    om_map *lb4_services, *ipcache_map, *cidr4_egress_map;
+    uint32_t n_portmap;
+    struct { uint16_t from, to; } portmap[16];
+    uint32_t n_l4_egress;
+    o_l4_allow l4_egress[64];
 } o_lxc_cfg;
 
 typedef struct o_node_cfg {       /* == gf_node_cfg (bpf/node_config.h values on the path) */
@@ -75,6 +83,9 @@ typedef struct o_node_cfg {       /* == gf_node_cfg (bpf/node_config.h values on
     uint8_t host_ip6[16];         /* HOST_IP */
     uint8_t host_mac[6];          /* HOST_IFINDEX_MAC */
     uint8_t node_mac[6];          /* NODE_MAC */
+    om_map *lxc_map;              /* cilium_lxc (egress endpoint lookup) */
+    uint32_t ipv4_cluster_range, ipv4_cluster_mask, ipv4_loopback, ipv4_mask, encap_ifindex;
+    om_map *tunnel_map;           /* cilium_tunnel_map */
 } o_node_cfg;
 
 /* Per-packet metadata of a batch (host arrays, may be NULL where unused). */
@@ -154,6 +165,19 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
  * (struct drop_notify + up to 128 captured bytes), a packet's record in its
  * slot, zero where the packet was not dropped. */
 void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_out *out, uint8_t *events);
+
+/* ---------------- endpoint egress (== gf_lxc_egress_classify) ----------------
+ * The from-container program of endpoint lxc_id[i] over each frame, in batch
+ * order (bpf/bpf_lxc.c:685-738, 427-658), its proxy-map log applied in batch
+ * order, then handle_policy over the local deliveries in batch order. */
+typedef struct o_egress_out {       /* == gf_egress_out (24 B) */
+    uint8_t stage, action, reason, ct_ret, flags, eg_ct_ret;
+    uint16_t proxy_port, ifindex_lo, slave, rev_nat, eg_flags;
+    uint32_t tunnel_ip;
+    uint16_t lxc_id, pad;
+} o_egress_out;
+void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now_sec, o_egress_out *out,
+                    uint8_t *snap_out);
 
 /* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time);

@@ -28,12 +28,18 @@ class o_lxc_cfg(C.Structure):
     _fields_ = [("lxc_id", C.c_uint32), ("seclabel", C.c_uint32), ("policy_map", VP), ("ct_map4", VP),
                 ("ct_map6", VP), ("cidr4_ingress_map", VP), ("cidr6_ingress_map", VP), ("revnat4_map", VP),
                 ("revnat6_map", VP), ("flags", C.c_uint32), ("n_l4_ingress", C.c_uint32),
-                ("l4_ingress", o_l4_allow * 64)]
+                ("l4_ingress", o_l4_allow * 64), ("lxc_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6),
+                ("lxc_ipv4", C.c_uint32), ("lb4_services", VP), ("ipcache_map", VP), ("cidr4_egress_map", VP),
+                ("n_portmap", C.c_uint32), ("portmap", C.c_uint16 * 32), ("n_l4_egress", C.c_uint32),
+                ("l4_egress", o_l4_allow * 64)]
 
 
 class o_node_cfg(C.Structure):
     _fields_ = [("host_ifindex", C.c_uint32), ("proxy4_map", VP), ("proxy6_map", VP), ("ipv4_gateway", C.c_uint32),
-                ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6)]
+                ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6),
+                ("lxc_map", VP), ("ipv4_cluster_range", C.c_uint32), ("ipv4_cluster_mask", C.c_uint32),
+                ("ipv4_loopback", C.c_uint32), ("ipv4_mask", C.c_uint32), ("encap_ifindex", C.c_uint32),
+                ("tunnel_map", VP)]
 
 
 class o_batch(C.Structure):
@@ -81,6 +87,7 @@ _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
 _s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32, VP)
 _s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
+_s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
@@ -94,6 +101,9 @@ ING_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flag
 PIPE_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
                      ("pad0", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
                      ("rev_nat", "<u2"), ("dport", "<u2"), ("daddr4", "<u4"), ("lxc_id", "<u2"), ("pad1", "<u2")])
+EG_OUT = np.dtype([("stage", "u1"), ("action", "u1"), ("reason", "u1"), ("ct_ret", "u1"), ("flags", "u1"),
+                   ("eg_ct_ret", "u1"), ("proxy_port", "<u2"), ("ifindex_lo", "<u2"), ("slave", "<u2"),
+                   ("rev_nat", "<u2"), ("eg_flags", "<u2"), ("tunnel_ip", "<u4"), ("lxc_id", "<u2"), ("pad", "<u2")])
 
 
 class OMap:
@@ -232,3 +242,11 @@ def ingress_events(prog_array, b, out):
     ev = np.zeros((b.n, 160), np.uint8)
     lib.o_ingress_events(prog_array, C.byref(b), out.ctypes.data, ev.ctypes.data)
     return ev[ev[:, 0] == 1]
+
+
+def egress(prog_array, b, now):
+    """o_egress_batch: returns (records EG_OUT, rewritten snaps)."""
+    out = np.zeros(b.n, EG_OUT)
+    snap = np.zeros((b.n, b.snap_stride), np.uint8)
+    lib.o_egress_batch(prog_array, C.byref(b), now, out.ctypes.data, snap.ctypes.data)
+    return out, snap

@@ -6,6 +6,26 @@ import numpy as np
 from . import oracle as O
 
 
+def _be16(x):
+    return ((x & 0xff) << 8) | (x >> 8)
+
+
+def egress_fields(c, e, h):
+    """The from-container section of an endpoint config (o_lxc_cfg / gf_lxc_cfg)."""
+    c.lxc_mac[:] = list(e.get("lxc_mac", bytes(6)))
+    c.node_mac[:] = list(e.get("node_mac", bytes(6)))
+    c.lxc_ipv4 = e.get("lxc_ipv4", 0)
+    c.lb4_services, c.ipcache_map, c.cidr4_egress_map = h(e.get("lb4")), h(e.get("ipcache")), h(e.get("cidr4e"))
+    pm = e.get("portmap") or []
+    c.n_portmap = len(pm)
+    for i, (frm, to) in enumerate(pm):
+        c.portmap[2 * i], c.portmap[2 * i + 1] = _be16(frm), _be16(to)
+    l4 = e.get("l4e") or []
+    c.n_l4_egress = len(l4)
+    for i, (port, proxy, nh) in enumerate(l4):
+        c.l4_egress[i].port, c.l4_egress[i].proxy, c.l4_egress[i].nexthdr = _be16(port), _be16(proxy), nh
+
+
 class OracleDP:
     def __init__(self, sc, shards=1):
         self.sc = sc
@@ -21,7 +41,10 @@ class OracleDP:
         self._node = O.o_node_cfg(sc.host_ifindex, p(nd.get("proxy4")), p(nd.get("proxy6")), nd.get("ipv4_gateway", 0),
                                   (C.c_uint8 * 16)(*nd.get("host_ip6", bytes(16))),
                                   (C.c_uint8 * 6)(*nd.get("host_mac", bytes(6))),
-                                  (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))))
+                                  (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))),
+                                  p(nd.get("lxc_map")), nd.get("ipv4_cluster_range", 0), nd.get("ipv4_cluster_mask", 0),
+                                  nd.get("ipv4_loopback", 0), nd.get("ipv4_mask", 0), nd.get("encap_ifindex", 0),
+                                  p(nd.get("tunnel_map")))
         O.lib.o_set_node(C.byref(self._node))
         self.xdp_cfg = self.lb_cfg = None
         if sc.xdp:
@@ -49,6 +72,7 @@ class OracleDP:
                     c.l4_ingress[i].port = ((port & 0xff) << 8) | (port >> 8)
                     c.l4_ingress[i].proxy = ((proxy & 0xff) << 8) | (proxy >> 8)
                     c.l4_ingress[i].nexthdr = nh
+                egress_fields(c, e, p)
                 self.cfgs.append(c)
                 O.lib.o_prog_array_set(self.arr, e["lxc_id"], C.byref(c))
 
@@ -82,6 +106,10 @@ class OracleDP:
                                           C.pointer(self.lb_cfg) if self.lb_cfg is not None else None,
                                           C.pointer(self._nd), self.arr)
         return O.pipeline(self._pipe, self.batch(pk), now, threads, events)
+
+    def egress(self, pk, now):
+        O.lib.o_set_node(C.byref(self._node))
+        return O.egress(self.arr, self.batch(pk), now)
 
     def ct_gc(self, name, filter_time):
         return self.m[name].ct_gc(filter_time)
