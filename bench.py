@@ -11,8 +11,9 @@ partitioned; the only collective is the RCCL all-reduce of the counter block
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.  At N=1
 the line also carries "configs": the other BASELINE configurations measured the
 same way (config 1 XDP prefilter, config 3 service LB, config 4 full pipeline
-over raw frames, config 5 IPv6 ingress), each with its own roofline and CPU
-baseline (`--config N` prints that configuration alone as the line).
+over raw frames, config 5 IPv6 ingress, and the endpoint egress path of SURVEY
+§8(f)), each with its own roofline and CPU baseline (`--config N` prints that
+configuration alone as the line).
 """
 import argparse
 import glob
@@ -450,7 +451,71 @@ def cpu_config5(sc, st, W, K, S0):
             "sample": f"{done} packets (flows of 1/8 of the address pairs, same warm-up)"}
 
 
-EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_config5}
+# ----------------------------------------------------------------------------- endpoint egress
+def bench_egress(args, dev):
+    """The from-container program (handle_ipv4_from_lxc) over frames sent by 256
+    local endpoints, local deliveries continuing into handle_policy: 4M flows,
+    one 64-B frame each per step; each step a quarter of the flows starts anew
+    (new source port), the rest are established."""
+    import torch
+    from cilium_amd import synth
+    from cilium_amd.datapath import Datapath
+    W, K = 3, max(4, args.steps // 2)
+    n = args.egress_flows
+    sc, meta = synth.egress_tables(ct_max=args.ct_max)
+    f, lens, lid, fh = synth.egress_flows(meta, n)
+    dp = Datapath(sc, pin_prefix=None)
+    base = torch.from_numpy(f).to(dev)
+    q = n // 4
+    frames = []
+    for s in range(W + K):
+        fs = base.clone()
+        a, port = (s % 4) * q, 20000 + 7 * s
+        fs[a:a + q, 34], fs[a:a + q, 35] = port >> 8, port & 0xff
+        frames.append(fs)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+    len_t, lid_t, fh_t = t(lens, np.int32), t(lid, np.int16), t(fh, np.int32)
+
+    class FB:
+        pass
+
+    def fbatch(i):
+        b = FB()
+        b.frames, b.len, b.lxc_id, b.flow_hash, b.n, b.device = frames[i], len_t, lid_t, fh_t, n, dev
+        return b
+
+    fbs = [fbatch(i) for i in range(W + K)]
+    out = torch.empty((n, 24), dtype=torch.uint8, device=dev)
+    el, c, _, kern = timed(lambda s: dp.egress(fbs[s], sc.now + s, out=out, snap_out=False), W, K, dev)
+    cpu = None
+    if not args.no_cpu:
+        from oracle.scenario import OracleDP
+        from cilium_amd.synth import Packets
+        ref = OracleDP(sc)
+        m = (lid % 16) == 0
+        done, tt = 0, 0.0
+        for s in range(W + K):
+            pk = Packets(frames[s][torch.from_numpy(m).to(dev)].cpu().numpy(), lens[m], None, None, lid[m], None, fh[m])
+            a = time.perf_counter()
+            ref.egress(pk, sc.now + s)
+            if s >= W:
+                tt += time.perf_counter() - a
+                done += pk.n
+                if tt >= args.cpu_seconds / 2:
+                    break
+        cpu = {"value": round(done / tt / 1e6, 2), "unit": "Mpps", "cores": 1, "kind": "port",
+               "sample": f"{done} packets (the flows of 1/16 of the endpoints, same steps and warm-up), "
+                         "sequential oracle restatement"}
+    return {"workload": "egress: bpf_lxc from-container handle_ipv4_from_lxc (+ handle_policy of local deliveries), "
+                        f"256 endpoints, {n} flows/step (35% world, 20% tunnel, 25% local, 20% service VIPs), "
+                        "1/4 new per step",
+            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "packets_per_step": int(c[268]) // K, "warmup": W,
+            "roofline": roofline(kern, list(kern), float(c[270]) / K, "all egress kernels (frames -> verdicts)"),
+            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu}
+
+
+EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_config5, "egress": bench_egress}
 
 
 def add_traffic(cfg, r):
@@ -476,7 +541,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--config", default="2", choices=["1", "2", "3", "4", "5"],
+    ap.add_argument("--config", default="2", choices=["1", "2", "3", "4", "5", "egress"],
                     help="BASELINE configuration printed as the line (default: 2, the headline)")
     ap.add_argument("--flows-per-step", type=int, default=4 << 20)
     ap.add_argument("--pairs", type=int, default=1 << 20)
@@ -484,6 +549,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="config 2 only (skip the other configurations)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--egress-flows", type=int, default=4 << 20)
     args = ap.parse_args()
 
     import torch

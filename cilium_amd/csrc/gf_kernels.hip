@@ -1988,7 +1988,12 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         {   // the frame, rewritten in place from here on
             const uint8_t *src = fr.snap + (size_t)i * S;
             uint8_t *dst = E.snap + (size_t)i * S;
-            if (src != dst) for (uint32_t k = 0; k < S; k++) dst[k] = src[k];
+            if (src != dst) {
+                if (!(S & 15u) && !(((uintptr_t)src | (uintptr_t)dst) & 15u))
+                    for (uint32_t k = 0; k < S; k += 16) *reinterpret_cast<uint4 *>(dst + k) = *reinterpret_cast<const uint4 *>(src + k);
+                else
+                    for (uint32_t k = 0; k < S; k++) dst[k] = src[k];
+            }
         }
         Row w = eg_row(E, i, len);
         gf_egress_out o{};

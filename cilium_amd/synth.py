@@ -1148,3 +1148,77 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
         fh = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
         sc.batches.append(Packets(f, lens, None, None, lid, None, fh))
     return sc
+
+
+def egress_tables(n_ep=256, n_svc=1024, backends=4, ct_max=64_000_000, seed=0xE6E5):
+    """Egress measurement tables (the agent's production flag set: no
+    POLICY_EGRESS): n_ep local endpoints (10.1.x.y) with their MACs, one global
+    CT map, services whose backends are local endpoints (so some translate back
+    to the sender: loopback SNAT), a tunnel map covering 10.128.0.0/16, and
+    per-endpoint ingress policy admitting the endpoints' identities (local
+    deliveries continue into handle_policy)."""
+    rng = np.random.default_rng(seed)
+    sc = Scenario("egress_bench", now=10_000, host_ifindex=3)
+    ep4 = (ip4("10.1.0.0") + 1 + np.arange(n_ep)).astype(np.uint32)
+    lxc_id = (1000 + np.arange(n_ep)).astype(np.uint32)
+    seclabel = (256 + np.arange(n_ep)).astype(np.uint32)
+    macs = rng.integers(0, 256, (n_ep, 6)).astype(np.uint8)
+    node_mac = bytes([0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde])
+    ev = endpoint_infos(10 + np.arange(n_ep), seclabel, lxc_id, np.zeros(n_ep))
+    ev[:, 16:22] = macs
+    ev[:, 24:30] = np.frombuffer(node_mac, np.uint8)
+    sc.add_map(MapSpec("cilium_lxc", HASH, 20, 112, 65535, 0, endpoint_keys4(ep4), ev))
+    sc.add_map(MapSpec("ct4", LRU_HASH, 14, 48, ct_max, 0))
+    sc.add_map(MapSpec("ct6", LRU_HASH, 40, 48, 1 << 16, 0))
+    vip = (ip4("10.96.0.0") + 1 + np.arange(n_svc)).astype(np.uint32)
+    sport = rng.choice(np.array([80, 443, 8080, 53], np.uint32), n_svc)
+    tgt = ep4[rng.integers(0, n_ep, (n_svc, backends))]
+    keys = [lb4_keys(vip, sport, np.zeros(n_svc))]
+    vals = [lb4_vals(np.zeros(n_svc), np.zeros(n_svc), np.full(n_svc, backends), np.zeros(n_svc))]
+    for b in range(backends):
+        keys.append(lb4_keys(vip, sport, np.full(n_svc, b + 1)))
+        vals.append(lb4_vals(tgt[:, b], np.where(np.arange(n_svc) % 3 == 0, 8080, sport), np.zeros(n_svc),
+                             1 + np.arange(n_svc)))
+    sc.add_map(MapSpec("lb4", HASH, 8, 12, 1 << 20, 0, np.concatenate(keys), np.concatenate(vals)))
+    rk, rv = revnat4_entries(1 + np.arange(n_svc), vip, sport)
+    sc.add_map(MapSpec("revnat4", HASH, 2, 6, 1 << 16, 0, rk, rv))
+    sc.add_map(MapSpec("tunnel", HASH, 20, 20, 65536, 0, endpoint_keys4(np.array([ip4("10.128.0.0")], np.uint32)),
+                       endpoint_keys4(np.array([ip4("192.168.7.2")], np.uint32))))
+    pk = policy_keys(seclabel, np.zeros(n_ep), np.zeros(n_ep))
+    pv = policy_vals(np.zeros(n_ep))
+    for e in range(n_ep):
+        sc.add_map(MapSpec(f"pol{e}", HASH, 8, 24, 16384, 0, pk, pv))
+        sc.lxc.append({"lxc_id": int(lxc_id[e]), "seclabel": int(seclabel[e]), "policy": f"pol{e}", "ct4": "ct4",
+                       "ct6": "ct6", "revnat4": "revnat4", "flags": LXC_PRODUCTION, "lxc_mac": bytes(macs[e]),
+                       "node_mac": node_mac, "lxc_ipv4": int(be32_bytes([ep4[e]]).view("<u4")[0, 0]), "lb4": "lb4"})
+    raw_be = lambda a: int(be32_bytes([a]).view("<u4")[0, 0])
+    sc.node = {"lxc_map": "cilium_lxc", "ipv4_cluster_range": raw_be(ip4("10.0.0.0")),
+               "ipv4_cluster_mask": raw_be(0xFF000000), "ipv4_loopback": raw_be(ip4("10.255.255.245")),
+               "ipv4_mask": raw_be(0xFFFF0000), "encap_ifindex": 5, "tunnel_map": "tunnel",
+               "host_mac": bytes([0xce, 0x72, 0xa7, 0x03, 0x88, 0x56]), "node_mac": node_mac}
+    meta = dict(ep4=ep4, lxc_id=lxc_id, macs=macs, vip=vip, sport=sport, node_mac=node_mac)
+    return sc, meta
+
+
+def egress_flows(meta, n_flows, seed=0xE6E6):
+    """n_flows egress flows (one frame each, 64-B snaps): 35% world peers (to the
+    stack), 20% tunnel peers (encap), 25% other local endpoints (local delivery),
+    20% service VIPs (lb4_local to a local backend).  Returns (frames, lens,
+    lxc_id, flow_hash, sport column offset)."""
+    rng = np.random.default_rng(seed)
+    ep4, n_ep = meta["ep4"], len(meta["ep4"])
+    e = rng.integers(0, n_ep, n_flows)
+    kind = rng.random(n_flows)
+    world = (ip4("100.64.0.0") + rng.integers(0, 1 << 20, n_flows)).astype(np.uint32)
+    tun = (ip4("10.128.0.0") + rng.integers(0, 1 << 16, n_flows)).astype(np.uint32)
+    peer = ep4[(e + 1 + rng.integers(0, n_ep - 1, n_flows)) % n_ep]
+    si = rng.integers(0, len(meta["vip"]), n_flows)
+    d = np.where(kind < 0.35, world, np.where(kind < 0.55, tun, np.where(kind < 0.80, peer, meta["vip"][si])))
+    dp = np.where(kind >= 0.80, meta["sport"][si], rng.choice(np.array([80, 443, 53, 8080], np.uint32), n_flows))
+    pr = np.where(rng.random(n_flows) < 0.8, TCP, UDP).astype(np.uint8)
+    sp = 1024 + rng.integers(0, 60000, n_flows)
+    f, lens = frames_v4(n_flows, 64, ep4[e], d, pr, sp, dp, F_ACK, payload=rng.integers(0, 64, n_flows))
+    f[:, 6:12] = meta["macs"][e]
+    f[:, 0:6] = np.frombuffer(meta["node_mac"], np.uint8)
+    fh = rng.integers(0, 1 << 32, n_flows, dtype=np.uint64).astype(np.uint32)
+    return f, lens, meta["lxc_id"][e].astype(np.uint16), fh
