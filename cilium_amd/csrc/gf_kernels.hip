@@ -1677,6 +1677,57 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
     if (stats) st.flush(stats);
 }
 
+// ---- ingest re-partition (real traffic on N GPUs): the owner rank of each
+// frame is the rank of its flow group, the unordered address pair that the
+// CT of handle_policy sees, i.e. after bpf_lb's translation (stateless, so it
+// can run before the exchange).  Same rule as the synthetic stream's
+// (cilium_amd/stream.py pair_rank): fmix64 of (max << 32 | min) of the
+// host-order addresses, mod the rank count.  Frames that cannot reach
+// conntrack stay on their rank.
+__device__ __forceinline__ uint32_t pair_rank4(uint32_t sa_raw, uint32_t da_raw, uint32_t world) {
+    const uint64_t a = __builtin_bswap32(sa_raw), b = __builtin_bswap32(da_raw);
+    uint64_t x = ((a < b ? b : a) << 32) | (a < b ? a : b);
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return (uint32_t)(x & 0xffffffffull) % world;
+}
+// lb_v6's translated address (d6 unchanged unless it translates); kept out of
+// line: inlined into k_partition, the hipcc of this image merged the target's
+// third word with the lookup key's (observed on gfx950, the parity test pins it)
+__device__ __attribute__((noinline)) void lb_v6_daddr(const LbDev &L, const PktHdr &h, uint32_t fh, uint32_t len,
+                                                      uint32_t *d6) {
+    const PktHdrA ha{h, fh};
+    gf_lb_out lo{};
+    uint32_t n6[4], ab = 0, kd = 0;
+    if (lb_v6(L, ha, len, lo, n6, ab, kd) == TC_REDIRECT)
+        for (int k = 0; k < 4; k++) d6[k] = n6[k];
+}
+__global__ __launch_bounds__(BLOCK) void k_partition(gf_frames fr, const uint32_t *flow_hash, PipeDev P, uint32_t self,
+                                                     uint32_t world, uint32_t *owner, uint32_t *counts) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= fr.n) return;
+    const uint32_t len = fr.len[i], S = fr.snap_stride;
+    const uint32_t cap = S < len ? S : len;
+    PktHdr h;
+    parse_row(fr.snap + (size_t)i * S, cap, len, h);
+    const PktHdrA ha{h, flow_hash ? flow_hash[i] : 0u};
+    uint32_t r = self, ab = 0, kd = 0;
+    if (h.et == 0x0800 && len >= 34) {
+        uint32_t da = h.da;
+        if (P.has_lb && !(P.L.flags & GF_LB_F_NO_IPV4)) {
+            gf_lb_out lo{};
+            if (lb_v4(P.L, ha, len, lo, ab, kd) == TC_REDIRECT) da = lo.new_daddr4;
+        }
+        r = pair_rank4(h.sa, da, world);
+    } else if (h.et == 0x86DD && len >= 54) {
+        // lb_v6 leaves d6 alone unless it translates (then it writes all four words)
+        uint32_t d6[4] = {h.d6[0], h.d6[1], h.d6[2], h.d6[3]};
+        if (P.has_lb && !(P.L.flags & GF_LB_F_NO_IPV6)) lb_v6_daddr(P.L, h, ha.fh, len, d6);
+        r = gf_pair_hash6(h.s6, d6) % world;
+    }
+    owner[i] = r;
+    atomicAdd(&counts[r], 1u);
+}
+
 // ================================================================ CT garbage collection
 // ctmap.GC / Flush (pkg/maps/ctmap/ctmap.go:277-368, GCFilterByTime): delete every
 // entry with lifetime < filter_time.  On the device the sweep also compacts each
@@ -3248,6 +3299,55 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     c2.flow_hash = b->flow_hash;
     return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out, fr.len,
                        snap_out ? snap_out : fr.snap, fr.snap_stride, snap_out);
+}
+
+// ---- ingest re-partition ----
+int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, uint32_t nranks, uint32_t *owner,
+                          uint32_t *order, uint32_t *counts, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(big_lock());
+    auto o = get_obj(pipe);
+    if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
+    auto p = std::static_pointer_cast<ProgPipe>(o);
+    if (!b || !owner || !order || !counts) return -EFAULT;
+    if (nranks == 0 || nranks > 65536 || self_rank >= nranks) return -EINVAL;
+    const gf_frames &fr = b->frames;
+    hipStream_t s = (hipStream_t)stream;
+    if (hip_ok(hipMemsetAsync(counts, 0, (size_t)nranks * 4, s), "partition counts")) return -EIO;
+    if (fr.n == 0) return 0;
+    if (!fr.snap || !fr.len) return -EFAULT;
+    if (fr.snap_stride < 14) return -EINVAL;
+    if (fr.n > (1u << 30)) return -E2BIG;
+    int r;
+    PipeDev P{};
+    if (p->lb) {
+        if ((r = push_map(p->lb->lb4, s)) || (r = push_map(p->lb->lb6, s))) return r;
+        if (p->lb->lb4) P.L.s4 = p->lb->lb4->hdesc();
+        if (p->lb->lb6) P.L.s6 = p->lb->lb6->hdesc();
+        P.L.flags = p->lb->cfg.flags;
+        P.has_lb = 1;
+    }
+    const uint32_t n = fr.n;
+    static DevBuf keys, vals, tmp;
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    if ((r = grow(keys, (size_t)n * 4))) return r;
+    {
+        ProfScope ps("k_partition", s);
+        hipLaunchKernelGGL(k_partition, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->flow_hash, P, self_rank,
+                           nranks, owner, counts);
+        if ((r = hip_ok(hipGetLastError(), "k_partition"))) return r;
+    }
+    // stable counting order by owner: radix sort of (owner, index) over the owner's bits
+    int bits = 1;
+    while ((1u << bits) < nranks) bits++;
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, owner, (uint32_t *)keys.p, rocprim::counting_iterator<uint32_t>(0u), order,
+                                    n, 0, bits, s);
+    if ((r = grow(tmp, tb + 256))) return r;
+    tb = tmp.bytes;
+    if (hip_ok(rocprim::radix_sort_pairs(tmp.p, tb, owner, (uint32_t *)keys.p, rocprim::counting_iterator<uint32_t>(0u),
+                                         order, n, 0, bits, s), "partition sort"))
+        return -EIO;
+    return 0;
 }
 
 // ---- conntrack GC ----

@@ -424,6 +424,17 @@ typedef struct gf_pipeline_out {   /* 24 B */
 int gf_pipeline_classify(int pipe, const gf_pipe_batch *batch, uint32_t now_sec, gf_pipeline_out *out,
                          uint8_t *new_daddr6, uint8_t *snap_out, void *stream);
 
+/* ---- ingest re-partition for N GPUs (real traffic) ----
+ * owner[i] = the rank owning packet i's flow group: the unordered address pair
+ * handle_policy's conntrack sees (after bpf_lb's translation, which is
+ * stateless), fmix64-hashed mod nranks (frames that cannot reach conntrack
+ * stay on self_rank); order = the packet indices stably grouped by owner;
+ * counts[r] = packets for rank r.  All DEVICE pointers (n, n, nranks
+ * elements).  The caller exchanges the frames (cilium_amd.shard: one RCCL
+ * all-to-all) and classifies what it receives. */
+int gf_pipeline_partition(int pipe, const gf_pipe_batch *batch, uint32_t self_rank, uint32_t nranks,
+                          uint32_t *owner, uint32_t *order, uint32_t *counts, void *stream);
+
 /* ---- conntrack garbage collection ----
  * ctmap.GC(m, name, GCFilterByTime) / ctmap.Flush (pkg/maps/ctmap/ctmap.go:277-368):
  * deletes every entry of a CT map (key ipv4_ct_tuple 14 B or ipv6_ct_tuple 40 B,

@@ -290,3 +290,23 @@ def test_egress_fuzz(seed, kw):
     for e in range(16):
         assert dp.dump_map(f"pol{e}") == ref.dump(f"pol{e}"), f"policy counters pol{e}"
     assert dp.dump_map("cilium_proxy4") == ref.dump("cilium_proxy4")
+
+
+def test_pipeline_partition_owners():
+    """gf_pipeline_partition (ingest re-partition for N GPUs): the owner of every
+    frame is its flow group's rank after bpf_lb's translation, as the host
+    restatement computes it from the oracle's LB results; stable owner order and
+    per-rank counts."""
+    from cilium_amd import shard
+    from test_shard import owners_host
+    sc = synth.pipeline_fuzz(seed=22, n_packets=20000, n_batches=2)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for world, rank in ((2, 1), (3, 0), (8, 5)):
+        for pk in sc.batches:
+            b = DeviceBatch(pk, parse=False)
+            owner, order, counts = shard.partition(dp, b.frames, b.len, rank, world, b.flow_hash, b.tc_index)
+            lo, nd6 = ref.lb(pk)
+            want = owners_host(lo, nd6, pk, rank, world)
+            assert np.array_equal(owner.cpu().numpy(), want)
+            assert np.array_equal(order.cpu().numpy(), np.argsort(want, kind="stable"))
+            assert np.array_equal(counts.cpu().numpy(), np.bincount(want, minlength=world))
