@@ -2009,8 +2009,16 @@ struct EgDev {
 };
 #define GF_CTLOG_WORDS 20u
 
-__device__ __forceinline__ Row eg_row(const EgDev &E, uint32_t i, uint32_t len) {
-    return Row{E.snap + (size_t)i * E.stride, E.stride < len ? E.stride : len};
+// The header bytes the IPv4 egress programs touch (< l4_off + 18 <= 92) are staged
+// per lane in LDS: one vector load per row instead of a global access per byte.
+#define GF_EG_STAGE 128u
+__device__ __forceinline__ uint32_t eg_stage_bytes(uint32_t S) { return S < GF_EG_STAGE ? S : GF_EG_STAGE; }
+__device__ __forceinline__ void eg_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
+    if (!(n & 15u) && !(((uintptr_t)src | (uintptr_t)dst) & 15u)) {
+        for (uint32_t k = 0; k < n; k += 16) *reinterpret_cast<uint4 *>(dst + k) = *reinterpret_cast<const uint4 *>(src + k);
+    } else {
+        for (uint32_t k = 0; k < n; k++) dst[k] = src[k];
+    }
 }
 __device__ __forceinline__ bool mac_eq(const Row &w, uint32_t off, const uint32_t *m) {
     return w.r32(off) == m[0] && w.r16(off + 4) == (m[1] & 0xffffu);
@@ -2031,22 +2039,18 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
                                                     unsigned long long *stats) {
     __shared__ uint32_t sl[272];
+    __shared__ uint4 lds[BLOCK * (GF_EG_STAGE / 16)];
     Stats st{sl};
     if (stats) st.init();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < fr.n) {
-        const uint32_t len = fr.len[i], S = fr.snap_stride;
-        {   // the frame, rewritten in place from here on
-            const uint8_t *src = fr.snap + (size_t)i * S;
-            uint8_t *dst = E.snap + (size_t)i * S;
-            if (src != dst) {
-                if (!(S & 15u) && !(((uintptr_t)src | (uintptr_t)dst) & 15u))
-                    for (uint32_t k = 0; k < S; k += 16) *reinterpret_cast<uint4 *>(dst + k) = *reinterpret_cast<const uint4 *>(src + k);
-                else
-                    for (uint32_t k = 0; k < S; k++) dst[k] = src[k];
-            }
-        }
-        Row w = eg_row(E, i, len);
+        const uint32_t len = fr.len[i], S = fr.snap_stride, K = eg_stage_bytes(S);
+        const uint8_t *src = fr.snap + (size_t)i * S;
+        uint8_t *dst = E.snap + (size_t)i * S;
+        uint8_t *row = reinterpret_cast<uint8_t *>(lds + threadIdx.x * (GF_EG_STAGE / 16));
+        eg_copy(row, src, K);                                 // the header, staged
+        if (S > K && src != dst) eg_copy(dst + K, src + K, S - K);   // the rest of the snap, as is
+        Row w{row, K < len ? K : len};
         gf_egress_out o{};
         EgRec r{};
         r.len = len;
@@ -2174,6 +2178,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         }
         erec[i] = r;
         keys[i] = key;
+        eg_copy(dst, row, K);                                 // the frame as the front left it
     }
     if (stats) st.flush(stats);
 }
@@ -2283,13 +2288,12 @@ __device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, u
 // The CT / policy part of handle_ipv4_from_lxc (bpf_lxc.c:499-658) for packet i.
 // Returns TC_OK / TC_REDIRECT / ND_TAILCALL (local delivery; ifx, lxc, mapped
 // filled) or an error.
-__device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, gf_egress_out &o, uint32_t &ifx, uint32_t &lxc,
-                          int *added, bool seq, uint32_t &ab) {
+__device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
+                          uint32_t &lxc, int *added, bool seq, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
     const int l4_off = r.l4_off;
     const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
     const uint32_t flags = gload<uint32_t>(&c->flags);
-    Row w = eg_row(E, i, len);
     const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
     // ct_lookup4(CT_EGRESS): the L4 words as the frame holds them now
     gf_rec hr{};
@@ -2406,8 +2410,13 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, gf_egress_
         const int r3 = redirect_checks(len, l4_off, nh);
         if (r3 < 0) return r3;
         const uint32_t od[1] = {r.orig_dip};
-        pol_redirect(E.X, i, len, l4_off, nh, t, false, (uint32_t)verdict & 0xffffu, od,
-                     gload<uint32_t>(&c->seclabel), 1u);
+        const uint32_t np = (uint32_t)verdict & 0xffffu, gw = E.X.gw;
+        l4_csum(w, len, l4_off + (int)co, t[2] & 0xffffu, np, 2u | fl);   // l4_modify_port (lxc.h:124)
+        w.w16((uint32_t)(l4_off + 2), np);
+        w.w32(30, gw);                                                    // daddr = IPV4_GATEWAY
+        l3_csum(w, len, 24, r.orig_dip, gw, 4);
+        if (co) l4_csum(w, len, l4_off + (int)co, r.orig_dip, gw, 4u | GF_F_PSEUDO_HDR | fl);
+        pol_redirect(E.X, i, len, l4_off, nh, t, false, np, od, gload<uint32_t>(&c->seclabel), 1u);
         o.eg_flags |= GF_EG_F_PROXY;
         o.proxy_port = (uint16_t)verdict;
         const int r4 = eg_ipv4_l3(w, len, nm, E.host_mac);
@@ -2467,9 +2476,12 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
                                                      uint32_t *ct_count, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
+    __shared__ uint4 lds[BLOCK * (GF_EG_STAGE / 16)];
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
+    uint8_t *row = reinterpret_cast<uint8_t *>(lds + threadIdx.x * (GF_EG_STAGE / 16));
+    const uint32_t K = eg_stage_bytes(E.stride);
     const uint32_t nb = GF_SCHED_NFAM(sched)[0], lane = threadIdx.x & 63u;
     uint32_t *queue = GF_SCHED_QUEUE(sched);
     const bool seq = *E.seq != 0;
@@ -2495,12 +2507,15 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
             o.stage = GF_STAGE_FROM_LXC;
             o.slave = r.slave; o.rev_nat = r.rev_nat; o.eg_flags = r.eflags;
             uint32_t ifx = 0, lxc = 0, ab = 24 + 34 + 32;
-            const int ret = eg_ct_part(E, r, i, o, ifx, lxc, &added, seq, ab);
+            uint8_t *g = E.snap + (size_t)i * E.stride;
+            eg_copy(row, g, K);
+            Row w{row, K < r.len ? K : r.len};
+            const int ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, ab);
+            eg_copy(g, row, K);
             o.ct_ret = o.eg_ct_ret;
             if (ret == ND_TAILCALL) {                   // handle_policy of the destination, next pass
                 o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; o.ct_ret = 0;
                 PktHdr h2;
-                const Row w = eg_row(E, i, r.len);
                 parse_row(w.p, w.cap, r.len, h2);
                 const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
                 key2[i] = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
@@ -3462,7 +3477,7 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     E.strict = strict;
     E.seq = (uint32_t *)ew.seq.p;
     E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
-    E.X.snap = wsnap; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;
+    E.X.snap = nullptr; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;   // writes: k_eg_groups
     memcpy(E.X.host6, node.host_ip6, 16);
     if ((r = px_log_begin(n, s, E.X))) return r;
     if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 4, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 4, s), "eg ctlog"))
