@@ -80,7 +80,8 @@ class gf_lxc_cfg(C.Structure):
                 ("node_mac", C.c_uint8 * 6), ("lxc_ipv4", C.c_uint32), ("lb4_services", C.c_int),
                 ("ipcache_map", C.c_int), ("cidr4_egress_map", C.c_int), ("n_portmap", C.c_uint32),
                 ("portmap", C.c_uint16 * 32), ("n_l4_egress", C.c_uint32),
-                ("l4_egress", gf_l4_allow * GF_MAX_L4_INGRESS)]
+                ("l4_egress", gf_l4_allow * GF_MAX_L4_INGRESS), ("lxc_ip6", C.c_uint8 * 16),
+                ("lb6_services", C.c_int), ("cidr6_egress_map", C.c_int)]
 
 
 class gf_prof_rec(C.Structure):
@@ -92,7 +93,7 @@ class gf_node_cfg(C.Structure):
                 ("ipv4_gateway", C.c_uint32), ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6),
                 ("node_mac", C.c_uint8 * 6), ("lxc_map", C.c_int), ("ipv4_cluster_range", C.c_uint32),
                 ("ipv4_cluster_mask", C.c_uint32), ("ipv4_loopback", C.c_uint32), ("ipv4_mask", C.c_uint32),
-                ("encap_ifindex", C.c_uint32), ("tunnel_map", C.c_int)]
+                ("encap_ifindex", C.c_uint32), ("tunnel_map", C.c_int), ("router_ip6", C.c_uint8 * 16)]
 
 
 class gf_netdev_cfg(C.Structure):

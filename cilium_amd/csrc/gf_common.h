@@ -231,4 +231,7 @@ struct gf_lxc_dev {
     gf_trie_desc cidr4e;
     uint32_t portmap[16];              // from | to << 16 (raw be16 each)
     gf_l4_allow_dev l4e[GF_MAX_L4];
+    uint32_t lxc_ip6[4];               // LXC_IP (LE words)
+    gf_htab_desc lb6;
+    gf_trie_desc cidr6e;
 };

@@ -114,7 +114,7 @@ struct ProgLb : Obj {
 struct ProgLxc : Obj {
     gf_lxc_cfg cfg{};
     std::shared_ptr<Map> policy, ct4, ct6, cidr4, cidr6, revnat4, revnat6;
-    std::shared_ptr<Map> lb4, ipcache, cidr4e;   // from-container section
+    std::shared_ptr<Map> lb4, ipcache, cidr4e, lb6, cidr6e;   // from-container section
     ProgLxc() : Obj(ObjKind::ProgLxc) {}
 };
 struct PolicyArray : Obj {

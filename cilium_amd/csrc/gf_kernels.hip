@@ -1997,12 +1997,14 @@ static_assert(sizeof(EgRec) == 32, "EgRec must be 32 bytes");
 struct EgDev {
     const gf_lxc_dev *cfgs;
     const uint16_t *slot_of;
-    gf_htab_desc ct4, lxc, tunnel;
+    gf_htab_desc ct4, ct6, lxc, tunnel;
     uint8_t *snap;                      // the frames, rewritten in place
+    uint8_t *s6out, *d6out;             // IPv6 addresses of the local deliveries (handle_policy's columns)
     uint32_t stride, now, host_ifindex, encap_ifindex;
     uint32_t cluster_range, cluster_mask, loopback, ipv4_mask;
     uint32_t host_mac[2];
-    uint32_t strict;                    // CT4 inserts check max_entries (forces the single bucket)
+    uint32_t router6[4], host6[4];      // ROUTER_IP, HOST_IP (LE words)
+    uint32_t strict;                    // bit0: CT4 inserts check max_entries (forces the single bucket); bit1: CT6
     uint32_t *seq;                      // device word: 1 = single-bucket batch (written by k_eg_front)
     uint32_t *ctlog, *ctlog_n;          // deferred service entries: {i, key[4], value[12], pad[3]}
     IngCtx X;                           // redirect writes + cilium_proxy4 log (pol_redirect)
@@ -2034,6 +2036,105 @@ __device__ __forceinline__ int eg_ipv4_l3(Row &w, uint32_t len, const uint32_t *
     return TC_OK;
 }
 
+// handle_ipv6 (bpf_lxc.c:388-416) + the stateless head of ipv6_l3_from_lxc (:120-185):
+// icmp6_handle's responders, the source checks, ipv6_hdrlen, lb6_extract_key +
+// lb6_lookup_service + lb6_local (lb6_xlate: daddr, the L4 checksum at l4_off + its
+// offset even when that offset is 0, the port), map_lxc_out.  TC_OK: continue in
+// k_eg_groups (r.st = 0); a stage-NONE responder returns TC_OK with r.st set.
+__device__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Row &w, uint32_t len, uint32_t fh, EgRec &r,
+                         gf_egress_out &o, uint32_t &ab) {
+    r.eflags = GF_EG_F_IPV6;
+    if (len < 54) return D_INVALID;
+    if (w.b(20) == 58) {                                // icmp6_handle (bpf/lib/icmp6.h:380-401)
+        if (len < 62) return D_INVALID;
+        const uint32_t type = w.b(54);
+        bool to_router = true;
+        for (int k = 0; k < 4; k++) to_router &= w.r32(38 + 4 * k) == E.router6[k];
+        if (type == 135 || (type == 128 && to_router)) {
+            o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_IPV6 | GF_EG_F_RESPONDER;
+            return TC_OK;
+        }
+    }
+    uint32_t m[2];
+    m[0] = gload<uint32_t>(&c->lxc_mac[0]); m[1] = gload<uint32_t>(&c->lxc_mac[1]);
+    if (!mac_eq(w, 6, m)) return D_INVALID_SMAC;
+    m[0] = gload<uint32_t>(&c->node_mac[0]); m[1] = gload<uint32_t>(&c->node_mac[1]);
+    if (!mac_eq(w, 0, m)) return D_INVALID_DMAC;
+    for (int k = 0; k < 4; k++)
+        if (w.r32(22 + 4 * k) != gload<uint32_t>(&c->lxc_ip6[k])) return D_INVALID_SIP;
+    PktHdr h;
+    parse_row(w.p, w.cap, len, h);                      // nexthdr / l4_off after ipv6_hdrlen (negative: added as is)
+    const uint32_t nh = h.proto;
+    const int l4_off = h.l4;
+    r.nh = (uint8_t)nh; r.l4_off = (int16_t)l4_off;
+    ab += 34 + 28;
+    const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+    bool lb_try = true;
+    uint32_t kport = 0;
+    if (nh == 6 || nh == 17) {
+        if (!skb_ok(l4_off + 2, 2, len)) return -GF_EFAULT;
+        kport = w.r16((uint32_t)(l4_off + 2));
+    } else if (nh != 1 && nh != 58) lb_try = false;
+    const gf_htab_desc lb = gload<gf_htab_desc>(&c->lb6);
+    if (lb_try && lb.slots) {
+        const uint8_t *svc = nullptr;
+        if (kport) {
+            uint32_t kw[5] = {h.d6[0], h.d6[1], h.d6[2], h.d6[3], kport};
+            const int64_t f = ht_find<20>(lb, kw, key_hash<20>(kw));
+            ab += 44;
+            if (f >= 0) { const uint8_t *v = ht_val(lb, f); if (gload<uint16_t>(v + 18)) svc = v; }
+            if (!svc) kport = 0;
+        }
+        if (!svc) {
+            uint32_t kw[5] = {h.d6[0], h.d6[1], h.d6[2], h.d6[3], kport};
+            const int64_t f = ht_find<20>(lb, kw, key_hash<20>(kw));
+            ab += 44;
+            if (f >= 0) { const uint8_t *v = ht_val(lb, f); if (gload<uint16_t>(v + 18)) svc = v; }
+        }
+        if (svc) {                                      // lb6_local, lb.h:425-445
+            const uint32_t count = gload<uint16_t>(svc + 18);
+            const uint32_t slave = (fh % count + 1u) & 0xffffu;
+            uint32_t kw[5] = {h.d6[0], h.d6[1], h.d6[2], h.d6[3], kport | (slave << 16)};
+            const int64_t f = ht_find<20>(lb, kw, key_hash<20>(kw));
+            ab += 44;
+            if (f < 0) return D_NO_SERVICE;
+            const uint8_t *be = ht_val(lb, f);
+            r.slave = (uint16_t)slave; r.eflags |= GF_EG_F_LB;
+            r.rev_nat = gload<uint16_t>(be + 20);
+            uint32_t sum = 0;
+            for (int k = 0; k < 4; k++) {               // lb6_xlate: ipv6_store_daddr + csum_diff
+                const uint32_t nw = gload<uint32_t>(be + 4 * k);
+                w.w32(38 + 4 * k, nw);
+                sum = ck_add(ck_add(sum, ~h.d6[k]), nw);
+            }
+            if (l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl) < 0) return D_CSUM_L4;
+            const uint32_t sp = gload<uint16_t>(be + 16);
+            if (sp && kport != sp && (nh == 6 || nh == 17)) {
+                if (l4_csum(w, len, l4_off + (int)co, kport, sp, 2u | fl) < 0) return D_CSUM_L4;
+                if (!skb_ok(l4_off + 2, 2, len)) return D_WRITE_ERROR;
+                w.w16((uint32_t)(l4_off + 2), sp);
+            }
+            ab += 24;
+        }
+    }
+    const uint32_t npm = gload<uint32_t>(&c->n_portmap);          // map_lxc_out
+    if (npm && (nh == 6 || nh == 17)) {
+        if (!skb_ok(l4_off, 2, len)) return D_INVALID;
+        const uint32_t sp = w.r16((uint32_t)l4_off);
+        for (uint32_t k = 0; k < npm && k < 16; k++) {
+            const uint32_t pm = gload<uint32_t>(&c->portmap[k]);
+            const uint32_t from = pm & 0xffffu, to = pm >> 16;
+            if (to != sp) continue;
+            if (l4_csum(w, len, l4_off + (int)co, sp, from, 2u | fl) < 0) return D_CSUM_L4;
+            if (!skb_ok(l4_off, 2, len)) return D_WRITE_ERROR;
+            w.w16((uint32_t)l4_off, from);
+            r.eflags |= GF_EG_F_PORTMAP;
+        }
+    }
+    r.st = 0;
+    return TC_OK;
+}
+
 // handle_ingress + the stateless head of handle_ipv4_from_lxc, one packet per lane
 __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t *lxc_id, const uint32_t *fhash, EgDev E,
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
@@ -2047,10 +2148,16 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         const uint32_t len = fr.len[i], S = fr.snap_stride, K = eg_stage_bytes(S);
         const uint8_t *src = fr.snap + (size_t)i * S;
         uint8_t *dst = E.snap + (size_t)i * S;
+        const uint32_t cap0 = S < len ? S : len;
+        const bool v6 = len >= 14 && fbyte(src, cap0, 12) == 0x86 && fbyte(src, cap0, 13) == 0xDD;
         uint8_t *row = reinterpret_cast<uint8_t *>(lds + threadIdx.x * (GF_EG_STAGE / 16));
-        eg_copy(row, src, K);                                 // the header, staged
-        if (S > K && src != dst) eg_copy(dst + K, src + K, S - K);   // the rest of the snap, as is
-        Row w{row, K < len ? K : len};
+        if (v6) {                                             // extension headers: the whole snap, in HBM
+            if (src != dst) eg_copy(dst, src, S);
+        } else {
+            eg_copy(row, src, K);                             // the header, staged
+            if (S > K && src != dst) eg_copy(dst + K, src + K, S - K);   // the rest of the snap, as is
+        }
+        Row w = v6 ? Row{dst, cap0} : Row{row, K < len ? K : len};
         gf_egress_out o{};
         EgRec r{};
         r.len = len;
@@ -2067,7 +2174,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             const uint32_t flags = gload<uint32_t>(&c->flags);
             if (et == 0x0806) { o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_ARP; break; }
             if (flags & GF_LXC_F_DROP_ALL) { ret = D_POLICY; break; }
-            if (et == 0x86DD) { o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_IPV6; break; }
+            if (et == 0x86DD) { ret = eg_front6(E, c, w, len, fhash ? fhash[i] : 0u, r, o, ab); break; }
             if (et != 0x0800) { ret = D_UNKNOWN_L3; break; }
             if (len < 34) { ret = D_INVALID; break; }
             const uint32_t nh = w.b(23);
@@ -2160,7 +2267,11 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             r.st = 0;                                       // continue in k_eg_groups
         } while (0);
         uint32_t key;
-        if (r.st == 0) {
+        if (r.st == 0 && (r.eflags & GF_EG_F_IPV6)) {
+            uint32_t s6[4], d6[4];
+            for (int k = 0; k < 4; k++) { s6[k] = w.r32(22 + 4 * k); d6[k] = w.r32(38 + 4 * k); }
+            key = gf_pair_hash6(s6, d6) & GF_KEY_HASH;        // (family 0: one egress launch serves both)
+        } else if (r.st == 0) {
             key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
             const uint32_t lo = E.loopback;
             if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || E.strict) *E.seq = 1u;
@@ -2169,7 +2280,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             if (o.stage == GF_STAGE_FROM_LXC) {
                 if (ret < 0 || ret == TC_SHOT) {
                     o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
-                    o.eg_flags = r.eflags & (GF_EG_F_LB | GF_EG_F_LOOPBACK | GF_EG_F_PORTMAP);
+                    o.eg_flags = r.eflags & (GF_EG_F_LB | GF_EG_F_LOOPBACK | GF_EG_F_PORTMAP | GF_EG_F_IPV6);
                     o.slave = r.slave; o.rev_nat = r.rev_nat;
                 } else o.action = (uint8_t)ret;
             }
@@ -2178,7 +2289,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         }
         erec[i] = r;
         keys[i] = key;
-        eg_copy(dst, row, K);                                 // the frame as the front left it
+        if (!v6) eg_copy(dst, row, K);                        // the frame as the front left it
     }
     if (stats) st.flush(stats);
 }
@@ -2225,14 +2336,14 @@ __device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int 
 // policy_can_egress4 (policy.h:241-264 with POLICY_EGRESS, else :282-289):
 // ipcache identity, __policy_can_access(dir = CT_EGRESS: key.egress = 1, the
 // CFG_L3L4_EGRESS list), reserved identities through CIDR4_EGRESS_MAP.
-__device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, uint32_t daddr, uint32_t dport,
-                         uint32_t proto, uint32_t len, uint32_t &ab) {
+__device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, const uint32_t *da, bool v6,
+                         uint32_t dport, uint32_t proto, uint32_t len, uint32_t &ab) {
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_EGRESS)) return TC_OK;
     uint32_t identity = dst_id;
     const gf_htab_desc ic = gload<gf_htab_desc>(&c->ipcache);
     if (ic.slots) {
-        uint32_t kw[5] = {daddr, 0, 0, 0, 1u};
+        uint32_t kw[5] = {da[0], v6 ? da[1] : 0u, v6 ? da[2] : 0u, v6 ? da[3] : 0u, v6 ? 2u : 1u};
         const int64_t f = ht_find<20>(ic, kw, key_hash<20>(kw));
         ab += 20;
         if (f >= 0) { identity = gload<uint16_t>(ht_val(ic, f)); ab += 8; }
@@ -2277,10 +2388,10 @@ __device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, u
             }
         }
     }
-    if (identity < 256 && verdict < 0) {               // identity_is_reserved -> lpm4_egress_lookup
-        const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr4e);
-        if (tr.root_bits) ab += 9;
-        verdict = trie_lookup(tr, &daddr) ? 0 : D_POLICY_CIDR;
+    if (identity < 256 && verdict < 0) {               // identity_is_reserved -> lpm{4,6}_egress_lookup
+        const gf_trie_desc tr = gload<gf_trie_desc>(v6 ? &c->cidr6e : &c->cidr4e);
+        if (tr.root_bits) ab += v6 ? 21 : 9;
+        verdict = trie_lookup(tr, da) ? 0 : D_POLICY_CIDR;
     }
     return verdict;
 }
@@ -2332,7 +2443,7 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf
     }
     o.eg_ct_ret = (uint8_t)ret;
     const uint32_t dst_id = ((r.orig_dip & E.cluster_mask) == E.cluster_range) ? 3u : 2u;   // CLUSTER_ID / WORLD_ID
-    const int verdict = eg_policy(c, flags, dst_id, t[1], t[2] & 0xffffu, nh, len, ab);
+    const int verdict = eg_policy(c, flags, dst_id, &t[1], false, t[2] & 0xffffu, nh, len, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ab += 14;
@@ -2468,12 +2579,192 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf
     return TC_OK;
 }
 
+// ipv6_l3 (bpf/lib/l3.h:31-52) + ipv6_dec_hoplimit (bpf/lib/ipv6.h:178-193); smac may
+// be null.  ND_ICMP6_TE: the hop limit ran out (icmp6_send_time_exceeded).
+__device__ __forceinline__ int eg_ipv6_l3(Row &w, const uint32_t *smac, const uint32_t *dmac) {
+    const uint32_t hl = w.b(21);
+    if (hl <= 1) return ND_ICMP6_TE;
+    w.w8(21, hl - 1);
+    if (smac) { w.w32(6, smac[0]); w.w16(10, smac[1] & 0xffffu); }
+    w.w32(0, dmac[0]); w.w16(4, dmac[1] & 0xffffu);
+    return TC_OK;
+}
+
+// The CT / policy part of ipv6_l3_from_lxc (bpf_lxc.c:186-386) for packet i, on
+// the frame in HBM (extension headers may put the L4 header anywhere in the snap).
+__device__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
+                           uint32_t &lxc, int *added, uint32_t &ab) {
+    const uint32_t len = r.len, nh = r.nh;
+    const int l4_off = r.l4_off;
+    const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
+    const uint32_t flags = gload<uint32_t>(&c->flags);
+    const uint32_t co = csum_l4_offset(nh), fl = nh == 17 ? GF_F_MANGLED_0 : 0u;
+    gf_rec hr{};
+    hr.len = len; hr.l4_off = (int16_t)l4_off;
+    for (int k = 0; k < 4; k++) { const int64_t off = (int64_t)l4_off + k; if (off >= 0 && off < (int64_t)len) hr.l4w0 |= w.b((uint32_t)off) << (8 * k); }
+    {
+        uint32_t w3 = 0;
+        for (int k = 0; k < 2; k++) { const int64_t off = (int64_t)l4_off + 12 + k; if (off >= 0 && off < (int64_t)len) w3 |= w.b((uint32_t)off) << (8 * k); }
+        hr.l4w3 = (uint16_t)w3;
+    }
+    uint32_t t[10];
+    for (int k = 0; k < 4; k++) { t[k] = w.r32(38 + 4 * k); t[4 + k] = w.r32(22 + 4 * k); }
+    const uint32_t od[4] = {t[0], t[1], t[2], t[3]};   // orig_dip (after lb6_local)
+    t[8] = 0; t[9] = nh;
+    uint32_t tfl = 1u;                                  // TUPLE_F_IN (egress)
+    int action; bool syn;
+    int e = ct_l4(nh, true, hr, t[8], tfl, action, syn);
+    if (e < 0) return e;
+    t[9] = nh | (tfl << 8);
+    if (!(flags & GF_LXC_DEV_HAS_CT6)) return D_CT_CREATE_FAILED;
+    const gf_htab_desc &ct = E.ct6;
+    const bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
+    uint32_t tf[10];
+    for (int k = 0; k < 4; k++) { tf[k] = t[4 + k]; tf[4 + k] = t[k]; }
+    tf[8] = (t[8] >> 16) | (t[8] << 16);
+    tf[9] = nh | ((tfl ^ 1u) << 8);
+    bool isb = false;
+    const int64_t f = ht_find2<40, GF_CT6_U>(ct, t, tf, key_hash<40, GF_HASH_CT>(t), &isb);
+    ab += 40;
+    CtState st{0, 0, 0};
+    int ret;
+    if (f >= 0 && !isb) {
+        ab += 96;
+        ct_hit_eg(ct, f, action, syn, len, E.now, acct, st);
+        ret = (tfl & 2u) ? CT_RELATED : CT_REPLY;
+    } else {
+        ab += 40;
+        for (int k = 0; k < 10; k++) t[k] = tf[k];
+        tfl ^= 1u;
+        if (f >= 0) { ab += 96; ct_hit_eg(ct, f, action, syn, len, E.now, acct, st); ret = CT_ESTABLISHED; }
+        else ret = CT_NEW;
+    }
+    o.eg_ct_ret = (uint8_t)ret;
+    const uint32_t dst_id = (w.r32(38) == E.router6[0] && w.r32(42) == E.router6[1]) ? 3u : 2u;
+    const int verdict = eg_policy(c, flags, dst_id, &t[4], true, t[8] & 0xffffu, nh, len, ab);
+    const bool strict = (E.strict & 2) != 0;
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) {
+            ab += 40;
+            ht_delete<40, GF_HASH_CT, GF_CT6_U>(ct, t, strict, added);
+            o.eg_flags |= GF_EG_F_DELETED;
+        }
+        return verdict;
+    }
+    if (ret == CT_NEW) {                                // ct_create6(CT_EGRESS), conntrack.h:446-493
+        ab += 2 * (40 + 48);
+        const uint32_t efl = (nh == 6) ? 0u : F_SEEN_NON_SYN;
+        const uint32_t life = E.now + ((efl & F_SEEN_NON_SYN) ? 43200u : 300u);
+        uint32_t v[12] = {life, efl | ((uint32_t)r.rev_nat << 16), 0u, 0u, 0u, 0u, 1u, 0u, len, 0u, 0u,
+                          gload<uint32_t>(&c->seclabel)};
+        if (ht_upsert<40, 12, GF_HASH_CT, GF_CT6_U>(ct, t, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+        uint32_t it[10];
+        for (int k = 0; k < 8; k++) it[k] = t[k];
+        it[8] = 0;
+        it[9] = 58u | ((((t[9] >> 8) & 0xffu) | 2u) << 8);
+        v[1] |= F_SEEN_NON_SYN;
+        if (ht_upsert<40, 12, GF_HASH_CT, GF_CT6_U>(ct, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+        o.eg_flags |= GF_EG_F_CREATED;
+    } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(flags 0)
+        const gf_htab_desc rn = gload<gf_htab_desc>(&c->revnat6);
+        uint32_t kw[1] = {st.rev_nat};
+        const int64_t fr_ = ht_find<2>(rn, kw, key_hash<2>(kw));
+        ab += 20;
+        if (fr_ >= 0) {
+            const uint8_t *nat = ht_val(rn, fr_);
+            const uint32_t port = gload<uint16_t>(nat + 16);
+            if (port) {
+                if (nh == 6 || nh == 17) {
+                    if (!skb_ok(l4_off, 2, len)) return -GF_EFAULT;
+                    const uint32_t old = w.r16((uint32_t)l4_off);
+                    if (port != old) {
+                        if (l4_csum(w, len, l4_off + (int)co, old, port, 2u | fl) < 0) return D_CSUM_L4;
+                        if (!skb_ok(l4_off, 2, len)) return D_WRITE_ERROR;
+                        w.w16((uint32_t)l4_off, port);
+                    }
+                } else if (nh != 1 && nh != 58) return D_UNKNOWN_L4;
+            }
+            uint32_t sum = 0;
+            for (int k = 0; k < 4; k++) {
+                const uint32_t os = w.r32(22 + 4 * k), nw = gload<uint32_t>(nat + 4 * k);
+                w.w32(22 + 4 * k, nw);
+                sum = ck_add(ck_add(sum, ~os), nw);
+            }
+            if (l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl) < 0) return D_CSUM_L4;
+        }
+        o.eg_flags |= GF_EG_F_REVNAT;
+    }
+    uint32_t nm[2] = {gload<uint32_t>(&c->node_mac[0]), gload<uint32_t>(&c->node_mac[1])};
+    if (verdict > 0) {                                  // ipv6_redirect_to_host_port + ipv6_l3 -> HOST_IFINDEX
+        const int r3 = redirect_checks(len, l4_off, nh);
+        if (r3 < 0) return r3;
+        const uint32_t np = (uint32_t)verdict & 0xffffu;
+        l4_csum(w, len, l4_off + (int)co, t[8] & 0xffffu, np, 2u | fl);   // l4_modify_port
+        w.w16((uint32_t)(l4_off + 2), np);
+        uint32_t sum = 0;
+        for (int k = 0; k < 4; k++) { w.w32(38 + 4 * k, E.host6[k]); sum = ck_add(ck_add(sum, ~od[k]), E.host6[k]); }
+        if (co) l4_csum(w, len, l4_off + (int)co, 0, sum, GF_F_PSEUDO_HDR | fl);
+        pol_redirect(E.X, i, len, l4_off, nh, t, true, np, od, gload<uint32_t>(&c->seclabel), 1u);
+        o.eg_flags |= GF_EG_F_PROXY;
+        o.proxy_port = (uint16_t)verdict;
+        const int r4 = eg_ipv6_l3(w, nm, E.host_mac);
+        if (r4 != TC_OK) return r4;
+        ifx = E.host_ifindex;
+        return TC_REDIRECT;
+    }
+    uint32_t d6[4];
+    for (int k = 0; k < 4; k++) d6[k] = w.r32(38 + 4 * k);
+    if (E.lxc.slots) {                                  // lookup_ip6_endpoint
+        uint32_t kw[5] = {d6[0], d6[1], d6[2], d6[3], 2u};
+        const int64_t fe = ht_find<20>(E.lxc, kw, key_hash<20>(kw));
+        ab += 20;
+        if (fe >= 0) {
+            const uint8_t *ep = ht_val(E.lxc, fe);
+            ab += 8;
+            if (gload<uint32_t>(ep + 8) & 1u) {         // ENDPOINT_F_HOST -> to_host
+                if (!E.host_ifindex) return D_NO_LXC;
+                const int r4 = eg_ipv6_l3(w, nm, E.host_mac);
+                if (r4 != TC_OK) return r4;
+                o.eg_flags |= GF_EG_F_TO_HOST;
+                ifx = E.host_ifindex;
+                return TC_REDIRECT;
+            }
+            uint32_t emac[2] = {gload<uint32_t>(ep + 16), gload<uint32_t>(ep + 20)};
+            uint32_t rmac[2] = {gload<uint32_t>(ep + 24), gload<uint32_t>(ep + 28)};
+            const int r4 = eg_ipv6_l3(w, rmac, emac);   // ipv6_local_delivery (l3.h:106-134)
+            if (r4 != TC_OK) return r4;
+            o.eg_flags |= GF_EG_F_LOCAL;
+            uint32_t mapped = 0, ndport = 0;
+            return delivery_tail(w, len, l4_off, nh, ep, ifx, lxc, mapped, ndport, ab);
+        }
+    }
+    if (E.encap_ifindex && E.tunnel.slots) {            // encap_and_redirect, key daddr/96
+        uint32_t kw[5] = {d6[0], d6[1], d6[2], 0u, 2u};
+        const int64_t ft = ht_find<20>(E.tunnel, kw, key_hash<20>(kw));
+        ab += 20;
+        if (ft >= 0) {
+            o.tunnel_ip = __builtin_bswap32(gload<uint32_t>(ht_val(E.tunnel, ft)));
+            o.eg_flags |= GF_EG_F_ENCAP;
+            ifx = E.encap_ifindex;
+            return TC_REDIRECT;
+        }
+    }
+    const int r4 = eg_ipv6_l3(w, nullptr, nm);         // pass_to_stack
+    if (r4 != TC_OK) return r4;
+    {                                                   // ipv6_store_flowlabel(SECLABEL_NB), ipv6.h:245-260
+        const uint32_t old = w.r32(14) & __builtin_bswap32(0x0FF00000u);
+        w.w32(14, __builtin_bswap32(0x60000000u) | __builtin_bswap32(gload<uint32_t>(&c->seclabel)) | old);
+    }
+    o.eg_flags |= GF_EG_F_TO_STACK;
+    return TC_OK;
+}
+
 // One bucket per lane from the longest-first queue (the ingress schedule), in
 // batch order.  Writes each packet's verdict, and for local deliveries the
 // handle_policy record + flow-group key of the ingress pass (rec2 / key2).
 __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
-                                                     uint32_t *ct_count, unsigned long long *stats) {
+                                                     uint32_t *ct_count, uint32_t *ct_count6, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     __shared__ uint4 lds[BLOCK * (GF_EG_STAGE / 16)];
@@ -2485,7 +2776,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
     const uint32_t nb = GF_SCHED_NFAM(sched)[0], lane = threadIdx.x & 63u;
     uint32_t *queue = GF_SCHED_QUEUE(sched);
     const bool seq = *E.seq != 0;
-    int added = 0;
+    int added = 0, added6 = 0;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -2508,25 +2799,38 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
             o.slave = r.slave; o.rev_nat = r.rev_nat; o.eg_flags = r.eflags;
             uint32_t ifx = 0, lxc = 0, ab = 24 + 34 + 32;
             uint8_t *g = E.snap + (size_t)i * E.stride;
-            eg_copy(row, g, K);
-            Row w{row, K < r.len ? K : r.len};
-            const int ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, ab);
-            eg_copy(g, row, K);
+            const bool v6 = (r.eflags & GF_EG_F_IPV6) != 0;
+            Row w = v6 ? Row{g, E.stride < r.len ? E.stride : r.len} : Row{row, K < r.len ? K : r.len};
+            int ret;
+            if (v6) ret = eg_ct_part6(E, r, i, w, o, ifx, lxc, &added6, ab);
+            else {
+                eg_copy(row, g, K);
+                ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, ab);
+                eg_copy(g, row, K);
+            }
             o.ct_ret = o.eg_ct_ret;
+            if (ret == ND_ICMP6_TE) {                   // ipv6_l3 -> icmp6_send_time_exceeded: the reply goes out
+                ret = TC_REDIRECT; ifx = 0;
+                o.eg_flags |= GF_EG_F_ICMP6_TE;
+            }
             if (ret == ND_TAILCALL) {                   // handle_policy of the destination, next pass
                 o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; o.ct_ret = 0;
                 PktHdr h2;
                 parse_row(w.p, w.cap, r.len, h2);
                 const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
                 key2[i] = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
-                                   gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, false,
+                                   gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, true,
                                    h2.s6, h2.d6, rr);
+                if (v6) {
+                    reinterpret_cast<uint4 *>(E.s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
+                    reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
+                }
                 if (stats) st.add_n(270, ab);
             } else {
                 if (ret < 0 || ret == TC_SHOT) {
                     o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
                     o.eg_flags &= (GF_EG_F_CREATED | GF_EG_F_DELETED | GF_EG_F_LB | GF_EG_F_LOOPBACK | GF_EG_F_PORTMAP |
-                                   GF_EG_F_REVNAT);
+                                   GF_EG_F_REVNAT | GF_EG_F_IPV6);
                     o.proxy_port = 0; o.tunnel_ip = 0;
                 } else {
                     o.action = (uint8_t)ret;
@@ -2543,6 +2847,14 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
         if (added) atomicAdd(&sadd, (uint32_t)added);
         __syncthreads();
         if (threadIdx.x == 0 && sadd && ct_count) atomicAdd(ct_count, sadd);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sadd = 0;
+    __syncthreads();
+    if (!(E.strict & 2)) {
+        if (added6) atomicAdd(&sadd, (uint32_t)added6);
+        __syncthreads();
+        if (threadIdx.x == 0 && sadd && ct_count6) atomicAdd(ct_count6, sadd);
     }
     if (stats) st.flush(stats);
 }
@@ -2775,7 +3087,8 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         {cfg->cidr6_ingress_map, 20, 0, true, &p->cidr6}, {cfg->revnat4_map, 2, 6, false, &p->revnat4},
         {cfg->revnat6_map, 2, 18, false, &p->revnat6},
         {cfg->lb4_services, 8, 12, false, &p->lb4},      {cfg->ipcache_map, 20, 8, false, &p->ipcache},
-        {cfg->cidr4_egress_map, 8, 0, true, &p->cidr4e},
+        {cfg->cidr4_egress_map, 8, 0, true, &p->cidr4e}, {cfg->lb6_services, 20, 24, false, &p->lb6},
+        {cfg->cidr6_egress_map, 20, 0, true, &p->cidr6e},
     };
     for (auto &b : binds) {
         if (!b.h) continue;
@@ -3024,7 +3337,7 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
     for (size_t k = 0; k < progs.size(); k++) {
         auto &p = progs[k];
         for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6, p->lb4, p->ipcache,
-                       p->cidr4e})
+                       p->cidr4e, p->lb6, p->cidr6e})
             if ((r = push_map(m, s))) return r;
         gf_lxc_dev &d = cfgs[k];
         memset(&d, 0, sizeof d);
@@ -3055,6 +3368,9 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
         if (p->lb4) d.lb4 = p->lb4->hdesc();
         if (p->ipcache) d.ipcache = p->ipcache->hdesc();
         if (p->cidr4e) d.cidr4e = p->cidr4e->tdesc();
+        memcpy(d.lxc_ip6, p->cfg.lxc_ip6, 16);
+        if (p->lb6) d.lb6 = p->lb6->hdesc();
+        if (p->cidr6e) d.cidr6e = p->cidr6e->tdesc();
     }
     size_t cb = cfgs.size() * sizeof(gf_lxc_dev);
     bool changed = a->dirty || a->h_cfgs.size() != cb || a->h_slot_of.size() != slot_of.size() ||
@@ -3421,7 +3737,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
 
 // ---- endpoint egress (from-container) ----
 namespace {
-struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp; };
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6; };
 EgWs &eg_ws() { static EgWs w; return w; }
 }  // namespace
 
@@ -3442,20 +3758,23 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     int r;
     std::vector<std::shared_ptr<ProgLxc>> progs;
     if ((r = prog_table(a, s, progs))) return r;
-    std::shared_ptr<Map> ct4m;
+    std::shared_ptr<Map> ct4m, ct6m;
     for (auto &p : progs) {
         if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
+        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
     }
+    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
     uint32_t strict = 0;
-    gf_htab_desc cfg_ct4{}, unused6{};
-    if ((r = ct_limits(ct4m, nullptr, n, 3, s, strict, cfg_ct4, unused6))) return r;
+    gf_htab_desc cfg_ct4{}, cfg_ct6{};
+    if ((r = ct_limits(ct4m, ct6m, n, 3, s, strict, cfg_ct4, cfg_ct6))) return r;
     auto lxc = node_map(1), tun = node_map(2);
     if ((r = push_map(lxc, s)) || (r = push_map(tun, s))) return r;
     EgWs &ew = eg_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
         (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 4)) || (r = grow(ew.ctlog_n, 4)) ||
-        (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = ws_grow(n)))
+        (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 16)) ||
+        (r = grow(ew.d6, (size_t)n * 16)) || (r = ws_grow(n)))
         return r;
     uint8_t *wsnap = snap_out;
     if (!wsnap) {
@@ -3466,7 +3785,9 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     EgDev E{};
     E.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
     E.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
-    E.ct4 = cfg_ct4;
+    E.ct4 = cfg_ct4; E.ct6 = cfg_ct6;
+    E.s6out = (uint8_t *)ew.s6.p; E.d6out = (uint8_t *)ew.d6.p;
+    memcpy(E.router6, node.router_ip6, 16); memcpy(E.host6, node.host_ip6, 16);
     if (lxc) E.lxc = lxc->hdesc();
     if (tun) E.tunnel = tun->hdesc();
     E.snap = wsnap; E.stride = S; E.now = now_sec; E.host_ifindex = host_ifindex();
@@ -3499,7 +3820,8 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
         ProfScope ps("k_eg_groups", s);
         hipLaunchKernelGGL(k_eg_groups, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p, (const uint2 *)w.order.p,
                            (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out, (gf_rec *)ew.rec2.p,
-                           (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, sink);
+                           (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr,
+                           ct6m ? (uint32_t *)ct6m->d_count.p : nullptr, sink);
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     // ct_create4's deferred service entries, in batch order
@@ -3529,13 +3851,15 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
         if ((r = hip_ok(hipGetLastError(), "k_ctlog_apply"))) return r;
     }
     if (ct4m) ct4m->device_modified();
-    // the egress redirects' cilium_proxy4 updates, in batch order
+    if (ct6m) ct6m->device_modified();
+    // the egress redirects' cilium_proxy{4,6} updates, in batch order
     if ((r = px_log_apply(E.X, s, wsnap, fr.len, S, (uint8_t *)out, true))) return r;
     // handle_policy of the local deliveries (the tail calls of ipv4_local_delivery)
     gf_pkt_cols c2{};
     c2.n = n;
     c2.len = fr.len;
     c2.flow_hash = b->flow_hash;
+    c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p;   // IPv6 deliveries' addresses
     auto pack = [&](const uint16_t *, gf_rec *rec, uint32_t *keys) -> int {
         if (hip_ok(hipMemcpyAsync(rec, ew.rec2.p, (size_t)n * sizeof(gf_rec), hipMemcpyDeviceToDevice, s), "rec2") ||
             hip_ok(hipMemcpyAsync(keys, ew.key2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))

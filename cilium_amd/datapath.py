@@ -41,6 +41,8 @@ def egress_fields(c, e, h):
     c.node_mac[:] = list(e.get("node_mac", bytes(6)))
     c.lxc_ipv4 = e.get("lxc_ipv4", 0)
     c.lb4_services, c.ipcache_map, c.cidr4_egress_map = h(e.get("lb4")), h(e.get("ipcache")), h(e.get("cidr4e"))
+    c.lb6_services, c.cidr6_egress_map = h(e.get("lb6")), h(e.get("cidr6e"))
+    c.lxc_ip6[:] = list(e.get("lxc_ip6", bytes(16)))
     pm = e.get("portmap") or []
     c.n_portmap = len(pm)
     for i, (frm, to) in enumerate(pm):
@@ -158,7 +160,8 @@ class Datapath:
                            (C.c_uint8 * 16)(*nd.get("host_ip6", bytes(16))), (C.c_uint8 * 6)(*nd.get("host_mac", bytes(6))),
                            (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))), h(nd.get("lxc_map")),
                            nd.get("ipv4_cluster_range", 0), nd.get("ipv4_cluster_mask", 0), nd.get("ipv4_loopback", 0),
-                           nd.get("ipv4_mask", 0), nd.get("encap_ifindex", 0), h(nd.get("tunnel_map")))
+                           nd.get("ipv4_mask", 0), nd.get("encap_ifindex", 0), h(nd.get("tunnel_map")),
+                           (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
         _check(lib.gf_node_config(C.byref(ncfg)), "gf_node_config")
         self.xdp_prog = self.lb_prog = self.policy_array = None
         if sc.xdp:

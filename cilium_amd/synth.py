@@ -677,6 +677,7 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
                 sid=ids[rng.integers(0, len(ids), npool)])
     pool["pr"][:40] = np.where(rng.random(40) < 0.6, TCP, UDP)
     sc.meta["pool"] = pool
+    sc.meta.update(ep6=ep6, rem6=rem6)
 
     # ---- XDP maps
     pl = np.array([24, 30, 16, 31, 8, 28, 25], np.uint32)
@@ -1050,7 +1051,28 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
             cn = np.array([ip4("100.64.0.0"), rem4[12] & 0xFFFFFF00, rem4[20]], np.uint32)
             ck, cv = lpm_dedup(lpm4_keys(cp[: 1 + e % 3], cn[: 1 + e % 3]), np.ones((1 + e % 3, 1), np.uint8), 32)
             sc.add_map(MapSpec(f"cidr4e_{e}", LPM, 8, 1, 1024, NO_PREALLOC, ck, cv))
+    ep6, rem6 = sc.meta["ep6"], sc.meta["rem6"]
+    vip6 = np.unique(sc.maps["lb6_svc"].keys[:, :16], axis=0)
+    router6 = bytes([0x20, 0x01, 0x0d, 0xb8, 0xaa, 0xbb, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1])
+    for e in range(n_ep):
+        if e % 2 == 1:
+            ck6, cv6 = lpm_dedup(lpm6_keys(np.array([32, 128]), rem6[[0, 5 + e % 8]]), np.ones((2, 1), np.uint8), 128)
+            sc.add_map(MapSpec(f"cidr6e_{e}", LPM, 20, 1, 1024, NO_PREALLOC, ck6, cv6))
+    ic6 = np.concatenate([rem6[:5], ep6[:3]])
+    icv6 = np.zeros((len(ic6), 8), np.uint8)
+    icv6[:, 0:2] = le_bytes(np.concatenate([rng.integers(256, 280, 4), [2], 256 + np.arange(3)]), "<u2")
+    ipc = sc.maps["cilium_ipcache"]
+    ipc.keys, ipc.vals = dedup(np.concatenate([ipc.keys, endpoint_keys6(ic6)]), np.concatenate([ipc.vals, icv6]))
+    tk6 = np.zeros((1, 20), np.uint8)
+    tk6[0, :12] = rem6[7][:12]
+    tk6[0, 16] = 2
+    tm = sc.maps["cilium_tunnel_map"]
+    tm.keys, tm.vals = np.concatenate([tm.keys, tk6]), np.concatenate([tm.vals, endpoint_keys4(np.array([ip4("192.168.7.9")], np.uint32))])
     for e, cfg in enumerate(sc.lxc):
+        cfg["lxc_ip6"] = bytes(ep6[e])
+        cfg["lb6"] = "lb6_svc" if e != 9 else None
+        if e % 2 == 1 and e % 4 in (1, 2):
+            cfg["cidr6e"] = f"cidr6e_{e}"
         cfg["lxc_mac"] = bytes(macs[e])
         cfg["node_mac"] = node_mac if e != 7 else bytes(6)
         cfg["lxc_ipv4"] = int(be32_bytes([ep4[e]]).view("<u4")[0, 0])
@@ -1066,7 +1088,7 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
     raw_be = lambda a: int(be32_bytes([a]).view("<u4")[0, 0])
     sc.node = dict(sc.node, lxc_map="cilium_lxc", ipv4_cluster_range=raw_be(ip4("10.0.0.0")),
                    ipv4_cluster_mask=raw_be(0xFF000000), ipv4_loopback=raw_be(ip4("10.255.255.245")),
-                   ipv4_mask=raw_be(0xFFFF0000), encap_ifindex=5, tunnel_map="cilium_tunnel_map")
+                   ipv4_mask=raw_be(0xFFFF0000), encap_ifindex=5, tunnel_map="cilium_tunnel_map", router_ip6=router6)
     # CT entries the egress path meets as replies / related (rev-NAT, loopback) and as established flows
     ct = sc.maps["ct4"]
     npre = 48
@@ -1134,11 +1156,41 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
         f[rows, off[ok]] = (ck[ok] >> 8).astype(np.uint8)
         f[rows, off[ok] + 1] = (ck[ok] & 0xff).astype(np.uint8)
         oth = rng.random(n)
-        i6 = np.nonzero(oth < 0.02)[0]
-        f[i6, 12], f[i6, 13] = 0x86, 0xdd
-        ia = np.nonzero((oth >= 0.02) & (oth < 0.04))[0]
+        i6 = np.nonzero(oth < 0.18)[0]                 # IPv6 from the endpoints (ipv6_l3_from_lxc)
+        m = len(i6)
+        if m:
+            e6 = e[i6]
+            k6 = rng.random(m)
+            peer6 = ep6[(e6 + 1 + rng.integers(0, n_ep - 1, m)) % n_ep] if not hazard else ep6[rng.integers(0, n_ep, m)]
+            rtr = np.frombuffer(router6, np.uint8)
+            clus = np.tile(rtr, (m, 1)); clus[:, 8:] = rng.integers(0, 256, (m, 8))
+            tun6 = np.tile(rem6[7], (m, 1)); tun6[:, 12:] = rng.integers(0, 256, (m, 4))
+            d6 = np.where((k6 < 0.25)[:, None], vip6[rng.integers(0, len(vip6), m)],
+                          np.where((k6 < 0.45)[:, None], peer6,
+                                   np.where((k6 < 0.75)[:, None], rem6[rng.integers(0, len(rem6), m)],
+                                            np.where((k6 < 0.85)[:, None], clus,
+                                                     np.where((k6 < 0.92)[:, None], tun6, np.tile(rtr, (m, 1)))))))
+            s6 = ep6[e6].copy()
+            bad6 = rng.random(m) < 0.03
+            s6[bad6] = rem6[rng.integers(0, len(rem6), int(bad6.sum()))]
+            nh6 = rng.choice(np.array([TCP, TCP, UDP, ICMPV6, ICMPV6, 47], np.uint8), m)
+            it6 = rng.choice(np.array([128, 129, 135, 1, 3, 2, 136], np.uint8), m)
+            ext = []
+            depth = np.where(rng.random(m) < 0.15, rng.integers(1, 6, m), 0)
+            for lvl in range(5):
+                t = rng.choice(np.array([0, 60, 43, 51, 44, 59, 0], np.uint8), m)
+                ext.append((np.where(depth > lvl, t, 255).astype(np.uint8), rng.integers(0, 3, m).astype(np.uint8)))
+            f6, l6 = frames_v6(m, 256, s6, d6, nh6, sp[i6], dp[i6], tf[i6], it6, ext=ext, payload=rng.integers(0, 64, m))
+            f6[:, 6:12] = macs[e6]
+            f6[:, 0:6] = np.frombuffer(node_mac, np.uint8)
+            f6[rng.random(m) < 0.02, 6] ^= 1
+            f6[:, 21] = np.where(rng.random(m) < 0.05, rng.integers(0, 2, m), rng.integers(2, 256, m))
+            ok6 = (nh6 == 6) | (nh6 == 17)
+            f[i6] = f6
+            lens[i6] = l6
+        ia = np.nonzero((oth >= 0.18) & (oth < 0.20))[0]
         f[ia, 12], f[ia, 13] = 0x08, 0x06
-        io = np.nonzero((oth >= 0.04) & (oth < 0.05))[0]
+        io = np.nonzero((oth >= 0.20) & (oth < 0.21))[0]
         f[io, 12], f[io, 13] = 0x88, 0xcc
         lens = lens.astype(np.int64)
         tr = rng.random(n) < 0.06

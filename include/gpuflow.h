@@ -265,6 +265,9 @@ typedef struct gf_lxc_cfg {
     gf_portmap portmap[GF_MAX_PORTMAP];
     uint32_t n_l4_egress;      /* CFG_L3L4_EGRESS entries (l4_egress_proxy_lookup) */
     gf_l4_allow l4_egress[GF_MAX_L4_INGRESS];
+    uint8_t  lxc_ip6[16];      /* LXC_IP (is_valid_lxc_src_ip) */
+    int lb6_services;          /* cilium_lb6_services (lb6_lookup_service / lb6_local), 0 = none */
+    int cidr6_egress_map;      /* CIDR6_EGRESS_MAP (LPM_TRIE), 0 = undefined (deny) */
 } gf_lxc_cfg;
 int gf_lxc_prog_load(const gf_lxc_cfg *cfg);
 
@@ -288,6 +291,7 @@ typedef struct gf_node_cfg {   /* node_config.h values used on the path */
     uint32_t ipv4_mask;        /* IPV4_MASK (raw be32), the tunnel map key of encap_and_redirect */
     uint32_t encap_ifindex;    /* ENCAP_IFINDEX, 0 = undefined (no tunnel) */
     int      tunnel_map;       /* cilium_tunnel_map (endpoint_key 20 B -> endpoint_key 20 B) */
+    uint8_t  router_ip6[16];   /* ROUTER_IP (the IPv6 egress path's CLUSTER_ID test) */
 } gf_node_cfg;
 int gf_node_config(const gf_node_cfg *cfg);
 
@@ -318,14 +322,15 @@ int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
  * destination's handle_policy (tail call into cilium_policy) in a second pass
  * over the batch, as gf_pipeline_classify does: every from-container effect
  * of the batch (CT, proxy map) precedes every handle_policy effect of its
- * deliveries.  IPv6 and ARP frames (the ICMPv6/ARP responders)
- * are reported as stage GF_STAGE_NONE, not classified. */
+ * deliveries.  IPv6 frames run tail_handle_ipv6 -> ipv6_l3_from_lxc
+ * (:120-416).  Frames for the ARP / ICMPv6 responders (tail_handle_arp,
+ * icmp6_handle's NS and echo-to-router) are reported as stage GF_STAGE_NONE. */
 typedef struct gf_lxc_batch {
     gf_frames frames;          /* DEVICE frames (snap_stride >= every header byte touched, <= 256) */
     const uint16_t *lxc_id;    /* DEVICE: the sending endpoint (whose from-container program runs) */
     const uint32_t *flow_hash; /* DEVICE get_hash_recalc(skb) (lb4_select_slave), may be NULL */
 } gf_lxc_batch;
-#define GF_STAGE_NONE     0    /* not classified: IPv6 / ARP from a container (responders) */
+#define GF_STAGE_NONE     0    /* not classified: ARP / ICMPv6 responders */
 #define GF_STAGE_FROM_LXC 5    /* the from-container verdict is final */
 /* GF_STAGE_POLICY (4): delivered locally, handle_policy of endpoint lxc_id */
 #define GF_EG_F_CREATED   0x0001  /* ct_create4(CT_EGRESS) */
@@ -340,7 +345,10 @@ typedef struct gf_lxc_batch {
 #define GF_EG_F_LOCAL     0x0200  /* ipv4_local_delivery (stage GF_STAGE_POLICY) */
 #define GF_EG_F_DELETED   0x0400  /* ct_delete4 of an ESTABLISHED flow the policy now denies */
 #define GF_EG_F_ARP       0x0800  /* stage NONE: ARP (tail_handle_arp, the responder) */
-#define GF_EG_F_IPV6      0x1000  /* stage NONE: IPv6 (tail_handle_ipv6) */
+#define GF_EG_F_IPV6      0x1000  /* the IPv6 path (ipv6_l3_from_lxc) */
+#define GF_EG_F_ICMP6_TE  0x2000  /* hop limit reached in ipv6_l3: icmp6_send_time_exceeded (action
+                                     REDIRECT; the reply itself is not built) */
+#define GF_EG_F_RESPONDER 0x4000  /* stage NONE: icmp6_handle's NS / echo-to-router responders */
 typedef struct gf_egress_out {   /* 24 B; bytes 0-9 as gf_pipeline_out */
     uint8_t  stage;       /* GF_STAGE_FROM_LXC / GF_STAGE_POLICY / GF_STAGE_NONE */
     uint8_t  action;      /* final TC_ACT_* */

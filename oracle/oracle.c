@@ -1038,7 +1038,7 @@ static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t next
     return 0;                                          /* cilium_proxy{4,6} update: §8(f) */
 }
 
-static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0, 0, 0, 0, NULL};   /* bpf/node_config.h */
+static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0, 0, 0, 0, NULL, {0}};   /* bpf/node_config.h */
 #define g_host_ifindex (g_node.host_ifindex)
 void o_set_node(const o_node_cfg *node) { g_node = *node; }
 
@@ -2018,6 +2018,223 @@ to_host:
     return TC_ACT_REDIRECT;
 }
 
+#define EG_F_ICMP6_TE 0x2000
+#define EG_F_RESPONDER 0x4000
+#define O_EG_RESPONDER 1001
+#define O_EG_ICMP6_TE 1002
+
+/* ipv6_l3 (bpf/lib/l3.h:31-52) + ipv6_dec_hoplimit (bpf/lib/ipv6.h:178-193) */
+static int ipv6_l3(const skb_t *s, uint8_t *w, const uint8_t *smac, const uint8_t *dmac) {
+    uint8_t hl = skb_byte(s, ETH_HLEN + 7);
+    if (hl <= 1) return O_EG_ICMP6_TE;                 /* icmp6_send_time_exceeded (a responder) */
+    uint8_t nh = (uint8_t)(hl - 1);
+    if (skb_store_bytes(s, w, ETH_HLEN + 7, &nh, 1) < 0) return DROP_WRITE_ERROR;
+    if (smac && skb_store_bytes(s, w, 6, smac, 6) < 0) return DROP_WRITE_ERROR;
+    if (skb_store_bytes(s, w, 0, dmac, 6) < 0) return DROP_WRITE_ERROR;
+    return TC_ACT_OK;
+}
+
+/* policy_can_egress6 (bpf/lib/policy.h:214-239 with POLICY_EGRESS, else :268-278) */
+static int policy_can_egress6(const o_lxc_cfg *c, const skb_t *s, const uint8_t *t, uint16_t dst_id,
+                              const uint8_t *daddr) {
+    if (c->flags & LXC_F_DROP_ALL) return DROP_POLICY;
+    if (!(c->flags & LXC_F_POLICY_EGRESS)) return TC_ACT_OK;
+    uint16_t identity = dst_id;
+    if (c->ipcache_map) {
+        uint8_t k[20] = {0}; memcpy(k, daddr, 16); k[16] = 2;
+        const uint8_t *info = om_lookup_ptr(c->ipcache_map, k);
+        if (info) identity = ge16(info, 0);
+    }
+    int verdict = __policy_can_access_dir(c, s, identity, ge16(t, 32), t[36], CT_EGRESS);
+    if (verdict < 0) verdict = DROP_POLICY;
+    if (identity < 256 && verdict < 0) {
+        int hit = 0;
+        if (c->cidr6_egress_map) {
+            uint8_t k[20]; uint32_t pl = 128; memcpy(k, &pl, 4); memcpy(k + 4, daddr, 16);
+            hit = om_lookup_ptr(c->cidr6_egress_map, k) != NULL;
+        }
+        verdict = hit ? 0 : DROP_POLICY_CIDR;
+    }
+    return verdict;
+}
+
+/* handle_ipv6 (bpf_lxc.c:388-416) -> ipv6_l3_from_lxc (:120-386) */
+static int from_lxc_ipv6(const o_lxc_cfg *c, skb_t *s, uint8_t *w, uint32_t now, eg_res *r, uint8_t *plog,
+                         nd_res *nr) {
+    if (s->len < ETH_HLEN + 40) return DROP_INVALID;
+    uint8_t d6[16];
+    for (int k = 0; k < 16; k++) d6[k] = skb_byte(s, 38 + k);
+    if (skb_byte(s, 20) == IPPROTO_ICMPV6) {
+        if (s->len < ETH_HLEN + 40 + 8) return DROP_INVALID;
+        uint8_t type = skb_byte(s, ETH_HLEN + 40);              /* icmp6_handle, bpf/lib/icmp6.h:380-401 */
+        if (type == 135) return O_EG_RESPONDER;                   /* icmp6_handle_ns (tail call) */
+        if (type == 128 && !memcmp(d6, g_node.router_ip6, 16)) return O_EG_RESPONDER;   /* echo reply */
+    }
+    for (int k = 0; k < 6; k++) if (skb_byte(s, 6 + k) != c->lxc_mac[k]) return DROP_INVALID_SMAC;
+    for (int k = 0; k < 6; k++) if (skb_byte(s, k) != c->node_mac[k]) return DROP_INVALID_DMAC;
+    for (int k = 0; k < 16; k++) if (skb_byte(s, 22 + k) != c->lxc_ip6[k]) return DROP_INVALID_SIP;
+    uint8_t t[40]; memset(t, 0, sizeof t);
+    t[36] = skb_byte(s, 20);
+    memcpy(t, d6, 16);
+    for (int k = 0; k < 16; k++) t[16 + k] = skb_byte(s, 22 + k);
+    int l4_off = ETH_HLEN + ipv6_hdrlen(s, ETH_HLEN, &t[36]);    /* added unchecked (bpf_lxc.c:145) */
+    const uint8_t nh = t[36];
+    const uint16_t co = csum_l4_offset(nh);
+    const uint32_t fl = csum_l4_flags(nh);
+    ct_state_t sn; memset(&sn, 0, sizeof sn);
+    uint8_t key[20] = {0}; memcpy(key, t, 16);                   /* lb6_extract_key(CT_EGRESS) */
+    int ret = extract_l4_port(s, nh, l4_off, (uint16_t *)(key + 16));
+    if (IS_ERR(ret)) {
+        if (ret != DROP_UNKNOWN_L4) return ret;
+        goto skip_service_lookup;
+    }
+    if (c->lb6_services) {
+        o_lb_cfg lc; memset(&lc, 0, sizeof lc);
+        lc.lb6_services = c->lb6_services; lc.flags = LB_F_L3 | LB_F_L4;
+        uint8_t *svc = lb6_lookup_service(&lc, key);
+        if (svc) {                                               /* lb6_local, lb.h:425-445 */
+            uint16_t count = ge16(svc, 18);
+            uint16_t slave = (uint16_t)((s->hash % count) + 1);
+            se16(key, 18, slave);
+            const uint8_t *be = om_lookup_ptr(c->lb6_services, key);
+            if (!be) return DROP_NO_SERVICE;
+            r->slave = slave; r->eg_flags |= EG_F_LB;
+            memcpy(t, be, 16);                                   /* tuple->daddr = svc->target */
+            sn.rev_nat_index = ge16(be, 20); r->rev_nat = sn.rev_nat_index;
+            wbytes(s, w, 38, be, 16);                            /* lb6_xlate: ipv6_store_daddr */
+            uint32_t sum = ck_diff(key, be, 16);
+            if (l4_csum_replace(s, w, l4_off + co, 0, sum, BPF_F_PSEUDO_HDR | fl) < 0) return DROP_CSUM_L4;
+            uint16_t sp = ge16(be, 16), kd = ge16(key, 16);
+            if (sp && kd != sp && (nh == IPPROTO_TCP || nh == IPPROTO_UDP)) {
+                if (l4_csum_replace(s, w, l4_off + co, kd, sp, 2 | fl) < 0) return DROP_CSUM_L4;
+                if (skb_store_bytes(s, w, l4_off + 2, &sp, 2) < 0) return DROP_WRITE_ERROR;
+            }
+        }
+    }
+skip_service_lookup: ;
+    uint8_t orig_dip[16]; memcpy(orig_dip, t, 16);
+    if (c->n_portmap && (nh == IPPROTO_TCP || nh == IPPROTO_UDP)) {    /* map_lxc_out */
+        uint16_t sport;
+        if (skb_load_bytes(s, l4_off, &sport, 2) < 0) return DROP_INVALID;
+        for (uint32_t k = 0; k < c->n_portmap && k < 16; k++) {
+            if (c->portmap[k].to != sport) continue;
+            uint16_t from = c->portmap[k].from;
+            if (l4_csum_replace(s, w, l4_off + co, sport, from, 2 | fl) < 0) return DROP_CSUM_L4;
+            if (skb_store_bytes(s, w, l4_off, &from, 2) < 0) return DROP_WRITE_ERROR;
+            r->eg_flags |= EG_F_PORTMAP;
+        }
+    }
+    ct_state_t st; memset(&st, 0, sizeof st);
+    ret = ct_lookup(c->ct_map6, t, s, l4_off, CT_EGRESS, &st, 1, now, (c->flags & LXC_F_CT_ACCOUNTING) != 0);
+    if (ret < 0) return ret;
+    r->ct_ret = (uint8_t)ret;
+    for (int k = 0; k < 16; k++) d6[k] = skb_byte(s, 38 + k);
+    uint16_t dst_id = !memcmp(d6, g_node.router_ip6, 8) ? CLUSTER_ID : WORLD_ID;   /* ipv6_match_prefix_64 */
+    int verdict = policy_can_egress6(c, s, t, dst_id, t + 16);   /* ipv6_ct_tuple_get_daddr = &tuple->saddr */
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { om_delete(c->ct_map6, t); r->eg_flags |= EG_F_DELETED; }
+        return verdict;
+    }
+    switch (ret) {
+    case CT_NEW:
+        sn.src_sec_id = c->seclabel;
+        ret = ct_create(c->ct_map6, t, s, CT_EGRESS, &sn, 1, now);
+        if (IS_ERR(ret)) return ret;
+        r->eg_flags |= EG_F_CREATED;
+        break;
+    case CT_ESTABLISHED:
+        break;
+    case CT_RELATED: case CT_REPLY:
+        s->cb[2] = 1;
+        if (st.rev_nat_index) {                                 /* lb6_rev_nat(flags 0), lb.h:253-316 */
+            const uint8_t *nat = c->revnat6_map ? om_lookup_ptr(c->revnat6_map, &st.rev_nat_index) : NULL;
+            if (nat) {
+                uint16_t port = ge16(nat, 16);
+                if (port) {
+                    switch (nh) {
+                    case IPPROTO_TCP: case IPPROTO_UDP: {
+                        uint16_t old;
+                        int rr = skb_load_bytes(s, l4_off, &old, 2);
+                        if (IS_ERR(rr)) return rr;
+                        if (port != old) {
+                            if (l4_csum_replace(s, w, l4_off + co, old, port, 2 | fl) < 0) return DROP_CSUM_L4;
+                            if (skb_store_bytes(s, w, l4_off, &port, 2) < 0) return DROP_WRITE_ERROR;
+                        }
+                        break;
+                    }
+                    case IPPROTO_ICMPV6: case IPPROTO_ICMP: break;
+                    default: return DROP_UNKNOWN_L4;
+                    }
+                }
+                uint8_t os[16];
+                for (int k = 0; k < 16; k++) os[k] = skb_byte(s, 22 + k);
+                wbytes(s, w, 22, nat, 16);                       /* ipv6_store_saddr */
+                if (l4_csum_replace(s, w, l4_off + co, 0, ck_diff(os, nat, 16), BPF_F_PSEUDO_HDR | fl) < 0)
+                    return DROP_CSUM_L4;
+            }
+            r->eg_flags |= EG_F_REVNAT;
+        }
+        break;
+    default:
+        return DROP_POLICY;
+    }
+    if (verdict > 0) {                                           /* ipv6_redirect_to_host_port + ipv6_l3 */
+        ret = redirect_to_host_port_checks(s, l4_off, nh);
+        if (IS_ERR(ret)) return ret;
+        pol_ctx x = {w, plog};
+        redirect_write(s, &x, l4_off, t, 1, (uint16_t)verdict, orig_dip, c->seclabel, now);
+        if (plog) plog[1] = 1;
+        r->eg_flags |= EG_F_PROXY; r->proxy = (uint16_t)verdict;
+        ret = ipv6_l3(s, w, c->node_mac, g_node.host_mac);
+        if (ret != TC_ACT_OK) return ret;
+        r->ifindex = g_node.host_ifindex;
+        return TC_ACT_REDIRECT;
+    }
+    for (int k = 0; k < 16; k++) d6[k] = skb_byte(s, 38 + k);
+    const uint8_t *ep = g_node.lxc_map ? endpoint_val6(g_node.lxc_map, d6) : NULL;
+    if (ep) {
+        uint32_t epf; memcpy(&epf, ep + 8, 4);
+        if (epf & ENDPOINT_F_HOST) {
+            if (!g_node.host_ifindex) return DROP_NO_LXC;
+            goto to_host;
+        }
+        s->cb[2] = 0;
+        ret = ipv6_l3(s, w, ep + 24, ep + 16);                   /* ipv6_local_delivery, l3.h:106-134 */
+        if (ret != TC_ACT_OK) return ret;
+        r->eg_flags |= EG_F_LOCAL;
+        return local_delivery_tail(s, w, l4_off, ep, nh, c->seclabel, nr);
+    }
+    if (g_node.encap_ifindex) {                                  /* encap_and_redirect, key daddr/96 */
+        uint8_t k[20] = {0};
+        memcpy(k, d6, 12); k[16] = 2;
+        const uint8_t *tun = g_node.tunnel_map ? om_lookup_ptr(g_node.tunnel_map, k) : NULL;
+        if (tun) {
+            r->tunnel_ip = bswap32(ge32(tun, 0));
+            r->ifindex = g_node.encap_ifindex;
+            r->eg_flags |= EG_F_ENCAP;
+            return TC_ACT_REDIRECT;
+        }
+    }
+    if (dst_id == CLUSTER_ID) s->cb[2] = 1;
+    ret = ipv6_l3(s, w, NULL, c->node_mac);                      /* pass_to_stack */
+    if (ret != TC_ACT_OK) return ret;
+    {                                                            /* ipv6_store_flowlabel(SECLABEL_NB) */
+        uint32_t old;
+        if (skb_load_bytes(s, ETH_HLEN, &old, 4) < 0) return DROP_INVALID;
+        old &= bswap32(0x0FF00000u);
+        old = bswap32(0x60000000u) | bswap32(c->seclabel) | old;
+        if (skb_store_bytes(s, w, ETH_HLEN, &old, 4) < 0) return DROP_WRITE_ERROR;
+    }
+    r->eg_flags |= EG_F_TO_STACK;
+    return TC_ACT_OK;
+to_host:
+    ret = ipv6_l3(s, w, c->node_mac, g_node.host_mac);
+    if (ret != TC_ACT_OK) return ret;
+    r->eg_flags |= EG_F_TO_HOST;
+    r->ifindex = g_node.host_ifindex;
+    return TC_ACT_REDIRECT;
+}
+
 /* handle_ingress (from-container, bpf_lxc.c:685-738) + tail_handle_ipv4 (:659-668) */
 static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_egress_out *o,
                            uint8_t *row, uint8_t *plog, uint8_t *skip, uint32_t *secctx, uint32_t *ifx,
@@ -2038,9 +2255,14 @@ static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, 
         o->stage = 0; o->eg_flags = EG_F_ARP; return;
     }
     if (c->flags & LXC_F_DROP_ALL) ret = DROP_POLICY;
-    else if (s.protocol == 0x86DD) { o->stage = 0; o->eg_flags = EG_F_IPV6; return; }
+    else if (s.protocol == 0x86DD) { r.eg_flags = EG_F_IPV6; ret = from_lxc_ipv6(c, &s, row, now, &r, plog, &nr); }
     else if (s.protocol == 0x0800) ret = from_lxc_ipv4(c, &s, row, now, &r, plog, &nr);
     else ret = DROP_UNKNOWN_L3;
+    if (ret == O_EG_RESPONDER) { o->stage = 0; o->eg_flags = EG_F_IPV6 | EG_F_RESPONDER; return; }
+    if (ret == O_EG_ICMP6_TE) {                  /* ipv6_l3 -> icmp6_send_time_exceeded: the reply goes back out */
+        r.eg_flags |= EG_F_ICMP6_TE; r.eg_flags &= (uint16_t)~(EG_F_LOCAL | EG_F_TO_STACK | EG_F_TO_HOST);
+        ret = TC_ACT_REDIRECT; r.ifindex = 0;
+    }
     o->eg_ct_ret = r.ct_ret; o->ct_ret = r.ct_ret;
     o->slave = r.slave; o->rev_nat = r.rev_nat; o->eg_flags = r.eg_flags;
     if (ret == O_NETDEV_TAILCALL) {
@@ -2054,7 +2276,8 @@ static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, 
         /* a cilium_proxy4 entry written by ipv4_redirect_to_host_port stays when
          * the ipv4_l3 that follows it drops the packet (lxc.h:137 before l3.h:54) */
         if (plog && !(r.eg_flags & EG_F_PROXY)) plog[0] = 0;
-        o->eg_flags &= (uint16_t)(EG_F_CREATED | EG_F_DELETED | EG_F_LB | EG_F_LOOPBACK | EG_F_PORTMAP | EG_F_REVNAT);
+        o->eg_flags &= (uint16_t)(EG_F_CREATED | EG_F_DELETED | EG_F_LB | EG_F_LOOPBACK | EG_F_PORTMAP | EG_F_REVNAT |
+                                  EG_F_IPV6);
         return;
     }
     o->action = (uint8_t)ret;

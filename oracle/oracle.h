@@ -74,6 +74,8 @@ typedef struct o_lxc_cfg {
     struct { uint16_t from, to; } portmap[16];
     uint32_t n_l4_egress;
     o_l4_allow l4_egress[64];
+    uint8_t lxc_ip6[16];
+    om_map *lb6_services, *cidr6_egress_map;
 } o_lxc_cfg;
 
 typedef struct o_node_cfg {       /* == gf_node_cfg (bpf/node_config.h values on the path) */
@@ -86,6 +88,7 @@ typedef struct o_node_cfg {       /* == gf_node_cfg (bpf/node_config.h values on
     om_map *lxc_map;              /* cilium_lxc (egress endpoint lookup) */
     uint32_t ipv4_cluster_range, ipv4_cluster_mask, ipv4_loopback, ipv4_mask, encap_ifindex;
     om_map *tunnel_map;           /* cilium_tunnel_map */
+    uint8_t router_ip6[16];       /* ROUTER_IP */
 } o_node_cfg;
 
 /* Per-packet metadata of a batch (host arrays, may be NULL where unused). */

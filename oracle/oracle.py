@@ -31,7 +31,8 @@ class o_lxc_cfg(C.Structure):
                 ("l4_ingress", o_l4_allow * 64), ("lxc_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6),
                 ("lxc_ipv4", C.c_uint32), ("lb4_services", VP), ("ipcache_map", VP), ("cidr4_egress_map", VP),
                 ("n_portmap", C.c_uint32), ("portmap", C.c_uint16 * 32), ("n_l4_egress", C.c_uint32),
-                ("l4_egress", o_l4_allow * 64)]
+                ("l4_egress", o_l4_allow * 64), ("lxc_ip6", C.c_uint8 * 16), ("lb6_services", VP),
+                ("cidr6_egress_map", VP)]
 
 
 class o_node_cfg(C.Structure):
@@ -39,7 +40,7 @@ class o_node_cfg(C.Structure):
                 ("host_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6), ("node_mac", C.c_uint8 * 6),
                 ("lxc_map", VP), ("ipv4_cluster_range", C.c_uint32), ("ipv4_cluster_mask", C.c_uint32),
                 ("ipv4_loopback", C.c_uint32), ("ipv4_mask", C.c_uint32), ("encap_ifindex", C.c_uint32),
-                ("tunnel_map", VP)]
+                ("tunnel_map", VP), ("router_ip6", C.c_uint8 * 16)]
 
 
 class o_batch(C.Structure):

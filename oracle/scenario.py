@@ -16,6 +16,8 @@ def egress_fields(c, e, h):
     c.node_mac[:] = list(e.get("node_mac", bytes(6)))
     c.lxc_ipv4 = e.get("lxc_ipv4", 0)
     c.lb4_services, c.ipcache_map, c.cidr4_egress_map = h(e.get("lb4")), h(e.get("ipcache")), h(e.get("cidr4e"))
+    c.lb6_services, c.cidr6_egress_map = h(e.get("lb6")), h(e.get("cidr6e"))
+    c.lxc_ip6[:] = list(e.get("lxc_ip6", bytes(16)))
     pm = e.get("portmap") or []
     c.n_portmap = len(pm)
     for i, (frm, to) in enumerate(pm):
@@ -44,7 +46,7 @@ class OracleDP:
                                   (C.c_uint8 * 6)(*nd.get("node_mac", bytes(6))),
                                   p(nd.get("lxc_map")), nd.get("ipv4_cluster_range", 0), nd.get("ipv4_cluster_mask", 0),
                                   nd.get("ipv4_loopback", 0), nd.get("ipv4_mask", 0), nd.get("encap_ifindex", 0),
-                                  p(nd.get("tunnel_map")))
+                                  p(nd.get("tunnel_map")), (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
         O.lib.o_set_node(C.byref(self._node))
         self.xdp_cfg = self.lb_cfg = None
         if sc.xdp:

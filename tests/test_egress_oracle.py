@@ -169,3 +169,26 @@ def test_fuzz_invariants():
         shot = o["action"] == 2
         assert np.all(o["reason"][shot] > 0) and np.all(o["reason"][~shot] == 0)
         assert np.all((o["eg_flags"][st == 4] & 0x0200) != 0)
+
+
+def test_ipv6_pass_to_stack_flowlabel_and_responders():
+    """ipv6_l3_from_lxc's pass_to_stack (bpf_lxc.c:370-385): hop limit - 1, dmac =
+    NODE_MAC, ipv6_store_flowlabel(SECLABEL_NB) keeping the traffic class
+    (bpf/lib/ipv6.h:245-260); icmp6_handle's NS goes to the responder (stage NONE)."""
+    sc = _scn()
+    s6 = bytes([0xf0, 0x0d] + [0] * 13 + [5])
+    d6 = bytes([0x20, 0x01, 0x0d, 0xb8] + [0] * 11 + [9])
+    sc.lxc[0]["lxc_ip6"] = s6
+    ref = OracleDP(sc)
+    f, lens = synth.frames_v6(2, 128, np.frombuffer(s6, np.uint8), np.frombuffer(d6, np.uint8),
+                              np.array([TCP, 58], np.uint8), 40000, 443, F_SYN, 135)
+    f[:, 0:6] = list(NODE_MAC)
+    f[:, 6:12] = list(LXC_MAC)
+    f[:, 15] = 0x3c                                     # traffic class bits in the first word
+    pk = synth.Packets(f, lens, None, None, np.array([100, 100], np.uint16), None, np.zeros(2, np.uint32))
+    o, snap = ref.egress(pk, NOW)
+    assert (o[0]["stage"], o[0]["action"]) == (5, 0) and o[0]["eg_flags"] == 0x1000 | 0x0100 | 0x0001
+    word = struct.unpack(">I", bytes(snap[0, 14:18]))[0]
+    assert word == 0x60000000 | (0x0FF00000 & struct.unpack(">I", bytes(f[0, 14:18]))[0]) | 300
+    assert snap[0, 21] == 63 and bytes(snap[0, 0:6]) == NODE_MAC
+    assert o[1]["stage"] == 0 and o[1]["eg_flags"] == 0x1000 | 0x4000

@@ -269,10 +269,11 @@ def test_drop_notify_events():
 @pytest.mark.parametrize("seed,kw", [(5, {"hazard": False}), (6, {"hazard": True}),
                                      (7, {"hazard": False, "proxy_max": 6})])
 def test_egress_fuzz(seed, kw):
-    """Endpoint egress (bpf_lxc.c handle_ingress -> handle_ipv4_from_lxc) over raw
-    frames, local deliveries through the destination's handle_policy: records,
-    rewritten frames, CT (service / loopback / related entries, tx accounting,
-    deletes), policy counters and cilium_proxy4 all bit-exact vs the oracle."""
+    """Endpoint egress (bpf_lxc.c handle_ingress -> handle_ipv4_from_lxc /
+    ipv6_l3_from_lxc) over raw frames, local deliveries through the destination's
+    handle_policy: records, rewritten frames, CT v4/v6 (service / loopback /
+    related entries, tx accounting, deletes), policy counters and the proxy maps
+    all bit-exact vs the oracle."""
     from cilium_amd.datapath import EG_OUT
     sc = synth.egress_fuzz(seed=seed, n_packets=20000, n_batches=3, **kw)
     dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
@@ -287,9 +288,11 @@ def test_egress_fuzz(seed, kw):
         assert len(bad) == 0, f"rewritten frames b{bi}: {len(bad)} rows differ, first {bad[:1]}"
         assert set(np.unique(ro["stage"])) >= {0, 4, 5}
     assert dp.dump_map("ct4") == ref.dump("ct4")
+    assert dp.dump_map("ct6") == ref.dump("ct6")
     for e in range(16):
         assert dp.dump_map(f"pol{e}") == ref.dump(f"pol{e}"), f"policy counters pol{e}"
     assert dp.dump_map("cilium_proxy4") == ref.dump("cilium_proxy4")
+    assert dp.dump_map("cilium_proxy6") == ref.dump("cilium_proxy6")
 
 
 def test_pipeline_partition_owners():
