@@ -2284,7 +2284,8 @@ static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, 
     o->proxy_port = r.proxy; o->ifindex_lo = (uint16_t)r.ifindex; o->tunnel_ip = r.tunnel_ip;
 }
 
-void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egress_out *out, uint8_t *snap_out) {
+void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egress_out *out, uint8_t *snap_out,
+                    uint8_t *events) {
     const uint32_t n = b->n;
     uint8_t *snap = snap_out ? snap_out : (uint8_t *)malloc((size_t)n * b->snap_stride + 1);
     uint8_t *skip = (uint8_t *)malloc((size_t)n + 1);
@@ -2317,6 +2318,22 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
         o_egress_out *o = &out[i];
         o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
         o->flags = ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
+    }
+    /* drop notifications: the sender's send_drop_notify(SECLABEL, 0, 0, 0, ret) for
+     * from-container drops (bpf_lxc.c:659-668), handle_policy's for local deliveries */
+    for (uint32_t i = 0; events && i < n; i++) {
+        uint8_t *e = events + (size_t)i * O_EVENT_RECORD;
+        memset(e, 0, O_EVENT_RECORD);
+        const o_egress_out *o = &out[i];
+        if (o->action != TC_ACT_SHOT) continue;
+        const uint8_t *row = snap + (size_t)i * b->snap_stride;
+        uint32_t hash = b->flow_hash ? b->flow_hash[i] : 0, len = b->len[i];
+        const o_lxc_cfg *c = o->stage == O_STAGE_POLICY ? a->slot[lxcid[i]]
+                                                         : a->slot[(b->lxc_id ? b->lxc_id[i] : 0) & 0xffff];
+        if (!c) drop_event(e, o->reason, 0, hash, len, 0, 0, 0, 0, row, b->snap_stride);
+        else if (o->stage == O_STAGE_POLICY)
+            drop_event(e, o->reason, c->lxc_id, hash, len, secctx[i], c->seclabel, c->lxc_id, ifx[i], row, b->snap_stride);
+        else drop_event(e, o->reason, c->lxc_id, hash, len, c->seclabel, 0, 0, 0, row, b->snap_stride);
     }
     free(plog2); free(ing); free(plog);
     if (!snap_out) free(snap);

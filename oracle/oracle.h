@@ -180,7 +180,7 @@ typedef struct o_egress_out {       /* == gf_egress_out (24 B) */
     uint16_t lxc_id, pad;
 } o_egress_out;
 void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now_sec, o_egress_out *out,
-                    uint8_t *snap_out);
+                    uint8_t *snap_out, uint8_t *events);   /* events: n * 160 B (drop_notify), may be NULL */
 
 /* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time);

@@ -88,7 +88,7 @@ _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
 _s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32, VP)
 _s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
-_s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP)
+_s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
@@ -245,9 +245,13 @@ def ingress_events(prog_array, b, out):
     return ev[ev[:, 0] == 1]
 
 
-def egress(prog_array, b, now):
-    """o_egress_batch: returns (records EG_OUT, rewritten snaps)."""
+def egress(prog_array, b, now, events=False):
+    """o_egress_batch: returns (records EG_OUT, rewritten snaps[, drop events in batch order])."""
     out = np.zeros(b.n, EG_OUT)
     snap = np.zeros((b.n, b.snap_stride), np.uint8)
-    lib.o_egress_batch(prog_array, C.byref(b), now, out.ctypes.data, snap.ctypes.data)
+    ev = np.zeros((b.n, 160), np.uint8) if events else None
+    lib.o_egress_batch(prog_array, C.byref(b), now, out.ctypes.data, snap.ctypes.data,
+                       None if ev is None else ev.ctypes.data)
+    if events:
+        return out, snap, ev[ev[:, 0] == 1]
     return out, snap

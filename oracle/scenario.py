@@ -109,9 +109,9 @@ class OracleDP:
                                           C.pointer(self._nd), self.arr)
         return O.pipeline(self._pipe, self.batch(pk), now, threads, events)
 
-    def egress(self, pk, now):
+    def egress(self, pk, now, events=False):
         O.lib.o_set_node(C.byref(self._node))
-        return O.egress(self.arr, self.batch(pk), now)
+        return O.egress(self.arr, self.batch(pk), now, events)
 
     def ct_gc(self, name, filter_time):
         return self.m[name].ct_gc(filter_time)

@@ -262,6 +262,24 @@ def test_drop_notify_events():
         got = recs[:n].cpu().numpy()
         bad = np.nonzero((got != e).any(axis=1))[0]
         assert len(bad) == 0, f"{len(bad)} event records differ, first {bad[:1]}: {got[bad[0]][:32]} vs {e[bad[0]][:32]}"
+        cnt.zero_()
+        # endpoint egress: the sender's drops and the local deliveries' handle_policy drops
+        from cilium_amd.datapath import EG_OUT
+        sc = synth.egress_fuzz(seed=5, n_packets=20000, n_batches=2, hazard=False)
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        exp = []
+        for bi, pk in enumerate(sc.batches):
+            out, snap = dp.egress(DeviceBatch(pk, parse=False), sc.now + bi)
+            ro, rs, ev = ref.egress(pk, sc.now + bi, events=True)
+            torch.cuda.synchronize()
+            _cmp_struct(to_numpy(out, EG_OUT), ro, f"egress b{bi}")
+            exp.append(ev)
+        e = np.concatenate(exp)
+        n = int(cnt.item())
+        assert n == len(e) > 100
+        got = recs[:n].cpu().numpy()
+        bad = np.nonzero((got != e).any(axis=1))[0]
+        assert len(bad) == 0, f"{len(bad)} egress event records differ, first {bad[:1]}: {got[bad[0]][:32]} vs {e[bad[0]][:32]}"
     finally:
         lib.gf_set_event_ring(None)
 
