@@ -462,9 +462,11 @@ def bench_egress(args, dev):
     from cilium_amd.datapath import Datapath
     W, K = 3, max(4, args.steps // 2)
     n = args.egress_flows
+    t0 = time.time()
     sc, meta = synth.egress_tables(ct_max=args.ct_max)
     f, lens, lid, fh = synth.egress_flows(meta, n)
     dp = Datapath(sc, pin_prefix=None)
+    log(f"egress: tables and {n} flows ({time.time() - t0:.1f}s)")
     base = torch.from_numpy(f).to(dev)
     q = n // 4
     frames = []
@@ -487,6 +489,7 @@ def bench_egress(args, dev):
     fbs = [fbatch(i) for i in range(W + K)]
     out = torch.empty((n, 24), dtype=torch.uint8, device=dev)
     el, c, _, kern = timed(lambda s: dp.egress(fbs[s], sc.now + s, out=out, snap_out=False), W, K, dev)
+    log(f"egress: timed {K} steps ({time.time() - t0:.1f}s)")
     cpu = None
     if not args.no_cpu:
         from oracle.scenario import OracleDP

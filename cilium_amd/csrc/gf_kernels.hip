@@ -2274,7 +2274,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         } else if (r.st == 0) {
             key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
             const uint32_t lo = E.loopback;
-            if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || E.strict) *E.seq = 1u;
+            if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || (E.strict & 1u)) *E.seq = 1u;
         } else {
             key = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
             if (o.stage == GF_STAGE_FROM_LXC) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profile of the bench workloads (run from the repo root on the GPU box):
 #   1. rocprofv3 --kernel-trace --stats, one process per BASELINE configuration
-#      (config 2 = the headline line; 1, 3, 4, 5 = the "configs" entries)
+#      (config 2 = the headline line; 1, 3, 4, 5, egress = the "configs" entries)
 #   2. --pmc passes, one counter group per run (MI355X guide: FETCH_SIZE and
 #      WRITE_SIZE in separate passes): the k_ing_groups request mix of config 2,
 #      FETCH/WRITE of the roofline kernels of configs 1, 3, 4, 5
@@ -15,7 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks2" -o run -- \
     python "$R/bench.py" --no-cpu --no-extra > "$O/ks2.json" 2> "$O/ks2.err"
 echo "kernel stats config 2 done"
-for C in 1 3 4 5; do
+for C in 1 3 4 5 egress; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks$C" -o run -- \
       python "$R/bench.py" --no-cpu --config $C > "$O/ks$C.json" 2> "$O/ks$C.err"
   echo "kernel stats config $C done"
@@ -27,7 +27,7 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "TCC_EA
       python "$R/bench.py" --no-cpu --no-extra --steps 2 --warmup 3 > "$O/pmc/c2p$i.json" 2> "$O/pmc/c2p$i.err"
   echo "config 2 pmc pass $i done"
 done
-for C in 1 3 4 5; do
+for C in 1 3 4 5 egress; do
   i=0
   for P in "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
