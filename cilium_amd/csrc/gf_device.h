@@ -368,10 +368,21 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
     else (*added)--;
 }
 
-// Coverage-trie membership of an address given as raw (LE-loaded) words.
+// Coverage-trie membership of an address given as NW raw (LE-loaded) words.
+// The words are copied to registers and a byte picked by selects: a dynamic
+// index into the caller's array would put that array in scratch.
+template <int NW>
 __device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_t *aw) {
     if (!t.root_bits) return false;
-    auto byte_at = [&](uint32_t k) -> uint32_t { return (aw[k >> 2] >> (8 * (k & 3))) & 0xffu; };
+    uint32_t a[NW];
+#pragma unroll
+    for (int j = 0; j < NW; j++) a[j] = aw[j];
+    auto byte_at = [&](uint32_t k) -> uint32_t {
+        uint32_t w = a[0];
+#pragma unroll
+        for (int j = 1; j < NW; j++) w = (k >> 2) == (uint32_t)j ? a[j] : w;
+        return (w >> (8 * (k & 3))) & 0xffu;
+    };
     uint32_t idx = t.root_bits == 16 ? ((byte_at(0) << 8) | byte_at(1)) : byte_at(0);
     uint32_t e = gload<uint32_t>(t.root + idx);
     if (e == 0) return false;

@@ -265,7 +265,7 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint
         ab += 10;
         if (x.has_h4) {
             ab += 9;
-            if (trie_lookup(x.l4, &sa)) drop = true;
+            if (trie_lookup<1>(x.l4, &sa)) drop = true;
             else { ab += 9; uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
         }
         if (drop) return XDP_DROP_;
@@ -280,7 +280,7 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint
         ab += 34;
         if (x.has_h6) {
             ab += 21;
-            if (trie_lookup(x.l6, sw)) drop = true;
+            if (trie_lookup<4>(x.l6, sw)) drop = true;
             else { ab += 21; uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
         }
         if (drop) return XDP_DROP_;
@@ -880,8 +880,8 @@ proxy: {
 deny:
     if (identity < 256) {                               // identity_is_reserved
         const gf_lxc_dev *c = ep.cfg(X);
-        if (v6) { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr6); if (tr.root_bits) ab += 21; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
-        else { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr4); if (tr.root_bits) ab += 9; if (trie_lookup(tr, cidr_addr)) return TC_OK; }
+        if (v6) { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr6); if (tr.root_bits) ab += 21; if (trie_lookup<4>(tr, cidr_addr)) return TC_OK; }
+        else { const gf_trie_desc tr = gload<gf_trie_desc>(&c->cidr4); if (tr.root_bits) ab += 9; if (trie_lookup<1>(tr, cidr_addr)) return TC_OK; }
     }
     return D_POLICY;
 }
@@ -2006,7 +2006,7 @@ struct EgDev {
     uint32_t router6[4], host6[4];      // ROUTER_IP, HOST_IP (LE words)
     uint32_t strict;                    // bit0: CT4 inserts check max_entries (forces the single bucket); bit1: CT6
     uint32_t *seq;                      // device word: 1 = single-bucket batch (written by k_eg_front)
-    uint32_t *ctlog, *ctlog_n;          // deferred service entries: {i, key[4], value[12], pad[3]}
+    uint32_t *ctlog, *ctlog_n;          // deferred service entries {i, key[4], value[12], pad[3]}; [n, v6 deliveries]
     IngCtx X;                           // redirect writes + cilium_proxy4 log (pol_redirect)
 };
 #define GF_CTLOG_WORDS 20u
@@ -2041,8 +2041,8 @@ __device__ __forceinline__ int eg_ipv4_l3(Row &w, uint32_t len, const uint32_t *
 // lb6_lookup_service + lb6_local (lb6_xlate: daddr, the L4 checksum at l4_off + its
 // offset even when that offset is 0, the port), map_lxc_out.  TC_OK: continue in
 // k_eg_groups (r.st = 0); a stage-NONE responder returns TC_OK with r.st set.
-__device__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Row &w, uint32_t len, uint32_t fh, EgRec &r,
-                         gf_egress_out &o, uint32_t &ab) {
+__device__ __forceinline__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Row &w, uint32_t len, uint32_t fh,
+                                         EgRec &r, gf_egress_out &o, uint32_t &ab) {
     r.eflags = GF_EG_F_IPV6;
     if (len < 54) return D_INVALID;
     if (w.b(20) == 58) {                                // icmp6_handle (bpf/lib/icmp6.h:380-401)
@@ -2136,28 +2136,34 @@ __device__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Row &w, uint32_t l
 }
 
 // handle_ingress + the stateless head of handle_ipv4_from_lxc, one packet per lane
+// FAM 6 takes the IPv6 frames, FAM 4 every other frame (two launches: the IPv6
+// path's registers and stack stay out of the IPv4 kernel).
+template <int FAM>
 __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t *lxc_id, const uint32_t *fhash, EgDev E,
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
                                                     unsigned long long *stats) {
     __shared__ uint32_t sl[272];
-    __shared__ uint4 lds[BLOCK * (GF_EG_STAGE / 16)];
+    __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
     Stats st{sl};
     if (stats) st.init();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < fr.n) {
-        const uint32_t len = fr.len[i], S = fr.snap_stride, K = eg_stage_bytes(S);
-        const uint8_t *src = fr.snap + (size_t)i * S;
+    const uint32_t S = fr.snap_stride;
+    const uint32_t len = i < fr.n ? fr.len[i] : 0u;
+    const uint8_t *src = fr.snap + (size_t)i * S;
+    const uint32_t cap0 = S < len ? S : len;
+    const bool v6 = i < fr.n && len >= 14 && fbyte(src, cap0, 12) == 0x86 && fbyte(src, cap0, 13) == 0xDD;
+    if (i < fr.n && v6 == (FAM == 6)) {
+        const uint32_t K = eg_stage_bytes(S);
         uint8_t *dst = E.snap + (size_t)i * S;
-        const uint32_t cap0 = S < len ? S : len;
-        const bool v6 = len >= 14 && fbyte(src, cap0, 12) == 0x86 && fbyte(src, cap0, 13) == 0xDD;
-        uint8_t *row = reinterpret_cast<uint8_t *>(lds + threadIdx.x * (GF_EG_STAGE / 16));
-        if (v6) {                                             // extension headers: the whole snap, in HBM
+        uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
+        if (FAM == 6) {                                       // extension headers: the whole snap, in HBM
             if (src != dst) eg_copy(dst, src, S);
         } else {
             eg_copy(row, src, K);                             // the header, staged
             if (S > K && src != dst) eg_copy(dst + K, src + K, S - K);   // the rest of the snap, as is
         }
-        Row w = v6 ? Row{dst, cap0} : Row{row, K < len ? K : len};
+        Row w{row, K < len ? K : len};                        // IPv4: the LDS copy (ds_* accesses)
+        Row wg{dst, cap0};                                    // IPv6: the frame in HBM
         gf_egress_out o{};
         EgRec r{};
         r.len = len;
@@ -2167,14 +2173,14 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         r.st = GF_EGR_FINAL;
         int ret = TC_OK;
         o.stage = GF_STAGE_FROM_LXC;
-        const uint32_t et = len >= 14 ? ((w.b(12) << 8) | w.b(13)) : 0u;
+        const uint32_t et = len >= 14 ? ((fbyte(src, cap0, 12) << 8) | fbyte(src, cap0, 13)) : 0u;
         do {
             if (!sl_) { ret = D_MISSED_TAIL_CALL; break; }
             const gf_lxc_dev *c = E.cfgs + (sl_ - 1);
             const uint32_t flags = gload<uint32_t>(&c->flags);
             if (et == 0x0806) { o.stage = GF_STAGE_NONE; o.eg_flags = GF_EG_F_ARP; break; }
             if (flags & GF_LXC_F_DROP_ALL) { ret = D_POLICY; break; }
-            if (et == 0x86DD) { ret = eg_front6(E, c, w, len, fhash ? fhash[i] : 0u, r, o, ab); break; }
+            if constexpr (FAM == 6) { ret = eg_front6(E, c, wg, len, fhash ? fhash[i] : 0u, r, o, ab); break; }
             if (et != 0x0800) { ret = D_UNKNOWN_L3; break; }
             if (len < 34) { ret = D_INVALID; break; }
             const uint32_t nh = w.b(23);
@@ -2267,10 +2273,10 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             r.st = 0;                                       // continue in k_eg_groups
         } while (0);
         uint32_t key;
-        if (r.st == 0 && (r.eflags & GF_EG_F_IPV6)) {
+        if (r.st == 0 && FAM == 6) {
             uint32_t s6[4], d6[4];
-            for (int k = 0; k < 4; k++) { s6[k] = w.r32(22 + 4 * k); d6[k] = w.r32(38 + 4 * k); }
-            key = gf_pair_hash6(s6, d6) & GF_KEY_HASH;        // (family 0: one egress launch serves both)
+            for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
+            key = (gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;   // the IPv6 family of the schedule
         } else if (r.st == 0) {
             key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
             const uint32_t lo = E.loopback;
@@ -2289,15 +2295,16 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         }
         erec[i] = r;
         keys[i] = key;
-        if (!v6) eg_copy(dst, row, K);                        // the frame as the front left it
+        if (FAM == 4) eg_copy(dst, row, K);                   // the frame as the front left it
     }
     if (stats) st.flush(stats);
 }
 
-// After the front: a flagged batch runs as one bucket (every key equal).
+// After the front: a flagged batch runs as one bucket per family (every IPv4
+// key equal; the IPv6 path writes no service entries and keeps its own bucket).
 __global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, uint32_t n, uint32_t *keys) {
     if (!*seq) return;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] = 0u;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] &= GF_KEY_FAM;
 }
 
 // __ct_lookup hit part for CT_EGRESS (conntrack.h:75-135): tx accounting (the
@@ -2336,7 +2343,7 @@ __device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int 
 // policy_can_egress4 (policy.h:241-264 with POLICY_EGRESS, else :282-289):
 // ipcache identity, __policy_can_access(dir = CT_EGRESS: key.egress = 1, the
 // CFG_L3L4_EGRESS list), reserved identities through CIDR4_EGRESS_MAP.
-__device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, const uint32_t *da, bool v6,
+__device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, const uint32_t *da, bool v6,
                          uint32_t dport, uint32_t proto, uint32_t len, uint32_t &ab) {
     if (flags & GF_LXC_F_DROP_ALL) return D_POLICY;
     if (!(flags & GF_LXC_F_POLICY_EGRESS)) return TC_OK;
@@ -2391,7 +2398,7 @@ __device__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, uint32_t dst_id, c
     if (identity < 256 && verdict < 0) {               // identity_is_reserved -> lpm{4,6}_egress_lookup
         const gf_trie_desc tr = gload<gf_trie_desc>(v6 ? &c->cidr6e : &c->cidr4e);
         if (tr.root_bits) ab += v6 ? 21 : 9;
-        verdict = trie_lookup(tr, da) ? 0 : D_POLICY_CIDR;
+        verdict = (v6 ? trie_lookup<4>(tr, da) : trie_lookup<1>(tr, da)) ? 0 : D_POLICY_CIDR;
     }
     return verdict;
 }
@@ -2592,8 +2599,8 @@ __device__ __forceinline__ int eg_ipv6_l3(Row &w, const uint32_t *smac, const ui
 
 // The CT / policy part of ipv6_l3_from_lxc (bpf_lxc.c:186-386) for packet i, on
 // the frame in HBM (extension headers may put the L4 header anywhere in the snap).
-__device__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
-                           uint32_t &lxc, int *added, uint32_t &ab) {
+__device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o,
+                                           uint32_t &ifx, uint32_t &lxc, int *added, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
     const int l4_off = r.l4_off;
     const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
@@ -2762,21 +2769,27 @@ __device__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint32_t i, Row &w, g
 // One bucket per lane from the longest-first queue (the ingress schedule), in
 // batch order.  Writes each packet's verdict, and for local deliveries the
 // handle_policy record + flow-group key of the ingress pass (rec2 / key2).
-__global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
+// FAM 4 runs the schedule's family 0 (IPv4 buckets and every packet the front
+// finished), FAM 6 family 1 (IPv6); the two touch disjoint state.
+template <int FAM>
+__global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
-                                                     uint32_t *ct_count, uint32_t *ct_count6, unsigned long long *stats) {
+                                                     uint32_t *ct_count, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
-    __shared__ uint4 lds[BLOCK * (GF_EG_STAGE / 16)];
+    __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    uint8_t *row = reinterpret_cast<uint8_t *>(lds + threadIdx.x * (GF_EG_STAGE / 16));
+    uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
     const uint32_t K = eg_stage_bytes(E.stride);
-    const uint32_t nb = GF_SCHED_NFAM(sched)[0], lane = threadIdx.x & 63u;
-    uint32_t *queue = GF_SCHED_QUEUE(sched);
+    constexpr int F = FAM == 6 ? 1 : 0;
+    const uint32_t *nfam = GF_SCHED_NFAM(sched);
+    const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
+    uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
+    if (F) order += nfam[0];
     const bool seq = *E.seq != 0;
-    int added = 0, added6 = 0;
+    int added = 0;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -2799,13 +2812,18 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
             o.slave = r.slave; o.rev_nat = r.rev_nat; o.eg_flags = r.eflags;
             uint32_t ifx = 0, lxc = 0, ab = 24 + 34 + 32;
             uint8_t *g = E.snap + (size_t)i * E.stride;
-            const bool v6 = (r.eflags & GF_EG_F_IPV6) != 0;
-            Row w = v6 ? Row{g, E.stride < r.len ? E.stride : r.len} : Row{row, K < r.len ? K : r.len};
+            constexpr bool v6 = FAM == 6;
             int ret;
-            if (v6) ret = eg_ct_part6(E, r, i, w, o, ifx, lxc, &added6, ab);
-            else {
+            PktHdr h2;                                  // the delivered header, re-parsed (local deliveries)
+            if constexpr (v6) {                         // the frame in HBM
+                Row w{g, E.stride < r.len ? E.stride : r.len};
+                ret = eg_ct_part6(E, r, i, w, o, ifx, lxc, &added, ab);
+                if (ret == ND_TAILCALL) parse_row(w.p, w.cap, r.len, h2);
+            } else {                                    // the LDS copy of the header bytes
                 eg_copy(row, g, K);
+                Row w{row, K < r.len ? K : r.len};
                 ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, ab);
+                if (ret == ND_TAILCALL) parse_row(w.p, w.cap, r.len, h2);
                 eg_copy(g, row, K);
             }
             o.ct_ret = o.eg_ct_ret;
@@ -2815,15 +2833,14 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
             }
             if (ret == ND_TAILCALL) {                   // handle_policy of the destination, next pass
                 o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; o.ct_ret = 0;
-                PktHdr h2;
-                parse_row(w.p, w.cap, r.len, h2);
                 const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
                 key2[i] = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
                                    gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, true,
                                    h2.s6, h2.d6, rr);
-                if (v6) {
+                if constexpr (v6) {
                     reinterpret_cast<uint4 *>(E.s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
                     reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
+                    atomicAdd(E.ctlog_n + 1, 1u);       // the ingress pass needs its IPv6 kernel
                 }
                 if (stats) st.add_n(270, ab);
             } else {
@@ -2843,18 +2860,10 @@ __global__ __launch_bounds__(BLOCK) void k_eg_groups(EgDev E, uint32_t *sched, c
             out[i] = o;
         }
     }
-    if (!(E.strict & 1)) {
+    if (!(E.strict & (FAM == 6 ? 2u : 1u))) {       // strict maps counted each insert inline
         if (added) atomicAdd(&sadd, (uint32_t)added);
         __syncthreads();
         if (threadIdx.x == 0 && sadd && ct_count) atomicAdd(ct_count, sadd);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) sadd = 0;
-    __syncthreads();
-    if (!(E.strict & 2)) {
-        if (added6) atomicAdd(&sadd, (uint32_t)added6);
-        __syncthreads();
-        if (threadIdx.x == 0 && sadd && ct_count6) atomicAdd(ct_count6, sadd);
     }
     if (stats) st.flush(stats);
 }
@@ -3772,7 +3781,7 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     EgWs &ew = eg_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
-        (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 4)) || (r = grow(ew.ctlog_n, 4)) ||
+        (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 4)) || (r = grow(ew.ctlog_n, 8)) ||
         (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 16)) ||
         (r = grow(ew.d6, (size_t)n * 16)) || (r = ws_grow(n)))
         return r;
@@ -3801,14 +3810,16 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     E.X.snap = nullptr; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;   // writes: k_eg_groups
     memcpy(E.X.host6, node.host_ip6, 16);
     if ((r = px_log_begin(n, s, E.X))) return r;
-    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 4, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 4, s), "eg ctlog"))
+    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 4, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
         return -EIO;
     unsigned long long *sink = (unsigned long long *)stats_sink();
     Workspace &w = ws();
     {
         ProfScope ps("k_eg_front", s);
-        hipLaunchKernelGGL(k_eg_front, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash, E,
-                           (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
+        hipLaunchKernelGGL(k_eg_front<4>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
+                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
+        hipLaunchKernelGGL(k_eg_front<6>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
+                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
         hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p, n,
                            (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_eg_front"))) return r;
@@ -3818,17 +3829,22 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
         uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
         ProfScope ps("k_eg_groups", s);
-        hipLaunchKernelGGL(k_eg_groups, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p, (const uint2 *)w.order.p,
-                           (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out, (gf_rec *)ew.rec2.p,
-                           (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr,
-                           ct6m ? (uint32_t *)ct6m->d_count.p : nullptr, sink);
+        hipLaunchKernelGGL(k_eg_groups<4>, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p,
+                           (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
+                           (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr,
+                           sink);
+        hipLaunchKernelGGL(k_eg_groups<6>, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p,
+                           (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
+                           (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct6m ? (uint32_t *)ct6m->d_count.p : nullptr,
+                           sink);
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     // ct_create4's deferred service entries, in batch order
-    uint32_t nlog = 0;
-    if (hip_ok(hipMemcpyAsync(&nlog, ew.ctlog_n.p, 4, hipMemcpyDeviceToHost, s), "ctlog count") ||
+    uint32_t cnts[2] = {0, 0};
+    if (hip_ok(hipMemcpyAsync(cnts, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost, s), "ctlog count") ||
         hip_ok(hipStreamSynchronize(s), "ctlog sync"))
         return -EIO;
+    const uint32_t nlog = cnts[0];
     if (nlog && ct4m) {
         if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
             (r = grow(ew.cval, (size_t)nlog * 4)) || (r = grow(ew.cperm, (size_t)nlog * 4)))
@@ -3859,7 +3875,7 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     c2.n = n;
     c2.len = fr.len;
     c2.flow_hash = b->flow_hash;
-    c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p;   // IPv6 deliveries' addresses
+    if (cnts[1]) { c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p; }   // IPv6 deliveries
     auto pack = [&](const uint16_t *, gf_rec *rec, uint32_t *keys) -> int {
         if (hip_ok(hipMemcpyAsync(rec, ew.rec2.p, (size_t)n * sizeof(gf_rec), hipMemcpyDeviceToDevice, s), "rec2") ||
             hip_ok(hipMemcpyAsync(keys, ew.key2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))
