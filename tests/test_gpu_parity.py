@@ -331,3 +331,46 @@ def test_pipeline_partition_owners():
             assert np.array_equal(owner.cpu().numpy(), want)
             assert np.array_equal(order.cpu().numpy(), np.argsort(want, kind="stable"))
             assert np.array_equal(counts.cpu().numpy(), np.bincount(want, minlength=world))
+
+
+def test_stream_counter_block():
+    """k_xdp / k_lb's wave-aggregated counter block (the block bench.py reads and
+    the multi-GPU all-reduce sums): reason / action bins, packets and wire bytes
+    equal the histogram of the oracle's verdicts, over a grid-stride launch with
+    a ragged tail."""
+    import ctypes as C
+    from cilium_amd._lib import lib
+    sc = synth.config3(n_packets=300_001, n_svc=5_000)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    lens = np.asarray(pk.lens, dtype=np.int64)
+    cnt = torch.zeros(512, dtype=torch.int64, device="cuda")
+    lib.gf_set_stats_sink(C.c_void_p(cnt.data_ptr()))
+    try:
+        lo, _ = dp.lb(DeviceBatch(pk))
+        torch.cuda.synchronize()
+    finally:
+        lib.gf_set_stats_sink(None)
+    c = cnt.cpu().numpy()
+    rl, _ = ref.lb(pk)
+    _cmp_struct(to_numpy(lo, LB_OUT), rl, "config3 lb")
+    assert c[268] == pk.n and c[269] == lens.sum()
+    for a in np.unique(rl["action"]):
+        assert c[256 + int(a)] == (rl["action"] == a).sum(), f"action {a}"
+    for r in range(1, 256):
+        assert c[r] == (rl["reason"] == r).sum(), f"reason {r}"
+
+    sc = synth.config1(n_packets=100_003, n_lpm=2_000, n_fix=500, n_ep=256)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    cnt.zero_()
+    lib.gf_set_stats_sink(C.c_void_p(cnt.data_ptr()))
+    try:
+        dp.xdp(DeviceBatch(pk))
+        torch.cuda.synchronize()
+    finally:
+        lib.gf_set_stats_sink(None)
+    c = cnt.cpu().numpy()
+    r = ref.xdp(pk)
+    assert c[268] == pk.n and c[269] == np.asarray(pk.lens, dtype=np.int64).sum()
+    assert c[257] == c[1] == (r == 1).sum() and c[258] == (r == 2).sum()
