@@ -17,6 +17,7 @@
 #include <rocprim/iterator/discard_iterator.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
+#include <stdlib.h>
 #include <functional>
 #include <string.h>
 
@@ -72,9 +73,10 @@ struct Stats {
     }
     // pkt() aggregated over the wave: one LDS atomic per distinct (reason,
     // action) pair and one per sum instead of five per lane.  Every lane of the
-    // wave must call it (act = the lane holds a packet).
+    // wave must call it (act = the lane counts a packet; ab is summed over every
+    // lane, so a lane without a packet passes 0).
     __device__ void pkt_wave(bool act, uint32_t reason, uint32_t action, uint32_t len, uint32_t ab) {
-        uint32_t n = act ? 1u : 0u, l = act ? len : 0u, a = act ? ab : 0u;
+        uint32_t n = act ? 1u : 0u, l = act ? len : 0u, a = ab;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             n += __shfl_xor(n, o); l += __shfl_xor(l, o); a += __shfl_xor(a, o);
@@ -91,7 +93,7 @@ struct Stats {
             }
             rem &= ~m;
         }
-        if (lane == 0 && n) { atomicAdd(&lds[268], n); atomicAdd(&lds[269], l); atomicAdd(&lds[270], a); }
+        if (lane == 0) { if (n) { atomicAdd(&lds[268], n); atomicAdd(&lds[269], l); } if (a) atomicAdd(&lds[270], a); }
     }
     __device__ void flush(unsigned long long *g) {
         __syncthreads();
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
             v = xdp_verdict(x, ColA{c, i}, len, c.ethertype[i], ab);
             verdict[i] = v;
         }
-        if (stats) st.pkt_wave(act, v == XDP_DROP_ ? 1u : 0u, v, len, ab);
+        if (stats) st.pkt_wave(act, v == XDP_DROP_ ? 1u : 0u, v, len, act ? ab : 0u);
     }
     if (stats) st.flush(stats);
 }
@@ -482,7 +484,7 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         if (nd6 && v6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
         else if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(0, 0, 0, 0);
       }
-      if (stats) st.pkt_wave(act, o.reason, o.action, len, ab);
+      if (stats) st.pkt_wave(act, o.reason, o.action, len, act ? ab : 0u);
     }
     if (stats) st.flush(stats);
 }
@@ -1604,7 +1606,9 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
     uint8_t *rows = reinterpret_cast<uint8_t *>(lds_rows);
     __shared__ uint32_t sl[272];
     Stats st{sl};
-    const uint32_t S = fr.snap_stride, b0 = blockIdx.x * NT;
+    if (stats) st.init();
+    const uint32_t S = fr.snap_stride;
+    const uint32_t b0 = blockIdx.x * NT;
     const uint32_t nb = fr.n - b0 < NT ? fr.n - b0 : NT;
     const size_t bytes = (size_t)nb * S;
     {
@@ -1617,8 +1621,10 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
         }
         for (size_t k = k0 + threadIdx.x; k < bytes; k += NT) rows[k] = src[k];
     }
-    if (stats) st.init(); else __syncthreads();
+    __syncthreads();
     const uint32_t i = b0 + threadIdx.x;
+    bool scnt = false;                                  // the lane's counter-block entry
+    uint32_t sreason = 0, saction = 0, slen = 0, sab = 0;
     if (i < fr.n) {
         const uint32_t len = fr.len[i];
         const uint32_t cap = S < len ? S : len;
@@ -1694,11 +1700,10 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
         keys[i] = key;
         out[i] = o;
         if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
-        if (stats) {
-            if (tail) st.add_n(270, ab);                // handle_policy counts the packet itself
-            else st.pkt(o.reason, o.action, len, ab);
-        }
+        sab = ab;                                       // a tail-called packet: handle_policy counts it
+        if (!tail) { scnt = true; sreason = o.reason; saction = o.action; slen = len; }
     }
+    if (stats) st.pkt_wave(scnt, sreason, saction, slen, sab);
     if (snap_out) {
         __syncthreads();
         uint8_t *dst = snap_out + (size_t)b0 * S;
@@ -3006,9 +3011,16 @@ uint32_t grid_for(uint32_t n) {
 #ifndef GF_STREAM_GRID
 #define GF_STREAM_GRID 16384
 #endif
-uint32_t stream_grid(uint32_t n) {
-    uint32_t g = grid_for(n);
-    return (GF_STREAM_GRID && g > (uint32_t)GF_STREAM_GRID) ? (uint32_t)GF_STREAM_GRID : g;
+// GPUFLOW_STREAM_GRID overrides the cap (the GPU tests force a few blocks so
+// every block runs several tiles of the grid-stride loop).
+uint32_t stream_grid_cap() {
+    const char *e = getenv("GPUFLOW_STREAM_GRID");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)GF_STREAM_GRID;
+}
+uint32_t stream_grid(uint32_t n, uint32_t per_block = BLOCK) {
+    const uint32_t g = n == 0 ? 1u : (n + per_block - 1) / per_block, cap = stream_grid_cap();
+    const uint32_t lim = cap ? cap : 65535u * 8;      // grid-stride covers the rest
+    return g > lim ? lim : g;
 }
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
@@ -3669,7 +3681,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     if ((r = grow(w.s6, (size_t)n * 16)) || (r = grow(w.d6, (size_t)n * 16))) return r;
     P.vec_copy = (fr.snap_stride % 16 == 0) && (((uintptr_t)fr.snap | (uintptr_t)snap_out) & 15u) == 0;
     unsigned long long *sink = (unsigned long long *)stats_sink();
-    const uint32_t grid = (n + nt - 1) / nt;
+    const uint32_t grid = (n + nt - 1) / nt;         // one NT-frame tile per block
     gf_pkt_cols c2{};
     c2.n = n;
     c2.saddr6 = (const uint8_t *)w.s6.p; c2.daddr6 = (const uint8_t *)w.d6.p;

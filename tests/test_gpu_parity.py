@@ -374,3 +374,30 @@ def test_stream_counter_block():
     r = ref.xdp(pk)
     assert c[268] == pk.n and c[269] == np.asarray(pk.lens, dtype=np.int64).sum()
     assert c[257] == c[1] == (r == 1).sum() and c[258] == (r == 2).sum()
+
+
+def test_stream_kernels_grid_stride(monkeypatch):
+    """k_xdp and k_lb with the grid capped at 3 blocks (every block runs many
+    tiles of its grid-stride loop, the last one ragged) stay bit-exact; the
+    pipeline (k_pipe_front's wave-aggregated counters, one tile per block) on a
+    ragged batch too, rewritten frames included."""
+    monkeypatch.setenv("GPUFLOW_STREAM_GRID", "3")
+    sc = synth.fuzz(seed=11, n_packets=5_003, n_batches=1)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    b = DeviceBatch(pk)
+    v, (lo, nd6) = dp.xdp(b), dp.lb(b)
+    torch.cuda.synchronize()
+    _cmp_struct(v.cpu().numpy(), ref.xdp(pk), "xdp")
+    rl, rn6 = ref.lb(pk)
+    _cmp_struct(to_numpy(lo, LB_OUT), rl, "lb")
+    assert np.array_equal(nd6.cpu().numpy(), rn6)
+    sc = synth.pipeline_fuzz(seed=12, n_packets=5_003, n_batches=2)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        out, nd6, snap = dp.pipeline(DeviceBatch(pk, parse=False), sc.now + bi)
+        torch.cuda.synchronize()
+        ro, rn6, rs = ref.pipeline(pk, sc.now + bi)
+        _cmp_struct(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
+        assert np.array_equal(snap.cpu().numpy(), rs), f"rewritten frames b{bi}"
+        assert np.array_equal(nd6.cpu().numpy(), rn6), f"pipeline nd6 b{bi}"
