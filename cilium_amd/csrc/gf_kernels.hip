@@ -510,13 +510,30 @@ struct IngCtx {
 
 // ---- handle_policy's own header writes (kept out of line: cold paths of the
 // hot kernel) and the proxy-map log ----
-__device__ __forceinline__ Row pol_row(const IngCtx &X, uint32_t i, uint32_t len) {
+// The IngCtx fields the writers read, passed by value to the out-of-line copies:
+// a reference (or a pointer to a local tuple) would keep the whole context (or
+// the tuple) in scratch for the entire IPv6 kernel.
+struct PolCtx {
+    uint8_t *snap;
+    uint32_t *plog, *plog_n;
+    uint32_t snap_stride, now, gw, host6[4];
+};
+__device__ __forceinline__ PolCtx pol_ctx(const IngCtx &X) {
+    PolCtx c;
+    c.snap = X.snap; c.plog = X.plog; c.plog_n = X.plog_n;
+    c.snap_stride = X.snap_stride; c.now = X.now; c.gw = X.gw;
+    for (int k = 0; k < 4; k++) c.host6[k] = X.host6[k];
+    return c;
+}
+template <class XC>
+__device__ __forceinline__ Row pol_row(const XC &X, uint32_t i, uint32_t len) {
     return Row{X.snap + (size_t)i * X.snap_stride, X.snap_stride < len ? X.snap_stride : len};
 }
 // reverse_map_l4_port (bpf/lib/lb.h:217-251) + __lb4_rev_nat / __lb6_rev_nat
 // (lb.h:253-293, 447-512; v4 with REV_NAT_F_TUPLE_SADDR: the old address is the
 // tuple's, v6 with flags 0: the frame's)
-__device__ __forceinline__ void pol_rev_nat_write(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+template <class XC>
+__device__ __forceinline__ void pol_rev_nat_write(const XC &X, uint32_t i, uint32_t len, int l4_off,
                                                             uint32_t nh, const uint8_t *nat, bool v6,
                                                             uint32_t old_sip4) {
     Row w = pol_row(X, i, len);
@@ -546,7 +563,8 @@ __device__ __forceinline__ void pol_rev_nat_write(const IngCtx &X, uint32_t i, u
     }
 }
 // ipv6_policy's "derive reverse NAT index and zero it" (bpf_lxc.c:774-790)
-__device__ __forceinline__ void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+template <class XC>
+__device__ __forceinline__ void pol_v6_zero_rn(const XC &X, uint32_t i, uint32_t len, int l4_off,
                                                          uint32_t nh, uint32_t rn) {
     Row w = pol_row(X, i, len);
     w.w16(38 + 12, 0);
@@ -557,7 +575,8 @@ __device__ __forceinline__ void pol_v6_zero_rn(const IngCtx &X, uint32_t i, uint
 // ipv{4,6}_redirect_to_host_port writes (lib/lxc.h:96-205) after their checks,
 // and the cilium_proxy{4,6} entry, logged for the in-order apply after the launch.
 // t: the CT tuple words as ct_lookup left them; od: the original daddr.
-__device__ __forceinline__ void pol_redirect(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+template <class XC>
+__device__ __forceinline__ void pol_redirect(const XC &X, uint32_t i, uint32_t len, int l4_off,
                                                        uint32_t nh, const uint32_t *t, bool v6, uint32_t new_port,
                                                        const uint32_t *od, uint32_t identity, uint32_t egress = 0) {
     const uint32_t pw = v6 ? t[8] : t[2];
@@ -1020,18 +1039,20 @@ __device__ __forceinline__ int ct_l4(uint32_t nh, bool v6, const gf_rec &r, uint
 
 // Out-of-line copies for the IPv6 kernel, whose register budget the inlined
 // cold paths would cut to 2 waves/SIMD (the IPv4 kernel keeps them inline).
-__device__ __attribute__((noinline)) void pol_rev_nat_write_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+__device__ __attribute__((noinline)) void pol_rev_nat_write_ol(PolCtx X, uint32_t i, uint32_t len, int l4_off,
                                                                uint32_t nh, const uint8_t *nat) {
     pol_rev_nat_write(X, i, len, l4_off, nh, nat, true, 0u);
 }
-__device__ __attribute__((noinline)) void pol_v6_zero_rn_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
+__device__ __attribute__((noinline)) void pol_v6_zero_rn_ol(PolCtx X, uint32_t i, uint32_t len, int l4_off,
                                                             uint32_t nh, uint32_t rn) {
     pol_v6_zero_rn(X, i, len, l4_off, nh, rn);
 }
-__device__ __attribute__((noinline)) void pol_redirect_ol(const IngCtx &X, uint32_t i, uint32_t len, int l4_off,
-                                                          uint32_t nh, const uint32_t *t, uint32_t new_port,
-                                                          const uint32_t *od, uint32_t identity) {
-    pol_redirect(X, i, len, l4_off, nh, t, true, new_port, od, identity);
+struct V6Tuple { uint32_t w[10]; };
+__device__ __attribute__((noinline)) void pol_redirect_ol(PolCtx X, uint32_t i, uint32_t len, int l4_off,
+                                                          uint32_t nh, V6Tuple t, uint32_t new_port,
+                                                          uint4 od, uint32_t identity) {
+    const uint32_t odw[4] = {od.x, od.y, od.z, od.w};
+    pol_redirect(X, i, len, l4_off, nh, t.w, true, new_port, odw, identity);
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
@@ -1119,7 +1140,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     uint32_t co = csum_l4_offset(nh);
     uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
     if (rn_new) {
-        if (X.snap) pol_v6_zero_rn_ol(X, i, len, r.l4_off, nh, rn_new);
+        if (X.snap) pol_v6_zero_rn_ol(pol_ctx(X), i, len, r.l4_off, nh, rn_new);
         if (co && !l4csum_ok(r.l4_off + (int)co, len)) return D_CSUM_L4;
     }
     uint32_t tfl = 0;
@@ -1150,7 +1171,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
             const uint8_t *nat = ht_val(rn, f);
             int r2 = rev_nat_checks(len, r.l4_off, nh, gload<uint16_t>(nat + 16), r.l4w0, true);
             if (r2 < 0) return r2;
-            if (X.snap) pol_rev_nat_write_ol(X, i, len, r.l4_off, nh, nat);
+            if (X.snap) pol_rev_nat_write_ol(pol_ctx(X), i, len, r.l4_off, nh, nat);
         }
     }
     int verdict = policy_ingress(X, ep, pl, pre, r.src_identity, t[8] & 0xffffu, nh, len, true, t + 4, ab, acc, pm);
@@ -1171,7 +1192,12 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
-        if (X.snap || X.plog) { const uint32_t od[4] = {d.x, d.y, d.z, d.w}; pol_redirect_ol(X, i, len, r.l4_off, nh, t, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
+        if (X.snap || X.plog) {
+            V6Tuple tv;
+#pragma unroll
+            for (int k = 0; k < 10; k++) tv.w[k] = t[k];
+            pol_redirect_ol(pol_ctx(X), i, len, r.l4_off, nh, tv, (uint32_t)verdict & 0xffffu, d, r.src_identity);
+        }
         ifindex = X.host_ifindex;
         ofl |= GF_INGRESS_F_PROXY;
         proxy = (uint16_t)verdict;
