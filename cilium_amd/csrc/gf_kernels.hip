@@ -1209,6 +1209,28 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
 // LDS (one record per thread, k_ing_groups) so that registers hold only the
 // state of the packet in flight: the register budget is what bounds waves per
 // SIMD, and waves in flight are what hide the probes' memory latency.
+// The lane's share of the counter block: wire / algorithmic byte sums and the
+// four CT-result counts (16 bits each; the packet count is their sum), kept per
+// lane so the common bins take no same-address LDS atomics; folded into the
+// block's bins before a field could wrap and at the end of the launch.
+struct LaneCnt {
+    uint32_t len, ab, c01, c23;
+    __device__ __forceinline__ void init() { len = ab = c01 = c23 = 0; }
+    __device__ __forceinline__ void fold(Stats &st) {
+        const uint32_t a = c01 & 0xffffu, b = c01 >> 16, c = c23 & 0xffffu, d = c23 >> 16;
+        st.add_n(264, a); st.add_n(265, b); st.add_n(266, c); st.add_n(267, d);
+        st.add_n(268, a + b + c + d); st.add_n(269, len); st.add_n(270, ab);
+        init();
+    }
+    __device__ __forceinline__ void add(uint32_t l, uint32_t a, uint32_t ct, Stats &st) {
+        len += l; ab += a;
+        const uint32_t sh = 16u * (ct & 1u);
+        uint32_t &w = ct < 2 ? c01 : c23;
+        w += 1u << sh;
+        if (((w >> sh) & 0xffffu) == 0xffffu || len >= 0xf0000000u || ab >= 0xf0000000u) fold(st);
+    }
+};
+
 template <int FAM>
 struct Lane {
     Ep ep;
@@ -1216,7 +1238,8 @@ struct Lane {
     PolMemo pm;
     RelCache<FAM == 6 ? 10 : 4> rc;
     int added;
-    __device__ __forceinline__ void init() { ep.init(); acc.init(); pm.init(); rc.init(); added = 0; }
+    LaneCnt sc;
+    __device__ __forceinline__ void init() { ep.init(); acc.init(); pm.init(); rc.init(); added = 0; sc.init(); }
 };
 
 // handle_policy, bpf/bpf_lxc.c:980-1024.  FAM selects the CT path compiled in:
@@ -1335,7 +1358,7 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     } else if (!(GF_DIAG & 1)) {
         out[i] = o;
     }
-    if (stats && !(GF_DIAG & 2)) { st.pkt(o.reason, o.action, r.len, ab); st.add(264 + (o.ct_ret & 3)); }
+    if (stats && !(GF_DIAG & 2)) { st.add(o.reason); st.add(256 + o.action); ln.sc.add(r.len, ab, o.ct_ret & 3u, st); }
 }
 
 __device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, int added, uint32_t *ct_count,
@@ -1405,6 +1428,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         }
     }
     ln.acc.flush(X);
+    if (stats) ln.sc.fold(st);
     flush_added(X, F ? 2u : 1u, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
 }

@@ -401,3 +401,33 @@ def test_stream_kernels_grid_stride(monkeypatch):
         _cmp_struct(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
         assert np.array_equal(snap.cpu().numpy(), rs), f"rewritten frames b{bi}"
         assert np.array_equal(nd6.cpu().numpy(), rn6), f"pipeline nd6 b{bi}"
+
+
+def test_ingress_counter_block():
+    """k_ing_groups' counter block (reason / action bins shared, byte sums and
+    CT-result counts kept per lane and folded at the end) equals the histogram
+    of the oracle's handle_policy outputs."""
+    import ctypes as C
+    from cilium_amd._lib import lib
+    sc = synth.fuzz(seed=13, n_packets=30_001, n_batches=2)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    cnt = torch.zeros(512, dtype=torch.int64, device="cuda")
+    want = np.zeros(512, dtype=np.int64)
+    for bi, pk in enumerate(sc.batches):
+        b = DeviceBatch(pk)
+        lib.gf_set_stats_sink(C.c_void_p(cnt.data_ptr()))
+        try:
+            io = dp.ingress(b, sc.now + bi)
+            torch.cuda.synchronize()
+        finally:
+            lib.gf_set_stats_sink(None)
+        ro = ref.ingress(pk, sc.now + bi)
+        _cmp_struct(to_numpy(io, ING_OUT), ro, f"ingress b{bi}")
+        np.add.at(want, ro["reason"].astype(np.int64), 1)
+        np.add.at(want, 256 + ro["action"].astype(np.int64), 1)
+        np.add.at(want, 264 + (ro["ct_ret"].astype(np.int64) & 3), 1)
+        want[268] += pk.n
+        want[269] += np.asarray(pk.lens, dtype=np.int64).sum()
+    c = cnt.cpu().numpy()
+    assert np.array_equal(c[:270], want[:270]), np.nonzero(c[:270] != want[:270])
+    assert c[270] > 0
