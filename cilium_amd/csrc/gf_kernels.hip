@@ -2243,6 +2243,8 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
     const uint8_t *src = fr.snap + (size_t)i * S;
     const uint32_t cap0 = S < len ? S : len;
     const bool v6 = i < fr.n && len >= 14 && fbyte(src, cap0, 12) == 0x86 && fbyte(src, cap0, 13) == 0xDD;
+    bool scnt = false;                                        // the lane's counter-block entry
+    uint32_t sreason = 0, saction = 0, slen = 0, sab = 0;
     if (i < fr.n && v6 == (FAM == 6)) {
         const uint32_t K = eg_stage_bytes(S);
         uint8_t *dst = E.snap + (size_t)i * S;
@@ -2382,13 +2384,13 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
                 } else o.action = (uint8_t)ret;
             }
             out[i] = o;
-            if (stats) st.pkt(o.reason, o.action, len, ab);
+            scnt = true; sreason = o.reason; saction = o.action; slen = len; sab = ab;
         }
         erec[i] = r;
         keys[i] = key;
         if (FAM == 4) eg_copy(dst, row, K);                   // the frame as the front left it
     }
-    if (stats) st.flush(stats);
+    if (stats) { st.pkt_wave(scnt, sreason, saction, slen, sab); st.flush(stats); }
 }
 
 // After the front: a flagged batch runs as one bucket per family (every IPv4
@@ -2869,7 +2871,11 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
+    __shared__ uint32_t lsum[3 * BLOCK];                // the lane's packets / wire bytes / algorithmic bytes
     Stats st{sl};
+    uint32_t *ls = lsum + 3 * threadIdx.x;
+    ls[0] = ls[1] = ls[2] = 0;
+    auto fold = [&]() { st.add_n(268, ls[0]); st.add_n(269, ls[1]); st.add_n(270, ls[2]); ls[0] = ls[1] = ls[2] = 0; };
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
     uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
@@ -2933,7 +2939,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
                     atomicAdd(E.ctlog_n + 1, 1u);       // the ingress pass needs its IPv6 kernel
                 }
-                if (stats) st.add_n(270, ab);
+                if (stats) { ls[2] += ab; if (ls[2] >= 0xf0000000u) fold(); }
             } else {
                 if (ret < 0 || ret == TC_SHOT) {
                     o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -2945,7 +2951,11 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     o.ifindex_lo = (uint16_t)ifx;
                 }
                 key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
-                if (stats) st.pkt(o.reason, o.action, r.len, ab);
+                if (stats) {
+                    st.add(o.reason); st.add(256 + o.action);
+                    ls[0] += 1; ls[1] += r.len; ls[2] += ab;
+                    if (ls[1] >= 0xf0000000u || ls[2] >= 0xf0000000u) fold();
+                }
             }
             rec2[i] = rr;
             out[i] = o;
@@ -2956,7 +2966,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
         __syncthreads();
         if (threadIdx.x == 0 && sadd && ct_count) atomicAdd(ct_count, sadd);
     }
-    if (stats) st.flush(stats);
+    if (stats) { fold(); st.flush(stats); }
 }
 
 // The deferred service entries of a launch, in batch order (k_px_apply's rule):

@@ -431,3 +431,32 @@ def test_ingress_counter_block():
     c = cnt.cpu().numpy()
     assert np.array_equal(c[:270], want[:270]), np.nonzero(c[:270] != want[:270])
     assert c[270] > 0
+
+
+def test_egress_counter_block():
+    """The endpoint-egress leg's counter block (k_eg_front wave-aggregated,
+    k_eg_groups per-lane sums, local deliveries counted by handle_policy): one
+    count per packet in its final reason / action bin, packets and wire bytes."""
+    import ctypes as C
+    from cilium_amd._lib import lib
+    from cilium_amd.datapath import EG_OUT
+    sc = synth.egress_fuzz(seed=8, n_packets=20001, n_batches=2, hazard=False)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    cnt = torch.zeros(512, dtype=torch.int64, device="cuda")
+    want = np.zeros(512, dtype=np.int64)
+    for bi, pk in enumerate(sc.batches):
+        lib.gf_set_stats_sink(C.c_void_p(cnt.data_ptr()))
+        try:
+            out, _ = dp.egress(DeviceBatch(pk, parse=False), sc.now + bi)
+            torch.cuda.synchronize()
+        finally:
+            lib.gf_set_stats_sink(None)
+        ro, _ = ref.egress(pk, sc.now + bi)
+        _cmp_struct(to_numpy(out, EG_OUT), ro, f"egress b{bi}")
+        np.add.at(want, ro["reason"].astype(np.int64), 1)
+        np.add.at(want, 256 + ro["action"].astype(np.int64), 1)
+        want[268] += pk.n
+        want[269] += np.asarray(pk.lens, dtype=np.int64).sum()
+    c = cnt.cpu().numpy()
+    assert c[268] == want[268] and c[269] == want[269]
+    assert np.array_equal(c[:264], want[:264]), np.nonzero(c[:264] != want[:264])
