@@ -35,7 +35,7 @@ GF_STATS_WORDS = 512
 class gf_map_info(C.Structure):
     _fields_ = [("map_type", C.c_uint32), ("key_size", C.c_uint32), ("value_size", C.c_uint32),
                 ("max_entries", C.c_uint32), ("map_flags", C.c_uint32), ("n_entries", C.c_uint32),
-                ("device_bytes", C.c_uint64)]
+                ("device_bytes", C.c_uint64), ("xfer_d2h", C.c_uint64), ("xfer_h2d", C.c_uint64)]
 
 
 class gf_pkt_cols(C.Structure):
@@ -135,6 +135,8 @@ _sig("gf_map_delete_elem", C.c_int, C.c_int, VP)
 _sig("gf_map_get_next_key", C.c_int, C.c_int, VP, VP)
 _sig("gf_map_update_batch", C.c_int, C.c_int, VP, VP, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32))
 _sig("gf_map_get_info", C.c_int, C.c_int, C.POINTER(gf_map_info))
+_sig("gf_map_lookup_batch", C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), VP, VP,
+     C.POINTER(C.c_uint32))
 _sig("gf_obj_pin", C.c_int, C.c_int, C.c_char_p)
 _sig("gf_obj_get", C.c_int, C.c_char_p)
 _sig("gf_obj_close", C.c_int, C.c_int)
@@ -153,6 +155,14 @@ _sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c
 _sig("gf_pipeline_load", C.c_int, C.POINTER(gf_pipeline_cfg))
 _sig("gf_pipeline_classify", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, VP, VP, VP, VP)
 _sig("gf_ct_gc", C.c_int, C.c_int, C.c_uint32, VP)
+
+
+class gf_ct_evict_rec(C.Structure):
+    _fields_ = [("seq", C.c_uint32), ("now_sec", C.c_uint32), ("cut_closing", C.c_uint64),
+                ("cut_other", C.c_uint64), ("evicted", C.c_uint64)]
+
+
+_sig("gf_ct_evict_log", C.c_int, C.c_int, C.POINTER(gf_ct_evict_rec), C.c_uint32)
 _sig("gf_pipeline_partition", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, C.c_uint32, VP, VP, VP, VP)
 _sig("gf_lxc_egress_classify", C.c_int, C.c_int, C.POINTER(gf_lxc_batch), C.c_uint32, VP, VP, VP)
 _sig("gf_set_event_ring", C.c_int, C.POINTER(gf_event_ring))
@@ -170,10 +180,10 @@ _sig("gf_version", C.c_char_p)
 # Every symbol the C header declares (checked by tests/test_abi.py).
 EXPORTED = [
     "gf_map_create", "gf_map_update_elem", "gf_map_lookup_elem", "gf_map_delete_elem",
-    "gf_map_get_next_key", "gf_map_update_batch", "gf_map_get_info", "gf_obj_pin", "gf_obj_get",
+    "gf_map_get_next_key", "gf_map_update_batch", "gf_map_lookup_batch", "gf_map_get_info", "gf_obj_pin", "gf_obj_get",
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
 ]

@@ -8,6 +8,8 @@ import ctypes as C
 import errno
 import os
 
+import numpy as np
+
 from ._lib import lib, gf_map_info
 
 # pkg/bpf/bpf.go:38-52
@@ -99,6 +101,22 @@ def GetNextKey(fd, key, keySize):
     return nk.raw
 
 
+def LookupBatch(fd, cursor, count, keySize, valueSize):
+    """gf_map_lookup_batch (chunked dump): up to `count` entries after `cursor`
+    (None = from the start).  Returns (keys uint8[n, keySize], values
+    uint8[n, valueSize], next_cursor, done)."""
+    keys = np.empty((count, keySize), np.uint8)
+    vals = np.empty((count, valueSize), np.uint8)
+    cin = C.c_uint64(cursor or 0)
+    cout = C.c_uint64(0)
+    n = C.c_uint32(count)
+    rc = lib.gf_map_lookup_batch(fd, C.byref(cin) if cursor is not None else None, C.byref(cout),
+                                 keys.ctypes.data, vals.ctypes.data, C.byref(n))
+    if rc and rc != -errno.ENOENT:
+        raise _err("Unable to dump map (batch)", rc)
+    return keys[:n.value], vals[:n.value], cout.value, rc == -errno.ENOENT
+
+
 def UpdateBatch(fd, keys, values, n, flags=BPF_ANY):
     done = C.c_uint32(0)
     rc = lib.gf_map_update_batch(fd, keys, values, n, flags, C.byref(done))
@@ -139,6 +157,8 @@ class MapInfo:
         self.Flags = i.map_flags
         self.Entries = i.n_entries
         self.DeviceBytes = i.device_bytes
+        self.XferD2H = i.xfer_d2h
+        self.XferH2D = i.xfer_h2d
 
 
 def GetMapInfo(fd):
@@ -207,7 +227,25 @@ class Map:
     def GetNextKey(self, key):
         return GetNextKey(self.fd, key, self.KeySize)
 
-    def DumpWithCallback(self, cb):
+    def DumpWithCallback(self, cb, chunk=4096):
+        """map.go:319-369: cb(key, value) for every entry (chunked dump)."""
+        cursor, done = None, False
+        while not done:
+            k, v, cursor, done = LookupBatch(self.fd, cursor, chunk, self.KeySize, self.ValueSize)
+            for i in range(len(k)):
+                cb(k[i].tobytes(), v[i].tobytes())
+
+    def DumpArrays(self, chunk=1 << 20):
+        """Every entry as (keys uint8[n, KeySize], values uint8[n, ValueSize])."""
+        ks, vs = [], []
+        cursor, done = None, False
+        while not done:
+            k, v, cursor, done = LookupBatch(self.fd, cursor, chunk, self.KeySize, self.ValueSize)
+            ks.append(k); vs.append(v)
+        return np.concatenate(ks), np.concatenate(vs)
+
+    def DumpKeyByKey(self, cb):
+        """The reference loop itself: GetNextKey + LookupElement per entry."""
         key = None
         while True:
             try:

@@ -148,6 +148,11 @@ GF_HD void gf_pol_decode(const uint8_t *in, uint8_t *ext) {
     __builtin_memcpy(ext + 2, in + 18, 6);
 }
 #define GF_CT_VSZ 48u
+// CT maps (the datapath inserts into them) get a fixed slot array of
+// GF_CT_SLOT_FACTOR x max_entries slots (a 1/4-loaded table; HBM is plentiful).
+#ifndef GF_CT_SLOT_FACTOR
+#define GF_CT_SLOT_FACTOR 4
+#endif
 GF_HD void gf_ct_encode(const uint8_t *ext, uint8_t *in) {
     const int map[12] = {8, 9, 0, 2, 1, 3, 4, 5, 6, 7, 10, 11};   // internal word k <- reference word map[k]
     uint32_t w[12];

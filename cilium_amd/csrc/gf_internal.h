@@ -12,7 +12,17 @@
 
 namespace gf {
 
-std::recursive_mutex &big_lock();
+// Locking (the reference: one RWMutex per bpf.Map, pkg/bpf/map.go:121, and
+// per-element RCU in the kernel):
+//  * every map operation holds that map's own mutex (Map::mu);
+//  * program objects, the cilium_policy arrays, node config and the classify
+//    calls (which share the per-call device workspaces) hold prog_lock(), and a
+//    classify also holds the mutex of every map it binds while it syncs them
+//    (MapLocks, address order, so two classify calls or a classify and a map
+//    operation never deadlock);
+//  * the object registry (handles, pins) has its own short lock.
+std::recursive_mutex &prog_lock();
+std::mutex &reg_lock();
 
 // ---- device buffer ----
 struct DevBuf {
@@ -64,13 +74,26 @@ struct Obj {
 
 struct Map : Obj {
     uint32_t type, ksz, vsz, max_entries, flags;
+    std::recursive_mutex mu;    // this map's lock (pkg/bpf/map.go:121)
     // hash types
     HTab ht;
     bool host_valid = true;     // host shadow up to date
     bool dev_valid = false;     // HBM replica up to date
     bool fixed_capacity = false; // device inserts into this map (CT): nslots sized by max_entries
     uint64_t dev_count_hi = 0;  // upper bound of the device element count (classify bookkeeping)
+    uint64_t dev_gen = 0;       // bumped on every device-side change (invalidates nk_cache)
+    uint64_t xfer_d2h = 0, xfer_h2d = 0;   // bytes the map API moved over PCIe (gf_map_info)
     DevBuf d_slots, d_vals, d_count;
+    DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits
+    uint32_t lru_seq = 0;       // classify calls that used this map (the eviction log's batch number)
+    // get_next_key over a device-authoritative map: a host copy of one chunk of
+    // slot headers, and the slot of the key returned last (the dump loop's next
+    // argument) so a walk is not needed to resume.
+    std::vector<uint8_t> nk_cache;
+    uint64_t nk_base = 0, nk_n = 0, nk_gen = ~0ull;
+    std::string nk_last_key;
+    int64_t nk_last_slot = -1;
+    uint64_t nk_last_gen = ~0ull;
     // LPM
     std::map<std::string, std::string, LpmKeyLess> lpm;   // orig key bytes -> value
     uint32_t lpm_len_cnt[129] = {0};
@@ -92,7 +115,17 @@ struct Map : Obj {
     // coherence
     int pull();                       // device -> host if !host_valid
     int push(hipStream_t s);          // host -> device if !dev_valid / trie dirty
-    void device_modified() { host_valid = false; }
+    void device_modified() { host_valid = false; dev_gen++; }
+    // Element access on the HBM replica of a device-authoritative hash map (the
+    // datapath wrote it last): walks the key's probe sequence with small reads
+    // instead of pulling the whole table back (a CT map is tens of GB).
+    bool dev_auth() const { return !is_lpm() && !host_valid && dev_valid && d_slots.p; }
+    int dev_find(const uint8_t *key, int64_t &slot, int64_t &ins);   // slot: -1 absent; ins: first TOMB/EMPTY
+    int dev_get_val(uint64_t i, uint8_t *ext);                       // reference layout
+    int dev_put_val(uint64_t i, const uint8_t *ext);
+    int dev_count(uint32_t &c);
+    int dev_set_count(uint32_t c);
+    int dev_next_full(uint64_t start, int64_t &slot);                // first FULL slot >= start, or -1
     void make_fixed_capacity(uint32_t factor = 2);
     void set_hash_mode(uint32_t mode);   // role-specific hashing (gf_key_hash), rehashes
     void set_value_codec(uint32_t codec); // role-specific value layout, converts stored values
@@ -149,5 +182,28 @@ uint64_t *stats_sink();
 // trie builder (host)
 void build_trie(const Map &m, std::vector<uint32_t> &root, std::vector<uint8_t> &nodes,
                 uint32_t &root_bits);
+
+// Chunked dump of a device-authoritative hash map (gf_kernels.hip): the FULL
+// slots of [start, start + range) in slot order, at most `max` of them, keys and
+// reference-layout values copied to the host arrays; *next = the slot after the
+// last one examined.
+int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals, uint32_t *n, uint64_t *next);
+
+// Bulk insert into a fixed-capacity hash map on the device (gf_map_update_batch
+// of >= 4096 entries into an empty or device-authoritative CT-like map), exactly
+// the outcome of the sequential updates: *fallback when it cannot guarantee that
+// (duplicate keys in the batch, NOEXIST over an existing key, a batch that could
+// exceed the element ceiling, no GPU), in which case nothing was written.
+int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n, uint64_t flags, bool &fallback);
+
+// Locks the mutexes of a set of maps in address order (deadlock-free), for the
+// duration of a classify call's host part.
+struct MapLocks {
+    std::vector<Map *> held;
+    bool locked = false;
+    void add(const std::shared_ptr<Map> &m) { if (m && !locked) held.push_back(m.get()); }
+    void lock();
+    ~MapLocks();
+};
 
 }  // namespace gf

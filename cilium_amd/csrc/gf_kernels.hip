@@ -14,6 +14,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
+#include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/discard_iterator.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
@@ -31,9 +32,6 @@ using namespace gfd;
 // Tuning knobs of the flow-group kernel (tools/variants.sh sweeps them).
 #ifndef GF_PREFETCH_REC
 #define GF_PREFETCH_REC 0   // load the lane's next packet record while the current one runs
-#endif
-#ifndef GF_CT_SLOT_FACTOR
-#define GF_CT_SLOT_FACTOR 4 // CT slots per max_entries (a 1/4-loaded table; HBM is plentiful)
 #endif
 #ifndef GF_KEY_BITS
 #define GF_KEY_BITS 32      // bucket key: family bit + (GF_KEY_BITS-1) bits of the group hash
@@ -1819,17 +1817,27 @@ __global__ __launch_bounds__(BLOCK) void k_partition(gf_frames fr, const uint32_
     atomicAdd(&counts[r], 1u);
 }
 
-// ================================================================ CT garbage collection
+// ================================================================ CT garbage collection / LRU eviction
 // ctmap.GC / Flush (pkg/maps/ctmap/ctmap.go:277-368, GCFilterByTime): delete every
-// entry with lifetime < filter_time.  On the device the sweep also compacts each
-// probe cluster (a maximal run of non-EMPTY slots) in place, so deleted entries
-// and the tombstones of ct_delete leave EMPTY slots behind: k_gc_starts marks
-// the cluster starts (a non-EMPTY slot after an EMPTY one) on the unmodified
-// table, then k_gc_clusters walks each cluster with one lane, dropping expired
-// entries and tombstones and moving every live entry to the first EMPTY slot at
-// or after its home — the invariant lookups rely on (no EMPTY slot between a
-// key's home and the key) holds after the move.
-__global__ __launch_bounds__(BLOCK) void k_gc_starts(gf_htab_desc d, uint32_t *bits) {
+// entry with lifetime < filter_time.  The LRU stand-in (below) deletes by the same
+// sweep with two cutoffs: closing entries (rx_closing or tx_closing set) with
+// lifetime < cut_c, the others with lifetime < cut_o.  On the device the sweep
+// also compacts each probe cluster (a maximal run of non-EMPTY slots) in place,
+// so deleted entries and the tombstones of ct_delete leave EMPTY slots behind:
+// k_gc_starts marks the cluster starts (a non-EMPTY slot after an EMPTY one) on
+// the unmodified table, then k_gc_clusters walks each cluster with one lane,
+// dropping deleted entries and tombstones and moving every live entry to the
+// first EMPTY slot at or after its home — the invariant lookups rely on (no
+// EMPTY slot between a key's home and the key) holds after the move.
+// Cutoffs live in device memory so an eviction decided on the device (no host
+// round trip) runs the same two kernels; active == 0 makes them no-ops.
+struct GcCut {
+    unsigned long long c, o;      // closing / other entries: deleted iff their age key < cut
+    uint32_t active;
+    uint32_t lru;                 // age key: 0 = lifetime (ctmap.GC), 1 = last use (the LRU stand-in)
+};
+__global__ __launch_bounds__(BLOCK) void k_gc_starts(gf_htab_desc d, uint32_t *bits, const GcCut *cut) {
+    if (!cut->active) return;
     const uint64_t nw = (d.mask + 1 + 31) / 32;
     for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t m = 0;
@@ -1857,10 +1865,25 @@ __device__ __forceinline__ void gc_move(const gf_htab_desc &d, uint64_t from, ui
 }
 
 // lt_off: byte offset of ct_entry.lifetime within the value bytes ht_val points at
-// (0 in the CT codec's hot block, 32 in the reference layout).  res[0] += deleted
-// entries, res[1] += tombstones cleared.
-__global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
+// (0 in the CT codec's hot block, 32 in the reference layout); the flags word
+// follows it in both.  res[0] += deleted entries, res[1] += tombstones cleared.
+// The time of an entry's last update: every writer of ct_entry.lifetime sets it to
+// now + the timeout its flags select (conntrack.h:47-62, 127, 527): CT_CLOSE_TIMEOUT
+// once both directions close, CT_DEFAULT_LIFETIME after a non-SYN packet, else
+// CT_SYN_TIMEOUT.  lifetime - that timeout is exact to the second.
+__device__ __forceinline__ long long ct_last_use(uint32_t lt, uint32_t fl) {
+    const uint32_t to = ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) ? 10u : ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+    return (long long)lt - (long long)to;
+}
+__device__ __forceinline__ bool gc_kill(uint32_t lt, uint32_t fl, const GcCut &c) {
+    const long long k = c.lru ? ct_last_use(lt, fl) : (long long)lt;
+    const unsigned long long cut = (fl & (F_RX_CLOSING | F_TX_CLOSING)) ? c.c : c.o;
+    return k < 0 || (unsigned long long)k < cut;
+}
+__global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t mode, uint32_t lt_off, const GcCut *cutp,
                                                        const uint32_t *bits, unsigned long long *res) {
+    if (!cutp->active) return;
+    const GcCut cut = *cutp;
     const uint64_t nw = (d.mask + 1 + 31) / 32;
     const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
     uint32_t dead = 0, tombs = 0;
@@ -1878,16 +1901,16 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
                     sl[d.ksz] = GF_SLOT_EMPTY;
                     tombs++;
                 } else {
-                    const uint32_t lt = *reinterpret_cast<const uint32_t *>(ht_val(d, j) + lt_off);
-                    if (lt < now) {
+                    const uint8_t *v = ht_val(d, j) + lt_off;
+                    const uint32_t lt = *reinterpret_cast<const uint32_t *>(v);
+                    const uint32_t fl = *reinterpret_cast<const uint16_t *>(v + 4);
+                    if (gc_kill(lt, fl, cut)) {
                         sl[d.ksz] = GF_SLOT_EMPTY;
                         dead++;
                     } else {
                         uint32_t kw[10];
-                        const uint32_t nkw = (d.ksz + 3) / 4;
                         for (uint32_t q = 0; q < 10; q++) kw[q] = 0;
                         for (uint32_t q = 0; q < d.ksz; q++) kw[q >> 2] |= (uint32_t)sl[q] << (8 * (q & 3));
-                        (void)nkw;
                         const uint64_t home = gf_home_slot(gf_key_hash(kw, d.ksz, mode), d.mask, d.slot_size);
                         for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
                             if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) { gc_move(d, j, p, vstride); break; }
@@ -1900,6 +1923,135 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
     }
     if (dead) atomicAdd(&res[0], (unsigned long long)dead);
     if (tombs) atomicAdd(&res[1], (unsigned long long)tombs);
+}
+
+// ---- LRU stand-in (CT maps are BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:53-75;
+// ctmap.go:38-39).  The kernel never fails an LRU insert: it evicts an entry
+// from its per-CPU LRU lists, in an order that is not reproducible.  Here an
+// LRU CT map may exceed max_entries inside a batch (the slot array has room);
+// at the end of every classify call that inserts into it, if the device count
+// exceeds max_entries, the least recently used entries are evicted until the
+// count is at most the low watermark max_entries - max_entries/8.  Age order:
+// closing entries (rx_closing or tx_closing: the connection is being torn down)
+// first, then the others, each by ascending last use (ct_last_use) in whole
+// one-second bins relative to `now` (bin 0 holds everything last used 65535 s
+// or more ago).  The smallest prefix of that order that reaches the watermark
+// is deleted by the GC sweep above — a deterministic rule the oracle restates
+// (o_ct_lru_cutoffs), and every eviction is logged (gf_ct_evict_log).
+#define GF_LRU_BINS 65536u
+#define GF_LRU_LOGCAP 4096u
+struct LruLog { uint32_t seq, now; unsigned long long cut_c, cut_o, evicted; };
+struct LruDev {
+    uint32_t hist[2 * GF_LRU_BINS];
+    GcCut cut;
+    unsigned long long res[2];
+    unsigned long long target;
+    uint32_t flag, nlog;
+    LruLog log[GF_LRU_LOGCAP];
+};
+__device__ __forceinline__ uint32_t lru_key(uint32_t lt, uint32_t fl, uint32_t now) {
+    const long long base = (long long)now - (long long)(GF_LRU_BINS - 1);
+    long long b = ct_last_use(lt, fl) - base;
+    b = b < 0 ? 0 : (b > (long long)(GF_LRU_BINS - 1) ? (long long)(GF_LRU_BINS - 1) : b);
+    return ((fl & (F_RX_CLOSING | F_TX_CLOSING)) ? 0u : GF_LRU_BINS) + (uint32_t)b;
+}
+__global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev *L) {
+    const uint32_t c = *count;
+    const bool f = c > max_entries;
+    if (threadIdx.x == 0) {
+        L->flag = f ? 1u : 0u;
+        L->cut.active = 0;
+        L->res[0] = L->res[1] = 0;
+        L->target = (unsigned long long)(max_entries - max_entries / 8u);
+    }
+    if (f)
+        for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
+}
+// Age histogram: wave-aggregated (a wave's entries mostly share a bin), then a
+// block-local direct-mapped LDS cache of bins, flushed with one global add each.
+#define GF_LRU_LDS 1024u
+__global__ __launch_bounds__(BLOCK) void k_lru_hist(gf_htab_desc d, uint32_t lt_off, uint32_t now, LruDev *L) {
+    if (!L->flag) return;
+    __shared__ uint32_t tag[GF_LRU_LDS], cnt[GF_LRU_LDS];
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) { tag[k] = ~0u; cnt[k] = 0; }
+    __syncthreads();
+    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < ns; b0 += stride) {   // wave-uniform trips
+        const uint64_t i = b0 + threadIdx.x;
+        uint32_t key = ~0u;
+        if (i < ns && d.slots[i * d.slot_size + d.ksz] == GF_SLOT_FULL) {
+            const uint8_t *v = ht_val(d, i) + lt_off;
+            key = lru_key(*reinterpret_cast<const uint32_t *>(v), *reinterpret_cast<const uint16_t *>(v + 4), now);
+        }
+        uint64_t rem = __ballot(key != ~0u);
+        while (rem) {
+            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
+            const uint32_t k = __shfl(key, (int)lead);
+            const uint64_t m = __ballot(key == k) & rem;
+            if (lane == lead) {
+                const uint32_t n = (uint32_t)__popcll(m), h = k & (GF_LRU_LDS - 1u);
+                uint32_t t = atomicCAS(&tag[h], ~0u, k);
+                if (t == ~0u || t == k) atomicAdd(&cnt[h], n);
+                else atomicAdd(&L->hist[k], n);
+            }
+            rem &= ~m;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x)
+        if (tag[k] != ~0u && cnt[k]) atomicAdd(&L->hist[tag[k]], cnt[k]);
+}
+// The smallest prefix of the age order whose removal leaves <= target entries:
+// one block scans the 2 x 65536 bins (128 per thread, then a block scan).
+__global__ __launch_bounds__(1024) void k_lru_cut(const uint32_t *count, uint32_t now, LruDev *L) {
+    if (!L->flag) return;
+    __shared__ unsigned long long part[1024];
+    constexpr uint32_t PER = 2 * GF_LRU_BINS / 1024;
+    const uint32_t t = threadIdx.x;
+    unsigned long long s = 0;
+    for (uint32_t k = 0; k < PER; k++) s += L->hist[t * PER + k];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan
+        unsigned long long v = t >= o ? part[t - o] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const unsigned long long c = *count, need = c > L->target ? c - L->target : 0ull;
+    const unsigned long long before = t ? part[t - 1] : 0ull;
+    if (need == 0) { if (t == 0) L->flag = 0; return; }
+    if (before < need && part[t] >= need) {              // the cut bin lies in this thread's range
+        unsigned long long acc = before;
+        uint32_t kb = t * PER;
+        for (uint32_t k = 0; k < PER; k++) {
+            acc += L->hist[t * PER + k];
+            if (acc >= need) { kb = t * PER + k; break; }
+        }
+        // delete bins [0, kb]: cutoffs in last-use terms
+        const long long base = (long long)now - (long long)(GF_LRU_BINS - 1);
+        auto cut_of = [&](uint32_t b) -> unsigned long long {   // bins [0, b] of a class -> lifetime < cut
+            const long long v = base + (long long)b + 1;
+            return b == GF_LRU_BINS - 1 ? (1ull << 32) : (v <= 0 ? 0ull : (unsigned long long)v);
+        };
+        if (kb < GF_LRU_BINS) { L->cut.c = cut_of(kb); L->cut.o = 0; }
+        else { L->cut.c = 1ull << 32; L->cut.o = cut_of(kb - GF_LRU_BINS); }
+        L->cut.lru = 1;
+        L->cut.active = 1;
+    }
+}
+__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L) {
+    if (!L->cut.active) return;
+    const unsigned long long ev = L->res[0];
+    *count = (uint32_t)(*count - ev);
+    const uint32_t k = L->nlog;
+    if (k < GF_LRU_LOGCAP) {
+        L->log[k].seq = seq; L->log[k].now = now;
+        L->log[k].cut_c = L->cut.c; L->log[k].cut_o = L->cut.o; L->log[k].evicted = ev;
+    }
+    L->nlog = k + 1;
+    L->cut.active = 0;
 }
 
 // ================================================================ drop notifications
@@ -3085,6 +3237,39 @@ uint32_t stream_grid(uint32_t n, uint32_t per_block = BLOCK) {
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
 
+// ---- locking and cross-stream ordering of the calls that share the device
+// workspaces (ws(), pipe_ws(), eg_ws(), px_ws(), the event / partition / GC
+// buffers).  Calls run one at a time on the host (prog_lock), and on the device
+// each call is ordered after the previous one even when the caller switches
+// streams: the call waits on an event recorded at the end of the last call, so a
+// kernel still reading a workspace (or a map replica) on another stream finishes
+// before this call rewrites it.
+struct CallOrder {
+    hipStream_t s;
+    explicit CallOrder(hipStream_t s_) : s(s_) {
+        auto &o = state();
+        if (o.have && o.last != s) (void)hipStreamWaitEvent(s, o.ev, 0);
+    }
+    ~CallOrder() {
+        auto &o = state();
+        if (!o.ev && hipEventCreateWithFlags(&o.ev, hipEventDisableTiming) != hipSuccess) { o.ev = nullptr; return; }
+        if (hipEventRecord(o.ev, s) == hipSuccess) { o.last = s; o.have = true; }
+    }
+    struct St { hipEvent_t ev = nullptr; hipStream_t last = nullptr; bool have = false; };
+    static St &state() { static St st; return st; }
+};
+void lock_lxc_maps(MapLocks &L, const std::shared_ptr<ProgLxc> &p) {
+    for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6, p->lb4, p->ipcache,
+                   p->cidr4e, p->lb6, p->cidr6e})
+        L.add(m);
+}
+void lock_array_maps(MapLocks &L, const std::shared_ptr<PolicyArray> &a) {
+    for (auto &kv : a->slots) lock_lxc_maps(L, kv.second);
+    L.add(proxy_map(4)); L.add(proxy_map(6)); L.add(node_map(1)); L.add(node_map(2));
+}
+void lock_xdp_maps(MapLocks &L, const ProgXdp &x) { L.add(x.m4h); L.add(x.m4l); L.add(x.m6h); L.add(x.m6l); L.add(x.lxc); }
+
+
 // blocks of BLOCK threads that fill the device at `per_cu` blocks per CU
 uint32_t resident_blocks(uint32_t per_cu) {
     static int cus = 0;
@@ -3114,7 +3299,7 @@ int gf_parse_frames(const gf_frames *fr, gf_pkt_cols_out *o, void *stream) {
 }
 
 int gf_xdp_prog_load(const gf_xdp_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgXdp>();
     p->cfg = *cfg;
@@ -3137,7 +3322,7 @@ int gf_xdp_prog_load(const gf_xdp_cfg *cfg) {
 }
 
 int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(prog);
     if (!o || o->kind != ObjKind::ProgXdp) return -EBADF;
     auto p = std::static_pointer_cast<ProgXdp>(o);
@@ -3145,6 +3330,10 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     if (c <= 0) return c;
     if (!verdict) return -EFAULT;
     hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    lock_xdp_maps(L, *p);
+    L.lock();
+    CallOrder co(s);
     int r;
     if ((r = push_map(p->m4h, s)) || (r = push_map(p->m4l, s)) || (r = push_map(p->m6h, s)) ||
         (r = push_map(p->m6l, s)) || (r = push_map(p->lxc, s)))
@@ -3162,7 +3351,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
 }
 
 int gf_lb_prog_load(const gf_lb_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgLb>();
     p->cfg = *cfg;
@@ -3180,7 +3369,7 @@ int gf_lb_prog_load(const gf_lb_cfg *cfg) {
 }
 
 int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *nd6, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(prog);
     if (!o || o->kind != ObjKind::ProgLb) return -EBADF;
     auto p = std::static_pointer_cast<ProgLb>(o);
@@ -3188,6 +3377,10 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
     if (c <= 0) return c;
     if (!out) return -EFAULT;
     hipStream_t s = (hipStream_t)stream;
+    MapLocks ML;
+    ML.add(p->lb4); ML.add(p->lb6);
+    ML.lock();
+    CallOrder co(s);
     int r;
     if ((r = push_map(p->lb4, s)) || (r = push_map(p->lb6, s))) return r;
     LbDev L{};
@@ -3201,7 +3394,7 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
 }
 
 int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     if (cfg->n_l4_ingress > GF_MAX_L4_INGRESS || cfg->n_l4_egress > GF_MAX_L4_INGRESS ||
         cfg->n_portmap > GF_MAX_PORTMAP)
@@ -3225,6 +3418,9 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
         if (m->ksz != b.k || m->is_lpm() != b.lpm || (!b.lpm && m->vsz != b.v)) return -EINVAL;
         *b.out = m;
     }
+    MapLocks L;
+    lock_lxc_maps(L, p);
+    L.lock();
     if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
     if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
     if (p->policy) { p->policy->set_hash_mode(GF_HASH_POLICY); p->policy->set_value_codec(GF_VCODEC_POL); }
@@ -3232,7 +3428,7 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
 }
 
 int gf_set_event_ring(const gf_event_ring *ring) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!ring) { event_ring() = gf_event_ring{}; return 0; }
     if (!ring->records || !ring->count) return -EFAULT;
     event_ring() = *ring;
@@ -3240,7 +3436,7 @@ int gf_set_event_ring(const gf_event_ring *ring) {
 }
 
 int gf_prof_enable(int on) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     prof_drain();
     prof().acc.clear();
     prof().on = on != 0;
@@ -3248,7 +3444,7 @@ int gf_prof_enable(int on) {
 }
 
 int gf_prof_read(gf_prof_rec *out, int max) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (max < 0 || (max > 0 && !out)) return -EFAULT;
     prof_drain();
     int k = 0;
@@ -3264,12 +3460,12 @@ int gf_prof_read(gf_prof_rec *out, int max) {
 }
 
 int gf_policy_array_create(void) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     return new_handle(std::make_shared<PolicyArray>());
 }
 
 int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     if (lxc_id > 0xffff) return -E2BIG;
@@ -3284,7 +3480,7 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 
 }  // extern "C"
 
-// handle_policy over a batch (caller holds big_lock and checked the columns).
+// handle_policy over a batch (caller holds prog_lock and the maps' locks, and checked the columns).
 // skip (DEVICE, may be null): packets a pipeline ended before the tail call.
 // Drop notifications of one classify call (no-op without an event ring).
 static int emit_drop_events(EvSrc E, hipStream_t s) {
@@ -3549,6 +3745,50 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
     return 0;
 }
 
+// ---- CT sweeps on the device: per-map LRU state (histogram, cutoffs, log) and
+// the cluster-start bits of the GC sweep.
+static int ct_sweep_bufs(Map &m, LruDev *&L, uint32_t *&bits) {
+    if (!m.d_lru.p) {
+        if (m.d_lru.ensure(sizeof(LruDev))) return -ENOMEM;
+        if (hip_ok(hipMemset(m.d_lru.p, 0, sizeof(LruDev)), "lru init")) return -EIO;
+    }
+    const size_t nw = (m.ht.nslots + 31) / 32;
+    if (m.d_gcbits.bytes < nw * 4 && m.d_gcbits.ensure(nw * 4)) return -ENOMEM;
+    L = (LruDev *)m.d_lru.p;
+    bits = (uint32_t *)m.d_gcbits.p;
+    return 0;
+}
+static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
+    const gf_htab_desc d = m.hdesc();
+    const uint32_t lt_off = m.ht.codec == GF_VCODEC_CT ? 0u : 32u;
+    const uint64_t nw = (d.mask + 1 + 31) / 32;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, 65535u * 8);
+    hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, bits, (const GcCut *)&L->cut);
+    hipLaunchKernelGGL(k_gc_clusters, dim3(grid), dim3(BLOCK), 0, s, d, m.ht.mode, lt_off, (const GcCut *)&L->cut,
+                       (const uint32_t *)bits, L->res);
+}
+// The LRU stand-in after a classify call (k_lru_*: see the kernels): fully on the
+// device, a no-op launch chain unless the map's count exceeds max_entries.
+static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s) {
+    if (!m || m->type != GF_MAP_TYPE_LRU_HASH || !m->d_slots.p) return 0;
+    m->lru_seq++;
+    if (m->dev_count_hi <= m->max_entries) return 0;    // cannot have crossed max_entries
+    LruDev *L;
+    uint32_t *bits;
+    int r;
+    if ((r = ct_sweep_bufs(*m, L, bits))) return r;
+    const gf_htab_desc d = m->hdesc();
+    const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
+    ProfScope ps("k_lru_evict", s);
+    hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, (const uint32_t *)d.count, m->max_entries, L);
+    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + BLOCK - 1) / BLOCK, resident_blocks(4));
+    hipLaunchKernelGGL(k_lru_hist, dim3(gh), dim3(BLOCK), 0, s, d, lt_off, now, L);
+    hipLaunchKernelGGL(k_lru_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, now, L);
+    ct_sweep_launch(*m, L, bits, s);
+    hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
+    return hip_ok(hipGetLastError(), "k_lru_evict");
+}
+
 // pack (may be empty): fills the records and bucket keys itself (the fused
 // pipeline front) instead of k_ing_pack; pout: pipeline records to complete.
 using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t *keys)>;
@@ -3644,6 +3884,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
+    if ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s))) return r;
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
     return 0;
@@ -3653,7 +3894,7 @@ extern "C" {
 
 int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
                                void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     auto a = std::static_pointer_cast<PolicyArray>(o);
@@ -3661,12 +3902,16 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (c <= 0) return c;
     if (!out) return -EFAULT;
     if (pkts->n > (1u << 30)) return -E2BIG;
+    MapLocks L;
+    lock_array_maps(L, a);
+    L.lock();
+    CallOrder co((hipStream_t)stream);
     return ingress_run(a, pkts, now_sec, out, (hipStream_t)stream);
 }
 
 // ---- full pipeline ----
 int gf_pipeline_load(const gf_pipeline_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgPipe>();
     p->cfg = *cfg;
@@ -3692,7 +3937,7 @@ int gf_pipeline_load(const gf_pipeline_cfg *cfg) {
 
 int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_pipeline_out *out,
                          uint8_t *nd6, uint8_t *snap_out, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(pipe);
     if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
     auto p = std::static_pointer_cast<ProgPipe>(o);
@@ -3703,6 +3948,13 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     if (fr.snap_stride < 14) return -EINVAL;
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    if (p->xdp) lock_xdp_maps(L, *p->xdp);
+    if (p->lb) { L.add(p->lb->lb4); L.add(p->lb->lb6); }
+    L.add(p->lxc);
+    lock_array_maps(L, p->policy);
+    L.lock();
+    CallOrder co(s);
     int r;
     const uint32_t n = fr.n;
     PipeDev P{};
@@ -3763,7 +4015,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
 // ---- ingest re-partition ----
 int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, uint32_t nranks, uint32_t *owner,
                           uint32_t *order, uint32_t *counts, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(pipe);
     if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
     auto p = std::static_pointer_cast<ProgPipe>(o);
@@ -3771,6 +4023,10 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, 
     if (nranks == 0 || nranks > 65536 || self_rank >= nranks) return -EINVAL;
     const gf_frames &fr = b->frames;
     hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    if (p->lb) { L.add(p->lb->lb4); L.add(p->lb->lb6); }
+    L.lock();
+    CallOrder co(s);
     if (hip_ok(hipMemsetAsync(counts, 0, (size_t)nranks * 4, s), "partition counts")) return -EIO;
     if (fr.n == 0) return 0;
     if (!fr.snap || !fr.len) return -EFAULT;
@@ -3811,14 +4067,17 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, 
 
 // ---- conntrack GC ----
 int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto m = get_map(map);
     if (!m) return -EBADF;
     if (m->is_lpm() || (m->ksz != 14 && m->ksz != 40) || m->vsz != 48) return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::recursive_mutex> mg(m->mu);
+    CallOrder co(s);
     const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
     if (m->host_valid || !m->dev_valid || !m->d_slots.p) {
         // host shadow authoritative: delete there, the replica is rebuilt on the next push
+        if (m->ht.slots.empty()) return 0;              // never materialised: no entries
         uint64_t dead = 0;
         std::vector<std::string> keys;
         uint8_t v[GF_CT_VSZ];
@@ -3832,22 +4091,24 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
         for (auto &k : keys) if (m->erase((const uint8_t *)k.data()) == 0) dead++;
         return (int)std::min<uint64_t>(dead, 0x7fffffff);
     }
-    gf_htab_desc d = m->hdesc();
-    const uint64_t nslots = d.mask + 1, nw = (nslots + 31) / 32;
-    static DevBuf bits, res;
-    if (bits.bytes < nw * 4 && bits.ensure(nw * 4)) return -ENOMEM;
-    if (res.bytes < 16 && res.ensure(16)) return -ENOMEM;
-    if (hip_ok(hipMemsetAsync(res.p, 0, 16, s), "gc res")) return -EIO;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, 65535u * 8);
+    LruDev *L;
+    uint32_t *bits;
+    int rr;
+    if ((rr = ct_sweep_bufs(*m, L, bits))) return rr;
+    GcCut cut{filter_time, filter_time, 1u, 0u};             // lifetime < filter_time
+    const unsigned long long zero2[2] = {0, 0};
+    if (hip_ok(hipMemcpyAsync(&L->cut, &cut, sizeof cut, hipMemcpyHostToDevice, s), "gc cut") ||
+        hip_ok(hipMemcpyAsync(L->res, zero2, sizeof zero2, hipMemcpyHostToDevice, s), "gc res"))
+        return -EIO;
     {
         ProfScope ps("k_gc", s);
-        hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, (uint32_t *)bits.p);
-        hipLaunchKernelGGL(k_gc_clusters, dim3(grid), dim3(BLOCK), 0, s, d, m->ht.mode, lt_off, filter_time,
-                           (const uint32_t *)bits.p, (unsigned long long *)res.p);
+        ct_sweep_launch(*m, L, bits, s);
     }
     if (hip_ok(hipGetLastError(), "k_gc")) return -EIO;
     unsigned long long r[2] = {0, 0};
-    if (hip_ok(hipMemcpyAsync(r, res.p, 16, hipMemcpyDeviceToHost, s), "gc result") ||
+    const GcCut off{0, 0, 0u, 0u};
+    if (hip_ok(hipMemcpyAsync(r, L->res, 16, hipMemcpyDeviceToHost, s), "gc result") ||
+        hip_ok(hipMemcpyAsync(&L->cut, &off, sizeof off, hipMemcpyHostToDevice, s), "gc cut off") ||
         hip_ok(hipStreamSynchronize(s), "gc sync"))
         return -EIO;
     // device element count: entries are deleted, tombstones were already uncounted
@@ -3860,8 +4121,246 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
 
+int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max) {
+    auto m = get_map(map);
+    if (!m) return -EBADF;
+    if (max && !out) return -EFAULT;
+    std::lock_guard<std::recursive_mutex> mg(m->mu);
+    if (!m->d_lru.p) return 0;
+    static_assert(sizeof(LruLog) == sizeof(gf_ct_evict_rec), "log record layout");
+    if (hip_ok(hipDeviceSynchronize(), "evict log sync")) return -EIO;
+    uint32_t n = 0;
+    LruDev *L = (LruDev *)m->d_lru.p;
+    if (hip_ok(hipMemcpy(&n, &L->nlog, 4, hipMemcpyDeviceToHost), "evict log count")) return -EIO;
+    const uint32_t k = std::min(std::min(n, GF_LRU_LOGCAP), max);
+    if (k && hip_ok(hipMemcpy(out, L->log, (size_t)k * sizeof(LruLog), hipMemcpyDeviceToHost), "evict log")) return -EIO;
+    return (int)std::min<uint32_t>(n, 0x7fffffffu);
+}
+
 }  // extern "C"
 
+
+// ================================================================ bulk insert (gf_map_update_batch)
+// A batch of distinct keys loaded straight into a fixed-capacity table in HBM:
+// one lane per element walks the key's probe sequence, overwrites the key's slot
+// (BPF_ANY) or claims the first EMPTY slot with a CAS on its state word (BUSY),
+// fills key and value and publishes FULL with a release store; readers acquire
+// the state word first.  Keys are distinct (checked first), so the outcome is
+// that of the sequential updates.
+__device__ __forceinline__ void bulk_key_words(const uint8_t *k, uint32_t ksz, uint32_t *kw) {
+    for (int q = 0; q < 16; q++) kw[q] = 0;
+    for (uint32_t b = 0; b < ksz; b++) kw[b >> 2] |= (uint32_t)k[b] << (8 * (b & 3));
+}
+__device__ __forceinline__ bool bulk_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
+    for (uint32_t q = 0; q < n; q++) if (a[q] != b[q]) return false;
+    return true;
+}
+__global__ __launch_bounds__(BLOCK) void k_bulk_hash(const uint8_t *keys, uint32_t ksz, uint32_t mode, uint32_t n, uint32_t *h) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t kw[16];
+        bulk_key_words(keys + (size_t)i * ksz, ksz, kw);
+        h[i] = gf_key_hash(kw, ksz, mode);
+    }
+}
+// flag[0]: two equal keys in the batch (equal keys have equal hashes: adjacent runs after the sort)
+__global__ __launch_bounds__(BLOCK) void k_bulk_dups(const uint32_t *hs, const uint32_t *idx, const uint8_t *keys,
+                                                     uint32_t ksz, uint32_t n, uint32_t *flag) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+        for (int64_t k = (int64_t)j - 1; k >= 0 && hs[k] == hs[j]; k--)
+            if (bulk_eq(keys + (size_t)idx[k] * ksz, keys + (size_t)idx[j] * ksz, ksz)) atomicOr(&flag[0], 1u);
+}
+__device__ __forceinline__ uint32_t bulk_state_word(const gf_htab_desc &d, uint64_t j) {
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(d.slots + j * d.slot_size + (d.ksz & ~3u));
+    return __hip_atomic_load(sw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// flag[1]: a key of the batch is already in the table
+__global__ __launch_bounds__(BLOCK) void k_bulk_probe(gf_htab_desc d, const uint8_t *keys, const uint32_t *h, uint32_t n,
+                                                      uint32_t *flag) {
+    const uint32_t sb = 8 * (d.ksz & 3u);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint8_t *k = keys + (size_t)i * d.ksz;
+        uint64_t j = gf_home_slot(h[i], d.mask, d.slot_size);
+        for (uint64_t p = 0; p <= d.mask; p++, j = (j + 1) & d.mask) {
+            const uint32_t st = (bulk_state_word(d, j) >> sb) & 0xffu;
+            if (st == GF_SLOT_EMPTY) break;
+            if (st == GF_SLOT_FULL && bulk_eq(d.slots + j * d.slot_size, k, d.ksz)) { atomicOr(&flag[1], 1u); break; }
+        }
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_bulk_insert(gf_htab_desc d, uint32_t codec, const uint8_t *keys,
+                                                       const uint8_t *vals, const uint32_t *h, uint32_t n) {
+    const uint32_t sb = 8 * (d.ksz & 3u), kw0 = d.ksz & ~3u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint8_t *k = keys + (size_t)i * d.ksz, *ext = vals + (size_t)i * d.vsz;
+        uint8_t in[128];
+        if (codec == GF_VCODEC_CT) gf_ct_encode(ext, in);
+        else if (codec == GF_VCODEC_POL) gf_pol_encode(ext, in);
+        else for (uint32_t b = 0; b < d.vsz; b++) in[b] = ext[b];
+        uint32_t keep = 0;
+        for (uint32_t b = kw0; b < d.ksz; b++) keep |= (uint32_t)k[b] << (8 * (b - kw0));
+        auto put_val = [&](uint64_t j) {
+            uint8_t *sl = d.slots + j * d.slot_size;
+            for (uint32_t b = 0; b < d.vin; b++) sl[d.voff + b] = in[b];
+            for (uint32_t b = d.vin; b < d.vsz; b++) d.vals[j * d.sstride + (b - d.vin)] = in[b];
+        };
+        uint64_t j = gf_home_slot(h[i], d.mask, d.slot_size);
+        for (uint64_t p = 0; p <= d.mask;) {
+            uint32_t *sw = reinterpret_cast<uint32_t *>(d.slots + j * d.slot_size + kw0);
+            uint32_t w = bulk_state_word(d, j);
+            const uint32_t st = (w >> sb) & 0xffu;
+            if (st == GF_SLOT_FULL && bulk_eq(d.slots + j * d.slot_size, k, d.ksz)) { put_val(j); break; }
+            if (st == GF_SLOT_EMPTY) {
+                const uint32_t busy = keep | ((uint32_t)GF_SLOT_BUSY << sb);
+                uint32_t seen = w;
+                __hip_atomic_compare_exchange_strong(sw, &seen, busy, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if (seen != w) continue;                       // lost the slot: look at it again
+                uint8_t *sl = d.slots + j * d.slot_size;
+                for (uint32_t b = 0; b < kw0; b++) sl[b] = k[b];
+                put_val(j);
+                __hip_atomic_store(sw, keep | ((uint32_t)GF_SLOT_FULL << sb), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(d.count, 1u);
+                break;
+            }
+            p++;
+            j = (j + 1) & d.mask;
+        }
+    }
+}
+
+namespace gf {
+int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n, uint64_t flags, bool &fallback) {
+    fallback = true;
+    int dc = 0;
+    if (hipGetDeviceCount(&dc) != hipSuccess || dc == 0 || m.vsz > 128 || m.ksz > 64) return 0;
+    const bool had = m.dev_auth();
+    uint64_t before = 0;
+    if (had) { uint32_t c; if (m.dev_count(c)) return 0; before = c; }
+    const uint64_t limit = m.type == GF_MAP_TYPE_LRU_HASH ? m.ht.nslots / 8 * 7 : m.max_entries;
+    if (before + n > limit) return 0;                   // the host path reports E2BIG at the exact element
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    static DevBuf dk, dv, dh, dhs, didx, tmp, dflag;
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    int r;
+    if ((r = grow(dk, (size_t)n * m.ksz)) || (r = grow(dv, (size_t)n * m.vsz)) || (r = grow(dh, (size_t)n * 4)) ||
+        (r = grow(dhs, (size_t)n * 4)) || (r = grow(didx, (size_t)n * 4)) || (r = grow(dflag, 8)))
+        return r;
+    if (!had) {                                          // create the (empty) replica
+        m.dev_valid = false;
+        if ((r = m.push((hipStream_t)0))) return r;
+    }
+    const hipStream_t s = (hipStream_t)0;
+    if (hip_ok(hipMemcpy(dk.p, keys, (size_t)n * m.ksz, hipMemcpyHostToDevice), "bulk keys") ||
+        hip_ok(hipMemcpy(dv.p, vals, (size_t)n * m.vsz, hipMemcpyHostToDevice), "bulk vals") ||
+        hip_ok(hipMemset(dflag.p, 0, 8), "bulk flags"))
+        return -EIO;
+    m.xfer_h2d += (size_t)n * (m.ksz + m.vsz);
+    const gf_htab_desc d = m.hdesc();
+    const uint32_t g = std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 65535u);
+    hipLaunchKernelGGL(k_bulk_hash, dim3(g), dim3(BLOCK), 0, s, (const uint8_t *)dk.p, m.ksz, m.ht.mode, n, (uint32_t *)dh.p);
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)dh.p, (uint32_t *)dhs.p, rocprim::counting_iterator<uint32_t>(0u),
+                                    (uint32_t *)didx.p, n, 0, 32, s);
+    if ((r = grow(tmp, tb + 256))) return r;
+    tb = tmp.bytes;
+    if (hip_ok(rocprim::radix_sort_pairs(tmp.p, tb, (uint32_t *)dh.p, (uint32_t *)dhs.p, rocprim::counting_iterator<uint32_t>(0u),
+                                         (uint32_t *)didx.p, n, 0, 32, s), "bulk sort"))
+        return -EIO;
+    hipLaunchKernelGGL(k_bulk_dups, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)dhs.p, (const uint32_t *)didx.p,
+                       (const uint8_t *)dk.p, m.ksz, n, (uint32_t *)dflag.p);
+    if (had && flags == GF_NOEXIST)
+        hipLaunchKernelGGL(k_bulk_probe, dim3(g), dim3(BLOCK), 0, s, d, (const uint8_t *)dk.p, (const uint32_t *)dh.p, n,
+                           (uint32_t *)dflag.p);
+    uint32_t fl[2] = {0, 0};
+    if (hip_ok(hipGetLastError(), "bulk check") || hip_ok(hipMemcpy(fl, dflag.p, 8, hipMemcpyDeviceToHost), "bulk flags"))
+        return -EIO;
+    if (fl[0] || fl[1]) return 0;                        // duplicates / EEXIST: the sequential host path
+    hipLaunchKernelGGL(k_bulk_insert, dim3(g), dim3(BLOCK), 0, s, d, m.ht.codec, (const uint8_t *)dk.p,
+                       (const uint8_t *)dv.p, (const uint32_t *)dh.p, n);
+    if (hip_ok(hipGetLastError(), "k_bulk_insert") || hip_ok(hipDeviceSynchronize(), "bulk sync")) return -EIO;
+    m.host_valid = false;
+    m.dev_gen++;
+    m.dev_count_hi = before + n;
+    fallback = false;
+    return 0;
+}
+}  // namespace gf
+
+// ================================================================ chunked dump (gf_map_lookup_batch)
+// The FULL slots of a range of a device-authoritative hash map, compacted in
+// slot order on the device (rocPRIM select over the slot indices), their keys
+// and reference-layout values gathered into a staging buffer: only the entries
+// cross PCIe, a 64M-entry CT dumps without its 16 GB slot arrays moving.
+struct SlotFull {
+    const uint8_t *slots;
+    uint64_t base;
+    uint32_t ss, ksz;
+    __device__ bool operator()(uint32_t j) const { return slots[(base + j) * ss + ksz] == GF_SLOT_FULL; }
+};
+__global__ __launch_bounds__(BLOCK) void k_dump_gather(gf_htab_desc d, uint32_t codec, uint64_t base, const uint32_t *sel,
+                                                       const uint32_t *nsel, uint32_t cap, uint8_t *keys, uint8_t *vals) {
+    const uint32_t n = min(*nsel, cap);
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const uint64_t i = base + sel[t];
+        const uint8_t *sl = d.slots + i * d.slot_size;
+        for (uint32_t b = 0; b < d.ksz; b++) keys[(size_t)t * d.ksz + b] = sl[b];
+        uint8_t in[128], ext[128];
+        for (uint32_t b = 0; b < d.vin; b++) in[b] = sl[d.voff + b];
+        for (uint32_t b = d.vin; b < d.vsz; b++) in[b] = d.vals[i * d.sstride + (b - d.vin)];
+        if (codec == GF_VCODEC_CT) gf_ct_decode(in, ext);
+        else if (codec == GF_VCODEC_POL) gf_pol_decode(in, ext);
+        else for (uint32_t b = 0; b < d.vsz; b++) ext[b] = in[b];
+        for (uint32_t b = 0; b < d.vsz; b++) vals[(size_t)t * d.vsz + b] = ext[b];
+    }
+}
+
+namespace gf {
+int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals, uint32_t *n, uint64_t *next) {
+    static std::mutex mu;                                // the staging buffers below
+    std::lock_guard<std::mutex> g(mu);
+    static DevBuf sel, nsel, tmp, dk, dv;
+    *n = 0; *next = start;
+    if (!max || start >= m.ht.nslots) { *next = m.ht.nslots; return 0; }
+    if (m.vsz > 128) return -EOPNOTSUPP;
+    const uint64_t R = std::min<uint64_t>(m.ht.nslots - start, std::min<uint64_t>(1ull << 24, std::max<uint64_t>(1ull << 16, 4ull * max)));
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(max, R);
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    int r;
+    if ((r = grow(sel, R * 4)) || (r = grow(nsel, 8)) || (r = grow(dk, (size_t)cap * m.ksz)) || (r = grow(dv, (size_t)cap * m.vsz)))
+        return r;
+    gf_htab_desc d = m.hdesc();
+    SlotFull pred{d.slots, start, d.slot_size, d.ksz};
+    size_t tb = 0;
+    (void)rocprim::select(nullptr, tb, rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)sel.p, (uint32_t *)nsel.p,
+                          (size_t)R, pred, (hipStream_t)0);
+    if ((r = grow(tmp, tb + 256))) return r;
+    tb = tmp.bytes;
+    if (hip_ok(rocprim::select(tmp.p, tb, rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)sel.p, (uint32_t *)nsel.p,
+                               (size_t)R, pred, (hipStream_t)0), "dump select"))
+        return -EIO;
+    const uint32_t g2 = (uint32_t)std::min<uint64_t>((cap + BLOCK - 1) / BLOCK, 65535u);
+    hipLaunchKernelGGL(k_dump_gather, dim3(g2 ? g2 : 1), dim3(BLOCK), 0, (hipStream_t)0, d, m.ht.codec, start,
+                       (const uint32_t *)sel.p, (const uint32_t *)nsel.p, cap, (uint8_t *)dk.p, (uint8_t *)dv.p);
+    if (hip_ok(hipGetLastError(), "k_dump_gather")) return -EIO;
+    uint32_t ns = 0;
+    if (hip_ok(hipMemcpy(&ns, nsel.p, 4, hipMemcpyDeviceToHost), "dump count")) return -EIO;
+    const uint32_t got = std::min(ns, cap);
+    m.xfer_d2h += 4 + (size_t)got * (m.ksz + m.vsz);
+    if (got && (hip_ok(hipMemcpy(keys, dk.p, (size_t)got * m.ksz, hipMemcpyDeviceToHost), "dump keys") ||
+                hip_ok(hipMemcpy(vals, dv.p, (size_t)got * m.vsz, hipMemcpyDeviceToHost), "dump vals")))
+        return -EIO;
+    if (ns > cap) {                                      // stopped inside the range: resume after the last one
+        uint32_t last = 0;
+        if (hip_ok(hipMemcpy(&last, (const uint32_t *)sel.p + (cap - 1), 4, hipMemcpyDeviceToHost), "dump last")) return -EIO;
+        *next = start + last + 1;
+    } else {
+        *next = start + R;
+    }
+    *n = got;
+    return 0;
+}
+}  // namespace gf
 
 // ---- endpoint egress (from-container) ----
 namespace {
@@ -3871,7 +4370,7 @@ EgWs &eg_ws() { static EgWs w; return w; }
 
 extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t now_sec, gf_egress_out *out,
                                       uint8_t *snap_out, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     auto a = std::static_pointer_cast<PolicyArray>(o);
@@ -3882,6 +4381,10 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    lock_array_maps(L, a);
+    L.lock();
+    CallOrder co(s);
     const uint32_t n = fr.n, S = fr.snap_stride;
     int r;
     std::vector<std::shared_ptr<ProgLxc>> progs;

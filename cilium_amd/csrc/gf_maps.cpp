@@ -23,9 +23,24 @@
 
 namespace gf {
 
-std::recursive_mutex &big_lock() {
+std::recursive_mutex &prog_lock() {
     static std::recursive_mutex m;
     return m;
+}
+std::mutex &reg_lock() {
+    static std::mutex m;
+    return m;
+}
+
+void MapLocks::lock() {
+    std::sort(held.begin(), held.end());
+    held.erase(std::unique(held.begin(), held.end()), held.end());
+    for (Map *m : held) m->mu.lock();
+    locked = true;
+}
+MapLocks::~MapLocks() {
+    if (!locked) return;
+    for (auto it = held.rbegin(); it != held.rend(); ++it) (*it)->mu.unlock();
 }
 
 int hip_ok(hipError_t e, const char *what) {
@@ -172,6 +187,15 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
     if (!is_lpm()) {
         if (type == GF_MAP_TYPE_LRU_HASH) { fixed_capacity = true; ht.init(k, v, 0); ht.nslots = gf_pow2ceil32(std::max<uint32_t>(64, 2 * m)); }
         else ht.init(k, v, 64);
+        // Maps of the CT shape (ipv4_ct_tuple / ipv6_ct_tuple -> ct_entry) and of the policy
+        // shape (policy_key -> policy_entry) take their datapath layout at creation, while
+        // they are empty: it is invisible through the API (the codecs convert) and saves the
+        // re-layout of a filled table when a program binds the map later.
+        if ((k == 14 || k == 40) && v == GF_CT_VSZ) {
+            set_hash_mode(GF_HASH_CT); set_value_codec(GF_VCODEC_CT); make_fixed_capacity(GF_CT_SLOT_FACTOR);
+        } else if (k == 8 && v == GF_POL_VSZ) {
+            set_hash_mode(GF_HASH_POLICY); set_value_codec(GF_VCODEC_POL);
+        }
     }
 }
 
@@ -242,6 +266,7 @@ int Map::pull() {
     if (is_lpm() || host_valid) return 0;
     materialize(ht);
     if (hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize")) return -EIO;
+    xfer_d2h += ht.slots.size() + (ht.sstride ? ht.vals.size() : 0);
     if (d_slots.p && hip_ok(hipMemcpy(ht.slots.data(), d_slots.p, ht.slots.size(), hipMemcpyDeviceToHost), "pull slots")) return -EIO;
     if (ht.sstride && d_vals.p && hip_ok(hipMemcpy(ht.vals.data(), d_vals.p, ht.vals.size(), hipMemcpyDeviceToHost), "pull vals")) return -EIO;
     // recount (device inserts/deletes)
@@ -279,6 +304,7 @@ int Map::push(hipStream_t s) {
         if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
         if (ht.sstride && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
     } else {
+        xfer_h2d += ht.slots.size() + (ht.sstride ? ht.vals.size() : 0);
         if (hip_ok(hipMemcpyAsync(d_slots.p, ht.slots.data(), ht.slots.size(), hipMemcpyHostToDevice, s), "push slots")) return -EIO;
         if (ht.sstride && hip_ok(hipMemcpyAsync(d_vals.p, ht.vals.data(), ht.vals.size(), hipMemcpyHostToDevice, s), "push vals")) return -EIO;
     }
@@ -310,6 +336,143 @@ gf_trie_desc Map::tdesc() {
     return d;
 }
 
+
+// ------------------------------------------------------------------ device-side element access
+// A map the datapath wrote last (CT entries, policy counters, proxy entries) is
+// authoritative in HBM.  The map API reaches its elements there directly: the
+// key's probe sequence is read in 512-B pieces, values and state bytes are
+// written in place, and the element count is the device counter (exact between
+// classify calls).  The whole-table pull is kept only for re-layouts.
+static int dev_rd(Map &m, void *dst, const void *src, size_t n) {
+    m.xfer_d2h += n;
+    return hip_ok(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), "map read") ? -EIO : 0;
+}
+static int dev_wr(Map &m, void *dst, const void *src, size_t n) {
+    m.xfer_h2d += n;
+    return hip_ok(hipMemcpy(dst, src, n, hipMemcpyHostToDevice), "map write") ? -EIO : 0;
+}
+
+int Map::dev_find(const uint8_t *key, int64_t &slot, int64_t &ins) {
+    slot = -1; ins = -1;
+    if (hip_ok(hipDeviceSynchronize(), "map sync")) return -EIO;   // kernels that write the map are done
+    const uint64_t mask = ht.nslots - 1;
+    const uint32_t ss = ht.slot_size, per = std::max<uint32_t>(1, 512 / ss);
+    std::vector<uint8_t> buf((size_t)per * ss);
+    uint64_t i = gf_home_slot(ht.hash(key), mask, ss);
+    for (uint64_t p = 0; p < ht.nslots;) {
+        const uint64_t nr = std::min<uint64_t>(per, ht.nslots - i);      // a piece never wraps
+        int r = dev_rd(*this, buf.data(), (const uint8_t *)d_slots.p + i * ss, nr * ss);
+        if (r) return r;
+        for (uint64_t k = 0; k < nr; k++) {
+            const uint8_t *sl = &buf[k * ss];
+            const uint8_t st = sl[ksz];
+            if (st == GF_SLOT_EMPTY) { if (ins < 0) ins = (int64_t)(i + k); return 0; }
+            if (st == GF_SLOT_TOMB) { if (ins < 0) ins = (int64_t)(i + k); continue; }
+            if (st == GF_SLOT_FULL && memcmp(sl, key, ksz) == 0) { slot = (int64_t)(i + k); return 0; }
+        }
+        p += nr;
+        i = (i + nr) & mask;
+    }
+    return 0;
+}
+
+int Map::dev_get_val(uint64_t i, uint8_t *ext) {
+    std::vector<uint8_t> inb(vsz);
+    uint8_t *in = inb.data();
+    int r;
+    if (ht.vin && (r = dev_rd(*this, in, (const uint8_t *)d_slots.p + i * ht.slot_size + ht.voff, ht.vin))) return r;
+    if (ht.vin < vsz && (r = dev_rd(*this, in + ht.vin, (const uint8_t *)d_vals.p + i * ht.sstride, vsz - ht.vin))) return r;
+    if (ht.codec != GF_VCODEC_IDENT) codec_decode(ht.codec, in, ext);
+    else memcpy(ext, in, vsz);
+    return 0;
+}
+
+int Map::dev_put_val(uint64_t i, const uint8_t *ext) {
+    std::vector<uint8_t> inb(vsz);
+    uint8_t *in = inb.data();
+    if (ht.codec != GF_VCODEC_IDENT) codec_encode(ht.codec, ext, in);
+    else memcpy(in, ext, vsz);
+    int r;
+    if (ht.vin && (r = dev_wr(*this, (uint8_t *)d_slots.p + i * ht.slot_size + ht.voff, in, ht.vin))) return r;
+    if (ht.vin < vsz && (r = dev_wr(*this, (uint8_t *)d_vals.p + i * ht.sstride, in + ht.vin, vsz - ht.vin))) return r;
+    dev_gen++;
+    return 0;
+}
+
+int Map::dev_count(uint32_t &c) {
+    c = 0;
+    if (hip_ok(hipDeviceSynchronize(), "map sync")) return -EIO;
+    return dev_rd(*this, &c, d_count.p, 4);
+}
+
+int Map::dev_set_count(uint32_t c) {
+    dev_count_hi = c;
+    return dev_wr(*this, d_count.p, &c, 4);
+}
+
+// First FULL slot at or after `start` (chunks of slot headers cached on the
+// host until the device changes), for get_next_key.
+int Map::dev_next_full(uint64_t start, int64_t &slot) {
+    slot = -1;
+    const uint64_t CH = 65536;
+    const uint32_t ss = ht.slot_size;
+    for (uint64_t c = start; c < ht.nslots;) {
+        const uint64_t base = c / CH * CH;
+        if (nk_gen != dev_gen || nk_base != base || nk_n == 0) {
+            if (hip_ok(hipDeviceSynchronize(), "map sync")) return -EIO;
+            nk_n = std::min<uint64_t>(CH, ht.nslots - base);
+            nk_cache.resize(nk_n * ss);
+            int r = dev_rd(*this, nk_cache.data(), (const uint8_t *)d_slots.p + base * ss, nk_n * ss);
+            if (r) { nk_n = 0; return r; }
+            nk_base = base;
+            nk_gen = dev_gen;
+        }
+        for (uint64_t j = c - base; j < nk_n; j++)
+            if (nk_cache[j * ss + ksz] == GF_SLOT_FULL) { slot = (int64_t)(base + j); return 0; }
+        c = base + nk_n;
+    }
+    return 0;
+}
+
+// Element ceiling of a device insert: HASH maps end at max_entries (-E2BIG);
+// LRU maps (which the kernel never lets fail: it evicts) take entries up to the
+// slot array's 7/8 load and are brought back under max_entries by the eviction
+// sweep at the next batch boundary (gf_ct_evict).
+static uint64_t dev_insert_limit(const Map &m) {
+    return m.type == GF_MAP_TYPE_LRU_HASH ? m.ht.nslots / 8 * 7 : m.max_entries;
+}
+
+static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t fl, bool &fallback) {
+    fallback = false;
+    int64_t s, ins;
+    int r = m.dev_find(key, s, ins);
+    if (r) return r;
+    if (s >= 0) {
+        if (fl == GF_NOEXIST) return -EEXIST;
+        return m.dev_put_val((uint64_t)s, value);
+    }
+    if (fl == GF_EXIST) return -ENOENT;
+    uint32_t c;
+    if ((r = m.dev_count(c))) return r;
+    if (c >= dev_insert_limit(m)) return -E2BIG;
+    // a map the host sizes by element count (load <= 1/2) grows on the host
+    if (ins < 0 || (!m.fixed_capacity && ((uint64_t)c + 1) * 2 > m.ht.nslots)) { fallback = true; return 0; }
+    const uint32_t ss = m.ht.slot_size;
+    std::vector<uint8_t> sl(ss, 0), inb(m.vsz);
+    uint8_t *in = inb.data();
+    if (m.ht.codec != GF_VCODEC_IDENT) codec_encode(m.ht.codec, value, in);
+    else memcpy(in, value, m.vsz);
+    memcpy(sl.data(), key, m.ksz);
+    sl[m.ksz] = GF_SLOT_FULL;
+    if (m.ht.vin) memcpy(&sl[m.ht.voff], in, m.ht.vin);
+    if (m.ht.vin < m.vsz && (r = dev_wr(m, (uint8_t *)m.d_vals.p + (uint64_t)ins * m.ht.sstride, in + m.ht.vin,
+                                       m.vsz - m.ht.vin)))
+        return r;
+    if ((r = dev_wr(m, (uint8_t *)m.d_slots.p + (uint64_t)ins * ss, sl.data(), ss))) return r;
+    m.dev_gen++;
+    return m.dev_set_count(c + 1);
+}
+
 int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
     if (fl > GF_EXIST) return -EINVAL;
     if (is_lpm()) {
@@ -330,6 +493,11 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
         lpm_len_cnt[plen]++;
         trie_dirty = true;
         return 0;
+    }
+    if (dev_auth()) {
+        bool fallback;
+        int r = dev_update(*this, key, value, fl, fallback);
+        if (!fallback) return r;
     }
     int r = pull(); if (r) return r;
     materialize(ht);
@@ -368,6 +536,13 @@ int Map::lookup(const uint8_t *key, uint8_t *value) {
         }
         return -ENOENT;
     }
+    if (dev_auth()) {
+        int64_t s, ins;
+        int r = dev_find(key, s, ins);
+        if (r) return r;
+        if (s < 0) return -ENOENT;
+        return dev_get_val((uint64_t)s, value);
+    }
     int r = pull(); if (r) return r;
     if (ht.slots.empty()) return -ENOENT;
     int64_t i = ht.find(key);
@@ -387,6 +562,18 @@ int Map::erase(const uint8_t *key) {
         lpm_len_cnt[plen]--;
         trie_dirty = true;
         return 0;
+    }
+    if (dev_auth()) {
+        int64_t s, ins;
+        int r = dev_find(key, s, ins);
+        if (r) return r;
+        if (s < 0) return -ENOENT;
+        const uint8_t tomb = GF_SLOT_TOMB;
+        if ((r = dev_wr(*this, (uint8_t *)d_slots.p + (uint64_t)s * ht.slot_size + ksz, &tomb, 1))) return r;
+        dev_gen++;
+        uint32_t c;
+        if ((r = dev_count(c))) return r;
+        return dev_set_count(c ? c - 1 : 0);
     }
     int r = pull(); if (r) return r;
     if (ht.slots.empty()) return -ENOENT;
@@ -410,6 +597,28 @@ int Map::next_key(const uint8_t *key, uint8_t *next) {
             }
         }
         memcpy(next, lpm.begin()->first.data(), ksz);
+        return 0;
+    }
+    if (dev_auth()) {
+        uint64_t start = 0;
+        int r;
+        if (key) {
+            if (nk_last_gen == dev_gen && nk_last_slot >= 0 && nk_last_key.size() == ksz &&
+                memcmp(nk_last_key.data(), key, ksz) == 0) {
+                start = (uint64_t)nk_last_slot + 1;
+            } else {
+                int64_t s, ins;
+                if ((r = dev_find(key, s, ins))) return r;
+                if (s >= 0) start = (uint64_t)s + 1;
+            }
+        }
+        int64_t s;
+        if ((r = dev_next_full(start, s))) return r;
+        if (s < 0) return -ENOENT;
+        memcpy(next, &nk_cache[((uint64_t)s - nk_base) * ht.slot_size], ksz);
+        nk_last_key.assign((const char *)next, ksz);
+        nk_last_slot = s;
+        nk_last_gen = dev_gen;
         return 0;
     }
     int r = pull(); if (r) return r;
@@ -518,6 +727,7 @@ struct Registry {
 static Registry &reg() { static Registry r; return r; }
 
 std::shared_ptr<Obj> get_obj(int h) {
+    std::lock_guard<std::mutex> g(reg_lock());
     auto &r = reg();
     auto it = r.handles.find(h);
     return it == r.handles.end() ? nullptr : it->second;
@@ -528,6 +738,7 @@ std::shared_ptr<Map> get_map(int h) {
     return std::static_pointer_cast<Map>(o);
 }
 int new_handle(std::shared_ptr<Obj> o) {
+    std::lock_guard<std::mutex> g(reg_lock());
     auto &r = reg();
     int h = r.next++;
     r.handles[h] = std::move(o);
@@ -548,7 +759,6 @@ extern "C" {
 
 int gf_map_create(uint32_t map_type, uint32_t key_size, uint32_t value_size,
                   uint32_t max_entries, uint32_t map_flags) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     if (!key_size || !value_size || !max_entries) return -EINVAL;
     switch (map_type) {
     case GF_MAP_TYPE_HASH:
@@ -571,20 +781,31 @@ int gf_map_create(uint32_t map_type, uint32_t key_size, uint32_t value_size,
 }
 
 int gf_map_update_elem(int h, const void *key, const void *value, uint64_t flags) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto m = get_map(h);
     if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (!key || !value) return -EFAULT;
     return m->update((const uint8_t *)key, (const uint8_t *)value, flags);
 }
 
 int gf_map_update_batch(int h, const void *keys, const void *values, uint32_t n,
                         uint64_t flags, uint32_t *n_done) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto m = get_map(h);
     if (n_done) *n_done = 0;
     if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (n && (!keys || !values)) return -EFAULT;
+    if (n >= 4096 && m->fixed_capacity && !m->is_lpm() && (flags == GF_ANY || flags == GF_NOEXIST) &&
+        (m->dev_auth() || (m->ht.slots.empty() && m->ht.count == 0))) {
+        // a table the datapath inserts into, filled in bulk (the agent restoring a CT,
+        // a benchmark's pre-population): loaded in HBM directly, no host shadow built
+        bool fallback = false;
+        int r = dev_bulk_insert(*m, (const uint8_t *)keys, (const uint8_t *)values, n, flags, fallback);
+        if (!fallback) {
+            if (!r && n_done) *n_done = n;
+            return r;
+        }
+    }
     for (uint32_t i = 0; i < n; i++) {
         int r = m->update((const uint8_t *)keys + (size_t)i * m->ksz,
                           (const uint8_t *)values + (size_t)i * m->vsz, flags);
@@ -595,47 +816,114 @@ int gf_map_update_batch(int h, const void *keys, const void *values, uint32_t n,
 }
 
 int gf_map_lookup_elem(int h, const void *key, void *value) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto m = get_map(h);
     if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (!key || !value) return -EFAULT;
     return m->lookup((const uint8_t *)key, (uint8_t *)value);
 }
 
 int gf_map_delete_elem(int h, const void *key) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto m = get_map(h);
     if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (!key) return -EFAULT;
     return m->erase((const uint8_t *)key);
 }
 
 int gf_map_get_next_key(int h, const void *key, void *next_key) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto m = get_map(h);
     if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (!next_key) return -EFAULT;
     return m->next_key((const uint8_t *)key, (uint8_t *)next_key);
 }
 
-int gf_map_get_info(int h, gf_map_info *info) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+// Chunked dump: what DumpWithCallback (pkg/bpf/map.go:319-369) obtains with one
+// GetNextKey + LookupElement pair per entry, a chunk of entries per call (the
+// kernel's later BPF_MAP_LOOKUP_BATCH contract).  Cursor = slot index (hash
+// maps) or ordinal (LPM tries, post-order).
+int gf_map_lookup_batch(int h, const uint64_t *in_batch, uint64_t *out_batch, void *keys, void *values,
+                        uint32_t *count) {
     auto m = get_map(h);
     if (!m) return -EBADF;
+    if (!out_batch || !count || (*count && (!keys || !values))) return -EFAULT;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
+    const uint32_t want = *count;
+    uint64_t cur = in_batch ? *in_batch : 0;
+    uint8_t *ko = (uint8_t *)keys, *vo = (uint8_t *)values;
+    uint32_t n = 0;
+    *count = 0;
+    if (m->is_lpm()) {
+        uint64_t k = 0;
+        auto it = m->lpm.begin();
+        for (; it != m->lpm.end() && k < cur; ++it, ++k) {}
+        for (; it != m->lpm.end() && n < want; ++it, ++k, ++n) {
+            memcpy(ko + (size_t)n * m->ksz, it->first.data(), m->ksz);
+            memcpy(vo + (size_t)n * m->vsz, it->second.data(), m->vsz);
+        }
+        *count = n; *out_batch = k;
+        return it == m->lpm.end() ? -ENOENT : 0;
+    }
+    if (m->dev_auth()) {
+        if (hip_ok(hipDeviceSynchronize(), "map sync")) return -EIO;
+        while (n < want && cur < m->ht.nslots) {
+            uint32_t got = 0;
+            uint64_t next = cur;
+            int r = dev_dump(*m, cur, want - n, ko + (size_t)n * m->ksz, vo + (size_t)n * m->vsz, &got, &next);
+            if (r) return r;
+            n += got; cur = next;
+        }
+        *count = n; *out_batch = cur;
+        return cur >= m->ht.nslots ? -ENOENT : 0;
+    }
+    int r = m->pull();
+    if (r) return r;
+    const HTab &t = m->ht;
+    if (t.slots.empty()) { *out_batch = t.nslots; return -ENOENT; }
+    std::vector<uint8_t> v(m->vsz);
+    for (; cur < t.nslots && n < want; cur++) {
+        if (t.state(cur) != GF_SLOT_FULL) continue;
+        memcpy(ko + (size_t)n * m->ksz, t.key(cur), m->ksz);
+        t.get_val(cur, v.data());
+        if (t.codec != GF_VCODEC_IDENT) codec_decode(t.codec, v.data(), vo + (size_t)n * m->vsz);
+        else memcpy(vo + (size_t)n * m->vsz, v.data(), m->vsz);
+        n++;
+    }
+    while (cur < t.nslots && t.state(cur) != GF_SLOT_FULL) cur++;     // ENOENT as soon as nothing is left
+    *count = n; *out_batch = cur;
+    return cur >= t.nslots ? -ENOENT : 0;
+}
+
+int gf_map_get_info(int h, gf_map_info *info) {
+    auto m = get_map(h);
+    if (!m) return -EBADF;
+    std::lock_guard<std::recursive_mutex> g(m->mu);
     if (!info) return -EFAULT;
-    m->pull();
     info->map_type = m->type; info->key_size = m->ksz; info->value_size = m->vsz;
     info->max_entries = m->max_entries; info->map_flags = m->flags;
     info->n_entries = m->n_entries();
+    if (m->dev_auth()) {                 // the device counter (exact between classify calls)
+        uint32_t c;
+        int r = m->dev_count(c);
+        if (r) return r;
+        info->n_entries = c;
+    } else if (!m->host_valid) {
+        int r = m->pull();
+        if (r) return r;
+        info->n_entries = m->n_entries();
+    }
     info->device_bytes = m->device_bytes();
+    info->xfer_d2h = m->xfer_d2h;
+    info->xfer_h2d = m->xfer_h2d;
     return 0;
 }
 
 int gf_obj_pin(int h, const char *path) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     auto o = get_obj(h);
     if (!o) return -EBADF;
     if (!path || !*path) return -EINVAL;
+    std::lock_guard<std::mutex> g(reg_lock());
     auto &r = reg();
     if (r.pins.count(path)) return -EEXIST;
     r.pins[path] = o;
@@ -643,23 +931,32 @@ int gf_obj_pin(int h, const char *path) {
 }
 
 int gf_obj_get(const char *path) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     if (!path) return -EFAULT;
-    auto &r = reg();
-    auto it = r.pins.find(path);
-    if (it == r.pins.end()) return -ENOENT;
-    return new_handle(it->second);
+    std::shared_ptr<Obj> o;
+    {
+        std::lock_guard<std::mutex> g(reg_lock());
+        auto &r = reg();
+        auto it = r.pins.find(path);
+        if (it == r.pins.end()) return -ENOENT;
+        o = it->second;
+    }
+    return new_handle(o);
 }
 
 int gf_obj_unpin(const char *path) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
     if (!path) return -EFAULT;
+    std::lock_guard<std::mutex> g(reg_lock());
     return reg().pins.erase(path) ? 0 : -ENOENT;
 }
 
 int gf_obj_close(int h) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
-    return reg().handles.erase(h) ? 0 : -EBADF;
+    std::shared_ptr<Obj> o;              // released outside the registry lock
+    std::lock_guard<std::mutex> g(reg_lock());
+    auto it = reg().handles.find(h);
+    if (it == reg().handles.end()) return -EBADF;
+    o = std::move(it->second);
+    reg().handles.erase(it);
+    return 0;
 }
 
 uint32_t gf_now_sec(void) {
@@ -669,7 +966,7 @@ uint32_t gf_now_sec(void) {
 }
 
 int gf_node_config(const gf_node_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     std::shared_ptr<Map> m4, m6;
     if (cfg->proxy4_map) {
@@ -694,7 +991,7 @@ int gf_node_config(const gf_node_cfg *cfg) {
         if (tun->ksz != 20 || tun->vsz != 20 || tun->is_lpm()) return -EINVAL;
     }
     // the datapath inserts into the proxy maps: fixed slot arrays (1/2 load at max_entries)
-    for (auto &m : {m4, m6}) if (m) m->make_fixed_capacity(2);
+    for (auto &m : {m4, m6}) if (m) { std::lock_guard<std::recursive_mutex> mg(m->mu); m->make_fixed_capacity(2); }
     reg().host_ifindex = cfg->host_ifindex;
     reg().node = *cfg;
     reg().px4 = m4; reg().px6 = m6;
@@ -703,7 +1000,7 @@ int gf_node_config(const gf_node_cfg *cfg) {
 }
 
 int gf_set_stats_sink(uint64_t *dev_counters) {
-    std::lock_guard<std::recursive_mutex> g(big_lock());
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
     reg().stats = dev_counters;
     return 0;
 }

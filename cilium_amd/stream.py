@@ -262,3 +262,72 @@ def to_frames6(cols_np, stride=96):
     f[:, 54:58] = cols_np["l4w0"].astype(np.uint32).view(np.uint8).reshape(n, 4)
     f[:, 66:68] = cols_np["l4w3"].astype(np.uint16).view(np.uint8).reshape(n, 2)
     return f, lens
+
+
+class Stream6Frames(Stream):
+    """Config 5: the flow model over IPv6 raw frames (80-B snaps) for the full
+    pipeline.  A pair's remote end is a cluster source (ROUTER_IP's /64, its
+    identity in the flow label) or, for the CIDR class, a NAT64 world source;
+    the endpoint end is its IPv6 address.  5% of flows answer connections the
+    endpoint opened (their egress CT entries are in the pre-fill)."""
+
+    def __init__(self, pairs, meta, **kw):
+        super().__init__(pairs, **kw)
+        import torch
+        own = self.own
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        self.src6 = T(meta["src6"][own])
+        self.dst6 = T(meta["dst6"][own])
+        world = pairs["cls"][own] == 2
+        self.flabel = T(np.where(world, 0, pairs["pid"][own]).astype(np.int64))
+        self._s6, self._d6 = meta["src6"][own], meta["dst6"][own]
+
+    def pair_addrs6(self):
+        return self._s6, self._d6
+
+    def reply_ct6_entries(self, n_steps):
+        """Egress-created CT6 entries (tuple + ICMPv6 related) of every reply flow
+        of steps [0, n_steps), in ipv6_ct_tuple / ct_entry layout."""
+        torch = self.torch
+        f = torch.arange(0, n_steps * self.F, device=self.device, dtype=torch.int64)
+        p, proto, sport, dport, reply, related, rst = self._flows(f)
+        m = reply & (proto != ICMP)
+        p, proto, sport, dport = p[m].cpu().numpy(), proto[m].cpu().numpy(), sport[m].cpu().numpy(), dport[m].cpu().numpy()
+        E, R = self._d6[p], self._s6[p]
+        n = len(p)
+        k = synth.ct6_keys(E, R, synth.raw16(sport), synth.raw16(dport), proto, np.zeros(n))
+        rk = synth.ct6_keys(E, R, np.zeros(n), np.zeros(n), np.full(n, 58), np.full(n, 2))
+        v = synth.ct_vals(n, 100_000 + 43200, 16, 0, 0, tx=(1, 100))
+        return synth.dedup(np.concatenate([k, rk]), np.concatenate([v, v]))
+
+    def step(self, s):
+        """Frames of step s: (frames uint8[n, 80], len int32[n], pair index)."""
+        torch = self.torch
+        cols, p, n = Stream.step(self, s)
+        length = cols["len"].to(torch.int64) + 20                     # 40-B header instead of 20
+        proto = cols["proto"].to(torch.int64)
+        w0 = cols["l4w0"].to(torch.int64) & 0xFFFFFFFF
+        icmp = proto == ICMP
+        # ICMP echo (8) -> ICMPv6 echo request (128), DEST_UNREACH (3) -> ICMPv6 DEST_UNREACH (1)
+        w0 = torch.where(icmp, torch.where((w0 & 0xff) == 3, 1, 128), w0)
+        proto = torch.where(icmp, 58, proto)
+        w3 = cols["l4w3"].to(torch.int64) & 0xFFFF
+        fl = self.flabel[p]
+        f = torch.zeros((n, 80), dtype=torch.uint8, device=self.device)
+        f[:, 12], f[:, 13] = 0x86, 0xDD
+        f[:, 14] = 0x60
+        f[:, 15] = ((fl >> 16) & 0xF).to(torch.uint8)
+        f[:, 16] = ((fl >> 8) & 0xFF).to(torch.uint8)
+        f[:, 17] = (fl & 0xFF).to(torch.uint8)
+        pl = (length - 54).clamp(0, 0xFFFF)
+        f[:, 18] = (pl >> 8).to(torch.uint8)
+        f[:, 19] = (pl & 0xFF).to(torch.uint8)
+        f[:, 20] = proto.to(torch.uint8)
+        f[:, 21] = 64
+        f[:, 22:38] = self.src6[p]
+        f[:, 38:54] = self.dst6[p]
+        for b in range(4):
+            f[:, 54 + b] = ((w0 >> (8 * b)) & 0xFF).to(torch.uint8)
+        f[:, 66] = (w3 & 0xFF).to(torch.uint8)
+        f[:, 67] = (w3 >> 8).to(torch.uint8)
+        return f, length.to(torch.int32), p

@@ -652,10 +652,11 @@ def config2(n_flows=16_777_216, n_pairs=1 << 20, n_ep=256, n_ids=4096, n_l3=2000
 
 
 # ------------------------------------------------------------------ parity fuzz scenario
-def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
+def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128, ct_max=100000, ct6_max=100000):
     """Small shared pools so that map hits, repeated flows, replies, related
     ICMP, deletes, proxies, rev-NAT, weird IHL, truncation and IPv6
-    extension-header chains all occur.  Used by the parity tests."""
+    extension-header chains all occur.  Used by the parity tests (a small
+    ct_max / ct6_max makes the LRU CT maps overflow and exercises eviction)."""
     rng = np.random.default_rng(seed)
     sc = Scenario(f"fuzz{seed}", now=5000)
     n_ep = 16
@@ -748,7 +749,7 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
     ev[:, 36:38] = le_bytes(fl, "<u2")
     ev[:, 38:40] = le_bytes(rn, "<u2")
     k, v = dedup(np.concatenate([ek, rel]), np.concatenate([ev, ct_vals(npre, 4000, 16)]))
-    sc.add_map(MapSpec("ct4", LRU_HASH, 14, 48, 100000, 0, k, v))
+    sc.add_map(MapSpec("ct4", LRU_HASH, 14, 48, ct_max, 0, k, v))
     n6 = 12
     E6, R6 = ep6[rng.integers(0, n_ep, n6)], rem6[rng.integers(0, len(rem6), n6)]
     k6 = pack_rows(E6, R6, le_bytes(raw16(ports[rng.integers(0, len(ports), n6)]), "<u2"),
@@ -756,7 +757,7 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128):
                    np.full((n6, 1), TCP, np.uint8), np.zeros((n6, 1), np.uint8), np.zeros((n6, 2), np.uint8))
     v6 = ct_vals(n6, 4000, 16, 0, 300)
     v6[:, 38:40] = le_bytes(np.where(rng.random(n6) < 0.5, raw16(rng.integers(1, 4, n6)), 0), "<u2")
-    sc.add_map(MapSpec("ct6", LRU_HASH, 40, 48, 100000, 0, *dedup(k6, v6)))
+    sc.add_map(MapSpec("ct6", LRU_HASH, 40, 48, ct6_max, 0, *dedup(k6, v6)))
     flag_sets = [LXC_PRODUCTION] * 10 + [LXC_PRODUCTION | LXC_DROP_ALL, LXC_PRODUCTION & ~LXC_POLICY_INGRESS,
                                          LXC_PRODUCTION & ~LXC_LXC_IPV4, LXC_PRODUCTION & ~LXC_HAVE_L4_POLICY,
                                          LXC_PRODUCTION & ~LXC_CT_ACCOUNTING, LXC_PRODUCTION]
@@ -991,6 +992,111 @@ def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000
     return sc, P, vip
 
 
+# ------------------------------------------------------------------ config 5: IPv6 pipeline
+ROUTER6 = bytes([0x20, 0x01, 0x0d, 0xb8, 0xaa, 0xaa, 0xbb, 0xbb, 0, 0, 0, 0, 0, 0, 0, 1])   # ROUTER_IP
+NAT64 = bytes([0x00, 0x64, 0xff, 0x9b] + [0] * 12)                                        # 64:ff9b::/96
+
+
+def v6_embed(prefix16, v4):
+    """Addresses prefix16[:12] + the IPv4 address (host order) in bytes 12..15."""
+    v4 = np.asarray(v4, np.uint32)
+    a = np.tile(np.frombuffer(bytes(prefix16), np.uint8), (len(v4), 1))
+    a[:, 12:16] = be32_bytes(v4)
+    return a
+
+
+def config5_tables(n_pairs=1 << 20, prefill=8_000_000, n_fix=100_000, n_dyn=10_000, ct6_max=10_485_760,
+                   seed=0xC1D40005, now=100_000, reply_steps=16, flows_per_step=1 << 20):
+    """BASELINE config 5 / SURVEY §8(d): the IPv6 path a packet takes on a node —
+    bpf_xdp check_v6 (v6_dyn LPM: n_dyn prefixes /32-/127; v6_fix hash: n_fix
+    /128s; cilium_lxc endpoint check) -> bpf_netdev handle_ipv6 (the identity of a
+    source inside ROUTER_IP's /64 is its flow label, others are WORLD) ->
+    handle_policy / ipv6_policy (ct_lookup6 on cilium_ct6_global, max_entries
+    ct6_max, LRU, pre-filled to `prefill` entries: egress-created reply entries of
+    the stream's reply flows plus older unrelated connections, 20% of them
+    closing).  Endpoints, identities and per-endpoint policy are config 2's; the
+    pairs' remote addresses become cluster sources (identity classes) or NAT64
+    world sources (CIDR class, per-endpoint v6 CIDR maps of the same prefixes).
+    Returns (scenario, pairs, meta)."""
+    sc, P, rng = config2_tables(n_pairs=n_pairs, ct_max=1 << 16, seed=0xC1D40002, now=now)
+    rng5 = np.random.default_rng(seed)
+    sc.name = "config5_ipv6"
+    n_ep = len(P["ep_ip"])
+    ep6 = np.zeros((n_ep, 16), np.uint8)
+    ep6[:, 0:2] = (0xfd, 0x00)
+    ep6[:, 8:10] = (0x0a, 0x01)                      # bytes 12-13 zero: no rev-NAT index (bpf_lxc.c:776)
+    ep6[:, 14:16] = be16_bytes(1 + np.arange(n_ep))
+    world = P["cls"] == 2
+    src6 = np.where(world[:, None], v6_embed(NAT64, P["raddr"]), v6_embed(ROUTER6[:8] + bytes(8), P["raddr"]))
+    dst6 = ep6[P["pe"]]
+    # per-endpoint v6 CIDR ingress maps: the v4 prefixes of config 2 under 64:ff9b::/96
+    crng = np.random.default_rng(0xC1D40002 ^ 0x66)
+    for e, cfg in enumerate(sc.lxc):
+        k4 = sc.maps[cfg["cidr4"]].keys
+        plen = k4[:, 0:4].copy().view("<u4").ravel()
+        net = k4[:, 4:8].copy().view(">u4").ravel()
+        ck, cv = lpm_dedup(lpm6_keys(96 + plen, v6_embed(NAT64, net)), np.ones((len(plen), 1), np.uint8), 128)
+        name = f"cilium_cidr6_ingress_{cfg['lxc_id']}"
+        sc.add_map(MapSpec(name, LPM, 20, 1, 16384, NO_PREALLOC, ck, cv))
+        cfg.update(ct6="cilium_ct6_global", cidr6=name, revnat6="cilium_lb6_reverse_nat")
+    rk, rv = revnat6_entries(np.arange(1, 257), v6_embed(bytes([0xfd, 0, 0, 0, 0, 0, 0, 0, 0, 0x60] + [0] * 6),
+                                                        np.arange(256)), np.full(256, 80))
+    sc.add_map(MapSpec("cilium_lb6_reverse_nat", HASH, 2, 18, 65536, 0, rk, rv))
+    # cilium_lxc: the endpoints' IPv6 addresses (family 2) with their MACs
+    ev = endpoint_infos(P["ifidx"], 256 + np.arange(n_ep), P["lxc_id"], np.zeros(n_ep))
+    ev[:, 16:22] = rng5.integers(0, 256, (n_ep, 6))
+    ev[:, 24:30] = rng5.integers(0, 256, (n_ep, 6))
+    sc.add_map(MapSpec("cilium_lxc", HASH, 20, 112, 65535, 0, endpoint_keys6(ep6), ev))
+    # prefilter: v6_fix /128s and v6_dyn /32-/127 prefixes (sized with the CIDR4 constants, bpf_xdp.c:73,83)
+    fx = rand_v6(rng5, n_fix, prefix=(0x20, 0x01, 0x0d, 0xb8, 0xf0))
+    hit = rng5.integers(0, n_pairs, 64)
+    fx[:64] = src6[hit]
+    k, v = dedup(lpm6_keys(np.full(n_fix, 128), fx), np.ones((n_fix, 1), np.uint8))
+    sc.add_map(MapSpec("cilium_cidr_v6_fix", HASH, 20, 1, 20971520, NO_PREALLOC, k, v))
+    dl = rng5.integers(32, 128, n_dyn)
+    dn = rand_v6(rng5, n_dyn, prefix=(0x2a,))          # 2a00::/8: disjoint from the sources' /32s
+    cov = rng5.random(n_dyn) < 0.02                  # a few prefixes cover pair sources
+    dn[cov] = src6[rng5.integers(0, n_pairs, int(cov.sum()))]
+    dl = np.where(cov, rng5.integers(120, 128, n_dyn), dl)
+    k, v = lpm_dedup(lpm6_keys(dl, dn), np.ones((n_dyn, 1), np.uint8), 128)
+    sc.add_map(MapSpec("cilium_cidr_v6_dyn", LPM, 20, 1, 65536, NO_PREALLOC, k, v))
+    sc.xdp = {"cidr4_hmap": None, "cidr4_lmap": None, "cidr6_hmap": "cilium_cidr_v6_fix",
+              "cidr6_lmap": "cilium_cidr_v6_dyn", "lxc_map": "cilium_lxc"}
+    sc.lb = None
+    sc.netdev = {"lxc_map": "cilium_lxc", "flags": 0, "router_ip6": ROUTER6}
+    sc.add_map(MapSpec("cilium_ct6_global", LRU_HASH, 40, 48, ct6_max, 0))
+    meta = dict(ep6=ep6, src6=src6, dst6=dst6, prefill=prefill, reply_steps=reply_steps,
+                flows_per_step=flows_per_step)
+    return sc, P, meta
+
+
+def ct6_keys(d16, s16, dport_raw, sport_raw, nexthdr, flags):
+    n = len(d16)
+    return pack_rows(np.asarray(d16, np.uint8), np.asarray(s16, np.uint8), le_bytes(dport_raw, "<u2"),
+                     le_bytes(sport_raw, "<u2"), np.asarray(nexthdr, np.uint8).reshape(n, 1),
+                     np.asarray(flags, np.uint8).reshape(n, 1), np.zeros((n, 2), np.uint8))
+
+
+def ct6_prefill(meta, reply_keys, reply_vals, now, seed=0xC1D40055):
+    """cilium_ct6_global's pre-population: the reply flows' egress entries plus
+    older connections of unrelated remote peers up to meta['prefill'] entries
+    (lifetimes spread over the last 11 hours, 20% closing with short lifetimes)."""
+    rng = np.random.default_rng(seed)
+    n = max(0, meta["prefill"] - len(reply_keys))
+    E = meta["ep6"][rng.integers(0, len(meta["ep6"]), n)]
+    R = rand_v6(rng, n, prefix=(0x20, 0x01, 0x0d, 0xb8, 0x50, 0x00))
+    pr = np.where(rng.random(n) < 0.7, TCP, UDP).astype(np.uint8)
+    k = ct6_keys(E, R, raw16(rng.integers(1024, 65536, n)), raw16(rng.integers(1, 65536, n)), pr,
+                 rng.integers(0, 2, n))
+    closing = rng.random(n) < 0.2
+    life = np.where(closing, now - rng.integers(0, 600, n) + 10, now - rng.integers(0, 40000, n) + 43200)
+    v = ct_vals(n, 0, 0, 0, 0, rx=(3, 300), tx=(2, 200))
+    v[:, 32:36] = le_bytes(life.astype(np.uint32), "<u4")
+    v[:, 36:38] = le_bytes(np.where(closing, 3, 16).astype(np.uint16), "<u2")
+    v[:, 44:48] = le_bytes(rng.integers(256, 4352, n).astype(np.uint32), "<u4")
+    return dedup(np.concatenate([reply_keys, k]), np.concatenate([reply_vals, v]))
+
+
 # ------------------------------------------------------------------ endpoint egress (from-container)
 LXC_POLICY_EGRESS = 32
 
@@ -1202,13 +1308,20 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
     return sc
 
 
+TENANT = 16      # endpoints per tenant in the egress workload
+
+
 def egress_tables(n_ep=256, n_svc=1024, backends=4, ct_max=64_000_000, seed=0xE6E5):
     """Egress measurement tables (the agent's production flag set: no
     POLICY_EGRESS): n_ep local endpoints (10.1.x.y) with their MACs, one global
     CT map, services whose backends are local endpoints (so some translate back
     to the sender: loopback SNAT), a tunnel map covering 10.128.0.0/16, and
     per-endpoint ingress policy admitting the endpoints' identities (local
-    deliveries continue into handle_policy)."""
+    deliveries continue into handle_policy).  Endpoints form tenants of TENANT
+    (endpoint e is in tenant e // TENANT); service s belongs to tenant
+    s % (n_ep // TENANT) and its backends are that tenant's endpoints, so local
+    traffic never crosses tenants and a tenant is a closed set of flow groups
+    (the bench's parity sample)."""
     rng = np.random.default_rng(seed)
     sc = Scenario("egress_bench", now=10_000, host_ifindex=3)
     ep4 = (ip4("10.1.0.0") + 1 + np.arange(n_ep)).astype(np.uint32)
@@ -1224,7 +1337,8 @@ def egress_tables(n_ep=256, n_svc=1024, backends=4, ct_max=64_000_000, seed=0xE6
     sc.add_map(MapSpec("ct6", LRU_HASH, 40, 48, 1 << 16, 0))
     vip = (ip4("10.96.0.0") + 1 + np.arange(n_svc)).astype(np.uint32)
     sport = rng.choice(np.array([80, 443, 8080, 53], np.uint32), n_svc)
-    tgt = ep4[rng.integers(0, n_ep, (n_svc, backends))]
+    nten = n_ep // TENANT
+    tgt = ep4[(np.arange(n_svc) % nten)[:, None] * TENANT + rng.integers(0, TENANT, (n_svc, backends))]
     keys = [lb4_keys(vip, sport, np.zeros(n_svc))]
     vals = [lb4_vals(np.zeros(n_svc), np.zeros(n_svc), np.full(n_svc, backends), np.zeros(n_svc))]
     for b in range(backends):
@@ -1263,8 +1377,9 @@ def egress_flows(meta, n_flows, seed=0xE6E6):
     kind = rng.random(n_flows)
     world = (ip4("100.64.0.0") + rng.integers(0, 1 << 20, n_flows)).astype(np.uint32)
     tun = (ip4("10.128.0.0") + rng.integers(0, 1 << 16, n_flows)).astype(np.uint32)
-    peer = ep4[(e + 1 + rng.integers(0, n_ep - 1, n_flows)) % n_ep]
-    si = rng.integers(0, len(meta["vip"]), n_flows)
+    ten, nten = e // TENANT, n_ep // TENANT                # local peers and services of the own tenant
+    peer = ep4[ten * TENANT + (e % TENANT + 1 + rng.integers(0, TENANT - 1, n_flows)) % TENANT]
+    si = ten + nten * rng.integers(0, len(meta["vip"]) // nten, n_flows)
     d = np.where(kind < 0.35, world, np.where(kind < 0.55, tun, np.where(kind < 0.80, peer, meta["vip"][si])))
     dp = np.where(kind >= 0.80, meta["sport"][si], rng.choice(np.array([80, 443, 53, 8080], np.uint32), n_flows))
     pr = np.where(rng.random(n_flows) < 0.8, TCP, UDP).astype(np.uint8)

@@ -123,10 +123,23 @@ int gf_map_get_next_key(int map, const void *key, void *next_key);
 int gf_map_update_batch(int map, const void *keys, const void *values,
                         uint32_t n, uint64_t flags, uint32_t *n_done);
 
+/* Chunked dump (what bpf.Map.DumpWithCallback, pkg/bpf/map.go:319-369, gets
+ * from one GetNextKey + LookupElement pair per entry; the kernel's later
+ * BPF_MAP_LOOKUP_BATCH contract): copies up to *count entries after the
+ * opaque cursor *in_batch (NULL = from the start) into keys / values (host
+ * arrays, reference layouts), sets *count to the number copied and *out_batch
+ * to the cursor to resume from.  Returns 0, or -ENOENT once the map holds no
+ * entry past the cursor (*count may still be > 0).  Device-authoritative maps
+ * are compacted on the device; only the entries cross PCIe. */
+int gf_map_lookup_batch(int map, const uint64_t *in_batch, uint64_t *out_batch,
+                        void *keys, void *values, uint32_t *count);
+
 typedef struct gf_map_info {
     uint32_t map_type, key_size, value_size, max_entries, map_flags;
     uint32_t n_entries;        /* current element count */
     uint64_t device_bytes;     /* HBM bytes of the replica (0 if never synced) */
+    uint64_t xfer_d2h;         /* bytes the map API has copied device -> host (element walks, */
+    uint64_t xfer_h2d;         /* dumps, pulls) and host -> device (element writes, pushes) */
 } gf_map_info;
 int gf_map_get_info(int map, gf_map_info *info);
 
@@ -451,6 +464,25 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *batch, uint32_t self_ra
  * datapath owns the map (compacting probe clusters in the same sweep), else on the
  * host shadow.  Synchronous on `stream`. */
 int gf_ct_gc(int map, uint32_t filter_time, void *stream);
+
+/* ---- LRU CT maps (BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:53-75) ----
+ * The kernel evicts from per-CPU LRU lists in a nondeterministic order and
+ * never fails an insert.  libgpuflow's deterministic stand-in:
+ * inside a batch an LRU CT map may exceed max_entries (up to the 7/8 load of
+ * its slot array, 4 x max_entries); at the end of every classify call that
+ * uses it, if the count exceeds max_entries, the oldest entries are deleted
+ * until at most max_entries - max_entries/8 remain — closing entries first,
+ * then the others, each by ascending last use (lifetime minus the timeout its
+ * flags select) in one-second bins.  Every eviction is logged: */
+typedef struct gf_ct_evict_rec {
+    uint32_t seq;              /* the map's classify call (1 = first call that used the map) */
+    uint32_t now_sec;          /* that call's now_sec */
+    uint64_t cut_closing;      /* closing entries last used before cut_closing were deleted */
+    uint64_t cut_other;        /* other entries last used before cut_other were deleted */
+    uint64_t evicted;          /* entries deleted */
+} gf_ct_evict_rec;
+/* Copies up to max records (oldest first) and returns the number logged. */
+int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max);
 
 /* ---- drop notifications (bpf/lib/drop.h:38-107, DROP_NOTIFY) ----
  * With a ring set, gf_policy_ingress_classify and gf_pipeline_classify append

@@ -226,6 +226,17 @@ int om_lookup(om_map *m, const void *key, void *value_out) {
     return 0;
 }
 
+/* Element ceiling of an insert.  HASH / LPM: max_entries (E2BIG / ENOSPC).
+ * LRU_HASH: the kernel never fails an LRU insert (it evicts); with the LRU
+ * stand-in above the table may exceed max_entries inside a batch, up to the 7/8
+ * load of libgpuflow's CT slot array (4 x max_entries rounded up to a power of 2). */
+static uint32_t om_insert_limit(const om_map *m) {
+    if (m->type != OM_LRU_HASH) return m->max_entries;
+    uint64_t want = 4ull * m->max_entries, p = 64;
+    while (p < want) p <<= 1;
+    return (uint32_t)(p / 8 * 7 > 0xffffffffull ? 0xffffffffu : p / 8 * 7);
+}
+
 /* map_update_elem(): kernel htab_map_update_elem / trie_update_elem. */
 int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
     if (flags > 2) return -EINVAL;
@@ -245,7 +256,7 @@ int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
     }
     if (flags == 2) return -ENOENT;
     uint32_t c = __atomic_add_fetch(&m->count, 1, __ATOMIC_RELAXED);
-    if (c > m->max_entries) {
+    if (c > om_insert_limit(m)) {
         __atomic_sub_fetch(&m->count, 1, __ATOMIC_RELAXED);
         return is_lpm(m) ? -ENOSPC : -E2BIG;
     }
@@ -258,6 +269,16 @@ int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
     memcpy(h->vals + j * m->vsz, value, m->vsz);
     h->used++;
     if (is_lpm(m)) { uint32_t plen; memcpy(&plen, key, 4); m->lens_cnt[plen]++; }
+    return 0;
+}
+
+/* n sequential om_update calls; stops at the first error (returns it, *done = applied). */
+int om_update_many(om_map *m, const void *keys, const void *values, uint32_t n, uint64_t flags, uint32_t *done) {
+    for (uint32_t i = 0; i < n; i++) {
+        int r = om_update(m, (const uint8_t *)keys + (size_t)i * m->ksz, (const uint8_t *)values + (size_t)i * m->vsz, flags);
+        if (r) { if (done) *done = i; return r; }
+    }
+    if (done) *done = n;
     return 0;
 }
 
@@ -1038,7 +1059,9 @@ static int redirect_to_host_port_checks(const skb_t *s, int l4_off, uint8_t next
     return 0;                                          /* cilium_proxy{4,6} update: §8(f) */
 }
 
-static o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0, 0, 0, 0, NULL, {0}};   /* bpf/node_config.h */
+/* per thread: several oracle instances may run side by side (bench.py egress leg);
+ * run_mt hands the caller's copy to its workers */
+static __thread o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0, 0, 0, 0, NULL, {0}};   /* bpf/node_config.h */
 #define g_host_ifindex (g_node.host_ifindex)
 void o_set_node(const o_node_cfg *node) { g_node = *node; }
 
@@ -1286,6 +1309,7 @@ typedef struct mt_arg {
     /* pipeline front pass (kind 3) */
     const o_pipeline_cfg *pc; o_pipeline_out *po; uint8_t *snap_out, *skip_w;
     uint32_t *secctx, *ifx; uint16_t *lxcid;
+    o_node_cfg node;                    /* the caller's node config (thread-local g_node) */
 } mt_arg;
 
 static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i, uint8_t *row, o_pipeline_out *o,
@@ -1323,6 +1347,7 @@ static uint32_t pkt_group(const o_batch *b, uint32_t i) {
 
 static void *mt_worker(void *p) {
     mt_arg *m = (mt_arg *)p;
+    g_node = m->node;
     const o_batch *b = m->b;
     uint32_t T = m->nthreads, t = m->tid;
     uint32_t lo = (uint32_t)((uint64_t)b->n * t / T), hi = (uint32_t)((uint64_t)b->n * (t + 1) / T);
@@ -1361,6 +1386,7 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
     if (threads < 1) threads = 1;
     pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
     mt_arg *args = (mt_arg *)calloc(threads, sizeof(mt_arg));
+    tmpl->node = g_node;
     for (uint32_t t = 0; t < threads; t++) {
         args[t] = *tmpl; args[t].tid = t; args[t].nthreads = threads;
         pthread_create(&th[t], NULL, mt_worker, &args[t]);
@@ -1732,6 +1758,77 @@ static void gc_visit(const void *k, const void *v, void *c_) {
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
     gc_ctx c = {filter_time, 0, 0, m->ksz, NULL};
     om_foreach(m, gc_visit, &c);
+    uint32_t dead = 0;
+    for (uint32_t i = 0; i < c.n; i++) if (om_delete(m, c.keys + (size_t)i * c.ksz) == 0) dead++;
+    free(c.keys);
+    return dead;
+}
+
+/* ------------------------------------------------------------------ */
+/* LRU stand-in (the CT maps are BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:  */
+/* 53-75).  The kernel evicts from per-CPU LRU lists in an order that   */
+/* is not reproducible; libgpuflow and this restatement share one       */
+/* deterministic rule instead: after a batch, if count >     */
+/* max_entries, delete the smallest prefix of the age order — closing   */
+/* entries (rx_closing | tx_closing) first, then the others, each by    */
+/* ascending last use in one-second bins relative to now (bin 0 =       */
+/* last used 65535 s or more ago) — that leaves at most                 */
+/* max_entries - max_entries / 8 entries.  Last use = lifetime minus   */
+/* the timeout the entry's flags select (every lifetime writer sets it  */
+/* to now + that timeout, conntrack.h:47-62,127,527).                   */
+/* ------------------------------------------------------------------ */
+#define LRU_BINS 65536u
+typedef struct lru_ctx { uint32_t now; uint64_t *hist; } lru_ctx;
+static int64_t ct_last_use(uint32_t lt, uint16_t fl) {
+    const uint32_t to = ((fl & 1u) && (fl & 2u)) ? CT_CLOSE_TIMEOUT : ((fl & 16u) ? CT_DEFAULT_LIFETIME : CT_SYN_TIMEOUT);
+    return (int64_t)lt - (int64_t)to;
+}
+static uint32_t lru_key(uint32_t lt, uint16_t fl, uint32_t now) {
+    const int64_t base = (int64_t)now - (int64_t)(LRU_BINS - 1);
+    int64_t b = ct_last_use(lt, fl) - base;
+    b = b < 0 ? 0 : (b > (int64_t)(LRU_BINS - 1) ? (int64_t)(LRU_BINS - 1) : b);
+    return ((fl & 3u) ? 0u : LRU_BINS) + (uint32_t)b;
+}
+static void lru_visit(const void *k, const void *v, void *c_) {
+    (void)k;
+    lru_ctx *c = (lru_ctx *)c_;
+    uint32_t lt; uint16_t fl;
+    memcpy(&lt, (const uint8_t *)v + 32, 4); memcpy(&fl, (const uint8_t *)v + 36, 2);
+    c->hist[lru_key(lt, fl, c->now)]++;
+}
+int o_ct_lru_cutoffs(om_map *m, uint32_t now, uint64_t *cut_c, uint64_t *cut_o) {
+    *cut_c = *cut_o = 0;
+    if (m->count <= m->max_entries) return 0;
+    const uint64_t target = m->max_entries - m->max_entries / 8u, need = m->count - target;
+    uint64_t *h = (uint64_t *)calloc(2 * LRU_BINS, sizeof(uint64_t));
+    lru_ctx c = {now, h};
+    om_foreach(m, lru_visit, &c);
+    uint64_t acc = 0;
+    uint32_t kb = 2 * LRU_BINS - 1;
+    for (uint32_t k = 0; k < 2 * LRU_BINS; k++) { acc += h[k]; if (acc >= need) { kb = k; break; } }
+    free(h);
+    const int64_t base = (int64_t)now - (int64_t)(LRU_BINS - 1);
+    #define CUT_OF(b) ((b) == LRU_BINS - 1 ? (1ull << 32) : (base + (int64_t)(b) + 1 <= 0 ? 0ull : (uint64_t)(base + (int64_t)(b) + 1)))
+    if (kb < LRU_BINS) { *cut_c = CUT_OF(kb); *cut_o = 0; }
+    else { *cut_c = 1ull << 32; *cut_o = CUT_OF(kb - LRU_BINS); }
+    #undef CUT_OF
+    return 1;
+}
+typedef struct gc2_ctx { uint64_t cc, co; uint32_t n, cap, ksz; uint8_t *keys; } gc2_ctx;
+static void gc2_visit(const void *k, const void *v, void *c_) {
+    gc2_ctx *c = (gc2_ctx *)c_;
+    uint32_t lt; uint16_t fl;
+    memcpy(&lt, (const uint8_t *)v + 32, 4); memcpy(&fl, (const uint8_t *)v + 36, 2);
+    const int64_t age = ct_last_use(lt, fl);
+    if (age >= 0 && (uint64_t)age >= ((fl & 3u) ? c->cc : c->co)) return;
+    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 1024; c->keys = (uint8_t *)realloc(c->keys, (size_t)c->cap * c->ksz); }
+    memcpy(c->keys + (size_t)c->n * c->ksz, k, c->ksz);
+    c->n++;
+}
+/* The sweep of the rule above: closing entries last used before cut_c, the others before cut_o. */
+uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o) {
+    gc2_ctx c = {cut_c, cut_o, 0, 0, m->ksz, NULL};
+    om_foreach(m, gc2_visit, &c);
     uint32_t dead = 0;
     for (uint32_t i = 0; i < c.n; i++) if (om_delete(m, c.keys + (size_t)i * c.ksz) == 0) dead++;
     free(c.keys);

@@ -39,6 +39,7 @@ void    om_destroy(om_map *m);
 int     om_update(om_map *m, const void *key, const void *value, uint64_t flags);
 int     om_lookup(om_map *m, const void *key, void *value_out); /* 0 / -ENOENT */
 int     om_delete(om_map *m, const void *key);
+int     om_update_many(om_map *m, const void *keys, const void *values, uint32_t n, uint64_t flags, uint32_t *done);
 uint32_t om_count(om_map *m);
 /* Iterate all entries (order unspecified). Returns number visited. */
 typedef void (*om_visit_fn)(const void *key, const void *value, void *ctx);
@@ -184,6 +185,10 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now_sec, o
 
 /* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time);
+/* LRU stand-in (== libgpuflow): 1 and the cutoffs if count > max_entries. */
+int o_ct_lru_cutoffs(om_map *m, uint32_t now, uint64_t *cut_c, uint64_t *cut_o);
+/* Deletes closing entries last used before cut_c and the others last used before cut_o. */
+uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o);
 
 /* Shard of a CT key (unordered address pair), exposed for pre-population. */
 uint32_t o_ct_pair_hash4(uint32_t a, uint32_t b);

@@ -73,6 +73,7 @@ _s("om_destroy", None, VP)
 _s("om_update", C.c_int, VP, VP, VP, C.c_uint64)
 _s("om_lookup", C.c_int, VP, VP, VP)
 _s("om_delete", C.c_int, VP, VP)
+_s("om_update_many", C.c_int, VP, VP, VP, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32))
 _s("om_count", C.c_uint32, VP)
 _s("om_dump", C.c_uint32, VP, VP, VP, C.c_uint32)
 _s("o_parse_batch", None, C.POINTER(o_batch), C.POINTER(o_cols))
@@ -90,6 +91,8 @@ _s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C
 _s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
 _s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
+_s("o_ct_lru_cutoffs", C.c_int, VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
+_s("o_ct_gc2", C.c_uint32, VP, C.c_uint64, C.c_uint64)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
 _s("o_lpm4_iter_lookup", C.c_int, C.c_uint32, VP, C.c_int, C.c_uint32)
@@ -120,15 +123,13 @@ class OMap:
         return lib.om_update(self.ptr, key, value, flags)
 
     def update_many(self, keys, values, flags=0):
-        kb, vb = bytes(keys), bytes(values)
-        n = len(kb) // self.ksz
-        kbuf = C.create_string_buffer(kb, len(kb))
-        vbuf = C.create_string_buffer(vb, len(vb))
-        ka, va = C.addressof(kbuf), C.addressof(vbuf)
-        for i in range(n):
-            rc = lib.om_update(self.ptr, ka + i * self.ksz, va + i * self.vsz, flags)
-            if rc:
-                raise OSError(-rc, "om_update")
+        k = np.ascontiguousarray(keys, np.uint8).reshape(-1)
+        v = np.ascontiguousarray(values, np.uint8).reshape(-1)
+        n = len(k) // self.ksz
+        done = C.c_uint32(0)
+        rc = lib.om_update_many(self.ptr, k.ctypes.data, v.ctypes.data, n, flags, C.byref(done))
+        if rc:
+            raise OSError(-rc, f"om_update (entry {done.value})")
 
     def lookup(self, key):
         v = C.create_string_buffer(self.vsz)
@@ -143,6 +144,24 @@ class OMap:
 
     def ct_gc(self, filter_time):
         return lib.o_ct_gc(self.ptr, filter_time)
+
+    def lru_cutoffs(self, now):
+        """The LRU stand-in's cutoffs for this map's own contents (None: no eviction)."""
+        cc, co = C.c_uint64(0), C.c_uint64(0)
+        if not lib.o_ct_lru_cutoffs(self.ptr, now, C.byref(cc), C.byref(co)):
+            return None
+        return cc.value, co.value
+
+    def gc2(self, cut_c, cut_o):
+        return lib.o_ct_gc2(self.ptr, cut_c, cut_o)
+
+    def dump_arrays(self):
+        """All entries as (keys uint8[n, ksz], values uint8[n, vsz])."""
+        n = self.count()
+        k = np.zeros((max(1, n), self.ksz), np.uint8)
+        v = np.zeros((max(1, n), self.vsz), np.uint8)
+        m = lib.om_dump(self.ptr, k.ctypes.data, v.ctypes.data, n)
+        return k[:min(m, n)], v[:min(m, n)]
 
     def dump(self):
         n = self.count()

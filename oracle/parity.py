@@ -1,0 +1,121 @@
+"""Full-scale parity helpers — TEST INFRASTRUCTURE ONLY (bench.py's CPU leg and
+tests/; the product never imports this).
+
+The bench runs the CPU restatement on a *flow-group sample* of each workload:
+the packets whose unordered address pair satisfies `pair_sampled` (a hash of
+the pair, so a sample holds whole flow groups — every packet, CT entry and
+ICMP-related entry of a pair is in or out together, which is what makes a
+sampled run of the stateful path exact: conntrack state never crosses flow
+groups).  The GPU classifies the full batch; its records for the
+sampled packets and its CT entries of the sampled pairs must equal the
+oracle's bit for bit.
+"""
+import numpy as np
+
+SALT = np.uint64(0x5A3C_9E37_79B9_7F4A)
+_M1, _M2 = np.uint64(0xff51afd7ed558ccd), np.uint64(0xc4ceb9fe1a85ec53)
+
+
+def _fmix64(x):
+    x = np.asarray(x, dtype=np.uint64)
+    x = x ^ (x >> np.uint64(33))
+    x = x * _M1
+    x = x ^ (x >> np.uint64(33))
+    x = x * _M2
+    return x ^ (x >> np.uint64(33))
+
+
+def pair_sampled(a, b, div):
+    """IPv4: a, b = the two addresses as raw u32 words (network-order bytes loaded
+    little-endian, the column / CT-key form).  True where the unordered pair is in
+    the sample (1 in `div` pairs)."""
+    a = np.asarray(a).astype(np.uint32).astype(np.uint64)
+    b = np.asarray(b).astype(np.uint32).astype(np.uint64)
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    return (_fmix64(((hi << np.uint64(32)) | lo) ^ SALT) >> np.uint64(40)) % np.uint64(div) == 0
+
+
+def pair_sampled6(a16, b16, div):
+    """IPv6: a16, b16 = uint8[n, 16] addresses."""
+    a16 = np.ascontiguousarray(a16, np.uint8)
+    b16 = np.ascontiguousarray(b16, np.uint8)
+    ah, al = a16[:, :8].copy().view(">u8").ravel().astype(np.uint64), a16[:, 8:].copy().view(">u8").ravel().astype(np.uint64)
+    bh, bl = b16[:, :8].copy().view(">u8").ravel().astype(np.uint64), b16[:, 8:].copy().view(">u8").ravel().astype(np.uint64)
+    a_lt = (ah < bh) | ((ah == bh) & (al < bl))
+    lh, ll = np.where(a_lt, ah, bh), np.where(a_lt, al, bl)
+    hh, hl = np.where(a_lt, bh, ah), np.where(a_lt, bl, al)
+    x = _fmix64(lh ^ SALT)
+    x = _fmix64(x ^ ll)
+    x = _fmix64(x ^ hh)
+    x = _fmix64(x ^ hl)
+    return (x >> np.uint64(40)) % np.uint64(div) == 0
+
+
+def ct_sampled(keys, div):
+    """Rows of a CT dump (ipv4_ct_tuple 14 B / ipv6_ct_tuple 40 B keys) whose
+    address pair is in the sample."""
+    keys = np.ascontiguousarray(keys, np.uint8)
+    if keys.shape[1] == 14:
+        w = keys[:, :8].copy().view("<u4")
+        return pair_sampled(w[:, 0], w[:, 1], div)
+    return pair_sampled6(keys[:, 0:16], keys[:, 16:32], div)
+
+
+def compare_records(gpu, ref):
+    """Number of differing records and the first differing position (or -1)."""
+    g = np.ascontiguousarray(gpu).view(np.uint8).reshape(len(gpu), -1)
+    r = np.ascontiguousarray(ref).view(np.uint8).reshape(len(ref), -1)
+    if g.shape != r.shape:
+        return max(len(g), len(r)), 0
+    bad = np.nonzero((g != r).any(axis=1))[0]
+    return int(len(bad)), int(bad[0]) if len(bad) else -1
+
+
+def _sort_rows(k, v):
+    """Rows sorted by key bytes (lexicographic)."""
+    if len(k) == 0:
+        return k, v
+    w = (k.shape[1] + 7) // 8
+    pad = np.zeros((len(k), 8 * w), np.uint8)
+    pad[:, :k.shape[1]] = k
+    words = pad.view(">u8")                       # big-endian words: numeric order == byte order
+    o = np.lexsort([words[:, j] for j in range(w - 1, -1, -1)])
+    return k[o], v[o]
+
+
+def compare_tables(gk, gv, rk, rv):
+    """Entries of two dumps (keys/values arrays): (entries compared, entries that
+    differ or exist on one side only)."""
+    gk, gv = _sort_rows(np.ascontiguousarray(gk), np.ascontiguousarray(gv))
+    rk, rv = _sort_rows(np.ascontiguousarray(rk), np.ascontiguousarray(rv))
+    if len(gk) != len(rk):
+        gs = {bytes(x) for x in gk} if len(gk) < 2_000_000 else None
+        rs = {bytes(x) for x in rk} if len(rk) < 2_000_000 else None
+        only = len(gs ^ rs) if gs is not None and rs is not None else abs(len(gk) - len(rk))
+        return max(len(gk), len(rk)), max(only, abs(len(gk) - len(rk)))
+    kd = (gk != rk).any(axis=1)
+    vd = (gv != rv).any(axis=1)
+    return int(len(gk)), int((kd | vd).sum())
+
+
+def gpu_table_sampled(fd, ksz, vsz, div, chunk=1 << 20, pred=ct_sampled):
+    """The GPU map's entries of the sampled pairs, streamed through the chunked
+    dump (gf_map_lookup_batch) and filtered chunk by chunk."""
+    from cilium_amd import bpf
+    ks, vs = [], []
+    cursor, done, total = None, False, 0
+    while not done:
+        k, v, cursor, done = bpf.LookupBatch(fd, cursor, chunk, ksz, vsz)
+        total += len(k)
+        if len(k):
+            m = pred(k, div)
+            ks.append(k[m]); vs.append(v[m])
+    if not ks:
+        return np.zeros((0, ksz), np.uint8), np.zeros((0, vsz), np.uint8), total
+    return np.concatenate(ks), np.concatenate(vs), total
+
+
+def oracle_table_sampled(omap, div, pred=ct_sampled):
+    k, v = omap.dump_arrays()
+    m = pred(k, div) if len(k) else np.zeros(0, bool)
+    return k[m], v[m]

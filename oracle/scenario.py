@@ -59,6 +59,14 @@ class OracleDP:
         self.arr = None
         self._pipe = None
         self.cfgs = []
+        # LRU stand-in: the CT maps the programs bind, each with its
+        # classify-call counter; lru_replay[name] = {seq: (cut_c, cut_o)} replays the
+        # GPU's logged evictions instead (a sampled run holds only part of the table)
+        self.lru_maps = sorted({e[k] for e in sc.lxc for k in ("ct4", "ct6") if e.get(k)
+                                and sc.maps[e[k]].type == 9})
+        self.lru_seq = {n: 0 for n in self.lru_maps}
+        self.lru_replay = {}
+        self.lru_log = {n: [] for n in self.lru_maps}
         if sc.lxc:
             self.arr = O.lib.o_prog_array_create()
             for e in sc.lxc:
@@ -91,14 +99,32 @@ class OracleDP:
     def lb(self, pk, threads=1):
         return O.lb(self.lb_cfg, self.batch(pk), threads)
 
-    def ingress(self, pk, now, threads=1):
-        O.lib.o_set_node(C.byref(self._node))           # node_config.h is process-global in the restatement
-        return O.ingress(self.arr, self.batch(pk), now, threads)
+    def lru_after_call(self, now):
+        """After every classify call: the LRU stand-in on each bound CT map."""
+        for n in self.lru_maps:
+            self.lru_seq[n] += 1
+            seq = self.lru_seq[n]
+            if n in self.lru_replay:
+                cut = self.lru_replay[n].get(seq)
+            else:
+                cut = self.m[n].lru_cutoffs(now)
+            if cut is not None:
+                ev = self.m[n].gc2(*cut)
+                self.lru_log[n].append((seq, now, cut[0], cut[1], ev))
+
+    def ingress(self, pk, now, threads=1, lru=True):
+        """handle_policy over the batch; lru=False: part of a call whose LRU step
+        comes with its last part (a batch split across calls)."""
+        O.lib.o_set_node(C.byref(self._node))           # node_config.h is per thread in the restatement
+        out = O.ingress(self.arr, self.batch(pk), now, threads)
+        if lru:
+            self.lru_after_call(now)
+        return out
 
     def ingress_events(self, pk, out):
         return O.ingress_events(self.arr, self.batch(pk), out)
 
-    def pipeline(self, pk, now, threads=1, events=False):
+    def pipeline(self, pk, now, threads=1, events=False, lru=True):
         O.lib.o_set_node(C.byref(self._node))
         if self._pipe is None:
             nd = self.sc.netdev
@@ -107,11 +133,16 @@ class OracleDP:
             self._pipe = O.o_pipeline_cfg(C.pointer(self.xdp_cfg) if self.xdp_cfg is not None else None,
                                           C.pointer(self.lb_cfg) if self.lb_cfg is not None else None,
                                           C.pointer(self._nd), self.arr)
-        return O.pipeline(self._pipe, self.batch(pk), now, threads, events)
+        r = O.pipeline(self._pipe, self.batch(pk), now, threads, events)
+        if lru:
+            self.lru_after_call(now)
+        return r
 
     def egress(self, pk, now, events=False):
         O.lib.o_set_node(C.byref(self._node))
-        return O.egress(self.arr, self.batch(pk), now, events)
+        r = O.egress(self.arr, self.batch(pk), now, events)
+        self.lru_after_call(now)
+        return r
 
     def ct_gc(self, name, filter_time):
         return self.m[name].ct_gc(filter_time)

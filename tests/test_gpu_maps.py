@@ -1,0 +1,184 @@
+"""The map API on device-authoritative maps (pkg/bpf/map.go:322-498 semantics on
+the HBM replica, no whole-table pull), per-map locking under concurrent callers,
+and the LRU stand-in of the CT maps — all against the oracle."""
+import ctypes as C
+import errno
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from cilium_amd import bpf, synth
+from cilium_amd._lib import lib, gf_ct_evict_rec
+from cilium_amd.datapath import Datapath, DeviceBatch, ING_OUT, to_numpy
+from oracle.scenario import OracleDP
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _cmp(a, b, what):
+    if not np.array_equal(a, b):
+        bad = np.nonzero(a != b)[0]
+        raise AssertionError(f"{what}: {len(bad)} mismatches, first at {bad[0]}: gpu={a[bad[0]]} ref={b[bad[0]]}")
+
+
+def test_device_map_element_ops():
+    """After classify calls the CT and policy maps live in HBM.  Lookup / update /
+    delete / get_next_key / the chunked dump reach their elements there (a few
+    hundred bytes over PCIe per element operation, never the table), and traffic
+    after host-side edits sees exactly what the oracle sees after the same edits."""
+    sc = synth.fuzz(seed=21, n_packets=20000, n_batches=3)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi in range(2):
+        pk = sc.batches[bi]
+        io = dp.ingress(DeviceBatch(pk), sc.now + bi)
+        torch.cuda.synchronize()
+        _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, sc.now + bi), f"ingress b{bi}")
+    fd = dp.fd["ct4"]
+    info0 = bpf.GetMapInfo(fd)
+    want = ref.dump("ct4")
+    assert info0.Entries == len(want)
+    keys = sorted(want)
+    rnd = np.random.default_rng(1)
+    pick = [keys[i] for i in rnd.choice(len(keys), 64, replace=False)]
+    for k in pick:
+        assert bpf.LookupElement(fd, k, 48) == want[k]
+    with pytest.raises(bpf.BPFError) as e:
+        bpf.LookupElement(fd, b"\x01" * 14, 48)
+    assert e.value.errno == errno.ENOENT
+    info1 = bpf.GetMapInfo(fd)
+    assert info1.XferD2H - info0.XferD2H < 64 * 4096, "element lookups must not pull the table"
+    # edits on both sides: deletes, overwrites, NOEXIST / EXIST errors, new entries
+    om = ref.m["ct4"]
+    for k in pick[:16]:
+        bpf.DeleteElement(fd, k)
+        assert om.delete(k) == 0
+    for k in pick[16:32]:
+        v = bytearray(want[k]); v[32:36] = (sc.now + 7).to_bytes(4, "little")
+        bpf.UpdateElement(fd, k, bytes(v), bpf.BPF_EXIST)
+        assert om.update(k, bytes(v), 2) == 0
+    for k in pick[32:40]:
+        with pytest.raises(bpf.BPFError) as e:
+            bpf.UpdateElement(fd, k, want[k], bpf.BPF_NOEXIST)
+        assert e.value.errno == errno.EEXIST
+    for j in range(8):
+        k = bytes([10, 9, 8, j]) + bytes([100, 64, 1, j]) + bytes([0, 80, 0x9c, 0x40, 6, 0])
+        v = synth.ct_vals(1, sc.now + 300, 0, 0, 300)[0].tobytes()
+        bpf.UpdateElement(fd, k, v, bpf.BPF_NOEXIST)
+        assert om.update(k, v, 1) == 0
+    info2 = bpf.GetMapInfo(fd)
+    assert info2.Entries == om.count()
+    assert info2.XferD2H < info0.DeviceBytes / 4
+    # the reference's dump loop on the device replica, and the chunked dump
+    m = bpf.Map("ct4", 9, 14, 48, 100000)
+    m.fd = fd
+    kbk = {}
+    m.DumpKeyByKey(lambda k, v: kbk.__setitem__(k, v))
+    assert kbk == ref.dump("ct4") == dp.dump_map("ct4")
+    # traffic after the edits
+    pk = sc.batches[2]
+    io = dp.ingress(DeviceBatch(pk), sc.now + 2)
+    torch.cuda.synchronize()
+    _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, sc.now + 2), "ingress after edits")
+    assert dp.dump_map("ct4") == ref.dump("ct4")
+    for e in range(16):
+        assert dp.dump_map(f"pol{e}") == ref.dump(f"pol{e}"), f"policy counters pol{e}"
+
+
+def test_concurrent_map_ops_and_classify():
+    """Map updates, lookups and dumps from several threads while another thread
+    classifies: per-map locks serialise each map, classify calls hold the maps
+    they bind; verdicts and final state equal the oracle's (the concurrent edits
+    touch maps the traffic does not read, so their order does not matter)."""
+    sc = synth.fuzz(seed=23, n_packets=20000, n_batches=4)
+    sc.add_map(synth.MapSpec("side_hash", synth.HASH, 8, 24, 100000, 0))
+    sc.add_map(synth.MapSpec("side_lpm", synth.LPM, 8, 1, 10000, synth.NO_PREALLOC))
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    errs, outs = [], []
+    stop = threading.Event()
+
+    def classify():
+        try:
+            for bi, pk in enumerate(sc.batches):
+                io = dp.ingress(DeviceBatch(pk), sc.now + bi)
+                torch.cuda.synchronize()
+                outs.append(to_numpy(io, ING_OUT))
+        except Exception as e:        # reported by the main thread
+            errs.append(e)
+        finally:
+            stop.set()
+
+    def writer(tid):
+        try:
+            rnd = np.random.default_rng(tid)
+            fd = dp.fd["side_hash"] if tid % 2 else dp.fd["side_lpm"]
+            i = 0
+            while not stop.is_set() or i < 200:
+                if tid % 2:
+                    k = int(tid * 1_000_000 + i).to_bytes(8, "little")
+                    bpf.UpdateElement(fd, k, bytes(24))
+                    assert bpf.LookupElement(fd, k, 24) == bytes(24)
+                else:
+                    k = (24).to_bytes(4, "little") + bytes([10, tid, i % 256, 0])
+                    bpf.UpdateElement(fd, k, b"\x01")
+                i += 1
+        except Exception as e:
+            errs.append(e)
+
+    def reader():
+        try:
+            while not stop.is_set():
+                bpf.GetMapInfo(dp.fd["ct4"])
+                bpf.GetMapInfo(dp.fd["pol0"])
+        except Exception as e:
+            errs.append(e)
+
+    th = [threading.Thread(target=classify)] + [threading.Thread(target=writer, args=(t,)) for t in range(1, 5)] + \
+        [threading.Thread(target=reader)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert len(outs) == len(sc.batches)
+    for bi, pk in enumerate(sc.batches):
+        _cmp(outs[bi], ref.ingress(pk, sc.now + bi), f"ingress b{bi}")
+    assert dp.dump_map("ct4") == ref.dump("ct4")
+    assert bpf.GetMapInfo(dp.fd["side_hash"]).Entries >= 400
+
+
+def _evict_log(fd):
+    recs = (gf_ct_evict_rec * 4096)()
+    n = lib.gf_ct_evict_log(fd, recs, 4096)
+    assert n >= 0
+    return [(r.seq, r.now_sec, r.cut_closing, r.cut_other, r.evicted) for r in recs[:n]]
+
+
+@pytest.mark.parametrize("seed", [4, 6])
+def test_lru_eviction_matches_oracle(seed):
+    """LRU CT maps overflowing max_entries: after every batch the device evicts by
+    the deterministic age rule (closing entries, then by lifetime) down to the
+    7/8 watermark, exactly as the oracle's restatement of the rule; verdicts of
+    the following batches, the CT contents and the eviction logs are identical,
+    and the count is back under max_entries at every batch boundary."""
+    sc = synth.fuzz(seed=seed, n_packets=20000, n_batches=5, ct_max=2500, ct6_max=300)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        now = sc.now + 40 * bi
+        io = dp.ingress(DeviceBatch(pk), now)
+        torch.cuda.synchronize()
+        _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, now), f"ingress b{bi}")
+        for name, mx in (("ct4", 2500), ("ct6", 300)):
+            assert bpf.GetMapInfo(dp.fd[name]).Entries == ref.m[name].count() <= mx, name
+    for name in ("ct4", "ct6"):
+        assert dp.dump_map(name) == ref.dump(name), name
+        assert _evict_log(dp.fd[name]) == ref.lru_log[name], name
+    assert len(ref.lru_log["ct4"]) >= 2 and len(ref.lru_log["ct6"]) >= 1

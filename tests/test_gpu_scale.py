@@ -1,0 +1,121 @@
+"""Bit-exact parity at the configurations' real table shapes (BASELINE configs 2
+and 5): the device stream of the bench, checked against the oracle on a
+flow-group sample (whole address pairs, so the sampled run of the stateful path
+is exact) — every sampled record and, after the last step, every CT entry of the
+sampled pairs."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from cilium_amd import synth, stream
+from cilium_amd.datapath import Datapath, ING_OUT, PIPE_OUT
+from cilium_amd.synth import Packets
+from oracle.scenario import OracleDP
+from oracle import parity as PY
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+class _Cols:
+    def __init__(self, cols, n):
+        from cilium_amd.datapath import DeviceBatch
+        self.n, self.device, self.cdict = n, "cuda", cols
+        self.saddr6 = self.daddr6 = self.flow_hash = None
+        for k, v in cols.items():
+            setattr(self, k, v)
+        self._cols = DeviceBatch.cols
+
+    def cols(self):
+        return self._cols(self)
+
+
+def _host_packets(cdict, idx):
+    c = {k: v[idx].cpu().numpy() for k, v in cdict.items()}
+    to_u = {np.dtype(np.int32): np.uint32, np.dtype(np.int16): np.uint16}
+    c = {k: (v.view(to_u[v.dtype]) if v.dtype in to_u else v) for k, v in c.items()}
+    f, lens = stream.to_frames(c)
+    return Packets(f, lens, c["src_identity"], c["ifindex"], c["lxc_id"], c["tc_index"])
+
+
+def test_config2_real_shape_sampled_parity():
+    """Config 2 at its real table shape: 256 endpoints, 4,352 identities, full-size
+    per-endpoint policy (2,000 L3 + 4,000 L4 + 32 wildcard entries) and CIDR maps,
+    2^20 address pairs; the bench's steady-state stream (1M packets per step, 4
+    steps) with its pre-inserted egress replies.  1/8 of the pairs through the
+    oracle: records and the sampled pairs' CT entries bit-exact."""
+    sc, P, _ = synth.config2_tables(n_pairs=1 << 20, ct_max=1 << 24)
+    st = stream.Stream(P, flows_per_step=1 << 18, device="cuda")
+    S0, N = 3, 4
+    rk, rv = st.reply_ct_entries(S0 + N)
+    sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc, shards=8)
+    div = 8
+    samp = torch.from_numpy(PY.pair_sampled(st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy(), div)).cuda()
+    compared = 0
+    for s in range(N):
+        cols, p, n = st.step(S0 + s)
+        b = _Cols(cols, n)
+        out = dp.ingress(b, sc.now + s)
+        torch.cuda.synchronize()
+        idx = torch.nonzero(samp[p]).squeeze(1)
+        r = ref.ingress(_host_packets(cols, idx), sc.now + s, threads=8)
+        g = out[idx].cpu().numpy().view(ING_OUT).ravel()
+        bad, first = PY.compare_records(g, r)
+        assert bad == 0, f"step {s}: {bad} mismatches, first sampled row {first}: gpu={g[first]} ref={r[first]}"
+        compared += len(r)
+    assert compared > 400_000
+    assert len(np.unique(r["ct_ret"])) == 4 and (r["action"] == 2).any() and (r["action"] == 7).any()
+    gk, gv, gtot = PY.gpu_table_sampled(dp.fd["cilium_ct4_global"], 14, 48, div)
+    ok, ov = PY.oracle_table_sampled(ref.m["cilium_ct4_global"], div)
+    n, bad = PY.compare_tables(gk, gv, ok, ov)
+    assert bad == 0 and n > 100_000, (n, bad, gtot)
+
+
+def test_config5_real_shape_parity_with_eviction():
+    """Config 5 at its real table shape: v6_fix 100k /128s and v6_dyn 10k /32-/127
+    prefixes through bpf_xdp's check_v6, bpf_netdev's handle_ipv6 (flow-label
+    identities), ipv6_policy / ct_lookup6 on a 10,485,760-entry LRU CT pre-filled
+    past its low watermark, so the LRU stand-in evicts at full scale after every
+    batch.  The whole stream (262k packets per step) through the oracle: records,
+    the eviction logs and the full CT6 bit-exact."""
+    from cilium_amd import bpf
+    from cilium_amd._lib import lib, gf_ct_evict_rec
+    sc, P, meta = synth.config5_tables(n_pairs=1 << 20, prefill=10_300_000)
+    st = stream.Stream6Frames(P, meta, flows_per_step=1 << 16, device="cuda")
+    S0, N = 3, 4
+    rk, rv = st.reply_ct6_entries(S0 + N)
+    ct6 = sc.maps["cilium_ct6_global"]
+    ct6.keys, ct6.vals = synth.ct6_prefill(meta, rk, rv, sc.now)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc, shards=8)
+    for s in range(N):
+        f, lens, p = st.step(S0 + s)
+
+        class B:
+            pass
+        b = B()
+        b.frames, b.len, b.tc_index, b.flow_hash, b.n, b.device = f, lens, None, None, f.shape[0], "cuda"
+        out, _, _ = dp.pipeline(b, sc.now + s, snap_out=False)
+        torch.cuda.synchronize()
+        r = ref.pipeline(Packets(f.cpu().numpy(), lens.cpu().numpy().view(np.uint32)), sc.now + s, threads=8)[0]
+        g = out.cpu().numpy().view(PIPE_OUT).ravel()
+        bad, first = PY.compare_records(g, r)
+        assert bad == 0, f"step {s}: {bad} mismatches, first row {first}: gpu={g[first]} ref={r[first]}"
+        assert bpf.GetMapInfo(dp.fd["cilium_ct6_global"]).Entries == ref.m["cilium_ct6_global"].count() <= 10_485_760
+    assert set(np.unique(r["stage"])) >= {1, 4} and len(np.unique(r["ct_ret"][r["stage"] == 4])) >= 3
+    recs = (gf_ct_evict_rec * 64)()
+    nlog = lib.gf_ct_evict_log(dp.fd["cilium_ct6_global"], recs, 64)
+    glog = [(x.seq, x.now_sec, x.cut_closing, x.cut_other, x.evicted) for x in recs[:nlog]]
+    assert glog == ref.lru_log["cilium_ct6_global"] and len(glog) >= 1
+    m = bpf.Map("ct6", 9, 40, 48, 10_485_760)
+    m.fd = dp.fd["cilium_ct6_global"]
+    gk, gv = m.DumpArrays()
+    ok, ov = ref.m["cilium_ct6_global"].dump_arrays()
+    n, bad = PY.compare_tables(gk, gv, ok, ov)
+    assert bad == 0 and n > 9_000_000, (n, bad)

@@ -59,6 +59,54 @@ def test_hash_semantics_vs_oracle(ksz, vsz):
     m.DumpWithCallback(lambda k, v: got.__setitem__(k, v))
     assert got == om.dump()
     assert bpf.GetMapInfo(fd).Entries == om.count()
+    # the reference's own loop (GetNextKey + LookupElement) and small dump chunks agree
+    kbk, small = [], []
+    m.DumpKeyByKey(lambda k, v: kbk.append((k, v)))
+    m.DumpWithCallback(lambda k, v: small.append((k, v)), chunk=7)
+    assert kbk == small and dict(kbk) == got
+
+
+def test_lookup_batch_cursor_contract():
+    """gf_map_lookup_batch: every entry exactly once across chunks, -ENOENT with the
+    last chunk, an exhausted cursor keeps returning -ENOENT with count 0; LPM tries
+    dump in get_next_key's post-order."""
+    fd, om = _ops(bpf.BPF_MAP_TYPE_HASH, 14, 48, 500, seed=9, nops=2000, keyspace=400)
+    seen, cur, done, calls = [], None, False, 0
+    while not done:
+        k, v, cur, done = bpf.LookupBatch(fd, cur, 13, 14, 48)
+        assert len(k) <= 13
+        seen += [(a.tobytes(), b.tobytes()) for a, b in zip(k, v)]
+        calls += 1
+    assert dict(seen) == om.dump() and len(seen) == len(om.dump())
+    k, v, cur2, done = bpf.LookupBatch(fd, cur, 13, 14, 48)
+    assert len(k) == 0 and done
+    lfd, lom = _ops(bpf.BPF_MAP_TYPE_LPM_TRIE, 8, 1, 120, seed=3)
+    lm = bpf.Map("l", 11, 8, 1, 120)
+    lm.fd = lfd
+    a, b = [], []
+    lm.DumpKeyByKey(lambda k, v: a.append(k))
+    lm.DumpWithCallback(lambda k, v: b.append(k), chunk=5)
+    assert a == b
+
+
+def test_gc_on_fresh_lru_ct_map():
+    """ctmap.GC / Flush on a CT map that holds no entry yet — freshly opened (an
+    LRU map's slot array is not materialised until its first insert) and after a
+    program bound it but before any classify — deletes nothing and succeeds."""
+    import ctypes as C
+    from cilium_amd._lib import lib, gf_lxc_cfg
+    for ksz in (14, 40):
+        fd = bpf.CreateMap(bpf.BPF_MAP_TYPE_LRU_HASH, ksz, 48, 1 << 16)
+        assert lib.gf_ct_gc(fd, 5000, None) == 0
+        assert lib.gf_ct_gc(fd, 0xFFFFFFFF, None) == 0           # Flush
+    ct4 = bpf.CreateMap(bpf.BPF_MAP_TYPE_LRU_HASH, 14, 48, 1 << 16)
+    pol = bpf.CreateMap(bpf.BPF_MAP_TYPE_HASH, 8, 24, 16384)
+    cfg = gf_lxc_cfg()
+    cfg.lxc_id, cfg.seclabel, cfg.policy_map, cfg.ct_map4, cfg.flags = 7, 300, pol, ct4, 0x1e
+    assert lib.gf_lxc_prog_load(C.byref(cfg)) > 0
+    assert lib.gf_ct_gc(ct4, 5000, None) == 0
+    assert lib.gf_ct_gc(ct4, 0xFFFFFFFF, None) == 0
+    assert bpf.GetMapInfo(ct4).Entries == 0
 
 
 @pytest.mark.parametrize("ksz", [8, 20])
