@@ -47,6 +47,10 @@ def _worker(rank, world, port, q):
     from oracle.scenario import OracleDP
     sc = synth.pipeline_fuzz(seed=21, n_packets=6000, n_batches=2)
     ref, mine = OracleDP(sc), OracleDP(sc)
+    for n in ("ct4", "ct6"):                       # a rank holds only its CT partition, pre-inserted entries too
+        for k in list(mine.dump(n)):
+            if _ct_owner(k, world) != rank:
+                mine.m[n].delete(k)
     ok = True
     for bi, pk in enumerate(sc.batches):
         arrive = [np.nonzero(np.arange(pk.n) % world == s)[0] for s in range(world)]
@@ -76,9 +80,8 @@ def _worker(rank, world, port, q):
     for n in ("ct4", "ct6"):
         union = {}
         for r, g in enumerate(gathered):
-            for k, v in g[n].items():
-                if _ct_owner(k, world) == r:
-                    union[k] = v
+            ct_ok &= all(_ct_owner(k, world) == r for k in g[n])    # no entry on a rank that does not own it
+            union.update(g[n])
         ct_ok &= union == ref.dump(n)
     q.put((rank, ok, ct_ok))
     dist.destroy_process_group()
