@@ -1,0 +1,75 @@
+"""Connectivity matrices of the reference's runtime suite (test/runtime/Policies.go
+"L3/L4 Checks", "L4Policy Checks", "CIDR" checks; tests/golden/runtime_policies.json)
+replayed as packets: the CPU oracle must reproduce every allow/deny the
+reference asserts, and the HIP path must produce the oracle's records
+bit-for-bit on the same packets.
+
+The older shell tests the verdict names (tests/01-ct.sh, tests/16-cidr-ingress-policy.sh)
+exit 0 at their top in this tree — replaced by the Ginkgo suite transcribed
+here — so their matrices are not asserted.  01-ct.sh also expects app -> server
+traffic to pass under PolicyEnforcement=always without an egress rule, which
+1.0's egress enforcement (Policies.go:762-786) contradicts."""
+import pytest
+
+from tests import runtime_matrix as RM
+
+DOC = RM.load()
+CASES = DOC["cases"]
+
+
+def _ids():
+    return [c["name"] for c in CASES]
+
+
+def test_fixture_covers_reference_checks():
+    assert len(CASES) >= 10
+    n = sum(len(RM.expand(c)) for c in CASES)
+    assert n >= 80
+    assert {c["enforcement"] for c in CASES} == {"default", "always"}
+    # both outcomes in both directions of enforcement
+    assert any(not ok for c in CASES for *_, ok in RM.expand(c))
+
+
+def test_agent_restatement_flags():
+    """Default enforcement: a direction is enforced only when a rule selecting
+    the endpoint has rules in it (GetRulesMatching)."""
+    topo = RM.Topology(DOC["endpoints"])
+    sc = RM.compile_case(CASES[0], topo)
+    fl = {topo.names[i]: c["flags"] for i, c in enumerate(sc.lxc)}
+    I, E = RM.S.LXC_POLICY_INGRESS, RM.S.LXC_POLICY_EGRESS
+    assert fl["httpd1"] & I and not fl["httpd1"] & E
+    assert fl["app3"] & E and not fl["app3"] & I
+    assert not fl["app1"] & (I | E)
+    sc = RM.compile_case(next(c for c in CASES if c["enforcement"] == "always"), topo)
+    assert all(c["flags"] & I and c["flags"] & E for c in sc.lxc)
+
+
+@pytest.mark.parametrize("case", CASES, ids=_ids())
+def test_oracle_matches_reference_matrix(case):
+    topo = RM.Topology(DOC["endpoints"])
+    res, _ = RM.run_case(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
+    bad = RM.outcome_mismatches(case, res)
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_gpu_matches_reference_matrix_and_oracle():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    from oracle import parity as PY
+    topo = RM.Topology(DOC["endpoints"])
+    for case in CASES:
+        sc = RM.compile_case(case, topo)
+        gpu = RM.GpuBackend(sc)
+        try:
+            gres, glog = RM.run_case(case, topo, gpu)
+        finally:
+            gpu.close()
+        ores, olog = RM.run_case(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
+        assert not RM.outcome_mismatches(case, gres), (case["name"], RM.outcome_mismatches(case, gres))
+        assert [(k, s) for k, s, _ in glog] == [(k, s) for k, s, _ in olog], case["name"]
+        for (kind, step, g), (_, _, o) in zip(glog, olog):
+            bad, first = PY.compare_records(g, o)
+            assert bad == 0, (case["name"], kind, step, g[first], o[first])
