@@ -82,6 +82,7 @@ struct Map : Obj {
     bool fixed_capacity = false; // device inserts into this map (CT): nslots sized by max_entries
     uint64_t dev_count_hi = 0;  // upper bound of the device element count (classify bookkeeping)
     uint64_t dev_gen = 0;       // bumped on every device-side change (invalidates nk_cache)
+    uint64_t host_gen = 0;      // bumped on every update / delete through the map API
     uint64_t xfer_d2h = 0, xfer_h2d = 0;   // bytes the map API moved over PCIe (gf_map_info)
     DevBuf d_slots, d_vals, d_count;
     DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits

@@ -20,6 +20,9 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <functional>
+#include <unordered_set>
+#include <algorithm>
+#include <array>
 #include <string.h>
 
 using namespace gf;
@@ -2251,7 +2254,37 @@ struct EgDev {
     uint32_t *seq;                      // device word: 1 = single-bucket batch (written by k_eg_front)
     uint32_t *ctlog, *ctlog_n;          // deferred service entries {i, key[4], value[12], pad[3]}; [n, v6 deliveries]
     IngCtx X;                           // redirect writes + cilium_proxy4 log (pol_redirect)
+    uint64_t *hz_ck;                    // per packet: connection key of the frame tuple after the front (0: none)
+    uint64_t *hz_pk;                    // per packet: key of its unordered address pair
+    uint64_t *hz_dk, *hz_sk;            // per packet: keys of its destination / source address
+    const uint32_t *vip4;               // the rev-NAT addresses of the programs' revNAT maps (open addressing,
+    const uint4 *vip6;                  //   0 = empty), vip*_mask + 1 slots; null: none
+    uint32_t vip4_mask, vip6_mask;
+    uint8_t *hz_fl;                     // per packet: GF_HZ_* (null: no ordering check)
+    uint32_t *hz;                       // device words: [0] 1 = ordering hazard (k_eg_groups idles), [1] GF_HZ_* kinds seen
 };
+// The ordering check.  The reference runs a local delivery's
+// handle_policy right after its from-container program, before the next packet;
+// the batch runs every from-container part first.  The two orders differ only
+// when a packet's from-container CT lookup reads an entry an earlier delivery's
+// handle_policy writes: a packet whose tuple is the reverse of an earlier
+// packet's (a reply in the same batch), or the tuples of the single-bucket class
+// (saddr == daddr, IPV4_LOOPBACK, lb4_local back to the sender).  The front keys
+// each packet by its unordered 5-tuple (ICMP: ports 0) and direction; such a
+// batch is cut into contiguous runs without a hazard, run one after the other.
+// ICMP packets also read the related entry every new flow of their address pair
+// creates (ct_create4/6): an ICMP packet conflicts with any earlier packet of its pair.
+#define GF_HZ_VALID   1u                // continues past the front
+#define GF_HZ_DIR     2u                // the tuple's direction within its connection key
+#define GF_HZ_SPECIAL 4u                // single-bucket tuple: runs alone
+#define GF_HZ_ICMP    8u                // ICMP / ICMPv6: probes the pair key
+// A reply a service backend sends is rev-NATed (lb4_rev_nat / lb6_rev_nat) before
+// its delivery: handle_policy's tuple is {service address, one of the packet's own
+// addresses} (the loopback branch moves the source into daddr).  It meets a later
+// packet only if that one goes to the service address without translation.  Such
+// a packet (GF_HZ_VIP) conflicts with any earlier packet that has its source
+// address as source or destination.
+#define GF_HZ_VIP    16u
 #define GF_CTLOG_WORDS 20u
 
 // The header bytes the IPv4 egress programs touch (< l4_off + 18 <= 92) are staged
@@ -2381,6 +2414,50 @@ __device__ __forceinline__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Ro
 // handle_ingress + the stateless head of handle_ipv4_from_lxc, one packet per lane
 // FAM 6 takes the IPv6 frames, FAM 4 every other frame (two launches: the IPv6
 // path's registers and stack stay out of the IPv4 kernel).
+__device__ __forceinline__ bool vip4_has(const EgDev &E, uint32_t a) {
+    if (!E.vip4 || !a) return false;
+    uint32_t slot = (a * 0x9E3779B1u) & E.vip4_mask;
+    for (uint32_t k = 0; k <= E.vip4_mask; k++) {
+        const uint32_t v = E.vip4[slot];
+        if (v == a) return true;
+        if (!v) return false;
+        slot = (slot + 1u) & E.vip4_mask;
+    }
+    return false;
+}
+__device__ __forceinline__ bool vip6_has(const EgDev &E, const uint32_t *a) {
+    if (!E.vip6 || !(a[0] | a[1] | a[2] | a[3])) return false;
+    uint32_t slot = ((a[0] ^ a[1] ^ a[2] ^ a[3]) * 0x9E3779B1u) & E.vip6_mask;
+    for (uint32_t k = 0; k <= E.vip6_mask; k++) {
+        const uint4 v = E.vip6[slot];
+        if (v.x == a[0] && v.y == a[1] && v.z == a[2] && v.w == a[3]) return true;
+        if (!(v.x | v.y | v.z | v.w)) return false;
+        slot = (slot + 1u) & E.vip6_mask;
+    }
+    return false;
+}
+__device__ __forceinline__ uint64_t hz_mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdull;
+    return h ^ (h >> 31);
+}
+// Connection key of a tuple: order-free hash of {(sa, sp), (da, dp)} + nexthdr;
+// dir = the (sa, sp) side sorts second.
+__device__ __forceinline__ uint64_t hz_key(const uint32_t *sa, const uint32_t *da, int nw, uint32_t sp, uint32_t dp,
+                                           uint32_t nh, bool &dir) {
+    int c = 0;
+    for (int k = 0; k < nw && !c; k++) c = sa[k] < da[k] ? -1 : (sa[k] > da[k] ? 1 : 0);
+    if (!c) c = sp < dp ? -1 : (sp > dp ? 1 : 0);
+    dir = c > 0;
+    const uint32_t *lo = dir ? da : sa, *hi = dir ? sa : da;
+    uint64_t h = 0x5eed0000ull | (uint64_t)nw;
+    for (int k = 0; k < nw; k++) h = hz_mix(h, lo[k]);
+    h = hz_mix(h, dir ? dp : sp);
+    for (int k = 0; k < nw; k++) h = hz_mix(h, hi[k]);
+    h = hz_mix(h, ((dir ? sp : dp) << 8) | nh);
+    return h | 1ull;
+}
+
 template <int FAM>
 __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t *lxc_id, const uint32_t *fhash, EgDev E,
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
@@ -2518,6 +2595,44 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             r.st = 0;                                       // continue in k_eg_groups
         } while (0);
         uint32_t key;
+        uint64_t hck = 0, hpk = 0, hdk = 0, hsk = 0;
+        uint32_t hfl = 0;
+        if (r.st == 0) {
+            const int lo4 = r.l4_off;
+            const bool tu = (r.nh == 6 || r.nh == 17) && skb_ok(lo4 + 0, 4, len);
+            bool dir = false;
+            if (FAM == 6) {
+                const uint32_t sp = tu ? wg.r16((uint32_t)lo4) : 0u, dp = tu ? wg.r16((uint32_t)lo4 + 2u) : 0u;
+                uint32_t s6[4], d6[4];
+                for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
+                hck = hz_key(s6, d6, 4, sp, dp, r.nh, dir);
+                bool pd, same = true;
+                hpk = hz_key(s6, d6, 4, 0u, 0u, 0x1ffu, pd);
+                hdk = hz_key(d6, d6, 4, 0u, 0u, 0x2ffu, pd);
+                hsk = hz_key(s6, s6, 4, 0u, 0u, 0x2ffu, pd);
+                for (int k = 0; k < 4; k++) same &= s6[k] == d6[k];
+                const bool vip = !(r.eflags & GF_EG_F_LB) && vip6_has(E, d6);
+                hfl = GF_HZ_VALID | (dir ? GF_HZ_DIR : 0u) | (same ? GF_HZ_SPECIAL : 0u) | (r.nh == 58 ? GF_HZ_ICMP : 0u) |
+                      (vip ? GF_HZ_VIP : 0u);
+            } else {
+                const uint32_t sp = tu ? w.r16((uint32_t)lo4) : 0u, dp = tu ? w.r16((uint32_t)lo4 + 2u) : 0u;
+                const uint32_t fs = w.r32(26), fd = w.r32(30), lo = E.loopback;
+                hck = hz_key(&fs, &fd, 1, sp, dp, r.nh, dir);
+                bool pd;
+                hpk = hz_key(&fs, &fd, 1, 0u, 0u, 0x1ffu, pd);
+                hdk = hz_key(&fd, &fd, 1, 0u, 0u, 0x2ffu, pd);
+                hsk = hz_key(&fs, &fs, 1, 0u, 0u, 0x2ffu, pd);
+                const bool vip = !(r.eflags & GF_EG_F_LB) && vip4_has(E, fd);
+                const bool sp_ = (r.eflags & GF_EG_F_LOOPBACK) || r.t_saddr == r.t_daddr || fs == fd ||
+                                 (lo && (r.t_saddr == lo || r.t_daddr == lo || fs == lo || fd == lo));
+                hfl = GF_HZ_VALID | (dir ? GF_HZ_DIR : 0u) | (sp_ ? GF_HZ_SPECIAL : 0u) | (r.nh == 1 ? GF_HZ_ICMP : 0u) |
+                      (vip ? GF_HZ_VIP : 0u);
+            }
+        }
+        if (E.hz_fl) {
+            E.hz_ck[i] = hck; E.hz_pk[i] = hpk; E.hz_dk[i] = hdk; E.hz_sk[i] = hsk; E.hz_fl[i] = (uint8_t)hfl;
+            if (hfl & (GF_HZ_ICMP | GF_HZ_VIP)) atomicOr(E.hz + 1, hfl);   // the batch's kinds
+        }
         if (r.st == 0 && FAM == 6) {
             uint32_t s6[4], d6[4];
             for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
@@ -2550,6 +2665,63 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
 __global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, uint32_t n, uint32_t *keys) {
     if (!*seq) return;
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] &= GF_KEY_FAM;
+}
+
+// The ordering check: every continuing packet records the first batch index of
+// its connection key per direction (open addressing, key 0 = empty)...
+__device__ __forceinline__ void hz_put(unsigned long long k, uint32_t half, uint32_t i, unsigned long long *tkey,
+                                       uint32_t *tfirst, uint32_t mask) {
+    uint32_t slot = (uint32_t)(k >> 32) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const unsigned long long old = atomicCAS(&tkey[slot], 0ull, k);
+        if (old == 0ull || old == k) { atomicMin(&tfirst[2 * slot + half], i); return; }
+        slot = (slot + 1u) & mask;
+    }
+}
+__device__ __forceinline__ uint32_t hz_get(unsigned long long k, uint32_t half, const unsigned long long *tkey,
+                                           const uint32_t *tfirst, uint32_t mask) {
+    uint32_t slot = (uint32_t)(k >> 32) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const unsigned long long t = tkey[slot];
+        if (t == k) return tfirst[2 * slot + half];
+        if (t == 0ull) break;
+        slot = (slot + 1u) & mask;
+    }
+    return 0xffffffffu;
+}
+__global__ __launch_bounds__(BLOCK) void k_hz_insert(const uint64_t *ck, const uint64_t *pk, const uint64_t *dk,
+                                                     const uint64_t *sk, const uint8_t *fl, uint32_t n, const uint32_t *hz,
+                                                     unsigned long long *tkey, uint32_t *tfirst, uint32_t mask) {
+    const uint32_t kinds = hz[1];                       // pair / destination keys only when a packet probes them
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t f = fl[i];
+        if ((f & (GF_HZ_VALID | GF_HZ_SPECIAL)) != GF_HZ_VALID) continue;
+        hz_put(ck[i], (f & GF_HZ_DIR) ? 1u : 0u, i, tkey, tfirst, mask);
+        if (kinds & GF_HZ_ICMP) hz_put(pk[i], 0u, i, tkey, tfirst, mask);
+        if (kinds & GF_HZ_VIP) { hz_put(dk[i], 0u, i, tkey, tfirst, mask); hz_put(sk[i], 0u, i, tkey, tfirst, mask); }
+    }
+}
+// ... then a packet whose reverse direction appeared earlier in the batch, or a
+// single-bucket tuple in a batch of two or more, flags the batch.
+__global__ __launch_bounds__(BLOCK) void k_hz_probe(const uint64_t *ck, const uint64_t *pk, const uint64_t *sk,
+                                                    const uint8_t *fl, uint32_t n, const unsigned long long *tkey,
+                                                    const uint32_t *tfirst, uint32_t mask, uint32_t *hz) {
+    bool hit = false;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t f = fl[i];
+        if (!(f & GF_HZ_VALID)) continue;
+        if (f & GF_HZ_SPECIAL) { hit = true; continue; }
+        if (f & GF_HZ_ICMP) hit |= hz_get(pk[i], 0u, tkey, tfirst, mask) < i;
+        else hit |= hz_get(ck[i], (f & GF_HZ_DIR) ? 0u : 1u, tkey, tfirst, mask) < i;
+        if (f & GF_HZ_VIP) hit |= hz_get(sk[i], 0u, tkey, tfirst, mask) < i;
+    }
+    if (__any(hit) && (threadIdx.x & 63u) == 0) atomicOr(hz, 1u);
+}
+
+// Adds a call's counter block to the registered sink.
+__global__ void k_stats_fold(const unsigned long long *src, unsigned long long *dst) {
+    for (int k = threadIdx.x; k < 272; k += blockDim.x)
+        if (src[k]) atomicAdd(&dst[k], src[k]);
 }
 
 // __ct_lookup hit part for CT_EGRESS (conntrack.h:75-135): tx accounting (the
@@ -3020,6 +3192,7 @@ template <int FAM>
 __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
                                                      uint32_t *ct_count, unsigned long long *stats) {
+    if (E.hz && *E.hz) return;                          // hazard: the batch reruns in ordered runs
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
@@ -3795,7 +3968,7 @@ using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t 
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
                        const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
-                       uint8_t *wsnap = nullptr) {
+                       uint8_t *wsnap = nullptr, bool lru = true) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -3884,7 +4057,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
-    if ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s))) return r;
+    if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
     return 0;
@@ -4364,28 +4537,83 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 
 // ---- endpoint egress (from-container) ----
 namespace {
-struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6; };
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6,
+             hzck, hzpk, hzdk, hzsk, hzfl, hztk, hztf, hzst, vip4, vip6;
+             std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
+             uint32_t vip4_mask = 0, vip6_mask = 0; bool vip4_any = false, vip6_any = false; };
 EgWs &eg_ws() { static EgWs w; return w; }
 }  // namespace
 
-extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t now_sec, gf_egress_out *out,
-                                      uint8_t *snap_out, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
-    auto o = get_obj(array);
-    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
-    auto a = std::static_pointer_cast<PolicyArray>(o);
-    if (!b) return -EFAULT;
+static int egress_ordered(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru);
+// The rev-NAT addresses of the programs' revNAT maps as device sets (the ordering
+// check's GF_HZ_VIP), rebuilt when a map changed through the API.
+static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew, hipStream_t s) {
+    std::vector<std::pair<const Map *, uint64_t>> stamp;
+    std::vector<Map *> m4, m6;
+    for (auto &p : progs) {
+        if (p->revnat4 && std::find(m4.begin(), m4.end(), p->revnat4.get()) == m4.end()) m4.push_back(p->revnat4.get());
+        if (p->revnat6 && std::find(m6.begin(), m6.end(), p->revnat6.get()) == m6.end()) m6.push_back(p->revnat6.get());
+    }
+    for (Map *m : m4) stamp.push_back({m, m->host_gen * 2});
+    for (Map *m : m6) stamp.push_back({m, m->host_gen * 2 + 1});
+    if (stamp == ew.vip_stamp) return 0;                // (no maps and nothing built compare equal too)
+    std::vector<uint32_t> a4;
+    std::vector<std::array<uint32_t, 4>> a6;
+    std::vector<uint8_t> v(32);
+    for (int fam = 4; fam <= 6; fam += 2) {
+        for (Map *m : fam == 4 ? m4 : m6) {
+            std::lock_guard<std::recursive_mutex> g(m->mu);
+            int r = m->pull();
+            if (r) return r;
+            for (uint64_t i = 0; i < m->ht.nslots; i++) {
+                if (m->ht.state(i) != GF_SLOT_FULL) continue;
+                m->ht.get_val(i, v.data());
+                if (fam == 4) { uint32_t x; memcpy(&x, v.data(), 4); if (x) a4.push_back(x); }
+                else { std::array<uint32_t, 4> x; memcpy(x.data(), v.data(), 16); if (x[0] | x[1] | x[2] | x[3]) a6.push_back(x); }
+            }
+        }
+    }
+    auto build = [&](size_t cnt, uint32_t &mask) { mask = 15; while ((uint64_t)mask + 1 < 4ull * cnt) mask = mask * 2 + 1; };
+    ew.vip4_any = !a4.empty(); ew.vip6_any = !a6.empty();
+    if (ew.vip4_any) {
+        build(a4.size(), ew.vip4_mask);
+        std::vector<uint32_t> t(ew.vip4_mask + 1, 0);
+        for (uint32_t x : a4) {
+            uint32_t slot = (x * 0x9E3779B1u) & ew.vip4_mask;
+            while (t[slot] && t[slot] != x) slot = (slot + 1u) & ew.vip4_mask;
+            t[slot] = x;
+        }
+        if (ew.vip4.ensure(t.size() * 4) ||
+            hip_ok(hipMemcpyAsync(ew.vip4.p, t.data(), t.size() * 4, hipMemcpyHostToDevice, s), "vip4") ||
+            hip_ok(hipStreamSynchronize(s), "vip4 sync"))
+            return -EIO;
+    }
+    if (ew.vip6_any) {
+        build(a6.size(), ew.vip6_mask);
+        std::vector<std::array<uint32_t, 4>> t(ew.vip6_mask + 1, std::array<uint32_t, 4>{0, 0, 0, 0});
+        for (auto &x : a6) {
+            uint32_t slot = ((x[0] ^ x[1] ^ x[2] ^ x[3]) * 0x9E3779B1u) & ew.vip6_mask;
+            while ((t[slot][0] | t[slot][1] | t[slot][2] | t[slot][3]) && t[slot] != x) slot = (slot + 1u) & ew.vip6_mask;
+            t[slot] = x;
+        }
+        if (ew.vip6.ensure(t.size() * 16) ||
+            hip_ok(hipMemcpyAsync(ew.vip6.p, t.data(), t.size() * 16, hipMemcpyHostToDevice, s), "vip6") ||
+            hip_ok(hipStreamSynchronize(s), "vip6 sync"))
+            return -EIO;
+    }
+    ew.vip_stamp = stamp;
+    return 0;
+}
+// One ordered run of an egress batch: check = run the ordering check first (a
+// flagged batch is split into runs, each through this function again); lru = the
+// LRU stand-in after it (once per classify call).
+static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool check, bool lru) {
     const gf_frames &fr = b->frames;
-    if (fr.n == 0) return 0;
-    if (!fr.snap || !fr.len || !out) return -EFAULT;
-    if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
-    if (fr.n > (1u << 30)) return -E2BIG;
-    hipStream_t s = (hipStream_t)stream;
-    MapLocks L;
-    lock_array_maps(L, a);
-    L.lock();
-    CallOrder co(s);
     const uint32_t n = fr.n, S = fr.snap_stride;
+    if (n == 0) return 0;
+    check = check && n > 1;
     int r;
     std::vector<std::shared_ptr<ProgLxc>> progs;
     if ((r = prog_table(a, s, progs))) return r;
@@ -4402,12 +4630,21 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     if ((r = push_map(lxc, s)) || (r = push_map(tun, s))) return r;
     EgWs &ew = eg_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    uint32_t hmask = 1023;                               // up to four keys per packet at <= 2/3 load
+    while (check && (uint64_t)hmask + 1 < 6ull * n) hmask = hmask * 2 + 1;
     if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
-        (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 4)) || (r = grow(ew.ctlog_n, 8)) ||
+        (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 16)) || (r = grow(ew.ctlog_n, 8)) ||
         (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 16)) ||
-        (r = grow(ew.d6, (size_t)n * 16)) || (r = ws_grow(n)))
+        (r = grow(ew.d6, (size_t)n * 16)) || (r = grow(ew.hzst, 272 * 8)) || (r = ws_grow(n)))
         return r;
-    uint8_t *wsnap = snap_out;
+    if (check && ((r = grow(ew.hzck, (size_t)n * 8)) || (r = grow(ew.hzpk, (size_t)n * 8)) || (r = grow(ew.hzfl, (size_t)n)) ||
+                  (r = grow(ew.hzdk, (size_t)n * 8)) || (r = grow(ew.hzsk, (size_t)n * 8)) ||
+                  (r = grow(ew.hztk, (size_t)(hmask + 1) * 8)) || (r = grow(ew.hztf, (size_t)(hmask + 1) * 8))))
+        return r;
+    // In place (snap_out == the frames) with the check: the flagged pass must leave
+    // the frames as they came, so the rewrites go to scratch and are copied at the end.
+    const bool inplace = check && snap_out == fr.snap;
+    uint8_t *wsnap = inplace ? nullptr : snap_out;
     if (!wsnap) {
         if ((r = grow(ew.snap, (size_t)n * S))) return r;
         wsnap = (uint8_t *)ew.snap.p;
@@ -4429,22 +4666,52 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     E.strict = strict;
     E.seq = (uint32_t *)ew.seq.p;
     E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
+    uint32_t *d_hz = (uint32_t *)ew.seq.p + 1;           // word 1 of the seq buffer: the hazard flag
+    if (check) {
+        E.hz_ck = (uint64_t *)ew.hzck.p; E.hz_pk = (uint64_t *)ew.hzpk.p; E.hz_fl = (uint8_t *)ew.hzfl.p; E.hz = d_hz;
+        E.hz_dk = (uint64_t *)ew.hzdk.p; E.hz_sk = (uint64_t *)ew.hzsk.p;
+        if ((r = vip_sets(progs, ew, s))) return r;
+        if (ew.vip4_any) { E.vip4 = (const uint32_t *)ew.vip4.p; E.vip4_mask = ew.vip4_mask; }
+        if (ew.vip6_any) { E.vip6 = (const uint4 *)ew.vip6.p; E.vip6_mask = ew.vip6_mask; }
+    }
     E.X.snap = nullptr; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;   // writes: k_eg_groups
     memcpy(E.X.host6, node.host_ip6, 16);
     if ((r = px_log_begin(n, s, E.X))) return r;
-    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 4, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
+    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 16, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
         return -EIO;
     unsigned long long *sink = (unsigned long long *)stats_sink();
+    // With the check, the front counts into a scratch block folded into the sink
+    // only when the batch runs as it is (a flagged batch's runs count themselves).
+    unsigned long long *fsink = sink;
+    if (check && sink) {
+        fsink = (unsigned long long *)ew.hzst.p;
+        if (hip_ok(hipMemsetAsync(fsink, 0, 272 * 8, s), "hz stats")) return -EIO;
+    }
     Workspace &w = ws();
     {
         ProfScope ps("k_eg_front", s);
         hipLaunchKernelGGL(k_eg_front<4>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
-                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
+                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
         hipLaunchKernelGGL(k_eg_front<6>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
-                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, sink);
+                           E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
         hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p, n,
                            (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_eg_front"))) return r;
+    }
+    if (check) {
+        ProfScope ps("k_hz_check", s);
+        if (hip_ok(hipMemsetAsync(ew.hztk.p, 0, (size_t)(hmask + 1) * 8, s), "hz keys") ||
+            hip_ok(hipMemsetAsync(ew.hztf.p, 0xff, (size_t)(hmask + 1) * 8, s), "hz first"))
+            return -EIO;
+        hipLaunchKernelGGL(k_hz_insert, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzck.p,
+                           (const uint64_t *)ew.hzpk.p, (const uint64_t *)ew.hzdk.p, (const uint64_t *)ew.hzsk.p,
+                           (const uint8_t *)ew.hzfl.p, n,
+                           (const uint32_t *)d_hz, (unsigned long long *)ew.hztk.p, (uint32_t *)ew.hztf.p, hmask);
+        hipLaunchKernelGGL(k_hz_probe, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzck.p,
+                           (const uint64_t *)ew.hzpk.p, (const uint64_t *)ew.hzsk.p, (const uint8_t *)ew.hzfl.p, n,
+                           (const unsigned long long *)ew.hztk.p,
+                           (const uint32_t *)ew.hztf.p, hmask, d_hz);
+        if ((r = hip_ok(hipGetLastError(), "k_hz_check"))) return r;
     }
     if ((r = schedule_groups(n, s))) return r;
     {
@@ -4462,10 +4729,16 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     // ct_create4's deferred service entries, in batch order
-    uint32_t cnts[2] = {0, 0};
+    uint32_t cnts[2] = {0, 0}, hz = 0;
     if (hip_ok(hipMemcpyAsync(cnts, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost, s), "ctlog count") ||
+        (check && hip_ok(hipMemcpyAsync(&hz, d_hz, 4, hipMemcpyDeviceToHost, s), "hz flag")) ||
         hip_ok(hipStreamSynchronize(s), "ctlog sync"))
         return -EIO;
+    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru);
+    if (check && sink) {
+        hipLaunchKernelGGL(k_stats_fold, dim3(1), dim3(256), 0, s, (const unsigned long long *)fsink, sink);
+        if ((r = hip_ok(hipGetLastError(), "k_stats_fold"))) return r;
+    }
     const uint32_t nlog = cnts[0];
     if (nlog && ct4m) {
         if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
@@ -4504,5 +4777,82 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
             return -EIO;
         return 0;
     };
-    return ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap);
+    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru))) return r;
+    if (inplace && hip_ok(hipMemcpyAsync(snap_out, wsnap, (size_t)n * S, hipMemcpyDeviceToDevice, s), "snap copy"))
+        return -EIO;
+    return 0;
+}
+
+// A flagged batch: the cut points (a new run starts at a packet whose reverse
+// direction is in the current run, and around every single-bucket tuple), then
+// every run through egress_call in order.  Nothing of the flagged pass changed
+// the maps: k_eg_groups idled, and the front only reads them.
+static int egress_ordered(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru) {
+    EgWs &ew = eg_ws();
+    const uint32_t n = b->frames.n, S = b->frames.snap_stride;
+    std::vector<uint64_t> ck(n), pk(n), dk(n), sk(n);
+    std::vector<uint8_t> fl(n);
+    if (hip_ok(hipMemcpyAsync(ck.data(), ew.hzck.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz ck") ||
+        hip_ok(hipMemcpyAsync(pk.data(), ew.hzpk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz pk") ||
+        hip_ok(hipMemcpyAsync(dk.data(), ew.hzdk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz dk") ||
+        hip_ok(hipMemcpyAsync(sk.data(), ew.hzsk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz sk") ||
+        hip_ok(hipMemcpyAsync(fl.data(), ew.hzfl.p, n, hipMemcpyDeviceToHost, s), "hz fl") ||
+        hip_ok(hipStreamSynchronize(s), "hz sync"))
+        return -EIO;
+    std::vector<uint32_t> cut{0};
+    std::unordered_set<uint64_t> seen;
+    const uint64_t DIRBIT = 1ull;                      // keys are odd: bit 0 carries the direction
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t f = fl[j];
+        if (!(f & GF_HZ_VALID)) continue;
+        if (f & GF_HZ_SPECIAL) {
+            if (j > cut.back()) cut.push_back(j);
+            cut.push_back(j + 1);
+            seen.clear();
+            continue;
+        }
+        const uint64_t me = (ck[j] & ~DIRBIT) | ((f & GF_HZ_DIR) ? DIRBIT : 0ull), pair = pk[j] & ~DIRBIT;
+        bool hit = (f & GF_HZ_ICMP) ? seen.count(pair) != 0 : seen.count(me ^ DIRBIT) != 0;
+        if (f & GF_HZ_VIP) hit = hit || seen.count(sk[j] & ~DIRBIT) != 0;
+        if (hit) { cut.push_back(j); seen.clear(); }
+        seen.insert(me);
+        seen.insert(pair);
+        seen.insert(dk[j] & ~DIRBIT);
+        seen.insert(sk[j] & ~DIRBIT);
+    }
+    if (cut.back() != n) cut.push_back(n);
+    for (size_t k = 0; k + 1 < cut.size(); k++) {
+        const uint32_t lo = cut[k], hi = cut[k + 1];
+        gf_lxc_batch sub = *b;
+        sub.frames.n = hi - lo;
+        sub.frames.snap = b->frames.snap + (size_t)lo * S;
+        sub.frames.len = b->frames.len + lo;
+        if (b->lxc_id) sub.lxc_id = b->lxc_id + lo;
+        if (b->flow_hash) sub.flow_hash = b->flow_hash + lo;
+        int r = egress_call(a, &sub, now_sec, out + lo, snap_out ? snap_out + (size_t)lo * S : nullptr, s, false,
+                            lru && k + 2 == cut.size());
+        if (r) return r;
+    }
+    return 0;
+}
+
+extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t now_sec, gf_egress_out *out,
+                                      uint8_t *snap_out, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    if (!b) return -EFAULT;
+    const gf_frames &fr = b->frames;
+    if (fr.n == 0) return 0;
+    if (!fr.snap || !fr.len || !out) return -EFAULT;
+    if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
+    if (fr.n > (1u << 30)) return -E2BIG;
+    hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    lock_array_maps(L, a);
+    L.lock();
+    CallOrder co(s);
+    return egress_call(a, b, now_sec, out, snap_out, s, true, true);
 }

@@ -474,6 +474,7 @@ static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t
 }
 
 int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
+    host_gen++;
     if (fl > GF_EXIST) return -EINVAL;
     if (is_lpm()) {
         uint32_t plen; memcpy(&plen, key, 4);
@@ -553,6 +554,7 @@ int Map::lookup(const uint8_t *key, uint8_t *value) {
 }
 
 int Map::erase(const uint8_t *key) {
+    host_gen++;
     if (is_lpm()) {
         uint32_t plen; memcpy(&plen, key, 4);
         if (plen > lpm_bits()) return -EINVAL;
@@ -795,6 +797,7 @@ int gf_map_update_batch(int h, const void *keys, const void *values, uint32_t n,
     if (!m) return -EBADF;
     std::lock_guard<std::recursive_mutex> g(m->mu);
     if (n && (!keys || !values)) return -EFAULT;
+    m->host_gen++;
     if (n >= 4096 && m->fixed_capacity && !m->is_lpm() && (flags == GF_ANY || flags == GF_NOEXIST) &&
         (m->dev_auth() || (m->ht.slots.empty() && m->ht.count == 0))) {
         // a table the datapath inserts into, filled in bulk (the agent restoring a CT,

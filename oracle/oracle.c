@@ -1111,22 +1111,23 @@ static void redirect_write(const skb_t *s, pol_ctx *x, int l4_off, const uint8_t
  * DROP_PROXYMAP_CREATE_FAILED) is the one sequential execution gives.  A failed
  * packet's verdict is patched; a successful one gets the MAC stores of
  * ipv{4,6}_policy that follow the redirect (bpf_lxc.c:840-846, 955-961). */
-static void proxy_apply(const o_batch *b, const uint8_t *plog, o_ingress_out *out, uint8_t *wsnap) {
-    for (uint32_t i = 0; i < b->n; i++) {
-        const uint8_t *e = plog + (size_t)i * O_PLOG;
-        if (!e[0]) continue;
-        om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
-        int r = m ? om_update(m, e + 4, e + 28, 0) : 0;
-        if (r < 0) {
-            out[i].action = TC_ACT_SHOT; out[i].reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
-            out[i].flags &= 2; out[i].proxy_port = 0; out[i].ifindex_lo = 0;
-        } else if (wsnap) {
-            skb_t s; skb_init(&s, b, i);
-            uint8_t *w = wsnap + (size_t)i * b->snap_stride;
-            wbytes(&s, w, 6, g_node.node_mac, 6);      /* eth_store_saddr(NODE_MAC) */
-            wbytes(&s, w, 0, g_node.host_mac, 6);      /* eth_store_daddr(HOST_IFINDEX_MAC) */
-        }
+static void proxy_apply_one(const o_batch *b, const uint8_t *plog, o_ingress_out *out, uint8_t *wsnap, uint32_t i) {
+    const uint8_t *e = plog + (size_t)i * O_PLOG;
+    if (!e[0]) return;
+    om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
+    int r = m ? om_update(m, e + 4, e + 28, 0) : 0;
+    if (r < 0) {
+        out[i].action = TC_ACT_SHOT; out[i].reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
+        out[i].flags &= 2; out[i].proxy_port = 0; out[i].ifindex_lo = 0;
+    } else if (wsnap) {
+        skb_t s; skb_init(&s, b, i);
+        uint8_t *w = wsnap + (size_t)i * b->snap_stride;
+        wbytes(&s, w, 6, g_node.node_mac, 6);      /* eth_store_saddr(NODE_MAC) */
+        wbytes(&s, w, 0, g_node.host_mac, 6);      /* eth_store_daddr(HOST_IFINDEX_MAC) */
     }
+}
+static void proxy_apply(const o_batch *b, const uint8_t *plog, o_ingress_out *out, uint8_t *wsnap) {
+    for (uint32_t i = 0; i < b->n; i++) proxy_apply_one(b, plog, out, wsnap, i);
 }
 
 /* ipv4_policy, bpf/bpf_lxc.c:865-970 */
@@ -2389,29 +2390,29 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
     uint32_t *secctx = (uint32_t *)malloc((size_t)n * 4 + 4), *ifx = (uint32_t *)malloc((size_t)n * 4 + 4);
     uint16_t *lxcid = (uint16_t *)malloc((size_t)n * 2 + 2);
     uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
-    for (uint32_t i = 0; i < n; i++)
-        from_container(a, b, i, now, &out[i], snap + (size_t)i * b->snap_stride, plog + (size_t)i * O_PLOG, &skip[i],
-                       &secctx[i], &ifx[i], &lxcid[i]);
-    /* the egress redirects' cilium_proxy4 updates, in batch order (lxc.h:137) */
-    for (uint32_t i = 0; i < n; i++) {
-        const uint8_t *e = plog + (size_t)i * O_PLOG;
-        if (!e[0]) continue;
-        om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
-        if (m && om_update(m, e + 4, e + 28, 0) < 0) {
-            o_egress_out *o = &out[i];
-            o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
-            o->flags &= (uint8_t)~1u; o->proxy_port = 0; o->ifindex_lo = 0;
-        }
-    }
-    /* handle_policy of the local deliveries, over the rewritten frames */
-    o_batch b2 = *b;
-    b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
     uint8_t *plog2 = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
     o_ingress_out *ing = (o_ingress_out *)calloc((size_t)n + 1, sizeof(o_ingress_out));
-    for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(a, &b2, i, now, &ing[i], plog2, snap);
-    proxy_apply(&b2, plog2, ing, snap);
+    o_batch b2 = *b;                                   /* the local deliveries, over the rewritten frames */
+    b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+    /* One packet at a time, as on one CPU: the from-container program, its
+     * cilium_proxy{4,6} update (lxc.h:137), then — for a local delivery — the
+     * destination's handle_policy (the tail call of ipv4_local_delivery) and its
+     * proxy update, before the next packet. */
     for (uint32_t i = 0; i < n; i++) {
+        from_container(a, b, i, now, &out[i], snap + (size_t)i * b->snap_stride, plog + (size_t)i * O_PLOG, &skip[i],
+                       &secctx[i], &ifx[i], &lxcid[i]);
+        const uint8_t *e = plog + (size_t)i * O_PLOG;
+        if (e[0]) {
+            om_map *m = e[0] == 4 ? g_node.proxy4_map : g_node.proxy6_map;
+            if (m && om_update(m, e + 4, e + 28, 0) < 0) {
+                o_egress_out *o = &out[i];
+                o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_PROXYMAP_CREATE_FAILED_);
+                o->flags &= (uint8_t)~1u; o->proxy_port = 0; o->ifindex_lo = 0;
+            }
+        }
         if (skip[i]) continue;
+        handle_policy(a, &b2, i, now, &ing[i], plog2, snap);
+        proxy_apply_one(&b2, plog2, ing, snap, i);
         o_egress_out *o = &out[i];
         o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
         o->flags = ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;

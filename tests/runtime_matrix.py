@@ -266,6 +266,31 @@ def run_case(case, topo, backend):
     return res, log
 
 
+def run_case_one_batch(case, topo, backend):
+    """Every packet of every request in ONE from-container batch, in wave order
+    (all first packets, then all replies, then the ACKs): a reply shares the batch
+    with its request, so its CT lookup must see the entry the request's
+    handle_policy created — the per-packet order of the reference.  Only for
+    cases whose servers are endpoints.  Returns (outcomes, records)."""
+    flows = [Flow(j, c, s, r) for j, (c, s, r, _) in enumerate(expand(case))]
+    assert not any(f.server.startswith("host") for f in flows)
+    rows = []
+    for step in range(3):
+        for f in flows:
+            if step < len(f.steps):
+                fr, ln, src, _ = _frame(topo, f, step)
+                rows.append((f, fr, ln, src))
+    pk = S.Packets(np.concatenate([x[1] for x in rows]), np.concatenate([x[2] for x in rows]),
+                   lxc_id=np.array([topo.lxc_id[x[3]] for x in rows], np.uint16))
+    r = backend.egress(pk, case.get("now", 5000))
+    for (f, *_), rec in zip(rows, r):
+        f.delivered += rec["stage"] in (4, 5) and rec["action"] != 2
+    res = {}
+    for f in flows:
+        res.setdefault((f.client, f.server, f.req), []).append(f.delivered == len(f.steps))
+    return res, r
+
+
 def expected(case):
     return {(c, s, r): ok for c, s, r, ok in expand(case)}
 
@@ -312,6 +337,12 @@ class GpuBackend:
         out = self.dp.ingress(DeviceBatch(pk), now)
         torch.cuda.synchronize()
         return out.cpu().numpy().view(ING_OUT).ravel()
+
+    def dump(self, name, ksz):
+        from cilium_amd import bpf
+        m = bpf.Map(name, 9, ksz, 48, 1 << 16)
+        m.fd = self.dp.fd[name]
+        return m.DumpArrays()
 
     def close(self):
         self.dp.close()

@@ -52,6 +52,47 @@ def test_oracle_matches_reference_matrix(case):
     assert not bad, bad
 
 
+ONE_BATCH = [c for c in CASES if not any(s.startswith("host") for _, s, *_ in c["checks"])]
+
+
+@pytest.mark.parametrize("case", ONE_BATCH, ids=[c["name"] for c in ONE_BATCH])
+def test_oracle_one_batch_request_and_reply(case):
+    """Requests, replies and ACKs in one batch: the per-packet order of the
+    reference gives the reference's outcomes."""
+    topo = RM.Topology(DOC["endpoints"])
+    res, _ = RM.run_case_one_batch(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
+    bad = RM.outcome_mismatches(case, res)
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_gpu_one_batch_request_and_reply_ordered():
+    """The same batches on the HIP path: the ordering check must split them so
+    that every record and every CT entry equals the per-packet oracle's."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    from oracle import parity as PY
+    topo = RM.Topology(DOC["endpoints"])
+    for case in ONE_BATCH:
+        gpu = RM.GpuBackend(RM.compile_case(case, topo))
+        ref = RM.OracleBackend(RM.compile_case(case, topo))
+        try:
+            gres, g = RM.run_case_one_batch(case, topo, gpu)
+            ores, o = RM.run_case_one_batch(case, topo, ref)
+            bad, first = PY.compare_records(g, o)
+            assert bad == 0, (case["name"], first, g[first], o[first])
+            assert not RM.outcome_mismatches(case, gres), case["name"]
+            for name, ksz in (("ct4", 14), ("ct6", 40)):
+                gk, gv = gpu.dump(name, ksz)
+                ok, ov = ref.dp.m[name].dump_arrays()
+                n, badc = PY.compare_tables(gk, gv, ok, ov)
+                assert badc == 0 and n == len(ok), (case["name"], name, n, badc)
+        finally:
+            gpu.close()
+
+
 @pytest.mark.gpu
 def test_gpu_matches_reference_matrix_and_oracle():
     torch = pytest.importorskip("torch")
