@@ -619,7 +619,7 @@ def _evictions(dp, name):
 # ----------------------------------------------------------------------------- endpoint egress
 def bench_egress(args, dev):
     """The from-container program (handle_ipv4_from_lxc) over frames sent by 256
-    local endpoints in 16 tenants, local deliveries continuing into handle_policy:
+    local endpoints (synth.TENANT per tenant), local deliveries continuing into handle_policy:
     4M flows, one 64-B frame each per step; each step a quarter of the flows
     starts anew (new source port), the rest are established."""
     import torch
@@ -637,8 +637,10 @@ def bench_egress(args, dev):
     frames = []
     for s in range(W + K):
         fs = base.clone()
-        a, port = (s % 4) * q, 20000 + 7 * s
-        fs[a:a + q, 34], fs[a:a + q, 35] = port >> 8, port & 0xff
+        a = (s % 4) * q                    # a new source port for each flow of this quarter
+        sp = base[a:a + q, 34].to(torch.int64) * 256 + base[a:a + q, 35].to(torch.int64)
+        sp = 1024 + (sp - 1024 + 7919 * (s + 1)) % 60000
+        fs[a:a + q, 34], fs[a:a + q, 35] = (sp >> 8).to(torch.uint8), (sp & 0xff).to(torch.uint8)
         frames.append(fs)
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
     len_t, lid_t, fh_t = t(lens, np.int32), t(lid, np.int16), t(fh, np.int32)
@@ -650,7 +652,7 @@ def bench_egress(args, dev):
     if not args.no_cpu:
         cpu, par = oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K)
     return {"workload": "egress: bpf_lxc from-container handle_ipv4_from_lxc (+ handle_policy of local deliveries), "
-                        f"256 endpoints in 4 tenants, {n} flows/step (35% world, 20% tunnel, 25% local, 20% service "
+                        f"256 endpoints, {n} flows/step (35% world, 20% tunnel, 25% local, 20% service "
                         "VIPs), 1/4 new per step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
@@ -671,7 +673,9 @@ def oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
     ep_idx = lid.astype(np.int64) - int(meta["lxc_id"][0])
     ten = ep_idx // TENANT
     T = cpu_threads()
-    par = Parity("tenant 0 of 4 (its 64 endpoints' flows: a closed set of flow groups), every step")
+    nten = len(meta["ep4"]) // TENANT
+    par = Parity(f"tenant 0 of {nten} (its {TENANT} endpoints' flows: a closed set of flow groups), every step"
+                 if nten > 1 else "every packet of every step (one tenant)")
     ref = OracleDP(sc)
     lru_replay(dp, ref)
     m0 = np.nonzero(ten == 0)[0]

@@ -19,8 +19,10 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <errno.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <functional>
 #include <unordered_set>
+#include <chrono>
 #include <algorithm>
 #include <array>
 #include <string.h>
@@ -2254,9 +2256,7 @@ struct EgDev {
     uint32_t *seq;                      // device word: 1 = single-bucket batch (written by k_eg_front)
     uint32_t *ctlog, *ctlog_n;          // deferred service entries {i, key[4], value[12], pad[3]}; [n, v6 deliveries]
     IngCtx X;                           // redirect writes + cilium_proxy4 log (pol_redirect)
-    uint64_t *hz_ck;                    // per packet: connection key of the frame tuple after the front (0: none)
-    uint64_t *hz_pk;                    // per packet: key of its unordered address pair
-    uint64_t *hz_dk, *hz_sk;            // per packet: keys of its destination / source address
+    uint64_t *hz_k;                     // per packet, GF_HZ_NK keys (hz_key order below), n apart
     const uint32_t *vip4;               // the rev-NAT addresses of the programs' revNAT maps (open addressing,
     const uint4 *vip6;                  //   0 = empty), vip*_mask + 1 slots; null: none
     uint32_t vip4_mask, vip6_mask;
@@ -2265,26 +2265,42 @@ struct EgDev {
 };
 // The ordering check.  The reference runs a local delivery's
 // handle_policy right after its from-container program, before the next packet;
-// the batch runs every from-container part first.  The two orders differ only
-// when a packet's from-container CT lookup reads an entry an earlier delivery's
-// handle_policy writes: a packet whose tuple is the reverse of an earlier
-// packet's (a reply in the same batch), or the tuples of the single-bucket class
-// (saddr == daddr, IPV4_LOOPBACK, lb4_local back to the sender).  The front keys
-// each packet by its unordered 5-tuple (ICMP: ports 0) and direction; such a
-// batch is cut into contiguous runs without a hazard, run one after the other.
-// ICMP packets also read the related entry every new flow of their address pair
-// creates (ct_create4/6): an ICMP packet conflicts with any earlier packet of its pair.
+// the batch runs every from-container part first, then every handle_policy.  The
+// two orders differ only when a packet's from-container part touches a CT entry an
+// earlier packet's handle_policy touches.  The CT keys a packet can touch follow
+// from its tuples (conntrack.h:170-289 lookups, :446-580 creates):
+//  * handle_policy: its tuple (the frame after the from-container rewrites) and
+//    the reverse, for ICMP the related entry of the address pair;
+//  * from-container: its CT tuple (after lb4_local) and the reverse, the related
+//    entry of the pair for ICMP, and lb4_local's loopback service entry (the frame
+//    pair after the SNAT).
+// A handle_policy tuple and a later from-container tuple share an entry only in
+// opposite directions (the lookups differ in TUPLE_F_IN); so the front keys each
+// packet by the connection of its frame tuple and of its CT tuple (unordered 5-tuple,
+// ICMP ports 0, + direction), their address pairs, and its two addresses:
+//   a later packet whose CT connection equals an earlier frame connection in the
+//     other direction (a reply in the same batch);
+//   an ICMP packet after any packet of its CT pair, any packet after an ICMP packet
+//     of its pair (the related entries);
+//   a loopback packet whose frame connection appeared earlier (its service entry);
+//   a packet to a rev-NAT address without translation after any packet with its
+//     source address (a reply rev-NATed by lb4/6_rev_nat reaches handle_policy as
+//     {service address, one of its own addresses});
+// flags the batch, which then runs in contiguous runs free of these, in order.
+#define GF_HZ_NK      6u                // keys per packet: conn(frame), conn(CT), pair(frame), pair(CT), src, dst
 #define GF_HZ_VALID   1u                // continues past the front
-#define GF_HZ_DIR     2u                // the tuple's direction within its connection key
-#define GF_HZ_SPECIAL 4u                // single-bucket tuple: runs alone
-#define GF_HZ_ICMP    8u                // ICMP / ICMPv6: probes the pair key
-// A reply a service backend sends is rev-NATed (lb4_rev_nat / lb6_rev_nat) before
-// its delivery: handle_policy's tuple is {service address, one of the packet's own
-// addresses} (the loopback branch moves the source into daddr).  It meets a later
-// packet only if that one goes to the service address without translation.  Such
-// a packet (GF_HZ_VIP) conflicts with any earlier packet that has its source
-// address as source or destination.
-#define GF_HZ_VIP    16u
+#define GF_HZ_DIRI    2u                // direction of the frame tuple within its connection
+#define GF_HZ_DIRE    4u                // direction of the CT tuple within its connection
+#define GF_HZ_ICMP    8u                // ICMP / ICMPv6
+#define GF_HZ_VIP    16u                // to a rev-NAT address without lb4/6_local translation
+#define GF_HZ_LOOP   32u                // lb4_local back to the sender (loopback SNAT)
+#define GF_HZ_V6     64u                // the IPv6 path
+#define GF_HZ_DLV   128u                // may reach ipv4/6_local_delivery (daddr an endpoint, or IPV4_LOOPBACK
+                                        // whose rev-NAT restores the sender): only these enter handle_policy
+// A CT map that could fill during the batch (strict accounting) makes every
+// insert order-dependent (E2BIG for whichever comes last): a batch with a
+// continuing packet of that family is flagged 2 and runs one packet at a time.
+#define GF_HZ_ICMPSALT 0x6a09e667f3bcc908ull   // the related-entry space of ICMP packets' pairs
 #define GF_CTLOG_WORDS 20u
 
 // The header bytes the IPv4 egress programs touch (< l4_off + 18 <= 92) are staged
@@ -2414,9 +2430,14 @@ __device__ __forceinline__ int eg_front6(const EgDev &E, const gf_lxc_dev *c, Ro
 // handle_ingress + the stateless head of handle_ipv4_from_lxc, one packet per lane
 // FAM 6 takes the IPv6 frames, FAM 4 every other frame (two launches: the IPv6
 // path's registers and stack stay out of the IPv4 kernel).
+// the slot of a rev-NAT address (fmix32: raw be32 addresses share their low bytes)
+GF_HD uint32_t vip_slot(uint32_t x) {
+    x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+    return x;
+}
 __device__ __forceinline__ bool vip4_has(const EgDev &E, uint32_t a) {
     if (!E.vip4 || !a) return false;
-    uint32_t slot = (a * 0x9E3779B1u) & E.vip4_mask;
+    uint32_t slot = vip_slot(a) & E.vip4_mask;
     for (uint32_t k = 0; k <= E.vip4_mask; k++) {
         const uint32_t v = E.vip4[slot];
         if (v == a) return true;
@@ -2427,7 +2448,7 @@ __device__ __forceinline__ bool vip4_has(const EgDev &E, uint32_t a) {
 }
 __device__ __forceinline__ bool vip6_has(const EgDev &E, const uint32_t *a) {
     if (!E.vip6 || !(a[0] | a[1] | a[2] | a[3])) return false;
-    uint32_t slot = ((a[0] ^ a[1] ^ a[2] ^ a[3]) * 0x9E3779B1u) & E.vip6_mask;
+    uint32_t slot = vip_slot(a[0] ^ vip_slot(a[1] ^ vip_slot(a[2] ^ vip_slot(a[3])))) & E.vip6_mask;
     for (uint32_t k = 0; k <= E.vip6_mask; k++) {
         const uint4 v = E.vip6[slot];
         if (v.x == a[0] && v.y == a[1] && v.z == a[2] && v.w == a[3]) return true;
@@ -2595,42 +2616,43 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             r.st = 0;                                       // continue in k_eg_groups
         } while (0);
         uint32_t key;
-        uint64_t hck = 0, hpk = 0, hdk = 0, hsk = 0;
-        uint32_t hfl = 0;
-        if (r.st == 0) {
-            const int lo4 = r.l4_off;
-            const bool tu = (r.nh == 6 || r.nh == 17) && skb_ok(lo4 + 0, 4, len);
-            bool dir = false;
-            if (FAM == 6) {
-                const uint32_t sp = tu ? wg.r16((uint32_t)lo4) : 0u, dp = tu ? wg.r16((uint32_t)lo4 + 2u) : 0u;
-                uint32_t s6[4], d6[4];
-                for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
-                hck = hz_key(s6, d6, 4, sp, dp, r.nh, dir);
-                bool pd, same = true;
-                hpk = hz_key(s6, d6, 4, 0u, 0u, 0x1ffu, pd);
-                hdk = hz_key(d6, d6, 4, 0u, 0u, 0x2ffu, pd);
-                hsk = hz_key(s6, s6, 4, 0u, 0u, 0x2ffu, pd);
-                for (int k = 0; k < 4; k++) same &= s6[k] == d6[k];
-                const bool vip = !(r.eflags & GF_EG_F_LB) && vip6_has(E, d6);
-                hfl = GF_HZ_VALID | (dir ? GF_HZ_DIR : 0u) | (same ? GF_HZ_SPECIAL : 0u) | (r.nh == 58 ? GF_HZ_ICMP : 0u) |
-                      (vip ? GF_HZ_VIP : 0u);
-            } else {
-                const uint32_t sp = tu ? w.r16((uint32_t)lo4) : 0u, dp = tu ? w.r16((uint32_t)lo4 + 2u) : 0u;
-                const uint32_t fs = w.r32(26), fd = w.r32(30), lo = E.loopback;
-                hck = hz_key(&fs, &fd, 1, sp, dp, r.nh, dir);
-                bool pd;
-                hpk = hz_key(&fs, &fd, 1, 0u, 0u, 0x1ffu, pd);
-                hdk = hz_key(&fd, &fd, 1, 0u, 0u, 0x2ffu, pd);
-                hsk = hz_key(&fs, &fs, 1, 0u, 0u, 0x2ffu, pd);
-                const bool vip = !(r.eflags & GF_EG_F_LB) && vip4_has(E, fd);
-                const bool sp_ = (r.eflags & GF_EG_F_LOOPBACK) || r.t_saddr == r.t_daddr || fs == fd ||
-                                 (lo && (r.t_saddr == lo || r.t_daddr == lo || fs == lo || fd == lo));
-                hfl = GF_HZ_VALID | (dir ? GF_HZ_DIR : 0u) | (sp_ ? GF_HZ_SPECIAL : 0u) | (r.nh == 1 ? GF_HZ_ICMP : 0u) |
-                      (vip ? GF_HZ_VIP : 0u);
-            }
-        }
         if (E.hz_fl) {
-            E.hz_ck[i] = hck; E.hz_pk[i] = hpk; E.hz_dk[i] = hdk; E.hz_sk[i] = hsk; E.hz_fl[i] = (uint8_t)hfl;
+            uint64_t K[GF_HZ_NK] = {0, 0, 0, 0, 0, 0};
+            uint32_t hfl = 0;
+            if (r.st == 0) {
+                const int lo4 = r.l4_off;
+                const bool tu = (r.nh == 6 || r.nh == 17) && skb_ok(lo4 + 0, 4, len);
+                bool di = false, de = false, pd;
+                if (FAM == 6) {
+                    const uint32_t sp = tu ? wg.r16((uint32_t)lo4) : 0u, dp = tu ? wg.r16((uint32_t)lo4 + 2u) : 0u;
+                    uint32_t s6[4], d6[4];
+                    for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
+                    K[0] = K[1] = hz_key(s6, d6, 4, sp, dp, r.nh, di);           // the IPv6 path keeps its addresses
+                    de = di;
+                    K[2] = K[3] = hz_key(s6, d6, 4, 0u, 0u, 0x1ffu, pd);
+                    K[4] = hz_key(s6, s6, 4, 0u, 0u, 0x2ffu, pd);
+                    K[5] = hz_key(d6, d6, 4, 0u, 0u, 0x2ffu, pd);
+                    const bool vip = !(r.eflags & GF_EG_F_LB) && vip6_has(E, d6);
+                    const bool dlv = E.lxc.slots && lxc_has6(E.lxc, d6);
+                    hfl = (r.nh == 58 ? GF_HZ_ICMP : 0u) | (vip ? GF_HZ_VIP : 0u) | GF_HZ_V6 | (dlv ? GF_HZ_DLV : 0u);
+                } else {
+                    const uint32_t sp = tu ? w.r16((uint32_t)lo4) : 0u, dp = tu ? w.r16((uint32_t)lo4 + 2u) : 0u;
+                    const uint32_t fs = w.r32(26), fd = w.r32(30), ts = r.t_saddr, td = r.t_daddr;
+                    K[0] = hz_key(&fs, &fd, 1, sp, dp, r.nh, di);
+                    K[1] = hz_key(&ts, &td, 1, sp, dp, r.nh, de);
+                    K[2] = hz_key(&fs, &fd, 1, 0u, 0u, 0x1ffu, pd);
+                    K[3] = hz_key(&ts, &td, 1, 0u, 0u, 0x1ffu, pd);
+                    K[4] = hz_key(&fs, &fs, 1, 0u, 0u, 0x2ffu, pd);
+                    K[5] = hz_key(&fd, &fd, 1, 0u, 0u, 0x2ffu, pd);
+                    const bool vip = !(r.eflags & GF_EG_F_LB) && vip4_has(E, fd);
+                    const bool dlv = (E.lxc.slots && lxc_has4(E.lxc, fd)) || (E.loopback && fd == E.loopback);
+                    hfl = (r.nh == 1 ? GF_HZ_ICMP : 0u) | (vip ? GF_HZ_VIP : 0u) |
+                          ((r.eflags & GF_EG_F_LOOPBACK) ? GF_HZ_LOOP : 0u) | (dlv ? GF_HZ_DLV : 0u);
+                }
+                hfl |= GF_HZ_VALID | (di ? GF_HZ_DIRI : 0u) | (de ? GF_HZ_DIRE : 0u);
+            }
+            for (uint32_t k = 0; k < GF_HZ_NK; k++) E.hz_k[(size_t)k * fr.n + i] = K[k];
+            E.hz_fl[i] = (uint8_t)hfl;
             if (hfl & (GF_HZ_ICMP | GF_HZ_VIP)) atomicOr(E.hz + 1, hfl);   // the batch's kinds
         }
         if (r.st == 0 && FAM == 6) {
@@ -2689,33 +2711,97 @@ __device__ __forceinline__ uint32_t hz_get(unsigned long long k, uint32_t half, 
     }
     return 0xffffffffu;
 }
-__global__ __launch_bounds__(BLOCK) void k_hz_insert(const uint64_t *ck, const uint64_t *pk, const uint64_t *dk,
-                                                     const uint64_t *sk, const uint8_t *fl, uint32_t n, const uint32_t *hz,
-                                                     unsigned long long *tkey, uint32_t *tfirst, uint32_t mask) {
-    const uint32_t kinds = hz[1];                       // pair / destination keys only when a packet probes them
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint32_t f = fl[i];
-        if ((f & (GF_HZ_VALID | GF_HZ_SPECIAL)) != GF_HZ_VALID) continue;
-        hz_put(ck[i], (f & GF_HZ_DIR) ? 1u : 0u, i, tkey, tfirst, mask);
-        if (kinds & GF_HZ_ICMP) hz_put(pk[i], 0u, i, tkey, tfirst, mask);
-        if (kinds & GF_HZ_VIP) { hz_put(dk[i], 0u, i, tkey, tfirst, mask); hz_put(sk[i], 0u, i, tkey, tfirst, mask); }
+struct HzTab { unsigned long long *key; uint32_t *first; uint32_t mask; };
+// The connection table is never cleared: a slot belongs to the current call when
+// its key word carries the call's 16-bit generation (key = gen << 48 | 48 hash
+// bits), and a first-index word is (gen << 32 | ~index), kept by atomicMax.  The
+// host clears it when the generation wraps or the table is reallocated.
+struct HzGen { unsigned long long *key; unsigned long long *first; uint32_t mask; uint32_t gen; };
+__device__ __forceinline__ void hzg_put(const HzGen &T, unsigned long long k, uint32_t half, uint32_t i) {
+    const unsigned long long want = ((unsigned long long)T.gen << 48) | (k & 0xffffffffffffull);
+    uint32_t slot = (uint32_t)(k >> 32) & T.mask;
+    for (uint32_t probe = 0; probe <= T.mask;) {
+        unsigned long long cur = T.key[slot];
+        if ((uint32_t)(cur >> 48) != T.gen) {          // a stale slot: claim it
+            const unsigned long long old = atomicCAS(&T.key[slot], cur, want);
+            if (old != cur) continue;                   // changed under us: look again
+            cur = want;
+        }
+        if (cur == want) {
+            atomicMax(&T.first[2 * slot + half], ((unsigned long long)T.gen << 32) | (0xffffffffull - i));
+            return;
+        }
+        slot = (slot + 1u) & T.mask;
+        probe++;
     }
 }
-// ... then a packet whose reverse direction appeared earlier in the batch, or a
-// single-bucket tuple in a batch of two or more, flags the batch.
-__global__ __launch_bounds__(BLOCK) void k_hz_probe(const uint64_t *ck, const uint64_t *pk, const uint64_t *sk,
-                                                    const uint8_t *fl, uint32_t n, const unsigned long long *tkey,
-                                                    const uint32_t *tfirst, uint32_t mask, uint32_t *hz) {
-    bool hit = false;
+__device__ __forceinline__ uint32_t hzg_get(const HzGen &T, unsigned long long k, uint32_t half) {
+    const unsigned long long want = ((unsigned long long)T.gen << 48) | (k & 0xffffffffffffull);
+    uint32_t slot = (uint32_t)(k >> 32) & T.mask;
+    for (uint32_t probe = 0; probe <= T.mask; probe++) {
+        const unsigned long long cur = T.key[slot];
+        if ((uint32_t)(cur >> 48) != T.gen) break;
+        if (cur == want) {
+            const unsigned long long w = T.first[2 * slot + half];
+            return (uint32_t)(w >> 32) == T.gen ? 0xffffffffu - (uint32_t)w : 0xffffffffu;
+        }
+        slot = (slot + 1u) & T.mask;
+    }
+    return 0xffffffffu;
+}
+// The pair / address keys live in a second table, cleared (here, on the device)
+// only for a batch with ICMP or GF_HZ_VIP packets.
+__global__ __launch_bounds__(BLOCK) void k_hz_clear(HzTab A, const uint32_t *hz) {
+    if (!(hz[1] & (GF_HZ_ICMP | GF_HZ_VIP))) return;
+    for (uint64_t k = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; k <= A.mask; k += (uint64_t)gridDim.x * BLOCK) {
+        A.key[k] = 0ull;
+        A.first[2 * k] = A.first[2 * k + 1] = 0xffffffffu;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_hz_insert(const uint64_t *K, const uint8_t *fl, uint32_t n,
+                                                     const uint32_t *hz, HzGen C, HzTab A) {
+    const uint32_t kinds = hz[1];                       // pair / address keys only when a packet probes them
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         const uint32_t f = fl[i];
         if (!(f & GF_HZ_VALID)) continue;
-        if (f & GF_HZ_SPECIAL) { hit = true; continue; }
-        if (f & GF_HZ_ICMP) hit |= hz_get(pk[i], 0u, tkey, tfirst, mask) < i;
-        else hit |= hz_get(ck[i], (f & GF_HZ_DIR) ? 0u : 1u, tkey, tfirst, mask) < i;
-        if (f & GF_HZ_VIP) hit |= hz_get(sk[i], 0u, tkey, tfirst, mask) < i;
+        if (f & GF_HZ_DLV) hzg_put(C, K[i], (f & GF_HZ_DIRI) ? 1u : 0u, i);
+        if (kinds & GF_HZ_ICMP) {
+            hz_put(K[2ull * n + i], 0u, i, A.key, A.first, A.mask);
+            if (f & GF_HZ_ICMP) hz_put(K[2ull * n + i] ^ GF_HZ_ICMPSALT, 0u, i, A.key, A.first, A.mask);
+        }
+        if (kinds & GF_HZ_VIP) {
+            hz_put(K[4ull * n + i], 0u, i, A.key, A.first, A.mask);
+            hz_put(K[5ull * n + i], 0u, i, A.key, A.first, A.mask);
+        }
     }
-    if (__any(hit) && (threadIdx.x & 63u) == 0) atomicOr(hz, 1u);
+}
+// ... then each packet probes what its from-container part touches; a hit on an
+// earlier index flags the batch.
+__global__ __launch_bounds__(BLOCK) void k_hz_probe(const uint64_t *K, const uint8_t *fl, uint32_t n, HzGen C,
+                                                    HzTab A, uint32_t strict, uint32_t *hz) {
+    const uint32_t kinds = hz[1];
+    bool hit = false, each = false;
+    uint32_t first = 0xffffffffu;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t f = fl[i];
+        if (!(f & GF_HZ_VALID)) continue;
+        each |= (strict & ((f & GF_HZ_V6) ? 2u : 1u)) != 0;
+        hit |= hzg_get(C, K[1ull * n + i], (f & GF_HZ_DIRE) ? 0u : 1u) < i;
+        if (kinds & GF_HZ_ICMP) {
+            if (f & GF_HZ_ICMP) hit |= hz_get(K[3ull * n + i], 0u, A.key, A.first, A.mask) < i;
+            hit |= hz_get(K[3ull * n + i] ^ GF_HZ_ICMPSALT, 0u, A.key, A.first, A.mask) < i;
+        }
+        if (f & GF_HZ_LOOP)
+            hit |= hzg_get(C, K[i], 0u) < i || hzg_get(C, K[i], 1u) < i;
+        if (f & GF_HZ_VIP) hit |= hz_get(K[4ull * n + i], 0u, A.key, A.first, A.mask) < i;
+        if (hit && first == 0xffffffffu) first = i;
+    }
+    // the earliest flagged packet: everything before it is a run without a hazard
+    uint32_t m = first;
+    for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor(m, o));
+    if ((threadIdx.x & 63u) == 0 && m != 0xffffffffu) atomicMin(hz + 2, m);
+    if (__any(each) && (threadIdx.x & 63u) == 0) atomicOr(hz, 2u);
+    else if (__any(hit) && (threadIdx.x & 63u) == 0) atomicOr(hz, 1u);
 }
 
 // Adds a call's counter block to the registered sink.
@@ -3746,7 +3832,9 @@ static int schedule_groups(uint32_t n, hipStream_t s) {
 // apply after the launch (see k_px_apply).
 struct PxWs { DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp; };
 static PxWs &px_ws() { static PxWs w; return w; }
-static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X) {
+// keep: continue the log the from-container pass of the same egress call wrote
+// (each packet logs at most one update: an egress redirect is never delivered).
+static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X, bool keep = false) {
     auto px4 = proxy_map(4), px6 = proxy_map(6);
     X.plog = nullptr; X.plog_n = nullptr;
     if (!px4 && !px6) return 0;
@@ -3754,7 +3842,7 @@ static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X) {
     int r;
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     if ((r = grow(w.plog, (size_t)n * 64)) || (r = grow(w.plog_n, 4))) return r;
-    if (hip_ok(hipMemsetAsync(w.plog_n.p, 0, 4, s), "plog_n")) return -EIO;
+    if (!keep && hip_ok(hipMemsetAsync(w.plog_n.p, 0, 4, s), "plog_n")) return -EIO;
     for (auto &m : {px4, px6})
         if (m && (r = push_map(m, s))) return r;
     X.plog = (uint32_t *)w.plog.p; X.plog_n = (uint32_t *)w.plog_n.p;
@@ -3968,7 +4056,7 @@ using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t 
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
                        const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
-                       uint8_t *wsnap = nullptr, bool lru = true) {
+                       uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -4019,7 +4107,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     const gf_node_cfg &node = node_cfg();
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
-    if ((r = px_log_begin(n, s, X))) return r;
+    if ((r = px_log_begin(n, s, X, px_keep))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
@@ -4538,14 +4626,23 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 // ---- endpoint egress (from-container) ----
 namespace {
 struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6,
-             hzck, hzpk, hzdk, hzsk, hzfl, hztk, hztf, hzst, vip4, vip6;
+             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6;
+             uint32_t hz_gen = 0, hz_cap = 0;
              std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
              uint32_t vip4_mask = 0, vip6_mask = 0; bool vip4_any = false, vip6_any = false; };
 EgWs &eg_ws() { static EgWs w; return w; }
 }  // namespace
 
 static int egress_ordered(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
-                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru);
+                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru, uint32_t first, uint32_t depth);
+static int egress_runs(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru, const std::vector<uint32_t> &cut);
+static int egress_each(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru) {
+    std::vector<uint32_t> cut(b->frames.n + 1);
+    for (uint32_t j = 0; j <= b->frames.n; j++) cut[j] = j;
+    return egress_runs(a, b, now_sec, out, snap_out, s, lru, cut);
+}
 // The rev-NAT addresses of the programs' revNAT maps as device sets (the ordering
 // check's GF_HZ_VIP), rebuilt when a map changed through the API.
 static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew, hipStream_t s) {
@@ -4580,7 +4677,7 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
         build(a4.size(), ew.vip4_mask);
         std::vector<uint32_t> t(ew.vip4_mask + 1, 0);
         for (uint32_t x : a4) {
-            uint32_t slot = (x * 0x9E3779B1u) & ew.vip4_mask;
+            uint32_t slot = vip_slot(x) & ew.vip4_mask;
             while (t[slot] && t[slot] != x) slot = (slot + 1u) & ew.vip4_mask;
             t[slot] = x;
         }
@@ -4593,7 +4690,7 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
         build(a6.size(), ew.vip6_mask);
         std::vector<std::array<uint32_t, 4>> t(ew.vip6_mask + 1, std::array<uint32_t, 4>{0, 0, 0, 0});
         for (auto &x : a6) {
-            uint32_t slot = ((x[0] ^ x[1] ^ x[2] ^ x[3]) * 0x9E3779B1u) & ew.vip6_mask;
+            uint32_t slot = vip_slot(x[0] ^ vip_slot(x[1] ^ vip_slot(x[2] ^ vip_slot(x[3])))) & ew.vip6_mask;
             while ((t[slot][0] | t[slot][1] | t[slot][2] | t[slot][3]) && t[slot] != x) slot = (slot + 1u) & ew.vip6_mask;
             t[slot] = x;
         }
@@ -4609,7 +4706,7 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
 // flagged batch is split into runs, each through this function again); lru = the
 // LRU stand-in after it (once per classify call).
 static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
-                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool check, bool lru) {
+                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool check, bool lru, uint32_t depth = 0) {
     const gf_frames &fr = b->frames;
     const uint32_t n = fr.n, S = fr.snap_stride;
     if (n == 0) return 0;
@@ -4630,16 +4727,17 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     if ((r = push_map(lxc, s)) || (r = push_map(tun, s))) return r;
     EgWs &ew = eg_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
-    uint32_t hmask = 1023;                               // up to four keys per packet at <= 2/3 load
-    while (check && (uint64_t)hmask + 1 < 6ull * n) hmask = hmask * 2 + 1;
+    uint32_t hmask = 1023, amask = 1023;                 // conn keys at <= 1/2 load, up to 4 aux keys at <= 1/2
+    while (check && (uint64_t)hmask + 1 < 2ull * n) hmask = hmask * 2 + 1;
+    while (check && (uint64_t)amask + 1 < 8ull * n) amask = amask * 2 + 1;
     if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
         (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 16)) || (r = grow(ew.ctlog_n, 8)) ||
         (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 16)) ||
         (r = grow(ew.d6, (size_t)n * 16)) || (r = grow(ew.hzst, 272 * 8)) || (r = ws_grow(n)))
         return r;
-    if (check && ((r = grow(ew.hzck, (size_t)n * 8)) || (r = grow(ew.hzpk, (size_t)n * 8)) || (r = grow(ew.hzfl, (size_t)n)) ||
-                  (r = grow(ew.hzdk, (size_t)n * 8)) || (r = grow(ew.hzsk, (size_t)n * 8)) ||
-                  (r = grow(ew.hztk, (size_t)(hmask + 1) * 8)) || (r = grow(ew.hztf, (size_t)(hmask + 1) * 8))))
+    if (check && ((r = grow(ew.hzk, (size_t)n * 8 * GF_HZ_NK)) || (r = grow(ew.hzfl, (size_t)n)) ||
+                  (r = grow(ew.hztk, (size_t)(hmask + 1) * 8)) || (r = grow(ew.hztf, (size_t)(hmask + 1) * 16)) ||
+                  (r = grow(ew.hzak, (size_t)(amask + 1) * 8)) || (r = grow(ew.hzaf, (size_t)(amask + 1) * 8))))
         return r;
     // In place (snap_out == the frames) with the check: the flagged pass must leave
     // the frames as they came, so the rewrites go to scratch and are copied at the end.
@@ -4668,8 +4766,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
     uint32_t *d_hz = (uint32_t *)ew.seq.p + 1;           // word 1 of the seq buffer: the hazard flag
     if (check) {
-        E.hz_ck = (uint64_t *)ew.hzck.p; E.hz_pk = (uint64_t *)ew.hzpk.p; E.hz_fl = (uint8_t *)ew.hzfl.p; E.hz = d_hz;
-        E.hz_dk = (uint64_t *)ew.hzdk.p; E.hz_sk = (uint64_t *)ew.hzsk.p;
+        E.hz_k = (uint64_t *)ew.hzk.p; E.hz_fl = (uint8_t *)ew.hzfl.p; E.hz = d_hz;
         if ((r = vip_sets(progs, ew, s))) return r;
         if (ew.vip4_any) { E.vip4 = (const uint32_t *)ew.vip4.p; E.vip4_mask = ew.vip4_mask; }
         if (ew.vip6_any) { E.vip6 = (const uint4 *)ew.vip6.p; E.vip6_mask = ew.vip6_mask; }
@@ -4677,7 +4774,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.X.snap = nullptr; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;   // writes: k_eg_groups
     memcpy(E.X.host6, node.host_ip6, 16);
     if ((r = px_log_begin(n, s, E.X))) return r;
-    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 16, s), "eg seq") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
+    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 12, s), "eg seq") || hip_ok(hipMemsetAsync(d_hz + 2, 0xff, 4, s), "eg hz") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
         return -EIO;
     unsigned long long *sink = (unsigned long long *)stats_sink();
     // With the check, the front counts into a scratch block folded into the sink
@@ -4700,17 +4797,20 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     }
     if (check) {
         ProfScope ps("k_hz_check", s);
-        if (hip_ok(hipMemsetAsync(ew.hztk.p, 0, (size_t)(hmask + 1) * 8, s), "hz keys") ||
-            hip_ok(hipMemsetAsync(ew.hztf.p, 0xff, (size_t)(hmask + 1) * 8, s), "hz first"))
-            return -EIO;
-        hipLaunchKernelGGL(k_hz_insert, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzck.p,
-                           (const uint64_t *)ew.hzpk.p, (const uint64_t *)ew.hzdk.p, (const uint64_t *)ew.hzsk.p,
-                           (const uint8_t *)ew.hzfl.p, n,
-                           (const uint32_t *)d_hz, (unsigned long long *)ew.hztk.p, (uint32_t *)ew.hztf.p, hmask);
-        hipLaunchKernelGGL(k_hz_probe, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzck.p,
-                           (const uint64_t *)ew.hzpk.p, (const uint64_t *)ew.hzsk.p, (const uint8_t *)ew.hzfl.p, n,
-                           (const unsigned long long *)ew.hztk.p,
-                           (const uint32_t *)ew.hztf.p, hmask, d_hz);
+        if (ew.hz_cap != hmask + 1 || ew.hz_gen >= 0xffffu) {   // new table or wrapped generation
+            if (hip_ok(hipMemsetAsync(ew.hztk.p, 0, (size_t)(hmask + 1) * 8, s), "hz keys") ||
+                hip_ok(hipMemsetAsync(ew.hztf.p, 0, (size_t)(hmask + 1) * 16, s), "hz first"))
+                return -EIO;
+            ew.hz_cap = hmask + 1; ew.hz_gen = 0;
+        }
+        const HzGen C{(unsigned long long *)ew.hztk.p, (unsigned long long *)ew.hztf.p, hmask, ++ew.hz_gen};
+        const HzTab A{(unsigned long long *)ew.hzak.p, (uint32_t *)ew.hzaf.p, amask};
+        hipLaunchKernelGGL(k_hz_clear, dim3(std::min<uint32_t>((amask + 1) / BLOCK, 8192)), dim3(BLOCK), 0, s, A,
+                           (const uint32_t *)d_hz);
+        hipLaunchKernelGGL(k_hz_insert, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzk.p,
+                           (const uint8_t *)ew.hzfl.p, n, (const uint32_t *)d_hz, C, A);
+        hipLaunchKernelGGL(k_hz_probe, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzk.p,
+                           (const uint8_t *)ew.hzfl.p, n, C, A, strict, d_hz);
         if ((r = hip_ok(hipGetLastError(), "k_hz_check"))) return r;
     }
     if ((r = schedule_groups(n, s))) return r;
@@ -4729,12 +4829,16 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     // ct_create4's deferred service entries, in batch order
-    uint32_t cnts[2] = {0, 0}, hz = 0;
+    uint32_t cnts[2] = {0, 0}, hzw[3] = {0, 0, 0}, &hz = hzw[0];
     if (hip_ok(hipMemcpyAsync(cnts, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost, s), "ctlog count") ||
-        (check && hip_ok(hipMemcpyAsync(&hz, d_hz, 4, hipMemcpyDeviceToHost, s), "hz flag")) ||
+        (check && hip_ok(hipMemcpyAsync(hzw, d_hz, 12, hipMemcpyDeviceToHost, s), "hz flag")) ||
         hip_ok(hipStreamSynchronize(s), "ctlog sync"))
         return -EIO;
-    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru);
+    if (hz & 2u) {
+        if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
+        return egress_each(a, b, now_sec, out, snap_out, s, lru);
+    }
+    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru, hzw[2], depth);
     if (check && sink) {
         hipLaunchKernelGGL(k_stats_fold, dim3(1), dim3(256), 0, s, (const unsigned long long *)fsink, sink);
         if ((r = hip_ok(hipGetLastError(), "k_stats_fold"))) return r;
@@ -4763,8 +4867,9 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     }
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
-    // the egress redirects' cilium_proxy{4,6} updates, in batch order
-    if ((r = px_log_apply(E.X, s, wsnap, fr.len, S, (uint8_t *)out, true))) return r;
+    // The egress redirects' cilium_proxy{4,6} updates stay in the log: the
+    // deliveries' handle_policy appends theirs and the whole log is applied in
+    // packet order after it (nothing on these paths reads the proxy maps).
     // handle_policy of the local deliveries (the tail calls of ipv4_local_delivery)
     gf_pkt_cols c2{};
     c2.n = n;
@@ -4777,7 +4882,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             return -EIO;
         return 0;
     };
-    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru))) return r;
+    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru, true))) return r;
     if (inplace && hip_ok(hipMemcpyAsync(snap_out, wsnap, (size_t)n * S, hipMemcpyDeviceToDevice, s), "snap copy"))
         return -EIO;
     return 0;
@@ -4787,41 +4892,73 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
 // direction is in the current run, and around every single-bucket tuple), then
 // every run through egress_call in order.  Nothing of the flagged pass changed
 // the maps: k_eg_groups idled, and the front only reads them.
+static int egress_greedy(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                         gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru);
 static int egress_ordered(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
-                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru) {
+                          gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru, uint32_t first, uint32_t depth) {
+    const uint32_t n = b->frames.n;
+    if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: ordering hazard at %u (run %u)\n", n, first, depth + 1);
+    if (first == 0 || first >= n || depth >= 32) return egress_greedy(a, b, now_sec, out, snap_out, s, lru);
+    // [0, first) has no hazard; the rest runs after it, checked again
+    std::vector<uint32_t> cut{0, first};
+    int r = egress_runs(a, b, now_sec, out, snap_out, s, false, cut);
+    if (r) return r;
+    const uint32_t S = b->frames.snap_stride;
+    gf_lxc_batch rest = *b;
+    rest.frames.n = n - first;
+    rest.frames.snap = b->frames.snap + (size_t)first * S;
+    rest.frames.len = b->frames.len + first;
+    if (b->lxc_id) rest.lxc_id = b->lxc_id + first;
+    if (b->flow_hash) rest.flow_hash = b->flow_hash + first;
+    return egress_call(a, &rest, now_sec, out + first, snap_out ? snap_out + (size_t)first * S : nullptr, s, true, lru,
+                       depth + 1);
+}
+// Many runs: the cut points on the host, in one pass over the batch's keys.
+static int egress_greedy(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                         gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru) {
     EgWs &ew = eg_ws();
-    const uint32_t n = b->frames.n, S = b->frames.snap_stride;
-    std::vector<uint64_t> ck(n), pk(n), dk(n), sk(n);
+    const uint32_t n = b->frames.n;
+    std::vector<uint64_t> K((size_t)n * GF_HZ_NK);
     std::vector<uint8_t> fl(n);
-    if (hip_ok(hipMemcpyAsync(ck.data(), ew.hzck.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz ck") ||
-        hip_ok(hipMemcpyAsync(pk.data(), ew.hzpk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz pk") ||
-        hip_ok(hipMemcpyAsync(dk.data(), ew.hzdk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz dk") ||
-        hip_ok(hipMemcpyAsync(sk.data(), ew.hzsk.p, (size_t)n * 8, hipMemcpyDeviceToHost, s), "hz sk") ||
+    if (hip_ok(hipMemcpyAsync(K.data(), ew.hzk.p, K.size() * 8, hipMemcpyDeviceToHost, s), "hz keys") ||
         hip_ok(hipMemcpyAsync(fl.data(), ew.hzfl.p, n, hipMemcpyDeviceToHost, s), "hz fl") ||
         hip_ok(hipStreamSynchronize(s), "hz sync"))
         return -EIO;
+    // the rules of k_hz_insert / k_hz_probe over the current run (keys are odd:
+    // bit 0 carries a connection key's direction)
     std::vector<uint32_t> cut{0};
     std::unordered_set<uint64_t> seen;
-    const uint64_t DIRBIT = 1ull;                      // keys are odd: bit 0 carries the direction
+    const uint64_t D = 1ull;
+    uint32_t why[5] = {0, 0, 0, 0, 0};
+    auto k = [&](uint32_t which, uint32_t j) { return K[(size_t)which * n + j] & ~D; };
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t f = fl[j];
         if (!(f & GF_HZ_VALID)) continue;
-        if (f & GF_HZ_SPECIAL) {
-            if (j > cut.back()) cut.push_back(j);
-            cut.push_back(j + 1);
-            seen.clear();
-            continue;
-        }
-        const uint64_t me = (ck[j] & ~DIRBIT) | ((f & GF_HZ_DIR) ? DIRBIT : 0ull), pair = pk[j] & ~DIRBIT;
-        bool hit = (f & GF_HZ_ICMP) ? seen.count(pair) != 0 : seen.count(me ^ DIRBIT) != 0;
-        if (f & GF_HZ_VIP) hit = hit || seen.count(sk[j] & ~DIRBIT) != 0;
-        if (hit) { cut.push_back(j); seen.clear(); }
-        seen.insert(me);
-        seen.insert(pair);
-        seen.insert(dk[j] & ~DIRBIT);
-        seen.insert(sk[j] & ~DIRBIT);
+        const bool h0 = seen.count(k(1, j) | ((f & GF_HZ_DIRE) ? 0ull : D)) != 0;
+        const bool h1 = (f & GF_HZ_ICMP) && seen.count(k(3, j) ^ 2ull) != 0;
+        const bool h2 = seen.count((k(3, j) ^ GF_HZ_ICMPSALT) & ~D) != 0;
+        const bool h3 = (f & GF_HZ_LOOP) && (seen.count(k(0, j)) || seen.count(k(0, j) | D));
+        const bool h4 = (f & GF_HZ_VIP) && seen.count(k(4, j) ^ 2ull) != 0;
+        why[0] += h0; why[1] += h1; why[2] += h2; why[3] += h3; why[4] += h4;
+        if (h0 || h1 || h2 || h3 || h4) { cut.push_back(j); seen.clear(); }
+        if (f & GF_HZ_DLV) seen.insert(k(0, j) | ((f & GF_HZ_DIRI) ? D : 0ull));
+        seen.insert(k(2, j) ^ 2ull);
+        if (f & GF_HZ_ICMP) seen.insert((k(2, j) ^ GF_HZ_ICMPSALT) & ~D);
+        seen.insert(k(4, j) ^ 2ull);
+        seen.insert(k(5, j) ^ 2ull);
     }
     if (cut.back() != n) cut.push_back(n);
+    if (getenv("GF_HZ_DEBUG"))
+        fprintf(stderr, "[gf] egress n=%u: %zu ordered runs (reply %u, icmp-after %u, after-icmp %u, loopback %u, vip %u)\n",
+                n, cut.size() - 1, why[0], why[1], why[2], why[3], why[4]);
+    return egress_runs(a, b, now_sec, out, snap_out, s, lru, cut);
+}
+
+// The runs [cut[k], cut[k+1]) of a batch through egress_call, in order; the LRU
+// stand-in after the last.
+static int egress_runs(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
+                       gf_egress_out *out, uint8_t *snap_out, hipStream_t s, bool lru, const std::vector<uint32_t> &cut) {
+    const uint32_t S = b->frames.snap_stride;
     for (size_t k = 0; k + 1 < cut.size(); k++) {
         const uint32_t lo = cut[k], hi = cut[k + 1];
         gf_lxc_batch sub = *b;
@@ -4854,5 +4991,14 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     lock_array_maps(L, a);
     L.lock();
     CallOrder co(s);
-    return egress_call(a, b, now_sec, out, snap_out, s, true, true);
+    static const bool nocheck = getenv("GF_EG_NOCHECK") != nullptr;     // diagnosis only: the unordered schedule
+    static const bool dbg = getenv("GF_HZ_DEBUG") != nullptr;
+    if (!dbg) return egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);
+    hipStreamSynchronize(s);
+    auto t0 = std::chrono::steady_clock::now();
+    int r = egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);
+    hipStreamSynchronize(s);
+    fprintf(stderr, "[gf] egress n=%u: %.3f ms\n", fr.n,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return r;
 }

@@ -1308,7 +1308,7 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
     return sc
 
 
-TENANT = 64      # endpoints per tenant in the egress workload
+TENANT = 256     # endpoints per tenant in the egress workload (256: one tenant, every endpoint talks to every other)
 
 
 def egress_tables(n_ep=256, n_svc=1024, backends=4, ct_max=64_000_000, seed=0xE6E5):
