@@ -72,17 +72,20 @@ def cpu_base(value, T, sample, single=None):
 
 
 # ----------------------------------------------------------------------------- timing
-def timed(run_step, W, K, dev, world=1):
+def timed(run_step, W, K, dev, world=1, ranged=False):
     """W untimed warm-up steps, then K steps bracketed by barrier + synchronize,
-    with the verdict counter sink and the launch profiler on.  Returns
-    (elapsed_s (max over ranks), counters (summed over ranks), local counters,
-    {kernel: (launches, total_ms)})."""
+    with the verdict counter sink and the launch profiler on (ranged: run_step(a, b)
+    runs steps a..b-1 in one call).  Returns (elapsed_s (max over ranks), counters
+    (summed over ranks), local counters, {kernel: (launches, total_ms)})."""
     import torch
     import torch.distributed as dist
     import ctypes as C
     from cilium_amd._lib import lib, gf_prof_rec
-    for s in range(W):
-        run_step(s)
+    if ranged:
+        run_step(0, W)
+    else:
+        for s in range(W):
+            run_step(s)
     torch.cuda.synchronize()
     counters = torch.zeros(512, dtype=torch.int64, device=dev)
     lib.gf_set_stats_sink(C.c_void_p(counters.data_ptr()))
@@ -91,8 +94,11 @@ def timed(run_step, W, K, dev, world=1):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(W, W + K):
-        run_step(s)
+    if ranged:
+        run_step(W, W + K)
+    else:
+        for s in range(W, W + K):
+            run_step(s)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -235,7 +241,14 @@ def bench_config2(args, dev, rank, world):
     torch.cuda.synchronize()
     log(f"rank {rank}: generated {W + K} steps ({time.time() - t0:.1f}s)")
     now = sc.now
-    elapsed, c, lc, kern = timed(lambda s: dp.ingress(batches[s], now + s, out=outs[s]), W, K, dev, world)
+    if not args.pipeline:
+        elapsed, c, lc, kern = timed(lambda s: dp.ingress(batches[s], now + s, out=outs[s]), W, K, dev, world)
+    else:
+        # the stream of batches through gf_policy_ingress_classify_batches: batch s+1's
+        # schedule is built on a second stream while handle_policy of batch s runs
+        # (measured slower: the overlapped kernels share the memory system)
+        elapsed, c, lc, kern = timed(lambda a, b: dp.ingress_batches(batches[a:b], [now + s for s in range(a, b)],
+                                                                      outs[a:b]), W, K, dev, world, ranged=True)
     total_pkts = int(c[268])
     local_pkts = sum(batches[s].n for s in range(W, W + K))
     if world == 1 and not os.environ.get("GPUFLOW_DIAG_LIB"):
@@ -822,6 +835,8 @@ def main():
                     help="CT max_entries (LRU): 134,217,728, above the entries a default run creates")
     ap.add_argument("--ct6-prefill", type=int, default=8_000_000)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the parity legs")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="config 2: the steps through gf_policy_ingress_classify_batches (schedule overlap)")
     ap.add_argument("--no-extra", action="store_true", help="config 2 only (skip the other configurations)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-div", type=int, default=4, help="parity sample: 1 in N address pairs")

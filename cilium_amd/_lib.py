@@ -152,6 +152,8 @@ _sig("gf_policy_array_create", C.c_int)
 _sig("gf_policy_array_update", C.c_int, C.c_int, C.c_uint32, C.c_int)
 _sig("gf_node_config", C.c_int, C.POINTER(gf_node_cfg))
 _sig("gf_policy_ingress_classify", C.c_int, C.c_int, C.POINTER(gf_pkt_cols), C.c_uint32, VP, VP)
+_sig("gf_policy_ingress_classify_batches", C.c_int, C.c_int, C.c_uint32, C.POINTER(C.POINTER(gf_pkt_cols)),
+     C.POINTER(C.c_uint32), C.POINTER(VP), VP)
 _sig("gf_pipeline_load", C.c_int, C.POINTER(gf_pipeline_cfg))
 _sig("gf_pipeline_classify", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, VP, VP, VP, VP)
 _sig("gf_ct_gc", C.c_int, C.c_int, C.c_uint32, VP)
@@ -184,6 +186,6 @@ EXPORTED = [
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_policy_ingress_classify_batches", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
 ]

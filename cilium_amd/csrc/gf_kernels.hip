@@ -3456,7 +3456,10 @@ void prof_drain() {
 struct Workspace {
     DevBuf rec, keys, skeys, perm, cnt, off, tmp, sched, order;
 };
-Workspace &ws() { static Workspace w; return w; }
+// Two workspaces: gf_policy_ingress_classify_batches builds the schedule of
+// batch k+1 in one while handle_policy of batch k runs from the other.
+int g_ws_slot = 0;
+Workspace &ws() { static Workspace w[2]; return w[g_ws_slot]; }
 gf_event_ring &event_ring() { static gf_event_ring r{}; return r; }
 struct PipeWs {
     DevBuf s6, d6;             // IPv6 addresses of the rewritten frames (read by handle_policy)
@@ -4056,7 +4059,7 @@ using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t 
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
                        const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
-                       uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false) {
+                       uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false, bool prepared = false) {
     int r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
@@ -4082,8 +4085,11 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     // 2. group by flow group (records and keys first), 3. longest-first bucket order
     uint32_t n = pkts->n;
     Workspace &w = ws();
-    if ((r = ws_grow(n))) return r;
-    if (pack) {
+    if (prepared) {
+        // pack + schedule already built in ws() (ingress_prepare)
+    } else if ((r = ws_grow(n))) {
+        return r;
+    } else if (pack) {
         if ((r = pack((const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p))) return r;
     } else {
         ProfScope ps("k_ing_pack", s);
@@ -4092,7 +4098,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                            (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
-    if ((r = schedule_groups(n, s))) return r;
+    if (!prepared && (r = schedule_groups(n, s))) return r;
     uint32_t *d_sched = (uint32_t *)w.sched.p;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
     IngCtx X{};
@@ -4151,7 +4157,87 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     return 0;
 }
 
+// The stateless half of ingress_run (k_ing_pack + the flow-group schedule) into ws().
+static int ingress_prepare(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, hipStream_t s) {
+    const uint32_t n = pkts->n;
+    Workspace &w = ws();
+    int r;
+    if ((r = ws_grow(n))) return r;
+    {
+        ProfScope ps("k_ing_pack", s);
+        hipLaunchKernelGGL(k_ing_pack, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *pkts,
+                           (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p);
+        if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
+    }
+    return schedule_groups(n, s);
+}
+
+// The stream that builds the next batch's schedule, and the events between the two.
+struct PipeSync {
+    hipStream_t aux = nullptr;
+    hipEvent_t ready = nullptr, built[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    int init() {
+        if (aux) return 0;
+        if (hip_ok(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking), "aux stream")) return -EIO;
+        for (hipEvent_t *e : {&ready, &built[0], &built[1], &done[0], &done[1]})
+            if (hip_ok(hipEventCreateWithFlags(e, hipEventDisableTiming), "pipe event")) return -EIO;
+        return 0;
+    }
+};
+static PipeSync &pipe_sync() { static PipeSync p; return p; }
+
 extern "C" {
+
+int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols *const *batches,
+                                       const uint32_t *now_sec, gf_ingress_out *const *outs, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    auto o = get_obj(array);
+    if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
+    auto a = std::static_pointer_cast<PolicyArray>(o);
+    if (nb && (!batches || !now_sec || !outs)) return -EFAULT;
+    for (uint32_t k = 0; k < nb; k++) {
+        const int c = check_cols(batches[k]);
+        if (c < 0) return c;
+        if (c && !outs[k]) return -EFAULT;
+        if (batches[k]->n > (1u << 30)) return -E2BIG;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    MapLocks L;
+    lock_array_maps(L, a);
+    L.lock();
+    CallOrder co(s);
+    PipeSync &P = pipe_sync();
+    int r;
+    if ((r = P.init())) return r;
+    std::vector<std::shared_ptr<ProgLxc>> progs;
+    if ((r = prog_table(a, s, progs))) return r;          // the program table k_ing_pack reads, on s
+    if (hip_ok(hipEventRecord(P.ready, s), "ready") || hip_ok(hipStreamWaitEvent(P.aux, P.ready, 0), "aux wait"))
+        return -EIO;
+    auto prep = [&](uint32_t k) -> int {                  // batch k's schedule on the aux stream, workspace k & 1
+        const int slot = (int)(k & 1u);
+        if (k >= 2 && hip_ok(hipStreamWaitEvent(P.aux, P.done[slot], 0), "aux wait done")) return -EIO;
+        g_ws_slot = slot;
+        int rr = batches[k]->n ? ingress_prepare(a, batches[k], P.aux) : 0;
+        g_ws_slot = 0;
+        if (rr) return rr;
+        return hip_ok(hipEventRecord(P.built[slot], P.aux), "built") ? -EIO : 0;
+    };
+    if (nb && (r = prep(0))) return r;
+    for (uint32_t k = 0; k < nb; k++) {
+        if (k + 1 < nb && (r = prep(k + 1))) return r;    // overlaps handle_policy of batch k
+        const int slot = (int)(k & 1u);
+        if (hip_ok(hipStreamWaitEvent(s, P.built[slot], 0), "wait built")) return -EIO;
+        if (batches[k]->n) {
+            g_ws_slot = slot;
+            r = ingress_run(a, batches[k], now_sec[k], outs[k], s, PackFn(), nullptr, nullptr, nullptr, 0, nullptr,
+                            true, false, true);
+            g_ws_slot = 0;
+            if (r) return r;
+        }
+        if (hip_ok(hipEventRecord(P.done[slot], s), "done")) return -EIO;
+    }
+    return 0;
+}
 
 int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
                                void *stream) {
@@ -4994,10 +5080,10 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     static const bool nocheck = getenv("GF_EG_NOCHECK") != nullptr;     // diagnosis only: the unordered schedule
     static const bool dbg = getenv("GF_HZ_DEBUG") != nullptr;
     if (!dbg) return egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     auto t0 = std::chrono::steady_clock::now();
     int r = egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     fprintf(stderr, "[gf] egress n=%u: %.3f ms\n", fr.n,
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     return r;

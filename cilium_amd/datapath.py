@@ -226,6 +226,21 @@ class Datapath:
                "gf_policy_ingress_classify")
         return out
 
+    def ingress_batches(self, bs, nows, outs=None):
+        """gf_policy_ingress_classify_batches: the batches in order, each batch's
+        schedule built on a second stream while the previous one runs."""
+        torch = _torch()
+        if outs is None:
+            outs = [torch.empty((b.n, 8), dtype=torch.uint8, device=b.device) for b in bs]
+        cols = [b.cols() for b in bs]
+        k = len(bs)
+        cp = (C.POINTER(gf_pkt_cols) * k)(*[C.pointer(c) for c in cols])
+        nw = (C.c_uint32 * k)(*[int(x) for x in nows])
+        op = (C.c_void_p * k)(*[_ptr(o) for o in outs])
+        _check(lib.gf_policy_ingress_classify_batches(self.policy_array, k, cp, nw, op, _stream()),
+               "gf_policy_ingress_classify_batches")
+        return outs
+
     def pipeline(self, b, now, out=None, snap_out=True):
         """Full pipeline over the batch's frames: returns (records [n,24] u8,
         new_daddr6 [n,16] u8, rewritten snaps [n,stride] u8 or None)."""

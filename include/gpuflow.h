@@ -326,6 +326,13 @@ typedef struct gf_ingress_out {
  * replaces bpf_ktime_get_sec() for the whole batch. */
 int gf_policy_ingress_classify(int policy_array, const gf_pkt_cols *pkts,
                                uint32_t now_sec, gf_ingress_out *out, void *stream);
+/* nb consecutive gf_policy_ingress_classify calls on `stream` (batch k with
+ * now_sec[k] into outs[k]), with identical results.  The stateless half of a
+ * batch (record pack, flow-group sort and schedule: no map state) is built on an
+ * internal second stream while handle_policy of the previous batch runs, so the
+ * schedule leaves the critical path of a stream of batches. */
+int gf_policy_ingress_classify_batches(int policy_array, uint32_t nb, const gf_pkt_cols *const *batches,
+                                       const uint32_t *now_sec, gf_ingress_out *const *outs, void *stream);
 
 /* ---- endpoint egress: the from-container program (bpf/bpf_lxc.c:685-738
  * handle_ingress -> tail_handle_ipv4 -> handle_ipv4_from_lxc :427-658) ----

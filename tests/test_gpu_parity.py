@@ -88,6 +88,25 @@ def test_config2_ingress_scaled():
     assert dp.dump_map("cilium_ct4_global") == ref.dump("cilium_ct4_global")
 
 
+def test_ingress_batches_pipelined_equals_oracle():
+    """gf_policy_ingress_classify_batches (schedule of batch k+1 on a second stream
+    while batch k runs) over the scaled config-2 stream and its fuzz sibling:
+    every record of every batch and the CT afterwards equal the oracle's
+    sequential batches."""
+    for sc in (synth.config2(n_flows=60_000, n_pairs=8_000, n_ep=32, n_ids=512, n_l3=200, n_l4=400, n_wc=8,
+                             n_cidr=32, ct_max=400_000), synth.fuzz(11, n_batches=4)):
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        bs = [DeviceBatch(pk) for pk in sc.batches]
+        nows = [sc.now + 3 * k for k in range(len(bs))]
+        outs = dp.ingress_batches(bs, nows)
+        torch.cuda.synchronize()
+        for bi, (pk, io) in enumerate(zip(sc.batches, outs)):
+            _cmp_struct(to_numpy(io, ING_OUT), ref.ingress(pk, nows[bi]), f"{sc.name} batch {bi}")
+        for name in sc.maps:
+            if sc.maps[name].ksz in (14, 40):
+                assert dp.dump_map(name) == ref.dump(name), name
+
+
 def test_ingress_large_batch_properties():
     """Full-size-style property checks without the oracle: replaying the same
     established stream twice is idempotent for the verdict of REPLY packets and
