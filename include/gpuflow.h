@@ -19,6 +19,8 @@
  *     gf_obj_get           <- bpf.ObjGet           pkg/bpf/bpf.go:246-266
  *     gf_obj_close         <- bpf.ObjClose         pkg/bpf/bpf.go:269-274
  *     gf_map_get_info      <- bpf.GetMapInfo       pkg/bpf/map.go:171-209 (fdinfo parse)
+ *     gf_map_lookup_batch  <- the GetNextKey + LookupElement loop of bpf.Map.DumpWithCallback
+ *                             pkg/bpf/map.go:319-369, in chunks
  *     gf_now_sec           <- bpf.GetMtime()/1e9   pkg/bpf/bpf.go:426-435, bpf/lib/utils.h:58-64
  *
  *  2. Program API (replaces the BPF programs of the hot path).  A "program"
@@ -29,6 +31,8 @@
  *     gf_xdp_classify            <- xdp_start/check_filters   bpf/bpf_xdp.c:88-184
  *     gf_lb_classify             <- from_netdev (bpf_lb)      bpf/bpf_lb.c:58-212
  *     gf_policy_ingress_classify <- handle_policy/ipv{4,6}_policy bpf/bpf_lxc.c:745-1024
+ *     gf_lxc_egress_classify     <- from-container handle_ingress bpf/bpf_lxc.c:427-738
+ *     gf_pipeline_classify       <- bpf_xdp -> bpf_lb -> bpf_netdev -> cilium_policy tail call
  *     gf_parse_frames            <- the skb_load_bytes()/revalidate_data() header
  *                                   accesses of those programs (bpf/lib/common.h:67-87,
  *                                   bpf/lib/ipv4.h:45-48, bpf/lib/ipv6.h:61-98)
@@ -37,7 +41,10 @@
  * the HBM replica at the next classify call (batch boundary; a documented
  * relaxation of the kernel's per-element RCU visibility).  Maps the
  * datapath writes (CT entries, policy counters) are device-authoritative:
- * the next host-side access pulls the HBM copy back first.
+ * host-side lookups, updates, deletes and get_next_key then walk the key's
+ * probe sequence in HBM with small reads / writes, and dumps stream in chunks
+ * selected on the device; no call copies a whole table.  Each map has its own
+ * lock; a classify call holds the locks of the maps its programs bind.
  *
  * All batch/column/output pointers passed to classify calls are DEVICE
  * pointers (hipMalloc / torch CUDA tensors).  `stream` is a hipStream_t
@@ -241,7 +248,8 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out,
 #define GF_LXC_F_HAVE_L4_POLICY  (1u << 2)  /* HAVE_L4_POLICY */
 #define GF_LXC_F_CT_ACCOUNTING   (1u << 3)  /* CONNTRACK_ACCOUNTING */
 #define GF_LXC_F_LXC_IPV4        (1u << 4)  /* LXC_IPV4 */
-#define GF_LXC_F_POLICY_EGRESS   (1u << 5)  /* POLICY_EGRESS (the agent does not emit it; lxc_config.h does) */
+#define GF_LXC_F_POLICY_EGRESS   (1u << 5)  /* POLICY_EGRESS (pkg/endpoint/endpoint.go:153-156, emitted when egress
+                                               is enforced, pkg/endpoint/policy.go:820-839) */
 #define GF_MAX_L4_INGRESS 64
 #define GF_MAX_PORTMAP 16
 typedef struct gf_portmap {    /* struct portmap (bpf/lib/common.h), LXC_PORT_MAPPINGS entries */
