@@ -98,7 +98,7 @@ class gf_node_cfg(C.Structure):
 
 class gf_netdev_cfg(C.Structure):
     _fields_ = [("lxc_map", C.c_int), ("flags", C.c_uint32), ("fixed_secctx", C.c_uint32),
-                ("router_ip6", C.c_uint8 * 16)]
+                ("router_ip6", C.c_uint8 * 16), ("ingress_ifindex", C.c_uint32)]
 
 
 class gf_pipeline_cfg(C.Structure):

@@ -282,40 +282,72 @@ __device__ __forceinline__ bool lxc_has6(const gf_htab_desc &lxc, const uint32_t
 }
 
 // xdp_start -> check_filters -> check_v4 / check_v6 (bpf/bpf_xdp.c:97-184) for
-// packet i; ab accumulates the algorithmic bytes.
+// packet i; ab accumulates the algorithmic bytes.  The three lookups (the LPM
+// trie, the /32 or /128 hash, the cilium_lxc endpoint) have no side effects, so
+// GF_XDP_PRE can load the hash probes' home lines before the trie walk (all in
+// flight together; the verdict still combines them in the reference's order).
+// Measured on config 1 (r2): 0.080 ms with both lines preloaded, 0.076 with the
+// prefix hash only, 0.075 with none — k_xdp is bound by the request rate of its
+// L2-resident tables, not by the latency of the chain, so the default issues
+// each probe only when the reference would.
+#define GF_XDP_U 2
+#ifndef GF_XDP_PRE
+#define GF_XDP_PRE 0      // home lines loaded before the trie walk: 0 none, 1 the prefix hash, 2 + cilium_lxc
+#endif
 template <class A>
 __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint32_t len, uint32_t et, uint32_t &ab) {
     if (len < 14) return XDP_DROP_;
     if (et == 0x0800) {
         if (len < 34) return XDP_DROP_;
         uint32_t sa = a.saddr4();
+        const uint32_t kw[2] = {32u, sa};
+        const uint32_t lk[5] = {a.daddr4(), 0, 0, 0, 1u};     // endpoint_key {ip4, pad.., family=1}
+        ProbeLine<20, GF_XDP_U> ll;
+        if (GF_XDP_PRE >= 2) ll.load(x.lxc, key_hash<20>(lk));
+        ProbeLine<8, GF_XDP_U> hl;
+        if (GF_XDP_PRE >= 1 && x.has_h4) hl.load(x.h4, key_hash<8>(kw));
         bool drop = false;
         ab += 10;
         if (x.has_h4) {
             ab += 9;
             if (trie_lookup<1>(x.l4, &sa)) drop = true;
-            else { ab += 9; uint32_t kw[2] = {32u, sa}; drop = ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0; }
+            else {
+                ab += 9;
+                if (GF_XDP_PRE < 1) hl.load(x.h4, key_hash<8>(kw));
+                drop = probe2<8, GF_XDP_U, 0>(x.h4, kw, kw, hl, false).f >= 0;
+            }
         }
         if (drop) return XDP_DROP_;
         ab += 20;
-        return lxc_has4(x.lxc, a.daddr4()) ? XDP_PASS_ : XDP_DROP_;
+        if (GF_XDP_PRE < 2) ll.load(x.lxc, key_hash<20>(lk));
+        return probe2<20, GF_XDP_U, 0>(x.lxc, lk, lk, ll, false).f >= 0 ? XDP_PASS_ : XDP_DROP_;
     }
     if (et == 0x86DD) {
         if (len < 54 || !a.has6()) return XDP_DROP_;
         uint4 s = a.saddr6();
         uint32_t sw[4] = {s.x, s.y, s.z, s.w};
+        const uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w};
+        const uint4 d = a.daddr6();
+        const uint32_t lk[5] = {d.x, d.y, d.z, d.w, 2u};
+        ProbeLine<20, GF_XDP_U> ll;
+        if (GF_XDP_PRE >= 2) ll.load(x.lxc, key_hash<20>(lk));
+        ProbeLine<20, GF_XDP_U> hl;
+        if (GF_XDP_PRE >= 1 && x.has_h6) hl.load(x.h6, key_hash<20>(kw));
         bool drop = false;
         ab += 34;
         if (x.has_h6) {
             ab += 21;
             if (trie_lookup<4>(x.l6, sw)) drop = true;
-            else { ab += 21; uint32_t kw[5] = {128u, s.x, s.y, s.z, s.w}; drop = ht_find<20>(x.h6, kw, key_hash<20>(kw)) >= 0; }
+            else {
+                ab += 21;
+                if (GF_XDP_PRE < 1) hl.load(x.h6, key_hash<20>(kw));
+                drop = probe2<20, GF_XDP_U, 0>(x.h6, kw, kw, hl, false).f >= 0;
+            }
         }
         if (drop) return XDP_DROP_;
         ab += 20;
-        uint4 d = a.daddr6();
-        uint32_t dw[4] = {d.x, d.y, d.z, d.w};
-        return lxc_has6(x.lxc, dw) ? XDP_PASS_ : XDP_DROP_;
+        if (GF_XDP_PRE < 2) ll.load(x.lxc, key_hash<20>(lk));
+        return probe2<20, GF_XDP_U, 0>(x.lxc, lk, lk, ll, false).f >= 0 ? XDP_PASS_ : XDP_DROP_;
     }
     return XDP_PASS_;
 }
@@ -509,6 +541,7 @@ struct IngCtx {
     uint32_t snap_stride;
     uint32_t *plog, *plog_n;   // cilium_proxy{4,6} update log (16 words per redirect) and its length
     uint32_t gw, host6[4];     // IPV4_GATEWAY, HOST_IP (node_config.h)
+    uint8_t *tmark, *tcap;     // trace notifications: per-packet GF_TR_* marks, 128-B captures (null: off)
 };
 
 // ---- handle_policy's own header writes (kept out of line: cold paths of the
@@ -531,6 +564,38 @@ __device__ __forceinline__ PolCtx pol_ctx(const IngCtx &X) {
 template <class XC>
 __device__ __forceinline__ Row pol_row(const XC &X, uint32_t i, uint32_t len) {
     return Row{X.snap + (size_t)i * X.snap_stride, X.snap_stride < len ? X.snap_stride : len};
+}
+// Trace notifications (bpf/lib/trace.h:59-106).  The records themselves are
+// written after the launches by the event pass (k_ev_*), from the verdict
+// records; the kernels only leave what the records cannot tell: a per-packet
+// mark byte and, for TRACE_TO_PROXY, the frame as it was when the redirect sent
+// it (before its own rewrites, lib/lxc.h:115-117 / 167-169).
+#define GF_TR_PX_EGRESS 1u    // from-container ipv{4,6}_redirect_to_host_port entered (TRACE_TO_PROXY)
+#define GF_TR_PX_POLICY 2u    // handle_policy's ipv{4,6}_redirect_to_host_port entered (TRACE_TO_PROXY)
+#define GF_TR_CLUSTER   4u    // from-container dstID == CLUSTER_ID (TRACE_TO_STACK's dst_label)
+#define GF_TR_CAPTURED 16u    // tcap holds the TO_PROXY capture
+// f: the frame in HBM; a/na: header bytes a kernel holds in an LDS copy (they
+// replace the frame's first na bytes); cap = min(len, stride, TRACE_PAYLOAD_LEN).
+__device__ __forceinline__ void trace_proxy(uint8_t *tmark, uint8_t *tcap, const uint8_t *f, const uint8_t *a,
+                                            uint32_t na, uint32_t cap, uint32_t i, uint32_t bit) {
+    uint32_t m = tmark[i] | bit;
+    if (f) {
+        uint8_t *d = tcap + (size_t)i * GF_TRACE_PAYLOAD_LEN;
+        for (uint32_t k = 0; k < GF_TRACE_PAYLOAD_LEN; k += 4) {
+            uint32_t v = 0;
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint32_t o = k + b;
+                if (o < cap) v |= (uint32_t)(o < na ? a[o] : f[o]) << (8 * b);
+            }
+            *reinterpret_cast<uint32_t *>(d + k) = v;
+        }
+        m |= GF_TR_CAPTURED;
+    }
+    tmark[i] = (uint8_t)m;
+}
+__device__ __forceinline__ uint32_t trace_cap_len(uint32_t len, uint32_t stride) {
+    const uint32_t c = len < stride ? len : stride;
+    return c < GF_TRACE_PAYLOAD_LEN ? c : GF_TRACE_PAYLOAD_LEN;
 }
 // reverse_map_l4_port (bpf/lib/lb.h:217-251) + __lb4_rev_nat / __lb6_rev_nat
 // (lb.h:253-293, 447-512; v4 with REV_NAT_F_TUPLE_SADDR: the old address is the
@@ -1118,6 +1183,9 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
         ofl |= GF_INGRESS_F_CREATED;
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        if (X.tmark)
+            trace_proxy(X.tmark, X.tcap, X.snap ? X.snap + (size_t)i * X.snap_stride : nullptr, nullptr, 0,
+                        trace_cap_len(len, X.snap_stride), i, GF_TR_PX_POLICY);
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
         if (X.snap || X.plog) { const uint32_t od[1] = {r.daddr}; pol_redirect(X, i, len, r.l4_off, nh, t, false, (uint32_t)verdict & 0xffffu, od, r.src_identity); }
@@ -1193,6 +1261,9 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
         ofl |= GF_INGRESS_F_CREATED;
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        if (X.tmark)
+            trace_proxy(X.tmark, X.tcap, X.snap ? X.snap + (size_t)i * X.snap_stride : nullptr, nullptr, 0,
+                        trace_cap_len(len, X.snap_stride), i, GF_TR_PX_POLICY);
         int r3 = redirect_checks(len, r.l4_off, nh);
         if (r3 < 0) return r3;
         if (X.snap || X.plog) {
@@ -1535,6 +1606,7 @@ struct PipeDev {
     LbDev L;
     NetdevDev nd;
     uint32_t has_xdp, has_lb, lb_redirect_ifindex, vec_copy;
+    uint8_t *tcap_in;              // TRACE_FROM_STACK captures (128 B per packet; null: the netdev does not trace)
 };
 // lb4_xlate / lb6_xlate writes (bpf/lib/lb.h:615-659, 397-423) of a translation
 // lb_v4/lb_v6 accepted (their checks passed, so every helper succeeds).
@@ -1725,6 +1797,16 @@ __global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *
                     n6[0] = n6[1] = n6[2] = n6[3] = 0;
                 }
             }
+            if (P.tcap_in) {                            // from_netdev's send_trace_notify (bpf_netdev.c:436)
+                uint8_t *d = P.tcap_in + (size_t)i * GF_TRACE_PAYLOAD_LEN;
+                const uint32_t cb = S < GF_TRACE_PAYLOAD_LEN ? S : GF_TRACE_PAYLOAD_LEN;
+                if (P.vec_copy) {
+                    for (uint32_t k = 0; k < cb; k += 16)
+                        *reinterpret_cast<uint4 *>(d + k) = *reinterpret_cast<const uint4 *>(w.p + k);
+                } else {
+                    for (uint32_t k = 0; k < cb; k++) d[k] = w.p[k];
+                }
+            }
             const int r = pipe_netdev(P.nd, w, h, et, len, sec, ifx, lxc, mapped, ndport, ab);
             if (mapped) { o.flags |= GF_PIPE_F_PORTMAP; o.dport = (uint16_t)ndport; }
             o.stage = GF_STAGE_NETDEV;
@@ -1898,6 +1980,10 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
             const int k = __builtin_ctz(m);
             m &= m - 1;
             uint64_t j = w * 32 + k;
+            // hole: a slot of this cluster before j was emptied by this walk.  Until
+            // then every slot from the cluster start to j is occupied, so the entry
+            // at j (whose home lies in that range) cannot move: no rehash needed.
+            bool hole = false;
             for (;;) {
                 uint8_t *sl = d.slots + j * d.slot_size;
                 const uint32_t st = sl[d.ksz];
@@ -1905,6 +1991,7 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
                 if (st == GF_SLOT_TOMB) {
                     sl[d.ksz] = GF_SLOT_EMPTY;
                     tombs++;
+                    hole = true;
                 } else {
                     const uint8_t *v = ht_val(d, j) + lt_off;
                     const uint32_t lt = *reinterpret_cast<const uint32_t *>(v);
@@ -1912,10 +1999,14 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
                     if (gc_kill(lt, fl, cut)) {
                         sl[d.ksz] = GF_SLOT_EMPTY;
                         dead++;
-                    } else {
+                        hole = true;
+                    } else if (hole) {
                         uint32_t kw[10];
                         for (uint32_t q = 0; q < 10; q++) kw[q] = 0;
-                        for (uint32_t q = 0; q < d.ksz; q++) kw[q >> 2] |= (uint32_t)sl[q] << (8 * (q & 3));
+                        for (uint32_t q = 0; q < d.ksz; q += 4) {       // slots are 4-B aligned
+                            const uint32_t x = *reinterpret_cast<const uint32_t *>(sl + q);
+                            kw[q >> 2] = d.ksz - q >= 4 ? x : (x & ((1u << (8 * (d.ksz - q))) - 1u));
+                        }
                         const uint64_t home = gf_home_slot(gf_key_hash(kw, d.ksz, mode), d.mask, d.slot_size);
                         for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
                             if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) { gc_move(d, j, p, vstride); break; }
@@ -1973,39 +2064,95 @@ __global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev 
         for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
 }
 // Age histogram: wave-aggregated (a wave's entries mostly share a bin), then a
-// block-local direct-mapped LDS cache of bins, flushed with one global add each.
-#define GF_LRU_LDS 1024u
-__global__ __launch_bounds__(BLOCK) void k_lru_hist(gf_htab_desc d, uint32_t lt_off, uint32_t now, LruDev *L) {
+// block-local direct-mapped LDS cache of bins: a 64-bit {bin, count} word per
+// line, updated by CAS; a bin that misses takes the line over and flushes the
+// previous bin's count with one global add, so a bin that is hot in the block
+// (every entry a batch created was last used `now`) stays in LDS instead of
+// serialising the device on one global address when a cold bin happened to
+// claim its line first.
+// The same pass writes the GC sweep's cluster-start bits (k_gc_starts' rule: a
+// non-EMPTY slot after an EMPTY one) from the state bytes it reads anyway, so
+// the eviction sweep reads the slot array twice instead of three times.  A
+// wave covers 64 consecutive slots (two bit words); lane 0 also reads the state
+// of the slot before them.
+#define GF_LRU_LDS 2048u
+// Each thread takes GF_LRU_U slots per trip (BLOCK apart, so a wave still
+// covers 64 consecutive slots) and issues all their loads before using any:
+// the state byte and, for maps whose hot value sits in the slot, the lifetime
+// and flags words of the same line (read whether or not the slot is FULL).
+#define GF_LRU_U 4
+__global__ __launch_bounds__(BLOCK) void k_lru_hist(gf_htab_desc d, uint32_t lt_off, uint32_t now, LruDev *L,
+                                                    uint32_t *bits) {
     if (!L->flag) return;
-    __shared__ uint32_t tag[GF_LRU_LDS], cnt[GF_LRU_LDS];
-    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) { tag[k] = ~0u; cnt[k] = 0; }
+    __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
     __syncthreads();
-    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * BLOCK * GF_LRU_U, nw = (ns + 31) / 32;
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < ns; b0 += stride) {   // wave-uniform trips
-        const uint64_t i = b0 + threadIdx.x;
-        uint32_t key = ~0u;
-        if (i < ns && d.slots[i * d.slot_size + d.ksz] == GF_SLOT_FULL) {
-            const uint8_t *v = ht_val(d, i) + lt_off;
-            key = lru_key(*reinterpret_cast<const uint32_t *>(v), *reinterpret_cast<const uint16_t *>(v + 4), now);
-        }
-        uint64_t rem = __ballot(key != ~0u);
-        while (rem) {
-            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
-            const uint32_t k = __shfl(key, (int)lead);
-            const uint64_t m = __ballot(key == k) & rem;
-            if (lane == lead) {
-                const uint32_t n = (uint32_t)__popcll(m), h = k & (GF_LRU_LDS - 1u);
-                uint32_t t = atomicCAS(&tag[h], ~0u, k);
-                if (t == ~0u || t == k) atomicAdd(&cnt[h], n);
-                else atomicAdd(&L->hist[k], n);
+    const bool inl = d.vin != 0;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * BLOCK * GF_LRU_U; b0 < ns; b0 += stride) {   // wave-uniform trips
+        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U];
+#pragma unroll
+        for (int u = 0; u < GF_LRU_U; u++) {
+            const uint64_t i = b0 + (uint64_t)u * BLOCK + threadIdx.x;
+            st[u] = i < ns ? d.slots[i * d.slot_size + d.ksz] : (uint32_t)GF_SLOT_EMPTY;
+            lt[u] = fl[u] = 0;
+            if (inl && i < ns) {
+                const uint8_t *v = ht_val(d, i) + lt_off;
+                lt[u] = *reinterpret_cast<const uint32_t *>(v);
+                fl[u] = *reinterpret_cast<const uint16_t *>(v + 4);
             }
-            rem &= ~m;
+        }
+#pragma unroll
+        for (int u = 0; u < GF_LRU_U; u++) {
+            const uint64_t i = b0 + (uint64_t)u * BLOCK + threadIdx.x;
+            uint32_t key = ~0u;
+            if (st[u] == GF_SLOT_FULL) {
+                if (!inl) {
+                    const uint8_t *v = ht_val(d, i) + lt_off;
+                    lt[u] = *reinterpret_cast<const uint32_t *>(v);
+                    fl[u] = *reinterpret_cast<const uint16_t *>(v + 4);
+                }
+                key = lru_key(lt[u], fl[u], now);
+            }
+            {
+                const uint64_t w0 = i - lane;             // the wave's first slot
+                uint32_t pv = 0;
+                if (lane == 0 && w0 < ns) pv = d.slots[((w0 - 1) & d.mask) * d.slot_size + d.ksz] != GF_SLOT_EMPTY;
+                pv = __shfl(pv, 0);
+                const uint64_t ne = __ballot(st[u] != GF_SLOT_EMPTY);
+                const uint64_t starts = ne & ~((ne << 1) | (uint64_t)pv);
+                const uint64_t wd = w0 / 32 + lane;
+                if (lane < 2 && w0 < ns && wd < nw) bits[wd] = (uint32_t)(starts >> (32 * lane));
+            }
+            uint64_t rem = __ballot(key != ~0u);
+            while (rem) {
+                const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
+                const uint32_t k = __shfl(key, (int)lead);
+                const uint64_t m = __ballot(key == k) & rem;
+                if (lane == lead) {
+                    const uint32_t n = (uint32_t)__popcll(m), h = (k ^ (k >> 11)) & (GF_LRU_LDS - 1u);
+                    unsigned long long cur = line[h];
+                    for (;;) {
+                        const uint32_t ck = (uint32_t)(cur >> 32);
+                        const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
+                        const unsigned long long seen = atomicCAS(&line[h], cur, want);
+                        if (seen == cur) {
+                            if (ck != k && ck != ~0u && (uint32_t)cur) atomicAdd(&L->hist[ck], (uint32_t)cur);
+                            break;
+                        }
+                        cur = seen;
+                    }
+                }
+                rem &= ~m;
+            }
         }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x)
-        if (tag[k] != ~0u && cnt[k]) atomicAdd(&L->hist[tag[k]], cnt[k]);
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
+        const unsigned long long v = line[k];
+        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) atomicAdd(&L->hist[(uint32_t)(v >> 32)], (uint32_t)v);
+    }
 }
 // The smallest prefix of the age order whose removal leaves <= target entries:
 // one block scans the 2 x 65536 bins (128 per thread, then a block scan).
@@ -2066,32 +2213,141 @@ __global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L
 // (per-block counts, an exclusive scan, then a block-local scan for the slots).
 struct EvSrc {
     const uint8_t *recs;      // per-packet verdict records
-    uint32_t stride, act_off; // record stride, offset of action (reason follows)
-    int32_t stage_off;        // pipeline: offset of the stage byte (-1: ingress records)
+    uint32_t stride, act_off; // record stride, offset of action (reason, ct_ret, flags follow)
+    int32_t stage_off;        // pipeline / egress: offset of the stage byte (-1: ingress records)
     const gf_rec *prec;       // handle_policy inputs (src_identity, ifindex, program slot)
     const gf_lxc_dev *cfgs;   // endpoint programs (LXC_ID, SECLABEL)
     const uint32_t *len, *flow_hash;
     const uint8_t *snap;      // frames to capture from (may be null)
     uint32_t snap_stride, n;
+    // trace notifications (trace.h:59-106); trace == 0: drop records only
+    uint32_t trace, kind;     // kind: 0 ingress, 1 pipeline, 2 egress
+    const uint8_t *tmark;     // GF_TR_* per packet
+    const uint8_t *tcap_px;   // TO_PROXY captures (GF_TR_CAPTURED)
+    const uint8_t *tcap_in;   // pipeline: TRACE_FROM_STACK captures
+    const uint8_t *orig;      // egress: the frames as sent (TRACE_FROM_LXC), snap_stride apart
+    const uint16_t *lxc_id, *slot_of;   // egress: the sender's program
+    uint32_t host_ifindex, encap_ifindex, nd_trace, nd_ifindex;
 };
-__device__ __forceinline__ bool ev_dropped(const EvSrc &E, uint32_t i) {
+// One notification: the 8 header words of struct drop_notify / trace_notify and
+// where its captured bytes come from.
+struct EvOne {
+    uint32_t w[8];
+    const uint8_t *pay;       // frame bytes (null: zeros)
+    uint32_t pstride;         // bytes present at pay
+};
+__device__ __forceinline__ EvOne ev_trace(uint32_t obs, uint32_t source, uint32_t hash, uint32_t len, uint32_t src,
+                                          uint32_t dst, uint32_t dst_id, uint32_t ifindex, uint32_t reason,
+                                          const uint8_t *pay, uint32_t pstride) {
+    EvOne e;
+    const uint32_t cap = len < GF_TRACE_PAYLOAD_LEN ? len : GF_TRACE_PAYLOAD_LEN;
+    e.w[0] = 4u /* CILIUM_NOTIFY_TRACE */ | (obs << 8) | ((source & 0xffffu) << 16);
+    e.w[1] = hash; e.w[2] = len; e.w[3] = cap; e.w[4] = src; e.w[5] = dst;
+    e.w[6] = (dst_id & 0xffffu) | ((reason & 0xffu) << 16);
+    e.w[7] = ifindex;
+    e.pay = pay; e.pstride = pstride;
+    return e;
+}
+enum { TR_TO_LXC = 0, TR_TO_PROXY = 1, TR_TO_HOST = 2, TR_TO_STACK = 3, TR_TO_OVERLAY = 4, TR_FROM_LXC = 5,
+       TR_FROM_STACK = 8 };
+// The notifications of packet i in the order the programs send them (k < 0:
+// just count them).  Drops: send_drop_notify / __send_drop_notify (drop.h:47-107)
+// after handle_policy (src_label, SECLABEL, LXC_ID, ifindex), the sender's
+// (SECLABEL, 0, 0, 0) after the from-container program, zeros for the callers'
+// send_drop_notify_error.  Traces: from_netdev's TRACE_FROM_STACK
+// (bpf_netdev.c:436), handle_ingress's TRACE_FROM_LXC (bpf_lxc.c:705), the
+// redirects' TRACE_TO_PROXY (lxc.h:116/168), TO_HOST / TO_STACK / TO_OVERLAY
+// of the from-container exits (bpf_lxc.c:364,381,650,669, encap.h:67) and
+// handle_policy's TRACE_TO_LXC when it did not redirect (bpf_lxc.c:1013-1016).
+__device__ uint32_t ev_list(const EvSrc &E, uint32_t i, int k, EvOne &out) {
     const uint8_t *r = E.recs + (size_t)i * E.stride;
-    return r[E.act_off] == TC_SHOT && (E.stage_off < 0 || r[E.stage_off] != GF_STAGE_XDP);
+    const uint32_t act = r[E.act_off], reason = r[E.act_off + 1], ct_ret = r[E.act_off + 2], ofl = r[E.act_off + 3];
+    const uint32_t stage = E.stage_off < 0 ? (uint32_t)GF_STAGE_POLICY : r[E.stage_off];
+    const uint32_t len = E.len[i], hash = E.flow_hash ? E.flow_hash[i] : 0u;
+    const uint8_t *fin = E.snap ? E.snap + (size_t)i * E.snap_stride : nullptr;
+    const uint32_t mark = E.tmark ? E.tmark[i] : 0u;
+    const uint8_t *pxc = (mark & GF_TR_CAPTURED) ? E.tcap_px + (size_t)i * GF_TRACE_PAYLOAD_LEN : fin;
+    const uint32_t pxs = (mark & GF_TR_CAPTURED) ? GF_TRACE_PAYLOAD_LEN : E.snap_stride;
+    uint32_t n = 0;
+    auto put = [&](const EvOne &e) { if ((int)n == k) out = e; n++; };
+    if (E.trace) {
+        if (E.kind == 1 && E.nd_trace && (stage == GF_STAGE_NETDEV || stage == GF_STAGE_POLICY))
+            put(ev_trace(TR_FROM_STACK, 0, hash, len, 0, 0, 0, E.nd_ifindex, 0,
+                         E.tcap_in + (size_t)i * GF_TRACE_PAYLOAD_LEN, GF_TRACE_PAYLOAD_LEN));
+        if (E.kind == 2) {
+            const uint32_t sl = E.slot_of[E.lxc_id ? E.lxc_id[i] : 0];
+            const gf_lxc_dev *sc = sl ? E.cfgs + (sl - 1) : nullptr;
+            if (sc && (gload<uint32_t>(&sc->flags) & GF_LXC_F_TRACE_NOTIFY)) {
+                const uint32_t lid = gload<uint32_t>(&sc->lxc_id), sec = gload<uint32_t>(&sc->seclabel);
+                const uint32_t fwd = r[5];                 // gf_egress_out.eg_ct_ret
+                const uint32_t ef = *reinterpret_cast<const uint16_t *>(r + 14);
+                put(ev_trace(TR_FROM_LXC, lid, hash, len, sec, 0, 0, 0, 0, E.orig + (size_t)i * E.snap_stride,
+                             E.snap_stride));
+                if (mark & GF_TR_PX_EGRESS)
+                    put(ev_trace(TR_TO_PROXY, lid, hash, len, sec, 0, 0, E.host_ifindex, fwd, pxc, pxs));
+                if (stage == GF_STAGE_FROM_LXC && act != TC_SHOT) {
+                    if (ef & GF_EG_F_TO_HOST)
+                        put(ev_trace(TR_TO_HOST, lid, hash, len, sec, 1u /* HOST_ID */, 0, E.host_ifindex, fwd, fin,
+                                     E.snap_stride));
+                    else if (ef & GF_EG_F_TO_STACK)
+                        put(ev_trace(TR_TO_STACK, lid, hash, len, sec, (mark & GF_TR_CLUSTER) ? 3u : 2u, 0, 0, fwd, fin,
+                                     E.snap_stride));
+                    else if (ef & GF_EG_F_ENCAP)
+                        put(ev_trace(TR_TO_OVERLAY, lid, hash, len, sec, 0, 0, E.encap_ifindex, 0, fin, E.snap_stride));
+                }
+            }
+        }
+        if (stage == GF_STAGE_POLICY) {                    // handle_policy of the destination
+            const gf_rec pr = E.prec[i];
+            const gf_lxc_dev *dc = pr.ep ? E.cfgs + (pr.ep - 1) : nullptr;
+            if (dc && (gload<uint32_t>(&dc->flags) & GF_LXC_F_TRACE_NOTIFY)) {
+                const uint32_t lid = gload<uint32_t>(&dc->lxc_id), sec = gload<uint32_t>(&dc->seclabel);
+                if (mark & GF_TR_PX_POLICY)
+                    put(ev_trace(TR_TO_PROXY, lid, hash, len, sec, 0, 0, E.host_ifindex, ct_ret, pxc, pxs));
+                if (act != TC_SHOT && !((ofl & GF_INGRESS_F_PROXY) && pr.ifindex != E.host_ifindex))
+                    put(ev_trace(TR_TO_LXC, lid, hash, len, pr.src_identity, sec, lid, pr.ifindex, ct_ret, fin,
+                                 E.snap_stride));
+            }
+        }
+    }
+    if (act == TC_SHOT && stage != GF_STAGE_XDP && (int)n == k) {
+        uint32_t src = 0, dst = 0, dst_id = 0, ifx = 0, source = 0;
+        if (stage == GF_STAGE_FROM_LXC) {
+            const gf_rec pr = E.prec[i];                // send_drop_notify(skb, SECLABEL, 0, 0, 0, ret) of the sender
+            if (pr.ep) { const gf_lxc_dev &cf = E.cfgs[pr.ep - 1]; src = cf.seclabel & 0xffffu; source = cf.lxc_id & 0xffffu; }
+        } else if (stage == GF_STAGE_POLICY) {
+            const gf_rec pr = E.prec[i];
+            if (pr.ep) {                                // handle_policy: send_drop_notify(src_label, SECLABEL, LXC_ID, ifindex)
+                const gf_lxc_dev &cf = E.cfgs[pr.ep - 1];
+                src = pr.src_identity & 0xffffu; dst = cf.seclabel & 0xffffu;
+                dst_id = cf.lxc_id; ifx = pr.ifindex; source = cf.lxc_id & 0xffffu;
+            }                                           // else the caller's send_drop_notify_error: zeros
+        }
+        out.w[0] = 1u /* CILIUM_NOTIFY_DROP */ | (reason << 8) | (source << 16);
+        out.w[1] = hash;
+        out.w[2] = len; out.w[3] = len < GF_TRACE_PAYLOAD_LEN ? len : GF_TRACE_PAYLOAD_LEN;
+        out.w[4] = src; out.w[5] = dst; out.w[6] = dst_id; out.w[7] = ifx;
+        out.pay = fin; out.pstride = E.snap_stride;
+    }
+    if (act == TC_SHOT && stage != GF_STAGE_XDP) n++;
+    return n;
 }
 __global__ __launch_bounds__(BLOCK) void k_ev_count(EvSrc E, uint32_t *blk) {
     __shared__ uint32_t c;
     if (threadIdx.x == 0) c = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < E.n && ev_dropped(E, i)) atomicAdd(&c, 1u);
+    EvOne e;
+    if (i < E.n) { const uint32_t m = ev_list(E, i, -1, e); if (m) atomicAdd(&c, m); }
     __syncthreads();
     if (threadIdx.x == 0) blk[blockIdx.x] = c;
 }
 __global__ __launch_bounds__(BLOCK) void k_ev_write(EvSrc E, const uint32_t *boff, gf_event_ring R) {
     __shared__ uint32_t sc[BLOCK];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    const bool d = i < E.n && ev_dropped(E, i);
-    sc[threadIdx.x] = d ? 1u : 0u;
+    EvOne e;
+    const uint32_t m = i < E.n ? ev_list(E, i, -1, e) : 0u;
+    sc[threadIdx.x] = m;
     __syncthreads();
     for (uint32_t o = 1; o < BLOCK; o <<= 1) {          // inclusive scan
         uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
@@ -2099,38 +2355,21 @@ __global__ __launch_bounds__(BLOCK) void k_ev_write(EvSrc E, const uint32_t *bof
         sc[threadIdx.x] += v;
         __syncthreads();
     }
-    if (!d) return;
-    const uint64_t pos = (uint64_t)*R.count + boff[blockIdx.x] + sc[threadIdx.x] - 1;
-    if (pos >= R.capacity) return;                      // ring full: the record is lost
-    const uint8_t *r = E.recs + (size_t)i * E.stride;
-    const uint32_t reason = r[E.act_off + 1];
-    uint32_t src = 0, dst = 0, dst_id = 0, ifx = 0, source = 0;
-    const bool policy = E.stage_off < 0 || r[E.stage_off] == GF_STAGE_POLICY;
-    if (E.stage_off >= 0 && r[E.stage_off] == GF_STAGE_FROM_LXC) {
-        const gf_rec pr = E.prec[i];                    // send_drop_notify(skb, SECLABEL, 0, 0, 0, ret) of the sender
-        if (pr.ep) { const gf_lxc_dev &cf = E.cfgs[pr.ep - 1]; src = cf.seclabel & 0xffffu; source = cf.lxc_id & 0xffffu; }
-    } else if (policy) {
-        const gf_rec pr = E.prec[i];
-        if (pr.ep) {                                    // handle_policy: send_drop_notify(src_label, SECLABEL, LXC_ID, ifindex)
-            const gf_lxc_dev &cf = E.cfgs[pr.ep - 1];
-            src = pr.src_identity & 0xffffu; dst = cf.seclabel & 0xffffu;
-            dst_id = cf.lxc_id; ifx = pr.ifindex; source = cf.lxc_id & 0xffffu;
-        }                                               // else the caller's send_drop_notify_error: zeros
-    }
-    const uint32_t len = E.len[i];
-    const uint32_t cap = len < GF_TRACE_PAYLOAD_LEN ? len : GF_TRACE_PAYLOAD_LEN;
-    uint32_t *w = reinterpret_cast<uint32_t *>(R.records + pos * GF_EVENT_RECORD);
-    w[0] = 1u /* CILIUM_NOTIFY_DROP */ | (reason << 8) | (source << 16);
-    w[1] = E.flow_hash ? E.flow_hash[i] : 0u;             // get_hash_recalc(skb)
-    w[2] = len; w[3] = cap; w[4] = src; w[5] = dst; w[6] = dst_id; w[7] = ifx;
-    const uint8_t *f = E.snap ? E.snap + (size_t)i * E.snap_stride : nullptr;
-    for (uint32_t k = 0; k < GF_TRACE_PAYLOAD_LEN / 4; k++) {
-        uint32_t v = 0;
-        for (uint32_t b = 0; b < 4; b++) {
-            const uint32_t off = 4 * k + b;
-            if (f && off < cap && off < E.snap_stride) v |= (uint32_t)f[off] << (8 * b);
+    for (uint32_t k = 0; k < m; k++) {
+        const uint64_t pos = (uint64_t)*R.count + boff[blockIdx.x] + sc[threadIdx.x] - m + k;
+        if (pos >= R.capacity) return;                  // ring full: the record is lost
+        ev_list(E, i, (int)k, e);
+        uint32_t *w = reinterpret_cast<uint32_t *>(R.records + pos * GF_EVENT_RECORD);
+        for (int q = 0; q < 8; q++) w[q] = e.w[q];
+        const uint32_t cap = e.w[3];
+        for (uint32_t q = 0; q < GF_TRACE_PAYLOAD_LEN / 4; q++) {
+            uint32_t v = 0;
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint32_t off = 4 * q + b;
+                if (e.pay && off < cap && off < e.pstride) v |= (uint32_t)e.pay[off] << (8 * b);
+            }
+            w[8 + q] = v;
         }
-        w[8 + k] = v;
     }
 }
 __global__ void k_ev_commit(const uint32_t *boff, const uint32_t *blk, uint32_t nb, gf_event_ring R) {
@@ -2953,6 +3192,7 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf
     }
     o.eg_ct_ret = (uint8_t)ret;
     const uint32_t dst_id = ((r.orig_dip & E.cluster_mask) == E.cluster_range) ? 3u : 2u;   // CLUSTER_ID / WORLD_ID
+    if (E.X.tmark && dst_id == 3u) E.X.tmark[i] |= GF_TR_CLUSTER;
     const int verdict = eg_policy(c, flags, dst_id, &t[1], false, t[2] & 0xffffu, nh, len, ab);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
@@ -3028,6 +3268,9 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf
     }
     uint32_t nm[2] = {gload<uint32_t>(&c->node_mac[0]), gload<uint32_t>(&c->node_mac[1])};
     if (verdict > 0) {                                  // ipv4_redirect_to_host_port + ipv4_l3 -> HOST_IFINDEX
+        if (E.X.tmark)
+            trace_proxy(E.X.tmark, E.X.tcap, E.snap + (size_t)i * E.stride, w.p, w.cap, trace_cap_len(len, E.stride), i,
+                        GF_TR_PX_EGRESS);
         const int r3 = redirect_checks(len, l4_off, nh);
         if (r3 < 0) return r3;
         const uint32_t od[1] = {r.orig_dip};
@@ -3151,6 +3394,7 @@ __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint3
     }
     o.eg_ct_ret = (uint8_t)ret;
     const uint32_t dst_id = (w.r32(38) == E.router6[0] && w.r32(42) == E.router6[1]) ? 3u : 2u;
+    if (E.X.tmark && dst_id == 3u) E.X.tmark[i] |= GF_TR_CLUSTER;
     const int verdict = eg_policy(c, flags, dst_id, &t[4], true, t[8] & 0xffffu, nh, len, ab);
     const bool strict = (E.strict & 2) != 0;
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
@@ -3206,6 +3450,8 @@ __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint3
     }
     uint32_t nm[2] = {gload<uint32_t>(&c->node_mac[0]), gload<uint32_t>(&c->node_mac[1])};
     if (verdict > 0) {                                  // ipv6_redirect_to_host_port + ipv6_l3 -> HOST_IFINDEX
+        if (E.X.tmark)
+            trace_proxy(E.X.tmark, E.X.tcap, w.p, nullptr, 0, trace_cap_len(len, E.stride), i, GF_TR_PX_EGRESS);
         const int r3 = redirect_checks(len, l4_off, nh);
         if (r3 < 0) return r3;
         const uint32_t np = (uint32_t)verdict & 0xffffu;
@@ -3744,7 +3990,34 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 
 // handle_policy over a batch (caller holds prog_lock and the maps' locks, and checked the columns).
 // skip (DEVICE, may be null): packets a pipeline ended before the tail call.
-// Drop notifications of one classify call (no-op without an event ring).
+// Trace notifications of a call: per-packet marks and captures (GF_TR_*),
+// allocated and the marks cleared by the caller before its first kernel.
+struct TraceWs { DevBuf mark, px, in; };
+static TraceWs &trace_ws() { static TraceWs t; return t; }
+struct TraceArgs {                 // the pipeline / egress callers' part of the event pass
+    uint32_t kind;                 // 1 pipeline, 2 egress
+    bool on;                       // this call traces (a ring is set and a program / the netdev traces)
+    uint32_t nd_trace, nd_ifindex; // pipeline: GF_NETDEV_F_TRACE_NOTIFY, skb->ingress_ifindex
+    const uint8_t *orig;           // egress: the frames as sent
+    const uint16_t *lxc_id;        // egress: the senders
+};
+static bool array_traces(const std::shared_ptr<PolicyArray> &a) {
+    if (!a) return false;
+    for (auto &kv : a->slots)
+        if (kv.second->cfg.flags & GF_LXC_F_TRACE_NOTIFY) return true;
+    return false;
+}
+static int trace_prepare(uint32_t n, bool with_in, hipStream_t s) {
+    TraceWs &t = trace_ws();
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    int r;
+    if ((r = grow(t.mark, (size_t)n + 16)) || (r = grow(t.px, (size_t)n * GF_TRACE_PAYLOAD_LEN)) ||
+        (with_in && (r = grow(t.in, (size_t)n * GF_TRACE_PAYLOAD_LEN))))
+        return r;
+    return hip_ok(hipMemsetAsync(t.mark.p, 0, n, s), "trace marks");
+}
+
+// Drop (and trace) notifications of one classify call (no-op without an event ring).
 static int emit_drop_events(EvSrc E, hipStream_t s) {
     gf_event_ring R = event_ring();
     if (!R.records || !R.count || !R.capacity || E.n == 0) return 0;
@@ -4022,12 +4295,14 @@ static int ct_sweep_bufs(Map &m, LruDev *&L, uint32_t *&bits) {
     bits = (uint32_t *)m.d_gcbits.p;
     return 0;
 }
-static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
+// starts_done: the cluster-start bits were written by k_lru_hist.
+static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s, bool starts_done = false) {
     const gf_htab_desc d = m.hdesc();
     const uint32_t lt_off = m.ht.codec == GF_VCODEC_CT ? 0u : 32u;
     const uint64_t nw = (d.mask + 1 + 31) / 32;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, 65535u * 8);
-    hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, bits, (const GcCut *)&L->cut);
+    if (!starts_done)
+        hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, bits, (const GcCut *)&L->cut);
     hipLaunchKernelGGL(k_gc_clusters, dim3(grid), dim3(BLOCK), 0, s, d, m.ht.mode, lt_off, (const GcCut *)&L->cut,
                        (const uint32_t *)bits, L->res);
 }
@@ -4045,10 +4320,11 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
     ProfScope ps("k_lru_evict", s);
     hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, (const uint32_t *)d.count, m->max_entries, L);
-    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + BLOCK - 1) / BLOCK, resident_blocks(4));
-    hipLaunchKernelGGL(k_lru_hist, dim3(gh), dim3(BLOCK), 0, s, d, lt_off, now, L);
+    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + BLOCK * GF_LRU_U - 1) / (BLOCK * GF_LRU_U),
+                                                     resident_blocks(8));
+    hipLaunchKernelGGL(k_lru_hist, dim3(gh), dim3(BLOCK), 0, s, d, lt_off, now, L, bits);
     hipLaunchKernelGGL(k_lru_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, now, L);
-    ct_sweep_launch(*m, L, bits, s);
+    ct_sweep_launch(*m, L, bits, s, true);
     hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
     return hip_ok(hipGetLastError(), "k_lru_evict");
 }
@@ -4059,8 +4335,13 @@ using PackFn = std::function<int(const uint16_t *slot_of, gf_rec *rec, uint32_t 
 static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols *pkts, uint32_t now_sec,
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
                        const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
-                       uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false, bool prepared = false) {
+                       uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false, bool prepared = false,
+                       const TraceArgs *ta = nullptr) {
     int r;
+    // trace notifications: the plain ingress call decides here, the pipeline and
+    // egress callers (whose earlier kernels mark packets) pass their decision
+    const bool tracing = ta ? ta->on : (event_ring().records && array_traces(a));
+    if (tracing && !ta && (r = trace_prepare(pkts->n, false, s))) return r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
     if ((r = prog_table(a, s, progs))) return r;
@@ -4113,6 +4394,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     const gf_node_cfg &node = node_cfg();
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
+    if (tracing) { X.tmark = (uint8_t *)trace_ws().mark.p; X.tcap = (uint8_t *)trace_ws().px.p; }
     if ((r = px_log_begin(n, s, X, px_keep))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
@@ -4146,6 +4428,18 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         E.prec = (const gf_rec *)w.rec.p; E.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
         E.len = ev_len ? ev_len : pkts->len; E.flow_hash = pkts->flow_hash; E.n = n;
         E.snap = ev_snap; E.snap_stride = ev_stride;
+        if (tracing) {
+            const TraceWs &t = trace_ws();
+            E.trace = 1; E.kind = ta ? ta->kind : 0u;
+            E.tmark = (const uint8_t *)t.mark.p; E.tcap_px = (const uint8_t *)t.px.p;
+            E.tcap_in = (const uint8_t *)t.in.p;
+            E.host_ifindex = host_ifindex(); E.encap_ifindex = node.encap_ifindex;
+            if (ta) {
+                E.nd_trace = ta->nd_trace; E.nd_ifindex = ta->nd_ifindex;
+                E.orig = ta->orig; E.lxc_id = ta->lxc_id;
+                E.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
+            }
+        }
         if ((r = emit_drop_events(E, s))) return r;
     }
     for (auto &p : progs) {
@@ -4339,6 +4633,13 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     if ((r = grow(w.s6, (size_t)n * 16)) || (r = grow(w.d6, (size_t)n * 16))) return r;
     P.vec_copy = (fr.snap_stride % 16 == 0) && (((uintptr_t)fr.snap | (uintptr_t)snap_out) & 15u) == 0;
+    TraceArgs ta{};
+    ta.kind = 1;
+    ta.nd_trace = (p->cfg.netdev.flags & GF_NETDEV_F_TRACE_NOTIFY) ? 1u : 0u;
+    ta.nd_ifindex = p->cfg.netdev.ingress_ifindex;
+    ta.on = event_ring().records && (ta.nd_trace || array_traces(p->policy));
+    if (ta.on && (r = trace_prepare(n, ta.nd_trace != 0, s))) return r;
+    if (ta.on && ta.nd_trace) P.tcap_in = (uint8_t *)trace_ws().in.p;
     unsigned long long *sink = (unsigned long long *)stats_sink();
     const uint32_t grid = (n + nt - 1) / nt;         // one NT-frame tile per block
     gf_pkt_cols c2{};
@@ -4356,7 +4657,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     };
     c2.flow_hash = b->flow_hash;
     return ingress_run(p->policy, &c2, now_sec, nullptr, s, front, (uint8_t *)out, fr.len,
-                       snap_out ? snap_out : fr.snap, fr.snap_stride, snap_out);
+                       snap_out ? snap_out : fr.snap, fr.snap_stride, snap_out, true, false, false, &ta);
 }
 
 // ---- ingest re-partition ----
@@ -4826,8 +5127,14 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
                   (r = grow(ew.hzak, (size_t)(amask + 1) * 8)) || (r = grow(ew.hzaf, (size_t)(amask + 1) * 8))))
         return r;
     // In place (snap_out == the frames) with the check: the flagged pass must leave
-    // the frames as they came, so the rewrites go to scratch and are copied at the end.
-    const bool inplace = check && snap_out == fr.snap;
+    // the frames as they came, so the rewrites go to scratch and are copied at the end
+    // (also when tracing: TRACE_FROM_LXC captures the frames as sent).
+    TraceArgs ta{};
+    ta.kind = 2;
+    ta.on = event_ring().records && array_traces(a);
+    ta.orig = fr.snap; ta.lxc_id = b->lxc_id;
+    if (ta.on && (r = trace_prepare(n, false, s))) return r;
+    const bool inplace = (check || ta.on) && snap_out == fr.snap;
     uint8_t *wsnap = inplace ? nullptr : snap_out;
     if (!wsnap) {
         if ((r = grow(ew.snap, (size_t)n * S))) return r;
@@ -4859,6 +5166,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     }
     E.X.snap = nullptr; E.X.snap_stride = S; E.X.now = now_sec; E.X.gw = node.ipv4_gateway;   // writes: k_eg_groups
     memcpy(E.X.host6, node.host_ip6, 16);
+    if (ta.on) { E.X.tmark = (uint8_t *)trace_ws().mark.p; E.X.tcap = (uint8_t *)trace_ws().px.p; }
     if ((r = px_log_begin(n, s, E.X))) return r;
     if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 12, s), "eg seq") || hip_ok(hipMemsetAsync(d_hz + 2, 0xff, 4, s), "eg hz") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
         return -EIO;
@@ -4968,7 +5276,9 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             return -EIO;
         return 0;
     };
-    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru, true))) return r;
+    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru, true, false,
+                         &ta)))
+        return r;
     if (inplace && hip_ok(hipMemcpyAsync(snap_out, wsnap, (size_t)n * S, hipMemcpyDeviceToDevice, s), "snap copy"))
         return -EIO;
     return 0;

@@ -197,7 +197,7 @@ class Datapath:
         if sc.netdev and self.policy_array:
             nd = sc.netdev
             ncfg = gf_netdev_cfg(h(nd["lxc_map"]), nd.get("flags", 0), nd.get("fixed_secctx", 0),
-                                 (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
+                                 (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))), nd.get("ingress_ifindex", 0))
             pcfg = gf_pipeline_cfg(self.xdp_prog or 0, self.lb_prog or 0, ncfg, self.policy_array)
             self.pipe = _check(lib.gf_pipeline_load(C.byref(pcfg)), "gf_pipeline_load")
 

@@ -1099,6 +1099,8 @@ def ct6_prefill(meta, reply_keys, reply_vals, now, seed=0xC1D40055):
 
 # ------------------------------------------------------------------ endpoint egress (from-container)
 LXC_POLICY_EGRESS = 32
+LXC_TRACE_NOTIFY = 64          # TRACE_NOTIFY (pkg/endpoint/endpoint.go:131-134)
+NETDEV_TRACE_NOTIFY = 2
 
 
 def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=True):

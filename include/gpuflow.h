@@ -250,6 +250,8 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out,
 #define GF_LXC_F_LXC_IPV4        (1u << 4)  /* LXC_IPV4 */
 #define GF_LXC_F_POLICY_EGRESS   (1u << 5)  /* POLICY_EGRESS (pkg/endpoint/endpoint.go:153-156, emitted when egress
                                                is enforced, pkg/endpoint/policy.go:820-839) */
+#define GF_LXC_F_TRACE_NOTIFY    (1u << 6)  /* TRACE_NOTIFY (pkg/endpoint/endpoint.go:131-134, on by default:
+                                               daemon/main.go:629): send_trace_notify records, see below */
 #define GF_MAX_L4_INGRESS 64
 #define GF_MAX_PORTMAP 16
 typedef struct gf_portmap {    /* struct portmap (bpf/lib/common.h), LXC_PORT_MAPPINGS entries */
@@ -409,11 +411,13 @@ int gf_lxc_egress_classify(int policy_array, const gf_lxc_batch *batch, uint32_t
  * arriving on the netdev; it has no equivalent call in the reference (the
  * kernel chains the programs), see DESIGN.md. */
 #define GF_NETDEV_F_FIXED_SECCTX (1u << 0)  /* FIXED_SRC_SECCTX defined */
+#define GF_NETDEV_F_TRACE_NOTIFY (1u << 1)  /* TRACE_NOTIFY: TRACE_FROM_STACK at from_netdev (bpf_netdev.c:436) */
 typedef struct gf_netdev_cfg {
     int lxc_map;               /* cilium_lxc (endpoint_key 20 B -> endpoint_info 112 B) */
     uint32_t flags;            /* GF_NETDEV_F_* */
     uint32_t fixed_secctx;     /* FIXED_SRC_SECCTX */
     uint8_t  router_ip6[16];   /* ROUTER_IP (node_config.h), derive_sec_ctx() */
+    uint32_t ingress_ifindex;  /* skb->ingress_ifindex of the frames (the netdev's ifindex) */
 } gf_netdev_cfg;
 typedef struct gf_pipeline_cfg {
     int xdp_prog;              /* gf_xdp_prog_load handle, 0 = no XDP program attached */
@@ -509,6 +513,18 @@ int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max);
  * frame (the pipeline's frames; zeros for column batches, which carry none).
  * *count accumulates across calls; records past `capacity` are lost (a perf ring
  * overrun). */
+/* ---- trace notifications (bpf/lib/trace.h:59-106, TRACE_NOTIFY) ----
+ * Programs loaded with GF_LXC_F_TRACE_NOTIFY (and a pipeline whose netdev has
+ * GF_NETDEV_F_TRACE_NOTIFY) also append struct trace_notify records to the same
+ * ring (type CILIUM_NOTIFY_TRACE=4, subtype = observation point TRACE_TO_LXC 0,
+ * TO_PROXY 1, TO_HOST 2, TO_STACK 3, TO_OVERLAY 4, FROM_LXC 5, FROM_STACK 8;
+ * source = EVENT_SOURCE, hash, len_orig, len_cap, src_label, dst_label, dst_id
+ * (u16), reason (the CT result that forwarded it), pad, ifindex — the layout
+ * pkg/monitor/datapath_trace.go TraceNotify decodes), followed by the first
+ * len_cap bytes of the frame as it was at the call.  Per packet the records are
+ * in the order the programs send them (from_netdev / handle_ingress first, the
+ * drop record last), packets in batch order.  Call sites: bpf_lxc.c:364,381,
+ * 650,669,705,1014, lib/lxc.h:116,168, lib/encap.h:67, bpf_netdev.c:436. */
 #define GF_TRACE_PAYLOAD_LEN 128u   /* TRACE_PAYLOAD_LEN, bpf/lib/common.h:213-215 */
 #define GF_EVENT_RECORD 160u
 typedef struct gf_event_ring {

@@ -354,6 +354,7 @@ typedef struct skb {
     uint32_t cb[5];
     uint32_t tc_index, hash;
     uint16_t protocol;                        /* host order ethertype */
+    uint32_t idx;                             /* packet index in the batch (trace sink slot) */
 } skb_t;
 
 static inline uint8_t skb_byte(const skb_t *s, uint32_t off) { return off < s->cap ? s->data[off] : 0; }
@@ -455,6 +456,7 @@ static void skb_init(skb_t *s, const o_batch *b, uint32_t i) {
     s->protocol = s->len >= 14 ? (uint16_t)((s->data[12] << 8) | s->data[13]) : 0;
     if (b->tc_index) s->tc_index = b->tc_index[i];
     if (b->flow_hash) s->hash = b->flow_hash[i];
+    s->idx = i;
 }
 
 static void l4_bytes(const skb_t *s, int l4_off, uint32_t *w0, uint16_t *w3) {
@@ -1065,6 +1067,46 @@ static __thread o_node_cfg g_node = {1, NULL, NULL, 0, {0}, {0}, {0}, NULL, 0, 0
 #define g_host_ifindex (g_node.host_ifindex)
 void o_set_node(const o_node_cfg *node) { g_node = *node; }
 
+/* send_trace_notify (bpf/lib/trace.h:59-106, TRACE_NOTIFY): struct trace_notify
+ * (32 B: type CILIUM_NOTIFY_TRACE=4, subtype = observation point, source =
+ * EVENT_SOURCE, hash, len_orig, len_cap, src_label, dst_label, dst_id, reason,
+ * pad, ifindex) followed by the first len_cap (<= TRACE_PAYLOAD_LEN) bytes of
+ * the skb as it is at the call.  Events go to a per-packet list (the sink):
+ * packet i's events in emission order at ev + (i * per + k) * 160, the count in
+ * cnt[i]; the drop notification of a dropped packet is appended last by the
+ * batch drivers.  Per thread, like g_node (run_mt hands it to its workers). */
+#define O_EVENT_RECORD 160
+enum { TRACE_TO_LXC, TRACE_TO_PROXY, TRACE_TO_HOST, TRACE_TO_STACK, TRACE_TO_OVERLAY, TRACE_FROM_LXC,
+       TRACE_FROM_PROXY, TRACE_FROM_HOST, TRACE_FROM_STACK, TRACE_FROM_OVERLAY };
+#define LXC_F_TRACE_NOTIFY (1u << 6)
+#define NETDEV_F_TRACE_NOTIFY (1u << 1)
+typedef struct o_trace_sink { uint8_t *ev; uint8_t *cnt; uint32_t per; int capture; } o_trace_sink;
+static __thread o_trace_sink g_tr = {NULL, NULL, 0, 0};
+void o_set_trace_sink(uint8_t *ev, uint8_t *cnt, uint32_t per_pkt, int capture) {
+    g_tr.ev = ev; g_tr.cnt = cnt; g_tr.per = per_pkt; g_tr.capture = capture;
+}
+static uint8_t *ev_slot(uint32_t i) {
+    if (!g_tr.ev || g_tr.cnt[i] >= g_tr.per) return NULL;
+    return g_tr.ev + ((size_t)i * g_tr.per + g_tr.cnt[i]++) * O_EVENT_RECORD;
+}
+static void trace_event(const skb_t *s, uint8_t obs, uint16_t source, uint32_t src, uint32_t dst, uint16_t dst_id,
+                        uint32_t ifindex, uint8_t reason) {
+    uint8_t *ev = ev_slot(s->idx);
+    if (!ev) return;
+    memset(ev, 0, O_EVENT_RECORD);
+    uint32_t cap = s->len < 128 ? s->len : 128;          /* min(TRACE_PAYLOAD_LEN, skb->len) */
+    uint32_t f[4] = {s->len, cap, src, dst};
+    ev[0] = 4;                                           /* CILIUM_NOTIFY_TRACE */
+    ev[1] = obs;
+    memcpy(ev + 2, &source, 2);
+    memcpy(ev + 4, &s->hash, 4);                         /* get_hash_recalc(skb) */
+    memcpy(ev + 8, f, 16);
+    memcpy(ev + 24, &dst_id, 2);
+    ev[26] = reason;
+    memcpy(ev + 28, &ifindex, 4);
+    if (g_tr.capture) memcpy(ev + 32, s->data, cap < s->cap ? cap : s->cap);
+}
+
 /* ipv{4,6}_redirect_to_host_port writes (lib/lxc.h:96-205) once its checks
  * passed, and the cilium_proxy{4,6} entry it creates (logged, see proxy_apply) */
 static void redirect_write(const skb_t *s, pol_ctx *x, int l4_off, const uint8_t *t, int v6, uint16_t new_port,
@@ -1170,6 +1212,9 @@ static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
         *oflags |= 2;
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        /* ipv4_redirect_to_host_port: traced before its rewrites (lib/lxc.h:115-117) */
+        if (c->flags & LXC_F_TRACE_NOTIFY)
+            trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_host_ifindex, (uint8_t)*fwd);
         ret = redirect_to_host_port_checks(s, l4_off, t[12]);
         if (IS_ERR(ret)) return ret;
         redirect_write(s, x, l4_off, t, 0, (uint16_t)verdict, (const uint8_t *)&daddr, src_label, now);
@@ -1234,6 +1279,8 @@ static int ipv6_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fw
         *oflags |= 2;
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        if (c->flags & LXC_F_TRACE_NOTIFY)                 /* lib/lxc.h:167-169 */
+            trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_host_ifindex, (uint8_t)*fwd);
         ret = redirect_to_host_port_checks(s, l4_off, t[36]);
         if (IS_ERR(ret)) return ret;
         redirect_write(s, x, l4_off, t, 1, (uint16_t)verdict, orig_dip, src_label, now);
@@ -1253,7 +1300,7 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
         o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL);
         return;
     }
-    uint32_t src_label = s.cb[0];
+    uint32_t src_label = s.cb[0], entry_ifindex = s.cb[1];
     int fwd = 0, ret;
     uint8_t fl = 0;
     uint16_t proxy = 0;
@@ -1269,6 +1316,9 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
         return;
     }
     o->proxy_port = proxy;
+    if ((c->flags & LXC_F_TRACE_NOTIFY) && entry_ifindex == s.cb[1])   /* not redirected to host / proxy */
+        trace_event(&s, TRACE_TO_LXC, (uint16_t)c->lxc_id, src_label, c->seclabel, (uint16_t)c->lxc_id, entry_ifindex,
+                    (uint8_t)fwd);
     uint32_t ifindex = s.cb[1];
     o->ifindex_lo = (uint16_t)ifindex;
     o->action = ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
@@ -1311,6 +1361,7 @@ typedef struct mt_arg {
     const o_pipeline_cfg *pc; o_pipeline_out *po; uint8_t *snap_out, *skip_w;
     uint32_t *secctx, *ifx; uint16_t *lxcid;
     o_node_cfg node;                    /* the caller's node config (thread-local g_node) */
+    o_trace_sink tr;                    /* the caller's trace sink (thread-local g_tr) */
 } mt_arg;
 
 static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i, uint8_t *row, o_pipeline_out *o,
@@ -1318,7 +1369,6 @@ static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i
 
 /* send_drop_notify + __send_drop_notify, bpf/lib/drop.h:47-107: the 32-B struct
  * drop_notify followed by the first len_cap (<= TRACE_PAYLOAD_LEN) frame bytes. */
-#define O_EVENT_RECORD 160
 static void drop_event(uint8_t *ev, int reason, uint32_t source, uint32_t hash, uint32_t len, uint32_t src,
                        uint32_t dst, uint32_t dst_id, uint32_t ifindex, const uint8_t *frame, uint32_t frame_bytes) {
     memset(ev, 0, O_EVENT_RECORD);
@@ -1349,6 +1399,7 @@ static uint32_t pkt_group(const o_batch *b, uint32_t i) {
 static void *mt_worker(void *p) {
     mt_arg *m = (mt_arg *)p;
     g_node = m->node;
+    g_tr = m->tr;
     const o_batch *b = m->b;
     uint32_t T = m->nthreads, t = m->tid;
     uint32_t lo = (uint32_t)((uint64_t)b->n * t / T), hi = (uint32_t)((uint64_t)b->n * (t + 1) / T);
@@ -1388,6 +1439,7 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
     pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
     mt_arg *args = (mt_arg *)calloc(threads, sizeof(mt_arg));
     tmpl->node = g_node;
+    tmpl->tr = g_tr;
     for (uint32_t t = 0; t < threads; t++) {
         args[t] = *tmpl; args[t].tid = t; args[t].nthreads = threads;
         pthread_create(&th[t], NULL, mt_worker, &args[t]);
@@ -1672,6 +1724,8 @@ static void pipeline_front(const o_pipeline_cfg *c, const o_batch *b, uint32_t i
     }
     nd_res nr; memset(&nr, 0, sizeof nr);
     int ret;
+    if (c->netdev->flags & NETDEV_F_TRACE_NOTIFY)           /* from_netdev, bpf_netdev.c:436 */
+        trace_event(&s, TRACE_FROM_STACK, 0, 0, 0, 0, c->netdev->ingress_ifindex, 0);
     if (s.protocol == 0x86DD) ret = netdev_ipv6(c->netdev, &s, row, &nr);
     else if (s.protocol == 0x0800) ret = netdev_ipv4(c->netdev, &s, row, &nr);   /* tail_handle_ipv4 */
     else ret = TC_ACT_OK;
@@ -1705,7 +1759,7 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
     if (c->policy) {
         /* handle_policy over the rewritten frames, flow groups of the rewritten addresses */
         o_batch b2 = *b;
-        b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+        b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = b->flow_hash;   /* the skb's hash (trace records) */
         uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
         if (threads == 1) {
             for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(c->policy, &b2, i, now, &ing[i], plog, snap);
@@ -1724,8 +1778,9 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
                 o->flags |= ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
             }
         }
-        if (!events) continue;
-        uint8_t *e = events + (size_t)i * O_EVENT_RECORD;
+        if (!events && !g_tr.ev) continue;
+        uint8_t tmp[O_EVENT_RECORD];
+        uint8_t *e = events ? events + (size_t)i * O_EVENT_RECORD : tmp;
         memset(e, 0, O_EVENT_RECORD);
         if (o->action != TC_ACT_SHOT || o->stage == 1) continue;
         const uint8_t *row = snap + (size_t)i * b->snap_stride;
@@ -1734,6 +1789,8 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
         if (lc) drop_event(e, o->reason, lc->lxc_id, hash, len, secctx[i], lc->seclabel, lc->lxc_id, ifx[i], row,
                            b->snap_stride);
         else drop_event(e, o->reason, 0, hash, len, 0, 0, 0, 0, row, b->snap_stride);
+        uint8_t *t = ev_slot(i);
+        if (t) memcpy(t, e, O_EVENT_RECORD);
     }
     if (!snap_out) free(snap);
     free(skip); free(secctx); free(ifx); free(lxcid); free(ing);
@@ -1840,8 +1897,9 @@ uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o) {
  * the packet's slot (ev: n * O_EVENT_RECORD, zero for the others).  Column
  * batches carry no frame bytes to capture. */
 void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_out *out, uint8_t *ev) {
+    uint8_t tmp[O_EVENT_RECORD];
     for (uint32_t i = 0; i < b->n; i++) {
-        uint8_t *e = ev + (size_t)i * O_EVENT_RECORD;
+        uint8_t *e = ev ? ev + (size_t)i * O_EVENT_RECORD : tmp;
         memset(e, 0, O_EVENT_RECORD);
         if (out[i].action != TC_ACT_SHOT) continue;
         uint32_t hash = b->flow_hash ? b->flow_hash[i] : 0, len = b->len[i];
@@ -1849,6 +1907,8 @@ void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_o
         if (c) drop_event(e, out[i].reason, c->lxc_id, hash, len, b->src_identity ? b->src_identity[i] : 0,
                           c->seclabel, c->lxc_id, b->ifindex ? b->ifindex[i] : 0, NULL, 0);
         else drop_event(e, out[i].reason, 0, hash, len, 0, 0, 0, 0, NULL, 0);   /* caller's send_drop_notify_error */
+        uint8_t *t = ev_slot(i);                         /* after the packet's traces */
+        if (t) memcpy(t, e, O_EVENT_RECORD);
     }
 }
 
@@ -1861,6 +1921,7 @@ void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_o
 #define DROP_NO_LXC -152
 #define DROP_POLICY_CIDR -162
 #define CLUSTER_ID 3u
+#define HOST_ID 1u
 #define EG_F_CREATED 0x0001
 #define EG_F_PROXY 0x0002
 #define EG_F_LB 0x0004
@@ -2065,7 +2126,9 @@ skip_service_lookup: ;
     default:
         return DROP_POLICY;
     }
+    const int tr = (c->flags & LXC_F_TRACE_NOTIFY) != 0;
     if (verdict > 0) {                                                   /* redirect_to_proxy */
+        if (tr) trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.host_ifindex, (uint8_t)fwd);
         ret = redirect_to_host_port_checks(s, l4_off, nh);
         if (IS_ERR(ret)) return ret;
         pol_ctx x = {w, plog};
@@ -2098,6 +2161,7 @@ skip_service_lookup: ;
         const uint8_t *tun = g_node.tunnel_map ? om_lookup_ptr(g_node.tunnel_map, k) : NULL;
         if (tun) {
             r->tunnel_ip = bswap32(ge32(tun, 0));                        /* bpf_htonl(tunnel->ip4) */
+            if (tr) trace_event(s, TRACE_TO_OVERLAY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.encap_ifindex, 0);
             r->ifindex = g_node.encap_ifindex;
             r->eg_flags |= EG_F_ENCAP;
             return TC_ACT_REDIRECT;
@@ -2106,11 +2170,14 @@ skip_service_lookup: ;
     if (dst_id == CLUSTER_ID) s->cb[2] = 1;                              /* policy_mark_skip */
     ret = ipv4_l3(s, w, NULL, c->node_mac);                              /* pass_to_stack */
     if (ret != TC_ACT_OK) return ret;
+    if (tr) trace_event(s, TRACE_TO_STACK, (uint16_t)c->lxc_id, c->seclabel, dst_id, 0, 0, (uint8_t)fwd);   /* :669 */
     r->eg_flags |= EG_F_TO_STACK;
     return TC_ACT_OK;
 to_host:
     ret = ipv4_l3(s, w, c->node_mac, g_node.host_mac);
     if (ret != TC_ACT_OK) return ret;
+    if (tr) trace_event(s, TRACE_TO_HOST, (uint16_t)c->lxc_id, c->seclabel, HOST_ID, 0, g_node.host_ifindex,
+                        (uint8_t)fwd);                                   /* :650 */
     r->eg_flags |= EG_F_TO_HOST;
     r->ifindex = g_node.host_ifindex;
     return TC_ACT_REDIRECT;
@@ -2276,7 +2343,10 @@ skip_service_lookup: ;
     default:
         return DROP_POLICY;
     }
+    const int tr = (c->flags & LXC_F_TRACE_NOTIFY) != 0;
+    const uint8_t fwd = r->ct_ret;                               /* forwarding_reason */
     if (verdict > 0) {                                           /* ipv6_redirect_to_host_port + ipv6_l3 */
+        if (tr) trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.host_ifindex, fwd);
         ret = redirect_to_host_port_checks(s, l4_off, nh);
         if (IS_ERR(ret)) return ret;
         pol_ctx x = {w, plog};
@@ -2308,6 +2378,7 @@ skip_service_lookup: ;
         const uint8_t *tun = g_node.tunnel_map ? om_lookup_ptr(g_node.tunnel_map, k) : NULL;
         if (tun) {
             r->tunnel_ip = bswap32(ge32(tun, 0));
+            if (tr) trace_event(s, TRACE_TO_OVERLAY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.encap_ifindex, 0);
             r->ifindex = g_node.encap_ifindex;
             r->eg_flags |= EG_F_ENCAP;
             return TC_ACT_REDIRECT;
@@ -2323,11 +2394,13 @@ skip_service_lookup: ;
         old = bswap32(0x60000000u) | bswap32(c->seclabel) | old;
         if (skb_store_bytes(s, w, ETH_HLEN, &old, 4) < 0) return DROP_WRITE_ERROR;
     }
+    if (tr) trace_event(s, TRACE_TO_STACK, (uint16_t)c->lxc_id, c->seclabel, dst_id, 0, 0, fwd);   /* :381 */
     r->eg_flags |= EG_F_TO_STACK;
     return TC_ACT_OK;
 to_host:
     ret = ipv6_l3(s, w, c->node_mac, g_node.host_mac);
     if (ret != TC_ACT_OK) return ret;
+    if (tr) trace_event(s, TRACE_TO_HOST, (uint16_t)c->lxc_id, c->seclabel, HOST_ID, 0, g_node.host_ifindex, fwd);  /* :364 */
     r->eg_flags |= EG_F_TO_HOST;
     r->ifindex = g_node.host_ifindex;
     return TC_ACT_REDIRECT;
@@ -2346,6 +2419,8 @@ static void from_container(const o_prog_array *a, const o_batch *b, uint32_t i, 
     const o_lxc_cfg *c = a->slot[(b->lxc_id ? b->lxc_id[i] : 0) & 0xffff];
     o->stage = O_STAGE_FROM_LXC;
     if (!c) { o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-DROP_MISSED_TAIL_CALL); return; }
+    if (c->flags & LXC_F_TRACE_NOTIFY)                   /* handle_ingress, bpf_lxc.c:705 */
+        trace_event(&s, TRACE_FROM_LXC, (uint16_t)c->lxc_id, c->seclabel, 0, 0, 0, 0);
     int ret;
     eg_res r; memset(&r, 0, sizeof r);
     nd_res nr; memset(&nr, 0, sizeof nr);
@@ -2393,7 +2468,7 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
     uint8_t *plog2 = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
     o_ingress_out *ing = (o_ingress_out *)calloc((size_t)n + 1, sizeof(o_ingress_out));
     o_batch b2 = *b;                                   /* the local deliveries, over the rewritten frames */
-    b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = NULL;
+    b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = b->flow_hash;   /* the skb's hash (trace records) */
     /* One packet at a time, as on one CPU: the from-container program, its
      * cilium_proxy{4,6} update (lxc.h:137), then — for a local delivery — the
      * destination's handle_policy (the tail call of ipv4_local_delivery) and its
@@ -2419,8 +2494,9 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
     }
     /* drop notifications: the sender's send_drop_notify(SECLABEL, 0, 0, 0, ret) for
      * from-container drops (bpf_lxc.c:659-668), handle_policy's for local deliveries */
-    for (uint32_t i = 0; events && i < n; i++) {
-        uint8_t *e = events + (size_t)i * O_EVENT_RECORD;
+    for (uint32_t i = 0; (events || g_tr.ev) && i < n; i++) {
+        uint8_t tmp[O_EVENT_RECORD];
+        uint8_t *e = events ? events + (size_t)i * O_EVENT_RECORD : tmp;
         memset(e, 0, O_EVENT_RECORD);
         const o_egress_out *o = &out[i];
         if (o->action != TC_ACT_SHOT) continue;
@@ -2432,6 +2508,8 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
         else if (o->stage == O_STAGE_POLICY)
             drop_event(e, o->reason, c->lxc_id, hash, len, secctx[i], c->seclabel, c->lxc_id, ifx[i], row, b->snap_stride);
         else drop_event(e, o->reason, c->lxc_id, hash, len, c->seclabel, 0, 0, 0, row, b->snap_stride);
+        uint8_t *t = ev_slot(i);
+        if (t) memcpy(t, e, O_EVENT_RECORD);
     }
     free(plog2); free(ing); free(plog);
     if (!snap_out) free(snap);

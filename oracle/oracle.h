@@ -144,8 +144,9 @@ void o_lb_batch_mt(const o_lb_cfg *cfg, const o_batch *b, o_lb_out *out, uint8_t
 #define O_NETDEV_F_FIXED_SECCTX 1u
 typedef struct o_netdev_cfg {
     om_map *lxc_map;
-    uint32_t flags, fixed_secctx;
+    uint32_t flags, fixed_secctx;   /* flags: bit 0 FIXED_SRC_SECCTX, bit 1 TRACE_NOTIFY */
     uint8_t router_ip6[16];
+    uint32_t ingress_ifindex;       /* skb->ingress_ifindex of the batch (TRACE_FROM_STACK) */
 } o_netdev_cfg;
 typedef struct o_pipeline_cfg {
     const o_xdp_cfg *xdp;           /* NULL: no XDP stage */
@@ -169,6 +170,14 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
  * (struct drop_notify + up to 128 captured bytes), a packet's record in its
  * slot, zero where the packet was not dropped. */
 void o_ingress_events(const o_prog_array *a, const o_batch *b, const o_ingress_out *out, uint8_t *events);
+/* Trace notifications (bpf/lib/trace.h:59-106, per program with o_lxc_cfg.flags
+ * bit 6 / o_netdev_cfg.flags bit 1 = TRACE_NOTIFY): while a sink is set, every
+ * batch call of this thread appends each packet's trace records in emission
+ * order, then its drop record, to that packet's list: ev holds n * per_pkt
+ * records of 160 B, cnt[i] (zeroed by the caller) counts packet i's.  capture = 0
+ * leaves the payload zero (column batches, whose frames the GPU path never
+ * sees).  NULL ev disables. */
+void o_set_trace_sink(uint8_t *ev, uint8_t *cnt, uint32_t per_pkt, int capture);
 
 /* ---------------- endpoint egress (== gf_lxc_egress_classify) ----------------
  * The from-container program of endpoint lxc_id[i] over each frame, in batch

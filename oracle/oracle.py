@@ -54,7 +54,8 @@ class o_cols(C.Structure):
 
 
 class o_netdev_cfg(C.Structure):
-    _fields_ = [("lxc_map", VP), ("flags", C.c_uint32), ("fixed_secctx", C.c_uint32), ("router_ip6", C.c_uint8 * 16)]
+    _fields_ = [("lxc_map", VP), ("flags", C.c_uint32), ("fixed_secctx", C.c_uint32), ("router_ip6", C.c_uint8 * 16),
+                ("ingress_ifindex", C.c_uint32)]
 
 
 class o_pipeline_cfg(C.Structure):
@@ -89,6 +90,7 @@ _s("o_ingress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP)
 _s("o_ingress_batch_mt", None, VP, C.POINTER(o_batch), C.c_uint32, VP, C.c_uint32)
 _s("o_pipeline_batch_mt", None, C.POINTER(o_pipeline_cfg), C.POINTER(o_batch), C.c_uint32, VP, VP, VP, C.c_uint32, VP)
 _s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
+_s("o_set_trace_sink", None, VP, VP, C.c_uint32, C.c_int)
 _s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_ct_lru_cutoffs", C.c_int, VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
@@ -255,6 +257,29 @@ def pipeline(cfg, b, now, threads=1, events=False):
     if events:
         return out, nd6, snap, ev[ev[:, 0] == 1]
     return out, nd6, snap
+
+
+class TraceSink:
+    """o_set_trace_sink for the calls inside a `with` block: each packet's trace
+    records (trace.h:59-106) then its drop record, per packet in emission order.
+    .events() = every record in batch order ([k, 160] u8), the ring's order."""
+    PER = 4
+
+    def __init__(self, n, capture=True):
+        self.ev = np.zeros((n, self.PER, 160), np.uint8)
+        self.cnt = np.zeros(n, np.uint8)
+        self.capture = capture
+
+    def __enter__(self):
+        lib.o_set_trace_sink(self.ev.ctypes.data, self.cnt.ctypes.data, self.PER, 1 if self.capture else 0)
+        return self
+
+    def __exit__(self, *a):
+        lib.o_set_trace_sink(None, None, 0, 0)
+
+    def events(self):
+        k = np.arange(self.PER)[None, :] < self.cnt[:, None]
+        return self.ev[k]
 
 
 def ingress_events(prog_array, b, out):

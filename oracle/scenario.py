@@ -129,7 +129,7 @@ class OracleDP:
         if self._pipe is None:
             nd = self.sc.netdev
             self._nd = O.o_netdev_cfg(self.m[nd["lxc_map"]].ptr, nd.get("flags", 0), nd.get("fixed_secctx", 0),
-                                      (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))))
+                                      (C.c_uint8 * 16)(*nd.get("router_ip6", bytes(16))), nd.get("ingress_ifindex", 0))
             self._pipe = O.o_pipeline_cfg(C.pointer(self.xdp_cfg) if self.xdp_cfg is not None else None,
                                           C.pointer(self.lb_cfg) if self.lb_cfg is not None else None,
                                           C.pointer(self._nd), self.arr)

@@ -9,6 +9,7 @@ pytestmark = pytest.mark.gpu
 from cilium_amd import synth
 from cilium_amd.datapath import Datapath, DeviceBatch, LB_OUT, ING_OUT, PIPE_OUT, to_numpy
 from oracle.scenario import OracleDP
+import oracle.oracle as O
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -299,6 +300,91 @@ def test_drop_notify_events():
         got = recs[:n].cpu().numpy()
         bad = np.nonzero((got != e).any(axis=1))[0]
         assert len(bad) == 0, f"{len(bad)} egress event records differ, first {bad[:1]}: {got[bad[0]][:32]} vs {e[bad[0]][:32]}"
+    finally:
+        lib.gf_set_event_ring(None)
+
+
+def _trace_on(sc, every=2, netdev_ifindex=None):
+    """TRACE_NOTIFY on every `every`-th endpoint program (per-endpoint define,
+    pkg/endpoint/endpoint.go:131-134) and, for a pipeline, on the netdev."""
+    for k, e in enumerate(sc.lxc):
+        if k % every == 0:
+            e["flags"] |= synth.LXC_TRACE_NOTIFY
+    if netdev_ifindex is not None and sc.netdev is not None:
+        sc.netdev = dict(sc.netdev, flags=sc.netdev.get("flags", 0) | synth.NETDEV_TRACE_NOTIFY,
+                         ingress_ifindex=netdev_ifindex)
+
+
+def _ring_check(recs, cnt, e, what):
+    n = int(cnt.item())
+    assert n == len(e), f"{what}: {n} records vs {len(e)}"
+    got = recs[:n].cpu().numpy()
+    bad = np.nonzero((got != e).any(axis=1))[0]
+    assert len(bad) == 0, f"{what}: {len(bad)} records differ, first {bad[:1]}: {got[bad[0]][:32]} vs {e[bad[0]][:32]}"
+    return got
+
+
+def test_trace_notify_events():
+    """send_trace_notify records (bpf/lib/trace.h:59-106) interleaved with the drop
+    records in the device event ring — per packet in the order the programs send
+    them (from_netdev / handle_ingress first, the redirects' TO_PROXY with the frame
+    before its rewrites, TO_HOST / TO_STACK / TO_OVERLAY / TO_LXC, the drop last) —
+    equal the oracle's per-packet event lists, capture bytes included, for the
+    ingress program, the full pipeline and endpoint egress; programs without
+    TRACE_NOTIFY send none."""
+    import ctypes as C
+    from cilium_amd._lib import lib, gf_event_ring
+    from cilium_amd.datapath import EG_OUT
+    cap = 400000
+    recs = torch.zeros((cap, 160), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ring = gf_event_ring(recs.data_ptr(), cap, cnt.data_ptr())
+    assert lib.gf_set_event_ring(C.byref(ring)) == 0
+    try:
+        sc = synth.fuzz(seed=2, n_packets=20000, n_batches=2)
+        _trace_on(sc)
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        exp = []
+        for bi, pk in enumerate(sc.batches):
+            io = dp.ingress(DeviceBatch(pk), sc.now + bi)
+            with O.TraceSink(pk.n, capture=False) as ts:
+                ro = ref.ingress(pk, sc.now + bi)
+                ref.ingress_events(pk, ro)
+            torch.cuda.synchronize()
+            _cmp_struct(to_numpy(io, ING_OUT), ro, f"ingress b{bi}")
+            exp.append(ts.events())
+        got = _ring_check(recs, cnt, np.concatenate(exp), "ingress")
+        assert (got[:, 0] == 4).sum() > 1000 and (got[:, 0] == 1).sum() > 100
+        cnt.zero_()
+        sc = synth.pipeline_fuzz(seed=3, n_packets=20000, n_batches=2)
+        _trace_on(sc, every=3, netdev_ifindex=7)
+        dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+        exp = []
+        for bi, pk in enumerate(sc.batches):
+            out, nd6, snap = dp.pipeline(DeviceBatch(pk, parse=False), sc.now + bi)
+            with O.TraceSink(pk.n) as ts:
+                ro, rn6, rs = ref.pipeline(pk, sc.now + bi)
+            torch.cuda.synchronize()
+            _cmp_struct(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
+            exp.append(ts.events())
+        got = _ring_check(recs, cnt, np.concatenate(exp), "pipeline")
+        assert set(np.unique(got[got[:, 0] == 4, 1])) >= {0, 8}
+        cnt.zero_()
+        for seed, kw in ((5, {"hazard": False}), (6, {"hazard": True})):
+            sc = synth.egress_fuzz(seed=seed, n_packets=20000, n_batches=2, **kw)
+            _trace_on(sc)
+            dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+            exp = []
+            for bi, pk in enumerate(sc.batches):
+                out, snap = dp.egress(DeviceBatch(pk, parse=False), sc.now + bi)
+                with O.TraceSink(pk.n) as ts:
+                    ro, rs = ref.egress(pk, sc.now + bi)
+                torch.cuda.synchronize()
+                _cmp_struct(to_numpy(out, EG_OUT), ro, f"egress s{seed} b{bi}")
+                exp.append(ts.events())
+            got = _ring_check(recs, cnt, np.concatenate(exp), f"egress s{seed}")
+            assert set(np.unique(got[got[:, 0] == 4, 1])) >= {0, 1, 3, 4, 5}, np.unique(got[got[:, 0] == 4, 1])
+            cnt.zero_()
     finally:
         lib.gf_set_event_ring(None)
 
