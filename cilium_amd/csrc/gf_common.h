@@ -191,6 +191,14 @@ GF_HD uint32_t gf_pair_hash4(uint32_t a, uint32_t b) {
     uint32_t w[2] = {lo, hi};
     return gf_hash_words(w, 2, 8);
 }
+// Connection group hash (IPv4): the unordered pair of (address, port)
+// endpoints plus the protocol, so a connection's two directions share it.
+// Ports are the raw be16 values of the CT tuple (0 for portless protocols).
+GF_HD uint32_t gf_conn_hash4(uint32_t a, uint32_t pa, uint32_t b, uint32_t pb, uint32_t nh) {
+    const bool sw = a > b || (a == b && pa > pb);
+    uint32_t w[4] = {sw ? b : a, sw ? a : b, sw ? (pb | (pa << 16)) : (pa | (pb << 16)), nh | 0x5a00u};
+    return gf_hash_words(w, 4, 16);
+}
 GF_HD uint32_t gf_pair_hash6(const uint32_t *a, const uint32_t *b) {
     // lexicographic byte compare of the two 16-byte addresses
     int less = 0;

@@ -542,6 +542,7 @@ struct IngCtx {
     uint32_t *plog, *plog_n;   // cilium_proxy{4,6} update log (16 words per redirect) and its length
     uint32_t gw, host6[4];     // IPV4_GATEWAY, HOST_IP (node_config.h)
     uint8_t *tmark, *tcap;     // trace notifications: per-packet GF_TR_* marks, 128-B captures (null: off)
+    uint32_t *rlog, *rlog_n;   // egress connection groups: ct_create4's related entries logged (null: written)
 };
 
 // ---- handle_policy's own header writes (kept out of line: cold paths of the
@@ -821,13 +822,27 @@ __device__ __forceinline__ int ct_lookup(const gf_htab_desc &d, ProbeLine<KSZ, U
     return CT_ESTABLISHED;
 }
 
+// A slot in a log shared by many lanes: one atomic per wave (the active lanes'
+// count), each lane its rank among them.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t *ctr) {
+    const uint64_t m = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63u, lead = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)lead);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 // ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0).  The
 // tuple goes to the EMPTY slot the lookup walk ended on (one CAS), the related
-// entry to its cached slot when this lane wrote it before.
+// entry to its cached slot when this lane wrote it before — or, with connection
+// groups (rlog), to the log applied after the run.
+
 template <int KSZ, int TW, int U>
 __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
                                          uint32_t len, uint32_t now, bool strict, const ProbeRes &pr, int *added,
-                                         RelCache<TW> &rc, uint32_t &ab) {
+                                         RelCache<TW> &rc, uint32_t &ab, uint32_t *rlog = nullptr,
+                                         uint32_t *rlog_n = nullptr, uint32_t order = 0) {
     constexpr int NHW = TW - 1;                         // word holding nexthdr | flags << 8
     ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written
     uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
@@ -843,6 +858,15 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     it[NHW - 1] = 0;                                    // sport = dport = 0
     it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
     v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
+    if constexpr (KSZ == 14) if (rlog) {                // connection groups: applied after the run, in order
+        uint32_t *lg = rlog + (size_t)20 * wave_reserve(rlog_n);
+        lg[0] = order;
+#pragma unroll
+        for (int k = 0; k < TW; k++) lg[1 + k] = it[k];
+#pragma unroll
+        for (int k = 0; k < 12; k++) lg[5 + k] = v[k];
+        return 0;
+    }
     bool same = rc.slot != ~0u;
 #pragma unroll
     for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
@@ -1178,7 +1202,8 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     }
     if (r.cls & 4) verdict = 0;                         // skip_proxy
     if (ret == CT_NEW && !(GF_DIAG & 8)) {
-        ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab);
+        ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab,
+                                         X.rlog, X.rlog_n, 2u * i + 1u);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -2501,6 +2526,14 @@ struct EgDev {
     uint32_t vip4_mask, vip6_mask;
     uint8_t *hz_fl;                     // per packet: GF_HZ_* (null: no ordering check)
     uint32_t *hz;                       // device words: [0] 1 = ordering hazard (k_eg_groups idles), [1] GF_HZ_* kinds seen
+    // Connection groups (IPv4): conn = 1 keys IPv4 packets by their
+    // connection and logs the ICMP-related entries ct_create4 writes (the only CT key
+    // two connections of a pair share, read only by ICMP errors); an IPv4 ICMP packet
+    // in the run sets *cflag and the run falls back to address-pair groups.
+    uint32_t conn;
+    uint32_t *cflag;                    // device word: 1 = pair groups (an IPv4 ICMP packet reaches conntrack)
+    uint32_t *keysP, *key2P;            // the pair keys of the front / of the deliveries (fallback)
+    uint32_t *rlog, *rlog_n;            // logged related entries {order, key[4], value[12], pad[3]}
 };
 // The ordering check.  The reference runs a local delivery's
 // handle_policy right after its from-container program, before the next packet;
@@ -2900,10 +2933,18 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             key = (gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;   // the IPv6 family of the schedule
         } else if (r.st == 0) {
             key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
+            if (E.conn) {
+                E.keysP[i] = key;
+                const bool tu = (r.nh == 6 || r.nh == 17) && skb_ok(r.l4_off, 4, len);
+                const uint32_t sp = tu ? w.r16((uint32_t)r.l4_off) : 0u, dp = tu ? w.r16((uint32_t)r.l4_off + 2u) : 0u;
+                key = gf_conn_hash4(r.t_saddr, sp, r.t_daddr, dp, r.nh) & GF_KEY_HASH;
+                if (r.nh == 1) atomicOr(E.cflag, 1u);
+            }
             const uint32_t lo = E.loopback;
             if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || (E.strict & 1u)) *E.seq = 1u;
         } else {
             key = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
+            if (E.conn) E.keysP[i] = key;
             if (o.stage == GF_STAGE_FROM_LXC) {
                 if (ret < 0 || ret == TC_SHOT) {
                     o.action = TC_SHOT; o.reason = (uint8_t)(-ret);
@@ -2923,9 +2964,15 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
 
 // After the front: a flagged batch runs as one bucket per family (every IPv4
 // key equal; the IPv6 path writes no service entries and keeps its own bucket).
-__global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, uint32_t n, uint32_t *keys) {
-    if (!*seq) return;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] &= GF_KEY_FAM;
+// With connection groups and an IPv4 ICMP packet in the run: the pair keys.
+__global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, const uint32_t *cflag,
+                                                       const uint32_t *keysP, uint32_t n, uint32_t *keys) {
+    if (*seq) {
+        for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] &= GF_KEY_FAM;
+    } else if (cflag && *cflag) {
+        for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK)
+            if (!(keys[i] & GF_KEY_FAM)) keys[i] = keysP[i];
+    }
 }
 
 // The ordering check: every continuing packet records the first batch index of
@@ -3149,7 +3196,7 @@ __device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, ui
 // Returns TC_OK / TC_REDIRECT / ND_TAILCALL (local delivery; ifx, lxc, mapped
 // filled) or an error.
 __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
-                          uint32_t &lxc, int *added, bool seq, uint32_t &ab) {
+                          uint32_t &lxc, int *added, bool seq, bool rlog, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
     const int l4_off = r.l4_off;
     const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
@@ -3227,7 +3274,14 @@ __device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf
         }
         uint32_t it[4] = {t[0], t[1], 0u, 1u | ((((t[3] >> 8) & 0xffu) | 2u) << 8)};
         v[1] |= F_SEEN_NON_SYN;
-        if (ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, it, v, strict, added) < 0) return D_CT_CREATE_FAILED;
+        if (rlog) {                                     // applied after the run, in packet order (the pair's
+            uint32_t *lg = E.rlog + (size_t)GF_CTLOG_WORDS * wave_reserve(E.rlog_n);   // other connections
+            lg[0] = 2u * i;                                                             // never read it)
+            for (int k = 0; k < 4; k++) lg[1 + k] = it[k];
+            for (int k = 0; k < 12; k++) lg[5 + k] = v[k];
+        } else if (ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, it, v, strict, added) < 0) {
+            return D_CT_CREATE_FAILED;
+        }
         o.eg_flags |= GF_EG_F_CREATED;
     } else if (ret == CT_REPLY || ret == CT_RELATED) {
         if (st.rev_nat) {                               // lb4_rev_nat(flags 0), lb.h:447-534
@@ -3543,6 +3597,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
     uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
     if (F) order += nfam[0];
     const bool seq = *E.seq != 0;
+    const bool rlog = FAM == 4 && E.conn && !seq && !*E.cflag;   // connection groups: related entries logged
     int added = 0;
     for (;;) {
         uint32_t base = 0;
@@ -3558,6 +3613,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
             gf_rec rr;
             if (r.st) {                                 // final in the front: not part of the ingress pass
                 key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
+                if (E.conn) E.key2P[i] = key2[i];
                 rec2[i] = rr;
                 continue;
             }
@@ -3576,7 +3632,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
             } else {                                    // the LDS copy of the header bytes
                 eg_copy(row, g, K);
                 Row w{row, K < r.len ? K : r.len};
-                ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, ab);
+                ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, rlog, ab);
                 if (ret == ND_TAILCALL) parse_row(w.p, w.cap, r.len, h2);
                 eg_copy(g, row, K);
             }
@@ -3588,9 +3644,18 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
             if (ret == ND_TAILCALL) {                   // handle_policy of the destination, next pass
                 o.stage = GF_STAGE_POLICY; o.lxc_id = (uint16_t)lxc; o.ct_ret = 0;
                 const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
-                key2[i] = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
-                                   gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, true,
-                                   h2.s6, h2.d6, rr);
+                uint32_t kk = pack_rec(i, h2.et, r.len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto,
+                                       gload<uint32_t>(&c->seclabel), ifx, E.slot_of[lxc & 0xffffu], 0, false, true,
+                                       h2.s6, h2.d6, rr);
+                if (E.conn) {                           // the delivery's connection (handle_policy's CT tuple)
+                    E.key2P[i] = kk;
+                    if (h2.et == 0x0800 && r.len >= 34) {
+                        const bool tu = h2.proto == 6 || h2.proto == 17;
+                        kk = gf_conn_hash4(h2.sa, tu ? (h2.w0 & 0xffffu) : 0u, h2.da, tu ? (h2.w0 >> 16) : 0u, h2.proto) &
+                             GF_KEY_HASH;
+                    }
+                }
+                key2[i] = kk;
                 if constexpr (v6) {
                     reinterpret_cast<uint4 *>(E.s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
                     reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
@@ -3608,6 +3673,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     o.ifindex_lo = (uint16_t)ifx;
                 }
                 key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
+                if (E.conn) E.key2P[i] = key2[i];
                 if (stats) {
                     st.add(o.reason); st.add(256 + o.action);
                     ls[0] += 1; ls[1] += r.len; ls[2] += ab;
@@ -3994,8 +4060,9 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 // allocated and the marks cleared by the caller before its first kernel.
 struct TraceWs { DevBuf mark, px, in; };
 static TraceWs &trace_ws() { static TraceWs t; return t; }
-struct TraceArgs {                 // the pipeline / egress callers' part of the event pass
+struct PassArgs {                  // what the pipeline / egress callers pass to their handle_policy pass
     uint32_t kind;                 // 1 pipeline, 2 egress
+    uint32_t *rlog, *rlog_n;       // egress connection groups: the related-entry log (null: written inline)
     bool on;                       // this call traces (a ring is set and a program / the netdev traces)
     uint32_t nd_trace, nd_ifindex; // pipeline: GF_NETDEV_F_TRACE_NOTIFY, skb->ingress_ifindex
     const uint8_t *orig;           // egress: the frames as sent
@@ -4336,7 +4403,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                        gf_ingress_out *out, hipStream_t s, const PackFn &pack = PackFn(), uint8_t *pout = nullptr,
                        const uint32_t *ev_len = nullptr, const uint8_t *ev_snap = nullptr, uint32_t ev_stride = 0,
                        uint8_t *wsnap = nullptr, bool lru = true, bool px_keep = false, bool prepared = false,
-                       const TraceArgs *ta = nullptr) {
+                       const PassArgs *ta = nullptr) {
     int r;
     // trace notifications: the plain ingress call decides here, the pipeline and
     // egress callers (whose earlier kernels mark packets) pass their decision
@@ -4395,6 +4462,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
     if (tracing) { X.tmark = (uint8_t *)trace_ws().mark.p; X.tcap = (uint8_t *)trace_ws().px.p; }
+    if (ta) { X.rlog = ta->rlog; X.rlog_n = ta->rlog_n; }
     if ((r = px_log_begin(n, s, X, px_keep))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
@@ -4633,7 +4701,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     if ((r = grow(w.s6, (size_t)n * 16)) || (r = grow(w.d6, (size_t)n * 16))) return r;
     P.vec_copy = (fr.snap_stride % 16 == 0) && (((uintptr_t)fr.snap | (uintptr_t)snap_out) & 15u) == 0;
-    TraceArgs ta{};
+    PassArgs ta{};
     ta.kind = 1;
     ta.nd_trace = (p->cfg.netdev.flags & GF_NETDEV_F_TRACE_NOTIFY) ? 1u : 0u;
     ta.nd_ifindex = p->cfg.netdev.ingress_ifindex;
@@ -5013,7 +5081,7 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 // ---- endpoint egress (from-container) ----
 namespace {
 struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6,
-             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6;
+             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n;
              uint32_t hz_gen = 0, hz_cap = 0;
              std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
              uint32_t vip4_mask = 0, vip6_mask = 0; bool vip4_any = false, vip6_any = false; };
@@ -5089,6 +5157,32 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
     ew.vip_stamp = stamp;
     return 0;
 }
+// A log of deferred CT4 writes {order, key[4], value[12], pad[3]} applied in
+// order (k_ctlog_keys / sort / k_ctlog_apply: the last writer of a key wins).
+static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32_t nlog, const gf_htab_desc &ct,
+                       uint32_t *ct_count, hipStream_t s) {
+    if (!nlog) return 0;
+    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
+    int r;
+    if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
+        (r = grow(ew.cval, (size_t)nlog * 4)) || (r = grow(ew.cperm, (size_t)nlog * 4)))
+        return r;
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
+                                    (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s);
+    if ((r = grow(ew.ctmp, tb + 256))) return r;
+    ProfScope ps("k_ctlog_apply", s);
+    const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_ctlog_keys, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p,
+                       (uint32_t *)ew.cval.p, nlog);
+    tb = ew.ctmp.bytes;
+    if (hip_ok(rocprim::radix_sort_pairs(ew.ctmp.p, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
+                                         (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s), "ctlog sort"))
+        return -EIO;
+    hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (const unsigned long long *)ew.ckey2.p,
+                       (const uint32_t *)ew.cperm.p, ct, ct_count);
+    return hip_ok(hipGetLastError(), "k_ctlog_apply");
+}
 // One ordered run of an egress batch: check = run the ordering check first (a
 // flagged batch is split into runs, each through this function again); lru = the
 // LRU stand-in after it (once per classify call).
@@ -5129,7 +5223,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     // In place (snap_out == the frames) with the check: the flagged pass must leave
     // the frames as they came, so the rewrites go to scratch and are copied at the end
     // (also when tracing: TRACE_FROM_LXC captures the frames as sent).
-    TraceArgs ta{};
+    PassArgs ta{};
     ta.kind = 2;
     ta.on = event_ring().records && array_traces(a);
     ta.orig = fr.snap; ta.lxc_id = b->lxc_id;
@@ -5157,6 +5251,21 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.strict = strict;
     E.seq = (uint32_t *)ew.seq.p;
     E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
+    // Connection groups for IPv4 (EgDev::conn): off when CT4 inserts are counted
+    // exactly (strict: the batch runs as one bucket anyway).
+    static const bool no_conn = getenv("GF_EG_PAIRS") != nullptr;   // diagnosis: address-pair groups only
+    const bool conn = ct4m && !(strict & 1u) && !no_conn;
+    uint32_t *d_rn = nullptr;                          // [0] related entries logged, [1] pair-group fallback
+    if (conn) {
+        if ((r = grow(ew.keysP, (size_t)n * 4)) || (r = grow(ew.key2P, (size_t)n * 4)) || (r = grow(ew.rlog_n, 8)) ||
+            (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4)))
+            return r;
+        d_rn = (uint32_t *)ew.rlog_n.p;
+        if (hip_ok(hipMemsetAsync(d_rn, 0, 8, s), "rlog count")) return -EIO;
+        E.conn = 1; E.cflag = d_rn + 1;
+        E.keysP = (uint32_t *)ew.keysP.p; E.key2P = (uint32_t *)ew.key2P.p;
+        E.rlog = (uint32_t *)ew.rlog.p; E.rlog_n = d_rn;
+    }
     uint32_t *d_hz = (uint32_t *)ew.seq.p + 1;           // word 1 of the seq buffer: the hazard flag
     if (check) {
         E.hz_k = (uint64_t *)ew.hzk.p; E.hz_fl = (uint8_t *)ew.hzfl.p; E.hz = d_hz;
@@ -5185,8 +5294,8 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
                            E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
         hipLaunchKernelGGL(k_eg_front<6>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
                            E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
-        hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p, n,
-                           (uint32_t *)w.keys.p);
+        hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p,
+                           (const uint32_t *)E.cflag, (const uint32_t *)E.keysP, n, (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_eg_front"))) return r;
     }
     if (check) {
@@ -5223,11 +5332,13 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     // ct_create4's deferred service entries, in batch order
-    uint32_t cnts[2] = {0, 0}, hzw[3] = {0, 0, 0}, &hz = hzw[0];
+    uint32_t cnts[2] = {0, 0}, hzw[3] = {0, 0, 0}, &hz = hzw[0], rn[2] = {0, 0};
     if (hip_ok(hipMemcpyAsync(cnts, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost, s), "ctlog count") ||
         (check && hip_ok(hipMemcpyAsync(hzw, d_hz, 12, hipMemcpyDeviceToHost, s), "hz flag")) ||
+        (conn && hip_ok(hipMemcpyAsync(rn, d_rn, 8, hipMemcpyDeviceToHost, s), "rlog count")) ||
         hip_ok(hipStreamSynchronize(s), "ctlog sync"))
         return -EIO;
+    const bool clog = conn && !rn[1];                  // connection groups held (no IPv4 ICMP in the run)
     if (hz & 2u) {
         if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
         return egress_each(a, b, now_sec, out, snap_out, s, lru);
@@ -5237,28 +5348,9 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         hipLaunchKernelGGL(k_stats_fold, dim3(1), dim3(256), 0, s, (const unsigned long long *)fsink, sink);
         if ((r = hip_ok(hipGetLastError(), "k_stats_fold"))) return r;
     }
-    const uint32_t nlog = cnts[0];
-    if (nlog && ct4m) {
-        if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
-            (r = grow(ew.cval, (size_t)nlog * 4)) || (r = grow(ew.cperm, (size_t)nlog * 4)))
-            return r;
-        size_t tb = 0;
-        (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
-                                        (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s);
-        if ((r = grow(ew.ctmp, tb + 256))) return r;
-        ProfScope ps("k_ctlog_apply", s);
-        const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-        hipLaunchKernelGGL(k_ctlog_keys, dim3(gl), dim3(BLOCK), 0, s, (const uint32_t *)ew.ctlog.p,
-                           (const uint32_t *)ew.ctlog_n.p, (unsigned long long *)ew.ckey.p, (uint32_t *)ew.cval.p, nlog);
-        tb = ew.ctmp.bytes;
-        if (hip_ok(rocprim::radix_sort_pairs(ew.ctmp.p, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
-                                             (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s), "ctlog sort"))
-            return -EIO;
-        hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, (const uint32_t *)ew.ctlog.p,
-                           (const uint32_t *)ew.ctlog_n.p, (const unsigned long long *)ew.ckey2.p,
-                           (const uint32_t *)ew.cperm.p, cfg_ct4, (uint32_t *)ct4m->d_count.p);
-        if ((r = hip_ok(hipGetLastError(), "k_ctlog_apply"))) return r;
-    }
+    if (ct4m && (r = ctlog_apply(ew, (const uint32_t *)ew.ctlog.p, (const uint32_t *)ew.ctlog_n.p, cnts[0], cfg_ct4,
+                                 (uint32_t *)ct4m->d_count.p, s)))
+        return r;
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
     // The egress redirects' cilium_proxy{4,6} updates stay in the log: the
@@ -5270,15 +5362,28 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     c2.len = fr.len;
     c2.flow_hash = b->flow_hash;
     if (cnts[1]) { c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p; }   // IPv6 deliveries
+    // the deliveries' keys: their connections, or address pairs when the run fell back
+    const DevBuf &k2 = (conn && !clog) ? ew.key2P : ew.key2;
     auto pack = [&](const uint16_t *, gf_rec *rec, uint32_t *keys) -> int {
         if (hip_ok(hipMemcpyAsync(rec, ew.rec2.p, (size_t)n * sizeof(gf_rec), hipMemcpyDeviceToDevice, s), "rec2") ||
-            hip_ok(hipMemcpyAsync(keys, ew.key2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))
+            hip_ok(hipMemcpyAsync(keys, k2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))
             return -EIO;
         return 0;
     };
-    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru, true, false,
-                         &ta)))
+    if (clog) { ta.rlog = d_rn ? (uint32_t *)ew.rlog.p : nullptr; ta.rlog_n = d_rn; }
+    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru && !clog, true,
+                         false, &ta)))
         return r;
+    if (clog) {                                        // both passes' related entries, in packet order
+        uint32_t nrl = 0;
+        if (hip_ok(hipMemcpyAsync(&nrl, d_rn, 4, hipMemcpyDeviceToHost, s), "rlog count") ||
+            hip_ok(hipStreamSynchronize(s), "rlog sync"))
+            return -EIO;
+        if ((r = ctlog_apply(ew, (const uint32_t *)ew.rlog.p, d_rn, nrl, cfg_ct4, (uint32_t *)ct4m->d_count.p, s)))
+            return r;
+        ct4m->device_modified();
+        if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
+    }
     if (inplace && hip_ok(hipMemcpyAsync(snap_out, wsnap, (size_t)n * S, hipMemcpyDeviceToDevice, s), "snap copy"))
         return -EIO;
     return 0;

@@ -1103,7 +1103,7 @@ LXC_TRACE_NOTIFY = 64          # TRACE_NOTIFY (pkg/endpoint/endpoint.go:131-134)
 NETDEV_TRACE_NOTIFY = 2
 
 
-def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=True):
+def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=True, icmp=True):
     """Frames sent by the local endpoints through their from-container program
     (bpf_lxc.c handle_ingress -> handle_ipv4_from_lxc): services whose backends
     are local endpoints (local delivery after lb4_local, loopback back to the
@@ -1239,6 +1239,8 @@ def egress_fuzz(seed=5, n_packets=20000, n_batches=3, proxy_max=524288, hazard=T
         e = np.where(use, pool["e"][pi], e)
         d = np.where(use, pool["d"][pi], d)
         pr = np.where(use, pool["pr"][pi], pr).astype(np.uint8)
+        if not icmp:                                   # no IPv4 ICMP: the connection-group schedule holds
+            pr = np.where(pr == ICMP, UDP, pr).astype(np.uint8)
         sp = np.where(use, pool["sp"][pi], sp)
         dp = np.where(use, pool["dp"][pi], dp)
         s = ep4[e].copy()

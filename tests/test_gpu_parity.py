@@ -390,7 +390,8 @@ def test_trace_notify_events():
 
 
 @pytest.mark.parametrize("seed,kw", [(5, {"hazard": False}), (6, {"hazard": True}),
-                                     (7, {"hazard": False, "proxy_max": 6})])
+                                     (7, {"hazard": False, "proxy_max": 6}),
+                                     (11, {"hazard": False, "icmp": False}), (12, {"hazard": True, "icmp": False})])
 def test_egress_fuzz(seed, kw):
     """Endpoint egress (bpf_lxc.c handle_ingress -> handle_ipv4_from_lxc /
     ipv6_l3_from_lxc) over raw frames, local deliveries through the destination's
