@@ -1536,7 +1536,9 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 // Bucket-size histogram per family (bit 31 of the bucket's sorted key):
 // block-local LDS bins, one global add per non-empty bin.
 #define GF_SCHED_ITEMS 4096
-__global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, const uint32_t *off, const uint32_t *skeys,
+// off[q]: the start of run q in the sorted keys (nruns of them); its length is
+// the distance to the next start (or to n).
+__global__ __launch_bounds__(BLOCK) void k_bucket_hist(uint32_t n, const uint32_t *off, const uint32_t *skeys,
                                                        uint32_t *sched) {
     __shared__ uint32_t h[2 * (GF_LCAP + 1)];
     for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
@@ -1544,7 +1546,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_hist(const uint32_t *cnt, cons
     uint32_t nq = *GF_SCHED_NRUNS(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
@@ -1589,7 +1591,7 @@ __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
 // order[] = {first sorted position, packet count} of the non-empty buckets,
 // family 0 then 1, each by count descending (ties in any order): block-local
 // counts per bin, one global reservation per (block, bin).
-__global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, const uint32_t *off, const uint32_t *skeys,
+__global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32_t *off, const uint32_t *skeys,
                                                         uint32_t *sched, uint2 *order) {
     __shared__ uint32_t h[2 * (GF_LCAP + 1)];
     for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
@@ -1599,7 +1601,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
     uint32_t *cursor = GF_SCHED_CURSOR(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
@@ -1607,7 +1609,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(const uint32_t *cnt, con
         if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = cnt[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
         if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = make_uint2(off[q], c);
     }
 }
@@ -2534,6 +2536,8 @@ struct EgDev {
     uint32_t *cflag;                    // device word: 1 = pair groups (an IPv4 ICMP packet reaches conntrack)
     uint32_t *keysP, *key2P;            // the pair keys of the front / of the deliveries (fallback)
     uint32_t *rlog, *rlog_n;            // logged related entries {order, key[4], value[12], pad[3]}
+    gf_rec *rec2;                       // the handle_policy pass's records: the front writes every packet's
+    uint32_t *key2;                     //   as "not delivered" in batch order, k_eg_groups only the deliveries
 };
 // The ordering check.  The reference runs a local delivery's
 // handle_policy right after its from-container program, before the next packet;
@@ -2957,6 +2961,13 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         }
         erec[i] = r;
         keys[i] = key;
+        {                                                     // not (yet) a local delivery: skipped by the
+            gf_rec rr;                                        // handle_policy pass (coalesced writes here,
+            const uint32_t k2 = pack_rec(i, 0, len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
+            E.rec2[i] = rr;                                   // none for most packets in k_eg_groups)
+            E.key2[i] = k2;
+            if (E.conn) E.key2P[i] = k2;
+        }
         if (FAM == 4) eg_copy(dst, row, K);                   // the frame as the front left it
     }
     if (stats) { st.pkt_wave(scnt, sreason, saction, slen, sab); st.flush(stats); }
@@ -3195,7 +3206,7 @@ __device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, ui
 // The CT / policy part of handle_ipv4_from_lxc (bpf_lxc.c:499-658) for packet i.
 // Returns TC_OK / TC_REDIRECT / ND_TAILCALL (local delivery; ifx, lxc, mapped
 // filled) or an error.
-__device__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
+__device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
                           uint32_t &lxc, int *added, bool seq, bool rlog, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
     const int l4_off = r.l4_off;
@@ -3611,12 +3622,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
             const uint32_t i = perm[oc.x + k];
             const EgRec r = erec[i];
             gf_rec rr;
-            if (r.st) {                                 // final in the front: not part of the ingress pass
-                key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
-                if (E.conn) E.key2P[i] = key2[i];
-                rec2[i] = rr;
-                continue;
-            }
+            if (r.st) continue;                         // final in the front (its pass-2 record is written)
             gf_egress_out o{};
             o.stage = GF_STAGE_FROM_LXC;
             o.slave = r.slave; o.rev_nat = r.rev_nat; o.eg_flags = r.eflags;
@@ -3656,6 +3662,7 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     }
                 }
                 key2[i] = kk;
+                rec2[i] = rr;
                 if constexpr (v6) {
                     reinterpret_cast<uint4 *>(E.s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
                     reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
@@ -3672,15 +3679,12 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     o.action = (uint8_t)ret;
                     o.ifindex_lo = (uint16_t)ifx;
                 }
-                key2[i] = pack_rec(i, 0, r.len, 0, 0, 0, 0, 0, 0, 0, 0, r.ep, 0, true, false, nullptr, nullptr, rr);
-                if (E.conn) E.key2P[i] = key2[i];
                 if (stats) {
                     st.add(o.reason); st.add(256 + o.action);
                     ls[0] += 1; ls[1] += r.len; ls[2] += ab;
                     if (ls[1] >= 0xf0000000u || ls[2] >= 0xf0000000u) fold();
                 }
             }
-            rec2[i] = rr;
             out[i] = o;
         }
     }
@@ -3766,7 +3770,7 @@ void prof_drain() {
 }
 
 struct Workspace {
-    DevBuf rec, keys, skeys, perm, cnt, off, tmp, sched, order;
+    DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
 };
 // Two workspaces: gf_policy_ingress_classify_batches builds the schedule of
 // batch k+1 in one while handle_policy of batch k runs from the other.
@@ -4114,59 +4118,130 @@ static int ws_grow(uint32_t n) {
     int r;
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
         (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
-        (r = grow(w.cnt, (size_t)n * 4)) || (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 8)) ||
+        (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 8)) ||
         (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
     return 0;
 }
 
 // The flow-group schedule of ws().keys[0..n): stable radix sort of (32-bit group
-// hash, index), run-length encoding of the sorted hashes (one bucket per run),
-// then the longest-first bucket order per family, built on the device (no host
-// round trip): ws().perm / order / sched.
+// hash, index), the start of every run of equal hashes (one bucket per run: a
+// select of the positions whose key differs from the one before), then the
+// longest-first bucket order per family, built on the device (no host round
+// trip): ws().perm / order / sched.
+#ifndef GF_SORT_RADIX
+#define GF_SORT_RADIX 8                // digit bits of the onesweep passes (rocPRIM's gfx950 default)
+#endif
+#ifndef GF_SORT_IPT
+#define GF_SORT_IPT 16
+#endif
+#if GF_SORT_RADIX == 8 && GF_SORT_IPT == 16
+using GfSortCfg = rocprim::default_config;
+#else
+using GfSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, GF_SORT_IPT>, rocprim::kernel_config<1024, GF_SORT_IPT>,
+                                        GF_SORT_RADIX, rocprim::block_radix_rank_algorithm::match>>;
+#endif
+// Run starts of the sorted keys in three passes over GF_RUN_ITEMS-key tiles:
+// count the starts per tile, scan the tile counts (one block), write each
+// tile's starts at its offset in position order (wave ballots + LDS scan).
+#define GF_RUN_ITEMS 4096u
+__device__ __forceinline__ bool run_start(const uint32_t *k, uint32_t j) { return j == 0 || k[j] != k[j - 1]; }
+__global__ __launch_bounds__(BLOCK) void k_run_count(uint32_t n, const uint32_t *skeys, uint32_t *tcnt) {
+    __shared__ uint32_t wc[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u;
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
+        const uint32_t j = b0 + k * BLOCK + threadIdx.x;
+        c += (uint32_t)__popcll(__ballot(j < n && run_start(skeys, j)));
+    }
+    if (lane == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < BLOCK / 64; w++) t += wc[w];
+        tcnt[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(1024) void k_run_scan(uint32_t nt, uint32_t *tcnt, uint32_t *nruns) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < nt; c0 += 1024) {         // exclusive scan in place, 1024 tiles at a time
+        const uint32_t t = c0 + threadIdx.x;
+        const uint32_t v = t < nt ? tcnt[t] : 0u;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t o = 1; o < 1024; o <<= 1) {
+            const uint32_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (t < nt) tcnt[t] = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *nruns = carry;
+}
+__global__ __launch_bounds__(BLOCK) void k_run_write(uint32_t n, const uint32_t *skeys, const uint32_t *toff,
+                                                     uint32_t *off) {
+    __shared__ uint32_t wc[BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t base = toff[blockIdx.x];
+    for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
+        const uint32_t j = b0 + k * BLOCK + threadIdx.x;
+        const bool f = j < n && run_start(skeys, j);
+        const uint64_t m = __ballot(f);
+        if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (uint32_t w = 0; w < BLOCK / 64; w++) { before += w < wv ? wc[w] : 0u; all += wc[w]; }
+        if (f) off[base + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = j;
+        base += all;
+        __syncthreads();
+    }
+}
 static int schedule_groups(uint32_t n, hipStream_t s) {
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
     uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
-    size_t sort_bytes = 0, rle_bytes = 0, scan_bytes = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
-                                    rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0, GF_KEY_BITS, s);
-    (void)rocprim::run_length_encode(nullptr, rle_bytes, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
-                                     (uint32_t *)w.cnt.p, d_nruns, s);
-    (void)rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
-                                  rocprim::plus<uint32_t>(), s);
-    if ((r = grow(w.tmp, std::max(std::max(sort_bytes, scan_bytes), rle_bytes) + 256))) return r;
+    size_t sort_bytes = 0;
+    (void)rocprim::radix_sort_pairs<GfSortCfg>(nullptr, sort_bytes, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
+                                               rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0,
+                                               GF_KEY_BITS, s);
+    const uint32_t nt = (n + GF_RUN_ITEMS - 1) / GF_RUN_ITEMS;
+    if ((r = grow(w.tmp, sort_bytes + 256)) || (r = grow(w.tcnt, (size_t)nt * 4 + 16))) return r;
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
-        if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
-                                             rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0,
-                                             GF_KEY_BITS, s), "radix_sort_pairs"))
+        if (hip_ok(rocprim::radix_sort_pairs<GfSortCfg>(w.tmp.p, tb, (uint32_t *)w.keys.p, (uint32_t *)w.skeys.p,
+                                                        rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p,
+                                                        n, 0, GF_KEY_BITS, s), "radix_sort_pairs"))
             return -EIO;
     }
     {
         ProfScope ps("bucket_runs", s);
-        // counts past the last run stay 0 so the offset scan can run over n
-        if (hip_ok(hipMemsetAsync(w.cnt.p, 0, (size_t)n * 4, s), "memset cnt")) return -EIO;
-        tb = w.tmp.bytes;
-        if (hip_ok(rocprim::run_length_encode(w.tmp.p, tb, (const uint32_t *)w.skeys.p, n, rocprim::make_discard_iterator(),
-                                              (uint32_t *)w.cnt.p, d_nruns, s), "run_length_encode"))
-            return -EIO;
-        tb = w.tmp.bytes;
-        if (hip_ok(rocprim::exclusive_scan(w.tmp.p, tb, (uint32_t *)w.cnt.p, (uint32_t *)w.off.p, 0u, n,
-                                           rocprim::plus<uint32_t>(), s), "exclusive_scan"))
-            return -EIO;
+        if (nt) hipLaunchKernelGGL(k_run_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
+                                   (uint32_t *)w.tcnt.p);
+        hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.tcnt.p, d_nruns);
+        if (nt) hipLaunchKernelGGL(k_run_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
+                                   (const uint32_t *)w.tcnt.p, (uint32_t *)w.off.p);
+        if ((r = hip_ok(hipGetLastError(), "run starts"))) return r;
     }
     {
         ProfScope ps("k_bucket_sched", s);
         if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
         uint32_t g = (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS;
-        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched);
+        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.off.p,
+                           (const uint32_t *)w.skeys.p, d_sched);
         hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
-        hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, (const uint32_t *)w.cnt.p,
-                           (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, d_sched, (uint2 *)w.order.p);
+        hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.off.p,
+                           (const uint32_t *)w.skeys.p, d_sched, (uint2 *)w.order.p);
     }
     return hip_ok(hipGetLastError(), "k_bucket_sched");
 }
@@ -5251,6 +5326,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.strict = strict;
     E.seq = (uint32_t *)ew.seq.p;
     E.ctlog = (uint32_t *)ew.ctlog.p; E.ctlog_n = (uint32_t *)ew.ctlog_n.p;
+    E.rec2 = (gf_rec *)ew.rec2.p; E.key2 = (uint32_t *)ew.key2.p;
     // Connection groups for IPv4 (EgDev::conn): off when CT4 inserts are counted
     // exactly (strict: the batch runs as one bucket anyway).
     static const bool no_conn = getenv("GF_EG_PAIRS") != nullptr;   // diagnosis: address-pair groups only
