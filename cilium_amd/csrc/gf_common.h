@@ -58,7 +58,9 @@ struct gf_trie_desc {
     const uint8_t  *nodes; // 128 B nodes
     uint32_t root_bits;    // 8 or 16; 0 => map absent/empty (never matches)
     uint32_t addr_bytes;   // 4 or 16
+    const uint64_t *rsum;  // root_bits 16: the root as two 2^16-bit maps (covered | has a node), else null
 };
+#define GF_TRIE_RSUM_BYTES 16384u
 #define GF_TRIE_NODE_BYTES 128u
 #define GF_TRIE_FULL 0xFFFFFFFFu
 

@@ -375,22 +375,22 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
 // The words are copied to registers and a byte picked by selects: a dynamic
 // index into the caller's array would put that array in scratch.
 template <int NW>
-__device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_t *aw) {
-    if (!t.root_bits) return false;
+struct AddrBytes {
     uint32_t a[NW];
+    __device__ __forceinline__ AddrBytes(const uint32_t *aw) {
 #pragma unroll
-    for (int j = 0; j < NW; j++) a[j] = aw[j];
-    auto byte_at = [&](uint32_t k) -> uint32_t {
+        for (int j = 0; j < NW; j++) a[j] = aw[j];
+    }
+    __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
         uint32_t w = a[0];
 #pragma unroll
         for (int j = 1; j < NW; j++) w = (k >> 2) == (uint32_t)j ? a[j] : w;
         return (w >> (8 * (k & 3))) & 0xffu;
-    };
-    uint32_t idx = t.root_bits == 16 ? ((byte_at(0) << 8) | byte_at(1)) : byte_at(0);
-    uint32_t e = gload<uint32_t>(t.root + idx);
-    if (e == 0) return false;
-    if (e == GF_TRIE_FULL) return true;
-    uint32_t node = e - 1;
+    }
+};
+// The node levels below the root, from `node` (the root entry - 1).
+template <int NW>
+__device__ __forceinline__ bool trie_nodes(const gf_trie_desc &t, const AddrBytes<NW> &byte_at, uint32_t node) {
 #if GF_TRIE_WIDE
     // One round trip per level: both bitmaps (the node's first 64 B) and the
     // child base are loaded together, the words picked in registers.
@@ -431,6 +431,16 @@ __device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_
     }
 #endif
     return false;
+}
+template <int NW>
+__device__ __forceinline__ bool trie_lookup(const gf_trie_desc &t, const uint32_t *aw) {
+    if (!t.root_bits) return false;
+    const AddrBytes<NW> byte_at(aw);
+    uint32_t idx = t.root_bits == 16 ? ((byte_at(0) << 8) | byte_at(1)) : byte_at(0);
+    uint32_t e = gload<uint32_t>(t.root + idx);
+    if (e == 0) return false;
+    if (e == GF_TRIE_FULL) return true;
+    return trie_nodes<NW>(t, byte_at, e - 1);
 }
 
 // skb_load_bytes / store / csum_replace bound rules (see oracle.c).

@@ -99,7 +99,7 @@ struct Map : Obj {
     std::map<std::string, std::string, LpmKeyLess> lpm;   // orig key bytes -> value
     uint32_t lpm_len_cnt[129] = {0};
     bool trie_dirty = true;
-    DevBuf d_root, d_nodes;
+    DevBuf d_root, d_nodes, d_rsum;   // coverage trie (+ root summary, root_bits 16)
     uint32_t trie_root_bits = 0;
 
     Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f);

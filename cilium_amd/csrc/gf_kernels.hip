@@ -373,6 +373,97 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
     if (stats) st.flush(stats);
 }
 
+// check_v4 with the prefilter's hot levels in LDS (k_xdp_lds): the trie's
+// 2^16-entry root as two bitmaps (covered: drop at once / has a node: walk on in
+// HBM), and — when they fit — the /32 hash's slot array and cilium_lxc's key
+// slots, staged once per block (one or two 1024-lane blocks per CU, grid-stride
+// over the batch).  The lookups and their order are xdp_verdict's; IPv6 and
+// other frames take xdp_verdict as it is.
+struct XdpLds { uint32_t h4_bytes, lxc_bytes; };  // 0: that table stays in HBM
+// Exact-match probe over a slot array held in LDS (layout as in HBM).
+template <int KSZ>
+__device__ __forceinline__ bool lds_has(const uint8_t *slots, uint64_t mask, uint32_t slot_size, const uint32_t *kw,
+                                        uint32_t h) {
+    constexpr int SW = KSZ / 4;
+    static_assert(KSZ % 4 == 0, "word keys");
+    const uint64_t i = gf_home_slot(h, mask, slot_size);
+    for (uint64_t p = 0; p <= mask; p++) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(slots + ((i + p) & mask) * slot_size);
+        const uint32_t st = w[SW] & 0xffu;
+        if (st == GF_SLOT_EMPTY) return false;
+        if (st == GF_SLOT_FULL) {
+            bool e = true;
+#pragma unroll
+            for (int k = 0; k < SW; k++) e &= w[k] == kw[k];
+            if (e) return true;
+        }
+    }
+    return false;
+}
+__global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLds L, uint8_t *verdict,
+                                                  unsigned long long *stats) {
+    extern __shared__ uint4 xl[];
+    __shared__ uint32_t sl[272];
+    Stats st{sl};
+    const uint64_t *rs = reinterpret_cast<const uint64_t *>(xl);
+    const uint8_t *h4s = reinterpret_cast<const uint8_t *>(xl) + GF_TRIE_RSUM_BYTES;
+    const uint8_t *lxs = h4s + L.h4_bytes;
+    {
+        uint4 *d = xl;
+        const uint4 *src = reinterpret_cast<const uint4 *>(x.l4.rsum);
+        for (uint32_t k = threadIdx.x; k < GF_TRIE_RSUM_BYTES / 16; k += blockDim.x) d[k] = src[k];
+        d += GF_TRIE_RSUM_BYTES / 16;
+        src = reinterpret_cast<const uint4 *>(x.h4.slots);
+        for (uint32_t k = threadIdx.x; k < L.h4_bytes / 16; k += blockDim.x) d[k] = src[k];
+        d += L.h4_bytes / 16;
+        src = reinterpret_cast<const uint4 *>(x.lxc.slots);
+        for (uint32_t k = threadIdx.x; k < L.lxc_bytes / 16; k += blockDim.x) d[k] = src[k];
+    }
+    if (stats) st.init(); else __syncthreads();
+    for (uint32_t b = blockIdx.x * blockDim.x; b < c.n; b += gridDim.x * blockDim.x) {   // wave-uniform trips
+        const uint32_t i = b + threadIdx.x;
+        const bool act = i < c.n;
+        uint32_t len = 0, ab = 1;
+        uint8_t v = 0;
+        if (act) {
+            len = c.len[i];
+            const uint32_t et = c.ethertype[i];
+            if (et != 0x0800 || len < 34) {
+                v = xdp_verdict(x, ColA{c, i}, len, et, ab);
+            } else {
+                const uint32_t sa = c.saddr4[i];
+                bool drop = false;
+                ab += 10;
+                if (x.has_h4) {
+                    ab += 9;
+                    const uint32_t idx = ((sa & 0xffu) << 8) | ((sa >> 8) & 0xffu);   // the first two address bytes
+                    if ((rs[idx >> 6] >> (idx & 63)) & 1ull) drop = true;
+                    else if ((rs[1024 + (idx >> 6)] >> (idx & 63)) & 1ull)
+                        drop = trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
+                    if (!drop) {
+                        ab += 9;
+                        const uint32_t kw[2] = {32u, sa};
+                        drop = L.h4_bytes ? lds_has<8>(h4s, x.h4.mask, x.h4.slot_size, kw, key_hash<8>(kw))
+                                          : ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0;
+                    }
+                }
+                if (drop) {
+                    v = XDP_DROP_;
+                } else {
+                    ab += 20;
+                    const uint32_t lk[5] = {c.daddr4[i], 0, 0, 0, 1u};
+                    const bool ep = L.lxc_bytes ? lds_has<20>(lxs, x.lxc.mask, x.lxc.slot_size, lk, key_hash<20>(lk))
+                                                : ht_find<20>(x.lxc, lk, key_hash<20>(lk)) >= 0;
+                    v = ep ? XDP_PASS_ : XDP_DROP_;
+                }
+            }
+            verdict[i] = v;
+        }
+        if (stats) st.pkt_wave(act, v == XDP_DROP_ ? 1u : 0u, v, len, act ? ab : 0u);
+    }
+    if (stats) st.flush(stats);
+}
+
 // ================================================================ LB
 struct LbDev {
     gf_htab_desc s4, s6;
@@ -3923,6 +4014,31 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     if (p->m6l) x.l6 = p->m6l->tdesc();
     x.lxc = p->lxc->hdesc();
     ProfScope ps("k_xdp", s);
+    // The LDS variant when the LPM map has a 16-bit root (its summary is 16 KB);
+    // the /32 hash and the endpoint keys join it while they fit.
+    static const bool no_lds = getenv("GF_XDP_NOLDS") != nullptr;     // diagnosis: the HBM-only kernel
+    if (!no_lds && x.l4.rsum && x.has_h4 && x.l4.addr_bytes == 4) {
+        static const uint32_t cap = getenv("GF_XDP_LDS_KB") ? 1024u * (uint32_t)atoi(getenv("GF_XDP_LDS_KB")) : 48u * 1024u;
+        XdpLds L{0, 0};
+        const uint64_t hb = (uint64_t)(x.h4.mask + 1) * x.h4.slot_size, lb = (uint64_t)(x.lxc.mask + 1) * x.lxc.slot_size;
+        if (x.h4.slots && x.h4.ksz == 8 && hb % 16 == 0 && GF_TRIE_RSUM_BYTES + hb <= std::min(cap, 96u * 1024u))
+            L.h4_bytes = (uint32_t)hb;
+        if (x.lxc.slots && x.lxc.ksz == 20 && lb % 16 == 0 && GF_TRIE_RSUM_BYTES + L.h4_bytes + lb <= cap)
+            L.lxc_bytes = (uint32_t)lb;
+        const uint32_t lds = GF_TRIE_RSUM_BYTES + L.h4_bytes + L.lxc_bytes;
+        static uint32_t lds_set = 0;
+        if (lds > lds_set) {
+            if (hip_ok(hipFuncSetAttribute((const void *)k_xdp_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                       "k_xdp_lds lds"))
+                return -EIO;
+            lds_set = lds;
+        }
+        const uint32_t per_cu = lds <= 78u * 1024u ? 2u : 1u;
+        const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(resident_blocks(per_cu), (pkts->n + 1023) / 1024));
+        hipLaunchKernelGGL(k_xdp_lds, dim3(grid), dim3(1024), lds, s, *pkts, x, L, verdict,
+                           (unsigned long long *)stats_sink());
+        return hip_ok(hipGetLastError(), "k_xdp_lds");
+    }
     hipLaunchKernelGGL(k_xdp, dim3(stream_grid(pkts->n)), dim3(BLOCK), 0, s, *pkts, x, verdict,
                        (unsigned long long *)stats_sink());
     return hip_ok(hipGetLastError(), "k_xdp");

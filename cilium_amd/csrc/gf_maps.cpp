@@ -291,6 +291,16 @@ int Map::push(hipStream_t s) {
         if ((r = d_nodes.ensure(std::max<size_t>(nodes.size(), GF_TRIE_NODE_BYTES)))) return r;
         if (hip_ok(hipMemcpy(d_root.p, root.data(), root.size() * 4, hipMemcpyHostToDevice), "push trie root")) return -EIO;
         if (!nodes.empty() && hip_ok(hipMemcpy(d_nodes.p, nodes.data(), nodes.size(), hipMemcpyHostToDevice), "push trie nodes")) return -EIO;
+        if (rb == 16) {                                // the root summary a kernel can keep in LDS
+            std::vector<uint64_t> sum(2 * 1024, 0);
+            for (size_t k = 0; k < root.size(); k++) {
+                if (root[k] == GF_TRIE_FULL) sum[k >> 6] |= 1ull << (k & 63);
+                else if (root[k]) sum[1024 + (k >> 6)] |= 1ull << (k & 63);
+            }
+            if ((r = d_rsum.ensure(GF_TRIE_RSUM_BYTES))) return r;
+            if (hip_ok(hipMemcpy(d_rsum.p, sum.data(), GF_TRIE_RSUM_BYTES, hipMemcpyHostToDevice), "push trie summary"))
+                return -EIO;
+        }
         trie_root_bits = rb;
         trie_dirty = false;
         return 0;
@@ -333,6 +343,7 @@ gf_trie_desc Map::tdesc() {
     d.nodes = (const uint8_t *)d_nodes.p;
     d.root_bits = lpm.empty() ? 0 : trie_root_bits;
     d.addr_bytes = ksz - 4;
+    d.rsum = (d.root_bits == 16 && d_rsum.p) ? (const uint64_t *)d_rsum.p : nullptr;
     return d;
 }
 
