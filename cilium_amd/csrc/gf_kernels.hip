@@ -43,6 +43,12 @@ using namespace gfd;
 #endif
 #define GF_KEY_FAM (1u << (GF_KEY_BITS - 1))
 #define GF_KEY_HASH (GF_KEY_FAM - 1u)
+// The key of every packet the handle_policy pass skips (a pipeline packet that
+// ended before the tail call, an egress packet that was not delivered locally):
+// they sort into one run, which the bucket schedule leaves out, so no lane reads
+// their records.  Group keys never take this value (gf_key_live).
+#define GF_KEY_SKIP GF_KEY_HASH
+__device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
 #endif
@@ -1497,10 +1503,11 @@ __device__ __forceinline__ uint32_t pack_rec(uint32_t i, uint32_t et, uint32_t l
     if (tci & 1) cls |= 4u;
     if (skipped) cls |= 8u;
     r.cls = (uint8_t)cls;
-    const bool ct_ok = !skipped && (((cls & 3) == 1 && len >= 34) || ((cls & 3) == 2 && len >= 54 && have6));
-    if (!ct_ok) return gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
-    if ((cls & 3) == 2) return (gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;
-    return gf_pair_hash4(sa, da) & GF_KEY_HASH;
+    if (skipped) return GF_KEY_SKIP;
+    const bool ct_ok = ((cls & 3) == 1 && len >= 34) || ((cls & 3) == 2 && len >= 54 && have6);
+    if (!ct_ok) return gf_key_live(gf_hash_words(&i, 1, 4) & GF_KEY_HASH);
+    if ((cls & 3) == 2) return gf_key_live(gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;
+    return gf_key_live(gf_pair_hash4(sa, da) & GF_KEY_HASH);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_t *slot_of, gf_rec *rec,
@@ -1637,8 +1644,9 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_hist(uint32_t n, const uint32_
     uint32_t nq = *GF_SCHED_NRUNS(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
-        if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
+        const uint32_t key = skeys[off[q]];
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
+        if (c && key != GF_KEY_SKIP) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
     uint32_t *hist = GF_SCHED_HIST(sched);
@@ -1692,16 +1700,19 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
     uint32_t *cursor = GF_SCHED_CURSOR(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
-        if (c) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
+        const uint32_t key = skeys[off[q]];
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
+        if (c && key != GF_KEY_SKIP) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
         if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = skeys[off[q]] >> (GF_KEY_BITS - 1);
-        if (c) order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = make_uint2(off[q], c);
+        const uint32_t key = skeys[off[q]];
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
+        if (c && key != GF_KEY_SKIP)
+            order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = make_uint2(off[q], c);
     }
 }
 
@@ -3025,20 +3036,20 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         if (r.st == 0 && FAM == 6) {
             uint32_t s6[4], d6[4];
             for (int k = 0; k < 4; k++) { s6[k] = wg.r32(22 + 4 * k); d6[k] = wg.r32(38 + 4 * k); }
-            key = (gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;   // the IPv6 family of the schedule
+            key = gf_key_live(gf_pair_hash6(s6, d6) & GF_KEY_HASH) | GF_KEY_FAM;   // the IPv6 family of the schedule
         } else if (r.st == 0) {
-            key = gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH;
+            key = gf_key_live(gf_pair_hash4(r.t_saddr, r.t_daddr) & GF_KEY_HASH);
             if (E.conn) {
                 E.keysP[i] = key;
                 const bool tu = (r.nh == 6 || r.nh == 17) && skb_ok(r.l4_off, 4, len);
                 const uint32_t sp = tu ? w.r16((uint32_t)r.l4_off) : 0u, dp = tu ? w.r16((uint32_t)r.l4_off + 2u) : 0u;
-                key = gf_conn_hash4(r.t_saddr, sp, r.t_daddr, dp, r.nh) & GF_KEY_HASH;
+                key = gf_key_live(gf_conn_hash4(r.t_saddr, sp, r.t_daddr, dp, r.nh) & GF_KEY_HASH);
                 if (r.nh == 1) atomicOr(E.cflag, 1u);
             }
             const uint32_t lo = E.loopback;
             if (r.t_saddr == r.t_daddr || (lo && (r.t_saddr == lo || r.t_daddr == lo)) || (E.strict & 1u)) *E.seq = 1u;
         } else {
-            key = gf_hash_words(&i, 1, 4) & GF_KEY_HASH;
+            key = GF_KEY_SKIP;                        // final in the front: k_eg_groups has nothing to do
             if (E.conn) E.keysP[i] = key;
             if (o.stage == GF_STAGE_FROM_LXC) {
                 if (ret < 0 || ret == TC_SHOT) {
@@ -3748,8 +3759,8 @@ __global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched
                     E.key2P[i] = kk;
                     if (h2.et == 0x0800 && r.len >= 34) {
                         const bool tu = h2.proto == 6 || h2.proto == 17;
-                        kk = gf_conn_hash4(h2.sa, tu ? (h2.w0 & 0xffffu) : 0u, h2.da, tu ? (h2.w0 >> 16) : 0u, h2.proto) &
-                             GF_KEY_HASH;
+                        kk = gf_key_live(gf_conn_hash4(h2.sa, tu ? (h2.w0 & 0xffffu) : 0u, h2.da, tu ? (h2.w0 >> 16) : 0u,
+                                                       h2.proto) & GF_KEY_HASH);
                     }
                 }
                 key2[i] = kk;
