@@ -891,6 +891,8 @@ def main():
                "roofline": r["roofline"], "kernels_ms_per_step": r["kernels_ms_per_step"],
                "cpu_baseline": r["cpu_baseline"], "parity": r.get("parity")}
     if rank == 0:
+        from cilium_amd import _lib
+        res["build_id"] = _lib.BUILD_ID          # gf_build_id(): the sources libgpuflow.so was compiled from
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

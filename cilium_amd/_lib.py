@@ -178,6 +178,7 @@ _sig("gf_memcpy_d2h", C.c_int, VP, VP, C.c_size_t, VP)
 _sig("gf_stream_sync", C.c_int, VP)
 _sig("gf_device_count", C.c_int)
 _sig("gf_version", C.c_char_p)
+_sig("gf_build_id", C.c_char_p)
 
 # Every symbol the C header declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -187,5 +188,30 @@ EXPORTED = [
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
     "gf_policy_ingress_classify", "gf_policy_ingress_classify_batches", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
-    "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version",
+    "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version", "gf_build_id",
 ]
+
+BUILD_ID = lib.gf_build_id().decode()
+
+
+def source_sha():
+    """sha256 prefix of the library's sources as they are in the tree now (the
+    same digest __graft_entry__.build() compiles in as gf_build_id())."""
+    import hashlib
+    root = os.path.dirname(_HERE)
+    files = [os.path.join(_HERE, "csrc", f) for f in sorted(os.listdir(os.path.join(_HERE, "csrc")))
+             if f.endswith((".hip", ".cpp", ".h"))] + [os.path.join(root, "include", "gpuflow.h")]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+# The in-tree library must be the one its sources build: a stale binary fails
+# here instead of running (ablation builds of tools/ carry no id).
+if not os.environ.get("GPUFLOW_DIAG_LIB") and os.path.isdir(os.path.join(_HERE, "csrc")):
+    if BUILD_ID != source_sha():
+        raise ImportError(f"libgpuflow.so was built from sources {BUILD_ID}, the tree holds {source_sha()}: "
+                          "run `python -c 'import __graft_entry__ as g; g.build()'`")

@@ -1038,5 +1038,9 @@ int gf_device_count(void) {
     return n;
 }
 const char *gf_version(void) { return "gpuflow 0.1 (gfx950)"; }
+#ifndef GF_SRC_SHA
+#define GF_SRC_SHA "unknown"
+#endif
+const char *gf_build_id(void) { return GF_SRC_SHA; }
 
 }  // extern "C"

@@ -562,6 +562,9 @@ int   gf_stream_sync(void *stream);
 /* Number of visible GPUs; a library built without a device returns 0. */
 int   gf_device_count(void);
 const char *gf_version(void);
+/* sha256 prefix of the sources (cilium_amd/csrc, include/gpuflow.h) this library
+ * was compiled from ("unknown" for builds outside __graft_entry__.build()). */
+const char *gf_build_id(void);
 
 #ifdef __cplusplus
 }
