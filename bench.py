@@ -220,7 +220,10 @@ def bench_config2(args, dev, rank, world):
     from cilium_amd.datapath import Datapath
     W, K = max(args.warmup, 3), args.steps
     t0 = time.time()
-    sc, P, _ = synth.config2_tables(n_pairs=args.pairs, ct_max=args.ct_max)
+    # Weak scaling: every rank serves --pairs address pairs (its RSS share of
+    # pairs x world), so the per-GPU step — packets, flow groups, bucket depth, CT
+    # partition — is the N=1 step at every N.
+    sc, P, _ = synth.config2_tables(n_pairs=args.pairs * world, ct_max=args.ct_max)
     st = stream.Stream(P, rank=rank, world=world, flows_per_step=args.flows_per_step, device=dev)
     # The stream ramps up over its first 3 steps (flows span 4 steps); the run starts at
     # stream step S0 = 3 so that every launch, warm-up included, is a full steady-state
@@ -288,7 +291,8 @@ def bench_config2(args, dev, rank, world):
             "workload": "config2: bpf_lxc ingress handle_policy (ct_lookup4 + policy_can_access), steady-state "
                         "stream, 4M new flows/step (16M active), 256 endpoints, 4352 identities",
             "packets_per_step_per_gpu": int(batches[W].n),
-            "address_pairs": int(args.pairs),
+            "address_pairs_per_gpu": int(args.pairs),
+            "address_pairs": int(args.pairs) * world,
             "ct_max_entries": int(args.ct_max),
             "ct_entries_at_end": int(bpf_entries(dp, "cilium_ct4_global")),
             "parallelism": f"dp{world} (flow-group sharded, tables replicated, CT partitioned)",
@@ -830,7 +834,7 @@ def main():
     ap.add_argument("--config", default="2", choices=["1", "2", "3", "4", "5", "egress"],
                     help="BASELINE configuration printed as the line (default: 2, the headline)")
     ap.add_argument("--flows-per-step", type=int, default=4 << 20)
-    ap.add_argument("--pairs", type=int, default=1 << 20)
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="address pairs per GPU (config 2: x N in total)")
     ap.add_argument("--ct-max", type=int, default=1 << 27,
                     help="CT max_entries (LRU): 134,217,728, above the entries a default run creates")
     ap.add_argument("--ct6-prefill", type=int, default=8_000_000)
