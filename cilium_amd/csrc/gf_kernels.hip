@@ -51,6 +51,16 @@ using namespace gfd;
 __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
+#ifndef GF_EG_MINW
+#define GF_EG_MINW 3        // k_eg_groups: min waves per SIMD (4 spills: 1.65 vs 1.60 ms, egress leg)
+#endif
+#ifndef GF_MEMO4
+#define GF_MEMO4 2          // policy decisions memoised per lane, IPv4 buckets
+#endif
+#ifndef GF_MEMO6
+#define GF_MEMO6 2          // IPv6 buckets (1 fits 4 blocks' lane state in LDS, but the 128-VGPR
+                            // budget that occupancy 4 then imposes spills: 1.93 vs 1.20 ms, config 5)
+#endif
 #endif
 
 // ---------------------------------------------------------------- constants
@@ -1055,18 +1065,29 @@ struct PolDecision {          // 24 B (kept in LDS with the rest of the lane sta
     uint32_t f;              // policy slot counted by the decision, ~0u: none
     int verdict;
 };
-struct PolMemo {             // two decisions (a group's flows use a couple of ports)
-    PolDecision d[2];
-    __device__ __forceinline__ void init() { d[0].slab = d[1].slab = 0; }
+template <int N>
+struct PolMemo {             // N decisions (a group's flows use a couple of ports)
+    PolDecision d[N];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < N; j++) d[j].slab = 0;
+    }
     __device__ __forceinline__ int find(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < N; j++)
             if ((d[j].slab & 0xffffu) == s && d[j].id == identity && d[j].pk == k && (identity >= 256 || d[j].sip == a))
                 return j;
         return -1;
     }
     __device__ __forceinline__ bool hit(uint32_t s, uint32_t identity, uint32_t k, uint32_t a) const {
         return find(s, identity, k, a) >= 0;
+    }
+    // the slot a new decision replaces: round-robin on bit 1 of the endpoint's bits
+    __device__ __forceinline__ PolDecision &victim(uint32_t &next) {
+        if constexpr (N == 1) return d[0];
+        PolDecision &v = d[(next >> 1) & 1u];
+        next ^= 2u;
+        return v;
     }
 };
 
@@ -1134,9 +1155,10 @@ deny:
 
 // policy_can_access_ingress with the counter update (policy.h:67-92), through the
 // lane's decision memo (IPv4, or any non-reserved identity).
+template <int N>
 __device__ __forceinline__ int policy_ingress(const IngCtx &X, Ep &ep, PolLine &pl, bool pl_loaded, uint32_t identity,
                                               uint32_t dport, uint32_t proto, uint32_t len, bool v6,
-                                              const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo &m) {
+                                              const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo<N> &m) {
     const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
     const bool memo_ok = !v6 || identity >= 256;
     const int j = memo_ok ? m.find(ep.sl, identity, pk, sip) : -1;
@@ -1151,11 +1173,10 @@ __device__ __forceinline__ int policy_ingress(const IngCtx &X, Ep &ep, PolLine &
     int v = policy_lookup(X, ep, pl, pl_loaded, identity, dport, proto, v6, cidr_addr, ab, fc);
     if (fc >= 0) policy_count(X, ep, fc, len, acc);
     if (memo_ok) {
-        PolDecision &d = m.d[(ep.next >> 1) & 1u];
+        PolDecision &d = m.victim(ep.next);
         d.id = identity; d.pk = pk; d.sip = sip; d.verdict = v;
         d.f = fc >= 0 ? (uint32_t)fc : ~0u;    // policy maps hold < 2^32 slots (max_entries is u32)
         d.slab = ep.sl | ((ab - ab0) << 16);
-        ep.next ^= 2u;
     }
     return v;
 }
@@ -1246,7 +1267,7 @@ __device__ __attribute__((noinline)) void pol_redirect_ol(PolCtx X, uint32_t i, 
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
-                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo &pm) {
+                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo<GF_MEMO4> &pm) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
     const uint32_t flags = ep.flags;
@@ -1321,7 +1342,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
 // ipv6_policy, bpf/bpf_lxc.c:745-862
 __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
                            uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc,
-                           RelCache<10> &rc, PolMemo &pm) {
+                           RelCache<10> &rc, PolMemo<GF_MEMO6> &pm) {
     uint32_t len = r.len;
     if (len < 54) return D_INVALID;
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
@@ -1431,7 +1452,7 @@ template <int FAM>
 struct Lane {
     Ep ep;
     PolAcc acc;
-    PolMemo pm;
+    PolMemo<FAM == 6 ? GF_MEMO6 : GF_MEMO4> pm;
     RelCache<FAM == 6 ? 10 : 4> rc;
     int added;
     LaneCnt sc;
@@ -3688,7 +3709,7 @@ __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint3
 // FAM 4 runs the schedule's family 0 (IPv4 buckets and every packet the front
 // finished), FAM 6 family 1 (IPv6); the two touch disjoint state.
 template <int FAM>
-__global__ __launch_bounds__(BLOCK, 3) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
+__global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
                                                      uint32_t *ct_count, unsigned long long *stats) {
     if (E.hz && *E.hz) return;                          // hazard: the batch reruns in ordered runs
