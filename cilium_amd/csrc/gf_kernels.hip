@@ -3822,28 +3822,42 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
 // The deferred service entries of a launch, in batch order (k_px_apply's rule):
 // sorted by (key hash, packet index), an entry is applied only if no later
 // entry of the batch has the same key.
-__global__ __launch_bounds__(BLOCK) void k_ctlog_keys(const uint32_t *lg, const uint32_t *n_, unsigned long long *key,
-                                                      uint32_t *val, uint32_t cap) {
-    const uint32_t n = *n_ < cap ? *n_ : cap;
-    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= cap) return;
-    if (j >= n) { key[j] = ~0ull; val[j] = j; return; }
-    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
-    key[j] = ((unsigned long long)key_hash<14, GF_HASH_CT>(e + 1) << 32) | e[0];
-    val[j] = j;
+// The logged ct_create entries (service entries of the from-container pass,
+// related entries of connection groups), applied last-writer-wins per CT key:
+// k_ctlog_max enters every entry into a scratch open-addressing set keyed by the
+// logged tuple (a slot holds 1 + the index of the first entry seen for its key
+// and 1 + the highest order entered for it), k_ctlog_apply upserts each entry
+// that holds its key's highest order.  Log entry: [0] order, [1..4] the 14-B key,
+// [5..16] the 48-B value.
+__device__ __forceinline__ bool ctlog_same(const uint32_t *a, const uint32_t *b) {
+    return a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && (a[4] & 0xffffu) == (b[4] & 0xffffu);
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, const unsigned long long *key,
-                                                       const uint32_t *perm, gf_htab_desc ct, uint32_t *ct_count) {
+__global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, uint2 *tab, uint32_t tmask) {
     const uint32_t n = *n_;
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * perm[p];
-    const uint32_t h = (uint32_t)(key[p] >> 32);
-    for (uint32_t q = p + 1; q < n && (uint32_t)(key[q] >> 32) == h; q++) {
-        const uint32_t *g = lg + (size_t)GF_CTLOG_WORDS * perm[q];
-        bool same = true;
-        for (int k = 1; k < 5; k++) same &= (k < 4 ? g[k] == e[k] : (g[4] & 0xffffu) == (e[4] & 0xffffu));
-        if (same) return;                               // a later update of the same key wins
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
+    for (uint32_t p = key_hash<14, GF_HASH_CT>(e + 1) & tmask;; p = (p + 1) & tmask) {
+        const uint32_t rep = atomicCAS(&tab[p].x, 0u, j + 1u);
+        if (rep == 0u || ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (rep - 1u), e)) {
+            atomicMax(&tab[p].y, e[0] + 1u);
+            return;
+        }
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, const uint2 *tab,
+                                                       uint32_t tmask, gf_htab_desc ct, uint32_t *ct_count) {
+    const uint32_t n = *n_;
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
+    for (uint32_t p = key_hash<14, GF_HASH_CT>(e + 1) & tmask;; p = (p + 1) & tmask) {
+        const uint2 t = tab[p];                         // the key is on this probe path (k_ctlog_max)
+        if (t.x == 0u) return;                          // (not reached)
+        if (t.x == j + 1u || ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (t.x - 1u), e)) {
+            if (t.y != e[0] + 1u) return;               // a later update of the same key wins
+            break;
+        }
     }
     int added = 0;
     ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
@@ -5303,7 +5317,7 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 
 // ---- endpoint egress (from-container) ----
 namespace {
-struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ckey2, cval, cperm, ctmp, s6, d6,
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
              hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n;
              uint32_t hz_gen = 0, hz_cap = 0;
              std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
@@ -5381,29 +5395,20 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
     return 0;
 }
 // A log of deferred CT4 writes {order, key[4], value[12], pad[3]} applied in
-// order (k_ctlog_keys / sort / k_ctlog_apply: the last writer of a key wins).
+// order (k_ctlog_max / k_ctlog_apply: the last writer of a key wins).
 static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32_t nlog, const gf_htab_desc &ct,
                        uint32_t *ct_count, hipStream_t s) {
     if (!nlog) return 0;
-    auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
-    int r;
-    if ((r = grow(ew.ckey, (size_t)nlog * 8)) || (r = grow(ew.ckey2, (size_t)nlog * 8)) ||
-        (r = grow(ew.cval, (size_t)nlog * 4)) || (r = grow(ew.cperm, (size_t)nlog * 4)))
-        return r;
-    size_t tb = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
-                                    (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s);
-    if ((r = grow(ew.ctmp, tb + 256))) return r;
+    uint32_t tmask = 1023;                             // the set at <= 1/2 load
+    while ((uint64_t)tmask + 1 < 2ull * nlog) tmask = tmask * 2 + 1;
+    const size_t tb = (size_t)(tmask + 1) * 8;
+    if (ew.ckey.bytes < tb && ew.ckey.ensure(tb)) return -ENOMEM;
     ProfScope ps("k_ctlog_apply", s);
+    if (hip_ok(hipMemsetAsync(ew.ckey.p, 0, tb, s), "ctlog set")) return -EIO;
     const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ctlog_keys, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p,
-                       (uint32_t *)ew.cval.p, nlog);
-    tb = ew.ctmp.bytes;
-    if (hip_ok(rocprim::radix_sort_pairs(ew.ctmp.p, tb, (unsigned long long *)ew.ckey.p, (unsigned long long *)ew.ckey2.p,
-                                         (uint32_t *)ew.cval.p, (uint32_t *)ew.cperm.p, nlog, 0, 64, s), "ctlog sort"))
-        return -EIO;
-    hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (const unsigned long long *)ew.ckey2.p,
-                       (const uint32_t *)ew.cperm.p, ct, ct_count);
+    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (uint2 *)ew.ckey.p, tmask);
+    hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (const uint2 *)ew.ckey.p, tmask, ct,
+                       ct_count);
     return hip_ok(hipGetLastError(), "k_ctlog_apply");
 }
 // One ordered run of an egress batch: check = run the ordering check first (a
@@ -5587,11 +5592,14 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     c2.flow_hash = b->flow_hash;
     if (cnts[1]) { c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p; }   // IPv6 deliveries
     // the deliveries' keys: their connections, or address pairs when the run fell back
-    const DevBuf &k2 = (conn && !clog) ? ew.key2P : ew.key2;
-    auto pack = [&](const uint16_t *, gf_rec *rec, uint32_t *keys) -> int {
-        if (hip_ok(hipMemcpyAsync(rec, ew.rec2.p, (size_t)n * sizeof(gf_rec), hipMemcpyDeviceToDevice, s), "rec2") ||
-            hip_ok(hipMemcpyAsync(keys, k2.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s), "key2"))
-            return -EIO;
+    // k_eg_groups wrote them in batch order: they become the workspace's records and
+    // keys by exchanging the buffers (the workspace's old ones are the next call's
+    // pass-2 buffers), not by copying n records
+    DevBuf &k2 = (conn && !clog) ? ew.key2P : ew.key2;
+    auto pack = [&](const uint16_t *, gf_rec *, uint32_t *) -> int {
+        Workspace &w = ws();
+        std::swap(w.rec.p, ew.rec2.p); std::swap(w.rec.bytes, ew.rec2.bytes);
+        std::swap(w.keys.p, k2.p); std::swap(w.keys.bytes, k2.bytes);
         return 0;
     };
     if (clog) { ta.rlog = d_rn ? (uint32_t *)ew.rlog.p : nullptr; ta.rlog_n = d_rn; }
