@@ -2891,16 +2891,29 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
     const uint32_t len = i < fr.n ? fr.len[i] : 0u;
     const uint8_t *src = fr.snap + (size_t)i * S;
     const uint32_t cap0 = S < len ? S : len;
-    const bool v6 = i < fr.n && len >= 14 && fbyte(src, cap0, 12) == 0x86 && fbyte(src, cap0, 13) == 0xDD;
+    // IPv4 frames that fit a row (and 16-B aligned): the block stages its frames
+    // with coalesced 16-B loads and stores them back the same way at the end
+    // (block-uniform); otherwise each lane stages its own header.
+    const bool coop = FAM == 4 && S <= GF_EG_STAGE && !(S & 15u) &&
+                      !(((uintptr_t)fr.snap | (uintptr_t)E.snap) & 15u);
+    const uint32_t b0 = blockIdx.x * BLOCK;
+    const uint32_t nv = b0 < fr.n ? ((fr.n - b0 < BLOCK ? fr.n - b0 : BLOCK) * S) / 16 : 0u;
+    if (coop) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(fr.snap + (size_t)b0 * S);
+        for (uint32_t k = threadIdx.x; k < nv; k += BLOCK) lds[k] = g[k];
+        __syncthreads();
+    }
+    uint8_t *row = reinterpret_cast<uint8_t *>(lds) + (FAM == 6 ? 0 : threadIdx.x * (coop ? S : GF_EG_STAGE));
+    const uint8_t *hdr = coop ? row : src;
+    const bool v6 = i < fr.n && len >= 14 && fbyte(hdr, cap0, 12) == 0x86 && fbyte(hdr, cap0, 13) == 0xDD;
     bool scnt = false;                                        // the lane's counter-block entry
     uint32_t sreason = 0, saction = 0, slen = 0, sab = 0;
     if (i < fr.n && v6 == (FAM == 6)) {
         const uint32_t K = eg_stage_bytes(S);
         uint8_t *dst = E.snap + (size_t)i * S;
-        uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
         if (FAM == 6) {                                       // extension headers: the whole snap, in HBM
             if (src != dst) eg_copy(dst, src, S);
-        } else {
+        } else if (!coop) {
             eg_copy(row, src, K);                             // the header, staged
             if (S > K && src != dst) eg_copy(dst + K, src + K, S - K);   // the rest of the snap, as is
         }
@@ -3091,7 +3104,12 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
             E.key2[i] = k2;
             if (E.conn) E.key2P[i] = k2;
         }
-        if (FAM == 4) eg_copy(dst, row, K);                   // the frame as the front left it
+        if (FAM == 4 && !coop) eg_copy(dst, row, K);         // the frame as the front left it
+    }
+    if (coop) {             // every row of the block (IPv6 rows unchanged: k_eg_front<6> rewrites them after)
+        __syncthreads();
+        uint4 *g = reinterpret_cast<uint4 *>(E.snap + (size_t)b0 * S);
+        for (uint32_t k = threadIdx.x; k < nv; k += BLOCK) g[k] = lds[k];
     }
     if (stats) { st.pkt_wave(scnt, sreason, saction, slen, sab); st.flush(stats); }
 }
