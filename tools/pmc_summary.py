@@ -21,6 +21,7 @@ import json
 import os
 
 KERNEL = "k_ing_groups"
+STEP_ENTRY = {"k_pipe_front", "k_eg_front", "k_ing_pack", "k_xdp", "k_xdp_lds", "k_lb", "k_parse"}
 
 
 def per_launch(path, nsteps):
@@ -43,7 +44,15 @@ def per_step(path, names, nsteps):
     (substrings; "gpuflow" = every libgpuflow kernel: k_* and its rocPRIM
     instantiations), divided by the number of bench steps the process ran."""
     out = collections.defaultdict(float)
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    # the classify calls only: from the first dispatch of a step's entry kernel on
+    # (the tables' setup before it — bulk inserts of pre-filled CT maps, pushes —
+    # is not part of any step)
+    first = min((int(r["Dispatch_Id"]) for r in rows
+                 if r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0] in STEP_ENTRY), default=0)
+    for r in rows:
+        if int(r["Dispatch_Id"]) < first:
+            continue
         name = r["Kernel_Name"]
         short = name.split("(")[0]
         ok = any((n == "gpuflow" and (" k_" in " " + short.replace("void ", "") or "ROCPRIM_400200" in name))
