@@ -55,13 +55,17 @@ struct gf_htab_desc {
 
 struct gf_trie_desc {
     const uint32_t *root;  // 2^root_bits entries: 0 empty, ~0u full, else node+1
-    const uint8_t  *nodes; // 128 B nodes
+    const uint8_t  *nodes; // 128-B nodes, four 32-B groups (GF_TRIE_GROUP_BYTES)
     uint32_t root_bits;    // 8 or 16; 0 => map absent/empty (never matches)
     uint32_t addr_bytes;   // 4 or 16
     const uint64_t *rsum;  // root_bits 16: the root as two 2^16-bit maps (covered | has a node), else null
 };
 #define GF_TRIE_RSUM_BYTES 16384u
 #define GF_TRIE_NODE_BYTES 128u
+// A node: for each 64 values of its byte (group w = byte >> 6, at 32 * w) the
+// full-coverage word, the child word (u64 LE each), then the node index of the
+// group's first child (u32: the children are contiguous, in byte order), 12 B pad.
+#define GF_TRIE_GROUP_BYTES 32u
 #define GF_TRIE_FULL 0xFFFFFFFFu
 
 GF_HD uint32_t gf_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

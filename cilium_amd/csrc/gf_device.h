@@ -368,9 +368,6 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
     else (*added)--;
 }
 
-#ifndef GF_TRIE_WIDE
-#define GF_TRIE_WIDE 1
-#endif
 // Coverage-trie membership of an address given as NW raw (LE-loaded) words.
 // The words are copied to registers and a byte picked by selects: a dynamic
 // index into the caller's array would put that array in scratch.
@@ -388,48 +385,23 @@ struct AddrBytes {
         return (w >> (8 * (k & 3))) & 0xffu;
     }
 };
-// The node levels below the root, from `node` (the root entry - 1).
+// The node levels below the root, from `node` (the root entry - 1).  A node is
+// four 32-B groups, one per 64 values of the level's byte (gf_common.h): the
+// byte's group alone answers the level — its full and child words in one 16-B
+// load and the index of the group's first child in one 4-B load, issued together.
 template <int NW>
 __device__ __forceinline__ bool trie_nodes(const gf_trie_desc &t, const AddrBytes<NW> &byte_at, uint32_t node) {
-#if GF_TRIE_WIDE
-    // One round trip per level: both bitmaps (the node's first 64 B) and the
-    // child base are loaded together, the words picked in registers.
     for (uint32_t k = t.root_bits / 8; k < t.addr_bytes; k++) {
-        uint32_t b = byte_at(k);
-        const uint8_t *nd = t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES;
-        const uint4 f0 = gload<uint4>(nd), f1 = gload<uint4>(nd + 16);
-        const uint4 c0 = gload<uint4>(nd + 32), c1 = gload<uint4>(nd + 48);
-        const uint32_t base = gload<uint32_t>(nd + 64);
-        const uint32_t w = b >> 6, bit = b & 63;
-        const uint64_t fw[4] = {f0.x | ((uint64_t)f0.y << 32), f0.z | ((uint64_t)f0.w << 32),
-                                f1.x | ((uint64_t)f1.y << 32), f1.z | ((uint64_t)f1.w << 32)};
-        const uint64_t cw4[4] = {c0.x | ((uint64_t)c0.y << 32), c0.z | ((uint64_t)c0.w << 32),
-                                 c1.x | ((uint64_t)c1.y << 32), c1.z | ((uint64_t)c1.w << 32)};
-        uint64_t fsel = fw[0], cw = cw4[0];
-        uint32_t rank = 0;
-#pragma unroll
-        for (uint32_t j = 1; j < 4; j++) {
-            fsel = w == j ? fw[j] : fsel;
-            cw = w == j ? cw4[j] : cw;
-            rank += j <= w ? (uint32_t)__popcll(cw4[j - 1]) : 0u;
-        }
-        if ((fsel >> bit) & 1ull) return true;
-        if (!((cw >> bit) & 1ull)) return false;
-        node = base + rank + (uint32_t)__popcll(cw & ((1ull << bit) - 1ull));
+        const uint32_t b = byte_at(k);
+        const uint8_t *g = t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES + GF_TRIE_GROUP_BYTES * (b >> 6);
+        const uint4 fc = gload<uint4>(g);
+        const uint32_t base = gload<uint32_t>(g + 16);
+        const uint32_t bit = b & 63u;
+        const uint64_t full = fc.x | ((uint64_t)fc.y << 32), child = fc.z | ((uint64_t)fc.w << 32);
+        if ((full >> bit) & 1ull) return true;
+        if (!((child >> bit) & 1ull)) return false;
+        node = base + (uint32_t)__popcll(child & ((1ull << bit) - 1ull));
     }
-#else
-    for (uint32_t k = t.root_bits / 8; k < t.addr_bytes; k++) {
-        uint32_t b = byte_at(k);
-        const uint8_t *nd = t.nodes + (uint64_t)node * GF_TRIE_NODE_BYTES;
-        uint32_t w = b >> 6, bit = b & 63;
-        if ((gload<uint64_t>(nd + 8 * w) >> bit) & 1ull) return true;
-        uint64_t cw = gload<uint64_t>(nd + 32 + 8 * w);
-        if (!((cw >> bit) & 1ull)) return false;
-        uint32_t rank = __popcll(cw & ((1ull << bit) - 1ull));
-        for (uint32_t j = 0; j < w; j++) rank += __popcll(gload<uint64_t>(nd + 32 + 8 * j));
-        node = gload<uint32_t>(nd + 64) + rank;
-    }
-#endif
     return false;
 }
 template <int NW>

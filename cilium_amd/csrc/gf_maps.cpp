@@ -719,10 +719,14 @@ void build_trie(const Map &m, std::vector<uint32_t> &root, std::vector<uint8_t> 
         uint64_t ch[4] = {0, 0, 0, 0};
         for (int b = 0; b < 256; b++)
             if (n->child[b] && !((n->full[b >> 6] >> (b & 63)) & 1)) ch[b >> 6] |= 1ull << (b & 63);
-        memcpy(o, n->full, 32);
-        memcpy(o + 32, ch, 32);
-        uint32_t cb = base[n];
-        memcpy(o + 64, &cb, 4);
+        uint32_t cb = base[n];                       // the node's first child
+        for (int w = 0; w < 4; w++) {                // group w: full, child, first child of the group
+            uint8_t *g = o + GF_TRIE_GROUP_BYTES * w;
+            memcpy(g, &n->full[w], 8);
+            memcpy(g + 8, &ch[w], 8);
+            memcpy(g + 16, &cb, 4);
+            cb += (uint32_t)__builtin_popcountll(ch[w]);
+        }
     }
     for (auto c : rchild) delete c;
 }
