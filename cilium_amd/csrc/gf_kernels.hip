@@ -114,6 +114,19 @@ struct Stats {
         }
         if (lane == 0) { if (n) { atomicAdd(&lds[268], n); atomicAdd(&lds[269], l); } if (a) atomicAdd(&lds[270], a); }
     }
+    // XDP verdict counts (reason 1 / XDP_DROP, reason 0 / XDP_PASS) and sums, summed
+    // per lane over a whole grid-stride loop: one wave reduction (every lane calls it)
+    __device__ void xdp_sums(uint32_t drop, uint32_t pass, uint32_t len, uint32_t ab) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            drop += __shfl_xor(drop, o); pass += __shfl_xor(pass, o);
+            len += __shfl_xor(len, o); ab += __shfl_xor(ab, o);
+        }
+        if ((threadIdx.x & 63u) == 0) {
+            add_n(1, drop); add_n(256 + 1, drop); add_n(0, pass); add_n(256 + 2, pass);
+            add_n(268, drop + pass); add_n(269, len); add_n(270, ab);
+        }
+    }
     __device__ void flush(unsigned long long *g) {
         __syncthreads();
         for (int k = threadIdx.x; k < 272; k += blockDim.x)
@@ -402,9 +415,9 @@ __device__ __forceinline__ bool lds_has(const uint8_t *slots, uint64_t mask, uin
                                         uint32_t h) {
     constexpr int SW = KSZ / 4;
     static_assert(KSZ % 4 == 0, "word keys");
-    const uint64_t i = gf_home_slot(h, mask, slot_size);
-    for (uint64_t p = 0; p <= mask; p++) {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(slots + ((i + p) & mask) * slot_size);
+    const uint32_t m = (uint32_t)mask, i = (uint32_t)gf_home_slot(h, mask, slot_size);   // LDS tables: < 2^32 slots
+    for (uint32_t p = 0; p <= m; p++) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(slots + ((i + p) & m) * slot_size);
         const uint32_t st = w[SW] & 0xffu;
         if (st == GF_SLOT_EMPTY) return false;
         if (st == GF_SLOT_FULL) {
@@ -436,6 +449,7 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
         for (uint32_t k = threadIdx.x; k < L.lxc_bytes / 16; k += blockDim.x) d[k] = src[k];
     }
     if (stats) st.init(); else __syncthreads();
+    uint32_t n_drop = 0, n_pass = 0, s_len = 0, s_ab = 0;      // the lane's counter sums, reduced once at the end
     for (uint32_t b = blockIdx.x * blockDim.x; b < c.n; b += gridDim.x * blockDim.x) {   // wave-uniform trips
         const uint32_t i = b + threadIdx.x;
         const bool act = i < c.n;
@@ -474,10 +488,13 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
                 }
             }
             verdict[i] = v;
+            n_drop += v == XDP_DROP_; n_pass += v == XDP_PASS_; s_len += len; s_ab += ab;
         }
-        if (stats) st.pkt_wave(act, v == XDP_DROP_ ? 1u : 0u, v, len, act ? ab : 0u);
     }
-    if (stats) st.flush(stats);
+    if (stats) {
+        st.xdp_sums(n_drop, n_pass, s_len, s_ab);
+        st.flush(stats);
+    }
 }
 
 // ================================================================ LB
@@ -4098,7 +4115,9 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
             lds_set = lds;
         }
         const uint32_t per_cu = lds <= 78u * 1024u ? 2u : 1u;
-        const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(resident_blocks(per_cu), (pkts->n + 1023) / 1024));
+        static const uint32_t grid_env = getenv("GF_XDP_GRID") ? (uint32_t)atoi(getenv("GF_XDP_GRID")) : 0u;   // diagnosis
+        const uint32_t grid = grid_env ? grid_env
+                                       : std::max<uint32_t>(1u, std::min<uint32_t>(resident_blocks(per_cu), (pkts->n + 1023) / 1024));
         hipLaunchKernelGGL(k_xdp_lds, dim3(grid), dim3(1024), lds, s, *pkts, x, L, verdict,
                            (unsigned long long *)stats_sink());
         return hip_ok(hipGetLastError(), "k_xdp_lds");
