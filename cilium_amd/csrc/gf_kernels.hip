@@ -114,6 +114,27 @@ struct Stats {
         }
         if (lane == 0) { if (n) { atomicAdd(&lds[268], n); atomicAdd(&lds[269], l); } if (a) atomicAdd(&lds[270], a); }
     }
+    // pkt_wave's (reason, action) bins alone: for grid-stride loops that keep the
+    // packet count and the byte sums per lane and hand them to sums() once
+    __device__ void bins_wave(bool act, uint32_t reason, uint32_t action) {
+        const uint32_t lane = threadIdx.x & 63u, key = (reason & 0xffu) | (action << 8);
+        uint64_t rem = __ballot(act);
+        while (rem) {
+            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
+            const uint32_t k = __shfl(key, (int)lead);
+            const uint64_t m = __ballot(act && key == k) & rem;
+            if (lane == lead) {
+                atomicAdd(&lds[k & 0xffu], (uint32_t)__popcll(m));
+                atomicAdd(&lds[256 + (k >> 8)], (uint32_t)__popcll(m));
+            }
+            rem &= ~m;
+        }
+    }
+    __device__ void sums(uint32_t n, uint32_t len, uint32_t ab) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { n += __shfl_xor(n, o); len += __shfl_xor(len, o); ab += __shfl_xor(ab, o); }
+        if ((threadIdx.x & 63u) == 0) { add_n(268, n); add_n(269, len); add_n(270, ab); }
+    }
     // XDP verdict counts (reason 1 / XDP_DROP, reason 0 / XDP_PASS) and sums, summed
     // per lane over a whole grid-stride loop: one wave reduction (every lane calls it)
     __device__ void xdp_sums(uint32_t drop, uint32_t pass, uint32_t len, uint32_t ab) {
@@ -386,20 +407,18 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
     __shared__ uint32_t sl[272];
     Stats st{sl};
     if (stats) st.init();
-    // wave-uniform trip count (the stats aggregation is a wave collective)
+    uint32_t n_drop = 0, n_pass = 0, s_len = 0, s_ab = 0;      // the lane's counter sums (Stats::xdp_sums)
     for (uint32_t b = blockIdx.x * blockDim.x; b < c.n; b += gridDim.x * blockDim.x) {
         const uint32_t i = b + threadIdx.x;
-        const bool act = i < c.n;
-        uint32_t len = 0, ab = 1;                         // output record
-        uint8_t v = 0;
-        if (act) {
-            len = c.len[i];
-            v = xdp_verdict(x, ColA{c, i}, len, c.ethertype[i], ab);
+        if (i < c.n) {
+            uint32_t ab = 1;                               // output record
+            const uint32_t len = c.len[i];
+            const uint8_t v = xdp_verdict(x, ColA{c, i}, len, c.ethertype[i], ab);
             verdict[i] = v;
+            n_drop += v == XDP_DROP_; n_pass += v == XDP_PASS_; s_len += len; s_ab += ab;
         }
-        if (stats) st.pkt_wave(act, v == XDP_DROP_ ? 1u : 0u, v, len, act ? ab : 0u);
     }
-    if (stats) st.flush(stats);
+    if (stats) { st.xdp_sums(n_drop, n_pass, s_len, s_ab); st.flush(stats); }
 }
 
 // check_v4 with the prefilter's hot levels in LDS (k_xdp_lds): the trie's
@@ -616,6 +635,7 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
     __shared__ uint32_t sl[272];
     Stats st{sl};
     if (stats) st.init();
+    uint32_t s_n = 0, s_len = 0, s_ab = 0;              // the lane's packet count and sums (Stats::sums)
     // wave-uniform trip count (the stats aggregation is a wave collective)
     for (uint32_t b = blockIdx.x * blockDim.x; b < c.n; b += gridDim.x * blockDim.x) {
       const uint32_t i = b + threadIdx.x;
@@ -643,9 +663,10 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
         if (nd6 && v6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(n6[0], n6[1], n6[2], n6[3]);
         else if (nd6) reinterpret_cast<uint4 *>(nd6)[i] = make_uint4(0, 0, 0, 0);
       }
-      if (stats) st.pkt_wave(act, o.reason, o.action, len, act ? ab : 0u);
+      if (act) { s_n++; s_len += len; s_ab += ab; }
+      if (stats) st.bins_wave(act, o.reason, o.action);
     }
-    if (stats) st.flush(stats);
+    if (stats) { st.sums(s_n, s_len, s_ab); st.flush(stats); }
 }
 
 // ================================================================ ingress (handle_policy)
