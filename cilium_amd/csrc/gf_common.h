@@ -66,6 +66,9 @@ struct gf_trie_desc {
 // full-coverage word, the child word (u64 LE each), then the node index of the
 // group's first child (u32: the children are contiguous, in byte order), 12 B pad.
 #define GF_TRIE_GROUP_BYTES 32u
+// Compact IPv4 address sets (Map::addr_set): 2^bits u32 slots, 0 = empty (address 0
+// is a flag of its own), linear probing from a Fibonacci hash of the raw address.
+GF_HD uint32_t gf_aset_home(uint32_t a, uint32_t bits) { return (a * 0x9E3779B1u) >> (32 - bits); }
 #define GF_TRIE_FULL 0xFFFFFFFFu
 
 GF_HD uint32_t gf_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

@@ -116,6 +116,14 @@ struct Map : Obj {
     // coherence
     int pull();                       // device -> host if !host_valid
     int push(hipStream_t s);          // host -> device if !dev_valid / trie dirty
+    // The IPv4 addresses of the keys as a compact open-addressing set for a
+    // kernel's LDS (kind 8: {prefixlen 32, addr} keys; kind 20: endpoint keys
+    // {addr, 0, 0, 0, family 1}); rebuilt when the map changed.  -E2BIG past
+    // max_slots, -EINVAL for another key size.
+    int addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero);
+    DevBuf d_aset;
+    uint64_t aset_gen = ~0ull;
+    uint32_t aset_kind = 0, aset_bits = 0, aset_zero = 0;
     void device_modified() { host_valid = false; dev_gen++; }
     // Element access on the HBM replica of a device-authoritative hash map (the
     // datapath wrote it last): walks the key's probe sequence with small reads

@@ -427,7 +427,21 @@ __global__ __launch_bounds__(BLOCK) void k_xdp(gf_pkt_cols c, XdpDev x, uint8_t 
 // slots, staged once per block (one or two 1024-lane blocks per CU, grid-stride
 // over the batch).  The lookups and their order are xdp_verdict's; IPv6 and
 // other frames take xdp_verdict as it is.
-struct XdpLds { uint32_t h4_bytes, lxc_bytes; };  // 0: that table stays in HBM
+struct XdpLds {
+    uint32_t h4_bytes, lxc_bytes;                  // slot arrays staged as they are (0: not staged)
+    const uint32_t *h4set, *lxset;                 // or the tables' compact address sets (Map::addr_set)
+    uint32_t h4bits, lxbits, h4zero, lxzero;
+};
+// Membership in a compact IPv4 address set held in LDS (gf_aset_home; <= 1/2 load).
+__device__ __forceinline__ bool aset_has(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
+    if (!a) return zero != 0;
+    const uint32_t m = (1u << bits) - 1u;
+    for (uint32_t k = gf_aset_home(a, bits);; k = (k + 1) & m) {
+        const uint32_t v = t[k];
+        if (v == a) return true;
+        if (!v) return false;
+    }
+}
 // Exact-match probe over a slot array held in LDS (layout as in HBM).
 template <int KSZ>
 __device__ __forceinline__ bool lds_has(const uint8_t *slots, uint64_t mask, uint32_t slot_size, const uint32_t *kw,
@@ -454,18 +468,19 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
     __shared__ uint32_t sl[272];
     Stats st{sl};
     const uint64_t *rs = reinterpret_cast<const uint64_t *>(xl);
+    const uint32_t h4b = L.h4set ? 4u << L.h4bits : L.h4_bytes, lxb = L.lxset ? 4u << L.lxbits : L.lxc_bytes;
     const uint8_t *h4s = reinterpret_cast<const uint8_t *>(xl) + GF_TRIE_RSUM_BYTES;
-    const uint8_t *lxs = h4s + L.h4_bytes;
+    const uint8_t *lxs = h4s + h4b;
     {
         uint4 *d = xl;
         const uint4 *src = reinterpret_cast<const uint4 *>(x.l4.rsum);
         for (uint32_t k = threadIdx.x; k < GF_TRIE_RSUM_BYTES / 16; k += blockDim.x) d[k] = src[k];
         d += GF_TRIE_RSUM_BYTES / 16;
-        src = reinterpret_cast<const uint4 *>(x.h4.slots);
-        for (uint32_t k = threadIdx.x; k < L.h4_bytes / 16; k += blockDim.x) d[k] = src[k];
-        d += L.h4_bytes / 16;
-        src = reinterpret_cast<const uint4 *>(x.lxc.slots);
-        for (uint32_t k = threadIdx.x; k < L.lxc_bytes / 16; k += blockDim.x) d[k] = src[k];
+        src = reinterpret_cast<const uint4 *>(L.h4set ? (const void *)L.h4set : (const void *)x.h4.slots);
+        for (uint32_t k = threadIdx.x; k < h4b / 16; k += blockDim.x) d[k] = src[k];
+        d += h4b / 16;
+        src = reinterpret_cast<const uint4 *>(L.lxset ? (const void *)L.lxset : (const void *)x.lxc.slots);
+        for (uint32_t k = threadIdx.x; k < lxb / 16; k += blockDim.x) d[k] = src[k];
     }
     if (stats) st.init(); else __syncthreads();
     uint32_t n_drop = 0, n_pass = 0, s_len = 0, s_ab = 0;      // the lane's counter sums, reduced once at the end
@@ -492,7 +507,8 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
                     if (!drop) {
                         ab += 9;
                         const uint32_t kw[2] = {32u, sa};
-                        drop = L.h4_bytes ? lds_has<8>(h4s, x.h4.mask, x.h4.slot_size, kw, key_hash<8>(kw))
+                        drop = L.h4set ? aset_has(reinterpret_cast<const uint32_t *>(h4s), L.h4bits, L.h4zero, sa)
+                             : L.h4_bytes ? lds_has<8>(h4s, x.h4.mask, x.h4.slot_size, kw, key_hash<8>(kw))
                                           : ht_find<8>(x.h4, kw, key_hash<8>(kw)) >= 0;
                     }
                 }
@@ -501,7 +517,8 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
                 } else {
                     ab += 20;
                     const uint32_t lk[5] = {c.daddr4[i], 0, 0, 0, 1u};
-                    const bool ep = L.lxc_bytes ? lds_has<20>(lxs, x.lxc.mask, x.lxc.slot_size, lk, key_hash<20>(lk))
+                    const bool ep = L.lxset ? aset_has(reinterpret_cast<const uint32_t *>(lxs), L.lxbits, L.lxzero, lk[0])
+                                  : L.lxc_bytes ? lds_has<20>(lxs, x.lxc.mask, x.lxc.slot_size, lk, key_hash<20>(lk))
                                                 : ht_find<20>(x.lxc, lk, key_hash<20>(lk)) >= 0;
                     v = ep ? XDP_PASS_ : XDP_DROP_;
                 }
@@ -4121,13 +4138,19 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     static const bool no_lds = getenv("GF_XDP_NOLDS") != nullptr;     // diagnosis: the HBM-only kernel
     if (!no_lds && x.l4.rsum && x.has_h4 && x.l4.addr_bytes == 4) {
         static const uint32_t cap = getenv("GF_XDP_LDS_KB") ? 1024u * (uint32_t)atoi(getenv("GF_XDP_LDS_KB")) : 48u * 1024u;
-        XdpLds L{0, 0};
+        XdpLds L{};
+        // the /32 hash and the endpoint keys as compact address sets (4 B a slot), else
+        // their slot arrays when those fit the budget
+        static const bool no_sets = getenv("GF_XDP_NOSETS") != nullptr;     // diagnosis
+        if (!no_sets && p->m4h->addr_set(8, 8192, &L.h4set, &L.h4bits, &L.h4zero)) L.h4set = nullptr;
+        if (!no_sets && p->lxc->addr_set(20, 8192, &L.lxset, &L.lxbits, &L.lxzero)) L.lxset = nullptr;
         const uint64_t hb = (uint64_t)(x.h4.mask + 1) * x.h4.slot_size, lb = (uint64_t)(x.lxc.mask + 1) * x.lxc.slot_size;
-        if (x.h4.slots && x.h4.ksz == 8 && hb % 16 == 0 && GF_TRIE_RSUM_BYTES + hb <= std::min(cap, 96u * 1024u))
+        if (!L.h4set && x.h4.slots && x.h4.ksz == 8 && hb % 16 == 0 && GF_TRIE_RSUM_BYTES + hb <= std::min(cap, 96u * 1024u))
             L.h4_bytes = (uint32_t)hb;
-        if (x.lxc.slots && x.lxc.ksz == 20 && lb % 16 == 0 && GF_TRIE_RSUM_BYTES + L.h4_bytes + lb <= cap)
+        const uint32_t h4b = L.h4set ? 4u << L.h4bits : L.h4_bytes;
+        if (!L.lxset && x.lxc.slots && x.lxc.ksz == 20 && lb % 16 == 0 && GF_TRIE_RSUM_BYTES + h4b + lb <= cap)
             L.lxc_bytes = (uint32_t)lb;
-        const uint32_t lds = GF_TRIE_RSUM_BYTES + L.h4_bytes + L.lxc_bytes;
+        const uint32_t lds = GF_TRIE_RSUM_BYTES + h4b + (L.lxset ? 4u << L.lxbits : L.lxc_bytes);
         static uint32_t lds_set = 0;
         if (lds > lds_set) {
             if (hip_ok(hipFuncSetAttribute((const void *)k_xdp_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),

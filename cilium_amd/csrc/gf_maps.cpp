@@ -325,6 +325,40 @@ int Map::push(hipStream_t s) {
     return 0;
 }
 
+int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero) {
+    std::lock_guard<std::recursive_mutex> g(mu);
+    if (is_lpm() || ksz != kind || (kind != 8 && kind != 20)) return -EINVAL;
+    if (aset_gen != host_gen || aset_kind != kind || !d_aset.p) {
+        int r;
+        if ((r = pull())) return r;
+        std::vector<uint32_t> a;
+        bool z = false;
+        uint32_t w[5];
+        for (uint64_t i = 0; i < (ht.slots.empty() ? 0 : ht.nslots); i++) {
+            if (ht.state(i) != GF_SLOT_FULL) continue;
+            memcpy(w, &ht.slots[i * ht.slot_size], kind);
+            uint32_t x;
+            if (kind == 8) { if (w[0] != 32u) continue; x = w[1]; }
+            else { if (w[1] | w[2] | w[3] || w[4] != 1u) continue; x = w[0]; }
+            if (x) a.push_back(x); else z = true;
+        }
+        uint32_t b = 4;                                  // load <= 1/2
+        while ((1ull << b) < 2ull * a.size()) b++;
+        if ((1ull << b) > max_slots) return -E2BIG;
+        std::vector<uint32_t> t(1u << b, 0u);
+        for (uint32_t x : a) {
+            uint32_t k = gf_aset_home(x, b);
+            while (t[k] && t[k] != x) k = (k + 1) & ((1u << b) - 1);
+            t[k] = x;
+        }
+        if ((r = d_aset.ensure(t.size() * 4))) return r;
+        if (hip_ok(hipMemcpy(d_aset.p, t.data(), t.size() * 4, hipMemcpyHostToDevice), "push address set")) return -EIO;
+        aset_gen = host_gen; aset_kind = kind; aset_bits = b; aset_zero = z;
+    }
+    *set = (const uint32_t *)d_aset.p; *bits = aset_bits; *zero = aset_zero;
+    return 0;
+}
+
 gf_htab_desc Map::hdesc() {
     gf_htab_desc d{};
     d.slots = (uint8_t *)d_slots.p;
