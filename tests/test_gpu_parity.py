@@ -67,6 +67,47 @@ def test_config1_xdp_scaled():
     assert 0.05 < (r == 1).mean() < 0.95
 
 
+def test_xdp_address_sets_edge_keys():
+    """k_xdp_lds's compact address sets (the /32 hash and cilium_lxc's IPv4 keys in
+    LDS): address 0 in both (its own flag), a /32 map key whose prefixlen is not 32
+    (never matched: the lookup key is {32, saddr}), and a map update between two
+    calls (the set is rebuilt) — verdicts equal the oracle's."""
+    from cilium_amd import bpf
+    sc = synth.config1(n_packets=20_000, n_lpm=2_000, n_fix=500, n_ep=256)
+    rng = np.random.default_rng(5)
+    x = np.uint32(synth.ip4("198.51.100.7"))
+    sc.maps["cilium_cidr_v4_fix"].keys = np.concatenate(
+        [sc.maps["cilium_cidr_v4_fix"].keys, synth.lpm4_keys([32, 24], np.array([0, x], np.uint32))])
+    sc.maps["cilium_cidr_v4_fix"].vals = np.concatenate([sc.maps["cilium_cidr_v4_fix"].vals, np.ones((2, 1), np.uint8)])
+    lx = sc.maps["cilium_lxc"]
+    lx.keys = np.concatenate([lx.keys, synth.endpoint_keys4(np.array([0], np.uint32))])
+    lx.vals = np.concatenate([lx.vals, lx.vals[:1]])
+    pk = sc.batches[0]
+    n = pk.n
+    ipv4 = (pk.frames[:, 12] == 8) & (pk.frames[:, 13] == 0) & (pk.lens >= 34)
+    rows = np.nonzero(ipv4)[0]
+    pick = rng.choice(rows, 600, replace=False)
+    ep0 = synth.be32_bytes([0])[0]
+    pk.frames[pick[:200], 26:30] = ep0                              # saddr 0.0.0.0: in the /32 set
+    pk.frames[pick[200:400], 30:34] = ep0                           # daddr 0.0.0.0: an endpoint
+    pk.frames[pick[400:], 26:30] = synth.be32_bytes([x])[0]         # only a /24 key holds x
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    v = dp.xdp(DeviceBatch(pk))
+    torch.cuda.synchronize()
+    r = ref.xdp(pk)
+    _cmp_struct(v.cpu().numpy(), r, "xdp edge keys")
+    assert (r[pick[:200]] == 1).all()
+    # a /32 for x through the map API: the next call sees it
+    k = synth.lpm4_keys([32], np.array([x], np.uint32))[0]
+    bpf.UpdateElement(dp.fd["cilium_cidr_v4_fix"], k.tobytes(), bytes([1]))
+    ref.m["cilium_cidr_v4_fix"].update(k.tobytes(), bytes([1]))
+    v = dp.xdp(DeviceBatch(pk))
+    torch.cuda.synchronize()
+    r2 = ref.xdp(pk)
+    _cmp_struct(v.cpu().numpy(), r2, "xdp after update")
+    assert (r2[pick[400:]] == 1).all()
+
+
 def test_config3_lb_scaled():
     sc = synth.config3(n_packets=200_000, n_svc=5_000)
     dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
