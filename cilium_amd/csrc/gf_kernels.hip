@@ -320,7 +320,22 @@ struct XdpDev {
     gf_htab_desc h4, h6, lxc;
     gf_trie_desc l4, l6;
     uint32_t has_h4, has_h6;
+    // optional: the /32 map's and cilium_lxc's IPv4 keys as compact address sets
+    // (Map::addr_set) probed in place of their hash tables (IPv4 only)
+    const uint32_t *h4set, *lxset;
+    uint32_t h4bits, lxbits, h4zero, lxzero;
 };
+// Membership in a compact IPv4 address set (gf_aset_home; <= 1/2 load), in LDS
+// (k_xdp_lds) or in HBM / L2.
+__device__ __forceinline__ bool aset_has(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
+    if (!a) return zero != 0;
+    const uint32_t m = (1u << bits) - 1u;
+    for (uint32_t k = gf_aset_home(a, bits);; k = (k + 1) & m) {
+        const uint32_t v = t[k];
+        if (v == a) return true;
+        if (!v) return false;
+    }
+}
 
 __device__ __forceinline__ bool lxc_has4(const gf_htab_desc &lxc, uint32_t daddr) {
     uint32_t kw[5] = {daddr, 0, 0, 0, 1u};          // endpoint_key {ip4, pad.., family=1}
@@ -360,15 +375,28 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint
         ab += 10;
         if (x.has_h4) {
             ab += 9;
-            if (trie_lookup<1>(x.l4, &sa)) drop = true;
+            bool cov;
+            if (x.l4.rsum) {                            // the root summary: covered / has a node / neither
+                const uint32_t idx = ((sa & 0xffu) << 8) | ((sa >> 8) & 0xffu);
+                cov = (gload<uint64_t>(x.l4.rsum + (idx >> 6)) >> (idx & 63)) & 1ull;
+                if (!cov && ((gload<uint64_t>(x.l4.rsum + 1024 + (idx >> 6)) >> (idx & 63)) & 1ull))
+                    cov = trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
+            } else {
+                cov = trie_lookup<1>(x.l4, &sa);
+            }
+            if (cov) drop = true;
             else {
                 ab += 9;
-                if (GF_XDP_PRE < 1) hl.load(x.h4, key_hash<8>(kw));
-                drop = probe2<8, GF_XDP_U, 0>(x.h4, kw, kw, hl, false).f >= 0;
+                if (x.h4set) drop = aset_has(x.h4set, x.h4bits, x.h4zero, sa);
+                else {
+                    if (GF_XDP_PRE < 1) hl.load(x.h4, key_hash<8>(kw));
+                    drop = probe2<8, GF_XDP_U, 0>(x.h4, kw, kw, hl, false).f >= 0;
+                }
             }
         }
         if (drop) return XDP_DROP_;
         ab += 20;
+        if (x.lxset) return aset_has(x.lxset, x.lxbits, x.lxzero, lk[0]) ? XDP_PASS_ : XDP_DROP_;
         if (GF_XDP_PRE < 2) ll.load(x.lxc, key_hash<20>(lk));
         return probe2<20, GF_XDP_U, 0>(x.lxc, lk, lk, ll, false).f >= 0 ? XDP_PASS_ : XDP_DROP_;
     }
@@ -432,16 +460,7 @@ struct XdpLds {
     const uint32_t *h4set, *lxset;                 // or the tables' compact address sets (Map::addr_set)
     uint32_t h4bits, lxbits, h4zero, lxzero;
 };
-// Membership in a compact IPv4 address set held in LDS (gf_aset_home; <= 1/2 load).
-__device__ __forceinline__ bool aset_has(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
-    if (!a) return zero != 0;
-    const uint32_t m = (1u << bits) - 1u;
-    for (uint32_t k = gf_aset_home(a, bits);; k = (k + 1) & m) {
-        const uint32_t v = t[k];
-        if (v == a) return true;
-        if (!v) return false;
-    }
-}
+
 // Exact-match probe over a slot array held in LDS (layout as in HBM).
 template <int KSZ>
 __device__ __forceinline__ bool lds_has(const uint8_t *slots, uint64_t mask, uint32_t slot_size, const uint32_t *kw,
@@ -4024,6 +4043,13 @@ uint32_t stream_grid(uint32_t n, uint32_t per_block = BLOCK) {
 }
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
+// The prefilter's compact address sets (Map::addr_set) for XdpDev, when they build.
+void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, XdpDev &x) {
+    static const bool no_sets = getenv("GF_XDP_NOSETS") != nullptr;     // diagnosis: the hash tables
+    if (no_sets) return;
+    if (h4 && h4->addr_set(8, 8192, &x.h4set, &x.h4bits, &x.h4zero)) x.h4set = nullptr;
+    if (lxc && lxc->addr_set(20, 8192, &x.lxset, &x.lxbits, &x.lxzero)) x.lxset = nullptr;
+}
 
 // ---- locking and cross-stream ordering of the calls that share the device
 // workspaces (ws(), pipe_ws(), eg_ws(), px_ws(), the event / partition / GC
@@ -4127,6 +4153,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
         (r = push_map(p->m6l, s)) || (r = push_map(p->lxc, s)))
         return r;
     XdpDev x{};
+    xdp_sets(p->m4h, p->lxc, x);
     if (p->m4h) { x.h4 = p->m4h->hdesc(); x.has_h4 = 1; }
     if (p->m6h) { x.h6 = p->m6h->hdesc(); x.has_h6 = 1; }
     if (p->m4l) x.l4 = p->m4l->tdesc();
@@ -4141,9 +4168,8 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
         XdpLds L{};
         // the /32 hash and the endpoint keys as compact address sets (4 B a slot), else
         // their slot arrays when those fit the budget
-        static const bool no_sets = getenv("GF_XDP_NOSETS") != nullptr;     // diagnosis
-        if (!no_sets && p->m4h->addr_set(8, 8192, &L.h4set, &L.h4bits, &L.h4zero)) L.h4set = nullptr;
-        if (!no_sets && p->lxc->addr_set(20, 8192, &L.lxset, &L.lxbits, &L.lxzero)) L.lxset = nullptr;
+        L.h4set = x.h4set; L.h4bits = x.h4bits; L.h4zero = x.h4zero;
+        L.lxset = x.lxset; L.lxbits = x.lxbits; L.lxzero = x.lxzero;
         const uint64_t hb = (uint64_t)(x.h4.mask + 1) * x.h4.slot_size, lb = (uint64_t)(x.lxc.mask + 1) * x.lxc.slot_size;
         if (!L.h4set && x.h4.slots && x.h4.ksz == 8 && hb % 16 == 0 && GF_TRIE_RSUM_BYTES + hb <= std::min(cap, 96u * 1024u))
             L.h4_bytes = (uint32_t)hb;
@@ -4995,6 +5021,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
         if (x.m4l) P.x.l4 = x.m4l->tdesc();
         if (x.m6l) P.x.l6 = x.m6l->tdesc();
         P.x.lxc = x.lxc->hdesc();
+        xdp_sets(x.m4h, x.lxc, P.x);
         P.has_xdp = 1;
     }
     if (p->lb) {
