@@ -118,8 +118,9 @@ struct Map : Obj {
     int push(hipStream_t s);          // host -> device if !dev_valid / trie dirty
     // The IPv4 addresses of the keys as a compact open-addressing set for a
     // kernel's LDS (kind 8: {prefixlen 32, addr} keys; kind 20: endpoint keys
-    // {addr, 0, 0, 0, family 1}); rebuilt when the map changed.  -E2BIG past
-    // max_slots, -EINVAL for another key size.
+    // {addr, 0, 0, 0, family 1}, followed by a second array: each address's slot
+    // in the table); rebuilt when the map changed.  zero: address 0's slot + 1
+    // (0: absent).  -E2BIG past max_slots, -EINVAL for another key size.
     int addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero);
     DevBuf d_aset;
     uint64_t aset_gen = ~0ull;

@@ -325,6 +325,16 @@ struct XdpDev {
     const uint32_t *h4set, *lxset;
     uint32_t h4bits, lxbits, h4zero, lxzero;
 };
+// The table slot of an address in an endpoint-key set (its second array), or -1.
+__device__ __forceinline__ int64_t aset_slot(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
+    if (!a) return (int64_t)zero - 1;
+    const uint32_t m = (1u << bits) - 1u;
+    for (uint32_t k = gf_aset_home(a, bits);; k = (k + 1) & m) {
+        const uint32_t v = t[k];
+        if (v == a) return (int64_t)t[(1u << bits) + k];
+        if (!v) return -1;
+    }
+}
 // Membership in a compact IPv4 address set (gf_aset_home; <= 1/2 load), in LDS
 // (k_xdp_lds) or in HBM / L2.
 __device__ __forceinline__ bool aset_has(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
@@ -1822,6 +1832,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
 // tail call and completes their pipeline records in place.
 struct NetdevDev {
     gf_htab_desc lxc;
+    const uint32_t *lxset;         // cilium_lxc's IPv4 keys: address set + slots (Map::addr_set), or null
+    uint32_t lxbits, lxzero;
     uint32_t flags, fixed_secctx;
     uint32_t router6[2];           // first 8 bytes of ROUTER_IP (LE words)
 };
@@ -1908,7 +1920,7 @@ __device__ int pipe_netdev(const NetdevDev &N, Row &w, const PktHdr &h, uint32_t
         if (len < 34) return D_INVALID;                 // revalidate_data
         sec = (N.flags & GF_NETDEV_F_FIXED_SECCTX) ? N.fixed_secctx : 2u;   // derive_ipv4_sec_ctx: WORLD_ID
         uint32_t kw[5] = {w.r32(30), 0, 0, 0, 1u};      // lookup_ip4_endpoint (post-LB daddr)
-        const int64_t f = ht_find<20>(N.lxc, kw, key_hash<20>(kw));
+        const int64_t f = N.lxset ? aset_slot(N.lxset, N.lxbits, N.lxzero, kw[0]) : ht_find<20>(N.lxc, kw, key_hash<20>(kw));
         ab += 20;
         if (f < 0) return TC_OK;
         const uint8_t *ep = ht_val(N.lxc, f);
@@ -5034,6 +5046,8 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     }
     if ((r = push_map(p->lxc, s))) return r;
     P.nd.lxc = p->lxc->hdesc();
+    if (getenv("GF_XDP_NOSETS") || p->lxc->addr_set(20, 8192, &P.nd.lxset, &P.nd.lxbits, &P.nd.lxzero))
+        P.nd.lxset = nullptr;
     P.nd.flags = p->cfg.netdev.flags;
     P.nd.fixed_secctx = p->cfg.netdev.fixed_secctx;
     memcpy(P.nd.router6, p->cfg.netdev.router_ip6, 8);

@@ -331,8 +331,8 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint3
     if (aset_gen != host_gen || aset_kind != kind || !d_aset.p) {
         int r;
         if ((r = pull())) return r;
-        std::vector<uint32_t> a;
-        bool z = false;
+        std::vector<std::pair<uint32_t, uint32_t>> a;   // (address, slot)
+        uint32_t z = 0;
         uint32_t w[5];
         for (uint64_t i = 0; i < (ht.slots.empty() ? 0 : ht.nslots); i++) {
             if (ht.state(i) != GF_SLOT_FULL) continue;
@@ -340,16 +340,18 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint3
             uint32_t x;
             if (kind == 8) { if (w[0] != 32u) continue; x = w[1]; }
             else { if (w[1] | w[2] | w[3] || w[4] != 1u) continue; x = w[0]; }
-            if (x) a.push_back(x); else z = true;
+            if (x) a.push_back({x, (uint32_t)i}); else z = (uint32_t)i + 1;
         }
         uint32_t b = 4;                                  // load <= 1/2
         while ((1ull << b) < 2ull * a.size()) b++;
-        if ((1ull << b) > max_slots) return -E2BIG;
-        std::vector<uint32_t> t(1u << b, 0u);
-        for (uint32_t x : a) {
-            uint32_t k = gf_aset_home(x, b);
-            while (t[k] && t[k] != x) k = (k + 1) & ((1u << b) - 1);
-            t[k] = x;
+        if ((1ull << b) > max_slots || ht.nslots > 0xffffffffull) return -E2BIG;
+        // addresses, then (endpoint keys) the slot of each address in the table
+        std::vector<uint32_t> t((kind == 20 ? 2u : 1u) << b, 0u);
+        for (auto &e : a) {
+            uint32_t k = gf_aset_home(e.first, b);
+            while (t[k] && t[k] != e.first) k = (k + 1) & ((1u << b) - 1);
+            t[k] = e.first;
+            if (kind == 20) t[(1u << b) + k] = e.second;
         }
         if ((r = d_aset.ensure(t.size() * 4))) return r;
         if (hip_ok(hipMemcpy(d_aset.p, t.data(), t.size() * 4, hipMemcpyHostToDevice), "push address set")) return -EIO;
