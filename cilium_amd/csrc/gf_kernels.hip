@@ -2721,6 +2721,8 @@ struct EgDev {
     const gf_lxc_dev *cfgs;
     const uint16_t *slot_of;
     gf_htab_desc ct4, ct6, lxc, tunnel;
+    const uint32_t *lxset;              // cilium_lxc's IPv4 keys: address set + slots (Map::addr_set), or null
+    uint32_t lxbits, lxzero;
     uint8_t *snap;                      // the frames, rewritten in place
     uint8_t *s6out, *d6out;             // IPv6 addresses of the local deliveries (handle_policy's columns)
     uint32_t stride, now, host_ifindex, encap_ifindex;
@@ -3143,7 +3145,8 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
                     K[4] = hz_key(&fs, &fs, 1, 0u, 0u, 0x2ffu, pd);
                     K[5] = hz_key(&fd, &fd, 1, 0u, 0u, 0x2ffu, pd);
                     const bool vip = !(r.eflags & GF_EG_F_LB) && vip4_has(E, fd);
-                    const bool dlv = (E.lxc.slots && lxc_has4(E.lxc, fd)) || (E.loopback && fd == E.loopback);
+                    const bool dlv = (E.lxc.slots && (E.lxset ? aset_has(E.lxset, E.lxbits, E.lxzero, fd) : lxc_has4(E.lxc, fd))) ||
+                                     (E.loopback && fd == E.loopback);
                     hfl = (r.nh == 1 ? GF_HZ_ICMP : 0u) | (vip ? GF_HZ_VIP : 0u) |
                           ((r.eflags & GF_EG_F_LOOPBACK) ? GF_HZ_LOOP : 0u) | (dlv ? GF_HZ_DLV : 0u);
                 }
@@ -3583,7 +3586,7 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
     const uint32_t dip = w.r32(30);
     if (E.lxc.slots) {                                  // lookup_ip4_endpoint
         uint32_t kw[5] = {dip, 0, 0, 0, 1u};
-        const int64_t fe = ht_find<20>(E.lxc, kw, key_hash<20>(kw));
+        const int64_t fe = E.lxset ? aset_slot(E.lxset, E.lxbits, E.lxzero, dip) : ht_find<20>(E.lxc, kw, key_hash<20>(kw));
         ab += 20;
         if (fe >= 0) {
             const uint8_t *ep = ht_val(E.lxc, fe);
@@ -5591,7 +5594,10 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.ct4 = cfg_ct4; E.ct6 = cfg_ct6;
     E.s6out = (uint8_t *)ew.s6.p; E.d6out = (uint8_t *)ew.d6.p;
     memcpy(E.router6, node.router_ip6, 16); memcpy(E.host6, node.host_ip6, 16);
-    if (lxc) E.lxc = lxc->hdesc();
+    if (lxc) {
+        E.lxc = lxc->hdesc();
+        if (getenv("GF_XDP_NOSETS") || lxc->addr_set(20, 8192, &E.lxset, &E.lxbits, &E.lxzero)) E.lxset = nullptr;
+    }
     if (tun) E.tunnel = tun->hdesc();
     E.snap = wsnap; E.stride = S; E.now = now_sec; E.host_ifindex = host_ifindex();
     E.encap_ifindex = node.encap_ifindex;
