@@ -2721,8 +2721,8 @@ struct EgDev {
     const gf_lxc_dev *cfgs;
     const uint16_t *slot_of;
     gf_htab_desc ct4, ct6, lxc, tunnel;
-    const uint32_t *lxset;              // cilium_lxc's IPv4 keys: address set + slots (Map::addr_set), or null
-    uint32_t lxbits, lxzero;
+    const uint32_t *lxset, *tnset;      // cilium_lxc's / the tunnel map's IPv4 keys: address set + slots
+    uint32_t lxbits, lxzero, tnbits, tnzero;   // (Map::addr_set), or null
     uint8_t *snap;                      // the frames, rewritten in place
     uint8_t *s6out, *d6out;             // IPv6 addresses of the local deliveries (handle_policy's columns)
     uint32_t stride, now, host_ifindex, encap_ifindex;
@@ -3611,7 +3611,7 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
     }
     if (E.encap_ifindex && E.tunnel.slots) {            // encap_and_redirect (lib/encap.h)
         uint32_t kw[5] = {dip & E.ipv4_mask, 0, 0, 0, 1u};
-        const int64_t ft = ht_find<20>(E.tunnel, kw, key_hash<20>(kw));
+        const int64_t ft = E.tnset ? aset_slot(E.tnset, E.tnbits, E.tnzero, kw[0]) : ht_find<20>(E.tunnel, kw, key_hash<20>(kw));
         ab += 20;
         if (ft >= 0) {
             o.tunnel_ip = __builtin_bswap32(gload<uint32_t>(ht_val(E.tunnel, ft)));
@@ -5598,7 +5598,10 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         E.lxc = lxc->hdesc();
         if (getenv("GF_XDP_NOSETS") || lxc->addr_set(20, 8192, &E.lxset, &E.lxbits, &E.lxzero)) E.lxset = nullptr;
     }
-    if (tun) E.tunnel = tun->hdesc();
+    if (tun) {
+        E.tunnel = tun->hdesc();
+        if (getenv("GF_XDP_NOSETS") || tun->addr_set(20, 8192, &E.tnset, &E.tnbits, &E.tnzero)) E.tnset = nullptr;
+    }
     E.snap = wsnap; E.stride = S; E.now = now_sec; E.host_ifindex = host_ifindex();
     E.encap_ifindex = node.encap_ifindex;
     E.cluster_range = node.ipv4_cluster_range; E.cluster_mask = node.ipv4_cluster_mask;
