@@ -125,6 +125,7 @@ struct Map : Obj {
     DevBuf d_aset;
     uint64_t aset_gen = ~0ull;
     uint32_t aset_kind = 0, aset_bits = 0, aset_zero = 0;
+    bool aset_big = false;             // the last build at aset_gen did not fit max_slots
     void device_modified() { host_valid = false; dev_gen++; }
     // Element access on the HBM replica of a device-authoritative hash map (the
     // datapath wrote it last): walks the key's probe sequence with small reads

@@ -328,6 +328,7 @@ int Map::push(hipStream_t s) {
 int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero) {
     std::lock_guard<std::recursive_mutex> g(mu);
     if (is_lpm() || ksz != kind || (kind != 8 && kind != 20)) return -EINVAL;
+    if (aset_gen == host_gen && aset_kind == kind && aset_big) return -E2BIG;   // this generation did not fit
     if (aset_gen != host_gen || aset_kind != kind || !d_aset.p) {
         int r;
         if ((r = pull())) return r;
@@ -344,7 +345,10 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint3
         }
         uint32_t b = 4;                                  // load <= 1/2
         while ((1ull << b) < 2ull * a.size()) b++;
-        if ((1ull << b) > max_slots || ht.nslots > 0xffffffffull) return -E2BIG;
+        if ((1ull << b) > max_slots || ht.nslots > 0xffffffffull) {
+            aset_gen = host_gen; aset_kind = kind; aset_big = true;
+            return -E2BIG;
+        }
         // addresses, then (endpoint keys) the slot of each address in the table
         std::vector<uint32_t> t((kind == 20 ? 2u : 1u) << b, 0u);
         for (auto &e : a) {
@@ -355,7 +359,7 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint3
         }
         if ((r = d_aset.ensure(t.size() * 4))) return r;
         if (hip_ok(hipMemcpy(d_aset.p, t.data(), t.size() * 4, hipMemcpyHostToDevice), "push address set")) return -EIO;
-        aset_gen = host_gen; aset_kind = kind; aset_bits = b; aset_zero = z;
+        aset_gen = host_gen; aset_kind = kind; aset_bits = b; aset_zero = z; aset_big = false;
     }
     *set = (const uint32_t *)d_aset.p; *bits = aset_bits; *zero = aset_zero;
     return 0;
