@@ -51,6 +51,9 @@ using namespace gfd;
 __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
+#ifndef GF_PERM_VEC
+#define GF_PERM_VEC 1       // k_ing_groups: the bucket's indices read four at a time (16-B loads; 2.625 -> 2.615 ms)
+#endif
 #ifndef GF_EG_MINW
 #define GF_EG_MINW 3        // k_eg_groups: min waves per SIMD (4 spills: 1.65 vs 1.60 ms, egress leg)
 #endif
@@ -1713,10 +1716,23 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = rec[i];
         ln.rc.slot = ~0u;                                // a new bucket: new flow groups
+#if GF_PERM_VEC
+        uint4 pw = make_uint4(0, 0, 0, 0);               // perm[j & ~3 .. +3], j = b + k + 2
+        if (c > 2) pw = *reinterpret_cast<const uint4 *>(perm + ((b + 2) & ~3u));
+#endif
         for (uint32_t k = 0; k < c; k++) {
             // the next record and the index after it are in flight while packet k runs
             uint32_t in2 = 0;
+#if GF_PERM_VEC
+            if (k + 2 < c) {
+                const uint32_t j = b + k + 2;
+                if (!(j & 3u) && k) pw = *reinterpret_cast<const uint4 *>(perm + j);
+                const uint32_t q = j & 3u;
+                in2 = q == 0 ? pw.x : q == 1 ? pw.y : q == 2 ? pw.z : pw.w;
+            }
+#else
             if (k + 2 < c) in2 = perm[b + k + 2];
+#endif
 #if GF_PREFETCH_REC
             gf_rec rn;
             if (k + 1 < c) rn = rec[inx];
@@ -4401,7 +4417,7 @@ static int ws_grow(uint32_t n) {
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
     if ((r = grow(w.rec, (size_t)n * sizeof(gf_rec))) || (r = grow(w.keys, (size_t)n * 4)) ||
-        (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4)) ||
+        (r = grow(w.skeys, (size_t)n * 4)) || (r = grow(w.perm, (size_t)n * 4 + 16)) ||
         (r = grow(w.off, (size_t)n * 4)) || (r = grow(w.order, (size_t)n * 8)) ||
         (r = grow(w.sched, GF_SCHED_WORDS * 4)))
         return r;
