@@ -121,7 +121,7 @@ struct Map : Obj {
     // {addr, 0, 0, 0, family 1}, followed by a second array: each address's slot
     // in the table); rebuilt when the map changed.  zero: address 0's slot + 1
     // (0: absent).  -E2BIG past max_slots, -EINVAL for another key size.
-    int addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero);
+    int addr_set(uint32_t kind, uint32_t max_slots, hipStream_t s, const uint32_t **set, uint32_t *bits, uint32_t *zero);
     DevBuf d_aset;
     uint64_t aset_gen = ~0ull;
     uint32_t aset_kind = 0, aset_bits = 0, aset_zero = 0;

@@ -4075,11 +4075,11 @@ uint32_t stream_grid(uint32_t n, uint32_t per_block = BLOCK) {
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
 // The prefilter's compact address sets (Map::addr_set) for XdpDev, when they build.
-void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, XdpDev &x) {
+void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, XdpDev &x, hipStream_t s) {
     static const bool no_sets = getenv("GF_XDP_NOSETS") != nullptr;     // diagnosis: the hash tables
     if (no_sets) return;
-    if (h4 && h4->addr_set(8, 8192, &x.h4set, &x.h4bits, &x.h4zero)) x.h4set = nullptr;
-    if (lxc && lxc->addr_set(20, 8192, &x.lxset, &x.lxbits, &x.lxzero)) x.lxset = nullptr;
+    if (h4 && h4->addr_set(8, 8192, s, &x.h4set, &x.h4bits, &x.h4zero)) x.h4set = nullptr;
+    if (lxc && lxc->addr_set(20, 8192, s, &x.lxset, &x.lxbits, &x.lxzero)) x.lxset = nullptr;
 }
 
 // ---- locking and cross-stream ordering of the calls that share the device
@@ -4184,7 +4184,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
         (r = push_map(p->m6l, s)) || (r = push_map(p->lxc, s)))
         return r;
     XdpDev x{};
-    xdp_sets(p->m4h, p->lxc, x);
+    xdp_sets(p->m4h, p->lxc, x, s);
     if (p->m4h) { x.h4 = p->m4h->hdesc(); x.has_h4 = 1; }
     if (p->m6h) { x.h6 = p->m6h->hdesc(); x.has_h6 = 1; }
     if (p->m4l) x.l4 = p->m4l->tdesc();
@@ -5052,7 +5052,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
         if (x.m4l) P.x.l4 = x.m4l->tdesc();
         if (x.m6l) P.x.l6 = x.m6l->tdesc();
         P.x.lxc = x.lxc->hdesc();
-        xdp_sets(x.m4h, x.lxc, P.x);
+        xdp_sets(x.m4h, x.lxc, P.x, s);
         P.has_xdp = 1;
     }
     if (p->lb) {
@@ -5065,7 +5065,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     }
     if ((r = push_map(p->lxc, s))) return r;
     P.nd.lxc = p->lxc->hdesc();
-    if (getenv("GF_XDP_NOSETS") || p->lxc->addr_set(20, 8192, &P.nd.lxset, &P.nd.lxbits, &P.nd.lxzero))
+    if (getenv("GF_XDP_NOSETS") || p->lxc->addr_set(20, 8192, s, &P.nd.lxset, &P.nd.lxbits, &P.nd.lxzero))
         P.nd.lxset = nullptr;
     P.nd.flags = p->cfg.netdev.flags;
     P.nd.fixed_secctx = p->cfg.netdev.fixed_secctx;
@@ -5612,11 +5612,11 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     memcpy(E.router6, node.router_ip6, 16); memcpy(E.host6, node.host_ip6, 16);
     if (lxc) {
         E.lxc = lxc->hdesc();
-        if (getenv("GF_XDP_NOSETS") || lxc->addr_set(20, 8192, &E.lxset, &E.lxbits, &E.lxzero)) E.lxset = nullptr;
+        if (getenv("GF_XDP_NOSETS") || lxc->addr_set(20, 8192, s, &E.lxset, &E.lxbits, &E.lxzero)) E.lxset = nullptr;
     }
     if (tun) {
         E.tunnel = tun->hdesc();
-        if (getenv("GF_XDP_NOSETS") || tun->addr_set(20, 8192, &E.tnset, &E.tnbits, &E.tnzero)) E.tnset = nullptr;
+        if (getenv("GF_XDP_NOSETS") || tun->addr_set(20, 8192, s, &E.tnset, &E.tnbits, &E.tnzero)) E.tnset = nullptr;
     }
     E.snap = wsnap; E.stride = S; E.now = now_sec; E.host_ifindex = host_ifindex();
     E.encap_ifindex = node.encap_ifindex;

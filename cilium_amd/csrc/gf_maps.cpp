@@ -325,7 +325,7 @@ int Map::push(hipStream_t s) {
     return 0;
 }
 
-int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint32_t *bits, uint32_t *zero) {
+int Map::addr_set(uint32_t kind, uint32_t max_slots, hipStream_t s, const uint32_t **set, uint32_t *bits, uint32_t *zero) {
     std::lock_guard<std::recursive_mutex> g(mu);
     if (is_lpm() || ksz != kind || (kind != 8 && kind != 20)) return -EINVAL;
     if (aset_gen == host_gen && aset_kind == kind && aset_big) return -E2BIG;   // this generation did not fit
@@ -358,7 +358,10 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, const uint32_t **set, uint3
             if (kind == 20) t[(1u << b) + k] = e.second;
         }
         if ((r = d_aset.ensure(t.size() * 4))) return r;
-        if (hip_ok(hipMemcpy(d_aset.p, t.data(), t.size() * 4, hipMemcpyHostToDevice), "push address set")) return -EIO;
+        // on the call's stream: ordered after the previous call's kernels (CallOrder)
+        if (hip_ok(hipMemcpyAsync(d_aset.p, t.data(), t.size() * 4, hipMemcpyHostToDevice, s), "push address set") ||
+            hip_ok(hipStreamSynchronize(s), "address set sync"))
+            return -EIO;
         aset_gen = host_gen; aset_kind = kind; aset_bits = b; aset_zero = z; aset_big = false;
     }
     *set = (const uint32_t *)d_aset.p; *bits = aset_bits; *zero = aset_zero;
