@@ -51,6 +51,9 @@ using namespace gfd;
 __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
+#ifndef GF_ING_BINS_WAVE
+#define GF_ING_BINS_WAVE 0  // k_ing_groups: reason / action bins aggregated over the active lanes (no effect: 2.728 ms both)
+#endif
 #ifndef GF_PERM_VEC
 #define GF_PERM_VEC 1       // k_ing_groups: the bucket's indices read four at a time (16-B loads; 2.625 -> 2.615 ms)
 #endif
@@ -1663,7 +1666,14 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     } else if (!(GF_DIAG & 1)) {
         out[i] = o;
     }
-    if (stats && !(GF_DIAG & 2)) { st.add(o.reason); st.add(256 + o.action); ln.sc.add(r.len, ab, o.ct_ret & 3u, st); }
+    if (stats && !(GF_DIAG & 2)) {
+#if GF_ING_BINS_WAVE
+        st.bins_wave(true, o.reason, o.action);         // the active lanes' bins, one LDS atomic per distinct pair
+#else
+        st.add(o.reason); st.add(256 + o.action);
+#endif
+        ln.sc.add(r.len, ab, o.ct_ret & 3u, st);
+    }
 }
 
 __device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, int added, uint32_t *ct_count,
