@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpuflow.so")
-# diagnostic ablation builds only (tools/diag.sh); never set in tests, smoke or bench runs
+# diagnostic / variant builds only (tools/diag.sh, tools/variants.sh); never set in tests, smoke or bench runs
 if os.environ.get("GPUFLOW_DIAG_LIB"):
     LIB_PATH = os.environ["GPUFLOW_DIAG_LIB"]
 
@@ -209,9 +209,16 @@ def source_sha():
     return h.hexdigest()[:16]
 
 
-# The in-tree library must be the one its sources build: a stale binary fails
-# here instead of running (ablation builds of tools/ carry no id).
-if not os.environ.get("GPUFLOW_DIAG_LIB") and os.path.isdir(os.path.join(_HERE, "csrc")):
-    if BUILD_ID != source_sha():
-        raise ImportError(f"libgpuflow.so was built from sources {BUILD_ID}, the tree holds {source_sha()}: "
+# The library must be the one the tree's sources build: a stale binary fails here
+# instead of running.  Variant builds of tools/ (GPUFLOW_DIAG_LIB) carry the same
+# digest plus "+<variant>" (tools/variants.sh, tools/diag.sh), so a variant compiled
+# from older sources — whose structs may no longer match this binding — fails too.
+if os.path.isdir(os.path.join(_HERE, "csrc")):
+    _want = source_sha()
+    if os.environ.get("GPUFLOW_DIAG_LIB"):
+        if not BUILD_ID.startswith(_want + "+"):
+            raise ImportError(f"variant library {LIB_PATH} was built from sources {BUILD_ID}, the tree holds "
+                              f"{_want}: rebuild it with tools/variants.sh build")
+    elif BUILD_ID != _want:
+        raise ImportError(f"libgpuflow.so was built from sources {BUILD_ID}, the tree holds {_want}: "
                           "run `python -c 'import __graft_entry__ as g; g.build()'`")

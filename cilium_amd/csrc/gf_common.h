@@ -29,7 +29,8 @@
 // datapath for membership ("is there a stored prefix covering addr"):
 // bpf_xdp.c:112 and maps.h:129,139 test the lookup result against NULL.  The
 // device form is therefore a coverage trie: a 2^R-entry root table followed by
-// 8-bit-stride nodes {full bitmap[256], child bitmap[256], child_base}.
+// 8-bit-stride 128-B nodes of four 32-B groups {full word, child word, first
+// child} (one group per 64 values of the byte; layout below, GF_TRIE_GROUP_BYTES).
 #pragma once
 #include <stdint.h>
 

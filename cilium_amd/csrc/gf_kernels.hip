@@ -25,6 +25,7 @@
 #include <chrono>
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <string.h>
 
 using namespace gf;
@@ -51,6 +52,7 @@ using namespace gfd;
 __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
+#endif
 #ifndef GF_ING_BINS_WAVE
 #define GF_ING_BINS_WAVE 0  // k_ing_groups: reason / action bins aggregated over the active lanes (no effect: 2.728 ms both)
 #endif
@@ -66,7 +68,6 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_MEMO6
 #define GF_MEMO6 2          // IPv6 buckets (1 fits 4 blocks' lane state in LDS, but the 128-VGPR
                             // budget that occupancy 4 then imposes spills: 1.93 vs 1.20 ms, config 5)
-#endif
 #endif
 
 // ---------------------------------------------------------------- constants
@@ -4218,13 +4219,21 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
         if (!L.lxset && x.lxc.slots && x.lxc.ksz == 20 && lb % 16 == 0 && GF_TRIE_RSUM_BYTES + h4b + lb <= cap)
             L.lxc_bytes = (uint32_t)lb;
         const uint32_t lds = GF_TRIE_RSUM_BYTES + h4b + (L.lxset ? 4u << L.lxbits : L.lxc_bytes);
-        static uint32_t lds_set = 0;
-        if (lds > lds_set) {
-            if (hip_ok(hipFuncSetAttribute((const void *)k_xdp_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                       "k_xdp_lds lds"))
-                return -EIO;
-            lds_set = lds;
+        // the address sets count against the budget too: larger maps take k_xdp,
+        // which reads the same sets and the root summary through L2
+        static std::atomic<uint32_t> lds_set{0};
+        bool fits = lds <= std::max(cap, GF_TRIE_RSUM_BYTES);
+        if (fits && lds > lds_set.load()) {
+            fits = hipFuncSetAttribute((const void *)k_xdp_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+                   hipSuccess;
+            if (fits) {
+                uint32_t cur = lds_set.load();
+                while (lds > cur && !lds_set.compare_exchange_weak(cur, lds)) {}
+            } else {
+                (void)hipGetLastError();
+            }
         }
+        if (fits) {
         const uint32_t per_cu = lds <= 78u * 1024u ? 2u : 1u;
         static const uint32_t grid_env = getenv("GF_XDP_GRID") ? (uint32_t)atoi(getenv("GF_XDP_GRID")) : 0u;   // diagnosis
         const uint32_t grid = grid_env ? grid_env
@@ -4232,6 +4241,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
         hipLaunchKernelGGL(k_xdp_lds, dim3(grid), dim3(1024), lds, s, *pkts, x, L, verdict,
                            (unsigned long long *)stats_sink());
         return hip_ok(hipGetLastError(), "k_xdp_lds");
+        }
     }
     hipLaunchKernelGGL(k_xdp, dim3(stream_grid(pkts->n)), dim3(BLOCK), 0, s, *pkts, x, verdict,
                        (unsigned long long *)stats_sink());

@@ -11,8 +11,12 @@
 //   trie: prefixlen > max -> -EINVAL; NEW key when full -> -ENOSPC; lookup =
 //         longest stored prefix with len <= key.prefixlen that matches;
 //         get_next_key in post-order (more specific prefixes first).
-//   LRU_HASH is treated as HASH without eviction (parity mode; LRU eviction
-//   order is nondeterministic in the kernel — parity configs never fill).
+//   LRU_HASH never fails an insert (the kernel evicts instead): here an insert
+//   through the API or the datapath is accepted up to the slot array's 7/8
+//   load, and the deterministic LRU stand-in (gf_kernels.hip lru_evict, DESIGN.md
+//   §4) brings the map back under max_entries after the next classify call that
+//   binds it.  Between an API insert and that call GetMapInfo may report more
+//   than max_entries entries (documented deviation; tests/test_maps.py).
 #include "gf_internal.h"
 #include <string.h>
 #include <errno.h>
@@ -180,12 +184,20 @@ bool LpmKeyLess::operator()(const std::string &a, const std::string &b) const {
     return la > lb;   // post-order: the more specific prefix first
 }
 
+static uint64_t pow2ceil64(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
 // ------------------------------------------------------------------ Map
 Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
     : Obj(ObjKind::Map), type(t), ksz(k), vsz(v), max_entries(m), flags(f),
       lpm(LpmKeyLess{k > 4 ? k - 4 : 0}) {
     if (!is_lpm()) {
-        if (type == GF_MAP_TYPE_LRU_HASH) { fixed_capacity = true; ht.init(k, v, 0); ht.nslots = gf_pow2ceil32(std::max<uint32_t>(64, 2 * m)); }
+        // LRU maps: a fixed slot array of 4 x max_entries (the CT maps' factor), whose
+        // 7/8 load bounds inserts between two eviction sweeps (dev_insert_limit)
+        if (type == GF_MAP_TYPE_LRU_HASH) { fixed_capacity = true; ht.init(k, v, 0); ht.nslots = pow2ceil64(std::max<uint64_t>(64, 4ull * m)); }
         else ht.init(k, v, 64);
         // Maps of the CT shape (ipv4_ct_tuple / ipv6_ct_tuple -> ct_entry) and of the policy
         // shape (policy_key -> policy_entry) take their datapath layout at creation, while
@@ -232,6 +244,7 @@ void Map::set_value_codec(uint32_t c) {
     ht.codec = c;
     uint32_t hs = c == GF_VCODEC_CT ? 1u : (c == GF_VCODEC_POL ? 2u : 0u);
     if (hs != ht.hot_split) { ht.hot_split = hs; ht.rehash(ht.nslots); }
+    host_gen++;                 // a re-layout moves slots: derived caches (addr_set's slot indices) rebuild
     dev_valid = false;
 }
 
@@ -240,14 +253,10 @@ void Map::set_hash_mode(uint32_t m) {
     pull();
     ht.mode = m;
     if (!ht.slots.empty()) ht.rehash(ht.nslots);
+    host_gen++;
     dev_valid = false;
 }
 
-static uint64_t pow2ceil64(uint64_t x) {
-    uint64_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
-}
 
 // Maps the device inserts into (CT) get a slot array sized from max_entries
 // once, never rehashed by the device.  `factor` slots per entry: 4 for CT maps
@@ -259,6 +268,7 @@ void Map::make_fixed_capacity(uint32_t factor) {
     uint64_t want = pow2ceil64(std::max<uint64_t>(64, (uint64_t)factor * max_entries));
     fixed_capacity = true;
     if (want != ht.nslots) ht.rehash(want);
+    host_gen++;
     dev_valid = false;
 }
 
@@ -566,9 +576,9 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
         return 0;
     }
     if (fl == GF_EXIST) return -ENOENT;
-    if (ht.count >= max_entries) return -E2BIG;
+    if (ht.count >= dev_insert_limit(*this)) return -E2BIG;
     if (fixed_capacity) {
-        if ((ht.count + ht.tombs + 1) * 4 > ht.nslots * 3) ht.rehash(ht.nslots);
+        if (ht.tombs && (ht.count + ht.tombs + 1) * 4 > ht.nslots * 3) ht.rehash(ht.nslots);   // drop tombstones
     } else if ((ht.count + ht.tombs + 1) * 2 > ht.nslots) {
         ht.rehash(std::max<uint64_t>(64, gf_pow2ceil32((uint32_t)((ht.count + 1) * 4))));
     }

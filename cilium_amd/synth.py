@@ -439,12 +439,13 @@ def config1(n_packets=1_000_000, n_lpm=10_000, n_fix=2_000, n_ep=1_024, seed=0xC
 
 
 # ------------------------------------------------------------------ config 3: service LB
-def config3(n_packets=16_000_000, n_svc=100_000, seed=0xC1D40003, stride=64, max_entries=2_000_000,
-            redirect=True):
-    """BASELINE config 3 / SURVEY §8(d): bpf_lb.c, 100k services / ~1M backends."""
-    rng = np.random.default_rng(seed)
-    sc = Scenario("config3_lb")
-    vip = (ip4("10.96.0.0") + np.arange(n_svc)).astype(np.uint32)
+def lb4_population(rng, n_svc, vip_base):
+    """Config 3's service population: n_svc frontends from vip_base
+    (90% VIP:port, 10% L3-only), 1..19 backends each (mean 10) on 10.200/12, 30% on
+    a port other than the frontend's; lbmap rows as AddSVC2BPFMap writes them
+    (pkg/maps/lbmap/lbmap.go:320-371: slaves 1..count, then the master with count).
+    Returns (vip, l3only, fport, revnat, keys, vals)."""
+    vip = (vip_base + np.arange(n_svc)).astype(np.uint32)
     l3only = rng.random(n_svc) < 0.10
     ports = np.array([80, 443, 8080, 53, 6379, 5432, 9090, 3306, 8443, 11211], np.uint32)
     fport = np.where(l3only, 0, ports[rng.integers(0, len(ports), n_svc)]).astype(np.uint32)
@@ -460,6 +461,15 @@ def config3(n_packets=16_000_000, n_svc=100_000, seed=0xC1D40003, stride=64, max
     keys = np.concatenate([lb4_keys(vip[svc_of_be], fport[svc_of_be], slave), lb4_keys(vip, fport, np.zeros(n_svc))])
     vals = np.concatenate([lb4_vals(be_addr, be_port, np.zeros(nb), revnat[svc_of_be]),
                            lb4_vals(np.zeros(n_svc), np.zeros(n_svc), nbe, np.zeros(n_svc))])
+    return vip, l3only, fport, revnat, keys, vals
+
+
+def config3(n_packets=16_000_000, n_svc=100_000, seed=0xC1D40003, stride=64, max_entries=2_000_000,
+            redirect=True):
+    """BASELINE config 3 / SURVEY §8(d): bpf_lb.c, 100k services / ~1M backends."""
+    rng = np.random.default_rng(seed)
+    sc = Scenario("config3_lb")
+    vip, l3only, fport, revnat, keys, vals = lb4_population(rng, n_svc, ip4("10.96.0.0"))
     sc.add_map(MapSpec("cilium_lb4_services", HASH, 8, 12, max_entries, 0, keys, vals))
     rk, rv = revnat4_entries(revnat, vip, fport)
     rk, rv = dedup(rk, rv)
@@ -938,13 +948,16 @@ def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed
 
 
 # ------------------------------------------------------------------ config 4: full pipeline tables
-def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000, seed=0xC1D40004, **kw):
+def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000, seed=0xC1D40004,
+                   n_svc=100_000, **kw):
     """BASELINE config 4 / SURVEY §8(d): the tables of configs 1-3 on one node,
     composed as bpf_xdp -> bpf_lb -> bpf_netdev -> handle_policy.  Config 2's
     endpoints/policies/CT; config 1's prefilter (10k LPM prefixes + 2k /32s);
     a service VIP per endpoint for each of SERVICE_PORTS (one backend: the
     endpoint itself, 30% on another port), present in cilium_lxc as host
-    entries so the prefilter's endpoint check passes them.  Returns
+    entries so the prefilter's endpoint check passes them; and config 3's
+    service population (n_svc services / ~10 x n_svc backends on 10.98/15, the
+    traffic's lookups probe the same 2M-entry lbmap).  Returns
     (scenario, pairs, vip_ip[n_ep])."""
     # traffic arriving on the netdev carries WORLD_ID (derive_ipv4_sec_ctx, bpf_netdev.c:249-261):
     # most pairs are world peers, admitted by the endpoints' CIDR / L4-wildcard rules
@@ -983,7 +996,10 @@ def config4_tables(n_pairs=1 << 20, n_lpm=10_000, n_fix=2_000, ct_max=64_000_000
     keys = np.concatenate([lb4_keys(sv_vip, sv_port, np.zeros(ns)), lb4_keys(sv_vip, sv_port, np.ones(ns))])
     vals = np.concatenate([lb4_vals(np.zeros(ns), np.zeros(ns), np.ones(ns), np.zeros(ns)),
                            lb4_vals(sv_ep, be_port, np.zeros(ns), (np.arange(ns) % 256) + 1)])
-    sc.add_map(MapSpec("cilium_lb4_services", HASH, 8, 12, 65536, 0, keys, vals))
+    if n_svc:
+        _, _, _, _, k3, v3 = lb4_population(np.random.default_rng(seed + 3), n_svc, ip4("10.98.0.0"))
+        keys, vals = np.concatenate([keys, k3]), np.concatenate([vals, v3])
+    sc.add_map(MapSpec("cilium_lb4_services", HASH, 8, 12, 2_000_000, 0, keys, vals))
     sc.xdp = {"cidr4_hmap": "cilium_cidr_v4_fix", "cidr4_lmap": "cilium_cidr_v4_dyn", "cidr6_hmap": None,
               "cidr6_lmap": None, "lxc_map": "cilium_lxc"}
     sc.lb = {"lb4": "cilium_lb4_services", "lb6": None, "flags": LB_L3 | LB_L4, "redirect_ifindex": 0}

@@ -119,3 +119,89 @@ def test_config5_real_shape_parity_with_eviction():
     ok, ov = ref.m["cilium_ct6_global"].dump_arrays()
     n, bad = PY.compare_tables(gk, gv, ok, ov)
     assert bad == 0 and n > 9_000_000, (n, bad)
+
+
+def test_config3_real_shape():
+    """Config 3 at its real table shape: bpf_lb over 100,000 services (90% VIP:port,
+    10% L3-only) and ~1,000,000 backend slots in one 2M-entry lbmap (the
+    AddSVC2BPFMap population of pkg/maps/lbmap/lbmap.go:320-371), 100k revNAT
+    entries; 2M packets (85% Zipf-1.1 VIP traffic, 5% L3-only VIPs on random ports,
+    10% non-service).  The whole batch against the oracle (lb.h:566-613 lookups,
+    slave = hash % count + 1, the lb4_xlate fields), plus the counter block."""
+    import ctypes as C
+    from cilium_amd._lib import lib
+    from cilium_amd.datapath import DeviceBatch, LB_OUT, to_numpy
+    sc = synth.config3(n_packets=2_000_000)
+    assert sc.maps["cilium_lb4_services"].n() > 1_000_000
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    cnt = torch.zeros(512, dtype=torch.int64, device="cuda")
+    lib.gf_set_stats_sink(C.c_void_p(cnt.data_ptr()))
+    try:
+        lo, _ = dp.lb(DeviceBatch(pk, with_v6=False))
+        torch.cuda.synchronize()
+    finally:
+        lib.gf_set_stats_sink(None)
+    g = to_numpy(lo, LB_OUT)
+    r, _ = ref.lb(pk, threads=8)
+    bad, first = PY.compare_records(g, r)
+    assert bad == 0, f"{bad} mismatches, first {first}: gpu={g[first]} ref={r[first]}"
+    # every outcome of the path is exercised at this shape
+    assert (r["action"] == 7).mean() > 0.8 and (r["reason"] == 158).sum() == 0
+    assert (r["new_dport"] != 0).any() and len(np.unique(r["slave"])) >= 19
+    c = cnt.cpu().numpy()
+    assert c[268] == pk.n and c[269] == np.asarray(pk.lens, np.int64).sum()
+    for a in np.unique(r["action"]):
+        assert c[256 + int(a)] == (r["action"] == a).sum(), f"action {a}"
+    for x in range(1, 256):
+        assert c[x] == (r["reason"] == x).sum(), f"reason {x}"
+
+
+def test_config4_real_shape_sampled():
+    """Config 4 at its real table shape: config 2's endpoints, policies and CIDR maps
+    over 2^20 address pairs, config 1's prefilter (10k LPM prefixes + 2k /32s),
+    config 3's service population (100k services / ~1M backends) next to the
+    endpoints' own VIPs, composed bpf_xdp -> bpf_lb -> bpf_netdev -> handle_policy
+    over raw frames of the bench's steady-state stream (4 steps of 1M frames, 30% of
+    the pairs addressed through a VIP).  1/8 of the post-LB address pairs through the
+    oracle: pipeline records and rewritten frames of every sampled packet, then the
+    sampled pairs' CT entries, bit-exact."""
+    sc, P, vip = synth.config4_tables(n_pairs=1 << 20, ct_max=1 << 24)
+    assert sc.maps["cilium_lb4_services"].n() > 1_000_000
+    st = stream.Stream(P, flows_per_step=1 << 18, device="cuda", vip_ip=vip)
+    S0, N = 3, 4
+    rk, rv = st.reply_ct_entries(S0 + N)
+    sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc, shards=8)
+    div = 8
+    samp = torch.from_numpy(PY.pair_sampled(st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy(), div)).cuda()
+    compared, stages, rets = 0, set(), set()
+    for s in range(N):
+        cols, p, n = st.step(S0 + s)
+        f, lens = stream.device_frames(cols)
+
+        class B:
+            pass
+        b = B()
+        b.frames, b.len, b.tc_index, b.flow_hash, b.n, b.device = f, lens, cols["tc_index"], None, n, "cuda"
+        out, _, snap = dp.pipeline(b, sc.now + s, snap_out=True)
+        torch.cuda.synchronize()
+        idx = torch.nonzero(samp[p]).squeeze(1)
+        pk = Packets(f[idx].cpu().numpy(), lens[idx].cpu().numpy().view(np.uint32),
+                     tc_index=cols["tc_index"][idx].cpu().numpy())
+        ro, _, rs = ref.pipeline(pk, sc.now + s, threads=8)
+        g = out[idx].cpu().numpy().view(PIPE_OUT).ravel()
+        bad, first = PY.compare_records(g, ro)
+        assert bad == 0, f"step {s}: {bad} mismatches, first sampled row {first}: gpu={g[first]} ref={ro[first]}"
+        gs = snap[idx].cpu().numpy()
+        bad_f = np.nonzero((gs != rs).any(axis=1))[0]
+        assert len(bad_f) == 0, f"step {s}: {len(bad_f)} rewritten frames differ, first sampled row {bad_f[0]}"
+        compared += len(ro)
+        stages |= set(np.unique(ro["stage"]).tolist())
+        rets |= set(np.unique(ro["ct_ret"][ro["stage"] == 4]).tolist())
+    assert compared > 400_000
+    assert {1, 4} <= stages and len(rets) == 4, (stages, rets)
+    gk, gv, gtot = PY.gpu_table_sampled(dp.fd["cilium_ct4_global"], 14, 48, div)
+    ok, ov = PY.oracle_table_sampled(ref.m["cilium_ct4_global"], div)
+    n, bad = PY.compare_tables(gk, gv, ok, ov)
+    assert bad == 0 and n > 100_000, (n, bad, gtot)

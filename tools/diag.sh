@@ -8,8 +8,9 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 VARIANTS=${VARIANTS:-"1 2 4 8 15"}
 if [ "$1" = build ]; then
   mkdir -p "$R/tools/_bin"
+  SHA=$(cd "$R" && python -c "import __graft_entry__ as g; print(g.source_sha())")
   for v in $VARIANTS; do
-    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -DGF_DIAG=$v -I "$R/include" \
+    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -DGF_SRC_SHA="\"$SHA+d$v\"" -DGF_DIAG=$v -I "$R/include" \
       "$R/cilium_amd/csrc/gf_maps.cpp" "$R/cilium_amd/csrc/gf_kernels.hip" -o "$R/tools/_bin/libgpuflow_d$v.so" &
   done
   wait

@@ -7,9 +7,10 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 mode=$1; shift
 if [ "$mode" = build ]; then
   mkdir -p "$R/tools/_bin"
+  SHA=$(cd "$R" && python -c "import __graft_entry__ as g; print(g.source_sha())")
   for spec in "$@"; do
     name=${spec%%:*}; flags=${spec#*:}
-    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared $flags -I "$R/include" \
+    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -DGF_SRC_SHA="\"$SHA+$name\"" $flags -I "$R/include" \
       "$R/cilium_amd/csrc/gf_maps.cpp" "$R/cilium_amd/csrc/gf_kernels.hip" -o "$R/tools/_bin/libgpuflow_$name.so" &
   done
   wait
