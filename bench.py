@@ -5,21 +5,29 @@ flow spans 4 steps), 2^20 address pairs, 4,352 identities, 256 endpoints.
 One step = gf_policy_ingress_classify over one batch resident in HBM (flow-group
 grouping + CT + policy + output).  N GPUs: one process per GPU, flow groups
 (unordered address pairs) sharded across ranks, tables replicated, CT
-partitioned; the only collective is the RCCL all-reduce of the counter block
-(and the timing max).  `python bench.py --gpus N` without a torch.distributed
-launcher spawns the N rank processes itself (before anything touches a GPU).
+partitioned; the only collective on the classify path is the RCCL all-reduce of
+the counter block (and the timing max).  `python bench.py --gpus N` without a
+torch.distributed launcher spawns the N rank processes itself, before anything
+in this process touches the HIP runtime.
 
 Prints ONE JSON line (rank 0) with roofline, cpu_baseline and parity objects.
 `parity` is the full-scale bit-exactness check: the CPU restatement (oracle/)
 runs the same stream on a flow-group sample (1/--parity-div of the address
 pairs: whole flow groups, so a sampled run of the stateful path is exact) and
 every sampled packet's GPU record, plus every CT entry of the sampled pairs at
-the end, must equal the oracle's.  At N=1 the line also carries "configs": the
-other BASELINE configurations measured the same way (config 1 XDP prefilter,
-config 3 service LB, config 4 full pipeline over raw frames, config 5 IPv6
-pipeline, and the endpoint egress path of SURVEY §8(f)), each with its own
-roofline, CPU baseline and parity (`--config N` prints that configuration
-alone as the line).
+the end, must equal the oracle's.  Every rank checks its own partition and the
+counts are summed over ranks.  The line also carries "configs": at N=1 the other
+BASELINE configurations measured the same way (config 1 XDP prefilter, config 3
+service LB, config 4 full pipeline over raw frames — device-resident and with
+the host->device copy of the frames —, config 5 IPv6 pipeline, and the endpoint
+egress path of SURVEY §8(f)); at N>1 config 4 across the ranks, with frames
+arriving on their owner rank (RSS-style) and with frames arriving anywhere and
+re-partitioned by gf_pipeline_partition + one all-to-all (`--config N` prints
+that configuration alone as the line).
+
+GPUFLOW_BENCH_SELFTEST=1 runs the same code on the CPU (gloo ranks, CPU tensors,
+small tables) with the oracle standing in for the device: a rehearsal of the
+launcher, the rank / stream / parity / all-reduce logic — it measures nothing.
 """
 import argparse
 import glob
@@ -44,15 +52,17 @@ def log(*a):
 
 
 # ----------------------------------------------------------------------------- CPU side facts
-def cpu_threads():
-    """Threads for the CPU baseline: this process's CPU share (OMP_NUM_THREADS on
-    the GPU box, else the affinity mask)."""
+def cpu_threads(local_world=1):
+    """Threads for the CPU legs of one rank: this process's CPU share
+    (OMP_NUM_THREADS on the GPU box, else the affinity mask), split between the
+    node's local ranks."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count() or 1
     e = os.environ.get("OMP_NUM_THREADS")
-    return max(1, min(int(e), aff)) if e and e.isdigit() else aff
+    t = max(1, min(int(e), aff)) if e and e.isdigit() else aff
+    return max(1, min(t, aff // max(1, local_world)))
 
 
 def cpu_model():
@@ -71,45 +81,206 @@ def cpu_base(value, T, sample, single=None):
             "single_core_mpps": None if single is None else round(single, 3), "sample": sample}
 
 
+# ----------------------------------------------------------------------------- backends
+class Gpu:
+    """The product path: libgpuflow's kernels on this rank's GPU (HIP streams,
+    the launch profiler and the device counter block)."""
+    rehearsal = False
+    tables_kw = {}
+    ct_max_cap = None
+
+    def __init__(self, local):
+        import torch
+        # GPUFLOW_BENCH_SHARE_GPU: several ranks on one device (a rehearsal of the
+        # N-rank path on a one-GPU box, with GPUFLOW_BENCH_BACKEND=gloo)
+        if os.environ.get("GPUFLOW_BENCH_SHARE_GPU"):
+            local %= max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+
+    @staticmethod
+    def close(dp):
+        """Release a datapath's device tables (the next configuration's need the HBM)."""
+        dp.close()
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize()
+
+    def datapath(self, sc):
+        from cilium_amd.datapath import Datapath
+        return Datapath(sc, pin_prefix=None)
+
+    def begin(self):
+        """Counter sink + launch profiler on (the timed region)."""
+        import torch
+        import ctypes as C
+        from cilium_amd._lib import lib
+        self.c = torch.zeros(512, dtype=torch.int64, device=self.dev)
+        lib.gf_set_stats_sink(C.c_void_p(self.c.data_ptr()))
+        lib.gf_prof_enable(1)
+
+    def end(self):
+        """(counter block, {kernel: (launches, total_ms)}) of the timed region."""
+        from cilium_amd._lib import lib, gf_prof_rec
+        lib.gf_set_stats_sink(None)
+        recs = (gf_prof_rec * 32)()
+        nrec = lib.gf_prof_read(recs, 32)
+        lib.gf_prof_enable(0)
+        return self.c, {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
+
+    def evict_log(self, dp, name):
+        from cilium_amd._lib import lib, gf_ct_evict_rec
+        recs = (gf_ct_evict_rec * 4096)()
+        n = lib.gf_ct_evict_log(dp.fd[name], recs, 4096)
+        return [(r.seq, r.now_sec, r.cut_closing, r.cut_other, r.evicted) for r in recs[:max(0, min(n, 4096))]]
+
+    def table_sampled(self, dp, name, ksz, div, pred):
+        from oracle import parity as PY
+        return PY.gpu_table_sampled(dp.fd[name], ksz, 48, div, pred=pred)
+
+    def entries(self, dp, name):
+        from cilium_amd import bpf
+        return bpf.GetMapInfo(dp.fd[name]).Entries
+
+    def partition(self, dp, fb, rank, world):
+        from cilium_amd import shard
+        return shard.partition(dp, fb.frames, fb.len, rank, world, fb.flow_hash, fb.tc_index)
+
+
+class Rehearsal:
+    """GPUFLOW_BENCH_SELFTEST: the bench's rank / stream / parity / all-reduce code
+    on the CPU (gloo, CPU tensors, small tables) with the oracle standing in for
+    the device.  It checks the harness, never the kernels: its numbers are not
+    measurements."""
+    rehearsal = True
+    tables_kw = {"n_ep": 16, "n_ids": 256, "n_l3": 64, "n_l4": 128, "n_wc": 8, "n_cidr": 16}
+    ct_max_cap = 1 << 20
+
+    def __init__(self):
+        import torch
+        self.dev = torch.device("cpu")
+        self.c = None
+
+    def sync(self):
+        pass
+
+    def datapath(self, sc):
+        return StandIn(sc, self)
+
+    @staticmethod
+    def close(dp):
+        pass
+
+    def begin(self):
+        import torch
+        self.c = torch.zeros(512, dtype=torch.int64)
+
+    def end(self):
+        c, self.c = self.c, None
+        return c, {}
+
+    def count(self, rec, lens):
+        """The counter block's bins from the stand-in's records (reason, action,
+        CT result, packets, wire bytes)."""
+        if self.c is None:
+            return
+        import torch
+        h = np.zeros(512, np.int64)
+        h[:256] += np.bincount(rec["reason"], minlength=256)[:256]
+        h[256:264] += np.bincount(rec["action"], minlength=8)[:8]
+        h[264:268] += np.bincount(np.minimum(rec["ct_ret"], 3), minlength=4)[:4]
+        h[268] += len(rec)
+        h[269] += int(np.asarray(lens, np.int64).sum())
+        self.c += torch.from_numpy(h)
+
+    def evict_log(self, dp, name):
+        return list(dp.ref.lru_log.get(name, []))
+
+    def table_sampled(self, dp, name, ksz, div, pred):
+        from oracle import parity as PY
+        k, v = PY.oracle_table_sampled(dp.ref.m[name], div, pred=pred)
+        return k, v, dp.ref.m[name].count()
+
+    def entries(self, dp, name):
+        return dp.ref.m[name].count()
+
+    def partition(self, dp, fb, rank, world):
+        import torch
+        from cilium_amd.synth import Packets
+        from oracle.parity import owners_host
+        pk = Packets(fb.frames.numpy(), fb.len.numpy().view(np.uint32),
+                     tc_index=None if fb.tc_index is None else fb.tc_index.numpy())
+        lo, nd6 = dp.ref.lb(pk)
+        own = owners_host(lo, nd6, pk, rank, world)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32))
+        return t(own), t(np.argsort(own, kind="stable")), t(np.bincount(own, minlength=world))
+
+
+class StandIn:
+    """The oracle in the device's place (Rehearsal only): the classify calls of
+    cilium_amd.datapath.Datapath over CPU tensors."""
+
+    def __init__(self, sc, be):
+        from oracle.scenario import OracleDP
+        self.sc, self.be, self.ref = sc, be, OracleDP(sc)
+
+    def _put(self, out, r):
+        import torch
+        out.copy_(torch.from_numpy(np.ascontiguousarray(r).view(np.uint8).reshape(len(r), -1)))
+
+    def ingress(self, b, now, out):
+        import torch
+        pk = cols_packets(b.cdict, torch.arange(b.n))
+        r = self.ref.ingress(pk, now)
+        self._put(out, r)
+        self.be.count(r, pk.lens)
+        return out
+
+    def ingress_batches(self, bs, nows, outs):
+        return [self.ingress(b, n, o) for b, n, o in zip(bs, nows, outs)]
+
+    def pipeline(self, fb, now, out, snap_out=False):
+        from cilium_amd.synth import Packets
+        pk = Packets(fb.frames.numpy(), fb.len.numpy().view(np.uint32),
+                     tc_index=None if fb.tc_index is None else fb.tc_index.numpy())
+        r = self.ref.pipeline(pk, now)[0]
+        self._put(out, r)
+        self.be.count(r, pk.lens)
+        return out, None, None
+
+
 # ----------------------------------------------------------------------------- timing
-def timed(run_step, W, K, dev, world=1, ranged=False):
+def timed(B, run_step, W, K, world=1, ranged=False):
     """W untimed warm-up steps, then K steps bracketed by barrier + synchronize,
     with the verdict counter sink and the launch profiler on (ranged: run_step(a, b)
     runs steps a..b-1 in one call).  Returns (elapsed_s (max over ranks), counters
     (summed over ranks), local counters, {kernel: (launches, total_ms)})."""
     import torch
     import torch.distributed as dist
-    import ctypes as C
-    from cilium_amd._lib import lib, gf_prof_rec
     if ranged:
         run_step(0, W)
     else:
         for s in range(W):
             run_step(s)
-    torch.cuda.synchronize()
-    counters = torch.zeros(512, dtype=torch.int64, device=dev)
-    lib.gf_set_stats_sink(C.c_void_p(counters.data_ptr()))
-    lib.gf_prof_enable(1)
+    B.sync()
+    B.begin()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    B.sync()
     t0 = time.perf_counter()
     if ranged:
         run_step(W, W + K)
     else:
         for s in range(W, W + K):
             run_step(s)
-    torch.cuda.synchronize()
+    B.sync()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    lib.gf_set_stats_sink(None)
-    recs = (gf_prof_rec * 32)()
-    nrec = lib.gf_prof_read(recs, 32)
-    lib.gf_prof_enable(0)
-    kern = {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
+    counters, kern = B.end()
     local = counters.clone()
-    tt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    tt = torch.tensor([t1 - t0], dtype=torch.float64, device=B.dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(counters, op=dist.ReduceOp.SUM)        # RCCL over xGMI: verdict counter block
@@ -151,7 +322,7 @@ def cpu_loop(fn, seconds):
 
 # ----------------------------------------------------------------------------- parity bookkeeping
 class Parity:
-    """Accumulates the full-scale comparison of one configuration."""
+    """Accumulates the full-scale comparison of one configuration (one rank)."""
 
     def __init__(self, sample):
         self.sample, self.packets, self.bad, self.first = sample, 0, 0, None
@@ -182,28 +353,44 @@ class Parity:
         return r
 
 
-def lru_replay(dp, ref):
-    """The GPU's LRU evictions (gf_ct_evict_log) replayed by a sampled oracle:
+def reduce_parity(B, par, rank, world):
+    """Parity counts summed over ranks (every rank checked its own flow groups);
+    the per-table detail is rank 0's."""
+    if world == 1 or par is None:
+        return par
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([par["packets_compared"], par["mismatches"], par.get("ct_entries_compared", 0),
+                      par.get("ct_mismatches", 0), 1 if par.get("first_mismatch") else 0], dtype=torch.int64,
+                     device=B.dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    v = t.cpu().tolist()
+    r = dict(par)
+    r.update({"packets_compared": v[0], "mismatches": v[1], "ct_entries_compared": v[2], "ct_mismatches": v[3],
+              "ranks": world, "ranks_with_mismatch": v[4],
+              "sample": par["sample"] + f", on each of the {world} ranks (its own flow groups and CT partition)"})
+    if "tables" in r:
+        r["tables_rank0"] = r.pop("tables")
+    return r
+
+
+def lru_replay(B, dp, ref):
+    """The device's LRU evictions (gf_ct_evict_log) replayed by a sampled oracle:
     eviction cutoffs depend on the whole table, which a sample does not hold."""
-    import ctypes as C
-    from cilium_amd._lib import lib, gf_ct_evict_rec
     for name in ref.lru_maps:
-        recs = (gf_ct_evict_rec * 4096)()
-        n = lib.gf_ct_evict_log(dp.fd[name], recs, 4096)
-        ref.lru_replay[name] = {r.seq: (r.cut_closing, r.cut_other) for r in recs[:max(0, min(n, 4096))]}
+        ref.lru_replay[name] = {seq: (cc, co) for seq, _, cc, co, _ in B.evict_log(dp, name)}
 
 
-def compare_ct(par, dp, ref, name, ksz, div, pred=None):
+def compare_ct(B, par, dp, ref, name, ksz, div, pred=None):
     from oracle import parity as PY
     pred = pred or PY.ct_sampled
-    gk, gv, gtot = PY.gpu_table_sampled(dp.fd[name], ksz, 48, div, pred=pred)
+    gk, gv, gtot = B.table_sampled(dp, name, ksz, div, pred)
     rk, rv = PY.oracle_table_sampled(ref.m[name], div, pred=pred)
     par.table(name, gk, gv, rk, rv, gtot)
 
 
 def cols_packets(cdict, idx, v6=False):
     """Host Packets (raw frames) for the rows idx of a column batch."""
-    import torch
     from cilium_amd import stream
     from cilium_amd.synth import Packets
     c = {k: v[idx].cpu().numpy() for k, v in cdict.items()}
@@ -213,18 +400,25 @@ def cols_packets(cdict, idx, v6=False):
     return Packets(f, lens, c["src_identity"], c["ifindex"], c["lxc_id"], c["tc_index"])
 
 
+def _sub(pk, idx):
+    from cilium_amd.synth import Packets
+    f = lambda x: None if x is None else np.asarray(x)[idx]
+    return Packets(pk.frames[idx], pk.lens[idx], f(pk.src_identity), f(pk.ifindex), f(pk.lxc_id), f(pk.tc_index),
+                   f(pk.flow_hash))
+
+
 # ----------------------------------------------------------------------------- config 2 (the headline)
-def bench_config2(args, dev, rank, world):
+def bench_config2(args, B, rank, world, local_world=1):
     import torch
     from cilium_amd import synth, stream
-    from cilium_amd.datapath import Datapath
     W, K = max(args.warmup, 3), args.steps
     t0 = time.time()
+    ct_max = min(args.ct_max, B.ct_max_cap or args.ct_max)
     # Weak scaling: every rank serves --pairs address pairs (its RSS share of
     # pairs x world), so the per-GPU step — packets, flow groups, bucket depth, CT
     # partition — is the N=1 step at every N.
-    sc, P, _ = synth.config2_tables(n_pairs=args.pairs * world, ct_max=args.ct_max)
-    st = stream.Stream(P, rank=rank, world=world, flows_per_step=args.flows_per_step, device=dev)
+    sc, P, _ = synth.config2_tables(n_pairs=args.pairs * world, ct_max=ct_max, **B.tables_kw)
+    st = stream.Stream(P, rank=rank, world=world, flows_per_step=args.flows_per_step, device=B.dev)
     # The stream ramps up over its first 3 steps (flows span 4 steps); the run starts at
     # stream step S0 = 3 so that every launch, warm-up included, is a full steady-state
     # batch (the rocprof --stats average over all launches then matches the timed one).
@@ -233,29 +427,29 @@ def bench_config2(args, dev, rank, world):
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
     log(f"rank {rank}: tables {sum(m.n() for m in sc.maps.values())} entries, {len(rk)} pre-inserted CT, "
         f"{len(st.own)} owned pairs ({time.time() - t0:.1f}s)")
-    dp = Datapath(sc, pin_prefix=None)
+    dp = B.datapath(sc)
     batches, ps = [], []
     for s in range(W + K):
         cols, p, n = st.step(S0 + s)
-        batches.append(ColBatch(cols, n, dev))
+        batches.append(ColBatch(cols, n, B.dev))
         ps.append(p)
     # one output buffer per step: the parity leg reads every step's records afterwards
-    outs = [torch.empty((b.n, 8), dtype=torch.uint8, device=dev) for b in batches]
-    torch.cuda.synchronize()
+    outs = [torch.empty((b.n, 8), dtype=torch.uint8, device=B.dev) for b in batches]
+    B.sync()
     log(f"rank {rank}: generated {W + K} steps ({time.time() - t0:.1f}s)")
     now = sc.now
     if not args.pipeline:
-        elapsed, c, lc, kern = timed(lambda s: dp.ingress(batches[s], now + s, out=outs[s]), W, K, dev, world)
+        elapsed, c, lc, kern = timed(B, lambda s: dp.ingress(batches[s], now + s, out=outs[s]), W, K, world)
     else:
         # the stream of batches through gf_policy_ingress_classify_batches: batch s+1's
         # schedule is built on a second stream while handle_policy of batch s runs
         # (measured slower: the overlapped kernels share the memory system)
-        elapsed, c, lc, kern = timed(lambda a, b: dp.ingress_batches(batches[a:b], [now + s for s in range(a, b)],
-                                                                      outs[a:b]), W, K, dev, world, ranged=True)
+        elapsed, c, lc, kern = timed(B, lambda a, b: dp.ingress_batches(batches[a:b], [now + s for s in range(a, b)],
+                                                                         outs[a:b]), W, K, world, ranged=True)
     total_pkts = int(c[268])
     local_pkts = sum(batches[s].n for s in range(W, W + K))
-    if world == 1 and not os.environ.get("GPUFLOW_DIAG_LIB"):
-        assert total_pkts == local_pkts, (total_pkts, local_pkts)
+    if not os.environ.get("GPUFLOW_DIAG_LIB"):
+        assert int(lc[268]) == local_pkts, (int(lc[268]), local_pkts)
     # roofline of the dominant kernel (k_ing_groups), this rank
     ki = kern.get("k_ing_groups", (0, 0.0))
     avg_ms = ki[1] / max(ki[0], 1)
@@ -263,7 +457,7 @@ def bench_config2(args, dev, rank, world):
     achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = traffic_src = None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
-    if pmc:
+    if pmc and not B.rehearsal:
         try:
             j = json.load(open(pmc[-1]))
             if j.get("kernel") == "k_ing_groups" and j.get("traffic_bytes_per_launch"):
@@ -272,8 +466,14 @@ def bench_config2(args, dev, rank, world):
         except Exception:
             traffic = None
     cpu = par = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, par = oracle_config2(args, sc, st, dp, batches, ps, outs, W, K)
+    if not args.no_cpu:
+        # every rank checks its own flow groups; the CPU baseline is rank 0's at N=1 only
+        cpu, par = oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world, local_world)
+        if world > 1:
+            cpu = None
+    par = reduce_parity(B, par, rank, world)
+    ct_end = int(B.entries(dp, "cilium_ct4_global"))
+    B.close(dp)
     return {
         "metric": METRIC,
         "value": round(total_pkts / elapsed / 1e6, 3),
@@ -293,8 +493,8 @@ def bench_config2(args, dev, rank, world):
             "packets_per_step_per_gpu": int(batches[W].n),
             "address_pairs_per_gpu": int(args.pairs),
             "address_pairs": int(args.pairs) * world,
-            "ct_max_entries": int(args.ct_max),
-            "ct_entries_at_end": int(bpf_entries(dp, "cilium_ct4_global")),
+            "ct_max_entries": int(ct_max),
+            "ct_entries_at_end": ct_end,
             "parallelism": f"dp{world} (flow-group sharded, tables replicated, CT partitioned)",
         },
         "roofline": {
@@ -316,11 +516,6 @@ def bench_config2(args, dev, rank, world):
     }
 
 
-def bpf_entries(dp, name):
-    from cilium_amd import bpf
-    return bpf.GetMapInfo(dp.fd[name]).Entries
-
-
 class ColBatch:
     """Device columns of one step (dict of tensors) in the DeviceBatch shape."""
 
@@ -337,7 +532,7 @@ class ColBatch:
         return self._cols(self)
 
 
-def oracle_config2(args, sc, st, dp, batches, ps, outs, W, K):
+def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_world=1):
     """The CPU restatement (oracle, multi-threaded, RSS-style partition by flow
     group) over the flow-group sample of every step (warm-up included): its
     records must equal the GPU's for every sampled packet and, after the last
@@ -349,10 +544,10 @@ def oracle_config2(args, sc, st, dp, batches, ps, outs, W, K):
     from cilium_amd.datapath import ING_OUT
     from oracle.scenario import OracleDP
     from oracle import parity as PY
-    T, div = cpu_threads(), args.parity_div
+    T, div = cpu_threads(local_world), parity_div(args, world)
     t0 = time.time()
     ref = OracleDP(sc, shards=T)
-    lru_replay(dp, ref)
+    lru_replay(B, dp, ref)
     sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
     samp = torch.from_numpy(PY.pair_sampled(sa, da, div)).to(st.device)
     one = torch.from_numpy(PY.pair_sampled(sa, da, div * 8)).to(st.device)
@@ -382,7 +577,7 @@ def oracle_config2(args, sc, st, dp, batches, ps, outs, W, K):
                 tt += time.perf_counter() - a
                 done += pk.n
         par.records(gout, r, f"step {s}")
-    compare_ct(par, dp, ref, "cilium_ct4_global", 14, div)
+    compare_ct(B, par, dp, ref, "cilium_ct4_global", 14, div)
     log(f"cpu baseline + parity: {par.packets} packets compared, {par.bad} mismatches; CT {par.ct}; "
         f"{done} packets in {tt:.2f}s on {T} threads ({time.time() - t0:.1f}s)")
     cpu = cpu_base(done / tt / 1e6 if tt else 0.0, T,
@@ -393,31 +588,32 @@ def oracle_config2(args, sc, st, dp, batches, ps, outs, W, K):
     return cpu, par.result(W + K)
 
 
-def _sub(pk, idx):
-    from cilium_amd.synth import Packets
-    f = lambda x: None if x is None else np.asarray(x)[idx]
-    return Packets(pk.frames[idx], pk.lens[idx], f(pk.src_identity), f(pk.ifindex), f(pk.lxc_id), f(pk.tc_index),
-                   f(pk.flow_hash))
+def parity_div(args, world):
+    """The flow-group sample of the parity legs: every pair at N=1 (the whole
+    stream), half of each rank's pairs at N>1 (eight oracles share one host)."""
+    if args.parity_div:
+        return args.parity_div
+    return 1 if world == 1 else 2
 
 
 # ----------------------------------------------------------------------------- config 1 / 3 (stateless)
-def bench_config1(args, dev):
+def bench_config1(args, B):
     import torch
     import ctypes as C
     from cilium_amd import synth
     from cilium_amd._lib import lib
-    from cilium_amd.datapath import Datapath, DeviceBatch
+    from cilium_amd.datapath import DeviceBatch
     sc = synth.config1()
     pk = sc.batches[0]
-    dp = Datapath(sc, pin_prefix=None)
+    dp = B.datapath(sc)
     b = DeviceBatch(pk)
-    out = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    out = torch.empty(b.n, dtype=torch.uint8, device=B.dev)
 
     def step(s):
         c = b.cols()
         lib.gf_xdp_classify(dp.xdp_prog, C.byref(c), out.data_ptr(), C.c_void_p(torch.cuda.current_stream().cuda_stream))
     W, K = 5, 50
-    el, c, _, kern = timed(step, W, K, dev)
+    el, c, _, kern = timed(B, step, W, K)
     cpu = par = None
     if not args.no_cpu:
         from oracle.scenario import OracleDP
@@ -434,6 +630,7 @@ def bench_config1(args, dev):
         t1 = time.perf_counter() - a
         cpu = cpu_base(done / tt / 1e6, T, f"{done} packets (the same 1M-packet batch, repeated)", pk.n / t1 / 1e6)
         par = par.result(1)
+    B.close(dp)
     return {"workload": "config1: bpf_xdp CIDR prefilter (10k LPM prefixes + 2k /32, 1025 endpoints), 1M packets/step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
@@ -442,24 +639,24 @@ def bench_config1(args, dev):
             "cpu_baseline": cpu, "parity": par}
 
 
-def bench_config3(args, dev):
+def bench_config3(args, B):
     import torch
     import ctypes as C
     from cilium_amd import synth
     from cilium_amd._lib import lib
-    from cilium_amd.datapath import Datapath, DeviceBatch, LB_OUT
+    from cilium_amd.datapath import DeviceBatch, LB_OUT
     sc = synth.config3(n_packets=16_000_000)
     pk = sc.batches[0]
-    dp = Datapath(sc, pin_prefix=None)
+    dp = B.datapath(sc)
     b = DeviceBatch(pk, with_v6=False)
-    out = torch.empty((b.n, 12), dtype=torch.uint8, device=dev)
+    out = torch.empty((b.n, 12), dtype=torch.uint8, device=B.dev)
 
     def step(s):
         c = b.cols()
         lib.gf_lb_classify(dp.lb_prog, C.byref(c), out.data_ptr(), None,
                            C.c_void_p(torch.cuda.current_stream().cuda_stream))
     W, K = 3, 10
-    el, c, _, kern = timed(step, W, K, dev)
+    el, c, _, kern = timed(B, step, W, K)
     cpu = par = None
     if not args.no_cpu:
         from oracle.scenario import OracleDP
@@ -479,6 +676,7 @@ def bench_config3(args, dev):
         t1 = time.perf_counter() - a
         cpu = cpu_base(pk.n / tfull / 1e6, T, f"{pk.n} packets (the whole batch, once)", sub.n / t1 / 1e6)
         par = par.result(1)
+    B.close(dp)
     return {"workload": "config3: bpf_lb lb4_lookup_service + slave select, 100k services / ~1M backends, "
                         "16M packets/step (Zipf 1.1)",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
@@ -494,68 +692,134 @@ class FrameBatch:
         self.n, self.device = frames.shape[0], dev
 
 
-def bench_config4(args, dev):
+def _spread(fb, samp, world):
+    """The NIC side of the exchange-ingest leg (untimed): contiguous slice j of this
+    rank's owned batch arrives on rank j, so every rank holds a mix of all ranks'
+    flow groups, in arrival order, and must re-partition before classifying.  The
+    sample bit travels with each frame (parity bookkeeping, not classifier input)."""
+    import torch
+    import torch.distributed as dist
+    n = fb.n
+    cuts = [n * j // world for j in range(world + 1)]
+    send = [cuts[j + 1] - cuts[j] for j in range(world)]
+    cnt = torch.tensor(send, dtype=torch.int64, device=fb.frames.device)
+    recv_cnt = torch.empty_like(cnt)
+    dist.all_to_all_single(recv_cnt, cnt)
+    recv = recv_cnt.cpu().tolist()
+    out = []
+    for t in (fb.frames, fb.len, fb.tc_index, samp):
+        r = torch.empty((sum(recv),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_to_all_single(r, t.contiguous(), recv, send)
+        out.append(r)
+    return FrameBatch(out[0], out[1], out[2], fb.device), out[3]
+
+
+def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
+    """BASELINE config 4 over raw frames.  ingest "owned": each rank's frames are
+    the packets of its own flow groups (the RSS of a NIC programmed with the owner
+    hash); "exchange" (N>1): frames arrive anywhere and each step first runs
+    gf_pipeline_partition + one all-to-all (cilium_amd.shard, RCCL over xGMI) —
+    inside the timed region."""
     import torch
     from cilium_amd import synth, stream
-    from cilium_amd.datapath import Datapath
+    from oracle import parity as PY
     W, K = 4, max(4, args.steps // 2)
-    sc, P, vip = synth.config4_tables(n_pairs=args.pairs, ct_max=args.ct_max)
-    st = stream.Stream(P, flows_per_step=args.flows_per_step, device=dev, vip_ip=vip)
+    ct_max = min(args.ct_max, B.ct_max_cap or args.ct_max)
+    kw = dict(B.tables_kw, n_svc=1000, n_lpm=500, n_fix=100) if B.rehearsal else {}
+    sc, P, vip = synth.config4_tables(n_pairs=args.pairs * world, ct_max=ct_max, **kw)
+    st = stream.Stream(P, rank=rank, world=world, flows_per_step=args.flows_per_step, device=B.dev, vip_ip=vip)
     S0 = 3
     rk, rv = st.reply_ct_entries(S0 + W + K)
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
-    dp = Datapath(sc, pin_prefix=None)
-    fbs, ps = [], []
+    dp = B.datapath(sc)
+    exch = ingest == "exchange" and world > 1
+    div = parity_div(args, world) * 2
+    sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
+    pm = torch.from_numpy(PY.pair_sampled(sa, da, div).astype(np.uint8) |
+                          (PY.pair_sampled(sa, da, div * 8).astype(np.uint8) << 1)).to(B.dev)
+    fbs, ps, samps = [], [], []
     for s in range(W + K):
         cols, p, n = st.step(S0 + s)
         f, lens = stream.device_frames(cols)
-        fbs.append(FrameBatch(f, lens, cols["tc_index"], dev))
+        fb = FrameBatch(f, lens, cols["tc_index"], B.dev)
+        sm = pm[p]
+        if exch:
+            fb, sm = _spread(fb, sm, world)
+        fbs.append(fb)
         ps.append(p)
-    outs = [torch.empty((b.n, 24), dtype=torch.uint8, device=dev) for b in fbs]
-    torch.cuda.synchronize()
-    el, c, _, kern = timed(lambda s: dp.pipeline(fbs[s], sc.now + s, out=outs[s], snap_out=False), W, K, dev)
+        samps.append(sm)
+    B.sync()
+    got = [None] * (W + K)            # exchange: the batch each step classified (its records' order)
+
+    if exch:
+        from cilium_amd import shard
+
+        def step(s):
+            fb = fbs[s]
+            owner, order, counts = B.partition(dp, fb, rank, world)
+            fr, ln, tc, sm = shard.exchange(order, counts, [fb.frames, fb.len, fb.tc_index, samps[s]])
+            mine = FrameBatch(fr, ln, tc, B.dev)
+            out = torch.empty((mine.n, 24), dtype=torch.uint8, device=B.dev)
+            dp.pipeline(mine, sc.now + s, out=out, snap_out=False)
+            got[s] = (mine, sm, out)
+    else:
+        outs = [torch.empty((b.n, 24), dtype=torch.uint8, device=B.dev) for b in fbs]
+
+        def step(s):
+            dp.pipeline(fbs[s], sc.now + s, out=outs[s], snap_out=False)
+            got[s] = (fbs[s], samps[s], outs[s])
+    el, c, lc, kern = timed(B, step, W, K, world)
     names = [k for k in kern]
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_config4(args, sc, st, dp, fbs, ps, outs, W, K)
-    return {"workload": "config4: bpf_xdp -> bpf_lb -> bpf_netdev delivery -> handle_policy over raw 64-B frames "
-                        "(config-2 stream, 30% of pairs via service VIPs; 10k-prefix prefilter), 16.8M packets/step",
-            "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
-            "packets_per_step": int(c[268]) // K, "warmup": W,
-            "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)"),
-            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, local_world=local_world)
+        if world > 1:
+            cpu = None
+    par = reduce_parity(B, par, rank, world)
+    B.close(dp)
+    r = {"workload": "config4: bpf_xdp -> bpf_lb -> bpf_netdev delivery -> handle_policy over raw 64-B frames "
+                     "(config-2 stream, 30% of pairs via service VIPs; 10k-prefix prefilter; config 3's 100k "
+                     "services / ~1M backends in the lbmap), 16.8M packets/step per GPU",
+         "ingest": ("frames arrive on any rank; gf_pipeline_partition + RCCL all-to-all re-partition them by "
+                    "post-LB flow group inside the timed step") if exch else
+                   "frames arrive on the rank that owns their flow group (RSS by the owner hash)",
+         "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+         "packets_per_step": int(c[268]) // K, "warmup": W, "n_gpus": world,
+         "roofline": roofline(kern, [k for k in names if k != "k_partition"], float(lc[270]) / K,
+                              "all pipeline kernels (frames -> verdicts), this rank"),
+         "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+    if world == 1 and not B.rehearsal and not args.no_h2d:
+        r["h2d"] = config4_h2d(args, B, sc, fbs, [g[2] for g in got], W, K)
+    return r
 
 
-def oracle_config4(args, sc, st, dp, fbs, ps, outs, W, K, ct_names=("cilium_ct4_global",), v6_pairs=None):
+def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global",), local_world=1):
     """The oracle pipeline over the flow-group sample of every step (the flow group
     is the post-LB address pair, i.e. the stream's pair), records and the sampled
-    pairs' CT entries compared; timed steps give the CPU baseline."""
+    pairs' CT entries compared; timed steps give the CPU baseline.  got[s] = (the
+    frames step s classified, their sample bits, their records); sample bit 0: the packet's
+    post-LB pair is in the 1/div sample, bit 1: in the 1/(8 div) single-core subsample."""
     import torch
     from cilium_amd.datapath import PIPE_OUT
     from cilium_amd.synth import Packets
     from oracle.scenario import OracleDP
-    from oracle import parity as PY
-    T, div = cpu_threads(), args.parity_div * 2
+    T = cpu_threads(local_world)
     ref = OracleDP(sc, shards=T)
-    lru_replay(dp, ref)
-    if v6_pairs is None:
-        sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
-        pm = PY.pair_sampled(sa, da, div)
-        pm1 = PY.pair_sampled(sa, da, div * 8)
-    else:
-        pm, pm1 = PY.pair_sampled6(*v6_pairs, div), PY.pair_sampled6(*v6_pairs, div * 8)
-    samp, one = torch.from_numpy(pm).to(st.device), torch.from_numpy(pm1).to(st.device)
+    lru_replay(B, dp, ref)
     par = Parity(f"1/{div} of the address pairs (whole flow groups), every step incl. warm-up")
     done = single_n = 0
     tt = single_t = 0.0
     for s in range(W + K):
-        idx = torch.nonzero(samp[ps[s]]).squeeze(1)
-        b = fbs[s]
-        pk = Packets(b.frames[idx].cpu().numpy(), b.len[idx].cpu().numpy().view(np.uint32),
-                     tc_index=None if b.tc_index is None else b.tc_index[idx].cpu().numpy())
-        gout = outs[s][idx].cpu().numpy().view(PIPE_OUT).ravel()
+        b, sm, out = got[s]
+        sbits = sm.cpu().numpy()
+        idx = np.nonzero(sbits & 1)[0]
+        it = torch.from_numpy(idx).to(b.frames.device)
+        pk = Packets(b.frames[it].cpu().numpy(), b.len[it].cpu().numpy().view(np.uint32),
+                     tc_index=None if b.tc_index is None else b.tc_index[it].cpu().numpy())
+        gout = out[it].cpu().numpy().view(PIPE_OUT).ravel()
         if s == W:
-            m1 = one[ps[s]][idx].cpu().numpy()
+            # 1/8 of the sampled groups (sample bit 1) on one core first (exact: groups are independent)
+            m1 = (sbits[idx] & 2) != 0
             a = time.perf_counter()
             r1 = ref.pipeline(_sub(pk, np.nonzero(m1)[0]), sc.now + s, threads=1, lru=False)[0]
             single_t, single_n = time.perf_counter() - a, int(m1.sum())
@@ -573,7 +837,7 @@ def oracle_config4(args, sc, st, dp, fbs, ps, outs, W, K, ct_names=("cilium_ct4_
                 done += pk.n
         par.records(gout, r, f"step {s}")
     for name in ct_names:
-        compare_ct(par, dp, ref, name, 14 if "4" in name else 40, div)
+        compare_ct(B, par, dp, ref, name, 14 if "4" in name else 40, div)
     cpu = cpu_base(done / tt / 1e6 if tt else 0.0, T,
                    f"{done} packets (flows of 1/{div} of the address pairs, the {K} timed steps after the same "
                    f"warm-up), {T} threads; single core: {single_n} packets of step {W}",
@@ -581,8 +845,62 @@ def oracle_config4(args, sc, st, dp, fbs, ps, outs, W, K, ct_names=("cilium_ct4_
     return cpu, par.result(W + K)
 
 
+def config4_h2d(args, B, sc, fbs, outs, W, K):
+    """Config 4 with the host->device copy of the frames in the timed region:
+    each step's 64-B frames start in pinned host memory and are copied over PCIe
+    on a copy stream (double-buffered: step s+1's copy runs under step s's
+    kernels).  A fresh datapath over the same steps; its records must equal the
+    device-resident run's bit for bit (same kernels, same state sequence)."""
+    import torch
+    t0 = time.time()
+    W, K = 2, min(K, 4)                    # the first W + K steps of the device-resident run (pinned host copies)
+    dp = B.datapath(sc)
+    n = fbs[0].n
+    host = [[t.cpu().pin_memory() for t in (fb.frames, fb.len, fb.tc_index)] for fb in fbs[:W + K]]
+    dbuf = [[torch.empty_like(t) for t in (fbs[0].frames, fbs[0].len, fbs[0].tc_index)] for _ in range(2)]
+    copy = torch.cuda.Stream()
+    comp = torch.cuda.current_stream()
+    ready = [torch.cuda.Event() for _ in range(2)]
+    free = [torch.cuda.Event() for _ in range(2)]
+    outs2 = [torch.empty((n, 24), dtype=torch.uint8, device=B.dev) for _ in range(W + K)]
+
+    def issue_copy(s):
+        j = s % 2
+        with torch.cuda.stream(copy):
+            copy.wait_event(free[j])
+            for d, h in zip(dbuf[j], host[s]):
+                d.copy_(h, non_blocking=True)
+            ready[j].record(copy)
+
+    def run(a, b):
+        issue_copy(a)
+        for s in range(a, b):
+            if s + 1 < b:
+                issue_copy(s + 1)
+            j = s % 2
+            comp.wait_event(ready[j])
+            f, ln, tc = dbuf[j]
+            dp.pipeline(FrameBatch(f, ln, tc, B.dev), sc.now + s, out=outs2[s], snap_out=False)
+            free[j].record(comp)
+    for j in range(2):
+        free[j].record(comp)
+    el, c, _, kern = timed(B, run, W, K, ranged=True)
+    B.sync()
+    same = all(torch.equal(outs[s], outs2[s]) for s in range(W + K))
+    B.close(dp)
+    byts = sum(t.numel() * t.element_size() for t in host[0])
+    log(f"config 4 + H2D: {int(c[268]) / el / 1e6:.1f} Mpps, records equal the device-resident run: {same} "
+        f"({time.time() - t0:.1f}s)")
+    return {"mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
+            "pcie_bytes_per_step": byts, "pcie_gbs": round(byts / (el / K) / 1e9, 2),
+            "records_equal_device_resident": bool(same),
+            "note": "frames + len + tc_index copied host->device every step (69 B/packet, pinned, double-buffered "
+                    "on a copy stream); "
+                    "reported beside the device-resident figure, never as the line's value"}
+
+
 # ----------------------------------------------------------------------------- config 5 (IPv6 pipeline)
-def bench_config5(args, dev):
+def bench_config5(args, B):
     """BASELINE config 5 through the path an IPv6 packet takes on a node: bpf_xdp's
     check_v6 (v6_dyn LPM, 10k /32-/127 prefixes; v6_fix hash, 100k /128s; endpoint
     check) -> bpf_netdev handle_ipv6 (identity from the flow label of cluster
@@ -590,66 +908,61 @@ def bench_config5(args, dev):
     10,485,760-entry LRU CT pre-filled to 8M entries."""
     import torch
     from cilium_amd import synth, stream
-    from cilium_amd.datapath import Datapath
+    from oracle import parity as PY
     W, K = 3, 4
     t0 = time.time()
     sc, P, meta = synth.config5_tables(n_pairs=args.pairs, prefill=args.ct6_prefill)
-    st = stream.Stream6Frames(P, meta, flows_per_step=1 << 20, device=dev)
+    st = stream.Stream6Frames(P, meta, flows_per_step=1 << 20, device=B.dev)
     S0 = 3
     rk, rv = st.reply_ct6_entries(S0 + W + K)
     ct6 = sc.maps["cilium_ct6_global"]
     ct6.keys, ct6.vals = synth.ct6_prefill(meta, rk, rv, sc.now)
-    dp = Datapath(sc, pin_prefix=None)
+    dp = B.datapath(sc)
     log(f"config5: tables + {sc.maps['cilium_ct6_global'].n()} pre-filled CT6 entries ({time.time() - t0:.1f}s)")
-    fbs, ps = [], []
+    div = parity_div(args, 1) * 2
+    a6, b6 = st.pair_addrs6()
+    pm = torch.from_numpy(PY.pair_sampled6(a6, b6, div).astype(np.uint8) |
+                          (PY.pair_sampled6(a6, b6, div * 8).astype(np.uint8) << 1)).to(B.dev)
+    fbs, got = [], []
     for s in range(W + K):
         f, lens, p = st.step(S0 + s)
-        fbs.append(FrameBatch(f, lens, None, dev))
-        ps.append(p)
-    outs = [torch.empty((b.n, 24), dtype=torch.uint8, device=dev) for b in fbs]
-    torch.cuda.synchronize()
-    el, c, _, kern = timed(lambda s: dp.pipeline(fbs[s], sc.now + s, out=outs[s], snap_out=False), W, K, dev)
+        fbs.append(FrameBatch(f, lens, None, B.dev))
+        got.append((fbs[-1], pm[p], torch.empty((f.shape[0], 24), dtype=torch.uint8, device=B.dev)))
+    B.sync()
+    el, c, _, kern = timed(B, lambda s: dp.pipeline(fbs[s], sc.now + s, out=got[s][2], snap_out=False), W, K)
     names = [k for k in kern]
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_config4(args, sc, st, dp, fbs, ps, outs, W, K, ct_names=("cilium_ct6_global",),
-                                  v6_pairs=st.pair_addrs6())
-    from cilium_amd import bpf
+        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct6_global",))
+    ct6_end, evictions = int(B.entries(dp, "cilium_ct6_global")), len(B.evict_log(dp, "cilium_ct6_global"))
+    B.close(dp)
     return {"workload": "config5: IPv6 bpf_xdp check_v6 (10k v6_dyn /32-/127 + 100k v6_fix /128) -> bpf_netdev "
                         "handle_ipv6 -> handle_policy ipv6_policy (ct_lookup6), CT6 max 10,485,760 (LRU) pre-filled "
                         f"to {args.ct6_prefill}, 1M new flows/step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
-            "ct6_entries_at_end": int(bpf.GetMapInfo(dp.fd["cilium_ct6_global"]).Entries),
-            "ct6_evictions": len(_evictions(dp, "cilium_ct6_global")),
+            "ct6_entries_at_end": ct6_end,
+            "ct6_evictions": evictions,
             "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)"),
             "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
-def _evictions(dp, name):
-    from cilium_amd._lib import lib, gf_ct_evict_rec
-    recs = (gf_ct_evict_rec * 4096)()
-    n = lib.gf_ct_evict_log(dp.fd[name], recs, 4096)
-    return [(r.seq, r.evicted) for r in recs[:max(0, min(n, 4096))]]
-
-
 # ----------------------------------------------------------------------------- endpoint egress (SURVEY §8(f) row 2)
-def bench_egress(args, dev):
+def bench_egress(args, B):
     """The from-container program (handle_ipv4_from_lxc) over frames sent by 256
     local endpoints (synth.TENANT per tenant), local deliveries continuing into handle_policy:
     4M flows, one 64-B frame each per step; each step a quarter of the flows
     starts anew (new source port), the rest are established."""
     import torch
     from cilium_amd import synth
-    from cilium_amd.datapath import Datapath
     W, K = 3, max(4, args.steps // 2)
     n = args.egress_flows
     t0 = time.time()
     sc, meta = synth.egress_tables(ct_max=args.ct_max)
     f, lens, lid, fh = synth.egress_flows(meta, n)
-    dp = Datapath(sc, pin_prefix=None)
+    dp = B.datapath(sc)
     log(f"egress: tables and {n} flows ({time.time() - t0:.1f}s)")
-    base = torch.from_numpy(f).to(dev)
+    base = torch.from_numpy(f).to(B.dev)
     q = n // 4
     frames = []
     for s in range(W + K):
@@ -659,15 +972,16 @@ def bench_egress(args, dev):
         sp = 1024 + (sp - 1024 + 7919 * (s + 1)) % 60000
         fs[a:a + q, 34], fs[a:a + q, 35] = (sp >> 8).to(torch.uint8), (sp & 0xff).to(torch.uint8)
         frames.append(fs)
-    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(B.dev)
     len_t, lid_t, fh_t = t(lens, np.int32), t(lid, np.int16), t(fh, np.int32)
-    fbs = [FrameBatch(frames[i], len_t, None, dev, lid_t, fh_t) for i in range(W + K)]
-    outs = [torch.empty((n, 24), dtype=torch.uint8, device=dev) for _ in range(W + K)]
-    el, c, _, kern = timed(lambda s: dp.egress(fbs[s], sc.now + s, out=outs[s], snap_out=False), W, K, dev)
+    fbs = [FrameBatch(frames[i], len_t, None, B.dev, lid_t, fh_t) for i in range(W + K)]
+    outs = [torch.empty((n, 24), dtype=torch.uint8, device=B.dev) for _ in range(W + K)]
+    el, c, _, kern = timed(B, lambda s: dp.egress(fbs[s], sc.now + s, out=outs[s], snap_out=False), W, K)
     log(f"egress: timed {K} steps ({time.time() - t0:.1f}s)")
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K)
+        cpu, par = oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K)
+    B.close(dp)
     return {"workload": "egress: bpf_lxc from-container handle_ipv4_from_lxc (+ handle_policy of local deliveries), "
                         f"256 endpoints, {n} flows/step (35% world, 20% tunnel, 25% local, 20% service "
                         "VIPs), 1/4 new per step",
@@ -677,7 +991,7 @@ def bench_egress(args, dev):
             "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
-def oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
+def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
     """Parity: tenant 0 (a closed set of flow groups: its endpoints only talk to
     each other, their services and remote peers) through the sequential oracle,
     records and CT entries compared.  CPU baseline: T oracle instances side by
@@ -694,7 +1008,7 @@ def oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
     par = Parity(f"tenant 0 of {nten} (its {TENANT} endpoints' flows: a closed set of flow groups), every step"
                  if nten > 1 else "every packet of every step (one tenant)")
     ref = OracleDP(sc)
-    lru_replay(dp, ref)
+    lru_replay(B, dp, ref)
     m0 = np.nonzero(ten == 0)[0]
     m0t = torch.from_numpy(m0).to(frames[0].device)
     for s in range(W + K):
@@ -703,7 +1017,7 @@ def oracle_egress(args, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
         par.records(outs[s][m0t].cpu().numpy().view(EG_OUT).ravel(), r, f"step {s}")
     t0set = {int(x) for x in synth_raw_be(meta["ep4"][:TENANT])}
     pred = lambda k, div: _tenant_keys(k, t0set)
-    compare_ct(par, dp, ref, "ct4", 14, 1, pred=pred)
+    compare_ct(B, par, dp, ref, "ct4", 14, 1, pred=pred)
     # CPU baseline: T instances over closed shares of the flow groups, the W + K steps (the
     # timed K measured): a tenant's local and service flows stay together, flows to world
     # and tunnel peers (no translation: the frame's own pair) spread by pair hash
@@ -786,16 +1100,33 @@ def _free_port():
     return p
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without the HIP runtime (the launcher
+    must not initialise the GPU before it starts the ranks): the device lists of
+    HIP/ROCR/CUDA_VISIBLE_DEVICES when set, else the GPU nodes of the KFD
+    topology (/sys/class/kfd/kfd/topology/nodes/*/gpu_id != 0)."""
+    lists = [os.environ[v] for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+             if v in os.environ]
+    if lists:
+        return min(len([x for x in v.split(",") if x.strip() not in ("", "-1")]) for v in lists)
+    n = 0
+    for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            with open(p) as f:
+                n += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    return n
+
+
 def spawn_ranks(n, argv):
     """`bench.py --gpus N` run directly (no torch.distributed launcher): start the N
-    rank processes before anything here touches a GPU (each child pins
-    LOCAL_RANK), wait for all, return the worst exit status."""
-    if not os.environ.get("GPUFLOW_BENCH_SELFTEST"):
-        import torch
-        vis = torch.cuda.device_count()         # does not initialise the GPU on this image
-        if n > vis:
-            log(f"--gpus {n} but only {vis} GPU(s) visible")
-            return 2
+    rank processes (each child pins LOCAL_RANK) before this process has imported
+    torch or touched the HIP runtime, wait for all, return the worst exit status."""
+    vis = visible_gpus()
+    if n > vis and not os.environ.get("GPUFLOW_BENCH_SHARE_GPU"):
+        log(f"--gpus {n} but only {vis} GPU(s) visible")
+        return 2
     port = _free_port()
     procs = []
     for r in range(n):
@@ -806,24 +1137,6 @@ def spawn_ranks(n, argv):
     for p in procs:
         rc = max(rc, p.wait())
     return rc
-
-
-def selftest_line(rank, world, backend):
-    """The launcher's CPU rehearsal (GPUFLOW_BENCH_SELFTEST=1, gloo): rendezvous,
-    the counter-block all-reduce and the single-line output, no GPU."""
-    import torch
-    import torch.distributed as dist
-    c = torch.zeros(512, dtype=torch.int64)
-    c[268] = 1000 + rank                      # packets of this rank
-    c[133] = rank + 1
-    tt = torch.tensor([0.5 + 0.1 * rank], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-    return {"metric": METRIC, "value": round(int(c[268]) / float(tt.item()) / 1e6, 6), "unit": "Mpps",
-            "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": round(float(tt.item()) * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "selftest",
-            "config": {"workload": "launcher selftest", "backend": backend}, "verdicts": verdicts(c.numpy())}
 
 
 def main():
@@ -842,61 +1155,77 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="config 2: the steps through gf_policy_ingress_classify_batches (schedule overlap)")
     ap.add_argument("--no-extra", action="store_true", help="config 2 only (skip the other configurations)")
+    ap.add_argument("--no-h2d", action="store_true", help="config 4: skip the leg with the host->device copy")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--parity-div", type=int, default=4, help="parity sample: 1 in N address pairs")
+    ap.add_argument("--parity-div", type=int, default=0,
+                    help="parity sample: 1 in N address pairs (default: every pair at N=1, 1 in 2 per rank at N>1)")
     ap.add_argument("--egress-flows", type=int, default=4 << 20)
     args = ap.parse_args()
 
-    selftest = bool(os.environ.get("GPUFLOW_BENCH_SELFTEST"))
+    rehearsal = bool(os.environ.get("GPUFLOW_BENCH_SELFTEST"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world != args.gpus:
         log(f"WORLD_SIZE {world} != --gpus {args.gpus}: the launcher's world size is used")
 
-    import torch
     import torch.distributed as dist
-    if selftest:
+    if rehearsal:
+        B = Rehearsal()
         if world > 1:
             dist.init_process_group("gloo")
-        res = selftest_line(rank, world, "gloo")
-        if rank == 0:
-            print(json.dumps(res), flush=True)
+    else:
+        B = Gpu(local)
         if world > 1:
-            dist.destroy_process_group()
-        return
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+            backend = os.environ.get("GPUFLOW_BENCH_BACKEND", "nccl")      # nccl = RCCL over xGMI
+            dist.init_process_group(backend, **({"device_id": B.dev} if backend == "nccl" else {}))
 
     if args.config == "2":
-        res = bench_config2(args, dev, rank, world)
-        if world == 1 and not args.no_extra:
+        res = bench_config2(args, B, rank, world, local_world)
+        extra = {} if args.no_extra else (
+            {k: v for k, v in EXTRA.items()} if world == 1 and not rehearsal else
+            {"4": lambda a, b: bench_config4(a, b, rank, world, "owned", local_world),
+             "4x": lambda a, b: bench_config4(a, b, rank, world, "exchange", local_world)} if world > 1 else
+            {"4": lambda a, b: bench_config4(a, b, rank, world, "owned", local_world)})
+        if extra:
             res["configs"] = {}
-            for k, fn in EXTRA.items():
-                t0 = time.time()
-                try:
-                    res["configs"][k] = add_traffic(k, fn(args, dev))
-                except Exception as e:                       # reported, never silently dropped
-                    res["configs"][k] = {"error": f"{type(e).__name__}: {e}"}
-                log(f"config {k}: {res['configs'][k].get('mpps')} Mpps ({time.time() - t0:.1f}s)")
+        for k, fn in extra.items():
+            t0 = time.time()
+            try:
+                res["configs"][k] = add_traffic(k, fn(args, B))
+            except Exception as e:                       # reported, never silently dropped
+                if world > 1:
+                    raise                                # a rank cannot skip a collective the others run
+                res["configs"][k] = {"error": f"{type(e).__name__}: {e}"}
+            log(f"config {k}: {res['configs'][k].get('mpps')} Mpps ({time.time() - t0:.1f}s)")
+            if not rehearsal:
+                import torch
                 torch.cuda.empty_cache()
     else:
-        if world > 1:
-            raise SystemExit("--config other than 2 runs on one GPU")
-        r = add_traffic(args.config, EXTRA[args.config](args, dev))
-        res = {"metric": METRIC, "value": r["mpps"], "unit": "Mpps", "n_gpus": 1, "steps": r["steps"],
+        if world > 1 and args.config != "4":
+            raise SystemExit("--config other than 2 and 4 runs on one GPU")
+        if args.config == "4":
+            r = bench_config4(args, B, rank, world, "owned", local_world)
+        else:
+            r = EXTRA[args.config](args, B)
+        r = add_traffic(args.config, r)
+        res = {"metric": METRIC, "value": r["mpps"], "unit": "Mpps", "n_gpus": world, "steps": r["steps"],
                "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "u32", "data": "synthetic",
                "config": {"workload": r["workload"], "packets_per_step": r["packets_per_step"]},
                "roofline": r["roofline"], "kernels_ms_per_step": r["kernels_ms_per_step"],
                "cpu_baseline": r["cpu_baseline"], "parity": r.get("parity")}
+        if "h2d" in r:
+            res["h2d"] = r["h2d"]
     if rank == 0:
-        from cilium_amd import _lib
-        res["build_id"] = _lib.BUILD_ID          # gf_build_id(): the sources libgpuflow.so was compiled from
+        if rehearsal:
+            res["data"] = "rehearsal (GPUFLOW_BENCH_SELFTEST): the oracle stood in for the device; not a measurement"
+        else:
+            from cilium_amd import _lib
+            res["build_id"] = _lib.BUILD_ID      # gf_build_id(): the sources libgpuflow.so was compiled from
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -278,11 +278,16 @@ class Datapath:
         return d
 
     def close(self):
-        for fd in self.fd.values():
+        """Close the program objects, then the maps (a program holds its maps, so
+        their device tables are released once both are closed)."""
+        progs = [self.pipe, self.policy_array, self.lb_prog, self.xdp_prog] + list(getattr(self, "lxc_progs", []))
+        for h in [h for h in progs if h] + list(self.fd.values()):
             try:
-                bpf.ObjClose(fd)
+                bpf.ObjClose(h)
             except OSError:
                 pass
+        self.pipe = self.policy_array = self.lb_prog = self.xdp_prog = None
+        self.lxc_progs = []
         self.fd = {}
 
 

@@ -1,36 +1,82 @@
-"""bench.py --gpus N without a torch.distributed launcher spawns the N rank
-processes itself; rehearsed on the CPU with gloo (GPUFLOW_BENCH_SELFTEST):
-rendezvous, the counter-block all-reduce, the timing max and the single JSON
-line of rank 0."""
+"""bench.py on N ranks, rehearsed on the CPU (GPUFLOW_BENCH_SELFTEST: gloo ranks,
+CPU tensors, small tables, the oracle standing in for the device).  The same
+code the GPU run takes: the launcher that spawns the ranks without touching the
+HIP runtime, the flow-group-sharded streams, config 4 with frames arriving on
+their owner and with the partition + all-to-all exchange, the parity legs on
+every rank and their all-reduce, the counter-block all-reduce and the single
+JSON line of rank 0."""
 import json
 import os
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--pairs", "512", "--flows-per-step", "2048", "--steps", "2", "--warmup", "1", "--ct-max", "65536"]
+
+# The parent runs bench.py's main() in-process and reports whether it imported
+# torch (i.e. could have initialised the HIP runtime) before the ranks ended.
+_PARENT = r"""
+import runpy, sys, json
+sys.argv = ["bench.py"] + sys.argv[1:]
+rc = 0
+try:
+    runpy.run_path(%r, run_name="__main__")
+except SystemExit as e:
+    rc = e.code or 0
+print("PARENT " + json.dumps({"rc": rc, "torch_imported": "torch" in sys.modules}), flush=True)
+""" % os.path.join(ROOT, "bench.py")
 
 
-def _run(n):
-    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1")
-    env.pop("WORLD_SIZE", None)
-    env.pop("RANK", None)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n)], env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert p.returncode == 0, p.stderr[-2000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout
-    return json.loads(lines[0])
+def _run(n, extra=(), visible="0,1"):
+    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1", HIP_VISIBLE_DEVICES=visible)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-c", _PARENT, "--gpus", str(n)] + SMALL + list(extra), env=env,
+                       capture_output=True, text=True, timeout=600, cwd="/tmp")
+    parent = json.loads([l for l in p.stdout.splitlines() if l.startswith("PARENT ")][-1][7:])
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return parent, lines, p.stderr
 
 
-def test_launcher_spawns_world_2_and_all_reduces():
-    r = _run(2)
-    assert r["n_gpus"] == 2
-    # each rank counts 1000 + rank packets and rank + 1 policy drops; rank 1 takes 0.6 s
-    assert r["verdicts"]["drop_reasons"] == {"133": 3}
-    assert r["ms_per_step"] == 600.0
-    assert abs(r["value"] - 2001 / 0.6 / 1e6) < 1e-6
+def test_launcher_world_2_rehearsal():
+    parent, lines, err = _run(2)
+    assert parent == {"rc": 0, "torch_imported": False}, err[-3000:]
+    assert len(lines) == 1
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["value"] > 0
+    # every packet of both ranks' timed steps is in the all-reduced counter block
+    v = r["verdicts"]
+    assert v["pass"] + v["drop"] + v["redirect"] == 2 * r["config"]["packets_per_step_per_gpu"] * r["steps"]
+    # parity on each rank, summed
+    p = r["parity"]
+    assert p["ranks"] == 2 and p["mismatches"] == 0 and p["ct_mismatches"] == 0
+    assert p["packets_compared"] > 10_000 and p["ct_entries_compared"] > 1_000
+    c4, c4x = r["configs"]["4"], r["configs"]["4x"]
+    for c in (c4, c4x):
+        assert c["n_gpus"] == 2 and c["parity"]["mismatches"] == 0 and c["parity"]["ct_mismatches"] == 0
+        assert c["parity"]["packets_compared"] > 5_000 and c["parity"]["ranks"] == 2
+    assert "all-to-all" in c4x["ingest"] and "owns" in c4["ingest"]
+    # the exchange moved every frame to its owner: the same packets, the same verdicts
+    assert c4["verdicts"] == c4x["verdicts"] and c4["packets_per_step"] == c4x["packets_per_step"]
+    assert c4["parity"]["packets_compared"] == c4x["parity"]["packets_compared"]
 
 
-def test_launcher_single_rank():
-    r = _run(1)
-    assert r["n_gpus"] == 1 and r["verdicts"]["drop_reasons"] == {"133": 1}
+def test_launcher_single_rank_and_device_count():
+    parent, lines, err = _run(1)
+    assert parent["rc"] == 0 and lines[0]["n_gpus"] == 1 and lines[0]["parity"]["mismatches"] == 0, err[-3000:]
+    assert lines[0]["configs"]["4"]["parity"]["mismatches"] == 0
+    # more ranks than visible GPUs: refused before any rank starts (counted without HIP)
+    parent, lines, err = _run(3, visible="0,1")
+    assert parent == {"rc": 2, "torch_imported": False} and not lines
+
+
+def test_visible_gpus_without_hip(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
+    assert bench.visible_gpus() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus() == 0

@@ -469,7 +469,7 @@ def test_pipeline_partition_owners():
     restatement computes it from the oracle's LB results; stable owner order and
     per-rank counts."""
     from cilium_amd import shard
-    from test_shard import owners_host
+    from oracle.parity import owners_host
     sc = synth.pipeline_fuzz(seed=22, n_packets=20000, n_batches=2)
     dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
     for world, rank in ((2, 1), (3, 0), (8, 5)):

@@ -12,24 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from cilium_amd import synth, shard, stream
-
-
-def owners_host(lb_out, nd6, pk, rank, world):
-    """The owner rule of gf_pipeline_partition restated on the host (checker)."""
-    f = pk.frames
-    et = (f[:, 12].astype(np.uint32) << 8) | f[:, 13]
-    v4 = (et == 0x0800) & (pk.lens >= 34)
-    v6 = (et == 0x86DD) & (pk.lens >= 54)
-    sa = f[:, 26:30].copy().view(">u4").ravel().astype(np.uint32)
-    da = f[:, 30:34].copy().view(">u4").ravel().astype(np.uint32)
-    nd = lb_out["new_daddr4"].astype(">u4").view("<u4").astype(np.uint32)      # raw be32 -> host order
-    da = np.where(lb_out["slave"] > 0, nd, da)
-    r = np.full(pk.n, rank, np.int64)
-    r[v4] = stream.pair_rank(sa[v4], da[v4], world)
-    d6 = np.where((lb_out["slave"] > 0)[:, None], nd6, f[:, 38:54])
-    if v6.any():
-        r[v6] = shard.pair_rank6(f[v6, 22:38], d6[v6], world)
-    return r
+from oracle.parity import owners_host  # noqa: F401  (the owner rule's host restatement)
 
 
 def _ct_owner(k, world):
