@@ -7,21 +7,37 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include "gf_common.h"
 #include "../../include/gpuflow.h"
 
 namespace gf {
 
 // Locking (the reference: one RWMutex per bpf.Map, pkg/bpf/map.go:121, and
-// per-element RCU in the kernel):
+// per-element RCU in the kernel; its programs run concurrently on every CPU):
 //  * every map operation holds that map's own mutex (Map::mu);
-//  * program objects, the cilium_policy arrays, node config and the classify
-//    calls (which share the per-call device workspaces) hold prog_lock(), and a
-//    classify also holds the mutex of every map it binds while it syncs them
-//    (MapLocks, address order, so two classify calls or a classify and a map
-//    operation never deadlock);
+//  * loading / changing program objects, cilium_policy arrays and the node
+//    config holds prog_lock() exclusively; classify calls hold it shared, so
+//    calls run concurrently with each other but never with a reconfiguration;
+//  * a classify call holds its stream's call context (the device workspaces
+//    of one call: CallCtx, gf_kernels.hip), the mutex of the cilium_policy array
+//    it runs and the mutex of every map it binds (MapLocks, address order, so two
+//    classify calls or a classify and a map operation never deadlock); on the
+//    device it is ordered after the last call that used any of those objects on
+//    another stream (OrderPt), so calls over disjoint programs and maps on
+//    different streams overlap;
 //  * the object registry (handles, pins) has its own short lock.
-std::recursive_mutex &prog_lock();
+// Lock order: prog_lock -> call context -> policy array -> maps -> registry.
+std::shared_mutex &prog_lock();
+
+// The device-side order of the calls that use one object (map, policy array):
+// the event recorded at the end of the last such call and its stream.
+struct OrderPt {
+    hipEvent_t ev = nullptr;
+    hipStream_t s = nullptr;
+    bool have = false;
+    ~OrderPt() { if (ev) (void)hipEventDestroy(ev); }
+};
 std::mutex &reg_lock();
 
 // ---- device buffer ----
@@ -75,6 +91,7 @@ struct Obj {
 struct Map : Obj {
     uint32_t type, ksz, vsz, max_entries, flags;
     std::recursive_mutex mu;    // this map's lock (pkg/bpf/map.go:121)
+    OrderPt ord;                // device order of the classify calls that bind it
     // hash types
     HTab ht;
     bool host_valid = true;     // host shadow up to date
@@ -169,6 +186,8 @@ struct PolicyArray : Obj {
     std::vector<uint8_t> h_cfgs;       // last uploaded program table (change detection)
     std::vector<uint16_t> h_slot_of;
     bool dirty = true;
+    std::mutex mu;             // one classify call at a time per array (its device image)
+    OrderPt ord;
     PolicyArray() : Obj(ObjKind::PolicyArray) {}
 };
 

@@ -4005,6 +4005,7 @@ namespace {
 struct ProfEntry { std::string name; hipEvent_t a, b; };
 struct Prof {
     bool on = false;
+    std::mutex mu;                     // concurrent classify calls record launches
     std::vector<ProfEntry> pending;
     std::map<std::string, std::pair<uint32_t, double>> acc;
 };
@@ -4023,10 +4024,12 @@ struct ProfScope {
     ~ProfScope() {
         if (!on) return;
         (void)hipEventRecord(e.b, s);
+        std::lock_guard<std::mutex> g(prof().mu);
         prof().pending.push_back(e);
     }
 };
 void prof_drain() {
+    std::lock_guard<std::mutex> g(prof().mu);
     for (auto &e : prof().pending) {
         float ms = 0;
         if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
@@ -4043,15 +4046,50 @@ void prof_drain() {
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
 };
-// Two workspaces: gf_policy_ingress_classify_batches builds the schedule of
-// batch k+1 in one while handle_policy of batch k runs from the other.
-int g_ws_slot = 0;
-Workspace &ws() { static Workspace w[2]; return w[g_ws_slot]; }
+// ---- call contexts: the device workspaces of one classify call.  Each HIP
+// stream has its own, so calls on different streams (over disjoint programs and
+// maps, see CallOrder) run concurrently, host and device; calls on one stream
+// take its context one at a time.  Workspace accessors keep one instance of
+// their type per context (CallCtx::get).
+struct CallCtx {
+    std::mutex mu;
+    int ws_slot = 0;      // gf_policy_ingress_classify_batches: schedule k+1 builds in one while k runs
+    std::map<const void *, std::shared_ptr<void>> bag;
+    template <class T> T &get(const void *tag) {
+        auto &p = bag[tag];
+        if (!p) p = std::make_shared<T>();
+        return *static_cast<T *>(p.get());
+    }
+};
+thread_local CallCtx *t_ctx = nullptr;
+CallCtx &ctx_for(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<hipStream_t, std::unique_ptr<CallCtx>> all;
+    std::lock_guard<std::mutex> g(mu);
+    auto &c = all[s];
+    if (!c) c = std::make_unique<CallCtx>();
+    return *c;
+}
+// The calling thread's context (map API paths outside a classify call: the
+// null stream's).
+CallCtx &cur_ctx() { return t_ctx ? *t_ctx : ctx_for(nullptr); }
+struct CtxScope {
+    CallCtx *prev, *c;
+    std::unique_lock<std::mutex> l;
+    explicit CtxScope(hipStream_t s) : prev(t_ctx), c(&ctx_for(s)), l(c->mu) { t_ctx = c; }
+    ~CtxScope() { t_ctx = prev; }
+};
+Workspace &ws() {
+    static const char tag = 0;
+    CallCtx &c = cur_ctx();
+    struct Two { Workspace w[2]; };
+    return c.get<Two>(&tag).w[c.ws_slot];
+}
 gf_event_ring &event_ring() { static gf_event_ring r{}; return r; }
 struct PipeWs {
     DevBuf s6, d6;             // IPv6 addresses of the rewritten frames (read by handle_policy)
 };
-PipeWs &pipe_ws() { static PipeWs w; return w; }
+PipeWs &pipe_ws() { static const char tag = 0; return cur_ctx().get<PipeWs>(&tag); }
 
 int check_cols(const gf_pkt_cols *p) {
     if (!p) return -EFAULT;
@@ -4093,26 +4131,41 @@ void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, X
     if (lxc && lxc->addr_set(20, 8192, s, &x.lxset, &x.lxbits, &x.lxzero)) x.lxset = nullptr;
 }
 
-// ---- locking and cross-stream ordering of the calls that share the device
-// workspaces (ws(), pipe_ws(), eg_ws(), px_ws(), the event / partition / GC
-// buffers).  Calls run one at a time on the host (prog_lock), and on the device
-// each call is ordered after the previous one even when the caller switches
-// streams: the call waits on an event recorded at the end of the last call, so a
-// kernel still reading a workspace (or a map replica) on another stream finishes
-// before this call rewrites it.
+// ---- device-side order of the calls that share an object.  Every map a call
+// binds and the cilium_policy array it runs carry the event of the last call
+// that used them (OrderPt): a call on another stream first waits on those
+// events, so a kernel still reading or writing a map replica (or a program
+// table) finishes before this call pushes into it or runs over it, and it records
+// its own end into each of them (under the objects' locks).  The workspaces are
+// per stream (CallCtx), so calls over disjoint objects on different streams do
+// not wait on each other.  With an event ring set, calls append to it in turn.
+std::mutex &ring_mu() { static std::mutex m; return m; }
+OrderPt &ring_ord() { static OrderPt o; return o; }
 struct CallOrder {
     hipStream_t s;
-    explicit CallOrder(hipStream_t s_) : s(s_) {
-        auto &o = state();
-        if (o.have && o.last != s) (void)hipStreamWaitEvent(s, o.ev, 0);
+    std::vector<OrderPt *> pts;
+    std::unique_lock<std::mutex> ring;
+    CallOrder(hipStream_t s_, std::vector<OrderPt *> p) : s(s_), pts(std::move(p)) {
+        if (event_ring().records) {
+            ring = std::unique_lock<std::mutex>(ring_mu());
+            pts.push_back(&ring_ord());
+        }
+        for (OrderPt *o : pts)
+            if (o->have && o->s != s) (void)hipStreamWaitEvent(s, o->ev, 0);
+    }
+    CallOrder(hipStream_t s_, const MapLocks &L, PolicyArray *a = nullptr) : CallOrder(s_, order_pts(L, a)) {}
+    static std::vector<OrderPt *> order_pts(const MapLocks &L, PolicyArray *a) {
+        std::vector<OrderPt *> v;
+        for (Map *m : L.held) v.push_back(&m->ord);
+        if (a) v.push_back(&a->ord);
+        return v;
     }
     ~CallOrder() {
-        auto &o = state();
-        if (!o.ev && hipEventCreateWithFlags(&o.ev, hipEventDisableTiming) != hipSuccess) { o.ev = nullptr; return; }
-        if (hipEventRecord(o.ev, s) == hipSuccess) { o.last = s; o.have = true; }
+        for (OrderPt *o : pts) {
+            if (!o->ev && hipEventCreateWithFlags(&o->ev, hipEventDisableTiming) != hipSuccess) { o->ev = nullptr; continue; }
+            if (hipEventRecord(o->ev, s) == hipSuccess) { o->s = s; o->have = true; }
+        }
     }
-    struct St { hipEvent_t ev = nullptr; hipStream_t last = nullptr; bool have = false; };
-    static St &state() { static St st; return st; }
 };
 void lock_lxc_maps(MapLocks &L, const std::shared_ptr<ProgLxc> &p) {
     for (auto m : {p->policy, p->ct4, p->ct6, p->cidr4, p->cidr6, p->revnat4, p->revnat6, p->lb4, p->ipcache,
@@ -4128,13 +4181,13 @@ void lock_xdp_maps(MapLocks &L, const ProgXdp &x) { L.add(x.m4h); L.add(x.m4l); 
 
 // blocks of BLOCK threads that fill the device at `per_cu` blocks per CU
 uint32_t resident_blocks(uint32_t per_cu) {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
+    static const int cus = [] {                   // thread-safe one-time init (concurrent calls)
+        int dev = 0, c = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return c;
+    }();
     return (uint32_t)cus * per_cu;
 }
 
@@ -4155,7 +4208,7 @@ int gf_parse_frames(const gf_frames *fr, gf_pkt_cols_out *o, void *stream) {
 }
 
 int gf_xdp_prog_load(const gf_xdp_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgXdp>();
     p->cfg = *cfg;
@@ -4178,7 +4231,7 @@ int gf_xdp_prog_load(const gf_xdp_cfg *cfg) {
 }
 
 int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(prog);
     if (!o || o->kind != ObjKind::ProgXdp) return -EBADF;
     auto p = std::static_pointer_cast<ProgXdp>(o);
@@ -4186,10 +4239,11 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     if (c <= 0) return c;
     if (!verdict) return -EFAULT;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
     MapLocks L;
     lock_xdp_maps(L, *p);
     L.lock();
-    CallOrder co(s);
+    CallOrder co(s, L);
     int r;
     if ((r = push_map(p->m4h, s)) || (r = push_map(p->m4l, s)) || (r = push_map(p->m6h, s)) ||
         (r = push_map(p->m6l, s)) || (r = push_map(p->lxc, s)))
@@ -4249,7 +4303,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
 }
 
 int gf_lb_prog_load(const gf_lb_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgLb>();
     p->cfg = *cfg;
@@ -4267,7 +4321,7 @@ int gf_lb_prog_load(const gf_lb_cfg *cfg) {
 }
 
 int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *nd6, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(prog);
     if (!o || o->kind != ObjKind::ProgLb) return -EBADF;
     auto p = std::static_pointer_cast<ProgLb>(o);
@@ -4275,10 +4329,11 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
     if (c <= 0) return c;
     if (!out) return -EFAULT;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
     MapLocks ML;
     ML.add(p->lb4); ML.add(p->lb6);
     ML.lock();
-    CallOrder co(s);
+    CallOrder co(s, ML);
     int r;
     if ((r = push_map(p->lb4, s)) || (r = push_map(p->lb6, s))) return r;
     LbDev L{};
@@ -4292,7 +4347,7 @@ int gf_lb_classify(int prog, const gf_pkt_cols *pkts, gf_lb_out *out, uint8_t *n
 }
 
 int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     if (cfg->n_l4_ingress > GF_MAX_L4_INGRESS || cfg->n_l4_egress > GF_MAX_L4_INGRESS ||
         cfg->n_portmap > GF_MAX_PORTMAP)
@@ -4326,7 +4381,7 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
 }
 
 int gf_set_event_ring(const gf_event_ring *ring) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!ring) { event_ring() = gf_event_ring{}; return 0; }
     if (!ring->records || !ring->count) return -EFAULT;
     event_ring() = *ring;
@@ -4334,7 +4389,7 @@ int gf_set_event_ring(const gf_event_ring *ring) {
 }
 
 int gf_prof_enable(int on) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     prof_drain();
     prof().acc.clear();
     prof().on = on != 0;
@@ -4342,7 +4397,7 @@ int gf_prof_enable(int on) {
 }
 
 int gf_prof_read(gf_prof_rec *out, int max) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (max < 0 || (max > 0 && !out)) return -EFAULT;
     prof_drain();
     int k = 0;
@@ -4358,12 +4413,12 @@ int gf_prof_read(gf_prof_rec *out, int max) {
 }
 
 int gf_policy_array_create(void) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     return new_handle(std::make_shared<PolicyArray>());
 }
 
 int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     if (lxc_id > 0xffff) return -E2BIG;
@@ -4383,7 +4438,7 @@ int gf_policy_array_update(int array, uint32_t lxc_id, int prog) {
 // Trace notifications of a call: per-packet marks and captures (GF_TR_*),
 // allocated and the marks cleared by the caller before its first kernel.
 struct TraceWs { DevBuf mark, px, in; };
-static TraceWs &trace_ws() { static TraceWs t; return t; }
+static TraceWs &trace_ws() { static const char tag = 0; return cur_ctx().get<TraceWs>(&tag); }
 struct PassArgs {                  // what the pipeline / egress callers pass to their handle_policy pass
     uint32_t kind;                 // 1 pipeline, 2 egress
     uint32_t *rlog, *rlog_n;       // egress connection groups: the related-entry log (null: written inline)
@@ -4412,7 +4467,10 @@ static int trace_prepare(uint32_t n, bool with_in, hipStream_t s) {
 static int emit_drop_events(EvSrc E, hipStream_t s) {
     gf_event_ring R = event_ring();
     if (!R.records || !R.count || !R.capacity || E.n == 0) return 0;
-    static DevBuf blk, boff, tmp;
+    struct EvWs { DevBuf blk, boff, tmp; };
+    static const char tag = 0;
+    EvWs &ew = cur_ctx().get<EvWs>(&tag);
+    DevBuf &blk = ew.blk, &boff = ew.boff, &tmp = ew.tmp;
     const uint32_t nb = (E.n + BLOCK - 1) / BLOCK;
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     int r;
@@ -4569,7 +4627,7 @@ static int schedule_groups(uint32_t n, hipStream_t s) {
 // cilium_proxy{4,6} update log of one launch (pol_redirect) and its in-order
 // apply after the launch (see k_px_apply).
 struct PxWs { DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp; };
-static PxWs &px_ws() { static PxWs w; return w; }
+static PxWs &px_ws() { static const char tag = 0; return cur_ctx().get<PxWs>(&tag); }
 // keep: continue the log the from-container pass of the same egress call wrote
 // (each packet logs at most one update: an egress redirect is never delivered).
 static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X, bool keep = false) {
@@ -4941,13 +4999,13 @@ struct PipeSync {
         return 0;
     }
 };
-static PipeSync &pipe_sync() { static PipeSync p; return p; }
+static PipeSync &pipe_sync() { static const char tag = 0; return cur_ctx().get<PipeSync>(&tag); }
 
 extern "C" {
 
 int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols *const *batches,
                                        const uint32_t *now_sec, gf_ingress_out *const *outs, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     auto a = std::static_pointer_cast<PolicyArray>(o);
@@ -4959,10 +5017,12 @@ int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols
         if (batches[k]->n > (1u << 30)) return -E2BIG;
     }
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
+    std::lock_guard<std::mutex> ag(a->mu);
     MapLocks L;
     lock_array_maps(L, a);
     L.lock();
-    CallOrder co(s);
+    CallOrder co(s, L, a.get());
     PipeSync &P = pipe_sync();
     int r;
     if ((r = P.init())) return r;
@@ -4973,9 +5033,9 @@ int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols
     auto prep = [&](uint32_t k) -> int {                  // batch k's schedule on the aux stream, workspace k & 1
         const int slot = (int)(k & 1u);
         if (k >= 2 && hip_ok(hipStreamWaitEvent(P.aux, P.done[slot], 0), "aux wait done")) return -EIO;
-        g_ws_slot = slot;
+        cur_ctx().ws_slot = slot;
         int rr = batches[k]->n ? ingress_prepare(a, batches[k], P.aux) : 0;
-        g_ws_slot = 0;
+        cur_ctx().ws_slot = 0;
         if (rr) return rr;
         return hip_ok(hipEventRecord(P.built[slot], P.aux), "built") ? -EIO : 0;
     };
@@ -4985,10 +5045,10 @@ int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols
         const int slot = (int)(k & 1u);
         if (hip_ok(hipStreamWaitEvent(s, P.built[slot], 0), "wait built")) return -EIO;
         if (batches[k]->n) {
-            g_ws_slot = slot;
+            cur_ctx().ws_slot = slot;
             r = ingress_run(a, batches[k], now_sec[k], outs[k], s, PackFn(), nullptr, nullptr, nullptr, 0, nullptr,
                             true, false, true);
-            g_ws_slot = 0;
+            cur_ctx().ws_slot = 0;
             if (r) return r;
         }
         if (hip_ok(hipEventRecord(P.done[slot], s), "done")) return -EIO;
@@ -4998,7 +5058,7 @@ int gf_policy_ingress_classify_batches(int array, uint32_t nb, const gf_pkt_cols
 
 int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_sec, gf_ingress_out *out,
                                void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     auto a = std::static_pointer_cast<PolicyArray>(o);
@@ -5006,16 +5066,18 @@ int gf_policy_ingress_classify(int array, const gf_pkt_cols *pkts, uint32_t now_
     if (c <= 0) return c;
     if (!out) return -EFAULT;
     if (pkts->n > (1u << 30)) return -E2BIG;
+    CtxScope cx((hipStream_t)stream);
+    std::lock_guard<std::mutex> ag(a->mu);
     MapLocks L;
     lock_array_maps(L, a);
     L.lock();
-    CallOrder co((hipStream_t)stream);
+    CallOrder co((hipStream_t)stream, L, a.get());
     return ingress_run(a, pkts, now_sec, out, (hipStream_t)stream);
 }
 
 // ---- full pipeline ----
 int gf_pipeline_load(const gf_pipeline_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     auto p = std::make_shared<ProgPipe>();
     p->cfg = *cfg;
@@ -5041,7 +5103,7 @@ int gf_pipeline_load(const gf_pipeline_cfg *cfg) {
 
 int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_pipeline_out *out,
                          uint8_t *nd6, uint8_t *snap_out, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(pipe);
     if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
     auto p = std::static_pointer_cast<ProgPipe>(o);
@@ -5052,13 +5114,15 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     if (fr.snap_stride < 14) return -EINVAL;
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
+    std::lock_guard<std::mutex> ag(p->policy->mu);
     MapLocks L;
     if (p->xdp) lock_xdp_maps(L, *p->xdp);
     if (p->lb) { L.add(p->lb->lb4); L.add(p->lb->lb6); }
     L.add(p->lxc);
     lock_array_maps(L, p->policy);
     L.lock();
-    CallOrder co(s);
+    CallOrder co(s, L, p->policy.get());
     int r;
     const uint32_t n = fr.n;
     PipeDev P{};
@@ -5129,7 +5193,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
 // ---- ingest re-partition ----
 int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, uint32_t nranks, uint32_t *owner,
                           uint32_t *order, uint32_t *counts, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(pipe);
     if (!o || o->kind != ObjKind::ProgPipe) return -EBADF;
     auto p = std::static_pointer_cast<ProgPipe>(o);
@@ -5137,10 +5201,11 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, 
     if (nranks == 0 || nranks > 65536 || self_rank >= nranks) return -EINVAL;
     const gf_frames &fr = b->frames;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
     MapLocks L;
     if (p->lb) { L.add(p->lb->lb4); L.add(p->lb->lb6); }
     L.lock();
-    CallOrder co(s);
+    CallOrder co(s, L);
     if (hip_ok(hipMemsetAsync(counts, 0, (size_t)nranks * 4, s), "partition counts")) return -EIO;
     if (fr.n == 0) return 0;
     if (!fr.snap || !fr.len) return -EFAULT;
@@ -5156,7 +5221,10 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, 
         P.has_lb = 1;
     }
     const uint32_t n = fr.n;
-    static DevBuf keys, vals, tmp;
+    struct PartWs { DevBuf keys, tmp; };
+    static const char tag = 0;
+    PartWs &pw = cur_ctx().get<PartWs>(&tag);
+    DevBuf &keys = pw.keys, &tmp = pw.tmp;
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
     if ((r = grow(keys, (size_t)n * 4))) return r;
     {
@@ -5181,13 +5249,13 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *b, uint32_t self_rank, 
 
 // ---- conntrack GC ----
 int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto m = get_map(map);
     if (!m) return -EBADF;
     if (m->is_lpm() || (m->ksz != 14 && m->ksz != 40) || m->vsz != 48) return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::recursive_mutex> mg(m->mu);
-    CallOrder co(s);
+    CallOrder co(s, std::vector<OrderPt *>{&m->ord});
     const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
     if (m->host_valid || !m->dev_valid || !m->d_slots.p) {
         // host shadow authoritative: delete there, the replica is rebuilt on the next push
@@ -5483,7 +5551,7 @@ struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
              uint32_t hz_gen = 0, hz_cap = 0;
              std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
              uint32_t vip4_mask = 0, vip6_mask = 0; bool vip4_any = false, vip6_any = false; };
-EgWs &eg_ws() { static EgWs w; return w; }
+EgWs &eg_ws() { static const char tag = 0; return cur_ctx().get<EgWs>(&tag); }
 }  // namespace
 
 static int egress_ordered(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch *b, uint32_t now_sec,
@@ -5876,7 +5944,7 @@ static int egress_runs(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
 
 extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t now_sec, gf_egress_out *out,
                                       uint8_t *snap_out, void *stream) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::shared_lock<std::shared_mutex> g(prog_lock());
     auto o = get_obj(array);
     if (!o || o->kind != ObjKind::PolicyArray) return -EBADF;
     auto a = std::static_pointer_cast<PolicyArray>(o);
@@ -5887,10 +5955,12 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
+    std::lock_guard<std::mutex> ag(a->mu);
     MapLocks L;
     lock_array_maps(L, a);
     L.lock();
-    CallOrder co(s);
+    CallOrder co(s, L, a.get());
     static const bool nocheck = getenv("GF_EG_NOCHECK") != nullptr;     // diagnosis only: the unordered schedule
     static const bool dbg = getenv("GF_HZ_DEBUG") != nullptr;
     if (!dbg) return egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);

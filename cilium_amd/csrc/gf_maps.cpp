@@ -27,8 +27,8 @@
 
 namespace gf {
 
-std::recursive_mutex &prog_lock() {
-    static std::recursive_mutex m;
+std::shared_mutex &prog_lock() {
+    static std::shared_mutex m;
     return m;
 }
 std::mutex &reg_lock() {
@@ -1037,7 +1037,7 @@ uint32_t gf_now_sec(void) {
 }
 
 int gf_node_config(const gf_node_cfg *cfg) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     if (!cfg) return -EFAULT;
     std::shared_ptr<Map> m4, m6;
     if (cfg->proxy4_map) {
@@ -1071,7 +1071,7 @@ int gf_node_config(const gf_node_cfg *cfg) {
 }
 
 int gf_set_stats_sink(uint64_t *dev_counters) {
-    std::lock_guard<std::recursive_mutex> g(prog_lock());
+    std::unique_lock<std::shared_mutex> g(prog_lock());
     reg().stats = dev_counters;
     return 0;
 }

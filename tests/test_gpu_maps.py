@@ -4,6 +4,7 @@ and the LRU stand-in of the CT maps — all against the oracle."""
 import ctypes as C
 import errno
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -182,3 +183,109 @@ def test_lru_eviction_matches_oracle(seed):
         assert dp.dump_map(name) == ref.dump(name), name
         assert _evict_log(dp.fd[name]) == ref.lru_log[name], name
     assert len(ref.lru_log["ct4"]) >= 2 and len(ref.lru_log["ct6"]) >= 1
+
+
+def test_concurrent_classify_two_streams():
+    """Two host threads, each running its own programs (a cilium_policy array with
+    its own CT, policy, CIDR and LB maps, its own prefilter) on its own HIP stream,
+    enter their classify calls together: no process-wide lock (the calls overlap
+    on the host), per-stream call contexts and per-object device order; every
+    record and both CT maps stay bit-exact vs the oracle
+    (pkg/bpf/map.go:121: per-map locks, programs concurrent on every CPU)."""
+    from cilium_amd.datapath import LB_OUT
+    scs = [synth.fuzz(seed=s, n_packets=12000, n_batches=3) for s in (31, 32)]
+    dps = [Datapath(sc, pin_prefix=None) for sc in scs]
+    refs = [OracleDP(sc) for sc in scs]
+    want = []
+    for sc, ref in zip(scs, refs):
+        want.append([(ref.xdp(pk), ref.lb(pk)[0], ref.ingress(pk, sc.now + bi)) for bi, pk in enumerate(sc.batches)])
+    bar = threading.Barrier(2)
+    spans = [[], []]
+    got = [[], []]
+    errs = []
+
+    def run(t):
+        try:
+            sc, dp = scs[t], dps[t]
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                bs = [DeviceBatch(pk) for pk in sc.batches]
+                st.synchronize()
+                for bi, b in enumerate(bs):
+                    bar.wait()
+                    a = time.perf_counter()
+                    v = dp.xdp(b)
+                    lo, _ = dp.lb(b)
+                    io = dp.ingress(b, sc.now + bi)
+                    spans[t].append((a, time.perf_counter()))
+                    got[t].append((v, lo, io))
+                st.synchronize()
+        except Exception as e:          # reported by the main thread
+            errs.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=run, args=(t,)) for t in (0, 1)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for t in (0, 1):
+        for bi, (v, lo, io) in enumerate(got[t]):
+            wx, wl, wi = want[t][bi]
+            _cmp(v.cpu().numpy(), wx, f"t{t} xdp b{bi}")
+            _cmp(to_numpy(lo, LB_OUT), wl, f"t{t} lb b{bi}")
+            _cmp(to_numpy(io, ING_OUT), wi, f"t{t} ingress b{bi}")
+        assert dps[t].dump_map("ct4") == refs[t].dump("ct4") and dps[t].dump_map("ct6") == refs[t].dump("ct6")
+    overlap = sum(1 for (a0, b0), (a1, b1) in zip(spans[0], spans[1]) if a0 < b1 and a1 < b0)
+    assert overlap >= 1, (spans, "classify calls never overlapped on the host")
+
+
+def test_prefilter_and_endpoint_edits_between_calls_on_two_streams():
+    """cilium_lxc and the /32 prefilter map edited (update and delete) between XDP
+    and pipeline calls issued alternately on two torch streams: the compact address
+    sets the kernels read are rebuilt on the issuing stream, ordered after the
+    previous call on the other stream, and every verdict equals the oracle's after
+    the same edits (the maps classify binds, not side maps)."""
+    from cilium_amd.datapath import PIPE_OUT
+    sc = synth.pipeline_fuzz(seed=41, n_packets=8000, n_batches=4)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    x = sc.xdp
+    fix, lxc = x["cidr4_hmap"], x["lxc_map"]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    rng = np.random.default_rng(5)
+    for bi, pk in enumerate(sc.batches):
+        f = np.asarray(pk.frames)
+        src = f[rng.integers(0, pk.n, 40), 26:30]
+        dst = f[rng.integers(0, pk.n, 40), 30:34]
+        # /32 entries for sources the traffic uses (then drop half of them again)
+        for k, a in enumerate(src):
+            key = (32).to_bytes(4, "little") + bytes(a)
+            bpf.UpdateElement(dp.fd[fix], key, b"\x01")
+            ref.m[fix].update(key, b"\x01")
+            if k % 2:
+                bpf.DeleteElement(dp.fd[fix], key)
+                ref.m[fix].delete(key)
+        # endpoints: delete some destinations the traffic uses, add others
+        for k, a in enumerate(dst):
+            key = bytes(a) + bytes(12) + b"\x01" + bytes(3)
+            if k % 3 == 0:
+                if ref.m[lxc].lookup(key) is not None:
+                    bpf.DeleteElement(dp.fd[lxc], key)
+                    ref.m[lxc].delete(key)
+            else:
+                val = bytes(4) + (300 + k).to_bytes(2, "little") + (1000 + k).to_bytes(2, "little") + bytes(104)
+                bpf.UpdateElement(dp.fd[lxc], key, val)
+                ref.m[lxc].update(key, val)
+        s = streams[bi % 2]
+        with torch.cuda.stream(s):
+            b = DeviceBatch(pk, parse=False)
+            b.parse()
+            v = dp.xdp(b)
+            out, _, snap = dp.pipeline(b, sc.now + bi)
+        s.synchronize()
+        _cmp(v.cpu().numpy(), ref.xdp(pk), f"xdp b{bi}")
+        ro, _, rs = ref.pipeline(pk, sc.now + bi)
+        _cmp(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
+        assert np.array_equal(snap.cpu().numpy(), rs), f"rewritten frames b{bi}"

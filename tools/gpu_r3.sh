@@ -17,5 +17,7 @@ for S in $STEPS; do
     ranks) GPUFLOW_BENCH_BACKEND=gloo GPUFLOW_BENCH_SHARE_GPU=1 timeout -k 10 900 python -u bench.py --gpus 2 \
                --flows-per-step 1048576 --ct-max 33554432 --steps 4 --warmup 3 > $O/ranks2.json 2> $O/ranks2.err
            echo ranks-ok ;;
+    variants) bash tools/variants.sh run $VARIANTS
+           echo variants-ok ;;
   esac
 done

@@ -19,7 +19,7 @@ fi
 O=$R/gpurun_out/variants
 mkdir -p "$O"
 for name in "$@"; do
-  GPUFLOW_DIAG_LIB=$R/tools/_bin/libgpuflow_$name.so timeout -k 10 200 python "$R/bench.py" --no-cpu --steps 4 \
-      > "$O/$name.json" 2> "$O/$name.err"
+  GPUFLOW_DIAG_LIB=$R/tools/_bin/libgpuflow_$name.so timeout -k 10 200 python "$R/bench.py" \
+      ${BENCH_ARGS:---no-cpu --no-extra --steps 8} > "$O/$name.json" 2> "$O/$name.err"
   echo "variant $name done"
 done
