@@ -31,12 +31,10 @@ namespace gf {
 std::shared_mutex &prog_lock();
 
 // The device-side order of the calls that use one object (map, policy array):
-// the event recorded at the end of the last such call and its stream.
+// the call context (one per stream, gf_kernels.hip) of the last such call.
+struct CallCtx;
 struct OrderPt {
-    hipEvent_t ev = nullptr;
-    hipStream_t s = nullptr;
-    bool have = false;
-    ~OrderPt() { if (ev) (void)hipEventDestroy(ev); }
+    CallCtx *last = nullptr;
 };
 std::mutex &reg_lock();
 

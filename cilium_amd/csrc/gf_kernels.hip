@@ -4051,8 +4051,12 @@ struct Workspace {
 // maps, see CallOrder) run concurrently, host and device; calls on one stream
 // take its context one at a time.  Workspace accessors keep one instance of
 // their type per context (CallCtx::get).
+}  // namespace
+namespace gf {
 struct CallCtx {
     std::mutex mu;
+    hipEvent_t ev = nullptr;       // recorded at the end of every call in this context
+    bool have = false;
     int ws_slot = 0;      // gf_policy_ingress_classify_batches: schedule k+1 builds in one while k runs
     std::map<const void *, std::shared_ptr<void>> bag;
     template <class T> T &get(const void *tag) {
@@ -4061,6 +4065,8 @@ struct CallCtx {
         return *static_cast<T *>(p.get());
     }
 };
+}  // namespace gf
+namespace {
 thread_local CallCtx *t_ctx = nullptr;
 CallCtx &ctx_for(hipStream_t s) {
     static std::mutex mu;
@@ -4132,26 +4138,38 @@ void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, X
 }
 
 // ---- device-side order of the calls that share an object.  Every map a call
-// binds and the cilium_policy array it runs carry the event of the last call
-// that used them (OrderPt): a call on another stream first waits on those
-// events, so a kernel still reading or writing a map replica (or a program
-// table) finishes before this call pushes into it or runs over it, and it records
-// its own end into each of them (under the objects' locks).  The workspaces are
-// per stream (CallCtx), so calls over disjoint objects on different streams do
-// not wait on each other.  With an event ring set, calls append to it in turn.
+// binds and the cilium_policy array it runs remember the call context (stream)
+// of the last call that used them (OrderPt): a call first waits on the end event
+// of each other context found there (one wait per context, on its latest call —
+// a conservative bound), so a kernel still reading or writing a map replica (or a
+// program table) finishes before this call pushes into it or runs over it; at its
+// end the call records its context's event once and marks every object with its
+// context (under the objects' locks).  The workspaces are per stream (CallCtx), so
+// calls over disjoint objects on different streams do not wait on each other.
+// With an event ring set, calls append to it in turn.
 std::mutex &ring_mu() { static std::mutex m; return m; }
 OrderPt &ring_ord() { static OrderPt o; return o; }
 struct CallOrder {
     hipStream_t s;
+    CallCtx *me;
     std::vector<OrderPt *> pts;
     std::unique_lock<std::mutex> ring;
-    CallOrder(hipStream_t s_, std::vector<OrderPt *> p) : s(s_), pts(std::move(p)) {
+    CallOrder(hipStream_t s_, std::vector<OrderPt *> p) : s(s_), me(&cur_ctx()), pts(std::move(p)) {
         if (event_ring().records) {
             ring = std::unique_lock<std::mutex>(ring_mu());
             pts.push_back(&ring_ord());
         }
-        for (OrderPt *o : pts)
-            if (o->have && o->s != s) (void)hipStreamWaitEvent(s, o->ev, 0);
+        CallCtx *waited[8];
+        int nw = 0;
+        for (OrderPt *o : pts) {
+            CallCtx *c = o->last;
+            if (!c || c == me || !c->have) continue;
+            bool seen = false;
+            for (int k = 0; k < nw; k++) seen |= waited[k] == c;
+            if (seen) continue;
+            (void)hipStreamWaitEvent(s, c->ev, 0);
+            if (nw < 8) waited[nw++] = c;
+        }
     }
     CallOrder(hipStream_t s_, const MapLocks &L, PolicyArray *a = nullptr) : CallOrder(s_, order_pts(L, a)) {}
     static std::vector<OrderPt *> order_pts(const MapLocks &L, PolicyArray *a) {
@@ -4161,10 +4179,10 @@ struct CallOrder {
         return v;
     }
     ~CallOrder() {
-        for (OrderPt *o : pts) {
-            if (!o->ev && hipEventCreateWithFlags(&o->ev, hipEventDisableTiming) != hipSuccess) { o->ev = nullptr; continue; }
-            if (hipEventRecord(o->ev, s) == hipSuccess) { o->s = s; o->have = true; }
-        }
+        if (!me->ev && hipEventCreateWithFlags(&me->ev, hipEventDisableTiming) != hipSuccess) { me->ev = nullptr; return; }
+        if (hipEventRecord(me->ev, s) != hipSuccess) return;
+        me->have = true;
+        for (OrderPt *o : pts) o->last = me;
     }
 };
 void lock_lxc_maps(MapLocks &L, const std::shared_ptr<ProgLxc> &p) {
@@ -4626,19 +4644,26 @@ static int schedule_groups(uint32_t n, hipStream_t s) {
 
 // cilium_proxy{4,6} update log of one launch (pol_redirect) and its in-order
 // apply after the launch (see k_px_apply).
-struct PxWs { DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp; };
+struct PxWs {
+    DevBuf plog, plog_n, pkey, pkey2, pval, pperm, ptmp;
+    bool live = false;         // a log was begun in this call (its count is valid)
+};
 static PxWs &px_ws() { static const char tag = 0; return cur_ctx().get<PxWs>(&tag); }
 // keep: continue the log the from-container pass of the same egress call wrote
 // (each packet logs at most one update: an egress redirect is never delivered).
+// Without proxy maps the updates are no-ops that succeed (the reference's maps
+// always exist), but a redirect still gets the MAC stores that follow it in
+// ipv{4,6}_policy when the call writes frames: the log is kept for those.
 static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X, bool keep = false) {
     auto px4 = proxy_map(4), px6 = proxy_map(6);
     X.plog = nullptr; X.plog_n = nullptr;
-    if (!px4 && !px6) return 0;
     PxWs &w = px_ws();
+    if (!px4 && !px6 && !X.snap && !(keep && w.live)) { w.live = keep && w.live; return 0; }
     int r;
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     if ((r = grow(w.plog, (size_t)n * 64)) || (r = grow(w.plog_n, 4))) return r;
-    if (!keep && hip_ok(hipMemsetAsync(w.plog_n.p, 0, 4, s), "plog_n")) return -EIO;
+    if ((!keep || !w.live) && hip_ok(hipMemsetAsync(w.plog_n.p, 0, 4, s), "plog_n")) return -EIO;
+    w.live = true;
     for (auto &m : {px4, px6})
         if (m && (r = push_map(m, s))) return r;
     X.plog = (uint32_t *)w.plog.p; X.plog_n = (uint32_t *)w.plog_n.p;
@@ -4648,6 +4673,7 @@ static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X, bool keep = false)
 static int px_log_apply(const IngCtx &X, hipStream_t s, uint8_t *wsnap, const uint32_t *len, uint32_t stride,
                         uint8_t *recs, bool wide) {
     if (!X.plog) return 0;
+    px_ws().live = false;
     auto px4 = proxy_map(4), px6 = proxy_map(6);
     const gf_node_cfg &node = node_cfg();
     PxWs &w = px_ws();
@@ -5254,6 +5280,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     if (!m) return -EBADF;
     if (m->is_lpm() || (m->ksz != 14 && m->ksz != 40) || m->vsz != 48) return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    CtxScope cx(s);
     std::lock_guard<std::recursive_mutex> mg(m->mu);
     CallOrder co(s, std::vector<OrderPt *>{&m->ord});
     const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;

@@ -195,7 +195,13 @@ def test_config4_real_shape_sampled():
         assert bad == 0, f"step {s}: {bad} mismatches, first sampled row {first}: gpu={g[first]} ref={ro[first]}"
         gs = snap[idx].cpu().numpy()
         bad_f = np.nonzero((gs != rs).any(axis=1))[0]
-        assert len(bad_f) == 0, f"step {s}: {len(bad_f)} rewritten frames differ, first sampled row {bad_f[0]}"
+        if len(bad_f):
+            det = []
+            for j in bad_f[:4]:
+                offs = np.nonzero(gs[j] != rs[j])[0]
+                det.append(f"row {j} rec={ro[j]} len={pk.lens[j]} offs={offs.tolist()} gpu={gs[j][offs].tolist()} "
+                           f"ref={rs[j][offs].tolist()} in={pk.frames[j][offs].tolist()} frame={pk.frames[j][:64].tolist()}")
+            raise AssertionError(f"step {s}: {len(bad_f)} rewritten frames differ:\n" + "\n".join(det))
         compared += len(ro)
         stages |= set(np.unique(ro["stage"]).tolist())
         rets |= set(np.unique(ro["ct_ret"][ro["stage"] == 4]).tolist())
