@@ -1652,7 +1652,7 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 // carry equal work and the deepest buckets start first.
 template <int FAM>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
-                                        Stats &st, bool stats, Lane<FAM> &ln) {
+                                        gf_ingress_out *sout, uint32_t pos, Stats &st, bool stats, Lane<FAM> &ln) {
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
@@ -1665,7 +1665,8 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
         *reinterpret_cast<uint2 *>(q) = a;
         *reinterpret_cast<uint2 *>(q + 8) = b;
     } else if (!(GF_DIAG & 1)) {
-        out[i] = o;
+        if (sout) sout[pos] = o;                        // in bucket order (k_out_scatter puts it at i)
+        else out[i] = o;
     }
     if (stats && !(GF_DIAG & 2)) {
 #if GF_ING_BINS_WAVE
@@ -1699,8 +1700,8 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, i
 template <int FAM>
 __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
                                                       const uint32_t *perm,
-                                                      const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
-                                                      unsigned long long *stats) {
+                                                      const gf_rec *rec, gf_ingress_out *out, gf_ingress_out *sout,
+                                                      uint32_t *ct_count, unsigned long long *stats) {
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     Stats st{sl};
@@ -1747,10 +1748,10 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 #if GF_PREFETCH_REC
             gf_rec rn;
             if (k + 1 < c) rn = rec[inx];
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
+            ing_one<FAM>(X, i, r, out, sout, b + k, st, stats != nullptr, ln);
             i = inx; inx = in2; r = rn;
 #else
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
+            ing_one<FAM>(X, i, r, out, sout, b + k, st, stats != nullptr, ln);
             i = inx; inx = in2;
             if (k + 1 < c) r = rec[i];
 #endif
@@ -4045,6 +4046,8 @@ void prof_drain() {
 
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
+    DevBuf bins, pairs, runs;          // the binned schedule (schedule_groups)
+    uint32_t *live = nullptr;          // device: packets in buckets (perm[0..live)), binned schedule only
 };
 // ---- call contexts: the device workspaces of one classify call.  Each HIP
 // stream has its own, so calls on different streams (over disjoint programs and
@@ -4601,8 +4604,285 @@ __global__ __launch_bounds__(BLOCK) void k_run_write(uint32_t n, const uint32_t 
         __syncthreads();
     }
 }
-static int schedule_groups(uint32_t n, hipStream_t s) {
+// ---- The flow-group schedule by key bins (the default; GF_SCHED=radix selects
+// the radix sort above).  A bucket — a run of equal keys — never crosses a bin of
+// the keys' top bits, so the batch is binned (count, scan, one unordered scatter
+// of (key, index) pairs: one atomic per packet) and every bin is sorted on its
+// own by (key, index) in LDS: the index restores batch order inside a bucket, so
+// the result is the stable sort's.  The same block finds the bin's runs and
+// counts them into the longest-first histogram, so one pass over the pairs
+// replaces four radix passes, the run detection and the bucket histogram.
+#ifndef GF_BIN_CAP
+#define GF_BIN_CAP 2048u                 // pairs a k_bin_sort block sorts in LDS (larger bins: k_bin_big)
+#endif
+#ifndef GF_BIN_TARGET
+#define GF_BIN_TARGET 512u               // mean pairs per bin the bin count aims at
+#endif
+// bins words: cnt[nb] | off[nb + 1] | cur[nb] | big[nb] | nbig | big cursor
+#define GF_BINS_WORDS(nb) (4u * (nb) + 3u)
+
+// exclusive sum / inclusive max over the block (BLOCK threads); tot = the block's sum / max
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *wsum, uint32_t &tot) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLOCK / 64; k++) { const uint32_t s = wsum[k]; before += k < wv ? s : 0u; tot += s; }
+    __syncthreads();
+    return before + x - v;
+}
+__device__ __forceinline__ uint32_t block_scan_max(uint32_t v, uint32_t *wsum, uint32_t &tot) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x = max(x, y);
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLOCK / 64; k++) { const uint32_t s = wsum[k]; if (k < wv) before = max(before, s); tot = max(tot, s); }
+    __syncthreads();
+    return max(before, x);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_bin_count(uint32_t n, const uint32_t *keys, uint32_t sh, uint32_t *cnt) {
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t k = keys[i];
+        if (k != GF_KEY_SKIP) atomicAdd(&cnt[k >> sh], 1u);
+    }
+}
+// off = exclusive scan of cnt (off[nb] = live packets), cur = off; clears the
+// big-bin list and the run count.  One block.
+__global__ __launch_bounds__(1024) void k_bin_scan(uint32_t nb, uint32_t *bins, uint32_t *sched) {
+    __shared__ uint32_t part[1024];
+    const uint32_t *cnt = bins;
+    uint32_t *off = bins + nb, *cur = off + nb + 1, *nbig = cur + 2 * nb;
+    const uint32_t per = (nb + 1023) / 1024, t0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per && t0 + k < nb; k++) s += cnt[t0 + k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (uint32_t k = 0; k < per && t0 + k < nb; k++) { off[t0 + k] = run; cur[t0 + k] = run; run += cnt[t0 + k]; }
+    if (threadIdx.x == 1023) { off[nb] = part[1023]; nbig[0] = 0; nbig[1] = 0; *GF_SCHED_NRUNS(sched) = 0; }
+}
+__global__ __launch_bounds__(BLOCK) void k_bin_scatter(uint32_t n, const uint32_t *keys, uint32_t sh, uint32_t *cur,
+                                                       unsigned long long *pairs) {
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t k = keys[i];
+        if (k != GF_KEY_SKIP) pairs[atomicAdd(&cur[k >> sh], 1u)] = ((unsigned long long)k << 32) | i;
+    }
+}
+__device__ __forceinline__ void run_out(uint32_t start, uint32_t c, uint32_t key, uint2 *runs, uint32_t at, uint32_t *h) {
+    const uint32_t f = key >> (GF_KEY_BITS - 1);
+    runs[at] = make_uint2(start, c | (f << 31));
+    atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
+}
+// One bin per block: bitonic sort of its (key, index) pairs in LDS, perm = the
+// indices in that order, and the bin's runs (start, count | family << 31)
+// appended to the run list and counted into the longest-first histogram.
+__global__ __launch_bounds__(BLOCK) void k_bin_sort(uint32_t nb, uint32_t cap, uint32_t *bins,
+                                                    const unsigned long long *pairs, uint32_t *perm, uint2 *runs,
+                                                    uint32_t *sched) {
+    __shared__ unsigned long long a[GF_BIN_CAP];
+    __shared__ uint32_t rs[GF_BIN_CAP + 1];
+    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
+    __shared__ uint32_t wsum[BLOCK / 64];
+    __shared__ uint32_t rbase;
+    const uint32_t *off = bins + nb;
+    uint32_t *big = bins + 3 * nb + 1, *nbig = big + nb;
+    const uint32_t b = blockIdx.x, o = off[b], m = off[b + 1] - o, tid = threadIdx.x;
+    if (m == 0) return;
+    if (m > cap) {
+        if (tid == 0) big[atomicAdd(nbig, 1u)] = b;
+        return;
+    }
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t j = tid; j < P; j += BLOCK) a[j] = j < m ? pairs[o + j] : ~0ull;
+    for (uint32_t j = tid; j < 2 * (GF_LCAP + 1); j += BLOCK) h[j] = 0;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t d = k >> 1; d > 0; d >>= 1) {
+            for (uint32_t t = tid; t < P / 2; t += BLOCK) {
+                const uint32_t i = ((t & ~(d - 1)) << 1) | (t & (d - 1)), j = i + d;
+                const unsigned long long x = a[i], y = a[j];
+                if ((x > y) == ((i & k) == 0)) { a[i] = y; a[j] = x; }
+            }
+            __syncthreads();
+        }
+    // run starts (the key differs from the one before), ranked over the block
+    const uint32_t per = (m + BLOCK - 1) / BLOCK, j0 = tid * per;
+    uint32_t c = 0;
+    for (uint32_t q = 0; q < per; q++) {
+        const uint32_t j = j0 + q;
+        if (j < m && (j == 0 || (a[j] >> 32) != (a[j - 1] >> 32))) c++;
+    }
+    uint32_t tot, r = block_scan_excl(c, wsum, tot);
+    for (uint32_t q = 0; q < per; q++) {
+        const uint32_t j = j0 + q;
+        if (j < m && (j == 0 || (a[j] >> 32) != (a[j - 1] >> 32))) rs[r++] = j;
+    }
+    if (tid == 0) { rs[tot] = m; rbase = atomicAdd(GF_SCHED_NRUNS(sched), tot); }
+    for (uint32_t j = tid; j < m; j += BLOCK) perm[o + j] = (uint32_t)a[j];
+    __syncthreads();
+    for (uint32_t q = tid; q < tot; q += BLOCK)
+        run_out(o + rs[q], rs[q + 1] - rs[q], (uint32_t)(a[rs[q]] >> 32), runs, rbase + q, h);
+    __syncthreads();
+    uint32_t *hist = GF_SCHED_HIST(sched);
+    for (uint32_t k = tid; k < 2 * (GF_LCAP + 1); k += BLOCK)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+// Bins over GF_BIN_CAP pairs (a flow group of thousands of packets in one
+// batch): one block sorts the bin in place in HBM (bitonic network for any
+// length: the first merge step of each stage compares mirrored pairs, so the
+// missing tail acts as +inf), then walks it for runs (block max-scan of the run
+// starts, carried over chunks).
+__device__ __forceinline__ void cas_asc(unsigned long long *A, uint32_t i, uint32_t j) {
+    const unsigned long long x = A[i], y = A[j];
+    if (x > y) { A[i] = y; A[j] = x; }
+}
+__global__ __launch_bounds__(BLOCK) void k_bin_big(uint32_t nb, uint32_t *bins, unsigned long long *pairs,
+                                                   uint32_t *perm, uint2 *runs, uint32_t *sched) {
+    __shared__ uint32_t wsum[BLOCK / 64];
+    __shared__ uint32_t qb, carry;
+    const uint32_t *off = bins + nb;
+    uint32_t *big = bins + 3 * nb + 1, *nbig = big + nb, *hist = GF_SCHED_HIST(sched);
+    const uint32_t tid = threadIdx.x;
+    for (;;) {
+        if (tid == 0) qb = atomicAdd(nbig + 1, 1u);
+        __syncthreads();
+        const uint32_t q = qb;
+        __syncthreads();
+        if (q >= nbig[0]) break;
+        const uint32_t b = big[q], o = off[b], m = off[b + 1] - o;
+        unsigned long long *A = pairs + o;
+        uint32_t P = 1;
+        while (P < m) P <<= 1;
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            const uint32_t hk = k >> 1;
+            for (uint32_t t = tid; t < P / 2; t += BLOCK) {
+                const uint32_t i = (t / hk) * k + (t % hk), j = i ^ (k - 1);
+                if (j < m) cas_asc(A, i, j);
+            }
+            __syncthreads();
+            for (uint32_t d = k >> 2; d > 0; d >>= 1) {
+                for (uint32_t t = tid; t < P / 2; t += BLOCK) {
+                    const uint32_t i = ((t & ~(d - 1)) << 1) | (t & (d - 1)), j = i + d;
+                    if (j < m) cas_asc(A, i, j);
+                }
+                __syncthreads();
+            }
+        }
+        if (tid == 0) carry = 0;
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < m; c0 += BLOCK) {
+            const uint32_t j = c0 + tid;
+            const uint32_t key = j < m ? (uint32_t)(A[j] >> 32) : 0u;
+            if (j < m) perm[o + j] = (uint32_t)A[j];
+            const bool st = j < m && (j == 0 || (uint32_t)(A[j - 1] >> 32) != key);
+            uint32_t tot, s0 = block_scan_max(st ? j : 0u, wsum, tot);
+            s0 = max(s0, carry);
+            const bool end = j < m && (j + 1 == m || (uint32_t)(A[j + 1] >> 32) != key);
+            if (end) run_out(o + s0, j - s0 + 1, key, runs, atomicAdd(GF_SCHED_NRUNS(sched), 1u), hist);
+            __syncthreads();
+            if (tid == 0) carry = max(carry, tot);
+            __syncthreads();
+        }
+    }
+}
+// order[] from the run list (k_bucket_order over runs instead of run starts)
+__global__ __launch_bounds__(BLOCK) void k_bucket_order_runs(const uint2 *runs, uint32_t *sched, uint2 *order) {
+    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const uint32_t nq = *GF_SCHED_NRUNS(sched), b0 = blockIdx.x * GF_SCHED_ITEMS;
+    const uint32_t *base = GF_SCHED_BASE(sched);
+    uint32_t *cursor = GF_SCHED_CURSOR(sched);
+    auto bin = [](uint2 r) { const uint32_t c = r.y & 0x7fffffffu; return (r.y >> 31) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP); };
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) atomicAdd(&h[bin(runs[q])], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
+        if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
+    __syncthreads();
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
+        const uint2 r = runs[q];
+        order[atomicAdd(&h[bin(r)], 1u)] = make_uint2(r.x, r.y & 0x7fffffffu);
+    }
+}
+// GPUFLOW_BIN_CAP lowers the LDS bin capacity (the GPU tests send most bins through k_bin_big)
+static uint32_t bin_cap() {
+    const char *e = getenv("GPUFLOW_BIN_CAP");
+    const uint32_t c = e ? (uint32_t)strtoul(e, nullptr, 10) : GF_BIN_CAP;
+    return c < GF_BIN_CAP ? c : GF_BIN_CAP;
+}
+// sout (bucket order) -> out (batch order)
+__global__ __launch_bounds__(BLOCK) void k_out_scatter(uint32_t n, const uint32_t *live, const uint32_t *perm,
+                                                       const gf_ingress_out *sout, gf_ingress_out *out) {
+    const uint32_t m = *live;
+    for (uint32_t p = blockIdx.x * BLOCK + threadIdx.x; p < m && p < n; p += gridDim.x * BLOCK) out[perm[p]] = sout[p];
+}
+static int schedule_bins(uint32_t n, hipStream_t s) {
     Workspace &w = ws();
+    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+    uint32_t B = 1;                                     // 2^B bins, about GF_BIN_TARGET pairs each (half per family)
+    while (B < 16 && B < GF_KEY_BITS && ((uint64_t)GF_BIN_TARGET << (B - 1)) < n) B++;
+    const uint32_t nb = 1u << B, sh = GF_KEY_BITS - B;
+    int r;
+    if ((r = grow(w.bins, (size_t)GF_BINS_WORDS(nb) * 4)) || (r = grow(w.pairs, (size_t)n * 8 + 8)) ||
+        (r = grow(w.runs, (size_t)n * 8 + 8)))
+        return r;
+    uint32_t *bins = (uint32_t *)w.bins.p, *d_sched = (uint32_t *)w.sched.p;
+    w.live = bins + 2 * nb;                             // off[nb]
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 8192));
+    {
+        ProfScope ps("bin_sort", s);
+        if (hip_ok(hipMemsetAsync(bins, 0, (size_t)nb * 4, s), "memset bins") ||
+            hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist"))
+            return -EIO;
+        hipLaunchKernelGGL(k_bin_count, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.keys.p, sh, bins);
+        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, nb, bins, d_sched);
+        hipLaunchKernelGGL(k_bin_scatter, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.keys.p, sh,
+                           bins + 2 * nb + 1, (unsigned long long *)w.pairs.p);
+        hipLaunchKernelGGL(k_bin_sort, dim3(nb), dim3(BLOCK), 0, s, nb, bin_cap(), bins, (const unsigned long long *)w.pairs.p,
+                           (uint32_t *)w.perm.p, (uint2 *)w.runs.p, d_sched);
+        hipLaunchKernelGGL(k_bin_big, dim3(64), dim3(BLOCK), 0, s, nb, bins, (unsigned long long *)w.pairs.p,
+                           (uint32_t *)w.perm.p, (uint2 *)w.runs.p, d_sched);
+        if ((r = hip_ok(hipGetLastError(), "bin sort"))) return r;
+    }
+    {
+        ProfScope ps("k_bucket_sched", s);
+        hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
+        const uint32_t go = std::max<uint32_t>(1, (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS);
+        hipLaunchKernelGGL(k_bucket_order_runs, dim3(go), dim3(BLOCK), 0, s, (const uint2 *)w.runs.p, d_sched,
+                           (uint2 *)w.order.p);
+    }
+    return hip_ok(hipGetLastError(), "k_bucket_sched");
+}
+
+static int schedule_groups(uint32_t n, hipStream_t s) {
+    static const bool radix = [] { const char *e = getenv("GF_SCHED"); return !(e && !strcmp(e, "bins")); }();
+    if (!radix) return schedule_bins(n, s);
+    Workspace &w = ws();
+    w.live = nullptr;
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
     uint32_t *d_sched = (uint32_t *)w.sched.p, *d_nruns = GF_SCHED_NRUNS(d_sched);
@@ -4946,6 +5226,10 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
     unsigned long long *sink = (unsigned long long *)stats_sink();
+    // GF_OUT_SORTED: the records are written in bucket order (each lane's run of
+    // consecutive slots merges in L2) and scattered to batch order afterwards
+    static const bool out_sorted = getenv("GF_OUT_SORTED") != nullptr;
+    gf_ingress_out *sout = (out_sorted && !pout && out && w.live) ? (gf_ingress_out *)w.pairs.p : nullptr;
     {
         // resident-grid launches: every wave loops on its family's queue until it is drained
         uint32_t grid = resident_blocks(8);
@@ -4955,16 +5239,23 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
             ProfScope ps("k_ing_groups", s);
             hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
                                (const uint32_t *)w.perm.p,
-                               (const gf_rec *)w.rec.p, out, cnt4, sink);
+                               (const gf_rec *)w.rec.p, out, sout, cnt4, sink);
         }
         if (pkts->saddr6) {    // IPv6 packets reach conntrack only with v6 columns
             ProfScope ps("k_ing_groups6", s);
             hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
                                (const uint32_t *)w.perm.p,
-                               (const gf_rec *)w.rec.p, out, cnt6, sink);
+                               (const gf_rec *)w.rec.p, out, sout, cnt6, sink);
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
+    if (sout) {
+        ProfScope ps("k_out_scatter", s);
+        hipLaunchKernelGGL(k_out_scatter, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 8192))),
+                           dim3(BLOCK), 0, s, n, (const uint32_t *)w.live, (const uint32_t *)w.perm.p,
+                           (const gf_ingress_out *)sout, out);
+        if ((r = hip_ok(hipGetLastError(), "k_out_scatter"))) return r;
+    }
     if ((r = px_log_apply(X, s, wsnap, ev_len ? ev_len : pkts->len, ev_stride, pout ? pout : (uint8_t *)out,
                           pout != nullptr)))
         return r;

@@ -133,6 +133,24 @@ def test_config2_ingress_scaled():
     assert dp.dump_map("cilium_ct4_global") == ref.dump("cilium_ct4_global")
 
 
+@pytest.mark.parametrize("n_pairs,n_flows,cap", [(3, 2_500, None), (40, 6_000, "700"), (2_000, 6_000, "64")])
+def test_ingress_elephant_groups(monkeypatch, n_pairs, n_flows, cap):
+    """Flow groups of thousands of packets in one batch: their key bins exceed what
+    one k_bin_sort block sorts in LDS (GF_BIN_CAP pairs), so k_bin_big sorts them in
+    HBM; with a lowered capacity (GPUFLOW_BIN_CAP) big and LDS-sized bins mix.
+    Records and the CT equal the oracle's."""
+    if cap:
+        monkeypatch.setenv("GPUFLOW_BIN_CAP", cap)
+    sc = synth.config2(n_flows=n_flows, n_pairs=n_pairs, n_ep=min(n_pairs, 8), n_ids=64, n_l3=40, n_l4=80, n_wc=8,
+                       n_cidr=16, ct_max=200_000)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        io = dp.ingress(DeviceBatch(pk), sc.now + bi)
+        torch.cuda.synchronize()
+        _cmp_struct(to_numpy(io, ING_OUT), ref.ingress(pk, sc.now + bi), f"elephants batch {bi}")
+    assert dp.dump_map("cilium_ct4_global") == ref.dump("cilium_ct4_global")
+
+
 def test_ingress_batches_pipelined_equals_oracle():
     """gf_policy_ingress_classify_batches (schedule of batch k+1 on a second stream
     while batch k runs) over the scaled config-2 stream and its fuzz sibling:
