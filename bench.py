@@ -1091,6 +1091,56 @@ def add_traffic(cfg, r):
     return r
 
 
+# Issue and request ceilings the roofline objects are also priced against
+# (the byte roofline alone names the wrong bound for request- or issue-bound
+# kernels):
+#   issue:    VALU + SALU wave-instructions per second / (256 CUs x 4 SIMDs x 2.4 GHz)
+#             (one wave-instruction per SIMD per clock; a wave64 VALU occupies its
+#             SIMD-32 for 2 clocks, so "valu_busy" = 2 x VALU / the same peak)
+#   requests: L2 -> fabric requests (TCC_EA0_RDREQ + WRREQ) per second / the random
+#             64-B request rate measured on MI355X by tools/primbench.hip
+#             (profiles/r1_primbench.txt: 39.6-42.4 G random 16-B loads/s)
+ISSUE_PEAK = 256 * 4 * 2.4e9
+REQUEST_PEAK = 40.0e9
+PMC_KERNELS = {"2": ["k_ing_groups"], "1": ["k_xdp", "k_xdp_lds"], "3": ["k_lb"]}   # else: every kernel
+
+
+def add_bounds(cfg, r):
+    """roofline.issue / roofline.requests of configuration `cfg` from its committed
+    per-kernel PMC summary (profiles/*pmc_kernels_c<cfg>.json, tools/pmc_kernels.py),
+    scaled per packet to this run and divided by this run's live launch time."""
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_kernels_c{cfg}.json")))
+    rf = r.get("roofline")
+    if not pmc or not rf or not rf.get("avg_launch_ms"):
+        return r
+    try:
+        j = json.load(open(pmc[-1]))
+        names = PMC_KERNELS.get(cfg) or list(j["kernels"])
+        ks = [j["kernels"][k] for k in names if k in j["kernels"]]
+        pk = r.get("packets_per_step") or r.get("config", {}).get("packets_per_step_per_gpu")
+        scale = float(pk) / float(j["packets_per_step"])
+        t = rf["avg_launch_ms"] * 1e-3
+        src = os.path.relpath(pmc[-1], ROOT)
+        cs = lambda n: sum(k["counters_per_step"].get(n, 0.0) for k in ks) * scale
+        valu, salu = cs("SQ_INSTS_VALU"), cs("SQ_INSTS_SALU")
+        if valu or salu:
+            rf["issue"] = {"frac": round((valu + salu) / t / ISSUE_PEAK, 4),
+                           "valu_busy": round(2 * valu / t / ISSUE_PEAK, 4),
+                           "wave_insts_per_s": (valu + salu) / t, "peak": ISSUE_PEAK,
+                           "wave_insts_per_64_packets": round((valu + salu) * 64 / float(pk), 1), "source": src}
+            gui = cs("GRBM_GUI_ACTIVE")
+            if gui:
+                rf["issue"]["effective_clock_ghz"] = round(gui / 8 / t / 1e9, 3)
+        req = cs("TCC_EA0_RDREQ_sum") + cs("TCC_EA0_WRREQ_sum")
+        if req:
+            rf["requests"] = {"frac": round(req / t / REQUEST_PEAK, 4), "per_s": req / t, "peak": REQUEST_PEAK,
+                              "per_packet": round(req / float(pk), 3), "source": src,
+                              "peak_source": "profiles/r1_primbench.txt"}
+    except Exception as e:                                   # reported, never silently dropped
+        rf["bounds_error"] = f"{type(e).__name__}: {e}"
+    return r
+
+
 # ----------------------------------------------------------------------------- launcher (--gpus N)
 def _free_port():
     s = socket.socket()
@@ -1184,7 +1234,7 @@ def main():
             dist.init_process_group(backend, **({"device_id": B.dev} if backend == "nccl" else {}))
 
     if args.config == "2":
-        res = bench_config2(args, B, rank, world, local_world)
+        res = add_bounds("2", bench_config2(args, B, rank, world, local_world))
         extra = {} if args.no_extra else (
             {k: v for k, v in EXTRA.items()} if world == 1 and not rehearsal else
             {"4": lambda a, b: bench_config4(a, b, rank, world, "owned", local_world),
@@ -1195,7 +1245,7 @@ def main():
         for k, fn in extra.items():
             t0 = time.time()
             try:
-                res["configs"][k] = add_traffic(k, fn(args, B))
+                res["configs"][k] = add_bounds(k, add_traffic(k, fn(args, B)))
             except Exception as e:                       # reported, never silently dropped
                 if world > 1:
                     raise                                # a rank cannot skip a collective the others run
@@ -1211,7 +1261,7 @@ def main():
             r = bench_config4(args, B, rank, world, "owned", local_world)
         else:
             r = EXTRA[args.config](args, B)
-        r = add_traffic(args.config, r)
+        r = add_bounds(args.config, add_traffic(args.config, r))
         res = {"metric": METRIC, "value": r["mpps"], "unit": "Mpps", "n_gpus": world, "steps": r["steps"],
                "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "u32", "data": "synthetic",

@@ -1,0 +1,89 @@
+"""Per-kernel PMC summary of one bench configuration: every counter of every
+rocprofv3 --pmc pass under DIR (DIR/p*/run_counter_collection.csv, one counter
+group per pass, tools/profile_round.sh), summed per kernel over the classify
+calls of the run and divided by the bench steps the process ran (warm-up +
+timed), so each number is "per step".
+
+Derived per kernel:
+  traffic_bytes      FETCH_SIZE + WRITE_SIZE (KB in the CSV) x 1024: the HBM-side
+                     bytes (FETCH_SIZE used raw: random 16-32 B loads are one 64-B
+                     request each, profiles/r1_pmc_calibration.json)
+  ea_requests        TCC_EA0_RDREQ_sum + TCC_EA0_WRREQ_sum (L2 -> fabric requests)
+  wave_insts         SQ_INSTS_VALU + SQ_INSTS_SALU (wave-instructions)
+  GRBM_GUI_ACTIVE    kept raw: / 8 XCDs / the kernel's time = its effective clock
+                     (bench.py divides by the live launch time)
+
+  python tools/pmc_kernels.py DIR --bench-json DIR/p1.json --out profiles/<tag>_pmc_kernels_c<cfg>.json
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+STEP_ENTRY = {"k_pipe_front", "k_eg_front", "k_ing_pack", "k_xdp", "k_xdp_lds", "k_lb", "k_parse"}
+
+
+def short(name):
+    s = name.split("(")[0].replace("void ", "").strip()
+    if "rocprim" in s or "ROCPRIM" in name:
+        return "rocprim"
+    return s.replace("<4>", "").replace("<6>", "6") if s.startswith("k_ing_groups") or s.startswith("k_eg_") else s
+
+
+def per_kernel(path, nsteps):
+    rows = list(csv.DictReader(open(path)))
+    base = lambda n: n.split("(")[0].replace("void ", "").split("<")[0].strip()
+    first = min((int(r["Dispatch_Id"]) for r in rows if base(r["Kernel_Name"]) in STEP_ENTRY), default=0)
+    out = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        if d < first:
+            continue
+        k = short(r["Kernel_Name"])
+        out[k][r["Counter_Name"]] += float(r["Counter_Value"]) / nsteps
+        disp[k].add(d)
+    return out, {k: len(v) / nsteps for k, v in disp.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--bench-json", required=True, help="the bench line of one pass (steps, warmup, packets)")
+    ap.add_argument("--packets", type=int, default=0, help="packets per step (default: from the bench line)")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    b = json.loads(open(a.bench_json).read().strip().splitlines()[-1])
+    nsteps = int(b["steps"]) + int(b["warmup"])
+    cf = b.get("config", {})
+    pk = a.packets or int(b.get("packets_per_step") or cf.get("packets_per_step_per_gpu") or cf.get("packets_per_step") or 0)
+    ks = collections.defaultdict(dict)
+    dps = {}
+    for f in sorted(glob.glob(os.path.join(a.dir, "p*", "run_counter_collection.csv"))):
+        c, d = per_kernel(f, nsteps)
+        for k, v in c.items():
+            ks[k].update(v)
+        dps.update(d)
+    res = {"packets_per_step": pk, "steps_run": nsteps, "source": os.path.relpath(a.dir), "kernels": {}}
+    for k, c in sorted(ks.items()):
+        e = {"dispatches_per_step": round(dps.get(k, 0), 3), "counters_per_step": {n: round(v, 1) for n, v in sorted(c.items())}}
+        if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+            t = (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024
+            e["traffic_bytes"] = t
+            e["traffic_bytes_per_packet"] = t / pk if pk else None
+        if "TCC_EA0_RDREQ_sum" in c:
+            e["ea_requests"] = c["TCC_EA0_RDREQ_sum"] + c.get("TCC_EA0_WRREQ_sum", 0.0)
+            e["ea_requests_per_packet"] = e["ea_requests"] / pk if pk else None
+        if "SQ_INSTS_VALU" in c:
+            e["wave_insts"] = c["SQ_INSTS_VALU"] + c.get("SQ_INSTS_SALU", 0.0)
+            e["wave_insts_per_64_packets"] = e["wave_insts"] * 64 / pk if pk else None
+        res["kernels"][k] = e
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps({k: {x: y for x, y in v.items() if x != "counters_per_step"} for k, v in res["kernels"].items()},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
