@@ -12,7 +12,6 @@
 #include "gf_internal.h"
 #include "gf_device.h"
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 #include <rocprim/device/device_select.hpp>
@@ -50,10 +49,7 @@ using namespace gfd;
 // they sort into one run, which the bucket schedule leaves out, so no lane reads
 // their records.  Group keys never take this value (gf_key_live).
 #define GF_KEY_SKIP GF_KEY_HASH
-// (nor any value of its 16-bit key bin, which the binned schedule then skips whole)
-__device__ __forceinline__ uint32_t gf_key_live(uint32_t k) {
-    return ((k & GF_KEY_HASH) >> 16) == (GF_KEY_SKIP >> 16) ? k ^ (1u << 16) : k;
-}
+__device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY_HASH) == GF_KEY_SKIP ? k - 1u : k; }
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
 #endif
@@ -4049,7 +4045,6 @@ void prof_drain() {
 
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
-    DevBuf bins, pairs, runs;          // the binned schedule (schedule_groups)
 };
 // ---- call contexts: the device workspaces of one classify call.  Each HIP
 // stream has its own, so calls on different streams (over disjoint programs and
@@ -4606,434 +4601,7 @@ __global__ __launch_bounds__(BLOCK) void k_run_write(uint32_t n, const uint32_t 
         __syncthreads();
     }
 }
-// ---- The flow-group schedule by key bins (the default; GF_SCHED=radix selects
-// the radix sort above).  A bucket — a run of equal keys — never crosses a bin of
-// the keys' top bits, so the batch is binned (count, scan, one unordered scatter
-// of (key, index) pairs: one atomic per packet) and every bin is sorted on its
-// own by (key, index) in LDS: the index restores batch order inside a bucket, so
-// the result is the stable sort's.  The same block finds the bin's runs and
-// counts them into the longest-first histogram, so one pass over the pairs
-// replaces four radix passes, the run detection and the bucket histogram.
-#ifndef GF_BIN_CAP
-#define GF_BIN_CAP 2048u                 // pairs a k_bin_sort block sorts in LDS (larger bins: k_bin_big)
-#endif
-#ifndef GF_BIN_TARGET
-#define GF_BIN_TARGET 512u               // mean pairs per bin the bin count aims at
-#endif
-// bins words: cnt[nb] | off[nb + 1] | cur[nb] | big[nb] | nbig | big cursor
-#define GF_BINS_WORDS(nb) (4u * (nb) + 3u)
-
-// a key rotated by 16 bits (GF_SCHED=bins16 sorts keys with their bin in the low half)
-__host__ __device__ __forceinline__ uint32_t rot16(uint32_t k) { return (k << 16) | (k >> 16); }
-struct Rot16 { __host__ __device__ uint32_t operator()(uint32_t k) const { return rot16(k); } };
-// exclusive sum / inclusive max over the block (BLOCK threads); tot = the block's sum / max
-__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *wsum, uint32_t &tot) {
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t before = 0;
-    tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < BLOCK / 64; k++) { const uint32_t s = wsum[k]; before += k < wv ? s : 0u; tot += s; }
-    __syncthreads();
-    return before + x - v;
-}
-__device__ __forceinline__ uint32_t block_scan_max(uint32_t v, uint32_t *wsum, uint32_t &tot) {
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x = max(x, y);
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t before = 0;
-    tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < BLOCK / 64; k++) { const uint32_t s = wsum[k]; if (k < wv) before = max(before, s); tot = max(tot, s); }
-    __syncthreads();
-    return max(before, x);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_bin_count(uint32_t n, const uint32_t *keys, uint32_t sh, uint32_t *cnt) {
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint32_t k = keys[i];
-        if (k != GF_KEY_SKIP) atomicAdd(&cnt[k >> sh], 1u);
-    }
-}
-// off = exclusive scan of cnt (off[nb] = live packets), cur = off; clears the
-// big-bin list and the run count.  One block.
-__global__ __launch_bounds__(1024) void k_bin_scan(uint32_t nb, uint32_t *bins, uint32_t *sched) {
-    __shared__ uint32_t part[1024];
-    const uint32_t *cnt = bins;
-    uint32_t *off = bins + nb, *cur = off + nb + 1, *nbig = cur + 2 * nb;
-    const uint32_t per = (nb + 1023) / 1024, t0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < per && t0 + k < nb; k++) s += cnt[t0 + k];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - s;
-    for (uint32_t k = 0; k < per && t0 + k < nb; k++) { off[t0 + k] = run; cur[t0 + k] = run; run += cnt[t0 + k]; }
-    if (threadIdx.x == 1023) { off[nb] = part[1023]; nbig[0] = 0; nbig[1] = 0; *GF_SCHED_NRUNS(sched) = 0; }
-}
-__global__ __launch_bounds__(BLOCK) void k_bin_scatter(uint32_t n, const uint32_t *keys, uint32_t sh, uint32_t *cur,
-                                                       unsigned long long *pairs) {
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint32_t k = keys[i];
-        if (k != GF_KEY_SKIP) pairs[atomicAdd(&cur[k >> sh], 1u)] = ((unsigned long long)k << 32) | i;
-    }
-}
-// A run (bucket) is recorded at its first sorted position: runlen[start] =
-// count | family << 31 (runlen is zero elsewhere: cleared before the sort).
-__device__ __forceinline__ void run_out(uint32_t start, uint32_t c, uint32_t key, uint32_t *runlen) {
-    runlen[start] = c | ((key >> (GF_KEY_BITS - 1)) << 31);
-}
-// One bin per block: bitonic sort of its (key, index) pairs in LDS, perm = the
-// indices in that order, and the bin's runs recorded at their starts (run_out).
-// skeys: the bins come from a radix pass over the keys' top bits (pairs = null:
-// the pair of position p is (rot16(skeys[p]), perm[p])); skip_bin: a bin holding only
-// GF_KEY_SKIP keys (left alone).
-__global__ __launch_bounds__(BLOCK) void k_bin_sort(uint32_t nb, uint32_t cap, uint32_t *bins,
-                                                    const unsigned long long *pairs, const uint32_t *skeys,
-                                                    uint32_t skip_bin, uint32_t *perm, uint32_t *runlen) {
-    __shared__ unsigned long long a[GF_BIN_CAP];
-    __shared__ uint32_t rs[GF_BIN_CAP + 1];
-    __shared__ uint32_t wsum[BLOCK / 64];
-    const uint32_t *off = bins + nb;
-    uint32_t *big = bins + 3 * nb + 1, *nbig = big + nb;
-    const uint32_t b = blockIdx.x, o = off[b], m = off[b + 1] - o, tid = threadIdx.x;
-    if (m == 0 || b == skip_bin) return;
-    if (m > cap) {
-        if (tid == 0) big[atomicAdd(nbig, 1u)] = b;
-        return;
-    }
-    uint32_t P = 1;
-    while (P < m) P <<= 1;
-    for (uint32_t j = tid; j < P; j += BLOCK)
-        a[j] = j >= m ? ~0ull : skeys ? ((unsigned long long)rot16(skeys[o + j]) << 32) | perm[o + j] : pairs[o + j];
-    __syncthreads();
-    // a stage with d <= 64 keeps each wave inside its own 128-element chunks: the
-    // waves sync by themselves unless this or the next stage crosses chunks
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t d = k >> 1; d > 0; d >>= 1) {
-            for (uint32_t t = tid; t < P / 2; t += BLOCK) {
-                const uint32_t i = ((t & ~(d - 1)) << 1) | (t & (d - 1)), j = i + d;
-                const unsigned long long x = a[i], y = a[j];
-                if ((x > y) == ((i & k) == 0)) { a[i] = y; a[j] = x; }
-            }
-            const uint32_t nd = d > 1 ? d >> 1 : k;
-            if (d >= 128 || (nd >= 128 && k < P)) {
-                __syncthreads();
-            } else {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-        }
-    __syncthreads();
-    // run starts (the key differs from the one before), ranked over the block
-    const uint32_t per = (m + BLOCK - 1) / BLOCK, j0 = tid * per;
-    uint32_t c = 0;
-    for (uint32_t q = 0; q < per; q++) {
-        const uint32_t j = j0 + q;
-        if (j < m && (j == 0 || (a[j] >> 32) != (a[j - 1] >> 32))) c++;
-    }
-    uint32_t tot, r = block_scan_excl(c, wsum, tot);
-    for (uint32_t q = 0; q < per; q++) {
-        const uint32_t j = j0 + q;
-        if (j < m && (j == 0 || (a[j] >> 32) != (a[j - 1] >> 32))) rs[r++] = j;
-    }
-    if (tid == 0) rs[tot] = m;
-    for (uint32_t j = tid; j < m; j += BLOCK) perm[o + j] = (uint32_t)a[j];
-    __syncthreads();
-    for (uint32_t q = tid; q < tot; q += BLOCK)
-        run_out(o + rs[q], rs[q + 1] - rs[q], (uint32_t)(a[rs[q]] >> 32), runlen);
-}
-// Bins over GF_BIN_CAP pairs (a flow group of thousands of packets in one
-// batch): one block sorts the bin in place in HBM (bitonic network for any
-// length: the first merge step of each stage compares mirrored pairs, so the
-// missing tail acts as +inf), then walks it for runs (block max-scan of the run
-// starts, carried over chunks).
-__device__ __forceinline__ void cas_asc(unsigned long long *A, uint32_t i, uint32_t j) {
-    const unsigned long long x = A[i], y = A[j];
-    if (x > y) { A[i] = y; A[j] = x; }
-}
-__global__ __launch_bounds__(BLOCK) void k_bin_big(uint32_t nb, uint32_t *bins, unsigned long long *pairs,
-                                                   const uint32_t *skeys, uint32_t *perm, uint32_t *runlen) {
-    __shared__ uint32_t wsum[BLOCK / 64];
-    __shared__ uint32_t qb, carry;
-    const uint32_t *off = bins + nb;
-    uint32_t *big = bins + 3 * nb + 1, *nbig = big + nb;
-    const uint32_t tid = threadIdx.x;
-    for (;;) {
-        if (tid == 0) qb = atomicAdd(nbig + 1, 1u);
-        __syncthreads();
-        const uint32_t q = qb;
-        __syncthreads();
-        if (q >= nbig[0]) break;
-        const uint32_t b = big[q], o = off[b], m = off[b + 1] - o;
-        unsigned long long *A = pairs + o;
-        if (skeys) {
-            for (uint32_t j = tid; j < m; j += BLOCK) A[j] = ((unsigned long long)rot16(skeys[o + j]) << 32) | perm[o + j];
-            __syncthreads();
-        }
-        uint32_t P = 1;
-        while (P < m) P <<= 1;
-        for (uint32_t k = 2; k <= P; k <<= 1) {
-            const uint32_t hk = k >> 1;
-            for (uint32_t t = tid; t < P / 2; t += BLOCK) {
-                const uint32_t i = (t / hk) * k + (t % hk), j = i ^ (k - 1);
-                if (j < m) cas_asc(A, i, j);
-            }
-            __syncthreads();
-            for (uint32_t d = k >> 2; d > 0; d >>= 1) {
-                for (uint32_t t = tid; t < P / 2; t += BLOCK) {
-                    const uint32_t i = ((t & ~(d - 1)) << 1) | (t & (d - 1)), j = i + d;
-                    if (j < m) cas_asc(A, i, j);
-                }
-                __syncthreads();
-            }
-        }
-        if (tid == 0) carry = 0;
-        __syncthreads();
-        for (uint32_t c0 = 0; c0 < m; c0 += BLOCK) {
-            const uint32_t j = c0 + tid;
-            const uint32_t key = j < m ? (uint32_t)(A[j] >> 32) : 0u;
-            if (j < m) perm[o + j] = (uint32_t)A[j];
-            const bool st = j < m && (j == 0 || (uint32_t)(A[j - 1] >> 32) != key);
-            uint32_t tot, s0 = block_scan_max(st ? j : 0u, wsum, tot);
-            s0 = max(s0, carry);
-            const bool end = j < m && (j + 1 == m || (uint32_t)(A[j + 1] >> 32) != key);
-            if (end) run_out(o + s0, j - s0 + 1, key, runlen);
-            __syncthreads();
-            if (tid == 0) carry = max(carry, tot);
-            __syncthreads();
-        }
-    }
-}
-// The longest-first histogram of the runs (k_bucket_hist over runlen)
-__device__ __forceinline__ uint32_t run_bin(uint32_t r) {
-    const uint32_t c = r & 0x7fffffffu;
-    return (r >> 31) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP);
-}
-__global__ __launch_bounds__(BLOCK) void k_bucket_hist_runs(uint32_t n, const uint32_t *runlen, uint32_t *sched) {
-    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
-    __syncthreads();
-    const uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
-    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < n; q += blockDim.x) {
-        const uint32_t r = runlen[q];
-        if (r) atomicAdd(&h[run_bin(r)], 1u);
-    }
-    __syncthreads();
-    uint32_t *hist = GF_SCHED_HIST(sched);
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
-        if (h[k]) atomicAdd(&hist[k], h[k]);
-}
-// order[] from the run list (k_bucket_order over runs instead of run starts)
-__global__ __launch_bounds__(BLOCK) void k_bucket_order_runs(uint32_t n, const uint32_t *runlen, uint32_t *sched,
-                                                             uint2 *order) {
-    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
-    __syncthreads();
-    const uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
-    const uint32_t *base = GF_SCHED_BASE(sched);
-    uint32_t *cursor = GF_SCHED_CURSOR(sched);
-    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < n; q += blockDim.x) {
-        const uint32_t r = runlen[q];
-        if (r) atomicAdd(&h[run_bin(r)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
-        if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
-    __syncthreads();
-    for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < n; q += blockDim.x) {
-        const uint32_t r = runlen[q];
-        if (r) order[atomicAdd(&h[run_bin(r)], 1u)] = make_uint2(q, r & 0x7fffffffu);
-    }
-}
-// Bin starts of rotated keys (rot16) sorted on their low 16 bits: off[b] = first
-// position of bin b (empty bins: the next bin's start), off[nb] = n.
-// (one binary search per bin)
-__global__ __launch_bounds__(BLOCK) void k_bin_bounds(uint32_t n, const uint32_t *skeys, uint32_t nb, uint32_t *off) {
-    for (uint32_t x = blockIdx.x * BLOCK + threadIdx.x; x <= nb; x += gridDim.x * BLOCK) {
-        uint32_t lo = 0, hi = n;                        // first p with bin(p) >= x
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((skeys[mid] & 0xffffu) < x) lo = mid + 1; else hi = mid;
-        }
-        off[x] = lo;
-    }
-}
-// GPUFLOW_BIN_CAP lowers the LDS bin capacity (the GPU tests send most bins through k_bin_big)
-static uint32_t bin_cap() {
-    const char *e = getenv("GPUFLOW_BIN_CAP");
-    const uint32_t c = e ? (uint32_t)strtoul(e, nullptr, 10) : GF_BIN_CAP;
-    return c < GF_BIN_CAP ? c : GF_BIN_CAP;
-}
-// k_bin_sort over every bin, then k_bin_big over the oversized ones (a few idle blocks otherwise)
-static int bin_sort_launch(uint32_t nb, uint32_t *bins, const uint32_t *skeys, uint32_t skip_bin, hipStream_t s) {
-    Workspace &w = ws();
-    ProfScope ps("bin_sort", s);
-    hipLaunchKernelGGL(k_bin_sort, dim3(nb), dim3(BLOCK), 0, s, nb, bin_cap(), bins,
-                       (const unsigned long long *)w.pairs.p, skeys, skip_bin, (uint32_t *)w.perm.p, (uint32_t *)w.runs.p);
-    hipLaunchKernelGGL(k_bin_big, dim3(64), dim3(BLOCK), 0, s, nb, bins, (unsigned long long *)w.pairs.p, skeys,
-                       (uint32_t *)w.perm.p, (uint32_t *)w.runs.p);
-    return hip_ok(hipGetLastError(), "bin sort");
-}
-// The list of buckets, longest first (k_bucket_base + k_bucket_order_runs)
-static int bucket_order_launch(uint32_t n, hipStream_t s) {
-    Workspace &w = ws();
-    uint32_t *d_sched = (uint32_t *)w.sched.p;
-    ProfScope ps("k_bucket_sched", s);
-    const uint32_t go = std::max<uint32_t>(1, (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS);
-    hipLaunchKernelGGL(k_bucket_hist_runs, dim3(go), dim3(BLOCK), 0, s, n, (const uint32_t *)w.runs.p, d_sched);
-    hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
-    hipLaunchKernelGGL(k_bucket_order_runs, dim3(go), dim3(BLOCK), 0, s, n, (const uint32_t *)w.runs.p, d_sched,
-                       (uint2 *)w.order.p);
-    return hip_ok(hipGetLastError(), "k_bucket_sched");
-}
-// GF_SCHED_CHECK (diagnosis): the schedule's invariants checked on the host
-// after each stage (the call syncs), with a message and -EIO on a violation.
-static bool sched_check_on() { static const bool on = getenv("GF_SCHED_CHECK") != nullptr; return on; }
-static int sched_check(const char *stage, uint32_t n, uint32_t nb, const uint32_t *d_off, hipStream_t s) {
-    Workspace &w = ws();
-    if (hip_ok(hipStreamSynchronize(s), stage)) { fprintf(stderr, "[gf] sched check: fault after %s\n", stage); return -EIO; }
-    std::vector<uint32_t> off(nb + 1), perm(n), sched(GF_SCHED_WORDS);
-    if (hip_ok(hipMemcpy(off.data(), d_off, (nb + 1) * 4, hipMemcpyDeviceToHost), "chk off") ||
-        hip_ok(hipMemcpy(perm.data(), w.perm.p, (size_t)n * 4, hipMemcpyDeviceToHost), "chk perm") ||
-        hip_ok(hipMemcpy(sched.data(), w.sched.p, GF_SCHED_WORDS * 4, hipMemcpyDeviceToHost), "chk sched"))
-        return -EIO;
-    {
-        std::vector<uint32_t> sk(n), k0(n);
-        if (hip_ok(hipMemcpy(sk.data(), w.skeys.p, (size_t)n * 4, hipMemcpyDeviceToHost), "chk skeys") ||
-            hip_ok(hipMemcpy(k0.data(), w.keys.p, (size_t)n * 4, hipMemcpyDeviceToHost), "chk keys"))
-            return -EIO;
-        uint32_t bad = 0, first = 0;
-        for (uint32_t p = 1; p < n; p++)
-            if ((sk[p] & 0xffffu) < (sk[p - 1] & 0xffffu)) { if (!bad) first = p; bad++; }
-        if (bad)
-            fprintf(stderr, "[gf] sched check %s: skeys unsorted at %u places, first %u: %08x %08x (keys[0..3] %08x %08x %08x)\n",
-                    stage, bad, first, sk[first - 1], sk[first], k0[0], k0[1], k0[2]);
-        std::vector<uint32_t> ref(nb + 1, 0);
-        for (uint32_t p = 0; p < n; p++) ref[(sk[p] & 0xffffu) + 1]++;
-        for (uint32_t b = 0; b < nb; b++) ref[b + 1] += ref[b];
-        uint32_t nbad = 0;
-        for (uint32_t b = 0; b <= nb; b++)
-            if (ref[b] != off[b]) { if (nbad < 4) fprintf(stderr, "[gf] sched check %s: off[%u]=%u host %u\n", stage, b, off[b], ref[b]); nbad++; }
-        if (nbad) fprintf(stderr, "[gf] sched check %s: %u bin starts differ from the host's\n", stage, nbad);
-    }
-    for (uint32_t b = 0; b < nb; b++)
-        if (off[b] > off[b + 1] || off[b + 1] > n) {
-            fprintf(stderr, "[gf] sched check %s: off[%u]=%u off[%u]=%u n=%u\n", stage, b, off[b], b + 1, off[b + 1], n);
-            return -EIO;
-        }
-    for (uint32_t p = 0; p < off[nb]; p++)
-        if (perm[p] >= n) { fprintf(stderr, "[gf] sched check %s: perm[%u]=%u n=%u\n", stage, p, perm[p], n); return -EIO; }
-    std::vector<uint32_t> rl(n);
-    if (hip_ok(hipMemcpy(rl.data(), w.runs.p, (size_t)n * 4, hipMemcpyDeviceToHost), "chk runs")) return -EIO;
-    uint64_t tot = 0, nr = 0;
-    for (uint32_t q = 0; q < n; q++) {
-        const uint32_t c = rl[q] & 0x7fffffffu;
-        if (!rl[q]) continue;
-        nr++; tot += c;
-        if (q + c > n) { fprintf(stderr, "[gf] sched check %s: run at %u count %u\n", stage, q, c); return -EIO; }
-    }
-    fprintf(stderr, "[gf] sched check %s ok: n=%u live=%u runs=%llu packets in runs=%llu\n", stage, n, off[nb],
-            (unsigned long long)nr, (unsigned long long)tot);
-    return 0;
-}
-// GF_SCHED=bins16: the bins by a stable radix sort of the keys' top 16 bits (two
-// onesweep passes instead of four), then k_bin_sort as above; the bin of
-// GF_KEY_SKIP holds only skipped packets (gf_key_live) and is left alone.  The
-// sort runs on the keys rotated by 16 (their bin in the low half, bits [0, 16)):
-// this image's rocPRIM left keys unsorted when asked for bits [16, 32).
-static int schedule_bins16(uint32_t n, hipStream_t s) {
-    static_assert(GF_KEY_BITS == 32, "bins16: the bin is the top half of a 32-bit key");
-    Workspace &w = ws();
-    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-    const uint32_t nb = 1u << 16, sh = GF_KEY_BITS - 16;
-    int r;
-    size_t sort_bytes = 0;
-    const auto rk = rocprim::make_transform_iterator((const uint32_t *)w.keys.p, Rot16{});
-    (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, rk, (uint32_t *)w.skeys.p,
-                                    rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0u, 16u, s);
-    if ((r = grow(w.bins, (size_t)GF_BINS_WORDS(nb) * 4)) || (r = grow(w.pairs, (size_t)n * 8 + 8)) ||
-        (r = grow(w.runs, (size_t)n * 4 + 4)) || (r = grow(w.tmp, sort_bytes + 256)))
-        return r;
-    uint32_t *bins = (uint32_t *)w.bins.p, *d_sched = (uint32_t *)w.sched.p;
-    {
-        ProfScope ps("rocprim_radix_sort", s);
-        size_t tb = w.tmp.bytes;
-        if (hip_ok(rocprim::radix_sort_pairs(w.tmp.p, tb, rk, (uint32_t *)w.skeys.p,
-                                             rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)w.perm.p, n, 0u, 16u,
-                                             s), "radix_sort_pairs 16"))
-            return -EIO;
-    }
-    {
-        ProfScope ps("bin_bounds", s);
-        if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist") ||
-            hip_ok(hipMemsetAsync(bins + 4 * nb + 1, 0, 8, s), "memset big") ||
-            hip_ok(hipMemsetAsync(w.runs.p, 0, (size_t)n * 4, s), "memset runs"))
-            return -EIO;
-        hipLaunchKernelGGL(k_bin_bounds, dim3((nb + BLOCK) / BLOCK), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p, nb,
-                           bins + nb);
-        if ((r = hip_ok(hipGetLastError(), "bin bounds"))) return r;
-    }
-    if (sched_check_on() && (r = sched_check("bounds", n, nb, bins + nb, s))) return r;
-    if ((r = bin_sort_launch(nb, bins, (const uint32_t *)w.skeys.p, GF_KEY_SKIP >> sh, s))) return r;
-    if (sched_check_on() && (r = sched_check("bin sort", n, nb, bins + nb, s))) return r;
-    if ((r = bucket_order_launch(n, s))) return r;
-    if (sched_check_on() && (r = sched_check("bucket order", n, nb, bins + nb, s))) return r;
-    return 0;
-}
-static int schedule_bins(uint32_t n, hipStream_t s) {
-    Workspace &w = ws();
-    auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-    uint32_t B = 1;                                     // 2^B bins, about GF_BIN_TARGET pairs each (half per family)
-    while (B < 16 && B < GF_KEY_BITS && ((uint64_t)GF_BIN_TARGET << (B - 1)) < n) B++;
-    const uint32_t nb = 1u << B, sh = GF_KEY_BITS - B;
-    int r;
-    if ((r = grow(w.bins, (size_t)GF_BINS_WORDS(nb) * 4)) || (r = grow(w.pairs, (size_t)n * 8 + 8)) ||
-        (r = grow(w.runs, (size_t)n * 4 + 4)))
-        return r;
-    uint32_t *bins = (uint32_t *)w.bins.p, *d_sched = (uint32_t *)w.sched.p;
-    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 8192));
-    if (hip_ok(hipMemsetAsync(bins, 0, (size_t)nb * 4, s), "memset bins") ||
-        hip_ok(hipMemsetAsync(w.runs.p, 0, (size_t)n * 4, s), "memset runs") ||
-        hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist"))
-        return -EIO;
-    {
-        ProfScope ps("bin_count", s);
-        hipLaunchKernelGGL(k_bin_count, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.keys.p, sh, bins);
-        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, nb, bins, d_sched);
-    }
-    {
-        ProfScope ps("bin_scatter", s);
-        hipLaunchKernelGGL(k_bin_scatter, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.keys.p, sh,
-                           bins + 2 * nb + 1, (unsigned long long *)w.pairs.p);
-    }
-    if ((r = bin_sort_launch(nb, bins, nullptr, ~0u, s))) return r;
-    return bucket_order_launch(n, s);
-}
-
 static int schedule_groups(uint32_t n, hipStream_t s) {
-    static const int mode = [] { const char *e = getenv("GF_SCHED"); return !e ? 0 : !strcmp(e, "bins") ? 1 : !strcmp(e, "bins16") ? 2 : 0; }();
-    if (mode == 1) return schedule_bins(n, s);
-    if (mode == 2) return schedule_bins16(n, s);
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
