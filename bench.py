@@ -269,13 +269,18 @@ def timed(B, run_step, W, K, world=1, ranged=False):
         dist.barrier()
     B.sync()
     t0 = time.perf_counter()
+    host = 0.0                                          # time inside the calls (host enqueue work + waits)
     if ranged:
         run_step(W, W + K)
     else:
         for s in range(W, W + K):
+            h0 = time.perf_counter()
             run_step(s)
+            host += time.perf_counter() - h0
     B.sync()
     t1 = time.perf_counter()
+    if not ranged:
+        log(f"host time inside the classify calls: {host / K * 1e3:.3f} ms/step of {(t1 - t0) / K * 1e3:.3f}")
     if world > 1:
         dist.barrier()
     counters, kern = B.end()

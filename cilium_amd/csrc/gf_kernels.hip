@@ -741,6 +741,7 @@ struct IngCtx {
     uint32_t gw, host6[4];     // IPV4_GATEWAY, HOST_IP (node_config.h)
     uint8_t *tmark, *tcap;     // trace notifications: per-packet GF_TR_* marks, 128-B captures (null: off)
     uint32_t *rlog, *rlog_n;   // egress connection groups: ct_create4's related entries logged (null: written)
+    const uint32_t *rlog_off;  // device word: nonzero = the run fell back to pair groups (entries written inline)
 };
 
 // ---- handle_policy's own header writes (kept out of line: cold paths of the
@@ -1357,8 +1358,10 @@ __device__ __attribute__((noinline)) void pol_redirect_ol(PolCtx X, uint32_t i, 
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
+// rlog: X.rlog unless the run fell back to pair groups (read once per kernel, k_ing_groups)
 __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
-                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo<GF_MEMO4> &pm) {
+                           uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo<GF_MEMO4> &pm,
+                           uint32_t *rlog) {
     uint32_t len = r.len;
     if (len < 34) return D_INVALID;
     const uint32_t flags = ep.flags;
@@ -1412,7 +1415,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (r.cls & 4) verdict = 0;                         // skip_proxy
     if (ret == CT_NEW && !(GF_DIAG & 8)) {
         ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab,
-                                         X.rlog, X.rlog_n, 2u * i + 1u);
+                                         rlog, X.rlog_n, 2u * i + 1u);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -1556,7 +1559,7 @@ struct Lane {
 // conntrack.  The sort key keeps the two sets in different buckets.
 template <int FAM>
 __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane<FAM> &ln,
-                                                       uint32_t &ab) {
+                                                       uint32_t &ab, uint32_t *rlog) {
     gf_ingress_out o{};
     uint32_t sl = r.ep;
     if (!sl) { o.action = TC_SHOT; o.reason = 140; return o; }   // missed tail call (DROP_MISSED_TAIL_CALL)
@@ -1575,7 +1578,8 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
+        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm,
+                                                  rlog);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
     else ret = D_UNKNOWN_L3;
@@ -1652,10 +1656,10 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 // carry equal work and the deepest buckets start first.
 template <int FAM>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
-                                        Stats &st, bool stats, Lane<FAM> &ln) {
+                                        Stats &st, bool stats, Lane<FAM> &ln, uint32_t *rlog) {
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab);
+    gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab, rlog);
     if (X.pout) {                                       // complete the pipeline record
         uint8_t *q = X.pout + 24 * (size_t)i;
         uint2 a = *reinterpret_cast<const uint2 *>(q), b = *reinterpret_cast<const uint2 *>(q + 8);
@@ -1701,19 +1705,21 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
                                                       const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
                                                       unsigned long long *stats) {
+    constexpr int F = FAM == 6 ? 1 : 0;
+    const uint32_t *nfam = GF_SCHED_NFAM(sched);
+    if (nfam[F] == 0) return;                          // no bucket of this family (nothing to count either)
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    constexpr int F = FAM == 6 ? 1 : 0;
-    const uint32_t *nfam = GF_SCHED_NFAM(sched);
     uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
     const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
     if (F) order += nfam[0];
     __shared__ Lane<FAM> lanes[BLOCK];
     Lane<FAM> &ln = lanes[threadIdx.x];
     ln.init();
+    uint32_t *const rlog = X.rlog && !(X.rlog_off && *X.rlog_off) ? X.rlog : nullptr;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -1747,10 +1753,10 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 #if GF_PREFETCH_REC
             gf_rec rn;
             if (k + 1 < c) rn = rec[inx];
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
+            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2; r = rn;
 #else
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln);
+            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2;
             if (k + 1 < c) r = rec[i];
 #endif
@@ -2674,6 +2680,14 @@ __device__ __forceinline__ int64_t px_upsert(const PxDev &P, const uint32_t *e, 
     if (e[1] == 6) return P.d6.slots ? ht_upsert<22, 7, GF_HASH_PLAIN>(P.d6, e + 2, e + 8, strict, added) : 0;
     return P.d4.slots ? ht_upsert<10, 4, GF_HASH_PLAIN>(P.d4, e + 2, e + 8, strict, added) : 0;
 }
+// Without proxy maps the updates are no-ops: only the redirects' MAC stores (frames written)
+__global__ __launch_bounds__(BLOCK) void k_px_macs(const uint32_t *plog, const uint32_t *n_, PxDev P) {
+    const uint32_t n = *n_;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
+        const uint32_t *e = plog + 16ull * j;
+        if (!e[15]) px_macs(P, e[0]);
+    }
+}
 __global__ __launch_bounds__(BLOCK) void k_px_keys(const uint32_t *plog, uint32_t n, bool by_index,
                                                    unsigned long long *key, uint32_t *val) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
@@ -3233,6 +3247,12 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
 // After the front: a flagged batch runs as one bucket per family (every IPv4
 // key equal; the IPv6 path writes no service entries and keeps its own bucket).
 // With connection groups and an IPv4 ICMP packet in the run: the pair keys.
+// The deliveries' keys of a run that fell back to pair groups (*cflag): their pair keys.
+__global__ __launch_bounds__(BLOCK) void k_eg_pick_keys(const uint32_t *cflag, const uint32_t *key2P, uint32_t n,
+                                                        uint32_t *keys) {
+    if (!*cflag) return;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) keys[i] = key2P[i];
+}
 __global__ __launch_bounds__(BLOCK) void k_eg_seq_keys(const uint32_t *seq, const uint32_t *cflag,
                                                        const uint32_t *keysP, uint32_t n, uint32_t *keys) {
     if (*seq) {
@@ -4460,6 +4480,7 @@ static TraceWs &trace_ws() { static const char tag = 0; return cur_ctx().get<Tra
 struct PassArgs {                  // what the pipeline / egress callers pass to their handle_policy pass
     uint32_t kind;                 // 1 pipeline, 2 egress
     uint32_t *rlog, *rlog_n;       // egress connection groups: the related-entry log (null: written inline)
+    const uint32_t *rlog_off;      // device word: the run fell back to pair groups (the log is not used)
     bool on;                       // this call traces (a ring is set and a program / the netdev traces)
     uint32_t nd_trace, nd_ifindex; // pipeline: GF_NETDEV_F_TRACE_NOTIFY, skb->ingress_ifindex
     const uint8_t *orig;           // egress: the frames as sent
@@ -4671,13 +4692,23 @@ static int px_log_begin(uint32_t n, hipStream_t s, IngCtx &X, bool keep = false)
 }
 // recs: the launch's verdict records (24-B pipeline/egress layout when wide, else gf_ingress_out)
 static int px_log_apply(const IngCtx &X, hipStream_t s, uint8_t *wsnap, const uint32_t *len, uint32_t stride,
-                        uint8_t *recs, bool wide) {
+                        uint8_t *recs, bool wide, uint32_t n) {
     if (!X.plog) return 0;
     px_ws().live = false;
     auto px4 = proxy_map(4), px6 = proxy_map(6);
     const gf_node_cfg &node = node_cfg();
     PxWs &w = px_ws();
     int r;
+    if (!px4 && !px6) {                               // the MAC stores alone: the count stays on the device
+        if (!wsnap) return 0;
+        PxDev P{};
+        P.snap = wsnap; P.len = len; P.snap_stride = stride;
+        memcpy(P.host_mac, node.host_mac, 6); memcpy(P.node_mac, node.node_mac, 6);
+        ProfScope ps("k_proxy_apply", s);
+        hipLaunchKernelGGL(k_px_macs, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)X.plog,
+                           (const uint32_t *)X.plog_n, P);
+        return hip_ok(hipGetLastError(), "k_px_macs");
+    }
     uint32_t cnt = 0;
     if (hip_ok(hipMemcpyAsync(&cnt, X.plog_n, 4, hipMemcpyDeviceToHost, s), "plog count") ||
         hip_ok(hipStreamSynchronize(s), "plog sync"))
@@ -4784,6 +4815,7 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
                    (cb && memcmp(a->h_cfgs.data(), cfgs.data(), cb)) ||
                    memcmp(a->h_slot_of.data(), slot_of.data(), slot_of.size() * 2);
     if (changed) {
+        if (getenv("GF_SYNC_DEBUG")) fprintf(stderr, "[gf] program table upload (dirty %d)\n", (int)a->dirty);
         if ((r = a->d_slot_of_lxc.ensure(65536 * 2))) return r;
         if ((r = a->d_cfgs.ensure(std::max<size_t>(1, cb)))) return r;
         a->h_cfgs.assign((const uint8_t *)cfgs.data(), (const uint8_t *)cfgs.data() + cb);
@@ -4811,7 +4843,11 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
         // entries stay until GC, bounded by the slot array (7/8 load = 3.5 x max_entries)
         uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
         if (m->host_valid) m->dev_count_hi = m->ht.count;
-        if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && !m->host_valid) {
+        // (no readback when the batch alone could exceed the limit: strict either way)
+        if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && (uint64_t)per_pkt * n <= limit && !m->host_valid) {
+            if (getenv("GF_SYNC_DEBUG"))
+                fprintf(stderr, "[gf] CT count readback (bound %llu + %u x %u > %llu)\n", (unsigned long long)m->dev_count_hi,
+                        per_pkt, n, (unsigned long long)limit);
             uint32_t dc = 0;
             if (hip_ok(hipStreamSynchronize(s), "ct count sync") ||
                 hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
@@ -4941,7 +4977,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
     if (tracing) { X.tmark = (uint8_t *)trace_ws().mark.p; X.tcap = (uint8_t *)trace_ws().px.p; }
-    if (ta) { X.rlog = ta->rlog; X.rlog_n = ta->rlog_n; }
+    if (ta) { X.rlog = ta->rlog; X.rlog_n = ta->rlog_n; X.rlog_off = ta->rlog_off; }
     if ((r = px_log_begin(n, s, X, px_keep))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
@@ -4966,7 +5002,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
     if ((r = px_log_apply(X, s, wsnap, ev_len ? ev_len : pkts->len, ev_stride, pout ? pout : (uint8_t *)out,
-                          pout != nullptr)))
+                          pout != nullptr, n)))
         return r;
     {
         EvSrc E{};
@@ -5576,6 +5612,8 @@ namespace {
 struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
              hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n;
              uint32_t hz_gen = 0, hz_cap = 0;
+             uint32_t *h_hz = nullptr;          // pinned: the ordering check's words, read back without a stream sync
+             hipEvent_t ev_hz = nullptr;
              std::vector<std::pair<const Map *, uint64_t>> vip_stamp;
              uint32_t vip4_mask = 0, vip6_mask = 0; bool vip4_any = false, vip6_any = false; };
 EgWs &eg_ws() { static const char tag = 0; return cur_ctx().get<EgWs>(&tag); }
@@ -5652,6 +5690,8 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
 }
 // A log of deferred CT4 writes {order, key[4], value[12], pad[3]} applied in
 // order (k_ctlog_max / k_ctlog_apply: the last writer of a key wins).
+// nlog: an upper bound of the entry count (*d_n, read by the kernels): no host
+// round trip for the count.
 static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32_t nlog, const gf_htab_desc &ct,
                        uint32_t *ct_count, hipStream_t s) {
     if (!nlog) return 0;
@@ -5806,8 +5846,26 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         hipLaunchKernelGGL(k_hz_probe, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t *)ew.hzk.p,
                            (const uint8_t *)ew.hzfl.p, n, C, A, strict, d_hz);
         if ((r = hip_ok(hipGetLastError(), "k_hz_check"))) return r;
+        // the check's verdict goes to pinned host memory behind an event: the host
+        // reads it while the device already builds the schedule (no stream sync)
+        if (!ew.h_hz && (hip_ok(hipHostMalloc((void **)&ew.h_hz, 16, hipHostMallocDefault), "hz host") ||
+                         hip_ok(hipEventCreateWithFlags(&ew.ev_hz, hipEventDisableTiming), "hz event")))
+            return -EIO;
+        if (hip_ok(hipMemcpyAsync(ew.h_hz, d_hz, 12, hipMemcpyDeviceToHost, s), "hz flag") ||
+            hip_ok(hipEventRecord(ew.ev_hz, s), "hz record"))
+            return -EIO;
     }
-    if ((r = schedule_groups(n, s))) return r;
+    if ((r = schedule_groups(n, s))) return r;           // (reads only the front's keys: harmless on a flagged batch)
+    uint32_t hz = 0, hz_first = 0;
+    if (check) {
+        if (hip_ok(hipEventSynchronize(ew.ev_hz), "hz sync")) return -EIO;
+        hz = ew.h_hz[0]; hz_first = ew.h_hz[2];
+    }
+    if (hz & 2u) {
+        if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
+        return egress_each(a, b, now_sec, out, snap_out, s, lru);
+    }
+    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru, hz_first, depth);
     {
         uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
@@ -5822,24 +5880,13 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
                            sink);
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
-    // ct_create4's deferred service entries, in batch order
-    uint32_t cnts[2] = {0, 0}, hzw[3] = {0, 0, 0}, &hz = hzw[0], rn[2] = {0, 0};
-    if (hip_ok(hipMemcpyAsync(cnts, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost, s), "ctlog count") ||
-        (check && hip_ok(hipMemcpyAsync(hzw, d_hz, 12, hipMemcpyDeviceToHost, s), "hz flag")) ||
-        (conn && hip_ok(hipMemcpyAsync(rn, d_rn, 8, hipMemcpyDeviceToHost, s), "rlog count")) ||
-        hip_ok(hipStreamSynchronize(s), "ctlog sync"))
-        return -EIO;
-    const bool clog = conn && !rn[1];                  // connection groups held (no IPv4 ICMP in the run)
-    if (hz & 2u) {
-        if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
-        return egress_each(a, b, now_sec, out, snap_out, s, lru);
-    }
-    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru, hzw[2], depth);
+    // ct_create4's deferred service entries, in batch order; every count from here
+    // on is read on the device (no host round trip inside the call)
     if (check && sink) {
         hipLaunchKernelGGL(k_stats_fold, dim3(1), dim3(256), 0, s, (const unsigned long long *)fsink, sink);
         if ((r = hip_ok(hipGetLastError(), "k_stats_fold"))) return r;
     }
-    if (ct4m && (r = ctlog_apply(ew, (const uint32_t *)ew.ctlog.p, (const uint32_t *)ew.ctlog_n.p, cnts[0], cfg_ct4,
+    if (ct4m && (r = ctlog_apply(ew, (const uint32_t *)ew.ctlog.p, (const uint32_t *)ew.ctlog_n.p, n, cfg_ct4,
                                  (uint32_t *)ct4m->d_count.p, s)))
         return r;
     if (ct4m) ct4m->device_modified();
@@ -5852,28 +5899,29 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     c2.n = n;
     c2.len = fr.len;
     c2.flow_hash = b->flow_hash;
-    if (cnts[1]) { c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p; }   // IPv6 deliveries
+    c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p;   // IPv6 deliveries (if any)
     // the deliveries' keys: their connections, or address pairs when the run fell back
     // k_eg_groups wrote them in batch order: they become the workspace's records and
     // keys by exchanging the buffers (the workspace's old ones are the next call's
-    // pass-2 buffers), not by copying n records
-    DevBuf &k2 = (conn && !clog) ? ew.key2P : ew.key2;
+    // pass-2 buffers), not by copying n records; a fallen-back run takes the pair
+    // keys on the device (k_eg_seq_keys' rule, *cflag)
     auto pack = [&](const uint16_t *, gf_rec *, uint32_t *) -> int {
         Workspace &w = ws();
         std::swap(w.rec.p, ew.rec2.p); std::swap(w.rec.bytes, ew.rec2.bytes);
-        std::swap(w.keys.p, k2.p); std::swap(w.keys.bytes, k2.bytes);
+        std::swap(w.keys.p, ew.key2.p); std::swap(w.keys.bytes, ew.key2.bytes);
+        if (conn) {
+            hipLaunchKernelGGL(k_eg_pick_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)E.cflag,
+                               (const uint32_t *)ew.key2P.p, n, (uint32_t *)w.keys.p);
+            return hip_ok(hipGetLastError(), "k_eg_pick_keys");
+        }
         return 0;
     };
-    if (clog) { ta.rlog = d_rn ? (uint32_t *)ew.rlog.p : nullptr; ta.rlog_n = d_rn; }
-    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru && !clog, true,
+    if (conn) { ta.rlog = (uint32_t *)ew.rlog.p; ta.rlog_n = d_rn; ta.rlog_off = E.cflag; }
+    if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru && !conn, true,
                          false, &ta)))
         return r;
-    if (clog) {                                        // both passes' related entries, in packet order
-        uint32_t nrl = 0;
-        if (hip_ok(hipMemcpyAsync(&nrl, d_rn, 4, hipMemcpyDeviceToHost, s), "rlog count") ||
-            hip_ok(hipStreamSynchronize(s), "rlog sync"))
-            return -EIO;
-        if ((r = ctlog_apply(ew, (const uint32_t *)ew.rlog.p, d_rn, nrl, cfg_ct4, (uint32_t *)ct4m->d_count.p, s)))
+    if (conn) {                                        // both passes' related entries, in packet order
+        if ((r = ctlog_apply(ew, (const uint32_t *)ew.rlog.p, d_rn, 2 * n, cfg_ct4, (uint32_t *)ct4m->d_count.p, s)))
             return r;
         ct4m->device_modified();
         if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
