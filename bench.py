@@ -1120,7 +1120,7 @@ def add_bounds(cfg, r):
         return r
     try:
         j = json.load(open(pmc[-1]))
-        names = PMC_KERNELS.get(cfg) or list(j["kernels"])
+        names = PMC_KERNELS.get(cfg) or [k for k in j["kernels"] if k.startswith("k_") or k == "rocprim"]
         ks = [j["kernels"][k] for k in names if k in j["kernels"]]
         pk = r.get("packets_per_step") or r.get("config", {}).get("packets_per_step_per_gpu")
         scale = float(pk) / float(j["packets_per_step"])
