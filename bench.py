@@ -1133,9 +1133,6 @@ def add_bounds(cfg, r):
                            "valu_busy": round(2 * valu / t / ISSUE_PEAK, 4),
                            "wave_insts_per_s": (valu + salu) / t, "peak": ISSUE_PEAK,
                            "wave_insts_per_64_packets": round((valu + salu) * 64 / float(pk), 1), "source": src}
-            gui = cs("GRBM_GUI_ACTIVE")
-            if gui:
-                rf["issue"]["effective_clock_ghz"] = round(gui / 8 / t / 1e9, 3)
         req = cs("TCC_EA0_RDREQ_sum") + cs("TCC_EA0_WRREQ_sum")
         if req:
             rf["requests"] = {"frac": round(req / t / REQUEST_PEAK, 4), "per_s": req / t, "peak": REQUEST_PEAK,

@@ -4037,8 +4037,9 @@ struct ProfScope {
     ProfScope(const char *n, hipStream_t s_) : on(prof().on), s(s_) {
         if (!on) return;
         e.name = n;
-        (void)hipEventCreate(&e.a);
-        (void)hipEventCreate(&e.b);
+        // timing only: no system-scope fence (an L2 writeback) at each launch boundary
+        (void)hipEventCreateWithFlags(&e.a, hipEventDisableSystemFence);
+        (void)hipEventCreateWithFlags(&e.b, hipEventDisableSystemFence);
         (void)hipEventRecord(e.a, s);
     }
     ~ProfScope() {
@@ -4066,6 +4067,34 @@ void prof_drain() {
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
 };
+// GF_HOST_PROF (diagnosis): the host time of a classify call's phases, one line
+// per call on stderr (where a call waits on the device, or spends its launches).
+struct HostMarks {
+    using clk = std::chrono::steady_clock;
+    bool on;
+    clk::time_point t0, last;
+    char buf[768];
+    int len = 0;
+    HostMarks *prev;
+    static HostMarks *&cur() { static thread_local HostMarks *c = nullptr; return c; }
+    HostMarks() : on(getenv("GF_HOST_PROF") != nullptr), prev(cur()) {
+        buf[0] = 0;
+        if (on) { t0 = last = clk::now(); cur() = this; }
+    }
+    static double us(clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); }
+    void mark(const char *what) {
+        if (!on) return;
+        const auto t = clk::now();
+        if (len < (int)sizeof buf - 40) len += snprintf(buf + len, sizeof buf - len, " %s %.0f", what, us(t - last));
+        last = t;
+    }
+    ~HostMarks() {
+        if (!on) return;
+        cur() = prev;
+        fprintf(stderr, "[gf] host us:%s | total %.0f\n", buf, us(clk::now() - t0));
+    }
+};
+void host_mark(const char *what) { if (HostMarks *m = HostMarks::cur()) m->mark(what); }
 // ---- call contexts: the device workspaces of one classify call.  Each HIP
 // stream has its own, so calls on different streams (over disjoint programs and
 // maps, see CallOrder) run concurrently, host and device; calls on one stream
@@ -4199,7 +4228,11 @@ struct CallOrder {
         return v;
     }
     ~CallOrder() {
-        if (!me->ev && hipEventCreateWithFlags(&me->ev, hipEventDisableTiming) != hipSuccess) { me->ev = nullptr; return; }
+        // (device-scope release: the event orders device work between streams)
+        if (!me->ev && hipEventCreateWithFlags(&me->ev, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
+            me->ev = nullptr;
+            return;
+        }
         if (hipEventRecord(me->ev, s) != hipSuccess) return;
         me->have = true;
         for (OrderPt *o : pts) o->last = me;
@@ -4926,7 +4959,9 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     if (tracing && !ta && (r = trace_prepare(pkts->n, false, s))) return r;
     // 1. sync tables, build the device program table
     std::vector<std::shared_ptr<ProgLxc>> progs;
+    host_mark("ing");
     if ((r = prog_table(a, s, progs))) return r;
+    host_mark("prog");
     // CT maps: one counter is tracked in non-strict mode, so all programs must share
     // one CT map per family (the production layout: cilium_ct4_global / ct6_global).
     std::shared_ptr<Map> ct4m, ct6m;
@@ -4945,6 +4980,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     uint32_t strict = 0;
     gf_htab_desc cfg_ct4{}, cfg_ct6{};
     if ((r = ct_limits(ct4m, ct6m, pkts->n, 2, s, strict, cfg_ct4, cfg_ct6))) return r;
+    host_mark("ctlim");
     // 2. group by flow group (records and keys first), 3. longest-first bucket order
     uint32_t n = pkts->n;
     Workspace &w = ws();
@@ -4961,7 +4997,9 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                            (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
+    host_mark("pack");
     if (!prepared && (r = schedule_groups(n, s))) return r;
+    host_mark("sched");
     uint32_t *d_sched = (uint32_t *)w.sched.p;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
     IngCtx X{};
@@ -5001,6 +5039,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
+    host_mark("groups");
     if ((r = px_log_apply(X, s, wsnap, ev_len ? ev_len : pkts->len, ev_stride, pout ? pout : (uint8_t *)out,
                           pout != nullptr, n)))
         return r;
@@ -5025,10 +5064,12 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
         if ((r = emit_drop_events(E, s))) return r;
     }
+    host_mark("px+ev");
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
     if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
+    host_mark("lru");
     if (ct4m) ct4m->device_modified();
     if (ct6m) ct6m->device_modified();
     return 0;
@@ -5176,6 +5217,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     if (fr.snap_stride < 14) return -EINVAL;
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    HostMarks hm;
     CtxScope cx(s);
     std::lock_guard<std::mutex> ag(p->policy->mu);
     MapLocks L;
@@ -5857,8 +5899,10 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     }
     if ((r = schedule_groups(n, s))) return r;           // (reads only the front's keys: harmless on a flagged batch)
     uint32_t hz = 0, hz_first = 0;
+    host_mark("front+sched");
     if (check) {
         if (hip_ok(hipEventSynchronize(ew.ev_hz), "hz sync")) return -EIO;
+        host_mark("hzwait");
         hz = ew.h_hz[0]; hz_first = ew.h_hz[2];
     }
     if (hz & 2u) {
@@ -6030,12 +6074,14 @@ extern "C" int gf_lxc_egress_classify(int array, const gf_lxc_batch *b, uint32_t
     if (fr.snap_stride < 34) return -EINVAL;           // an Ethernet + IPv4 header at least
     if (fr.n > (1u << 30)) return -E2BIG;
     hipStream_t s = (hipStream_t)stream;
+    HostMarks hm;
     CtxScope cx(s);
     std::lock_guard<std::mutex> ag(a->mu);
     MapLocks L;
     lock_array_maps(L, a);
     L.lock();
     CallOrder co(s, L, a.get());
+    host_mark("locks");
     static const bool nocheck = getenv("GF_EG_NOCHECK") != nullptr;     // diagnosis only: the unordered schedule
     static const bool dbg = getenv("GF_HZ_DEBUG") != nullptr;
     if (!dbg) return egress_call(a, b, now_sec, out, snap_out, s, !nocheck, true);
