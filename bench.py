@@ -582,6 +582,9 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
                 tt += time.perf_counter() - a
                 done += pk.n
         par.records(gout, r, f"step {s}")
+        if (s + 1) % 8 == 0:
+            log(f"parity: {s + 1} of {W + K} steps, {par.packets} packets compared, {par.bad} mismatches "
+                f"({time.time() - t0:.1f}s)")
     compare_ct(B, par, dp, ref, "cilium_ct4_global", 14, div)
     log(f"cpu baseline + parity: {par.packets} packets compared, {par.bad} mismatches; CT {par.ct}; "
         f"{done} packets in {tt:.2f}s on {T} threads ({time.time() - t0:.1f}s)")
