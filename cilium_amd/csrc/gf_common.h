@@ -109,12 +109,13 @@ GF_HD uint32_t gf_key_hash(const uint32_t *w, uint32_t ksz, uint32_t mode) {
         return gf_hash_words(c, 4, 14);
     }
     if (mode == GF_HASH_CT && ksz == 40) {
-        int less = 0;
-        for (int i = 0; i < 4; i++)
-            if (w[i] != w[4 + i]) { less = w[i] < w[4 + i]; break; }
-        const uint32_t *lo = less ? w : w + 4, *hi = less ? w + 4 : w;
+        // less: the first address is the smaller (word-wise compare); selects per
+        // word, not a pointer into w (which would put w in scratch on the device)
+        const bool less = w[0] != w[4] ? w[0] < w[4] : w[1] != w[5] ? w[1] < w[5]
+                        : w[2] != w[6] ? w[2] < w[6] : w[3] < w[7];
         uint32_t p0 = w[8] & 0xffffu, p1 = w[8] >> 16;
-        uint32_t c[10] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3],
+        uint32_t c[10] = {less ? w[0] : w[4], less ? w[1] : w[5], less ? w[2] : w[6], less ? w[3] : w[7],
+                          less ? w[4] : w[0], less ? w[5] : w[1], less ? w[6] : w[2], less ? w[7] : w[3],
                           (p0 < p1 ? p0 : p1) | ((p0 < p1 ? p1 : p0) << 16),
                           (w[9] & 0xffu) | (((w[9] >> 8) & 0xfeu) << 8)};
         return gf_hash_words(c, 10, 40);

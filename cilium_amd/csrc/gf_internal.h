@@ -101,6 +101,7 @@ struct Map : Obj {
     uint64_t xfer_d2h = 0, xfer_h2d = 0;   // bytes the map API moved over PCIe (gf_map_info)
     DevBuf d_slots, d_vals, d_count;
     DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits
+    DevBuf d_lrucodes;          // LRU CT maps: per-slot sweep codes (k_lru_hist -> k_lru_clusters)
     uint32_t lru_seq = 0;       // classify calls that used this map (the eviction log's batch number)
     // get_next_key over a device-authoritative map: a host copy of one chunk of
     // slot headers, and the slot of the key returned last (the dump loop's next

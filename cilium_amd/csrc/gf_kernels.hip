@@ -2215,7 +2215,10 @@ __device__ __forceinline__ void gc_move(const gf_htab_desc &d, uint64_t from, ui
     for (uint32_t k = 0; k < d.slot_size; k += 16) *reinterpret_cast<uint4 *>(b + k) = *reinterpret_cast<const uint4 *>(a + k);
     if (vstride) {
         uint8_t *va = d.vals + from * vstride, *vb = d.vals + to * vstride;
-        for (uint32_t k = 0; k < vstride; k += 4) *reinterpret_cast<uint32_t *>(vb + k) = *reinterpret_cast<const uint32_t *>(va + k);
+        if (vstride % 16 == 0)
+            for (uint32_t k = 0; k < vstride; k += 16) *reinterpret_cast<uint4 *>(vb + k) = *reinterpret_cast<const uint4 *>(va + k);
+        else
+            for (uint32_t k = 0; k < vstride; k += 4) *reinterpret_cast<uint32_t *>(vb + k) = *reinterpret_cast<const uint32_t *>(va + k);
     }
     a[d.ksz] = GF_SLOT_EMPTY;
 }
@@ -2311,7 +2314,9 @@ struct LruDev {
     GcCut cut;
     unsigned long long res[2];
     unsigned long long target;
+    unsigned long long moves[2];  // k_lru_clusters: entries moved found by the masks / by the table (GF_LRU_STATS)
     uint32_t flag, nlog;
+    uint32_t cut_key;             // k_lru_cut: age keys [0, cut_key] are evicted
     LruLog log[GF_LRU_LOGCAP];
 };
 __device__ __forceinline__ uint32_t lru_key(uint32_t lt, uint32_t fl, uint32_t now) {
@@ -2327,101 +2332,181 @@ __global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev 
         L->flag = f ? 1u : 0u;
         L->cut.active = 0;
         L->res[0] = L->res[1] = 0;
+        L->moves[0] = L->moves[1] = 0;
         L->target = (unsigned long long)(max_entries - max_entries / 8u);
     }
     if (f)
         for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
 }
-// Age histogram: wave-aggregated (a wave's entries mostly share a bin), then a
-// block-local direct-mapped LDS cache of bins: a 64-bit {bin, count} word per
-// line, updated by CAS; a bin that misses takes the line over and flushes the
-// previous bin's count with one global add, so a bin that is hot in the block
-// (every entry a batch created was last used `now`) stays in LDS instead of
-// serialising the device on one global address when a cold bin happened to
-// claim its line first.
-// The same pass writes the GC sweep's cluster-start bits (k_gc_starts' rule: a
-// non-EMPTY slot after an EMPTY one) from the state bytes it reads anyway, so
-// the eviction sweep reads the slot array twice instead of three times.  A
-// wave covers 64 consecutive slots (two bit words); lane 0 also reads the state
-// of the slot before them.
+// Age histogram: wave-aggregated (a wave's entries mostly share a bin), then
+// counted per block in LDS and flushed with one global add per non-zero bin.
+// The last GF_LRU_WIN seconds of each class are counted directly (one LDS slot
+// per bin, no collisions): a steady stream's live entries were all last used
+// within its flows' lifetimes, tens of seconds.  Older bins go through a
+// block-local LDS cache: a 64-bit {bin, count} word per line (Fibonacci-hashed),
+// updated by CAS; a bin that misses takes the line over and flushes the previous
+// bin's count with one global add.  (The cache alone, with an XOR-folded index,
+// mapped a closing bin and the non-closing bin 32 s from it to one line: once a
+// stream's live ages spanned more than 32 s, every wave alternated them and sent
+// a global add to a few hot addresses — 27-76 ms per 2^29-slot sweep.)
 #define GF_LRU_LDS 2048u
+#define GF_LRU_WIN 4096u
+#define GF_LRU_HB 1024u               // k_lru_hist block: 16 waves share the LDS bins
+// Per-slot sweep codes (k_lru_hist -> k_lru_clusters): the slot's state and, for
+// an entry, its age key (bits 0-17, + 2), whether its last use lies before time 0
+// (bit 20) and its distance from its home slot (bits 24-31; 255 = 255 or more).
+#define GF_LRU_C_EMPTY 0u
+#define GF_LRU_C_TOMB 1u
+#define GF_LRU_C_KEY 2u
+#define GF_LRU_C_KMASK 0x3ffffu
+#define GF_LRU_C_NEG (1u << 20)
+#define GF_LRU_C_DSH 24
 // Each thread takes GF_LRU_U slots per trip (BLOCK apart, so a wave still
 // covers 64 consecutive slots) and issues all their loads before using any:
 // the state byte and, for maps whose hot value sits in the slot, the lifetime
 // and flags words of the same line (read whether or not the slot is FULL).
 #define GF_LRU_U 4
-__global__ __launch_bounds__(BLOCK) void k_lru_hist(gf_htab_desc d, uint32_t lt_off, uint32_t now, LruDev *L,
-                                                    uint32_t *bits) {
-    if (!L->flag) return;
-    __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
-    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
-    __syncthreads();
-    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * BLOCK * GF_LRU_U, nw = (ns + 31) / 32;
+// An entry's home slot from its key bytes in the slot: the CT key sizes read with
+// constant indices (registers, not a scratch array).
+__device__ __forceinline__ uint64_t lru_home_any(const gf_htab_desc &d, uint64_t i, uint32_t mode) {
+    const uint32_t *k = reinterpret_cast<const uint32_t *>(d.slots + i * d.slot_size);
+    uint32_t w[10];
+#pragma unroll
+    for (uint32_t q = 0; q < 10; q++) {                  // constant indices: registers
+        const uint32_t x = 4 * q < d.ksz ? k[q] : 0u;
+        w[q] = d.ksz >= 4 * q + 4 ? x : (4 * q < d.ksz ? x & ((1u << (8 * (d.ksz - 4 * q))) - 1u) : 0u);
+    }
+    return gf_home_slot(gf_key_hash(w, d.ksz, mode), d.mask, d.slot_size);
+}
+__device__ __forceinline__ uint64_t lru_home(const gf_htab_desc &d, uint64_t i, uint32_t mode) {
+    const uint32_t *k = reinterpret_cast<const uint32_t *>(d.slots + i * d.slot_size);
+    if (d.ksz == 14) {
+        const uint32_t w[4] = {k[0], k[1], k[2], k[3] & 0xffffu};
+        return gf_home_slot(gf_key_hash(w, 14, mode), d.mask, d.slot_size);
+    }
+    if (d.ksz == 40) {
+        const uint32_t w[10] = {k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9]};
+        return gf_home_slot(gf_key_hash(w, 40, mode), d.mask, d.slot_size);
+    }
+    return lru_home_any(d, i, mode);
+}
+// One slot of k_lru_hist (called once per unrolled slot, so the per-trip values
+// stay in registers).
+template <int KIND>
+__device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mode, uint32_t lt_off, uint32_t now,
+                                              LruDev *L, uint32_t *bits, uint32_t *codes, unsigned long long *line,
+                                              uint32_t *win, uint64_t i, uint32_t st, uint32_t lt, uint32_t fl,
+                                              uint32_t kw0, uint32_t kw1, uint32_t kw2, uint32_t kw3) {
+    const uint64_t ns = d.mask + 1, nw = (ns + 31) / 32;
     const uint32_t lane = threadIdx.x & 63u;
     const bool inl = d.vin != 0;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * BLOCK * GF_LRU_U; b0 < ns; b0 += stride) {   // wave-uniform trips
-        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U];
-#pragma unroll
-        for (int u = 0; u < GF_LRU_U; u++) {
-            const uint64_t i = b0 + (uint64_t)u * BLOCK + threadIdx.x;
-            st[u] = i < ns ? d.slots[i * d.slot_size + d.ksz] : (uint32_t)GF_SLOT_EMPTY;
-            lt[u] = fl[u] = 0;
-            if (inl && i < ns) {
-                const uint8_t *v = ht_val(d, i) + lt_off;
-                lt[u] = *reinterpret_cast<const uint32_t *>(v);
-                fl[u] = *reinterpret_cast<const uint16_t *>(v + 4);
+    uint32_t key = ~0u, code = st == GF_SLOT_EMPTY ? GF_LRU_C_EMPTY : GF_LRU_C_TOMB;
+    if (st != GF_SLOT_EMPTY && st != GF_SLOT_TOMB) {
+        if (!inl) {
+            const uint8_t *v = ht_val(d, i) + lt_off;
+            lt = *reinterpret_cast<const uint32_t *>(v);
+            fl = *reinterpret_cast<const uint16_t *>(v + 4);
+        }
+        const uint32_t k = lru_key(lt, fl, now);
+        uint64_t home;
+        if (KIND == 1) {                                 // CT v4: the key came with the slot
+            const uint32_t w[4] = {kw0, kw1, kw2, kw3 & 0xffffu};
+            home = gf_home_slot(gf_key_hash(w, 14, mode), d.mask, d.slot_size);
+        } else {
+            home = lru_home(d, i, mode);
+        }
+        const uint64_t dist = (i - home) & d.mask;
+        code = GF_LRU_C_KEY + k + (ct_last_use(lt, fl) < 0 ? GF_LRU_C_NEG : 0u) +
+               ((uint32_t)(dist < 255 ? dist : 255) << GF_LRU_C_DSH);
+        if (st == GF_SLOT_FULL) key = k;
+    }
+    if (i < ns) codes[i] = code;
+    {
+        const uint64_t w0 = i - lane;             // the wave's first slot
+        uint32_t pv = 0;
+        if (lane == 0 && w0 < ns) pv = d.slots[((w0 - 1) & d.mask) * d.slot_size + d.ksz] != GF_SLOT_EMPTY;
+        pv = __shfl(pv, 0);
+        const uint64_t ne = __ballot(st != GF_SLOT_EMPTY);
+        const uint64_t starts = ne & ~((ne << 1) | (uint64_t)pv);
+        const uint64_t wd = w0 / 32 + lane;
+        if (lane < 2 && w0 < ns && wd < nw) bits[wd] = (uint32_t)(starts >> (32 * lane));
+    }
+    const uint32_t kb = key & (GF_LRU_BINS - 1u);
+    const bool inwin = key != ~0u && kb >= GF_LRU_BINS - GF_LRU_WIN;
+    if (inwin) atomicAdd(&win[(key >> 16) * GF_LRU_WIN + kb - (GF_LRU_BINS - GF_LRU_WIN)], 1u);
+    uint64_t rem = __ballot(key != ~0u && !inwin);  // older bins: wave-aggregated, cached
+    while (rem) {
+        const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
+        const uint32_t k = __shfl(key, (int)lead);
+        const uint64_t m = __ballot(key == k) & rem;
+        if (lane == lead) {
+            const uint32_t n = (uint32_t)__popcll(m), h = (k * 0x9E3779B1u) >> (32 - 11);
+            unsigned long long cur = line[h];
+            for (;;) {
+                const uint32_t ck = (uint32_t)(cur >> 32);
+                const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
+                const unsigned long long seen = atomicCAS(&line[h], cur, want);
+                if (seen == cur) {
+                    if (ck != k && ck != ~0u && (uint32_t)cur) atomicAdd(&L->hist[ck], (uint32_t)cur);
+                    break;
+                }
+                cur = seen;
             }
         }
+        rem &= ~m;
+    }
+}
+// KIND 1: the CT v4 slot (32 B: key 14, state at 14, hot value at 16 with the
+// lifetime first) read as two 16-B loads; KIND 0: any layout, field by field.
+template <int KIND>
+__global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
+                                                        LruDev *L, uint32_t *bits, uint32_t *codes) {
+    if (!L->flag) return;
+    __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
+    __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
+    for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
+    __syncthreads();
+    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * GF_LRU_HB * GF_LRU_U;
+    const bool inl = d.vin != 0;
+    static_assert(GF_LRU_U == 4, "k_lru_hist: four slots a trip");
+    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB * GF_LRU_U; b0 < ns; b0 += stride) {   // wave-uniform trips
+        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U], kw[GF_LRU_U][4];
 #pragma unroll
         for (int u = 0; u < GF_LRU_U; u++) {
-            const uint64_t i = b0 + (uint64_t)u * BLOCK + threadIdx.x;
-            uint32_t key = ~0u;
-            if (st[u] == GF_SLOT_FULL) {
-                if (!inl) {
+            const uint64_t i = b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x;
+            st[u] = GF_SLOT_EMPTY;
+            lt[u] = fl[u] = kw[u][0] = kw[u][1] = kw[u][2] = kw[u][3] = 0;
+            if (KIND == 1) {
+                if (i < ns) {
+                    const uint4 *q = reinterpret_cast<const uint4 *>(d.slots + i * 32);
+                    const uint4 a = q[0], b = q[1];
+                    kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
+                    st[u] = (a.w >> 16) & 0xffu;
+                    lt[u] = b.x;
+                    fl[u] = b.y & 0xffffu;
+                }
+            } else {
+                st[u] = i < ns ? d.slots[i * d.slot_size + d.ksz] : (uint32_t)GF_SLOT_EMPTY;
+                if (inl && i < ns) {
                     const uint8_t *v = ht_val(d, i) + lt_off;
                     lt[u] = *reinterpret_cast<const uint32_t *>(v);
                     fl[u] = *reinterpret_cast<const uint16_t *>(v + 4);
                 }
-                key = lru_key(lt[u], fl[u], now);
-            }
-            {
-                const uint64_t w0 = i - lane;             // the wave's first slot
-                uint32_t pv = 0;
-                if (lane == 0 && w0 < ns) pv = d.slots[((w0 - 1) & d.mask) * d.slot_size + d.ksz] != GF_SLOT_EMPTY;
-                pv = __shfl(pv, 0);
-                const uint64_t ne = __ballot(st[u] != GF_SLOT_EMPTY);
-                const uint64_t starts = ne & ~((ne << 1) | (uint64_t)pv);
-                const uint64_t wd = w0 / 32 + lane;
-                if (lane < 2 && w0 < ns && wd < nw) bits[wd] = (uint32_t)(starts >> (32 * lane));
-            }
-            uint64_t rem = __ballot(key != ~0u);
-            while (rem) {
-                const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
-                const uint32_t k = __shfl(key, (int)lead);
-                const uint64_t m = __ballot(key == k) & rem;
-                if (lane == lead) {
-                    const uint32_t n = (uint32_t)__popcll(m), h = (k ^ (k >> 11)) & (GF_LRU_LDS - 1u);
-                    unsigned long long cur = line[h];
-                    for (;;) {
-                        const uint32_t ck = (uint32_t)(cur >> 32);
-                        const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
-                        const unsigned long long seen = atomicCAS(&line[h], cur, want);
-                        if (seen == cur) {
-                            if (ck != k && ck != ~0u && (uint32_t)cur) atomicAdd(&L->hist[ck], (uint32_t)cur);
-                            break;
-                        }
-                        cur = seen;
-                    }
-                }
-                rem &= ~m;
             }
         }
+#pragma unroll
+        for (int u = 0; u < GF_LRU_U; u++)
+            lru_hist_slot<KIND>(d, mode, lt_off, now, L, bits, codes, line, win, b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x,
+                                st[u], lt[u], fl[u], kw[u][0], kw[u][1], kw[u][2], kw[u][3]);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
         const unsigned long long v = line[k];
         if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) atomicAdd(&L->hist[(uint32_t)(v >> 32)], (uint32_t)v);
     }
+    for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
+        if (win[k]) atomicAdd(&L->hist[(k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN], win[k]);
 }
 // The smallest prefix of the age order whose removal leaves <= target entries:
 // one block scans the 2 x 65536 bins (128 per thread, then a block scan).
@@ -2459,8 +2544,124 @@ __global__ __launch_bounds__(1024) void k_lru_cut(const uint32_t *count, uint32_
         if (kb < GF_LRU_BINS) { L->cut.c = cut_of(kb); L->cut.o = 0; }
         else { L->cut.c = 1ull << 32; L->cut.o = cut_of(kb - GF_LRU_BINS); }
         L->cut.lru = 1;
+        L->cut_key = kb;
         L->cut.active = 1;
     }
+}
+// The eviction sweep of the LRU stand-in: k_gc_clusters' compaction (one lane
+// per 32-slot word, walking the clusters that start in it) decided from the codes
+// k_lru_hist wrote instead of the table: an entry is evicted iff its age key is at
+// most cut_key or its last use lies before time 0 (gc_kill with the cutoffs
+// k_lru_cut derived from cut_key, in key terms).  The lane reads its word's 32
+// codes with eight 16-B loads and works on bit masks (EMPTY, TOMB, evicted, and
+// the occupancy of its chunk and the one before as the walk changes it); the table
+// is touched only where it changes — the state byte of an evicted entry or a
+// tombstone, and the entries that move.  A live entry after a hole moves to the
+// first EMPTY slot in [home, j), found from its code's home distance in the
+// occupancy masks (from the table's state bytes when the home lies further back).
+// Within a cluster all deletions of a chunk are applied before its moves, in slot
+// order: a move at j searches [home(j), j) only, where the deletions and earlier
+// moves are exactly those of k_gc_clusters' interleaved walk.  Needs nslots % 32
+// == 0 (LRU maps: >= 64, 2^k).
+struct LruMasks { uint32_t emp, tmb, kil; };
+__device__ __forceinline__ LruMasks lru_code_masks(const uint32_t *__restrict__ codes, uint64_t w, uint32_t ck) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(codes + w * 32);
+    uint4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = q[i];
+    uint32_t emp = 0, tmb = 0, kil = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t c4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t x = c4[c], bit = 1u << (4 * i + c);
+            const bool e = x == GF_LRU_C_EMPTY, t = x == GF_LRU_C_TOMB;
+            const bool k = !e && !t && ((x & GF_LRU_C_NEG) || (x & GF_LRU_C_KMASK) - GF_LRU_C_KEY <= ck);
+            emp |= e ? bit : 0u;
+            tmb |= t ? bit : 0u;
+            kil |= k ? bit : 0u;
+        }
+    }
+    return {emp, tmb, kil};
+}
+__global__ __launch_bounds__(BLOCK) void k_lru_clusters(gf_htab_desc d, uint32_t mode, const uint32_t *__restrict__ codes,
+                                                        const uint32_t *__restrict__ bits, LruDev *L) {
+    if (!L->cut.active) return;
+    const uint32_t ck = L->cut_key;
+    const uint64_t nw = (d.mask + 1) / 32;
+    const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
+    uint32_t dead = 0, tombs = 0, nmv0 = 0, nmv1 = 0;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t m = bits[w];
+        if (!m) continue;
+        const LruMasks m0 = lru_code_masks(codes, w, ck);
+        while (m) {
+            uint32_t from = (uint32_t)__builtin_ctz(m);
+            uint64_t cw = w;
+            uint32_t emp = m0.emp, tmb = m0.tmb, kil = m0.kil;
+            uint32_t prev = ~0u;                             // occupancy of the chunk before (none in reach)
+            bool hole = false;
+            for (;;) {
+                const uint32_t rng = ~0u << from, e = emp & rng;
+                const uint32_t in = e ? rng & ((1u << __builtin_ctz(e)) - 1u) : rng;   // this chunk's part
+                const uint32_t gone = (tmb | kil) & in;
+                tombs += (uint32_t)__popc(tmb & in);
+                dead += (uint32_t)__popc(kil & in);
+                for (uint32_t g = gone; g; g &= g - 1)
+                    d.slots[(cw * 32 + (uint32_t)__builtin_ctz(g)) * d.slot_size + d.ksz] = GF_SLOT_EMPTY;
+                uint32_t cur = ~emp & ~gone;                 // non-EMPTY slots of the chunk now
+                uint32_t mv = in & ~gone;
+                if (!hole) mv = gone ? mv & ~((2u << __builtin_ctz(gone)) - 1u) : 0u;
+                for (; mv; mv &= mv - 1) {                   // live entries after a hole, in slot order
+                    const uint32_t t = (uint32_t)__builtin_ctz(mv);
+                    const uint64_t j = cw * 32 + t;
+                    const uint32_t dist = codes[j] >> GF_LRU_C_DSH;
+                    if (dist <= 32 + t && dist < 255) {          // home within this chunk or the one before
+                        const uint64_t win = ((uint64_t)cur << 32) | prev;
+                        const uint32_t pj = 32 + t, ph = pj - dist;
+                        const uint64_t span = ((1ull << pj) - 1ull) & ~((1ull << ph) - 1ull);
+                        const uint64_t fr = ~win & span;
+                        if (fr) {
+                            const uint32_t pp = (uint32_t)__builtin_ctzll(fr);
+                            const uint64_t p = pp >= 32 ? cw * 32 + (pp - 32) : (cw ? cw - 1 : nw - 1) * 32 + pp;
+                            gc_move(d, j, p, vstride);
+                            nmv0++;
+                            cur &= ~(1u << t);
+                            if (pp >= 32) cur |= 1u << (pp - 32); else prev |= 1u << pp;
+                        }
+                    } else {                                     // further back: the table's state bytes
+                        uint64_t home = (j - dist) & d.mask;
+                        if (dist == 255) home = lru_home(d, j, mode);    // capped: the home from the key
+                        for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
+                            if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) {
+                                gc_move(d, j, p, vstride);
+                                nmv1++;
+                                cur &= ~(1u << t);
+                                if (p / 32 == cw) cur |= 1u << (p % 32);
+                                else if (p / 32 == (cw ? cw - 1 : nw - 1)) prev |= 1u << (p % 32);
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (gone) hole = true;
+                if (e) break;                                // the cluster ended in this chunk
+                // it continues into the next word (wrapping; a start implies an
+                // EMPTY slot before it, so the walk ends by word w at the latest)
+                cw = cw + 1 == nw ? 0 : cw + 1;
+                const LruMasks mc = lru_code_masks(codes, cw, ck);
+                emp = mc.emp; tmb = mc.tmb; kil = mc.kil;
+                prev = cur;
+                from = 0;
+            }
+            m = cw != w ? 0u : m & (m - 1);                  // past the word: no later start in it
+        }
+    }
+    if (dead) atomicAdd(&L->res[0], (unsigned long long)dead);
+    if (tombs) atomicAdd(&L->res[1], (unsigned long long)tombs);
+    if (nmv0) atomicAdd(&L->moves[0], (unsigned long long)nmv0);
+    if (nmv1) atomicAdd(&L->moves[1], (unsigned long long)nmv1);
 }
 __global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L) {
     if (!L->cut.active) return;
@@ -4931,16 +5132,32 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     uint32_t *bits;
     int r;
     if ((r = ct_sweep_bufs(*m, L, bits))) return r;
+    if (m->d_lrucodes.bytes < m->ht.nslots * 4 && m->d_lrucodes.ensure(m->ht.nslots * 4)) return -ENOMEM;
+    uint32_t *codes = (uint32_t *)m->d_lrucodes.p;
     const gf_htab_desc d = m->hdesc();
     const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
     ProfScope ps("k_lru_evict", s);
+    if ((d.mask + 1) % 32) return -EIO;                  // k_lru_clusters' word walk (LRU maps: >= 64, 2^k)
     hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, (const uint32_t *)d.count, m->max_entries, L);
-    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + BLOCK * GF_LRU_U - 1) / (BLOCK * GF_LRU_U),
-                                                     resident_blocks(8));
-    hipLaunchKernelGGL(k_lru_hist, dim3(gh), dim3(BLOCK), 0, s, d, lt_off, now, L, bits);
+    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + GF_LRU_HB * GF_LRU_U - 1) / (GF_LRU_HB * GF_LRU_U),
+                                                     resident_blocks(2));   // 48 KB of LDS a block
+    if (d.slot_size == 32 && d.ksz == 14 && d.vin && d.voff + lt_off == 16)
+        hipLaunchKernelGGL(k_lru_hist<1>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
+    else
+        hipLaunchKernelGGL(k_lru_hist<0>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
     hipLaunchKernelGGL(k_lru_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, now, L);
-    ct_sweep_launch(*m, L, bits, s, true);
+    const uint64_t nw = (d.mask + 1) / 32;
+    hipLaunchKernelGGL(k_lru_clusters, dim3((uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, resident_blocks(8))),
+                       dim3(BLOCK), 0, s, d, m->ht.mode, (const uint32_t *)codes, (const uint32_t *)bits, L);
     hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
+    static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
+    if (stats) {
+        LruDev h;
+        if (!hip_ok(hipMemcpyAsync(&h, L, offsetof(LruDev, log), hipMemcpyDeviceToHost, s), "lru stats") &&
+            !hip_ok(hipStreamSynchronize(s), "lru stats") && h.res[0] + h.res[1])
+            fprintf(stderr, "[lru] seq %u now %u: evicted %llu tombs %llu moved %llu (masks) + %llu (table)\n",
+                    m->lru_seq, now, h.res[0], h.res[1], h.moves[0], h.moves[1]);
+    }
     return hip_ok(hipGetLastError(), "k_lru_evict");
 }
 

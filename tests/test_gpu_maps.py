@@ -163,17 +163,19 @@ def _evict_log(fd):
     return [(r.seq, r.now_sec, r.cut_closing, r.cut_other, r.evicted) for r in recs[:n]]
 
 
-@pytest.mark.parametrize("seed", [4, 6])
-def test_lru_eviction_matches_oracle(seed):
+@pytest.mark.parametrize("seed,dt", [(4, 40), (6, 40), (5, 6000)])
+def test_lru_eviction_matches_oracle(seed, dt):
     """LRU CT maps overflowing max_entries: after every batch the device evicts by
     the deterministic age rule (closing entries, then by lifetime) down to the
     7/8 watermark, exactly as the oracle's restatement of the rule; verdicts of
     the following batches, the CT contents and the eviction logs are identical,
-    and the count is back under max_entries at every batch boundary."""
+    and the count is back under max_entries at every batch boundary.  dt = 6000 s
+    between batches puts the older entries' age bins outside k_lru_hist's direct
+    LDS window (the last 4096 s), through its hashed bin cache."""
     sc = synth.fuzz(seed=seed, n_packets=20000, n_batches=5, ct_max=2500, ct6_max=300)
     dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
     for bi, pk in enumerate(sc.batches):
-        now = sc.now + 40 * bi
+        now = sc.now + dt * bi
         io = dp.ingress(DeviceBatch(pk), now)
         torch.cuda.synchronize()
         _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, now), f"ingress b{bi}")
