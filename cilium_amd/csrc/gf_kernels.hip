@@ -2396,7 +2396,7 @@ template <int KIND>
 __device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mode, uint32_t lt_off, uint32_t now,
                                               LruDev *L, uint32_t *bits, uint32_t *codes, unsigned long long *line,
                                               uint32_t *win, uint64_t i, uint32_t st, uint32_t lt, uint32_t fl,
-                                              uint32_t kw0, uint32_t kw1, uint32_t kw2, uint32_t kw3) {
+                                              const uint32_t (&kw)[10]) {
     const uint64_t ns = d.mask + 1, nw = (ns + 31) / 32;
     const uint32_t lane = threadIdx.x & 63u;
     const bool inl = d.vin != 0;
@@ -2410,8 +2410,10 @@ __device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mo
         const uint32_t k = lru_key(lt, fl, now);
         uint64_t home;
         if (KIND == 1) {                                 // CT v4: the key came with the slot
-            const uint32_t w[4] = {kw0, kw1, kw2, kw3 & 0xffffu};
+            const uint32_t w[4] = {kw[0], kw[1], kw[2], kw[3] & 0xffffu};
             home = gf_home_slot(gf_key_hash(w, 14, mode), d.mask, d.slot_size);
+        } else if (KIND == 2) {                          // CT v6
+            home = gf_home_slot(gf_key_hash(kw, 40, mode), d.mask, d.slot_size);
         } else {
             home = lru_home(d, i, mode);
         }
@@ -2457,7 +2459,8 @@ __device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mo
     }
 }
 // KIND 1: the CT v4 slot (32 B: key 14, state at 14, hot value at 16 with the
-// lifetime first) read as two 16-B loads; KIND 0: any layout, field by field.
+// lifetime first) read as two 16-B loads; KIND 2: the CT v6 slot (64 B: key 40,
+// state at 40, hot value at 48) as four; KIND 0: any layout, field by field.
 template <int KIND>
 __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
                                                         LruDev *L, uint32_t *bits, uint32_t *codes) {
@@ -2467,17 +2470,33 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
     __syncthreads();
-    const uint64_t ns = d.mask + 1, stride = (uint64_t)gridDim.x * GF_LRU_HB * GF_LRU_U;
+    const uint64_t ns = d.mask + 1;
     const bool inl = d.vin != 0;
     static_assert(GF_LRU_U == 4, "k_lru_hist: four slots a trip");
-    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB * GF_LRU_U; b0 < ns; b0 += stride) {   // wave-uniform trips
-        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U], kw[GF_LRU_U][4];
+    constexpr uint32_t UT = KIND == 2 ? 2u : GF_LRU_U;
+    const uint64_t stride_k = (uint64_t)gridDim.x * GF_LRU_HB * UT;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB * UT; b0 < ns; b0 += stride_k) {   // wave-uniform trips
+        constexpr int UK = KIND == 2 ? 2 : GF_LRU_U;     // slots a trip (v6: 64 B each, fewer registers)
+        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U], kw[GF_LRU_U][10];
 #pragma unroll
         for (int u = 0; u < GF_LRU_U; u++) {
             const uint64_t i = b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x;
             st[u] = GF_SLOT_EMPTY;
-            lt[u] = fl[u] = kw[u][0] = kw[u][1] = kw[u][2] = kw[u][3] = 0;
-            if (KIND == 1) {
+            lt[u] = fl[u] = 0;
+#pragma unroll
+            for (int q = 0; q < 10; q++) kw[u][q] = 0;
+            if (KIND == 2) {
+                if (i < ns && u < UK) {
+                    const uint4 *q = reinterpret_cast<const uint4 *>(d.slots + i * 64);
+                    const uint4 a = q[0], b = q[1], c = q[2], e = q[3];
+                    kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
+                    kw[u][4] = b.x; kw[u][5] = b.y; kw[u][6] = b.z; kw[u][7] = b.w;
+                    kw[u][8] = c.x; kw[u][9] = c.y;
+                    st[u] = c.z & 0xffu;
+                    lt[u] = e.x;
+                    fl[u] = e.y & 0xffffu;
+                }
+            } else if (KIND == 1) {
                 if (i < ns) {
                     const uint4 *q = reinterpret_cast<const uint4 *>(d.slots + i * 32);
                     const uint4 a = q[0], b = q[1];
@@ -2497,8 +2516,9 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t
         }
 #pragma unroll
         for (int u = 0; u < GF_LRU_U; u++)
-            lru_hist_slot<KIND>(d, mode, lt_off, now, L, bits, codes, line, win, b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x,
-                                st[u], lt[u], fl[u], kw[u][0], kw[u][1], kw[u][2], kw[u][3]);
+            if (u < UK)
+                lru_hist_slot<KIND>(d, mode, lt_off, now, L, bits, codes, line, win, b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x,
+                                    st[u], lt[u], fl[u], kw[u]);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
@@ -5143,6 +5163,8 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
                                                      resident_blocks(2));   // 48 KB of LDS a block
     if (d.slot_size == 32 && d.ksz == 14 && d.vin && d.voff + lt_off == 16)
         hipLaunchKernelGGL(k_lru_hist<1>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
+    else if (d.slot_size == 64 && d.ksz == 40 && d.vin && d.voff + lt_off == 48)
+        hipLaunchKernelGGL(k_lru_hist<2>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
     else
         hipLaunchKernelGGL(k_lru_hist<0>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
     hipLaunchKernelGGL(k_lru_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, now, L);
