@@ -1136,6 +1136,12 @@ def add_bounds(cfg, r):
                            "valu_busy": round(2 * valu / t / ISSUE_PEAK, 4),
                            "wave_insts_per_s": (valu + salu) / t, "peak": ISSUE_PEAK,
                            "wave_insts_per_64_packets": round((valu + salu) * 64 / float(pk), 1), "source": src}
+        # traffic: FETCH_SIZE + WRITE_SIZE of the same kernels in the same summary (the
+        # round's own passes), per launch of this run
+        tb = sum(k.get("traffic_bytes_per_packet") or 0.0 for k in ks) * float(pk)
+        if tb:
+            rf["traffic"] = tb
+            rf["traffic_source"] = src
         req = cs("TCC_EA0_RDREQ_sum") + cs("TCC_EA0_WRREQ_sum")
         if req:
             rf["requests"] = {"frac": round(req / t / REQUEST_PEAK, 4), "per_s": req / t, "peak": REQUEST_PEAK,
