@@ -198,7 +198,72 @@ struct ProbeLine {
 #pragma unroll
         for (int u = 0; u < U; u++) hd[u].load(d.slots + ((i + u) & d.mask) * d.slot_size);
     }
+    // load() with the home line read by the lane's quad together (coop_line64)
+    // when all four lanes of the quad are here; otherwise each lane reads its own.
+    // For the layouts whose home step is one 64-B line (CT4: 2 x 32 B, CT6: 64 B).
+    __device__ __forceinline__ void load_quad(const gf_htab_desc &d, uint32_t h);
 };
+
+// ---- cooperative line loads (the quad of lanes 4q..4q+3 together) ----
+// A lane that reads its own 64-B line with four 16-B loads makes four
+// wave-instructions that each touch 64 different lines; over a table larger
+// than the GPU's page-translation reach (~2-4 GB on MI355X) those run at 16.5 G
+// lines/s, against 48 G/s when four lanes read one line with one 16-B load each
+// (16 lines per wave-instruction) — profiles/r4_primbench.txt, "tlb".  The CT
+// slot arrays are 4-32 GB.  So the quad reads its four lanes' lines together and
+// a 4 x 4 transpose over DPP quad permutes hands every lane its own line.
+// quad_perm dpp_ctrl: lane i of each quad reads quad lane p_i (p0 | p1 << 2 | ...)
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint4 quad_dpp4(uint4 v) {
+    return make_uint4(quad_dpp<CTRL>(v.x), quad_dpp<CTRL>(v.y), quad_dpp<CTRL>(v.z), quad_dpp<CTRL>(v.w));
+}
+template <int Q>
+__device__ __forceinline__ const uint8_t *quad_bcast_ptr(const uint8_t *p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = quad_dpp<Q * 0x55>((uint32_t)a), hi = quad_dpp<Q * 0x55>((uint32_t)(a >> 32));
+    return (const uint8_t *)(((uint64_t)hi << 32) | lo);
+}
+// Every lane of each quad must be active (convergent call).  p: the lane's 64-B
+// line (16-B aligned), nullptr for none (its words are then zero).
+__device__ __forceinline__ void coop_line64(const uint8_t *p, uint32_t (&w)[16]) {
+    const uint32_t j = threadIdx.x & 3u;
+    uint4 v[4];
+    const uint8_t *pq[4] = {quad_bcast_ptr<0>(p), quad_bcast_ptr<1>(p), quad_bcast_ptr<2>(p), quad_bcast_ptr<3>(p)};
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = pq[q] ? gload<uint4>(pq[q] + 16 * j) : make_uint4(0, 0, 0, 0);
+    // lane j holds chunk j of quad lane q's line in v[q]; wanted: chunk k of its own
+    // line in v[k], i.e. out[j][k] = in[k][j].  Stage b (b = 1, 2): keep v[k] where
+    // bit b of k equals that of j, else take lane j^b's v[k^b].
+    uint4 t[4];
+    t[0] = quad_dpp4<0xB1>(v[1]); t[1] = quad_dpp4<0xB1>(v[0]);     // [1,0,3,2]: lane j ^ 1
+    t[2] = quad_dpp4<0xB1>(v[3]); t[3] = quad_dpp4<0xB1>(v[2]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) if (((uint32_t)k ^ j) & 1u) v[k] = t[k];
+    t[0] = quad_dpp4<0x4E>(v[2]); t[1] = quad_dpp4<0x4E>(v[3]);     // [2,3,0,1]: lane j ^ 2
+    t[2] = quad_dpp4<0x4E>(v[0]); t[3] = quad_dpp4<0x4E>(v[1]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) if (((uint32_t)k ^ j) & 2u) v[k] = t[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { w[4 * k] = v[k].x; w[4 * k + 1] = v[k].y; w[4 * k + 2] = v[k].z; w[4 * k + 3] = v[k].w; }
+}
+template <int KSZ, int U, int XW>
+__device__ __forceinline__ void ProbeLine<KSZ, U, XW>::load_quad(const gf_htab_desc &d, uint32_t h) {
+    constexpr int NW = Hdr<KSZ, XW>::NW;
+    static_assert(U * NW == 16, "load_quad: the home step must be one 64-B line");
+    const uint64_t here = __ballot(1);
+    if (((here >> (threadIdx.x & 60u)) & 0xFull) != 0xFull) { load(d, h); return; }
+    i = gf_home_slot(h, d.mask, d.slot_size);
+    uint32_t w[16];
+    coop_line64(d.slots ? d.slots + i * d.slot_size : nullptr, w);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int k = 0; k < NW; k++) hd[u].w[k] = w[u * NW + k];
+}
 
 // Outcome of a probe walk: the slot of key A, else of key B (is_b), else -1;
 // plus the EMPTY slot that ended the walk — where an absent key is inserted —

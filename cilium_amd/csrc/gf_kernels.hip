@@ -36,9 +36,6 @@ using namespace gfd;
 #define GF_DIAG 0      // diagnostic ablations (tools/diag.sh); 0 in the product build
 #endif
 // Tuning knobs of the flow-group kernel (tools/variants.sh sweeps them).
-#ifndef GF_PREFETCH_REC
-#define GF_PREFETCH_REC 0   // load the lane's next packet record while the current one runs
-#endif
 #ifndef GF_KEY_BITS
 #define GF_KEY_BITS 32      // bucket key: family bit + (GF_KEY_BITS-1) bits of the group hash
 #endif
@@ -61,6 +58,12 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #endif
 #ifndef GF_EG_MINW
 #define GF_EG_MINW 3        // k_eg_groups: min waves per SIMD (4 spills: 1.65 vs 1.60 ms, egress leg)
+#endif
+#ifndef GF_CT_COOP
+#define GF_CT_COOP 1        // CT4 home lines read by complete lane quads together (ProbeLine::load_quad)
+#endif
+#ifndef GF_CT_COOP6
+#define GF_CT_COOP6 0       // the same for CT6 (costs k_ing_groups<6> a wave per SIMD: 165 -> 170 VGPRs)
 #endif
 #ifndef GF_MEMO4
 #define GF_MEMO4 2          // policy decisions memoised per lane, IPv4 buckets
@@ -1375,7 +1378,11 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT4) ? X.ct4 : gf_htab_desc{};
     // the CT home line and the policy home line of the source identity go out together
     ProbeLine<14, GF_CT4_U, 4> cl;
+#if GF_CT_COOP
+    cl.load_quad(ct, key_hash<14, GF_HASH_CT>(t));
+#else
     cl.load(ct, key_hash<14, GF_HASH_CT>(t));
+#endif
     // (unless the lane's policy memo already answers the NEW/ESTABLISHED question)
     PolLine pl;
     const bool pre = r.src_identity &&
@@ -1458,7 +1465,11 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     t[9] = nh | (tfl << 8);
     const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT6) ? X.ct6 : gf_htab_desc{};
     ProbeLine<40, GF_CT6_U, 4> cl;
+#if GF_CT_COOP6
+    cl.load_quad(ct, key_hash<40, GF_HASH_CT>(t));
+#else
     cl.load(ct, key_hash<40, GF_HASH_CT>(t));
+#endif
     PolLine pl;
     const bool pre = r.src_identity &&
                      (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS &&
@@ -1725,7 +1736,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         if (lane == 0) base = atomicAdd(queue, 64u);
         base = __shfl(base, 0);
         if (base >= nb) break;
-        uint32_t t = base + lane;
+        const uint32_t t = base + lane;
         if (t >= nb) continue;
         const uint2 oc = order[t];
         const uint32_t b = oc.x, c = oc.y;
@@ -1750,16 +1761,9 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 #else
             if (k + 2 < c) in2 = perm[b + k + 2];
 #endif
-#if GF_PREFETCH_REC
-            gf_rec rn;
-            if (k + 1 < c) rn = rec[inx];
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
-            i = inx; inx = in2; r = rn;
-#else
             ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2;
             if (k + 1 < c) r = rec[i];
-#endif
         }
     }
     ln.acc.flush(X);
@@ -4325,8 +4329,8 @@ void host_mark(const char *what) { if (HostMarks *m = HostMarks::cur()) m->mark(
 namespace gf {
 struct CallCtx {
     std::mutex mu;
-    hipEvent_t ev = nullptr;       // recorded at the end of every call in this context
-    bool have = false;
+    hipEvent_t ev = nullptr;       // recorded at the end of every call in this context (made with the context)
+    std::atomic<bool> have{false}; // ev has been recorded once (read by other contexts' CallOrder)
     int ws_slot = 0;      // gf_policy_ingress_classify_batches: schedule k+1 builds in one while k runs
     std::map<const void *, std::shared_ptr<void>> bag;
     template <class T> T &get(const void *tag) {
@@ -4343,7 +4347,12 @@ CallCtx &ctx_for(hipStream_t s) {
     static std::map<hipStream_t, std::unique_ptr<CallCtx>> all;
     std::lock_guard<std::mutex> g(mu);
     auto &c = all[s];
-    if (!c) c = std::make_unique<CallCtx>();
+    if (!c) {
+        c = std::make_unique<CallCtx>();
+        // the call-order event exists before any other thread can see the context
+        // (device-scope release: the event orders device work between streams)
+        if (hipEventCreateWithFlags(&c->ev, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) c->ev = nullptr;
+    }
     return *c;
 }
 // The calling thread's context (map API paths outside a classify call: the
@@ -4433,7 +4442,7 @@ struct CallOrder {
         int nw = 0;
         for (OrderPt *o : pts) {
             CallCtx *c = o->last;
-            if (!c || c == me || !c->have) continue;
+            if (!c || c == me || !c->have.load(std::memory_order_acquire)) continue;
             bool seen = false;
             for (int k = 0; k < nw; k++) seen |= waited[k] == c;
             if (seen) continue;
@@ -4449,13 +4458,8 @@ struct CallOrder {
         return v;
     }
     ~CallOrder() {
-        // (device-scope release: the event orders device work between streams)
-        if (!me->ev && hipEventCreateWithFlags(&me->ev, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
-            me->ev = nullptr;
-            return;
-        }
-        if (hipEventRecord(me->ev, s) != hipSuccess) return;
-        me->have = true;
+        if (!me->ev || hipEventRecord(me->ev, s) != hipSuccess) return;
+        me->have.store(true, std::memory_order_release);
         for (OrderPt *o : pts) o->last = me;
     }
 };

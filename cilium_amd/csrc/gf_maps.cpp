@@ -11,12 +11,14 @@
 //   trie: prefixlen > max -> -EINVAL; NEW key when full -> -ENOSPC; lookup =
 //         longest stored prefix with len <= key.prefixlen that matches;
 //         get_next_key in post-order (more specific prefixes first).
-//   LRU_HASH never fails an insert (the kernel evicts instead): here an insert
-//   through the API or the datapath is accepted up to the slot array's 7/8
-//   load, and the deterministic LRU stand-in (gf_kernels.hip lru_evict, DESIGN.md
-//   §4) brings the map back under max_entries after the next classify call that
-//   binds it.  Between an API insert and that call GetMapInfo may report more
-//   than max_entries entries (documented deviation; tests/test_maps.py).
+//   LRU_HASH never fails an insert (the kernel evicts instead).  The conntrack
+//   maps (CT key/value shape, GF_VCODEC_CT) accept inserts through the API or the
+//   datapath up to the slot array's 7/8 load, and the deterministic LRU stand-in
+//   (gf_kernels.hip lru_evict) brings such a map back under
+//   max_entries after the next classify call that binds it as ct4 / ct6; between
+//   an API insert and that call GetMapInfo may report more than max_entries
+//   entries.  Every other LRU map has no eviction path and stops at max_entries
+//   with E2BIG (documented deviations; tests/test_maps.py).
 #include "gf_internal.h"
 #include <string.h>
 #include <errno.h>
@@ -320,6 +322,12 @@ int Map::push(hipStream_t s) {
     if ((r = d_slots.ensure(ht.nslots * ht.slot_size))) return r;
     if (ht.sstride && (r = d_vals.ensure(ht.nslots * ht.sstride))) return r;
     if ((r = d_count.ensure(8))) return r;
+    // LRU conntrack maps: the eviction sweep's 4-B code per slot (k_lru_hist ->
+    // k_lru_clusters), allocated with the slots so its cost shows at the push and
+    // a classify call never fails on it after its inserts are on the device
+    if (type == GF_MAP_TYPE_LRU_HASH && ht.codec == GF_VCODEC_CT && d_lrucodes.bytes < ht.nslots * 4 &&
+        (r = d_lrucodes.ensure(ht.nslots * 4)))
+        return r;
     if (ht.slots.empty()) {
         if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
         if (ht.sstride && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
@@ -498,12 +506,13 @@ int Map::dev_next_full(uint64_t start, int64_t &slot) {
     return 0;
 }
 
-// Element ceiling of a device insert: HASH maps end at max_entries (-E2BIG);
-// LRU maps (which the kernel never lets fail: it evicts) take entries up to the
-// slot array's 7/8 load and are brought back under max_entries by the eviction
-// sweep at the next batch boundary (gf_ct_evict).
+// Element ceiling of an insert: HASH maps end at max_entries (-E2BIG).  LRU
+// conntrack maps (which the kernel never lets fail: it evicts) take entries up to
+// the slot array's 7/8 load and are brought back under max_entries by the
+// eviction sweep of the next classify call that binds them (lru_evict); other LRU
+// maps have no eviction path here and end at max_entries like HASH maps.
 static uint64_t dev_insert_limit(const Map &m) {
-    return m.type == GF_MAP_TYPE_LRU_HASH ? m.ht.nslots / 8 * 7 : m.max_entries;
+    return m.type == GF_MAP_TYPE_LRU_HASH && m.ht.codec == GF_VCODEC_CT ? m.ht.nslots / 8 * 7 : m.max_entries;
 }
 
 static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t fl, bool &fallback) {

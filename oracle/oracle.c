@@ -227,11 +227,13 @@ int om_lookup(om_map *m, const void *key, void *value_out) {
 }
 
 /* Element ceiling of an insert.  HASH / LPM: max_entries (E2BIG / ENOSPC).
- * LRU_HASH: the kernel never fails an LRU insert (it evicts); with the LRU
- * stand-in above the table may exceed max_entries inside a batch, up to the 7/8
- * load of libgpuflow's CT slot array (4 x max_entries rounded up to a power of 2). */
+ * LRU_HASH: the kernel never fails an LRU insert (it evicts).  libgpuflow evicts
+ * only the conntrack maps (ipv4/ipv6_ct_tuple -> ct_entry, the maps a classify
+ * call binds, LRU stand-in above): those may exceed max_entries inside a batch, up
+ * to the 7/8 load of their slot array (4 x max_entries rounded up to a power of
+ * 2).  Any other LRU map has no eviction path there and stops at max_entries. */
 static uint32_t om_insert_limit(const om_map *m) {
-    if (m->type != OM_LRU_HASH) return m->max_entries;
+    if (m->type != OM_LRU_HASH || !((m->ksz == 14 || m->ksz == 40) && m->vsz == 48)) return m->max_entries;
     uint64_t want = 4ull * m->max_entries, p = 64;
     while (p < want) p <<= 1;
     return (uint32_t)(p / 8 * 7 > 0xffffffffull ? 0xffffffffu : p / 8 * 7);

@@ -159,15 +159,18 @@ def test_errors_and_limits():
     assert e.value.errno == errno.EINVAL
 
 
-@pytest.mark.parametrize("ksz,vsz", [(14, 48), (8, 24)])
+@pytest.mark.parametrize("ksz,vsz", [(14, 48), (40, 48), (8, 24)])
 def test_lru_insert_never_fails_below_slot_limit(ksz, vsz):
-    """BPF_MAP_TYPE_LRU_HASH never fails an insert in the kernel (it evicts).  The
-    stand-in accepts inserts past max_entries up to 7/8 of its 4 x max_entries slot
-    array and evicts at the next classify call that binds the map, so
-    GetMapInfo may exceed max_entries in between — the oracle's OMap has the same
-    ceiling; a HASH map of the same shape stops at max_entries with E2BIG."""
+    """BPF_MAP_TYPE_LRU_HASH never fails an insert in the kernel (it evicts).  For
+    the conntrack shapes (ipv4/ipv6_ct_tuple -> ct_entry) the stand-in accepts
+    inserts past max_entries up to 7/8 of its 4 x max_entries slot array and evicts
+    at the next classify call that binds the map as ct4 / ct6, so
+    GetMapInfo may exceed max_entries in between.  Any other LRU map has no
+    eviction path and stops at max_entries with E2BIG, like a HASH map.  The
+    oracle's OMap has the same ceilings."""
     maxe = 100
-    lim = 512 // 8 * 7                                      # pow2ceil(4 * 100) = 512 slots
+    ct_shape = ksz in (14, 40) and vsz == 48
+    lim = 512 // 8 * 7 if ct_shape else maxe               # pow2ceil(4 * 100) = 512 slots
     fd = bpf.CreateMap(bpf.BPF_MAP_TYPE_LRU_HASH, ksz, vsz, maxe)
     om = O.OMap(bpf.BPF_MAP_TYPE_LRU_HASH, ksz, vsz, maxe)
     rnd = random.Random(ksz)
@@ -176,7 +179,10 @@ def test_lru_insert_never_fails_below_slot_limit(ksz, vsz):
     for i, k in enumerate(keys):
         a, b = lib.gf_map_update_elem(fd, k, bytes(vsz), 0), om.update(k, bytes(vsz), 0)
         assert a == b == (0 if i < lim else -errno.E2BIG), (i, a, b)
-    assert bpf.GetMapInfo(fd).Entries == om.count() == lim > maxe
+    assert bpf.GetMapInfo(fd).Entries == om.count() == lim
+    assert (lim > maxe) == ct_shape
+    # replacing an existing key at the ceiling still succeeds
+    assert lib.gf_map_update_elem(fd, keys[0], bytes([1]) * vsz, 0) == 0 == om.update(keys[0], bytes([1]) * vsz, 0)
     h = bpf.CreateMap(bpf.BPF_MAP_TYPE_HASH, ksz, vsz, maxe)
     rc = [lib.gf_map_update_elem(h, k, bytes(vsz), 0) for k in keys[:maxe + 1]]
     assert rc[:maxe] == [0] * maxe and rc[maxe] == -errno.E2BIG

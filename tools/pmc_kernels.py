@@ -5,9 +5,18 @@ calls of the run and divided by the bench steps the process ran (warm-up +
 timed), so each number is "per step".
 
 Derived per kernel:
-  traffic_bytes      FETCH_SIZE + WRITE_SIZE (KB in the CSV) x 1024: the HBM-side
-                     bytes (FETCH_SIZE used raw: random 16-32 B loads are one 64-B
-                     request each, profiles/r1_pmc_calibration.json)
+  traffic_bytes      the L2 -> fabric bytes, from the request-size counters when
+                     the run has them (round 4 on): reads = 128 x RDREQ_128B + 32 x
+                     RDREQ_32B + 64 x the rest, writes = 64 x WRREQ_64B + 32 x the
+                     rest.  On gfx950 FETCH_SIZE prices a 128-B read request at 64 B
+                     (it counts TCC_BUBBLE, which stays 0 there), so it reports half
+                     of every line fill: random 16-B loads are 128-B requests
+                     (profiles/r4_primbench_pmc.txt).  Runs without those counters
+                     fall back to FETCH_SIZE + WRITE_SIZE (KB in the CSV) x 1024,
+                     uncorrected, and say so ("traffic_model").
+  reads / writes     per packet: 128-B line reads, partial (32-B) writes, full
+                     64-B writes, atomics (counted among the writes)
+  l2_hit_rate        TCC_HIT / (TCC_HIT + TCC_MISS)
   ea_requests        TCC_EA0_RDREQ_sum + TCC_EA0_WRREQ_sum (L2 -> fabric requests)
   wave_insts         SQ_INSTS_VALU + SQ_INSTS_SALU (wave-instructions)
   GRBM_GUI_ACTIVE    kept raw: / 8 XCDs / the kernel's time = its effective clock
@@ -66,13 +75,30 @@ def main():
         for k, v in c.items():
             ks[k].update(v)
         dps.update(d)
-    res = {"packets_per_step": pk, "steps_run": nsteps, "source": os.path.relpath(a.dir), "kernels": {}}
+    res = {"packets_per_step": pk, "steps_run": nsteps, "source": os.path.relpath(a.dir),
+           "build_id": b.get("build_id"), "kernels": {}}
     for k, c in sorted(ks.items()):
         e = {"dispatches_per_step": round(dps.get(k, 0), 3), "counters_per_step": {n: round(v, 1) for n, v in sorted(c.items())}}
-        if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+        if "TCC_EA0_RDREQ_128B_sum" in c and "TCC_EA0_WRREQ_64B_sum" in c:
+            rd, r128, r32 = c["TCC_EA0_RDREQ_sum"], c["TCC_EA0_RDREQ_128B_sum"], c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+            wr, w64, at = c.get("TCC_EA0_WRREQ_sum", 0.0), c["TCC_EA0_WRREQ_64B_sum"], c.get("TCC_EA0_ATOMIC_sum", 0.0)
+            rb = 128 * r128 + 32 * r32 + 64 * max(rd - r128 - r32, 0.0)
+            wb = 64 * w64 + 32 * max(wr - w64, 0.0)
+            e["traffic_model"] = "request sizes (128-B line reads, 32/64-B writes)"
+            e["read_bytes"], e["write_bytes"] = rb, wb
+            e["traffic_bytes"] = rb + wb
+            e["traffic_bytes_per_packet"] = (rb + wb) / pk if pk else None
+            if pk:
+                e["per_packet"] = {"line_reads": round(rd / pk, 4), "reads_128B": round(r128 / pk, 4),
+                                   "partial_writes": round(max(wr - w64 - at, 0.0) / pk, 4),
+                                   "full_writes_64B": round(w64 / pk, 4), "atomics": round(at / pk, 4)}
+        elif "FETCH_SIZE" in c or "WRITE_SIZE" in c:
             t = (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024
+            e["traffic_model"] = "FETCH_SIZE + WRITE_SIZE (uncorrected)"
             e["traffic_bytes"] = t
             e["traffic_bytes_per_packet"] = t / pk if pk else None
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
+            e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
         if "TCC_EA0_RDREQ_sum" in c:
             e["ea_requests"] = c["TCC_EA0_RDREQ_sum"] + c.get("TCC_EA0_WRREQ_sum", 0.0)
             e["ea_requests_per_packet"] = e["ea_requests"] / pk if pk else None
