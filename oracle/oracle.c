@@ -2517,3 +2517,27 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
     if (!snap_out) free(snap);
     free(skip); free(secctx); free(ifx); free(lxcid);
 }
+
+/* ------------------------------------------------------------------ */
+/* Parity helper (checker only): a 64-bit fingerprint of each (key, value) row of */
+/* a table dump, so two dumps of ~10^8 entries compare as sorted u64 arrays      */
+/* (oracle/parity.py compare_tables) instead of a lexicographic row sort.        */
+static uint64_t o_fmix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+void o_rows_fp(const uint8_t *keys, const uint8_t *vals, uint64_t n, uint32_t ksz, uint32_t vsz, uint64_t *out) {
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)ksz << 32) ^ vsz;
+        const uint8_t *rows[2] = {keys + i * ksz, vals + i * vsz};
+        const uint32_t len[2] = {ksz, vsz};
+        for (int r = 0; r < 2; r++) {
+            for (uint32_t o = 0; o < len[r]; o += 8) {
+                uint64_t w = 0;
+                memcpy(&w, rows[r] + o, len[r] - o < 8 ? len[r] - o : 8);
+                h = o_fmix64(h ^ w) + 0x632BE59BD9B4E019ull * (uint64_t)(r + 1);
+            }
+        }
+        out[i] = h;
+    }
+}

@@ -198,6 +198,7 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time);
 int o_ct_lru_cutoffs(om_map *m, uint32_t now, uint64_t *cut_c, uint64_t *cut_o);
 /* Deletes closing entries last used before cut_c and the others last used before cut_o. */
 uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o);
+void o_rows_fp(const uint8_t *keys, const uint8_t *vals, uint64_t n, uint32_t ksz, uint32_t vsz, uint64_t *out);
 
 /* Shard of a CT key (unordered address pair), exposed for pre-population. */
 uint32_t o_ct_pair_hash4(uint32_t a, uint32_t b);

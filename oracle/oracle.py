@@ -95,10 +95,31 @@ _s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
 _s("o_ct_lru_cutoffs", C.c_int, VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 _s("o_ct_gc2", C.c_uint32, VP, C.c_uint64, C.c_uint64)
+_s("o_rows_fp", None, VP, VP, C.c_uint64, C.c_uint32, C.c_uint32, VP)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
 _s("o_lpm4_iter_lookup", C.c_int, C.c_uint32, VP, C.c_int, C.c_uint32)
 _s("o_ct_pair_hash4", C.c_uint32, C.c_uint32, C.c_uint32)
+
+def rows_fp(keys, vals):
+    """64-bit fingerprints of the (key, value) rows of a dump (uint64[n])."""
+    k = np.ascontiguousarray(keys, np.uint8)
+    v = np.ascontiguousarray(vals, np.uint8)
+    out = np.empty(len(k), np.uint64)
+    n, ks, vs = len(k), k.shape[1] if k.ndim == 2 else 0, v.shape[1] if v.ndim == 2 else 0
+    if not n:
+        return out
+    nt = min(16, os.cpu_count() or 1, max(1, n // (1 << 20)))
+    step = (n + nt - 1) // nt
+
+    def part(a):                      # ctypes drops the GIL: the chunks run in parallel
+        b = min(n, a + step)
+        lib.o_rows_fp(k.ctypes.data + a * ks, v.ctypes.data + a * vs, b - a, ks, vs, out.ctypes.data + 8 * a)
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(nt) as ex:
+        list(ex.map(part, range(0, n, step)))
+    return out
+
 
 LB_OUT = np.dtype([("action", "u1"), ("reason", "u1"), ("slave", "<u2"), ("new_dport", "<u2"),
                    ("rev_nat", "<u2"), ("new_daddr4", "<u4")])

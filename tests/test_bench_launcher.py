@@ -80,3 +80,21 @@ def test_visible_gpus_without_hip(monkeypatch):
     assert bench.visible_gpus() == 2
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert bench.visible_gpus() == 0
+
+
+def test_egress_sharded_parity_equals_sequential():
+    """The egress leg's parity runs T oracle instances over closed flow-group
+    shares (bench.oracle_egress).  Rehearsed here with one sequential oracle in
+    the device's place, every packet's record and the union of the instances' CT
+    tables must equal the sequential run's: the shares really are closed for the
+    egress workload (local, service, world and tunnel flows, new flows every step)."""
+    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "egress", "--egress-flows", "65536",
+                        "--steps", "8"], env=env, capture_output=True, text=True, timeout=600, cwd="/tmp")
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    par = r["parity"]
+    assert "oracle instances over closed flow-group shares" in par["sample"], par
+    assert par["mismatches"] == 0 and par["ct_mismatches"] == 0, par
+    assert par["packets_compared"] == 65536 * par["steps"] and par["ct_entries_compared"] > 100_000

@@ -22,7 +22,7 @@
 //   requests per access (TCC_EA0_RDREQ / _32B / _128B, WRREQ / _64B, ATOMIC).
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/primbench.hip -o tools/_bin/primbench
-//   tools/_bin/primbench [matrix|legacy|all|tlb]
+//   tools/_bin/primbench [matrix|legacy|all|tlb|pol]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -154,6 +154,42 @@ __global__ __launch_bounds__(256) void k_mrd_coop(const uint4 *__restrict__ tab,
     const uint64_t line = mix((t >> 2) + salt) & lmask;
     const uint4 v = tab[line * 4 + (t & 3)];
     if ((v.x ^ v.w) == 0x9e3779b9u) sink[t & 1023] = v.y;
+}
+typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
+// request size of a random 16-B read under each cache policy: plain, nontemporal
+// (nt), agent-coherent (sc1), system-coherent (sc0 sc1), and the same on an
+// uncached (hipDeviceMallocUncached) allocation
+template <int POL>
+__global__ __launch_bounds__(256) void k_mrd_pol(const uint4 *__restrict__ tab, uint64_t lmask, uint32_t *sink, uint32_t salt) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint4 *p = tab + (mix(t + salt) & lmask) * 4;
+    uint4 v;
+    if constexpr (POL == 0) v = *p;
+    else if constexpr (POL == 1) { const vu4 x = __builtin_nontemporal_load((const vu4 *)p); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    else if constexpr (POL == 2) { vu4 x; asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory"); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    else { vu4 x; asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory"); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    if ((v.x ^ v.w) == 0x9e3779b9u) sink[t & 1023] = v.y;
+}
+// the same four policies on the cooperative 64-B line read
+template <int POL>
+__global__ __launch_bounds__(256) void k_mrd_coop_pol(const uint4 *__restrict__ tab, uint64_t lmask, uint32_t *sink, uint32_t salt) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint4 *p = tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3);
+    uint4 v;
+    if constexpr (POL == 0) v = *p;
+    else if constexpr (POL == 1) { const vu4 x = __builtin_nontemporal_load((const vu4 *)p); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    else if constexpr (POL == 2) { vu4 x; asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory"); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    else { vu4 x; asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory"); v = make_uint4(x[0], x[1], x[2], x[3]); }
+    if ((v.x ^ v.w) == 0x9e3779b9u) sink[t & 1023] = v.y;
+}
+// partial 16-B and full 64-B stores, nontemporal, and the cooperative full-line store
+template <int POL>
+__global__ __launch_bounds__(256) void k_mst_pol(uint4 *__restrict__ tab, uint64_t lmask, uint32_t salt) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const vu4 v = {(uint32_t)t, 1u, 2u, 3u};
+    if constexpr (POL == 0) __builtin_nontemporal_store(v, (vu4 *)(tab + (mix(t + salt) & lmask) * 4));
+    else if constexpr (POL == 1) *(vu4 *)(tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3)) = v;     // 4 lanes: one full line
+    else __builtin_nontemporal_store(v, (vu4 *)(tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3)));
 }
 // chain<L>: persistent lanes, L dependent streams per lane
 template <int L>
@@ -362,6 +398,51 @@ static void tlb(int cus) {
     CK(hipFree(sink));
 }
 
+// request sizes and rates by cache policy (random 16-B reads, cooperative 64-B
+// line reads, stores) at 2 GB and 16 GB, and on an uncached allocation
+static void policies(int cus) {
+    Timer T;
+    uint32_t *sink; CK(hipMalloc(&sink, 4096));
+    const uint64_t BIG = 16ull << 30, acc = 1ull << 24;
+    uint8_t *big; CK(hipMalloc(&big, BIG)); CK(hipMemset(big, 0, BIG));
+    uint4 *tab = reinterpret_cast<uint4 *>(big);
+    const char *pn[4] = {"plain", "nt", "sc1", "sc0 sc1"};
+    printf("# cache policies: 16.8M random reads per launch\n");
+    for (uint64_t fp : {2ull << 30, 16ull << 30}) {
+        double ms;
+        char n[64];
+#define POLRD(P) ms = T.best([&](int r) { hipLaunchKernelGGL(k_mrd_pol<P>, dim3(acc / 256), dim3(256), 0, 0, tab, fp / 64 - 1, sink, 7u * r); }); \
+        snprintf(n, 64, "rd  W= 16B %s", pn[P]); line(n, fp, ms, (double)acc, 1.0);
+        POLRD(0) POLRD(1) POLRD(2) POLRD(3)
+#define POLCO(P) ms = T.best([&](int r) { hipLaunchKernelGGL(k_mrd_coop_pol<P>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, sink, 9u * r); }); \
+        snprintf(n, 64, "rd  W= 64B coop %s", pn[P]); line(n, fp, ms, (double)acc, 1.0);
+        POLCO(0) POLCO(1) POLCO(2) POLCO(3)
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<0>, dim3(acc / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
+        line("st  W= 16B nt", fp, ms, (double)acc, 1.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<1>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
+        line("st  W= 64B coop (full line)", fp, ms, (double)acc, 1.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<2>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
+        line("st  W= 64B coop nt (full line)", fp, ms, (double)acc, 1.0);
+    }
+    CK(hipFree(big));
+    uint8_t *ub = nullptr;
+    const uint64_t UB = 2ull << 30;
+    if (hipExtMallocWithFlags((void **)&ub, UB, hipDeviceMallocUncached) == hipSuccess && ub) {
+        CK(hipMemset(ub, 0, UB));
+        uint4 *ut = reinterpret_cast<uint4 *>(ub);
+        printf("# the same on a 2-GB hipDeviceMallocUncached allocation\n");
+        double ms = T.best([&](int r) { hipLaunchKernelGGL(k_mrd_pol<0>, dim3(acc / 256), dim3(256), 0, 0, ut, UB / 64 - 1, sink, 7u * r); });
+        line("rd  W= 16B plain (uncached mem)", UB, ms, (double)acc, 1.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mrd_coop_pol<0>, dim3(acc * 4 / 256), dim3(256), 0, 0, ut, UB / 64 - 1, sink, 9u * r); });
+        line("rd  W= 64B coop (uncached mem)", UB, ms, (double)acc, 1.0);
+        CK(hipFree(ub));
+    } else {
+        (void)hipGetLastError();
+        printf("# hipDeviceMallocUncached: not available\n");
+    }
+    CK(hipFree(sink));
+}
+
 static void matrix(uint8_t *big, uint64_t big_bytes, int cus) {
     Timer T;
     uint32_t *sink; CK(hipMalloc(&sink, 4096));
@@ -424,6 +505,7 @@ int main(int argc, char **argv) {
     const int cus = p.multiProcessorCount;
     printf("# %s, %d CUs\n", p.name, cus);
     if (!strcmp(mode, "tlb")) { tlb(cus); return 0; }
+    if (!strcmp(mode, "pol")) { policies(cus); return 0; }
     const uint64_t BIG = (16ull << 30) + (256ull << 20);
     uint8_t *big; CK(hipMalloc(&big, BIG)); CK(hipMemset(big, 0, BIG));
     if (!strcmp(mode, "legacy") || !strcmp(mode, "all")) legacy(big, BIG);
