@@ -810,19 +810,25 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
     return r
 
 
-def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global",), local_world=1):
+def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global",), local_world=1, replay=True):
     """The oracle pipeline over the flow-group sample of every step (the flow group
     is the post-LB address pair, i.e. the stream's pair), records and the sampled
     pairs' CT entries compared; timed steps give the CPU baseline.  got[s] = (the
     frames step s classified, their sample bits, their records); sample bit 0: the packet's
-    post-LB pair is in the 1/div sample, bit 1: in the 1/(8 div) single-core subsample."""
+    post-LB pair is in the 1/div sample, bit 1: in the 1/(8 div) single-core subsample.
+    replay=False (div must be 1: the oracle holds the whole table): the oracle's LRU
+    stand-in derives its own eviction cutoffs from its own table, and its eviction
+    log must equal the device's (gf_ct_evict_log) entry for entry."""
     import torch
     from cilium_amd.datapath import PIPE_OUT
     from cilium_amd.synth import Packets
     from oracle.scenario import OracleDP
     T = cpu_threads(local_world)
     ref = OracleDP(sc, shards=T)
-    lru_replay(B, dp, ref)
+    if replay:
+        lru_replay(B, dp, ref)
+    else:
+        assert div == 1, "independent eviction needs the whole table"
     par = Parity(f"1/{div} of the address pairs (whole flow groups), every step incl. warm-up")
     done = single_n = 0
     tt = single_t = 0.0
@@ -859,7 +865,17 @@ def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global
                    f"{done} packets (flows of 1/{div} of the address pairs, the {K} timed steps after the same "
                    f"warm-up), {T} threads; single core: {single_n} packets of step {W}",
                    single_n / single_t / 1e6 if single_t else None)
-    return cpu, par.result(W + K)
+    res = par.result(W + K)
+    if not replay:
+        for name in ct_names:
+            dev_log = [tuple(int(x) for x in e) for e in B.evict_log(dp, name)]
+            ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get(name, [])]
+            res.setdefault("evictions", {})[name] = {
+                "evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log), "sweeps_oracle": len(ora_log),
+                "entries_evicted": int(sum(e[4] for e in dev_log)),
+                "oracle": "own cutoffs from its whole table (never saw the device log)"}
+    return cpu, res
+
 
 
 def config4_h2d(args, B, sc, fbs, outs, W, K):
@@ -928,15 +944,17 @@ def bench_config5(args, B):
     from oracle import parity as PY
     W, K = 3, 4
     t0 = time.time()
-    sc, P, meta = synth.config5_tables(n_pairs=args.pairs, prefill=args.ct6_prefill)
-    st = stream.Stream6Frames(P, meta, flows_per_step=1 << 20, device=B.dev)
+    sc, P, meta = synth.config5_tables(n_pairs=args.pairs, prefill=args.ct6_prefill, ct6_max=args.ct6_max)
+    st = stream.Stream6Frames(P, meta, flows_per_step=args.c5_flows, device=B.dev)
     S0 = 3
     rk, rv = st.reply_ct6_entries(S0 + W + K)
     ct6 = sc.maps["cilium_ct6_global"]
     ct6.keys, ct6.vals = synth.ct6_prefill(meta, rk, rv, sc.now)
     dp = B.datapath(sc)
     log(f"config5: tables + {sc.maps['cilium_ct6_global'].n()} pre-filled CT6 entries ({time.time() - t0:.1f}s)")
-    div = parity_div(args, 1) * 2
+    # the whole stream: the oracle holds the whole CT6, so its LRU stand-in evicts on
+    # its own cutoffs and its eviction log is compared with the device's
+    div = 1
     a6, b6 = st.pair_addrs6()
     pm = torch.from_numpy(PY.pair_sampled6(a6, b6, div).astype(np.uint8) |
                           (PY.pair_sampled6(a6, b6, div * 8).astype(np.uint8) << 1)).to(B.dev)
@@ -950,12 +968,12 @@ def bench_config5(args, B):
     names = [k for k in kern]
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct6_global",))
+        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct6_global",), replay=False)
     ct6_end, evictions = int(B.entries(dp, "cilium_ct6_global")), len(B.evict_log(dp, "cilium_ct6_global"))
     B.close(dp)
     return {"workload": "config5: IPv6 bpf_xdp check_v6 (10k v6_dyn /32-/127 + 100k v6_fix /128) -> bpf_netdev "
-                        "handle_ipv6 -> handle_policy ipv6_policy (ct_lookup6), CT6 max 10,485,760 (LRU) pre-filled "
-                        f"to {args.ct6_prefill}, 1M new flows/step",
+                        f"handle_ipv6 -> handle_policy ipv6_policy (ct_lookup6), CT6 max {args.ct6_max:,} (LRU) pre-filled "
+                        f"to {args.ct6_prefill}, {args.c5_flows} new flows/step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
             "ct6_entries_at_end": ct6_end,
@@ -1218,6 +1236,8 @@ def main():
     ap.add_argument("--ct-max", type=int, default=1 << 27,
                     help="CT max_entries (LRU): 134,217,728, above the entries a default run creates")
     ap.add_argument("--ct6-prefill", type=int, default=8_000_000)
+    ap.add_argument("--ct6-max", type=int, default=10_485_760, help="config 5: CT6 max_entries (LRU)")
+    ap.add_argument("--c5-flows", type=int, default=1 << 20, help="config 5: new flows per step")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the parity legs")
     ap.add_argument("--pipeline", action="store_true",
                     help="config 2: the steps through gf_policy_ingress_classify_batches (schedule overlap)")

@@ -98,3 +98,20 @@ def test_egress_sharded_parity_equals_sequential():
     assert "oracle instances over closed flow-group shares" in par["sample"], par
     assert par["mismatches"] == 0 and par["ct_mismatches"] == 0, par
     assert par["packets_compared"] == 65536 * par["steps"] and par["ct_entries_compared"] > 100_000
+
+
+def test_config5_independent_eviction_rehearsal():
+    """Config 5's parity leg runs the oracle over the whole stream without the
+    device's eviction log: its own LRU stand-in picks the cutoffs from its own
+    table, and the two logs are compared entry for entry (rehearsed: a small CT6
+    that evicts on most steps)."""
+    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5", "--pairs", "4096",
+                        "--ct6-prefill", "30000", "--ct6-max", "32768", "--c5-flows", "8192"],
+                       env=env, capture_output=True, text=True, timeout=600, cwd="/tmp")
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    ev = r["parity"]["evictions"]["cilium_ct6_global"]
+    assert ev["evict_log_equal"] and ev["sweeps_device"] >= 3 and ev["entries_evicted"] > 10_000, ev
+    assert r["parity"]["mismatches"] == 0 and r["parity"]["ct_mismatches"] == 0
