@@ -404,9 +404,21 @@ def compare_ct(B, par, dp, ref, name, ksz, div, pred=None):
 
 
 def cols_packets(cdict, idx, v6=False):
-    """Host Packets (raw frames) for the rows idx of a column batch."""
+    """Host Packets (raw frames) for the rows idx of a column batch (idx None: all).
+    IPv4 frames are built on the device (stream.device_frames with TTL 0, byte for
+    byte stream.to_frames) and copied once."""
     from cilium_amd import stream
     from cilium_amd.synth import Packets
+    if not v6 and cdict["len"].is_cuda:
+        sub = cdict if idx is None else {k: v[idx] for k, v in cdict.items()}
+        f, lens = stream.device_frames(sub, ttl=0)
+        h = {k: sub[k].cpu().numpy() for k in ("src_identity", "ifindex", "lxc_id", "tc_index")}
+        to_u = {np.dtype(np.int32): np.uint32, np.dtype(np.int16): np.uint16}
+        h = {k: (v.view(to_u[v.dtype]) if v.dtype in to_u else v) for k, v in h.items()}
+        return Packets(f.cpu().numpy(), lens.cpu().numpy().view(np.uint32), h["src_identity"], h["ifindex"],
+                       h["lxc_id"], h["tc_index"])
+    if idx is None:
+        idx = slice(None)
     c = {k: v[idx].cpu().numpy() for k, v in cdict.items()}
     to_u = {np.dtype(np.int32): np.uint32, np.dtype(np.int16): np.uint16}
     c = {k: (v.view(to_u[v.dtype]) if v.dtype in to_u else v) for k, v in c.items()}
@@ -469,16 +481,6 @@ def bench_config2(args, B, rank, world, local_world=1):
     avg_ms = ki[1] / max(ki[0], 1)
     ab_per_launch = float(lc[270]) / max(K, 1)
     achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = traffic_src = None
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
-    if pmc and not B.rehearsal:
-        try:
-            j = json.load(open(pmc[-1]))
-            if j.get("kernel") == "k_ing_groups" and j.get("traffic_bytes_per_launch"):
-                traffic = j["traffic_bytes_per_launch"] * (batches[W].n / float(j["packets_per_launch"]))
-                traffic_src = os.path.relpath(pmc[-1], ROOT)
-        except Exception:
-            traffic = None
     cpu = par = None
     if not args.no_cpu:
         # every rank checks its own flow groups; the CPU baseline is rank 0's at N=1 only
@@ -518,8 +520,7 @@ def bench_config2(args, B, rank, world, local_world=1):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
+            "traffic": None,
             "algorithmic_bytes_per_launch": ab_per_launch,
             "avg_launch_ms": round(avg_ms, 4),
         },
@@ -568,12 +569,21 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
     par = Parity(f"1/{div} of the address pairs (whole flow groups), every step incl. warm-up")
     done = single_n = 0
     tt = single_t = 0.0
-    for s in range(W + K):
-        idx = torch.nonzero(samp[ps[s]]).squeeze(1)
+
+    def host_step(s):                                   # frames + GPU records of step s, on the host
+        idx = None if div == 1 else torch.nonzero(samp[ps[s]]).squeeze(1)
         pk = cols_packets(batches[s].cdict, idx)
-        gout = outs[s][idx].cpu().numpy().view(ING_OUT).ravel()
+        go = (outs[s] if idx is None else outs[s][idx]).cpu().numpy().view(ING_OUT).ravel()
+        m1 = (one[ps[s]] if idx is None else one[ps[s]][idx]).cpu().numpy() if s == W else None
+        return pk, go, m1
+    import concurrent.futures as cf
+    prep = cf.ThreadPoolExecutor(1)                     # step s+1 is prepared while the oracle runs step s
+    nxt = prep.submit(host_step, 0)
+    for s in range(W + K):
+        pk, gout, m1 = nxt.result()
+        if s + 1 < W + K:
+            nxt = prep.submit(host_step, s + 1)
         if s == W:
-            m1 = one[ps[s]][idx].cpu().numpy()
             a = time.perf_counter()
             r1 = ref.ingress(_sub(pk, np.nonzero(m1)[0]), sc.now + s, threads=1, lru=False)
             single_t = time.perf_counter() - a
@@ -594,6 +604,7 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
         if (s + 1) % 8 == 0:
             log(f"parity: {s + 1} of {W + K} steps, {par.packets} packets compared, {par.bad} mismatches "
                 f"({time.time() - t0:.1f}s)")
+    prep.shutdown()
     compare_ct(B, par, dp, ref, "cilium_ct4_global", 14, div)
     log(f"cpu baseline + parity: {par.packets} packets compared, {par.bad} mismatches; CT {par.ct}; "
         f"{done} packets in {tt:.2f}s on {T} threads ({time.time() - t0:.1f}s)")
@@ -1105,54 +1116,53 @@ def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
 EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_config5, "egress": bench_egress}
 
 
-def add_traffic(cfg, r):
-    """roofline.traffic of configuration `cfg` from its committed PMC summary
-    (profiles/*pmc_summary_c<cfg>.json: FETCH_SIZE + WRITE_SIZE per launch of the
-    roofline kernels, tools/pmc_summary.py), scaled per packet to this run."""
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_summary_c{cfg}.json")))
-    if not pmc or "roofline" not in r:
-        return r
-    try:
-        j = json.load(open(pmc[-1]))
-        ppl = float(j["packets_per_launch"])
-        if ppl > 0 and j.get("traffic_bytes_per_launch"):
-            r["roofline"]["traffic"] = j["traffic_bytes_per_launch"] * (r["packets_per_step"] / ppl)
-            r["roofline"]["traffic_source"] = os.path.relpath(pmc[-1], ROOT)
-    except Exception:
-        pass
-    return r
-
-
-# Issue and request ceilings the roofline objects are also priced against
-# (the byte roofline alone names the wrong bound for request- or issue-bound
-# kernels, DESIGN.md §6):
-#   issue:    VALU + SALU wave-instructions per second / (256 CUs x 4 SIMDs x 2.4 GHz)
-#             (one wave-instruction per SIMD per clock; a wave64 VALU occupies its
-#             SIMD-32 for 2 clocks, so "valu_busy" = 2 x VALU / the same peak)
-#   requests: L2 -> fabric requests (TCC_EA0_RDREQ + WRREQ) per second / the random
-#             64-B request rate measured on MI355X by tools/primbench.hip
-#             (profiles/r1_primbench.txt: 39.6-42.4 G random 16-B loads/s)
+# Issue and memory-operation ceilings the roofline objects are also priced against
+# (the byte roofline alone names the wrong bound for a kernel of random accesses,
+# DESIGN.md §6), all measured on MI355X by tools/primbench.hip
+# (profiles/r4_primbench.txt, request sizes in profiles/r4_primbench_pmc.txt):
+#   issue:   VALU + SALU wave-instructions per second / (256 CUs x 4 SIMDs x 2.4 GHz)
+#            ("valu_busy" = 2 x VALU / the same: a wave64 VALU holds its SIMD-32 2 clocks)
+#   memory:  per operation kind, its rate over the kernel's launch time against the
+#            best rate of that kind measured for random addresses over a 16-GB table:
+#            128-B line reads (every random read fills a whole 128-B L2 line) 54 G/s
+#            (nontemporal 16-B loads), partial (32-B) writes 21.7 G/s, full 64-B line
+#            writes 60.5 G/s (four lanes one 16-B store each), u64 atomics 17.3 G/s.
+#            frac = the largest of the four: the kind closest to its own ceiling.
 ISSUE_PEAK = 256 * 4 * 2.4e9
-REQUEST_PEAK = 40.0e9
+MEM_CEIL = {"line_reads": 54.0e9, "partial_writes": 21.7e9, "full_writes_64B": 60.5e9, "atomics": 17.3e9}
+PMC_ROUND = "r4"          # the round whose per-kernel PMC summaries price this run (built from the same sources)
 PMC_KERNELS = {"2": ["k_ing_groups"], "1": ["k_xdp", "k_xdp_lds"], "3": ["k_lb"]}   # else: every kernel
 
 
 def add_bounds(cfg, r):
-    """roofline.issue / roofline.requests of configuration `cfg` from its committed
-    per-kernel PMC summary (profiles/*pmc_kernels_c<cfg>.json, tools/pmc_kernels.py),
-    scaled per packet to this run and divided by this run's live launch time."""
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_kernels_c{cfg}.json")))
+    """roofline.traffic / .issue / .memory of configuration `cfg` from this round's
+    per-kernel PMC summary (profiles/<PMC_ROUND>_pmc_kernels_c<cfg>.json,
+    tools/pmc_kernels.py), scaled per packet to this run and divided by this run's
+    live launch time.  Only a summary built from the library this run loaded
+    (same gf_build_id) is used; otherwise the bound is marked stale."""
     rf = r.get("roofline")
-    if not pmc or not rf or not rf.get("avg_launch_ms"):
+    path = os.path.join(ROOT, "profiles", f"{PMC_ROUND}_pmc_kernels_c{cfg}.json")
+    if not rf or not rf.get("avg_launch_ms"):
+        return r
+    if not os.path.exists(path):
+        rf["bounds_source"] = f"missing: {os.path.relpath(path, ROOT)}"
         return r
     try:
-        j = json.load(open(pmc[-1]))
+        j = json.load(open(path))
+        src = os.path.relpath(path, ROOT)
+        try:
+            from cilium_amd import _lib
+            built = _lib.BUILD_ID
+        except Exception:
+            built = None
+        if j.get("build_id") != built:
+            rf["bounds_stale"] = {"source": src, "summary_build_id": j.get("build_id"), "library_build_id": built}
+            return r
         names = PMC_KERNELS.get(cfg) or [k for k in j["kernels"] if k.startswith("k_") or k == "rocprim"]
         ks = [j["kernels"][k] for k in names if k in j["kernels"]]
         pk = r.get("packets_per_step") or r.get("config", {}).get("packets_per_step_per_gpu")
         scale = float(pk) / float(j["packets_per_step"])
         t = rf["avg_launch_ms"] * 1e-3
-        src = os.path.relpath(pmc[-1], ROOT)
         cs = lambda n: sum(k["counters_per_step"].get(n, 0.0) for k in ks) * scale
         valu, salu = cs("SQ_INSTS_VALU"), cs("SQ_INSTS_SALU")
         if valu or salu:
@@ -1160,17 +1170,29 @@ def add_bounds(cfg, r):
                            "valu_busy": round(2 * valu / t / ISSUE_PEAK, 4),
                            "wave_insts_per_s": (valu + salu) / t, "peak": ISSUE_PEAK,
                            "wave_insts_per_64_packets": round((valu + salu) * 64 / float(pk), 1), "source": src}
-        # traffic: FETCH_SIZE + WRITE_SIZE of the same kernels in the same summary (the
-        # round's own passes), per launch of this run
         tb = sum(k.get("traffic_bytes_per_packet") or 0.0 for k in ks) * float(pk)
         if tb:
             rf["traffic"] = tb
             rf["traffic_source"] = src
-        req = cs("TCC_EA0_RDREQ_sum") + cs("TCC_EA0_WRREQ_sum")
-        if req:
-            rf["requests"] = {"frac": round(req / t / REQUEST_PEAK, 4), "per_s": req / t, "peak": REQUEST_PEAK,
-                              "per_packet": round(req / float(pk), 3), "source": src,
-                              "peak_source": "profiles/r1_primbench.txt"}
+            rf["traffic_model"] = ks[0].get("traffic_model") if ks else None
+            hits = cs("TCC_HIT_sum")
+            miss = cs("TCC_MISS_sum")
+            if hits + miss:
+                rf["l2_hit_rate"] = round(hits / (hits + miss), 4)
+        per = {}
+        for k in ks:
+            for n_, v in (k.get("per_packet") or {}).items():
+                per[n_] = per.get(n_, 0.0) + v
+        if per:
+            mem = {"source": src, "ceilings_source": "profiles/r4_primbench.txt", "per_packet": per}
+            fr = {}
+            for n_, ceil in MEM_CEIL.items():
+                rate = per.get(n_, 0.0) * float(pk) / t
+                fr[n_] = {"per_s": rate, "ceiling": ceil, "frac": round(rate / ceil, 4)}
+            mem["kinds"] = fr
+            bind = max(fr, key=lambda n_: fr[n_]["frac"])
+            mem["frac"], mem["binding"] = fr[bind]["frac"], bind
+            rf["memory"] = mem
     except Exception as e:                                   # reported, never silently dropped
         rf["bounds_error"] = f"{type(e).__name__}: {e}"
     return r
@@ -1282,7 +1304,7 @@ def main():
         for k, fn in extra.items():
             t0 = time.time()
             try:
-                res["configs"][k] = add_bounds(k, add_traffic(k, fn(args, B)))
+                res["configs"][k] = add_bounds(k, fn(args, B))
             except Exception as e:                       # reported, never silently dropped
                 if world > 1:
                     raise                                # a rank cannot skip a collective the others run
@@ -1298,7 +1320,7 @@ def main():
             r = bench_config4(args, B, rank, world, "owned", local_world)
         else:
             r = EXTRA[args.config](args, B)
-        r = add_bounds(args.config, add_traffic(args.config, r))
+        r = add_bounds(args.config, r)
         res = {"metric": METRIC, "value": r["mpps"], "unit": "Mpps", "n_gpus": world, "steps": r["steps"],
                "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "u32", "data": "synthetic",

@@ -65,6 +65,19 @@ __device__ __forceinline__ void gstore(void *p, T v) {
         *(GF_GLOBAL gf_u32x4 *)p = w;
     }
 }
+// Nontemporal 16-B load (global_load_dwordx4 ... nt): a random line read this
+// way ran at 54 G lines/s over a 16-GB table against 39 G/s plain
+// (profiles/r4_primbench.txt, "cache policies").
+__device__ __forceinline__ uint4 gload_nt16(const void *p) {
+    const gf_u32x4 v = __builtin_nontemporal_load((const GF_GLOBAL gf_u32x4 *)p);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+#ifndef GF_CT_NT
+#define GF_CT_NT 0          // coop_line64 reads with nontemporal loads
+#endif
+#ifndef GF_HDR_NT
+#define GF_HDR_NT 0         // every probe header load (Hdr::load) nontemporal
+#endif
 #ifndef GF_CAS_SCOPE
 #define GF_CAS_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #endif
@@ -117,7 +130,7 @@ struct Hdr {
     __device__ __forceinline__ void load(const uint8_t *s) {
 #pragma unroll
         for (int k = 0; k < NW; k += 4) {
-            uint4 v = gload<uint4>(s + 4 * k);
+            uint4 v = GF_HDR_NT ? gload_nt16(s + 4 * k) : gload<uint4>(s + 4 * k);
             w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
         }
     }
@@ -234,7 +247,8 @@ __device__ __forceinline__ void coop_line64(const uint8_t *p, uint32_t (&w)[16])
     uint4 v[4];
     const uint8_t *pq[4] = {quad_bcast_ptr<0>(p), quad_bcast_ptr<1>(p), quad_bcast_ptr<2>(p), quad_bcast_ptr<3>(p)};
 #pragma unroll
-    for (int q = 0; q < 4; q++) v[q] = pq[q] ? gload<uint4>(pq[q] + 16 * j) : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < 4; q++)
+        v[q] = pq[q] ? (GF_CT_NT ? gload_nt16(pq[q] + 16 * j) : gload<uint4>(pq[q] + 16 * j)) : make_uint4(0, 0, 0, 0);
     // lane j holds chunk j of quad lane q's line in v[q]; wanted: chunk k of its own
     // line in v[k], i.e. out[j][k] = in[k][j].  Stage b (b = 1, 2): keep v[k] where
     // bit b of k equals that of j, else take lane j^b's v[k^b].

@@ -62,6 +62,9 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_CT_COOP
 #define GF_CT_COOP 1        // CT4 home lines read by complete lane quads together (ProbeLine::load_quad)
 #endif
+#ifndef GF_REC_NT
+#define GF_REC_NT 0         // k_ing_groups: packet records read with nontemporal loads
+#endif
 #ifndef GF_CT_COOP6
 #define GF_CT_COOP6 0       // the same for CT6 (costs k_ing_groups<6> a wave per SIMD: 165 -> 170 VGPRs)
 #endif
@@ -1692,6 +1695,17 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     }
 }
 
+__device__ __forceinline__ gf_rec ld_rec(const gf_rec *rec, uint32_t i) {
+    if constexpr (GF_REC_NT) {
+        const uint4 a = gload_nt16(rec + i), b = gload_nt16(reinterpret_cast<const uint8_t *>(rec + i) + 16);
+        gf_rec r;
+        __builtin_memcpy(&r, &a, 16);
+        __builtin_memcpy(reinterpret_cast<uint8_t *>(&r) + 16, &b, 16);
+        return r;
+    } else {
+        return rec[i];
+    }
+}
 __device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, int added, uint32_t *ct_count,
                                             uint32_t *lds_added) {
     if (X.strict & fam_bit) return;
@@ -1742,7 +1756,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         const uint32_t b = oc.x, c = oc.y;
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
-        gf_rec r = rec[i];
+        gf_rec r = ld_rec(rec, i);
         ln.rc.slot = ~0u;                                // a new bucket: new flow groups
 #if GF_PERM_VEC
         uint4 pw = make_uint4(0, 0, 0, 0);               // perm[j & ~3 .. +3], j = b + k + 2
@@ -1763,7 +1777,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 #endif
             ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2;
-            if (k + 1 < c) r = rec[i];
+            if (k + 1 < c) r = ld_rec(rec, i);
         }
     }
     ln.acc.flush(X);

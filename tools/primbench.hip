@@ -191,6 +191,17 @@ __global__ __launch_bounds__(256) void k_mst_pol(uint4 *__restrict__ tab, uint64
     else if constexpr (POL == 1) *(vu4 *)(tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3)) = v;     // 4 lanes: one full line
     else __builtin_nontemporal_store(v, (vu4 *)(tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3)));
 }
+// a CT hit's shape: the 64-B line read cooperatively (4 lanes), then written back:
+// MODE 0 read only, 1 one 16-B partial store into it, 2 the whole line (4 lanes x 16 B)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mhit(uint4 *__restrict__ tab, uint64_t lmask, uint32_t *sink, uint32_t salt) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint4 *p = tab + (mix((t >> 2) + salt) & lmask) * 4 + (t & 3);
+    uint4 v = *p;
+    if (MODE == 1 && (t & 3) == 1) *p = make_uint4(v.x + 1, v.y, v.z + 64, v.w);
+    if (MODE == 2) *p = make_uint4(v.x + 1, v.y, v.z + 64, v.w);
+    if ((v.x ^ v.w) == 0x9e3779b9u) sink[t & 1023] = v.y;
+}
 // chain<L>: persistent lanes, L dependent streams per lane
 template <int L>
 __global__ __launch_bounds__(256) void k_mchain(const uint4 *__restrict__ tab, uint64_t lmask, uint32_t iters,
@@ -419,6 +430,12 @@ static void policies(int cus) {
         POLCO(0) POLCO(1) POLCO(2) POLCO(3)
         ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<0>, dim3(acc / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
         line("st  W= 16B nt", fp, ms, (double)acc, 1.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mhit<0>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, sink, 5u * r); });
+        line("hit: coop 64B read", fp, ms, (double)acc, 1.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mhit<1>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, sink, 5u * r); });
+        line("hit: coop read + 16B partial store", fp, ms, (double)acc, 2.0);
+        ms = T.best([&](int r) { hipLaunchKernelGGL(k_mhit<2>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, sink, 5u * r); });
+        line("hit: coop read + 64B line store", fp, ms, (double)acc, 2.0);
         ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<1>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
         line("st  W= 64B coop (full line)", fp, ms, (double)acc, 1.0);
         ms = T.best([&](int r) { hipLaunchKernelGGL(k_mst_pol<2>, dim3(acc * 4 / 256), dim3(256), 0, 0, tab, fp / 64 - 1, 3u * r); });
