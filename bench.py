@@ -129,6 +129,14 @@ class Gpu:
         lib.gf_prof_enable(0)
         return self.c, {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
 
+    def lru_stats(self, dp, name):
+        import ctypes as C
+        from cilium_amd._lib import lib
+        out = (C.c_uint64 * 4)()
+        if lib.gf_ct_lru_stats(dp.fd[name], out):
+            return None
+        return {"sweeps": int(out[0]), "partial": int(out[1]), "lines_read": int(out[2]), "fallbacks": int(out[3])}
+
     def evict_log(self, dp, name):
         from cilium_amd._lib import lib, gf_ct_evict_rec
         recs = (gf_ct_evict_rec * 4096)()
@@ -196,6 +204,9 @@ class Rehearsal:
 
     def evict_log(self, dp, name):
         return list(dp.ref.lru_log.get(name, []))
+
+    def lru_stats(self, dp, name):
+        return {"sweeps": len(dp.ref.lru_log.get(name, [])), "partial": 0, "lines_read": 0, "fallbacks": 0}
 
     def table_sampled(self, dp, name, ksz, div, pred):
         from oracle import parity as PY
@@ -449,20 +460,24 @@ def bench_config2(args, B, rank, world, local_world=1):
     # stream step S0 = 3 so that every launch, warm-up included, is a full steady-state
     # batch (the rocprof --stats average over all launches then matches the timed one).
     S0 = 3
-    rk, rv = st.reply_ct_entries(S0 + W + K)
+    # the long-horizon continuation (N = 1): steps W + K .. L - 1 run after the headline's
+    # timed steps on the same datapath, timed on their own, into the LRU sweeps a node
+    # reaches once its CT holds max_entries
+    L = max(args.long_steps, W + K) if world == 1 else W + K
+    rk, rv = st.reply_ct_entries(S0 + L)
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
     log(f"rank {rank}: tables {sum(m.n() for m in sc.maps.values())} entries, {len(rk)} pre-inserted CT, "
         f"{len(st.own)} owned pairs ({time.time() - t0:.1f}s)")
     dp = B.datapath(sc)
     batches, ps = [], []
-    for s in range(W + K):
+    for s in range(L):
         cols, p, n = st.step(S0 + s)
         batches.append(ColBatch(cols, n, B.dev))
         ps.append(p)
     # one output buffer per step: the parity leg reads every step's records afterwards
     outs = [torch.empty((b.n, 8), dtype=torch.uint8, device=B.dev) for b in batches]
     B.sync()
-    log(f"rank {rank}: generated {W + K} steps ({time.time() - t0:.1f}s)")
+    log(f"rank {rank}: generated {L} steps ({time.time() - t0:.1f}s)")
     now = sc.now
     if not args.pipeline:
         elapsed, c, lc, kern = timed(B, lambda s: dp.ingress(batches[s], now + s, out=outs[s]), W, K, world)
@@ -473,6 +488,18 @@ def bench_config2(args, B, rank, world, local_world=1):
         elapsed, c, lc, kern = timed(B, lambda a, b: dp.ingress_batches(batches[a:b], [now + s for s in range(a, b)],
                                                                          outs[a:b]), W, K, world, ranged=True)
     total_pkts = int(c[268])
+    long_h = None
+    if L > W + K and not args.pipeline:
+        C_ = L - W - K
+        el2, c2, _, kern2 = timed(B, lambda s: dp.ingress(batches[W + K + s], now + W + K + s, out=outs[W + K + s]),
+                                  0, C_, world)
+        lp = total_pkts + int(c2[268])
+        long_h = {"steps": K + C_, "after_warmup": W, "mpps": round(lp / (elapsed + el2) / 1e6, 3),
+                  "ms_per_step": round((elapsed + el2) / (K + C_) * 1e3, 4),
+                  "continuation": {"steps": C_, "mpps": round(int(c2[268]) / el2 / 1e6, 3),
+                                   "kernels_ms_per_step": kms(kern2)},
+                  "lru_sweeps": B.lru_stats(dp, "cilium_ct4_global")}
+        log(f"long horizon: {long_h['mpps']} Mpps over {K + C_} steps (continuation {long_h['continuation']['mpps']})")
     local_pkts = sum(batches[s].n for s in range(W, W + K))
     if not os.environ.get("GPUFLOW_DIAG_LIB"):
         assert int(lc[268]) == local_pkts, (int(lc[268]), local_pkts)
@@ -484,7 +511,7 @@ def bench_config2(args, B, rank, world, local_world=1):
     cpu = par = None
     if not args.no_cpu:
         # every rank checks its own flow groups; the CPU baseline is rank 0's at N=1 only
-        cpu, par = oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world, local_world)
+        cpu, par = oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world, local_world, L)
         if world > 1:
             cpu = None
     par = reduce_parity(B, par, rank, world)
@@ -513,6 +540,7 @@ def bench_config2(args, B, rank, world, local_world=1):
             "ct_entries_at_end": ct_end,
             "parallelism": f"dp{world} (flow-group sharded, tables replicated, CT partitioned)",
         },
+        "long_horizon": long_h and dict(long_h, ratio_to_headline=round(long_h["mpps"] / (total_pkts / elapsed / 1e6), 4)),
         "roofline": {
             "bound": "hbm",
             "kernel": "k_ing_groups (CT+policy stage: handle_policy over every packet of the step)",
@@ -547,7 +575,7 @@ class ColBatch:
         return self._cols(self)
 
 
-def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_world=1):
+def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_world=1, L=None):
     """The CPU restatement (oracle, multi-threaded, RSS-style partition by flow
     group) over the flow-group sample of every step (warm-up included): its
     records must equal the GPU's for every sampled packet and, after the last
@@ -560,9 +588,11 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
     from oracle.scenario import OracleDP
     from oracle import parity as PY
     T, div = cpu_threads(local_world), parity_div(args, world)
+    L = L or W + K
     t0 = time.time()
     ref = OracleDP(sc, shards=T)
-    lru_replay(B, dp, ref)
+    if div > 1:
+        lru_replay(B, dp, ref)          # a sample cannot derive the whole table's cutoffs
     sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
     samp = torch.from_numpy(PY.pair_sampled(sa, da, div)).to(st.device)
     one = torch.from_numpy(PY.pair_sampled(sa, da, div * 8)).to(st.device)
@@ -579,9 +609,9 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
     import concurrent.futures as cf
     prep = cf.ThreadPoolExecutor(1)                     # step s+1 is prepared while the oracle runs step s
     nxt = prep.submit(host_step, 0)
-    for s in range(W + K):
+    for s in range(L):
         pk, gout, m1 = nxt.result()
-        if s + 1 < W + K:
+        if s + 1 < L:
             nxt = prep.submit(host_step, s + 1)
         if s == W:
             a = time.perf_counter()
@@ -597,12 +627,12 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
         else:
             a = time.perf_counter()
             r = ref.ingress(pk, sc.now + s, threads=T)
-            if s >= W:
+            if W <= s < W + K:
                 tt += time.perf_counter() - a
                 done += pk.n
         par.records(gout, r, f"step {s}")
         if (s + 1) % 8 == 0:
-            log(f"parity: {s + 1} of {W + K} steps, {par.packets} packets compared, {par.bad} mismatches "
+            log(f"parity: {s + 1} of {L} steps, {par.packets} packets compared, {par.bad} mismatches "
                 f"({time.time() - t0:.1f}s)")
     prep.shutdown()
     compare_ct(B, par, dp, ref, "cilium_ct4_global", 14, div)
@@ -613,7 +643,15 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
                    f"{K} timed steps after the same {W} warm-up steps), oracle restatement, RSS-style flow-group "
                    f"partition over {T} threads; single core: {single_n} packets of step {W}",
                    single_n / single_t / 1e6 if single_t else None)
-    return cpu, par.result(W + K)
+    res = par.result(L)
+    if div == 1:
+        dev_log = [tuple(int(x) for x in e) for e in B.evict_log(dp, "cilium_ct4_global")]
+        ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get("cilium_ct4_global", [])]
+        res["evictions"] = {"cilium_ct4_global": {
+            "evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log), "sweeps_oracle": len(ora_log),
+            "entries_evicted": int(sum(e[4] for e in dev_log)),
+            "oracle": "own cutoffs from its whole table (never saw the device log)"}}
+    return cpu, res
 
 
 def parity_div(args, world):
@@ -1258,6 +1296,8 @@ def main():
     ap.add_argument("--ct-max", type=int, default=1 << 27,
                     help="CT max_entries (LRU): 134,217,728, above the entries a default run creates")
     ap.add_argument("--ct6-prefill", type=int, default=8_000_000)
+    ap.add_argument("--long-steps", type=int, default=64,
+                    help="config 2 at N=1: steps in all (warm-up + timed + a timed continuation into LRU eviction)")
     ap.add_argument("--ct6-max", type=int, default=10_485_760, help="config 5: CT6 max_entries (LRU)")
     ap.add_argument("--c5-flows", type=int, default=1 << 20, help="config 5: new flows per step")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the parity legs")

@@ -19,6 +19,7 @@
 #include <string.h>
 #include <errno.h>
 #include <pthread.h>
+#include <sys/mman.h>
 
 /* ------------------------------------------------------------------ */
 /* kernel-side constants                                               */
@@ -86,14 +87,17 @@
 /* ------------------------------------------------------------------ */
 /* maps: exact-match hash (kernel htab) and LPM trie                   */
 /* ------------------------------------------------------------------ */
+/* A shard's slots are records [state | key | pad | value | pad] (one cache line
+ * for the CT shapes), so a probe step touches one line, not three arrays. */
 typedef struct om_shard {
-    uint8_t *keys, *vals, *state;   /* state: 0 empty, 1 full, 2 deleted */
+    uint8_t *rec;                   /* cap records of om_map.rs bytes; state: 0 empty, 1 full, 2 deleted */
     uint64_t cap, used, tomb;
     pthread_mutex_t mu;
 } om_shard;
 
 struct om_map {
     uint32_t type, ksz, vsz, max_entries, nshards;
+    uint32_t koff, rs;              /* value offset in a record, record stride */
     uint32_t count;                 /* total elements (atomic across shards) */
     uint8_t lens_present[129];      /* LPM: prefix lengths present (count) */
     uint32_t lens_cnt[129];
@@ -107,6 +111,22 @@ static uint64_t fnv1a(const uint8_t *p, uint32_t n) {
 }
 
 static int is_lpm(const om_map *m) { return m->type == OM_LPM_TRIE; }
+#define SH_ST(m, h, i) ((h)->rec[(uint64_t)(i) * (m)->rs])
+#define SH_KEY(m, h, i) ((h)->rec + (uint64_t)(i) * (m)->rs + 1)
+#define SH_VAL(m, h, i) ((h)->rec + (uint64_t)(i) * (m)->rs + (m)->koff)
+/* zeroed record storage; large arrays are asked for transparent huge pages (the
+ * bench's CT shards reach gigabytes: fewer TLB misses per probe) */
+static uint8_t *sh_alloc(uint64_t bytes) {
+    if (bytes < (4u << 20)) return (uint8_t *)calloc(1, bytes);
+    void *p = NULL;
+    const uint64_t al = 2u << 20, sz = (bytes + al - 1) / al * al;
+    if (posix_memalign(&p, al, sz)) return NULL;
+#ifdef MADV_HUGEPAGE
+    madvise(p, sz, MADV_HUGEPAGE);
+#endif
+    memset(p, 0, sz);
+    return (uint8_t *)p;
+}
 static uint32_t lpm_bits(const om_map *m) { return (m->ksz - 4) * 8; }
 
 /* LPM keys are stored normalized: data bits beyond prefixlen cleared. */
@@ -129,14 +149,14 @@ om_map *om_create(uint32_t type, uint32_t key_size, uint32_t value_size,
     if (type == OM_LPM_TRIE && (key_size < 5 || key_size > 4 + 16)) return NULL;
     om_map *m = (om_map *)calloc(1, sizeof(*m));
     m->type = type; m->ksz = key_size; m->vsz = value_size; m->max_entries = max_entries;
+    m->koff = (1 + key_size + 7) / 8 * 8;
+    m->rs = m->koff + (value_size + 7) / 8 * 8;
     m->nshards = shards ? shards : 1;
     m->sh = (om_shard *)calloc(m->nshards, sizeof(om_shard));
     for (uint32_t s = 0; s < m->nshards; s++) {
         om_shard *h = &m->sh[s];
         h->cap = 64;
-        h->keys = (uint8_t *)calloc(h->cap, key_size);
-        h->vals = (uint8_t *)calloc(h->cap, value_size);
-        h->state = (uint8_t *)calloc(h->cap, 1);
+        h->rec = sh_alloc(h->cap * m->rs);
         pthread_mutex_init(&h->mu, NULL);
     }
     return m;
@@ -145,7 +165,7 @@ om_map *om_create(uint32_t type, uint32_t key_size, uint32_t value_size,
 void om_destroy(om_map *m) {
     if (!m) return;
     for (uint32_t s = 0; s < m->nshards; s++) {
-        free(m->sh[s].keys); free(m->sh[s].vals); free(m->sh[s].state);
+        free(m->sh[s].rec);
         pthread_mutex_destroy(&m->sh[s].mu);
     }
     free(m->sh); free(m);
@@ -154,9 +174,9 @@ void om_destroy(om_map *m) {
 static int64_t sh_find(const om_map *m, const om_shard *h, const uint8_t *key) {
     uint64_t mask = h->cap - 1, i = fnv1a(key, m->ksz) & mask;
     for (;;) {
-        uint8_t st = h->state[i];
+        uint8_t st = SH_ST(m, h, i);
         if (st == 0) return -1;
-        if (st == 1 && memcmp(h->keys + i * m->ksz, key, m->ksz) == 0) return (int64_t)i;
+        if (st == 1 && memcmp(SH_KEY(m, h, i), key, m->ksz) == 0) return (int64_t)i;
         i = (i + 1) & mask;
     }
 }
@@ -164,21 +184,18 @@ static int64_t sh_find(const om_map *m, const om_shard *h, const uint8_t *key) {
 static void sh_grow(const om_map *m, om_shard *h) {
     uint64_t ncap = h->cap;
     while ((h->used + 1) * 2 > ncap) ncap *= 2;
-    uint8_t *ok = h->keys, *ov = h->vals, *os = h->state; uint64_t ocap = h->cap;
+    uint8_t *old = h->rec; uint64_t ocap = h->cap;
     h->cap = ncap;
-    h->keys = (uint8_t *)calloc(ncap, m->ksz);
-    h->vals = (uint8_t *)calloc(ncap, m->vsz);
-    h->state = (uint8_t *)calloc(ncap, 1);
+    h->rec = sh_alloc(ncap * m->rs);
     h->tomb = 0;
     for (uint64_t j = 0; j < ocap; j++) {
-        if (os[j] != 1) continue;
-        uint64_t i = fnv1a(ok + j * m->ksz, m->ksz) & (ncap - 1);
-        while (h->state[i]) i = (i + 1) & (ncap - 1);
-        h->state[i] = 1;
-        memcpy(h->keys + i * m->ksz, ok + j * m->ksz, m->ksz);
-        memcpy(h->vals + i * m->vsz, ov + j * m->vsz, m->vsz);
+        const uint8_t *o = old + j * m->rs;
+        if (o[0] != 1) continue;
+        uint64_t i = fnv1a(o + 1, m->ksz) & (ncap - 1);
+        while (SH_ST(m, h, i)) i = (i + 1) & (ncap - 1);
+        memcpy(h->rec + i * m->rs, o, m->rs);
     }
-    free(ok); free(ov); free(os);
+    free(old);
 }
 
 /* Element lookup returning a pointer into the shard (NULL if absent). For
@@ -189,7 +206,7 @@ static uint8_t *om_ptr_exact(om_map *m, const uint8_t *key) {
     if (is_lpm(m)) { lpm_normalize(m, key, nk); k = nk; }
     om_shard *h = &m->sh[shard_of(m, k)];
     int64_t i = sh_find(m, h, k);
-    return i < 0 ? NULL : h->vals + (uint64_t)i * m->vsz;
+    return i < 0 ? NULL : SH_VAL(m, h, i);
 }
 
 /* kernel trie_lookup_elem: longest stored prefix with len <= key.prefixlen
@@ -216,7 +233,7 @@ static uint8_t *om_lookup_ptr(om_map *m, const void *key) {
     if (is_lpm(m)) return om_lpm_lookup_ptr(m, (const uint8_t *)key);
     om_shard *h = &m->sh[shard_of(m, (const uint8_t *)key)];
     int64_t i = sh_find(m, h, (const uint8_t *)key);
-    return i < 0 ? NULL : h->vals + (uint64_t)i * m->vsz;
+    return i < 0 ? NULL : SH_VAL(m, h, i);
 }
 
 int om_lookup(om_map *m, const void *key, void *value_out) {
@@ -253,7 +270,7 @@ int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
     int64_t i = sh_find(m, h, key);
     if (i >= 0) {
         if (flags == 1) return -EEXIST;
-        memcpy(h->vals + (uint64_t)i * m->vsz, value, m->vsz);
+        memcpy(SH_VAL(m, h, i), value, m->vsz);
         return 0;
     }
     if (flags == 2) return -ENOENT;
@@ -264,11 +281,11 @@ int om_update(om_map *m, const void *key_, const void *value, uint64_t flags) {
     }
     if ((h->used + h->tomb + 1) * 2 > h->cap) sh_grow(m, h);
     uint64_t mask = h->cap - 1, j = fnv1a(key, m->ksz) & mask;
-    while (h->state[j] == 1) j = (j + 1) & mask;
-    if (h->state[j] == 2) h->tomb--;
-    h->state[j] = 1;
-    memcpy(h->keys + j * m->ksz, key, m->ksz);
-    memcpy(h->vals + j * m->vsz, value, m->vsz);
+    while (SH_ST(m, h, j) == 1) j = (j + 1) & mask;
+    if (SH_ST(m, h, j) == 2) h->tomb--;
+    SH_ST(m, h, j) = 1;
+    memcpy(SH_KEY(m, h, j), key, m->ksz);
+    memcpy(SH_VAL(m, h, j), value, m->vsz);
     h->used++;
     if (is_lpm(m)) { uint32_t plen; memcpy(&plen, key, 4); m->lens_cnt[plen]++; }
     return 0;
@@ -295,7 +312,7 @@ int om_delete(om_map *m, const void *key_) {
     om_shard *h = &m->sh[shard_of(m, key)];
     int64_t i = sh_find(m, h, key);
     if (i < 0) return -ENOENT;
-    h->state[i] = 2; h->used--; h->tomb++;
+    SH_ST(m, h, i) = 2; h->used--; h->tomb++;
     __atomic_sub_fetch(&m->count, 1, __ATOMIC_RELAXED);
     if (is_lpm(m)) { uint32_t plen; memcpy(&plen, key, 4); m->lens_cnt[plen]--; }
     return 0;
@@ -308,7 +325,7 @@ uint32_t om_foreach(om_map *m, om_visit_fn fn, void *ctx) {
     for (uint32_t s = 0; s < m->nshards; s++) {
         om_shard *h = &m->sh[s];
         for (uint64_t i = 0; i < h->cap; i++)
-            if (h->state[i] == 1) { fn(h->keys + i * m->ksz, h->vals + i * m->vsz, ctx); n++; }
+            if (SH_ST(m, h, i) == 1) { fn(SH_KEY(m, h, i), SH_VAL(m, h, i), ctx); n++; }
     }
     return n;
 }
@@ -1029,7 +1046,10 @@ static uint32_t csum_l4_flags(uint8_t nexthdr);
  * its proxy-map log entry (applied in batch order after the batch, see
  * proxy_apply).  Log entry: [0] family 4/6, key at +4, value at +28. */
 #define O_PLOG 64
-typedef struct pol_ctx { uint8_t *w; uint8_t *plog; } pol_ctx;
+/* w: writable frame; plog: this packet's proxy-log entry; mark: its "entry written"
+ * byte (ingress batches: the log's pages are touched only by redirecting packets,
+ * proxy_apply scans the marks), NULL where the caller clears the entry itself */
+typedef struct pol_ctx { uint8_t *w; uint8_t *plog; uint8_t *mark; } pol_ctx;
 
 /* reverse_map_l4_port (bpf/lib/lb.h:217-251) + the address part of
  * __lb4_rev_nat / __lb6_rev_nat (lb.h:253-293, 447-512) */
@@ -1136,6 +1156,7 @@ static void redirect_write(const skb_t *s, pol_ctx *x, int l4_off, const uint8_t
     if (!e) return;
     memset(e, 0, O_PLOG);
     e[0] = v6 ? 6 : 4;
+    if (x->mark) *x->mark = 1;
     uint8_t *k = e + 4, *v = e + 28;
     int a = v6 ? 16 : 4;
     memcpy(k, t, a);                                  /* .saddr = tuple->daddr */
@@ -1170,9 +1191,16 @@ static void proxy_apply_one(const o_batch *b, const uint8_t *plog, o_ingress_out
         wbytes(&s, w, 0, g_node.host_mac, 6);      /* eth_store_daddr(HOST_IFINDEX_MAC) */
     }
 }
-static void proxy_apply(const o_batch *b, const uint8_t *plog, o_ingress_out *out, uint8_t *wsnap) {
-    for (uint32_t i = 0; i < b->n; i++) proxy_apply_one(b, plog, out, wsnap, i);
+static void proxy_apply(const o_batch *b, const uint8_t *plog, const uint8_t *mark, o_ingress_out *out, uint8_t *wsnap) {
+    for (uint32_t i = 0; i < b->n; i++) if (mark[i]) proxy_apply_one(b, plog, out, wsnap, i);
 }
+/* a batch's proxy log: n zeroed O_PLOG entries (mapped on first write) + n marks */
+typedef struct plog_t { uint8_t *log, *mark; } plog_t;
+static plog_t plog_new(uint32_t n) {
+    plog_t p = {(uint8_t *)calloc((size_t)n + 1, O_PLOG), (uint8_t *)calloc((size_t)n + 1, 1)};
+    return p;
+}
+static void plog_free(plog_t p) { free(p.log); free(p.mark); }
 
 /* ipv4_policy, bpf/bpf_lxc.c:865-970 */
 static int ipv4_policy(const o_lxc_cfg *c, skb_t *s, uint32_t src_label, int *fwd, uint32_t now, uint8_t *oflags,
@@ -1314,7 +1342,8 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
     o->flags = fl;
     if (ret < 0 || ret == TC_ACT_SHOT) {                /* IS_ERR */
         o->action = TC_ACT_SHOT; o->reason = (uint8_t)(-ret); o->flags = fl & 2;
-        if (x->plog) x->plog[0] = 0;                    /* no proxy entry for a dropped packet */
+        if (x->mark) { if (*x->mark) { x->plog[0] = 0; *x->mark = 0; } }   /* no proxy entry for a dropped packet */
+        else if (x->plog) x->plog[0] = 0;
         return;
     }
     o->proxy_port = proxy;
@@ -1327,12 +1356,11 @@ static void handle_policy_skb(const o_prog_array *a, skb_t s, uint32_t lxc_id, u
 }
 /* plog: the batch's proxy log (n * O_PLOG); wsnap: writable frames (pipeline) */
 static void handle_policy(const o_prog_array *a, const o_batch *b, uint32_t i, uint32_t now, o_ingress_out *o,
-                          uint8_t *plog, uint8_t *wsnap) {
+                          plog_t plog, uint8_t *wsnap) {
     skb_t s; skb_init(&s, b, i);
     s.cb[0] = b->src_identity ? b->src_identity[i] : 0;
     s.cb[1] = b->ifindex ? b->ifindex[i] : 0;
-    pol_ctx x = {wsnap ? wsnap + (size_t)i * b->snap_stride : NULL, plog + (size_t)i * O_PLOG};
-    x.plog[0] = 0;
+    pol_ctx x = {wsnap ? wsnap + (size_t)i * b->snap_stride : NULL, plog.log + (size_t)i * O_PLOG, plog.mark + i};
     handle_policy_skb(a, s, b->lxc_id ? b->lxc_id[i] : 0, now, o, &x);
 }
 
@@ -1341,10 +1369,10 @@ void o_prog_array_destroy(o_prog_array *a) { free(a); }
 void o_prog_array_set(o_prog_array *a, uint32_t lxc_id, const o_lxc_cfg *cfg) { a->slot[lxc_id & 0xffff] = cfg; }
 
 void o_ingress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out) {
-    uint8_t *plog = (uint8_t *)calloc((size_t)b->n + 1, O_PLOG);
+    plog_t plog = plog_new(b->n);
     for (uint32_t i = 0; i < b->n; i++) handle_policy(a, b, i, now, &out[i], plog, NULL);
-    proxy_apply(b, plog, out, NULL);
-    free(plog);
+    proxy_apply(b, plog.log, plog.mark, out, NULL);
+    plog_free(plog);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1358,7 +1386,8 @@ typedef struct mt_arg {
     uint32_t *owner, *cnt, *list, *start;
     int phase;
     const uint8_t *skip;                /* pipeline: packets that never reach handle_policy */
-    uint8_t *plog, *wsnap;              /* proxy log, writable frames (pipeline) */
+    plog_t plog;                        /* proxy log */
+    uint8_t *wsnap;                     /* writable frames (pipeline) */
     /* pipeline front pass (kind 3) */
     const o_pipeline_cfg *pc; o_pipeline_out *po; uint8_t *snap_out, *skip_w;
     uint32_t *secctx, *ifx; uint16_t *lxcid;
@@ -1451,7 +1480,7 @@ static void run_mt(mt_arg *tmpl, uint32_t threads) {
 }
 
 static void ingress_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads,
-                       const uint8_t *skip, uint8_t *plog, uint8_t *wsnap) {
+                       const uint8_t *skip, plog_t plog, uint8_t *wsnap) {
     if (threads < 1) threads = 1;
     if (threads > 1024) threads = 1024;
     uint32_t T = threads;
@@ -1477,10 +1506,10 @@ static void ingress_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_
     free(beg); free(m.owner); free(m.list); free(m.cnt); free(m.start);
 }
 void o_ingress_batch_mt(const o_prog_array *a, const o_batch *b, uint32_t now, o_ingress_out *out, uint32_t threads) {
-    uint8_t *plog = (uint8_t *)calloc((size_t)b->n + 1, O_PLOG);
+    plog_t plog = plog_new(b->n);
     ingress_mt(a, b, now, out, threads, NULL, plog, NULL);
-    proxy_apply(b, plog, out, NULL);
-    free(plog);
+    proxy_apply(b, plog.log, plog.mark, out, NULL);
+    plog_free(plog);
 }
 void o_xdp_batch_mt(const o_xdp_cfg *cfg, const o_batch *b, uint8_t *verdict, uint32_t threads) {
     mt_arg m; memset(&m, 0, sizeof m);
@@ -1762,14 +1791,14 @@ void o_pipeline_batch_mt(const o_pipeline_cfg *c, const o_batch *b, uint32_t now
         /* handle_policy over the rewritten frames, flow groups of the rewritten addresses */
         o_batch b2 = *b;
         b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = b->flow_hash;   /* the skb's hash (trace records) */
-        uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
+        plog_t plog = plog_new(n);
         if (threads == 1) {
             for (uint32_t i = 0; i < n; i++) if (!skip[i]) handle_policy(c->policy, &b2, i, now, &ing[i], plog, snap);
         } else {
             ingress_mt(c->policy, &b2, now, ing, threads, skip, plog, snap);
         }
-        proxy_apply(&b2, plog, ing, snap);
-        free(plog);
+        proxy_apply(&b2, plog.log, plog.mark, ing, snap);
+        plog_free(plog);
     }
     for (uint32_t i = 0; i < n; i++) {
         o_pipeline_out *o = &out[i];
@@ -2133,7 +2162,7 @@ skip_service_lookup: ;
         if (tr) trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.host_ifindex, (uint8_t)fwd);
         ret = redirect_to_host_port_checks(s, l4_off, nh);
         if (IS_ERR(ret)) return ret;
-        pol_ctx x = {w, plog};
+        pol_ctx x = {w, plog, NULL};
         redirect_write(s, &x, l4_off, t, 0, (uint16_t)verdict, (const uint8_t *)&orig_dip, c->seclabel, now);
         if (plog) plog[1] = 1;                                          /* egress entry: no policy MAC stores */
         r->eg_flags |= EG_F_PROXY; r->proxy = (uint16_t)verdict;
@@ -2351,7 +2380,7 @@ skip_service_lookup: ;
         if (tr) trace_event(s, TRACE_TO_PROXY, (uint16_t)c->lxc_id, c->seclabel, 0, 0, g_node.host_ifindex, fwd);
         ret = redirect_to_host_port_checks(s, l4_off, nh);
         if (IS_ERR(ret)) return ret;
-        pol_ctx x = {w, plog};
+        pol_ctx x = {w, plog, NULL};
         redirect_write(s, &x, l4_off, t, 1, (uint16_t)verdict, orig_dip, c->seclabel, now);
         if (plog) plog[1] = 1;
         r->eg_flags |= EG_F_PROXY; r->proxy = (uint16_t)verdict;
@@ -2467,7 +2496,7 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
     uint32_t *secctx = (uint32_t *)malloc((size_t)n * 4 + 4), *ifx = (uint32_t *)malloc((size_t)n * 4 + 4);
     uint16_t *lxcid = (uint16_t *)malloc((size_t)n * 2 + 2);
     uint8_t *plog = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
-    uint8_t *plog2 = (uint8_t *)calloc((size_t)n + 1, O_PLOG);
+    plog_t plog2 = plog_new(n);
     o_ingress_out *ing = (o_ingress_out *)calloc((size_t)n + 1, sizeof(o_ingress_out));
     o_batch b2 = *b;                                   /* the local deliveries, over the rewritten frames */
     b2.snap = snap; b2.src_identity = secctx; b2.ifindex = ifx; b2.lxc_id = lxcid; b2.flow_hash = b->flow_hash;   /* the skb's hash (trace records) */
@@ -2489,7 +2518,7 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
         }
         if (skip[i]) continue;
         handle_policy(a, &b2, i, now, &ing[i], plog2, snap);
-        proxy_apply_one(&b2, plog2, ing, snap, i);
+        proxy_apply_one(&b2, plog2.log, ing, snap, i);
         o_egress_out *o = &out[i];
         o->action = ing[i].action; o->reason = ing[i].reason; o->ct_ret = ing[i].ct_ret;
         o->flags = ing[i].flags; o->proxy_port = ing[i].proxy_port; o->ifindex_lo = ing[i].ifindex_lo;
@@ -2513,7 +2542,7 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now, o_egr
         uint8_t *t = ev_slot(i);
         if (t) memcpy(t, e, O_EVENT_RECORD);
     }
-    free(plog2); free(ing); free(plog);
+    plog_free(plog2); free(ing); free(plog);
     if (!snap_out) free(snap);
     free(skip); free(secctx); free(ifx); free(lxcid);
 }

@@ -15,7 +15,7 @@ O=$R/gpurun_out/prof_$T
 mkdir -p "$O/pmc"
 cd /tmp && export TMPDIR=/tmp
 for C in $CONFIGS; do
-  if [ "$C" = 2 ]; then A="--no-cpu --no-extra --steps 4 --warmup 3"; else A="--no-cpu --config $C"; fi
+  if [ "$C" = 2 ]; then A="--no-cpu --no-extra --steps 4 --warmup 3 --long-steps 0"; else A="--no-cpu --config $C"; fi
   [ "$C" = 4 ] && A="$A --no-h2d"                   # the H2D leg's extra steps would count twice
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks$C" -o run -- \
       python "$R/bench.py" $A > "$O/ks$C.json" 2> "$O/ks$C.err"
