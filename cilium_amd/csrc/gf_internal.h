@@ -120,6 +120,14 @@ struct Map : Obj {
     bool trie_dirty = true;
     DevBuf d_root, d_nodes, d_rsum;   // coverage trie (+ root summary, root_bits 16)
     uint32_t trie_root_bits = 0;
+    uint64_t trie_gen = 0;            // trie rebuilds (derived DIR-24-8 tables follow it)
+    // IPv4 LPM coverage as DIR-24-8 tables (GF_XDP_DIR24 A/B): tbl24 = 2^24 u16
+    // (0 none, 0xffff covered, else 1 + the /24's 256-bit group in tbl8); rebuilt
+    // after the trie.  -E2BIG past 65534 groups, -EINVAL for another key size.
+    int dir24(hipStream_t s, const uint16_t **t24, const uint32_t **t8);
+    DevBuf d_dir24, d_dir8;
+    uint64_t dir_gen = ~0ull;
+    bool dir_big = false;
 
     Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f);
     bool is_lpm() const { return type == GF_MAP_TYPE_LPM_TRIE; }

@@ -337,7 +337,19 @@ struct XdpDev {
     // (Map::addr_set) probed in place of their hash tables (IPv4 only)
     const uint32_t *h4set, *lxset;
     uint32_t h4bits, lxbits, h4zero, lxzero;
+    // optional (GF_XDP_DIR24, Map::dir24): the v4 prefixes as DIR-24-8 tables, read
+    // in place of the trie walk below a root-summary "has a node" bit
+    const uint16_t *d24;
+    const uint32_t *d8;
 };
+// DIR-24-8 coverage of an IPv4 source (raw network-order word): one 2-B read of
+// tbl24, one 4-B read of the /24's group when it holds longer prefixes.
+__device__ __forceinline__ bool dir24_cov(const uint16_t *t24, const uint32_t *t8, uint32_t sa) {
+    const uint32_t i24 = ((sa & 0xffu) << 16) | (sa & 0xff00u) | ((sa >> 16) & 0xffu), b = sa >> 24;
+    const uint32_t e = gload<uint16_t>(t24 + i24);
+    if (e == 0xffffu) return true;
+    return e && ((gload<uint32_t>(t8 + (e - 1u) * 8u + (b >> 5)) >> (b & 31u)) & 1u);
+}
 // The table slot of an address in an endpoint-key set (its second array), or -1.
 __device__ __forceinline__ int64_t aset_slot(const uint32_t *t, uint32_t bits, uint32_t zero, uint32_t a) {
     if (!a) return (int64_t)zero - 1;
@@ -403,7 +415,8 @@ __device__ __forceinline__ uint8_t xdp_verdict(const XdpDev &x, const A &a, uint
                 const uint32_t idx = ((sa & 0xffu) << 8) | ((sa >> 8) & 0xffu);
                 cov = (gload<uint64_t>(x.l4.rsum + (idx >> 6)) >> (idx & 63)) & 1ull;
                 if (!cov && ((gload<uint64_t>(x.l4.rsum + 1024 + (idx >> 6)) >> (idx & 63)) & 1ull))
-                    cov = trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
+                    cov = x.d24 ? dir24_cov(x.d24, x.d8, sa)
+                                : trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
             } else {
                 cov = trie_lookup<1>(x.l4, &sa);
             }
@@ -545,7 +558,8 @@ __global__ __launch_bounds__(1024) void k_xdp_lds(gf_pkt_cols c, XdpDev x, XdpLd
                     const uint32_t idx = ((sa & 0xffu) << 8) | ((sa >> 8) & 0xffu);   // the first two address bytes
                     if ((rs[idx >> 6] >> (idx & 63)) & 1ull) drop = true;
                     else if ((rs[1024 + (idx >> 6)] >> (idx & 63)) & 1ull)
-                        drop = trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
+                        drop = x.d24 ? dir24_cov(x.d24, x.d8, sa)
+                                     : trie_nodes<1>(x.l4, AddrBytes<1>(&sa), gload<uint32_t>(x.l4.root + idx) - 1u);
                     if (!drop) {
                         ab += 9;
                         const uint32_t kw[2] = {32u, sa};
@@ -4738,6 +4752,14 @@ uint32_t stream_grid(uint32_t n, uint32_t per_block = BLOCK) {
 }
 
 int push_map(const std::shared_ptr<Map> &m, hipStream_t s) { return m ? m->push(s) : 0; }
+// The v4 prefixes as DIR-24-8 tables for XdpDev (GF_XDP_DIR24=1: the A/B against
+// the trie walk), when they build.
+void xdp_dir(const std::shared_ptr<Map> &l4, XdpDev &x, hipStream_t s) {
+    const char *e = getenv("GF_XDP_DIR24");       // read per call: a test flips it in-process
+    const bool on = e && atoi(e) != 0;
+    x.d24 = nullptr; x.d8 = nullptr;
+    if (on && l4 && l4->dir24(s, &x.d24, &x.d8)) { x.d24 = nullptr; x.d8 = nullptr; }
+}
 // The prefilter's compact address sets (Map::addr_set) for XdpDev, when they build.
 void xdp_sets(const std::shared_ptr<Map> &h4, const std::shared_ptr<Map> &lxc, XdpDev &x, hipStream_t s) {
     static const bool no_sets = getenv("GF_XDP_NOSETS") != nullptr;     // diagnosis: the hash tables
@@ -4880,6 +4902,7 @@ int gf_xdp_classify(int prog, const gf_pkt_cols *pkts, uint8_t *verdict, void *s
     if (p->m6h) { x.h6 = p->m6h->hdesc(); x.has_h6 = 1; }
     if (p->m4l) x.l4 = p->m4l->tdesc();
     if (p->m6l) x.l6 = p->m6l->tdesc();
+    xdp_dir(p->m4l, x, s);
     x.lxc = p->lxc->hdesc();
     ProfScope ps("k_xdp", s);
     // The LDS variant when the LPM map has a 16-bit root (its summary is 16 KB);
@@ -5850,6 +5873,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
         if (x.m6l) P.x.l6 = x.m6l->tdesc();
         P.x.lxc = x.lxc->hdesc();
         xdp_sets(x.m4h, x.lxc, P.x, s);
+        xdp_dir(x.m4l, P.x, s);
         P.has_xdp = 1;
     }
     if (p->lb) {

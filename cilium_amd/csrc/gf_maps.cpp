@@ -315,6 +315,7 @@ int Map::push(hipStream_t s) {
         }
         trie_root_bits = rb;
         trie_dirty = false;
+        trie_gen++;
         return 0;
     }
     if (dev_valid) return 0;
@@ -389,6 +390,51 @@ int Map::addr_set(uint32_t kind, uint32_t max_slots, hipStream_t s, const uint32
         aset_gen = host_gen; aset_kind = kind; aset_bits = b; aset_zero = z; aset_big = false;
     }
     *set = (const uint32_t *)d_aset.p; *bits = aset_bits; *zero = aset_zero;
+    return 0;
+}
+
+int Map::dir24(hipStream_t s, const uint16_t **t24, const uint32_t **t8) {
+    std::lock_guard<std::recursive_mutex> g(mu);
+    if (!is_lpm() || ksz != 8) return -EINVAL;
+    if (dir_gen == trie_gen && dir_big) return -E2BIG;
+    if (dir_gen != trie_gen || !d_dir24.p) {
+        std::vector<uint16_t> t(1u << 24, 0);
+        std::vector<uint32_t> grp;                       // 8 words a group
+        // prefixes up to /24 first (whole /24 ranges), then the longer ones as
+        // byte ranges in their /24's group (a covered /24 needs none)
+        for (auto &kv : lpm) {
+            uint32_t L; memcpy(&L, kv.first.data(), 4);
+            if (L > 24) continue;
+            const uint8_t *a = (const uint8_t *)kv.first.data() + 4;
+            const uint32_t i24 = ((uint32_t)a[0] << 16) | ((uint32_t)a[1] << 8) | a[2];
+            const uint32_t span = 1u << (24 - L), st = i24 & ~(span - 1);
+            std::fill(t.begin() + st, t.begin() + st + span, (uint16_t)0xffff);
+        }
+        for (auto &kv : lpm) {
+            uint32_t L; memcpy(&L, kv.first.data(), 4);
+            if (L <= 24) continue;
+            const uint8_t *a = (const uint8_t *)kv.first.data() + 4;
+            const uint32_t i24 = ((uint32_t)a[0] << 16) | ((uint32_t)a[1] << 8) | a[2];
+            if (t[i24] == 0xffff) continue;
+            if (!t[i24]) {
+                if (grp.size() / 8 >= 65534) { dir_gen = trie_gen; dir_big = true; return -E2BIG; }
+                grp.resize(grp.size() + 8, 0u);
+                t[i24] = (uint16_t)(grp.size() / 8);
+            }
+            uint32_t *w = &grp[(t[i24] - 1u) * 8];
+            const uint32_t span = 1u << (32 - L), st = a[3] & ~(span - 1);
+            for (uint32_t b = st; b < st + span; b++) w[b >> 5] |= 1u << (b & 31);
+        }
+        if (grp.empty()) grp.assign(8, 0u);
+        int r;
+        if ((r = d_dir24.ensure(t.size() * 2)) || (r = d_dir8.ensure(grp.size() * 4))) return r;
+        if (hip_ok(hipMemcpyAsync(d_dir24.p, t.data(), t.size() * 2, hipMemcpyHostToDevice, s), "push tbl24") ||
+            hip_ok(hipMemcpyAsync(d_dir8.p, grp.data(), grp.size() * 4, hipMemcpyHostToDevice, s), "push tbl8") ||
+            hip_ok(hipStreamSynchronize(s), "dir24 sync"))
+            return -EIO;
+        dir_gen = trie_gen; dir_big = false;
+    }
+    *t24 = (const uint16_t *)d_dir24.p; *t8 = (const uint32_t *)d_dir8.p;
     return 0;
 }
 
