@@ -129,14 +129,6 @@ class Gpu:
         lib.gf_prof_enable(0)
         return self.c, {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
 
-    def lru_stats(self, dp, name):
-        import ctypes as C
-        from cilium_amd._lib import lib
-        out = (C.c_uint64 * 4)()
-        if lib.gf_ct_lru_stats(dp.fd[name], out):
-            return None
-        return {"sweeps": int(out[0]), "partial": int(out[1]), "lines_read": int(out[2]), "fallbacks": int(out[3])}
-
     def evict_log(self, dp, name):
         from cilium_amd._lib import lib, gf_ct_evict_rec
         recs = (gf_ct_evict_rec * 4096)()
@@ -204,9 +196,6 @@ class Rehearsal:
 
     def evict_log(self, dp, name):
         return list(dp.ref.lru_log.get(name, []))
-
-    def lru_stats(self, dp, name):
-        return {"sweeps": len(dp.ref.lru_log.get(name, [])), "partial": 0, "lines_read": 0, "fallbacks": 0}
 
     def table_sampled(self, dp, name, ksz, div, pred):
         from oracle import parity as PY
@@ -497,8 +486,7 @@ def bench_config2(args, B, rank, world, local_world=1):
         long_h = {"steps": K + C_, "after_warmup": W, "mpps": round(lp / (elapsed + el2) / 1e6, 3),
                   "ms_per_step": round((elapsed + el2) / (K + C_) * 1e3, 4),
                   "continuation": {"steps": C_, "mpps": round(int(c2[268]) / el2 / 1e6, 3),
-                                   "kernels_ms_per_step": kms(kern2)},
-                  "lru_sweeps": B.lru_stats(dp, "cilium_ct4_global")}
+                                   "kernels_ms_per_step": kms(kern2)}}
         log(f"long horizon: {long_h['mpps']} Mpps over {K + C_} steps (continuation {long_h['continuation']['mpps']})")
     local_pkts = sum(batches[s].n for s in range(W, W + K))
     if not os.environ.get("GPUFLOW_DIAG_LIB"):

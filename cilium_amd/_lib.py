@@ -165,7 +165,6 @@ class gf_ct_evict_rec(C.Structure):
 
 
 _sig("gf_ct_evict_log", C.c_int, C.c_int, C.POINTER(gf_ct_evict_rec), C.c_uint32)
-_sig("gf_ct_lru_stats", C.c_int, C.c_int, C.POINTER(C.c_uint64))
 _sig("gf_pipeline_partition", C.c_int, C.c_int, C.POINTER(gf_pipe_batch), C.c_uint32, C.c_uint32, VP, VP, VP, VP)
 _sig("gf_lxc_egress_classify", C.c_int, C.c_int, C.POINTER(gf_lxc_batch), C.c_uint32, VP, VP, VP)
 _sig("gf_set_event_ring", C.c_int, C.POINTER(gf_event_ring))
@@ -188,7 +187,7 @@ EXPORTED = [
     "gf_obj_close", "gf_obj_unpin", "gf_now_sec", "gf_parse_frames", "gf_xdp_prog_load",
     "gf_xdp_classify", "gf_lb_prog_load", "gf_lb_classify", "gf_lxc_prog_load",
     "gf_policy_array_create", "gf_policy_array_update", "gf_node_config",
-    "gf_policy_ingress_classify", "gf_policy_ingress_classify_batches", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_ct_lru_stats", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
+    "gf_policy_ingress_classify", "gf_policy_ingress_classify_batches", "gf_pipeline_load", "gf_pipeline_classify", "gf_pipeline_partition", "gf_lxc_egress_classify", "gf_ct_gc", "gf_ct_evict_log", "gf_set_event_ring", "gf_set_stats_sink", "gf_prof_enable", "gf_prof_read", "gf_dev_alloc", "gf_dev_free",
     "gf_memcpy_h2d", "gf_memcpy_d2h", "gf_stream_sync", "gf_device_count", "gf_version", "gf_build_id",
 ]
 

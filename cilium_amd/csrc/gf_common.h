@@ -52,7 +52,6 @@ struct gf_htab_desc {
     uint32_t  split, max_entries;
     uint32_t  vin;         // value bytes inline in the slot (at voff); the rest is in vals
     uint32_t  sstride;     // bytes per slot in vals (0: no side array)
-    uint32_t *lfloor;      // LRU CT maps: the age floor of each 128-B slot line (LRU sweeps), else nullptr
 };
 
 struct gf_trie_desc {

@@ -102,9 +102,6 @@ struct Map : Obj {
     DevBuf d_slots, d_vals, d_count;
     DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits
     DevBuf d_lrucodes;          // LRU CT maps: per-slot sweep codes (k_lru_hist -> k_lru_clusters)
-    DevBuf d_lfloor, d_lflist;  // LRU CT maps: age floor per 128-B slot line, the lines a partial sweep scans
-    int lf_clear(uint64_t slot);                 // LRU age floor of the slot's line: unknown
-    void lf_clear_all(hipStream_t s);            // every line's
     uint32_t lru_seq = 0;       // classify calls that used this map (the eviction log's batch number)
     // get_next_key over a device-authoritative map: a host copy of one chunk of
     // slot headers, and the slot of the key returned last (the dump loop's next

@@ -961,15 +961,6 @@ struct RelCache {
     __device__ __forceinline__ void init() { slot = ~0u; sec = 0; }
 };
 
-// LRU age floors (partial eviction sweeps, k_lf_*): an entry entering the
-// closing class moves to the front of the eviction order, below its line's floor,
-// so the writer clears the floor (0 = the next sweep scans the line).  Every other
-// datapath write only makes an entry younger or removes it.
-__device__ __forceinline__ void lf_touch_closing(const gf_htab_desc &d, uint64_t f, uint32_t fl_old, uint32_t fl_new) {
-    if (d.lfloor && !(fl_old & (F_RX_CLOSING | F_TX_CLOSING)) && (fl_new & (F_RX_CLOSING | F_TX_CLOSING)))
-        gstore<uint32_t>(d.lfloor + (f * d.slot_size >> 7), 0u);
-}
-
 // __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part.  CT
 // values use the GF_VCODEC_CT layout: `hot` = the entry's first 16 B
 // (lifetime, flags | rev_nat_index, rx_packets lo32, rx_bytes lo32), loaded
@@ -1003,7 +994,6 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
         fl |= F_RX_CLOSING;
         if ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) life = now + 10u;
     }
-    lf_touch_closing(d, (uint64_t)f, hot.y & 0xffffu, fl);
     hot.x = life;
     hot.y = (hot.y & 0xffff0000u) | fl;
     gstore<uint4>(e, hot);
@@ -2351,18 +2341,8 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
 struct LruLog { uint32_t seq, now; unsigned long long cut_c, cut_o, evicted; };
-#define GF_LF_CB 2048u               // coarse age bins of the partial sweep: key >> 6 (64 s)
 struct LruDev {
     uint32_t hist[2 * GF_LRU_BINS];
-    uint32_t mode;                // this sweep: 1 partial (lines with an old age floor), 0 the whole table
-    uint32_t T;                   // partial: the lines whose floor key <= T are scanned
-    uint32_t nlist, list_over;    // lines listed for the scan; the list overflowed
-    uint32_t cb, cb_need;         // the coarse bin holding the cut; entries still needed inside it
-    uint32_t fh[GF_LF_CB];        // lines by floor key (coarse; known floors)
-    uint32_t ch[GF_LF_CB];        // scanned entries with key <= T (coarse)
-    uint32_t fine[64];            // scanned entries of the coarse bin cb, per 1-s bin
-    uint32_t tried;               // this sweep attempted the partial form
-    unsigned long long stats[4];  // gf_ct_lru_stats: sweeps, partial sweeps, lines they read, fallbacks
     GcCut cut;
     unsigned long long res[2];
     unsigned long long target;
@@ -2382,17 +2362,13 @@ __global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev 
     const bool f = c > max_entries;
     if (threadIdx.x == 0) {
         L->flag = f ? 1u : 0u;
-        L->mode = 0; L->T = 0; L->nlist = 0; L->list_over = 0; L->cb = 0; L->cb_need = 0; L->tried = 0;
         L->cut.active = 0;
         L->res[0] = L->res[1] = 0;
         L->moves[0] = L->moves[1] = 0;
         L->target = (unsigned long long)(max_entries - max_entries / 8u);
     }
-    if (f) {
+    if (f)
         for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
-        for (uint32_t k = threadIdx.x; k < GF_LF_CB; k += blockDim.x) { L->fh[k] = 0; L->ch[k] = 0; }
-        for (uint32_t k = threadIdx.x; k < 64; k += blockDim.x) L->fine[k] = 0;
-    }
 }
 // Age histogram: wave-aggregated (a wave's entries mostly share a bin), then
 // counted per block in LDS and flushed with one global add per non-zero bin.
@@ -2520,7 +2496,7 @@ __device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mo
 template <int KIND>
 __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
                                                         LruDev *L, uint32_t *bits, uint32_t *codes) {
-    if (!L->flag || L->mode) return;
+    if (!L->flag) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
@@ -2587,7 +2563,7 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t
 // The smallest prefix of the age order whose removal leaves <= target entries:
 // one block scans the 2 x 65536 bins (128 per thread, then a block scan).
 __global__ __launch_bounds__(1024) void k_lru_cut(const uint32_t *count, uint32_t now, LruDev *L) {
-    if (!L->flag || L->mode) return;
+    if (!L->flag) return;
     __shared__ unsigned long long part[1024];
     constexpr uint32_t PER = 2 * GF_LRU_BINS / 1024;
     const uint32_t t = threadIdx.x;
@@ -2663,7 +2639,7 @@ __device__ __forceinline__ LruMasks lru_code_masks(const uint32_t *__restrict__ 
 }
 __global__ __launch_bounds__(BLOCK) void k_lru_clusters(gf_htab_desc d, uint32_t mode, const uint32_t *__restrict__ codes,
                                                         const uint32_t *__restrict__ bits, LruDev *L) {
-    if (!L->cut.active || L->mode) return;
+    if (!L->cut.active) return;
     const uint32_t ck = L->cut_key;
     const uint64_t nw = (d.mask + 1) / 32;
     const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
@@ -2739,299 +2715,8 @@ __global__ __launch_bounds__(BLOCK) void k_lru_clusters(gf_htab_desc d, uint32_t
     if (nmv0) atomicAdd(&L->moves[0], (unsigned long long)nmv0);
     if (nmv1) atomicAdd(&L->moves[1], (unsigned long long)nmv1);
 }
-// ---- partial sweeps over age floors ------------------------------------------
-// lfloor[l] bounds from below the age key of every entry in 128-B slot line l:
-// (class << 31) | (last use + 43200) / 2, class 0 = closing (the class ordered
-// first), rounded down, so it decodes to a time no later than any entry's last use;
-// 0 = unknown.  A sweep first streams the floors (one u32 per line), picks the
-// smallest key T whose lines number 1.5 x the entries to evict, and reads
-// only those lines: every entry whose key is <= T lies in one of them, so the
-// histogram of the scanned entries up to T is exact and the cut it gives is the
-// whole-table cut.  When the lines up to T turn out to hold fewer
-// entries than needed (or the list overflows) the sweep falls back to the whole
-// table on the device (L->mode = 0).  Writers keep the bound: a datapath write makes
-// an entry younger except the closing transition (lf_touch_closing clears the
-// floor); API writes, bulk loads, pushes and GC clear floors (Map code).
-__device__ __forceinline__ uint32_t lf_enc(uint32_t lt, uint32_t fl) {
-    const long long lu = ct_last_use(lt, fl) + 43200;   // >= 0 (lifetime >= 0, timeout <= 43200)
-    return (((fl & (F_RX_CLOSING | F_TX_CLOSING)) ? 0u : 1u) << 31) | (uint32_t)((unsigned long long)lu >> 1);
-}
-// the key lru_key would give an entry of the floor's class and last use, at time now
-__device__ __forceinline__ uint32_t lf_key(uint32_t f, uint32_t now) {
-    const long long lu = 2ll * (long long)(f & 0x7fffffffu) - 43200;
-    long long b = lu - ((long long)now - (long long)(GF_LRU_BINS - 1));
-    b = b < 0 ? 0 : (b > (long long)(GF_LRU_BINS - 1) ? (long long)(GF_LRU_BINS - 1) : b);
-    return ((f >> 31) ? GF_LRU_BINS : 0u) + (uint32_t)b;
-}
-__global__ __launch_bounds__(BLOCK) void k_lf_hist(const uint32_t *__restrict__ fl, uint64_t nl, uint32_t now, LruDev *L) {
-    if (!L->flag) return;
-    __shared__ uint32_t h[GF_LF_CB];
-    for (uint32_t k = threadIdx.x; k < GF_LF_CB; k += blockDim.x) h[k] = 0;
-    __syncthreads();
-    for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nl; l += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t f = fl[l];
-        if (f) atomicAdd(&h[lf_key(f, now) >> 6], 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < GF_LF_CB; k += blockDim.x)
-        if (h[k]) atomicAdd(&L->fh[k], h[k]);
-}
-// one block: T = the end of the smallest coarse prefix of known floors holding
-// 1.5 x need lines; none (e.g. floors never set: the first sweep) -> the whole table
-__global__ __launch_bounds__(1024) void k_lf_cut(const uint32_t *count, LruDev *L) {
-    if (!L->flag) return;
-    __shared__ unsigned long long part[1024];
-    const uint32_t t = threadIdx.x;
-    part[t] = (unsigned long long)L->fh[2 * t] + L->fh[2 * t + 1];
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        const unsigned long long v = t >= o ? part[t - o] : 0ull;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    const unsigned long long c = *count, need = c > L->target ? c - L->target : 0ull, want = need + need / 2;
-    if (t == 0) L->mode = 0;
-    __syncthreads();
-    const unsigned long long before = t ? part[t - 1] : 0ull;
-    if (need && before < want && part[t] >= want) {
-        const uint32_t b = (before + L->fh[2 * t] >= want) ? 2 * t : 2 * t + 1;
-        L->T = (b << 6) + 63u;
-        L->mode = 1;
-        L->tried = 1;
-    }
-}
-// the lines to scan: unknown floors and floors with key <= T (wave-compacted)
-__global__ __launch_bounds__(BLOCK) void k_lf_list(const uint32_t *__restrict__ fl, uint64_t nl, uint32_t now, LruDev *L,
-                                                   uint32_t *list, uint32_t cap) {
-    if (!L->flag || L->mode != 1) return;
-    const uint32_t T = L->T, lane = threadIdx.x & 63u;
-    for (uint64_t l0 = blockIdx.x * (uint64_t)blockDim.x; l0 < nl; l0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t l = l0 + threadIdx.x;
-        bool sel = false;
-        if (l < nl) { const uint32_t f = fl[l]; sel = !f || lf_key(f, now) <= T; }
-        const uint64_t m = __ballot(sel);
-        if (!m) continue;
-        uint32_t base = 0;
-        if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) base = atomicAdd(&L->nlist, (uint32_t)__popcll(m));
-        base = __shfl(base, __ffsll((unsigned long long)m) - 1);
-        const uint32_t k = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (sel) { if (k < cap) list[k] = (uint32_t)l; else L->list_over = 1; }
-    }
-}
-// A listed line read by 8 lanes, one 16-B chunk each (a line per 8 lanes: one
-// wave-instruction touches 8 lines, not 64).  For chunk c of the lane's line, the
-// slot it belongs to, and for the lane holding a slot's value chunk (lifetime,
-// flags) the slot's state (from the lane holding the state byte) and age key.
-// KIND 1: CT4 (32-B slots: chunk 2s key+state, 2s+1 hot); KIND 2: CT6 (64-B
-// slots: chunks 4s..4s+2 key, state in 4s+2, 4s+3 hot).
-struct LfSlot { uint64_t i; bool live, val; uint32_t st, lt, fl, key; };
-// wave-uniform loop over the listed lines, 8 per wave per trip: li, have
-#define LF_LINES_BEGIN(n)                                                                                   \
-    {                                                                                                       \
-        const uint64_t wv_ = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;                        \
-        const uint64_t nw_ = ((uint64_t)gridDim.x * blockDim.x) >> 6;                                       \
-        for (uint64_t w8_ = wv_ * 8; w8_ < (n); w8_ += nw_ * 8) {                                           \
-            const uint64_t li = w8_ + ((threadIdx.x & 63u) >> 3);                                           \
-            const bool have = li < (n);
-#define LF_LINES_END }}
-template <int KIND>
-__device__ __forceinline__ LfSlot lf_read(const gf_htab_desc &d, uint32_t line, bool have, uint32_t now) {
-    const uint32_t c = threadIdx.x & 7u;
-    const uint64_t first = (uint64_t)line * (128u / d.slot_size);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (have) v = gload<uint4>(d.slots + (uint64_t)line * 128u + 16u * c);
-    LfSlot r;
-    if (KIND == 1) {
-        const uint32_t st = __shfl_xor((int)((v.w >> 16) & 0xffu), 1);   // chunk 2s: state at byte 14
-        r.i = first + (c >> 1); r.val = have && (c & 1u); r.st = st; r.lt = v.x; r.fl = v.y & 0xffffu;
-    } else {
-        const uint32_t st = __shfl_xor((int)(v.z & 0xffu), 1);             // chunk 4s+2: state at byte 40
-        r.i = first + (c >> 2); r.val = have && (c & 3u) == 3u; r.st = st; r.lt = v.x; r.fl = v.y & 0xffffu;
-    }
-    r.live = r.val && r.st == GF_SLOT_FULL;
-    r.key = r.live ? lru_key(r.lt, r.fl, now) : ~0u;
-    return r;
-}
-template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_lf_scan(gf_htab_desc d, uint32_t now, LruDev *L, const uint32_t *list) {
-    if (!L->flag || L->mode != 1 || L->list_over) return;
-    __shared__ uint32_t h[GF_LF_CB];
-    for (uint32_t k = threadIdx.x; k < GF_LF_CB; k += blockDim.x) h[k] = 0;
-    __syncthreads();
-    const uint32_t n = L->nlist, T = L->T;
-    LF_LINES_BEGIN(n)
-        const LfSlot r = lf_read<KIND>(d, have ? list[li] : 0u, have, now);
-        if (r.live && r.key <= T) atomicAdd(&h[r.key >> 6], 1u);
-    LF_LINES_END
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < GF_LF_CB; k += blockDim.x)
-        if (h[k]) atomicAdd(&L->ch[k], h[k]);
-}
-// one block: the coarse bin of the cut among the scanned entries (all entries
-// with key <= T); too few of them -> the whole table
-__global__ __launch_bounds__(1024) void k_lf_cut2(const uint32_t *count, LruDev *L) {
-    if (!L->flag || L->mode != 1) return;
-    __shared__ unsigned long long part[1024];
-    const uint32_t t = threadIdx.x;
-    part[t] = (unsigned long long)L->ch[2 * t] + L->ch[2 * t + 1];
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        const unsigned long long v = t >= o ? part[t - o] : 0ull;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    const unsigned long long c = *count, need = c > L->target ? c - L->target : 0ull;
-    const unsigned long long before = t ? part[t - 1] : 0ull;
-    const bool ok = !L->list_over && part[1023] >= need && need;
-    __syncthreads();
-    if (!ok) { if (t == 0) L->mode = 0; return; }
-    if (before < need && part[t] >= need) {
-        const uint32_t b = (before + L->ch[2 * t] >= need) ? 2 * t : 2 * t + 1;
-        L->cb = b;
-        L->cb_need = (uint32_t)(need - (b == 2 * t ? before : before + L->ch[2 * t]));
-    }
-}
-template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_lf_fine(gf_htab_desc d, uint32_t now, LruDev *L, const uint32_t *list) {
-    if (!L->flag || L->mode != 1) return;
-    __shared__ uint32_t h[64];
-    if (threadIdx.x < 64) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t n = L->nlist, cb = L->cb;
-    LF_LINES_BEGIN(n)
-        const LfSlot r = lf_read<KIND>(d, have ? list[li] : 0u, have, now);
-        if (r.live && (r.key >> 6) == cb) atomicAdd(&h[r.key & 63u], 1u);
-    LF_LINES_END
-    __syncthreads();
-    if (threadIdx.x < 64 && h[threadIdx.x]) atomicAdd(&L->fine[threadIdx.x], h[threadIdx.x]);
-}
-// one wave: the cut bin inside cb and the cutoffs (k_lru_cut's, from the same key)
-__global__ void k_lf_cut3(uint32_t now, LruDev *L) {
-    if (!L->flag || L->mode != 1) return;
-    if (threadIdx.x) return;
-    unsigned long long acc = 0;
-    uint32_t kb = L->cb * 64u + 63u;
-    for (uint32_t j = 0; j < 64; j++) {
-        acc += L->fine[j];
-        if (acc >= L->cb_need) { kb = L->cb * 64u + j; break; }
-    }
-    const long long base = (long long)now - (long long)(GF_LRU_BINS - 1);
-    auto cut_of = [&](uint32_t b) -> unsigned long long {
-        const long long v = base + (long long)b + 1;
-        return b == GF_LRU_BINS - 1 ? (1ull << 32) : (v <= 0 ? 0ull : (unsigned long long)v);
-    };
-    if (kb < GF_LRU_BINS) { L->cut.c = cut_of(kb); L->cut.o = 0; }
-    else { L->cut.c = 1ull << 32; L->cut.o = cut_of(kb - GF_LRU_BINS); }
-    L->cut.lru = 1;
-    L->cut_key = kb;
-    L->cut.active = 1;
-    L->cb_need = 0;                                  // from here on: the owner count (k_lf_owners)
-}
-// The first entry each probe cluster loses (from a listed line; no entry of an
-// unlisted line is evicted) owns the cluster's compaction walk: a doomed entry
-// with no doomed entry between it and the cluster start (the EMPTY slot before).
-// Read-only, so every owner is decided on the table before any walk changes it.
-template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_lf_owners(gf_htab_desc d, uint32_t now, LruDev *L, const uint32_t *list,
-                                                     uint32_t *owners, uint32_t cap) {
-    if (!L->flag || L->mode != 1 || !L->cut.active) return;
-    const GcCut cut = L->cut;
-    const uint32_t n = L->nlist;
-    uint32_t *nown = &L->cb_need;                     // (cb_need is spent: it counts the owners now)
-    LF_LINES_BEGIN(n)
-        const LfSlot r = lf_read<KIND>(d, have ? list[li] : 0u, have, now);
-        bool own = false;
-        if (r.live && gc_kill(r.lt, r.fl, cut)) {
-            own = true;
-            for (uint64_t j = (r.i - 1) & d.mask; j != r.i; j = (j - 1) & d.mask) {
-                const uint8_t *sl = d.slots + j * d.slot_size;
-                const uint32_t st = sl[d.ksz];
-                if (st == GF_SLOT_EMPTY) break;
-                if (st == GF_SLOT_FULL) {
-                    const uint8_t *v = ht_val(d, j);
-                    if (gc_kill(*reinterpret_cast<const uint32_t *>(v), *reinterpret_cast<const uint16_t *>(v + 4), cut)) {
-                        own = false;
-                        break;
-                    }
-                }
-            }
-        }
-        if (own) {
-            const uint32_t k = atomicAdd(nown, 1u);
-            if (k < cap) owners[k] = (uint32_t)r.i;
-            else { L->list_over = 1; L->mode = 0; L->cut.active = 0; }   // the whole-table sweep instead
-        }
-    LF_LINES_END
-}
-// an owner's walk (k_gc_clusters' from its first hole): doomed entries and
-// tombstones emptied, every live entry after a hole moved to the first EMPTY slot
-// in [home, j); a line that receives an entry lowers its floor to the entry's
-__global__ __launch_bounds__(BLOCK) void k_lf_walk(gf_htab_desc d, uint32_t mode, LruDev *L, const uint32_t *owners) {
-    if (!L->flag || L->mode != 1 || !L->cut.active || L->list_over) return;
-    const GcCut cut = L->cut;
-    const uint32_t no = L->cb_need;
-    const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
-    uint32_t dead = 0, tombs = 0;
-    for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < no; o += gridDim.x * blockDim.x) {
-        uint64_t j = owners[o];
-        bool hole = false;
-        for (;;) {
-            uint8_t *sl = d.slots + j * d.slot_size;
-            const uint32_t st = sl[d.ksz];
-            if (st == GF_SLOT_EMPTY) break;
-            if (st == GF_SLOT_TOMB) {
-                sl[d.ksz] = GF_SLOT_EMPTY;
-                tombs++;
-                hole = true;
-            } else {
-                const uint8_t *v = ht_val(d, j);
-                const uint32_t lt = *reinterpret_cast<const uint32_t *>(v);
-                const uint32_t fl = *reinterpret_cast<const uint16_t *>(v + 4);
-                if (gc_kill(lt, fl, cut)) {
-                    sl[d.ksz] = GF_SLOT_EMPTY;
-                    dead++;
-                    hole = true;
-                } else if (hole) {
-                    const uint64_t home = lru_home(d, j, mode);
-                    for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
-                        if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) {
-                            gc_move(d, j, p, vstride);
-                            atomicMin(d.lfloor + (p * d.slot_size >> 7), lf_enc(lt, fl));
-                            break;
-                        }
-                    }
-                }
-            }
-            j = (j + 1) & d.mask;
-        }
-    }
-    if (dead) atomicAdd(&L->res[0], (unsigned long long)dead);
-    if (tombs) atomicAdd(&L->res[1], (unsigned long long)tombs);
-}
-// the listed lines' floors from their entries after the walks (a line left
-// empty: the class-1 floor of `now`); all lines in a full sweep (all = true)
-template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_lf_refloor(gf_htab_desc d, uint32_t now, LruDev *L, const uint32_t *list,
-                                                      bool all) {
-    if (!L->flag || (all ? L->mode != 0 : (L->mode != 1 || !L->cut.active || L->list_over))) return;
-    const uint64_t n = all ? (d.mask + 1) * d.slot_size / 128u : L->nlist;
-    LF_LINES_BEGIN(n)
-        const uint32_t line = have ? (all ? (uint32_t)li : list[li]) : 0u;
-        const LfSlot r = lf_read<KIND>(d, line, have, now);
-        uint32_t e = r.live ? lf_enc(r.lt, r.fl) : ~0u;
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) e = min(e, (uint32_t)__shfl_xor((int)e, o));
-        if (have && (threadIdx.x & 7u) == 0)
-            d.lfloor[line] = e != ~0u ? e : (1u << 31) | (uint32_t)(((unsigned long long)now + 43200ull) >> 1);
-    LF_LINES_END
-}
 __global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L) {
     if (!L->cut.active) return;
-    L->stats[0]++;
-    if (L->mode == 1) { L->stats[1]++; L->stats[2] += L->nlist; }
-    else if (L->tried) L->stats[3]++;
     const unsigned long long ev = L->res[0];
     *count = (uint32_t)(*count - ev);
     const uint32_t k = L->nlog;
@@ -3980,7 +3665,6 @@ __device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int 
         fl |= F_TX_CLOSING;
         if ((fl & F_RX_CLOSING) && (fl & F_TX_CLOSING)) life = now + 10u;
     }
-    lf_touch_closing(d, (uint64_t)f, hot.y & 0xffffu, fl);
     hot.x = life;
     hot.y = (hot.y & 0xffff0000u) | fl;
     gstore<uint4>(e, hot);
@@ -5516,37 +5200,11 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     ProfScope ps("k_lru_evict", s);
     if ((d.mask + 1) % 32) return -EIO;                  // k_lru_clusters' word walk (LRU maps: >= 64, 2^k)
     hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, (const uint32_t *)d.count, m->max_entries, L);
-    const int kind = (d.slot_size == 32 && d.ksz == 14 && d.vin && d.voff + lt_off == 16) ? 1
-                   : (d.slot_size == 64 && d.ksz == 40 && d.vin && d.voff + lt_off == 48) ? 2 : 0;
-    // partial sweep over the age floors (LRU CT maps of the CT layouts); it leaves
-    // L->mode = 0 (the whole-table sweep below runs instead) when it cannot decide
-    static const bool no_floors = getenv("GF_LRU_FULL") != nullptr;   // diagnosis: always the whole table
-    const bool part = kind && d.lfloor && m->d_lflist.p && !no_floors;
-    const uint64_t nl = (d.mask + 1) * d.slot_size / 128u;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(m->d_lflist.bytes / 8, 0xffffffffu);
-    uint32_t *list = (uint32_t *)m->d_lflist.p, *owners = list ? list + cap : nullptr;
-    const uint32_t gl = resident_blocks(8);
-    if (part) {
-        hipLaunchKernelGGL(k_lf_hist, dim3((uint32_t)std::min<uint64_t>((nl + BLOCK - 1) / BLOCK, gl)), dim3(BLOCK), 0, s,
-                           (const uint32_t *)d.lfloor, nl, now, L);
-        hipLaunchKernelGGL(k_lf_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, L);
-        hipLaunchKernelGGL(k_lf_list, dim3((uint32_t)std::min<uint64_t>((nl + BLOCK - 1) / BLOCK, gl)), dim3(BLOCK), 0, s,
-                           (const uint32_t *)d.lfloor, nl, now, L, list, cap);
-        if (kind == 1) hipLaunchKernelGGL(k_lf_scan<1>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list);
-        else hipLaunchKernelGGL(k_lf_scan<2>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list);
-        hipLaunchKernelGGL(k_lf_cut2, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, L);
-        if (kind == 1) hipLaunchKernelGGL(k_lf_fine<1>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list);
-        else hipLaunchKernelGGL(k_lf_fine<2>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list);
-        hipLaunchKernelGGL(k_lf_cut3, dim3(1), dim3(64), 0, s, now, L);
-        if (kind == 1) hipLaunchKernelGGL(k_lf_owners<1>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, owners, cap);
-        else hipLaunchKernelGGL(k_lf_owners<2>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, owners, cap);
-    }
-    // the whole table (L->mode == 0): the first sweep, a fallback, or no floors
     const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + GF_LRU_HB * GF_LRU_U - 1) / (GF_LRU_HB * GF_LRU_U),
                                                      resident_blocks(2));   // 48 KB of LDS a block
-    if (kind == 1)
+    if (d.slot_size == 32 && d.ksz == 14 && d.vin && d.voff + lt_off == 16)
         hipLaunchKernelGGL(k_lru_hist<1>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
-    else if (kind == 2)
+    else if (d.slot_size == 64 && d.ksz == 40 && d.vin && d.voff + lt_off == 48)
         hipLaunchKernelGGL(k_lru_hist<2>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
     else
         hipLaunchKernelGGL(k_lru_hist<0>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
@@ -5554,16 +5212,6 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     const uint64_t nw = (d.mask + 1) / 32;
     hipLaunchKernelGGL(k_lru_clusters, dim3((uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, resident_blocks(8))),
                        dim3(BLOCK), 0, s, d, m->ht.mode, (const uint32_t *)codes, (const uint32_t *)bits, L);
-    if (part || (kind && d.lfloor)) {
-        // floors: every line after a whole-table sweep; the scanned lines after a partial one
-        if (kind == 1) hipLaunchKernelGGL(k_lf_refloor<1>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, true);
-        else hipLaunchKernelGGL(k_lf_refloor<2>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, true);
-    }
-    if (part) {
-        hipLaunchKernelGGL(k_lf_walk, dim3(gl), dim3(BLOCK), 0, s, d, m->ht.mode, L, (const uint32_t *)owners);
-        if (kind == 1) hipLaunchKernelGGL(k_lf_refloor<1>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, false);
-        else hipLaunchKernelGGL(k_lf_refloor<2>, dim3(gl), dim3(BLOCK), 0, s, d, now, L, (const uint32_t *)list, false);
-    }
     hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
     static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
     if (stats) {
@@ -6037,7 +5685,6 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     cnt = cnt >= r[0] ? cnt - (uint32_t)r[0] : 0u;
     if (hip_ok(hipMemcpy(m->d_count.p, &cnt, 4, hipMemcpyHostToDevice), "gc count")) return -EIO;
     m->dev_count_hi = cnt;
-    m->lf_clear_all(s);                                 // the sweep moved entries between lines
     m->device_modified();
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
@@ -6056,21 +5703,6 @@ int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max) {
     const uint32_t k = std::min(std::min(n, GF_LRU_LOGCAP), max);
     if (k && hip_ok(hipMemcpy(out, L->log, (size_t)k * sizeof(LruLog), hipMemcpyDeviceToHost), "evict log")) return -EIO;
     return (int)std::min<uint32_t>(n, 0x7fffffffu);
-}
-
-int gf_ct_lru_stats(int map, uint64_t out[4]) {
-    auto m = get_map(map);
-    if (!m) return -EBADF;
-    if (!out) return -EFAULT;
-    std::lock_guard<std::recursive_mutex> mg(m->mu);
-    for (int k = 0; k < 4; k++) out[k] = 0;
-    if (!m->d_lru.p) return 0;
-    if (hip_ok(hipDeviceSynchronize(), "lru stats sync")) return -EIO;
-    LruDev *L = (LruDev *)m->d_lru.p;
-    unsigned long long v[4];
-    if (hip_ok(hipMemcpy(v, L->stats, sizeof v, hipMemcpyDeviceToHost), "lru stats")) return -EIO;
-    for (int k = 0; k < 4; k++) out[k] = v[k];
-    return 0;
 }
 
 }  // extern "C"
@@ -6214,7 +5846,6 @@ int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n
     if (fl[0] || fl[1]) return 0;                        // duplicates / EEXIST: the sequential host path
     hipLaunchKernelGGL(k_bulk_insert, dim3(g), dim3(BLOCK), 0, s, d, m.ht.codec, (const uint8_t *)dk.p,
                        (const uint8_t *)dv.p, (const uint32_t *)dh.p, n);
-    m.lf_clear_all(s);                                  // loaded entries carry any age
     if (hip_ok(hipGetLastError(), "k_bulk_insert") || hip_ok(hipDeviceSynchronize(), "bulk sync")) return -EIO;
     m.host_valid = false;
     m.dev_gen++;

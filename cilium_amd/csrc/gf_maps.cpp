@@ -326,15 +326,9 @@ int Map::push(hipStream_t s) {
     // LRU conntrack maps: the eviction sweep's 4-B code per slot (k_lru_hist ->
     // k_lru_clusters), allocated with the slots so its cost shows at the push and
     // a classify call never fails on it after its inserts are on the device
-    if (type == GF_MAP_TYPE_LRU_HASH && ht.codec == GF_VCODEC_CT) {
-        if (d_lrucodes.bytes < ht.nslots * 4 && (r = d_lrucodes.ensure(ht.nslots * 4))) return r;
-        // age floors (one u32 per 128-B line, 0 = unknown: the next sweep scans the
-        // line) and the partial sweep's line list (half of the lines at most)
-        const uint64_t nl = std::max<uint64_t>(1, ht.nslots * ht.slot_size / 128), cap = std::max<uint64_t>(nl / 2, 65536);
-        if (d_lfloor.bytes < nl * 4 && (r = d_lfloor.ensure(nl * 4))) return r;
-        if (d_lflist.bytes < cap * 8 && (r = d_lflist.ensure(cap * 8))) return r;   // lines | cluster owners
-        if (hip_ok(hipMemsetAsync(d_lfloor.p, 0, d_lfloor.bytes, s), "memset floors")) return -EIO;
-    }
+    if (type == GF_MAP_TYPE_LRU_HASH && ht.codec == GF_VCODEC_CT && d_lrucodes.bytes < ht.nslots * 4 &&
+        (r = d_lrucodes.ensure(ht.nslots * 4)))
+        return r;
     if (ht.slots.empty()) {
         if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
         if (ht.sstride && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
@@ -447,7 +441,6 @@ gf_htab_desc Map::hdesc() {
     d.ksz = ksz; d.vsz = vsz; d.slot_size = ht.slot_size; d.voff = ht.voff;
     d.split = ht.split; d.max_entries = max_entries;
     d.vin = ht.vin; d.sstride = ht.sstride;
-    d.lfloor = (uint32_t *)d_lfloor.p;
     return d;
 }
 
@@ -512,17 +505,6 @@ int Map::dev_get_val(uint64_t i, uint8_t *ext) {
     return 0;
 }
 
-// An API write can give a slot any age (an older lifetime, a closing flag): the
-// LRU age floor of its 128-B line is cleared (the next sweep scans the line).
-int Map::lf_clear(uint64_t slot) {
-    if (!d_lfloor.p) return 0;
-    const uint32_t z = 0;
-    return dev_wr(*this, (uint8_t *)d_lfloor.p + (slot * ht.slot_size / 128) * 4, &z, 4);
-}
-void Map::lf_clear_all(hipStream_t s) {
-    if (d_lfloor.p) (void)hip_ok(hipMemsetAsync(d_lfloor.p, 0, d_lfloor.bytes, s), "clear floors");
-}
-
 int Map::dev_put_val(uint64_t i, const uint8_t *ext) {
     std::vector<uint8_t> inb(vsz);
     uint8_t *in = inb.data();
@@ -531,7 +513,6 @@ int Map::dev_put_val(uint64_t i, const uint8_t *ext) {
     int r;
     if (ht.vin && (r = dev_wr(*this, (uint8_t *)d_slots.p + i * ht.slot_size + ht.voff, in, ht.vin))) return r;
     if (ht.vin < vsz && (r = dev_wr(*this, (uint8_t *)d_vals.p + i * ht.sstride, in + ht.vin, vsz - ht.vin))) return r;
-    if ((r = lf_clear(i))) return r;
     dev_gen++;
     return 0;
 }
@@ -607,7 +588,6 @@ static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t
                                        m.vsz - m.ht.vin)))
         return r;
     if ((r = dev_wr(m, (uint8_t *)m.d_slots.p + (uint64_t)ins * ss, sl.data(), ss))) return r;
-    if ((r = m.lf_clear((uint64_t)ins))) return r;
     m.dev_gen++;
     return m.dev_set_count(c + 1);
 }

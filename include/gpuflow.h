@@ -502,12 +502,6 @@ typedef struct gf_ct_evict_rec {
 } gf_ct_evict_rec;
 /* Copies up to max records (oldest first) and returns the number logged. */
 int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max);
-/* How the LRU sweeps of a map ran (a libgpuflow extension, no reference
- * counterpart): out[0] sweeps that evicted, out[1] of them partial (only the
- * 128-B slot lines whose age floor could hold a victim were read), out[2] lines
- * those partial sweeps read, out[3] partial attempts that fell back to the whole
- * table.  Returns 0 or -errno. */
-int gf_ct_lru_stats(int map, uint64_t out[4]);
 
 /* ---- drop notifications (bpf/lib/drop.h:38-107, DROP_NOTIFY) ----
  * With a ring set, gf_policy_ingress_classify and gf_pipeline_classify append

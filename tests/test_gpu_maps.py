@@ -1,7 +1,6 @@
 """The map API on device-authoritative maps (pkg/bpf/map.go:322-498 semantics on
 the HBM replica, no whole-table pull), per-map locking under concurrent callers,
 and the LRU stand-in of the CT maps — all against the oracle."""
-import ctypes as C
 import errno
 import threading
 import time
@@ -187,19 +186,10 @@ def test_lru_eviction_matches_oracle(seed, dt):
     assert len(ref.lru_log["ct4"]) >= 2 and len(ref.lru_log["ct6"]) >= 1
 
 
-def _lru_stats(fd):
-    from cilium_amd._lib import lib
-    out = (C.c_uint64 * 4)()
-    assert lib.gf_ct_lru_stats(fd, out) == 0
-    return list(out)
-
-
 @pytest.mark.parametrize("seed", [7, 8])
-def test_lru_partial_sweeps_match_oracle(seed):
-    """Many batches over small LRU CT maps: after the first whole-table sweep the
-    sweeps read only the 128-B slot lines whose age floor could hold a victim
-    (gf_ct_lru_stats counts them); every eviction log entry, verdict and CT entry
-    still equals the oracle's whole-table rule."""
+def test_lru_many_sweeps_match_oracle(seed):
+    """Ten batches over small LRU CT maps, a sweep after most of them: every
+    eviction log entry, verdict and CT entry equals the oracle's rule."""
     sc = synth.fuzz(seed=seed, n_packets=16000, n_batches=10, ct_max=2000, ct6_max=400)
     dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
     for bi, pk in enumerate(sc.batches):
@@ -210,8 +200,7 @@ def test_lru_partial_sweeps_match_oracle(seed):
     for name in ("ct4", "ct6"):
         assert dp.dump_map(name) == ref.dump(name), name
         assert _evict_log(dp.fd[name]) == ref.lru_log[name], name
-    st = _lru_stats(dp.fd["ct4"])
-    assert st[0] == len(ref.lru_log["ct4"]) >= 4 and st[1] >= 1, st
+    assert len(ref.lru_log["ct4"]) >= 4
 
 
 def test_concurrent_classify_two_streams():
