@@ -50,6 +50,9 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_ING_MINW
 #define GF_ING_MINW 4       // __launch_bounds__ min waves per SIMD (register budget)
 #endif
+#ifndef GF_ING_MINW6
+#define GF_ING_MINW6 3      // IPv6 buckets: the lane state (RelCache<10>) keeps the block at 3 per CU by LDS
+#endif
 #ifndef GF_ING_BINS_WAVE
 #define GF_ING_BINS_WAVE 0  // k_ing_groups: reason / action bins aggregated over the active lanes (no effect: 2.728 ms both)
 #endif
@@ -62,11 +65,20 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_CT_COOP
 #define GF_CT_COOP 1        // CT4 home lines read by complete lane quads together (ProbeLine::load_quad)
 #endif
+#ifndef GF_EG_COOP
+#define GF_EG_COOP 1        // k_eg_groups: the CT4 home line read by complete lane quads (load_quad)
+#endif
+#ifndef GF_FRONT_MINW
+#define GF_FRONT_MINW 8     // k_pipe_front: __launch_bounds__ min waves per SIMD (64 VGPRs: 1.294 vs 1.410 ms, config 4)
+#endif
+#ifndef GF_EG_DYN
+#define GF_EG_DYN 1         // k_eg_front: LDS rows sized by the snap stride (64-B snaps: half the LDS; 0.586 vs 0.622 ms)
+#endif
 #ifndef GF_REC_NT
 #define GF_REC_NT 0         // k_ing_groups: packet records read with nontemporal loads
 #endif
 #ifndef GF_CT_COOP6
-#define GF_CT_COOP6 0       // the same for CT6 (costs k_ing_groups<6> a wave per SIMD: 165 -> 170 VGPRs)
+#define GF_CT_COOP6 1       // the same for CT6 (168 VGPRs: fits the 3 waves the LDS allows; 1.242 vs 1.252 ms)
 #endif
 #ifndef GF_MEMO4
 #define GF_MEMO4 2          // policy decisions memoised per lane, IPv4 buckets
@@ -936,9 +948,12 @@ struct Ep {
         sl = s;
         const gf_lxc_dev *c = X.cfgs + (s - 1);
         flags = gload<uint32_t>(&c->flags);
-        pol = gload<uint8_t *>(&c->policy.slots);
+        // (diagnosis GF_DIAG & 32: every endpoint reads program 0's policy map — one
+        // L2-resident table instead of 256 in the MALL; verdicts differ)
+        const gf_lxc_dev *pc = (GF_DIAG & 32) ? X.cfgs : c;
+        pol = gload<uint8_t *>(&pc->policy.slots);
         pol_side = gload<uint8_t *>(&c->policy.vals);
-        pol_mask = (uint32_t)gload<uint64_t>(&c->policy.mask);
+        pol_mask = (uint32_t)gload<uint64_t>(&pc->policy.mask);
     }
     __device__ __forceinline__ const gf_lxc_dev *cfg(const IngCtx &X) const { return X.cfgs + (sl - 1); }
     __device__ __forceinline__ gf_htab_desc pdesc() const {
@@ -1136,7 +1151,9 @@ struct PolAcc {
     __device__ __forceinline__ void flush_one(const IngCtx &X, int j) {
         if (sl[j]) {
             uint8_t *side = gload<uint8_t *>(&X.cfgs[sl[j] - 1].policy.vals);
-            uint8_t *c = side + (uint64_t)f[j] * GF_POL_SIDE;
+            // (GF_DIAG & 32: the slot came from program 0's map; counted in the endpoint's own array)
+            const uint32_t fj = (GF_DIAG & 32) ? f[j] & (uint32_t)gload<uint64_t>(&X.cfgs[sl[j] - 1].policy.mask) : f[j];
+            uint8_t *c = side + (uint64_t)fj * GF_POL_SIDE;
             gadd64(c, (unsigned long long)pk[j]);
             gadd64(c + 8, (unsigned long long)by[j]);
         }
@@ -1272,6 +1289,12 @@ __device__ __forceinline__ int policy_ingress(const IngCtx &X, Ep &ep, PolLine &
                                               uint32_t dport, uint32_t proto, uint32_t len, bool v6,
                                               const uint32_t *cidr_addr, uint32_t &ab, PolAcc &acc, PolMemo<N> &m) {
     const uint32_t pk = dport | (proto << 16), sip = v6 ? 0u : cidr_addr[0];
+#if GF_DIAG & 16
+    // diagnosis (ceiling of any policy-map staging): no policy-map read, the counter
+    // update kept on a pseudo-random slot of the endpoint's map; verdicts differ
+    policy_count(X, ep, (int64_t)((identity * 0x9E3779B1u + pk) & ep.pol_mask), len, acc);
+    return TC_OK;
+#endif
     const bool memo_ok = !v6 || identity >= 256;
     const int j = memo_ok ? m.find(ep.sl, identity, pk, sip) : -1;
     if (j >= 0) {
@@ -1404,7 +1427,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     PolLine pl;
     const bool pre = r.src_identity &&
                      (flags & (GF_LXC_F_POLICY_INGRESS | GF_LXC_F_DROP_ALL)) == GF_LXC_F_POLICY_INGRESS &&
-                     !pm.hit(ep.sl, r.src_identity, (t[2] >> 16) | (nh << 16), r.saddr);
+                     !pm.hit(ep.sl, r.src_identity, (t[2] >> 16) | (nh << 16), r.saddr) && !(GF_DIAG & (4 | 16));
     if (pre) pl.load(ep.pdesc(), pol_home(r.src_identity, 0u, 0u));
     bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     CtState st{0, 0, 0};
@@ -1728,19 +1751,43 @@ __device__ __forceinline__ void flush_added(const IngCtx &X, uint32_t fam_bit, i
     if (threadIdx.x == 0 && *lds_added && ct_count) atomicAdd(ct_count, *lds_added);
 }
 
-// Schedule words (device): hist[2][GF_LCAP+1] | base[2][..] | cursor[2][..] |
-// nruns | queue[2] | nfam[2] (buckets per family; family 1's order follows 0's).
+// Bucket lists: family (IPv4 / IPv6 CT path) x endpoint class.  A bucket's class
+// is its first packet's endpoint slot mod GF_NCLS (a scheduling hint only: a bucket
+// is still one lane's, whole); the lanes of workgroup b start on the lists of class
+// b mod GF_NCLS — the XCD the workgroup runs on, dispatch being round-robin over the
+// 8 XCDs — and move to the other classes' lists when theirs is drained, so that an
+// XCD's L2 would hold the policy maps of its class of endpoints only.  Measured with
+// 8 classes: k_ing_groups 2.90 vs 2.40 ms on config 2 — most likely because a
+// wave's 64 buckets are no longer neighbours in key order, so their CT home lines
+// (placed by the same pair hash) no longer share pages — so one class (the plain
+// longest-first list) stays.
+#ifndef GF_NCLS
+#define GF_NCLS 1u
+#endif
+#define GF_NL (2u * GF_NCLS)
+// Schedule words (device): hist[GF_NL][GF_LCAP+1] | base[..] | cursor[..] | nruns |
+// queue[GF_NL] | nfam[2] | lcnt[GF_NL] | lstart[GF_NL] (lists in order: family 0's
+// classes, then family 1's; each list by bucket size, descending).
 #define GF_LCAP 1024u
 #define GF_SCHED_HIST(p) (p)
-#define GF_SCHED_BASE(p) ((p) + 2 * (GF_LCAP + 1))
-#define GF_SCHED_CURSOR(p) ((p) + 4 * (GF_LCAP + 1))
-#define GF_SCHED_NRUNS(p) ((p) + 6 * (GF_LCAP + 1))
-#define GF_SCHED_QUEUE(p) ((p) + 6 * (GF_LCAP + 1) + 1)
-#define GF_SCHED_NFAM(p) ((p) + 6 * (GF_LCAP + 1) + 3)
-#define GF_SCHED_WORDS (6 * (GF_LCAP + 1) + 5)
+#define GF_SCHED_BASE(p) ((p) + GF_NL * (GF_LCAP + 1))
+#define GF_SCHED_CURSOR(p) ((p) + 2 * GF_NL * (GF_LCAP + 1))
+#define GF_SCHED_NRUNS(p) ((p) + 3 * GF_NL * (GF_LCAP + 1))
+#define GF_SCHED_QUEUE(p) (GF_SCHED_NRUNS(p) + 1)
+#define GF_SCHED_NFAM(p) (GF_SCHED_QUEUE(p) + GF_NL)
+#define GF_SCHED_LCNT(p) (GF_SCHED_NFAM(p) + 2)
+#define GF_SCHED_LSTART(p) (GF_SCHED_LCNT(p) + GF_NL)
+#define GF_SCHED_WORDS (3 * GF_NL * (GF_LCAP + 1) + 1 + GF_NL + 2 + 2 * GF_NL)
+#define GF_SCHED_HBYTES (GF_NL * (GF_LCAP + 1) * 4)    // the block-local bins of k_bucket_hist / order (dynamic LDS)
+// The list of a bucket: family from its key, class from its first packet's record.
+__device__ __forceinline__ uint32_t sched_list(uint32_t key, const gf_rec *rec, const uint32_t *perm, uint32_t b) {
+    const uint32_t f = key >> (GF_KEY_BITS - 1);
+    const uint32_t x = rec ? (uint32_t)rec[perm[b]].ep % GF_NCLS : 0u;
+    return f * GF_NCLS + x;
+}
 
 template <int FAM>
-__global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
+__global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
                                                       const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
                                                       unsigned long long *stats) {
@@ -1752,13 +1799,18 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
     Stats st{sl};
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
-    const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
-    if (F) order += nfam[0];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t *lcnt = GF_SCHED_LCNT(sched), *lstart = GF_SCHED_LSTART(sched);
     __shared__ Lane<FAM> lanes[BLOCK];
     Lane<FAM> &ln = lanes[threadIdx.x];
     ln.init();
     uint32_t *const rlog = X.rlog && !(X.rlog_off && *X.rlog_off) ? X.rlog : nullptr;
+    const uint32_t x0 = blockIdx.x % GF_NCLS;           // this workgroup's XCD class first
+    for (uint32_t xi = 0; xi < GF_NCLS; xi++) {
+    const uint32_t L = F * GF_NCLS + (x0 + xi) % GF_NCLS;
+    uint32_t *queue = GF_SCHED_QUEUE(sched) + L;
+    const uint32_t nb = lcnt[L];
+    const uint2 *lorder = order + lstart[L];
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(queue, 64u);
@@ -1766,7 +1818,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
         if (base >= nb) break;
         const uint32_t t = base + lane;
         if (t >= nb) continue;
-        const uint2 oc = order[t];
+        const uint2 oc = lorder[t];
         const uint32_t b = oc.x, c = oc.y;
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
@@ -1794,6 +1846,7 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
             if (k + 1 < c) r = ld_rec(rec, i);
         }
     }
+    }
     ln.acc.flush(X);
     if (stats) ln.sc.fold(st);
     flush_added(X, F ? 2u : 1u, ln.added, ct_count, &sadd);
@@ -1807,34 +1860,38 @@ __global__ __launch_bounds__(BLOCK, GF_ING_MINW) void k_ing_groups(IngCtx X, uin
 // off[q]: the start of run q in the sorted keys (nruns of them); its length is
 // the distance to the next start (or to n).
 __global__ __launch_bounds__(BLOCK) void k_bucket_hist(uint32_t n, const uint32_t *off, const uint32_t *skeys,
-                                                       uint32_t *sched) {
-    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
+                                                       const gf_rec *rec, const uint32_t *perm, uint32_t *sched) {
+    extern __shared__ uint32_t h[];                     // GF_SCHED_HBYTES
+    for (uint32_t k = threadIdx.x; k < GF_NL * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
     uint32_t nq = *GF_SCHED_NRUNS(sched);
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         const uint32_t key = skeys[off[q]];
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
-        if (c && key != GF_KEY_SKIP) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q];
+        if (c && key != GF_KEY_SKIP)
+            atomicAdd(&h[sched_list(key, rec, perm, off[q]) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
     uint32_t *hist = GF_SCHED_HIST(sched);
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
+    for (uint32_t k = threadIdx.x; k < GF_NL * (GF_LCAP + 1); k += blockDim.x)
         if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-// base[f][c] = start of (family f, count c) in the order list: family 0 first,
-// each family by count descending.  One block of GF_LCAP threads (thread k owns
-// bin c = GF_LCAP - k); also clears the cursors and the work queues.
+// base[l][c] = start of (list l, count c) in the order array: the lists one after
+// the other, each by count descending.  One block of GF_LCAP threads (thread k owns
+// bin c = GF_LCAP - k); also clears the cursors and the work queues and writes each
+// list's count and start and each family's total.
 __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
     __shared__ uint32_t s[GF_LCAP];
-    __shared__ uint32_t tot0;
+    __shared__ uint32_t tot;
     const uint32_t k = threadIdx.x, c = GF_LCAP - k;
     const uint32_t *hist = GF_SCHED_HIST(sched);
     uint32_t *base = GF_SCHED_BASE(sched), *cursor = GF_SCHED_CURSOR(sched);
-    for (uint32_t f = 0; f < 2; f++) {
-        const uint32_t *hf = hist + f * (GF_LCAP + 1);
+    if (k == 0) { tot = 0; GF_SCHED_NFAM(sched)[0] = GF_SCHED_NFAM(sched)[1] = 0; }
+    __syncthreads();
+    for (uint32_t l = 0; l < GF_NL; l++) {
+        const uint32_t *hf = hist + l * (GF_LCAP + 1);
         s[k] = hf[c];
         __syncthreads();
         for (uint32_t d = 1; d < GF_LCAP; d <<= 1) {    // inclusive scan over bins GF_LCAP .. 1
@@ -1843,15 +1900,17 @@ __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
             s[k] += v;
             __syncthreads();
         }
-        uint32_t add = f ? tot0 : 0u;
-        base[f * (GF_LCAP + 1) + c] = add + s[k] - hf[c];
-        cursor[f * (GF_LCAP + 1) + c] = 0;
-        if (k == 0) { base[f * (GF_LCAP + 1)] = 0; cursor[f * (GF_LCAP + 1)] = 0; }
+        const uint32_t add = tot;
+        base[l * (GF_LCAP + 1) + c] = add + s[k] - hf[c];
+        cursor[l * (GF_LCAP + 1) + c] = 0;
+        if (k == 0) { base[l * (GF_LCAP + 1)] = add; cursor[l * (GF_LCAP + 1)] = 0; }
         __syncthreads();
         if (k == GF_LCAP - 1) {
-            GF_SCHED_NFAM(sched)[f] = s[k];
-            if (!f) tot0 = s[k];
-            GF_SCHED_QUEUE(sched)[f] = 0;
+            GF_SCHED_LCNT(sched)[l] = s[k];
+            GF_SCHED_LSTART(sched)[l] = add;
+            GF_SCHED_NFAM(sched)[l / GF_NCLS] += s[k];
+            GF_SCHED_QUEUE(sched)[l] = 0;
+            tot = add + s[k];
         }
         __syncthreads();
     }
@@ -1861,9 +1920,10 @@ __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
 // family 0 then 1, each by count descending (ties in any order): block-local
 // counts per bin, one global reservation per (block, bin).
 __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32_t *off, const uint32_t *skeys,
-                                                        uint32_t *sched, uint2 *order) {
-    __shared__ uint32_t h[2 * (GF_LCAP + 1)];
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
+                                                        const gf_rec *rec, const uint32_t *perm, uint32_t *sched,
+                                                        uint2 *order) {
+    extern __shared__ uint32_t h[];                     // GF_SCHED_HBYTES
+    for (uint32_t k = threadIdx.x; k < GF_NL * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
     uint32_t nq = *GF_SCHED_NRUNS(sched);
     const uint32_t *base = GF_SCHED_BASE(sched);
@@ -1871,18 +1931,20 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
     uint32_t b0 = blockIdx.x * GF_SCHED_ITEMS;
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         const uint32_t key = skeys[off[q]];
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
-        if (c && key != GF_KEY_SKIP) atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q];
+        if (c && key != GF_KEY_SKIP)
+            atomicAdd(&h[sched_list(key, rec, perm, off[q]) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < 2 * (GF_LCAP + 1); k += blockDim.x)
+    for (uint32_t k = threadIdx.x; k < GF_NL * (GF_LCAP + 1); k += blockDim.x)
         if (h[k]) h[k] = base[k] + atomicAdd(&cursor[k], h[k]);
     __syncthreads();
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         const uint32_t key = skeys[off[q]];
-        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q], f = key >> (GF_KEY_BITS - 1);
+        uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q];
         if (c && key != GF_KEY_SKIP)
-            order[atomicAdd(&h[f * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] = make_uint2(off[q], c);
+            order[atomicAdd(&h[sched_list(key, rec, perm, off[q]) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] =
+                make_uint2(off[q], c);
     }
 }
 
@@ -2024,7 +2086,7 @@ __device__ int pipe_netdev(const NetdevDev &N, Row &w, const PktHdr &h, uint32_t
 // bytes of dynamic shared memory) and copied back out only when the caller
 // asked for the rewritten frames.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_pipe_front(gf_frames fr, const uint8_t *tc_index, const uint32_t *flow_hash,
+__global__ __launch_bounds__(NT, GF_FRONT_MINW) void k_pipe_front(gf_frames fr, const uint8_t *tc_index, const uint32_t *flow_hash,
                                                       PipeDev P, const uint16_t *slot_of, gf_rec *rec, uint32_t *keys,
                                                       uint8_t *s6out, uint8_t *d6out, gf_pipeline_out *out,
                                                       uint8_t *nd6, uint8_t *snap_out, unsigned long long *stats) {
@@ -3265,7 +3327,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
                                                     unsigned long long *stats) {
     __shared__ uint32_t sl[272];
-    __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
+    extern __shared__ uint4 lds[];                      // BLOCK * eg_stage_bytes(S) (FAM 6: none)
     Stats st{sl};
     if (stats) st.init();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -3285,7 +3347,7 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
         for (uint32_t k = threadIdx.x; k < nv; k += BLOCK) lds[k] = g[k];
         __syncthreads();
     }
-    uint8_t *row = reinterpret_cast<uint8_t *>(lds) + (FAM == 6 ? 0 : threadIdx.x * (coop ? S : GF_EG_STAGE));
+    uint8_t *row = reinterpret_cast<uint8_t *>(lds) + (FAM == 6 ? 0 : threadIdx.x * (coop ? S : eg_stage_bytes(S)));
     const uint8_t *hdr = coop ? row : src;
     const bool v6 = i < fr.n && len >= 14 && fbyte(hdr, cap0, 12) == 0x86 && fbyte(hdr, cap0, 13) == 0xDD;
     bool scnt = false;                                        // the lane's counter-block entry
@@ -3763,7 +3825,16 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
     const bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     uint32_t tf[4] = {t[1], t[0], (t[2] >> 16) | (t[2] << 16), nh | ((tfl ^ 1u) << 8)};
     bool isb = false;
+#if GF_EG_COOP
+    // the home line read by the lane quad together (the egress CT4 holds 2^28 slots, 8 GB)
+    ProbeLine<14, GF_CT4_U, 4> cl;
+    cl.load_quad(ct, key_hash<14, GF_HASH_CT>(t));
+    const ProbeRes pr = probe2<14, GF_CT4_U, 4>(ct, t, tf, cl, true);
+    const int64_t f = pr.f;
+    isb = pr.is_b;
+#else
     const int64_t f = ht_find2<14, GF_CT4_U>(ct, t, tf, key_hash<14, GF_HASH_CT>(t), &isb);
+#endif
     ab += 14;
     CtState st{0, 0, 0};
     int ret;
@@ -4133,10 +4204,10 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
     uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
     const uint32_t K = eg_stage_bytes(E.stride);
     constexpr int F = FAM == 6 ? 1 : 0;
-    const uint32_t *nfam = GF_SCHED_NFAM(sched);
-    const uint32_t nb = nfam[F], lane = threadIdx.x & 63u;
-    uint32_t *queue = GF_SCHED_QUEUE(sched) + F;
-    if (F) order += nfam[0];
+    // the from-container pass schedules without records: every bucket is in class 0
+    const uint32_t nb = GF_SCHED_LCNT(sched)[F * GF_NCLS], lane = threadIdx.x & 63u;
+    uint32_t *queue = GF_SCHED_QUEUE(sched) + F * GF_NCLS;
+    order += GF_SCHED_LSTART(sched)[F * GF_NCLS];
     const bool seq = *E.seq != 0;
     const bool rlog = FAM == 4 && E.conn && !seq && !*E.cflag;   // connection groups: related entries logged
     int added = 0;
@@ -4917,7 +4988,9 @@ __global__ __launch_bounds__(BLOCK) void k_run_write(uint32_t n, const uint32_t 
         __syncthreads();
     }
 }
-static int schedule_groups(uint32_t n, hipStream_t s) {
+// rec: the packets' handle_policy records (the bucket's endpoint class), or null
+// (every bucket in class 0: the egress from-container pass).
+static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullptr) {
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
@@ -4947,13 +5020,21 @@ static int schedule_groups(uint32_t n, hipStream_t s) {
     }
     {
         ProfScope ps("k_bucket_sched", s);
-        if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, 2 * (GF_LCAP + 1) * 4, s), "memset hist")) return -EIO;
+        if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, GF_SCHED_HBYTES, s), "memset hist")) return -EIO;
+        static const bool lds_ok = [] {                  // the bins are > 64 KB of dynamic LDS
+            return hipFuncSetAttribute((const void *)k_bucket_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)GF_SCHED_HBYTES) == hipSuccess &&
+                   hipFuncSetAttribute((const void *)k_bucket_order, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)GF_SCHED_HBYTES) == hipSuccess;
+        }();
+        if (!lds_ok) return hip_ok(hipErrorInvalidValue, "k_bucket_sched LDS");
         uint32_t g = (n + GF_SCHED_ITEMS - 1) / GF_SCHED_ITEMS;
-        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.off.p,
-                           (const uint32_t *)w.skeys.p, d_sched);
+        const gf_rec *lrec = GF_NCLS > 1 ? rec : nullptr;
+        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
+                           (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched);
         hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
-        hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), 0, s, n, (const uint32_t *)w.off.p,
-                           (const uint32_t *)w.skeys.p, d_sched, (uint2 *)w.order.p);
+        hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
+                           (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched, (uint2 *)w.order.p);
     }
     return hip_ok(hipGetLastError(), "k_bucket_sched");
 }
@@ -5278,7 +5359,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
     host_mark("pack");
-    if (!prepared && (r = schedule_groups(n, s))) return r;
+    if (!prepared && (r = schedule_groups(n, s, (const gf_rec *)w.rec.p))) return r;
     host_mark("sched");
     uint32_t *d_sched = (uint32_t *)w.sched.p;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
@@ -5367,7 +5448,7 @@ static int ingress_prepare(const std::shared_ptr<PolicyArray> &a, const gf_pkt_c
                            (const uint16_t *)a->d_slot_of_lxc.p, (gf_rec *)w.rec.p, (uint32_t *)w.keys.p);
         if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
-    return schedule_groups(n, s);
+    return schedule_groups(n, s, (const gf_rec *)w.rec.p);
 }
 
 // The stream that builds the next batch's schedule, and the events between the two.
@@ -6144,9 +6225,11 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     Workspace &w = ws();
     {
         ProfScope ps("k_eg_front", s);
-        hipLaunchKernelGGL(k_eg_front<4>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
+        // the IPv4 kernel's LDS rows: one per lane, the staged header bytes (<= GF_EG_STAGE)
+        const uint32_t eg_lds = GF_EG_DYN ? BLOCK * std::min<uint32_t>(S, GF_EG_STAGE) : BLOCK * GF_EG_STAGE;
+        hipLaunchKernelGGL(k_eg_front<4>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), eg_lds, s, fr, b->lxc_id, b->flow_hash,
                            E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
-        hipLaunchKernelGGL(k_eg_front<6>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, fr, b->lxc_id, b->flow_hash,
+        hipLaunchKernelGGL(k_eg_front<6>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 16, s, fr, b->lxc_id, b->flow_hash,
                            E, (EgRec *)ew.erec.p, (uint32_t *)w.keys.p, out, fsink);
         hipLaunchKernelGGL(k_eg_seq_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint32_t *)ew.seq.p,
                            (const uint32_t *)E.cflag, (const uint32_t *)E.keysP, n, (uint32_t *)w.keys.p);

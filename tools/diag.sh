@@ -2,7 +2,9 @@
 # Ablation timing of k_ing_groups: builds libgpuflow variants with parts of the
 # per-packet work compiled out (results are NOT valid verdicts) and times each
 # with bench.py.  Build here:  tools/diag.sh build ;  run on the GPU box: tools/diag.sh run
-#   GF_DIAG bits: 1 no output store, 2 no LDS stats, 4 no policy, 8 no CT create
+#   GF_DIAG bits: 1 no output store, 2 no LDS stats, 4 no policy, 8 no CT create,
+#                 16 no policy-map read (counters kept on a pseudo-random slot),
+#                 32 every endpoint on program 0's policy map (one L2-resident table)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 VARIANTS=${VARIANTS:-"1 2 4 8 15"}
