@@ -74,6 +74,9 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_EG_DYN
 #define GF_EG_DYN 1         // k_eg_front: LDS rows sized by the snap stride (64-B snaps: half the LDS; 0.586 vs 0.622 ms)
 #endif
+#ifndef GF_EG_LEAN
+#define GF_EG_LEAN 1        // egress: the deferred-entry sets sized by the logged count, empty-family and no-IPv6 blocks skipped
+#endif
 #ifndef GF_REC_NT
 #define GF_REC_NT 0         // k_ing_groups: packet records read with nontemporal loads
 #endif
@@ -3075,6 +3078,7 @@ struct __attribute__((aligned(16))) EgRec {   // 32 B: what the CT part needs fr
 static_assert(sizeof(EgRec) == 32, "EgRec must be 32 bytes");
 struct EgDev {
     const gf_lxc_dev *cfgs;
+    uint8_t *v6blk;                     // per front block: holds an IPv6 frame (k_eg_front<4> writes, <6> reads), or null
     const uint16_t *slot_of;
     gf_htab_desc ct4, ct6, lxc, tunnel;
     const uint32_t *lxset, *tnset;      // cilium_lxc's / the tunnel map's IPv4 keys: address set + slots
@@ -3326,6 +3330,7 @@ template <int FAM>
 __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t *lxc_id, const uint32_t *fhash, EgDev E,
                                                     EgRec *erec, uint32_t *keys, gf_egress_out *out,
                                                     unsigned long long *stats) {
+    if (FAM == 6 && E.v6blk && !E.v6blk[blockIdx.x]) return;   // no IPv6 frame in this block
     __shared__ uint32_t sl[272];
     extern __shared__ uint4 lds[];                      // BLOCK * eg_stage_bytes(S) (FAM 6: none)
     Stats st{sl};
@@ -3350,6 +3355,10 @@ __global__ __launch_bounds__(BLOCK) void k_eg_front(gf_frames fr, const uint16_t
     uint8_t *row = reinterpret_cast<uint8_t *>(lds) + (FAM == 6 ? 0 : threadIdx.x * (coop ? S : eg_stage_bytes(S)));
     const uint8_t *hdr = coop ? row : src;
     const bool v6 = i < fr.n && len >= 14 && fbyte(hdr, cap0, 12) == 0x86 && fbyte(hdr, cap0, 13) == 0xDD;
+    if (FAM == 4 && E.v6blk) {                                // tells k_eg_front<6> which blocks to run
+        const int any6 = __syncthreads_or(v6 ? 1 : 0);
+        if (threadIdx.x == 0) E.v6blk[blockIdx.x] = any6 ? 1u : 0u;
+    }
     bool scnt = false;                                        // the lane's counter-block entry
     uint32_t sreason = 0, saction = 0, slen = 0, sab = 0;
     if (i < fr.n && v6 == (FAM == 6)) {
@@ -4191,6 +4200,7 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
                                                      uint32_t *ct_count, unsigned long long *stats) {
     if (E.hz && *E.hz) return;                          // hazard: the batch reruns in ordered runs
+    if (GF_EG_LEAN && !GF_SCHED_NFAM(sched)[FAM == 6 ? 1 : 0]) return;   // no bucket of this family (nothing to count)
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
     __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
@@ -4310,8 +4320,22 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
 __device__ __forceinline__ bool ctlog_same(const uint32_t *a, const uint32_t *b) {
     return a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && (a[4] & 0xffffu) == (b[4] & 0xffffu);
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, uint2 *tab, uint32_t tmask) {
-    const uint32_t n = *n_;
+// The set is sized for the entries actually logged (<= 1/2 load; the count is on
+// the device) inside an allocation made for the call's upper bound: k_ctlog_size
+// writes the mask, k_ctlog_clear clears only that part.
+__global__ void k_ctlog_size(const uint32_t *n_, uint32_t cap_mask, uint32_t *tm) {
+    const uint64_t want = GF_EG_LEAN ? 2ull * *n_ : (uint64_t)cap_mask + 1;
+    uint32_t t = 1023u;
+    while ((uint64_t)t + 1 < want && t < cap_mask) t = t * 2 + 1;
+    *tm = t < cap_mask ? t : cap_mask;
+}
+__global__ __launch_bounds__(BLOCK) void k_ctlog_clear(uint2 *tab, const uint32_t *tm) {
+    const uint64_t m = *tm;
+    for (uint64_t k = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; k <= m; k += (uint64_t)gridDim.x * BLOCK)
+        tab[k] = make_uint2(0u, 0u);
+}
+__global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, uint2 *tab, const uint32_t *tm) {
+    const uint32_t n = *n_, tmask = *tm;
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
@@ -4324,8 +4348,8 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const u
     }
 }
 __global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, const uint2 *tab,
-                                                       uint32_t tmask, gf_htab_desc ct, uint32_t *ct_count) {
-    const uint32_t n = *n_;
+                                                       const uint32_t *tm, gf_htab_desc ct, uint32_t *ct_count) {
+    const uint32_t n = *n_, tmask = *tm;
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
@@ -5294,6 +5318,10 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     hipLaunchKernelGGL(k_lru_clusters, dim3((uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, resident_blocks(8))),
                        dim3(BLOCK), 0, s, d, m->ht.mode, (const uint32_t *)codes, (const uint32_t *)bits, L);
     hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
+    // the chain leaves the device count at most max_entries (it evicts down to 7/8 of
+    // it when above): a tighter host bound, so ct_limits of the next calls does not
+    // read the count back (a stream sync) while the map runs near its capacity
+    m->dev_count_hi = std::min<uint64_t>(m->dev_count_hi, m->max_entries);
     static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
     if (stats) {
         LruDev h;
@@ -6013,8 +6041,8 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 
 // ---- endpoint egress (from-container) ----
 namespace {
-struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
-             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n;
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ctm, s6, d6,
+             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n, v6blk;
              uint32_t hz_gen = 0, hz_cap = 0;
              uint32_t *h_hz = nullptr;          // pinned: the ordering check's words, read back without a stream sync
              hipEvent_t ev_hz = nullptr;
@@ -6099,15 +6127,19 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
 static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32_t nlog, const gf_htab_desc &ct,
                        uint32_t *ct_count, hipStream_t s) {
     if (!nlog) return 0;
-    uint32_t tmask = 1023;                             // the set at <= 1/2 load
-    while ((uint64_t)tmask + 1 < 2ull * nlog) tmask = tmask * 2 + 1;
-    const size_t tb = (size_t)(tmask + 1) * 8;
+    uint32_t cap = 1023;                               // the set for the bound, at <= 1/2 load
+    while ((uint64_t)cap + 1 < 2ull * nlog) cap = cap * 2 + 1;
+    const size_t tb = (size_t)(cap + 1) * 8;
     if (ew.ckey.bytes < tb && ew.ckey.ensure(tb)) return -ENOMEM;
+    if (ew.ctm.bytes < 4 && ew.ctm.ensure(4)) return -ENOMEM;
     ProfScope ps("k_ctlog_apply", s);
-    if (hip_ok(hipMemsetAsync(ew.ckey.p, 0, tb, s), "ctlog set")) return -EIO;
+    uint32_t *tm = (uint32_t *)ew.ctm.p;
+    hipLaunchKernelGGL(k_ctlog_size, dim3(1), dim3(1), 0, s, d_n, cap, tm);
+    hipLaunchKernelGGL(k_ctlog_clear, dim3(std::min<uint32_t>((cap + BLOCK) / BLOCK, 2048u)), dim3(BLOCK), 0, s,
+                       (uint2 *)ew.ckey.p, (const uint32_t *)tm);
     const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (uint2 *)ew.ckey.p, tmask);
-    hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (const uint2 *)ew.ckey.p, tmask, ct,
+    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (uint2 *)ew.ckey.p, (const uint32_t *)tm);
+    hipLaunchKernelGGL(k_ctlog_apply, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (const uint2 *)ew.ckey.p, (const uint32_t *)tm, ct,
                        ct_count);
     return hip_ok(hipGetLastError(), "k_ctlog_apply");
 }
@@ -6167,6 +6199,8 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
     E.slot_of = (const uint16_t *)a->d_slot_of_lxc.p;
     E.ct4 = cfg_ct4; E.ct6 = cfg_ct6;
+    if ((r = grow(ew.v6blk, (n + BLOCK - 1) / BLOCK))) return r;
+    E.v6blk = GF_EG_LEAN ? (uint8_t *)ew.v6blk.p : nullptr;
     E.s6out = (uint8_t *)ew.s6.p; E.d6out = (uint8_t *)ew.d6.p;
     memcpy(E.router6, node.router_ip6, 16); memcpy(E.host6, node.host_ip6, 16);
     if (lxc) {
@@ -6333,6 +6367,15 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             return r;
         ct4m->device_modified();
         if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
+    }
+    static const bool logstats = getenv("GF_EG_LOGSTATS") != nullptr;   // diagnostics: syncs the stream
+    if (logstats) {
+        uint32_t c[2] = {0, 0}, rc[2] = {0, 0};
+        if (!hip_ok(hipStreamSynchronize(s), "logstats") &&
+            !hip_ok(hipMemcpy(c, ew.ctlog_n.p, 8, hipMemcpyDeviceToHost), "logstats") &&
+            (!conn || !hip_ok(hipMemcpy(rc, d_rn, 8, hipMemcpyDeviceToHost), "logstats")))
+            fprintf(stderr, "[gf] egress n=%u: service-entry log %u, related-entry log %u (fallback %u)\n", n, c[0], rc[0],
+                    rc[1]);
     }
     if (inplace && hip_ok(hipMemcpyAsync(snap_out, wsnap, (size_t)n * S, hipMemcpyDeviceToDevice, s), "snap copy"))
         return -EIO;
