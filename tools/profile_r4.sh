@@ -19,6 +19,7 @@ for C in $CONFIGS; do
   [ "$C" = 4 ] && A="$A --no-h2d"                   # the H2D leg's extra steps would count twice
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks$C" -o run -- \
       python "$R/bench.py" $A > "$O/ks$C.json" 2> "$O/ks$C.err"
+  rm -f "$O/ks$C/run_kernel_trace.csv"              # the stats are kept; the trace would overflow gpurun_out's 64 MiB
   echo "kernel stats config $C done"
   i=0
   for P in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum" \
