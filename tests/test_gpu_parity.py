@@ -291,6 +291,33 @@ def test_pipeline_fuzz(seed, kw):
     assert dp.dump_map("cilium_proxy6") == p6
 
 
+def test_pipeline_dir24_prefilter(monkeypatch):
+    """GF_XDP_DIR24=1 through the pipeline's front (k_pipe_front -> xdp_verdict): the
+    fuzz pipeline with 400 more v4_dyn prefixes (/22-/31, a 16-bit trie root, so the
+    DIR-24-8 tables are read) — records, rewritten frames and CT equal the oracle's."""
+    monkeypatch.setenv("GF_XDP_DIR24", "1")
+    sc = synth.pipeline_fuzz(seed=5, n_packets=20000, n_batches=2)
+    rng = np.random.default_rng(21)
+    pl = rng.integers(22, 32, 400).astype(np.uint32)
+    nets = (np.uint32(synth.ip4("100.64.0.0")) + rng.integers(0, 1 << 18, 400).astype(np.uint32)) & \
+        (~((np.uint32(1) << (32 - pl)) - np.uint32(1))).astype(np.uint32)
+    m = sc.maps["v4_dyn"]
+    keys = np.concatenate([m.keys, synth.lpm4_keys(pl, nets)])
+    vals = np.concatenate([m.vals, np.ones((len(pl), m.vals.shape[1]), m.vals.dtype)])
+    _, first = np.unique(keys, axis=0, return_index=True)
+    m.keys, m.vals = keys[np.sort(first)], vals[np.sort(first)]
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        b = DeviceBatch(pk, parse=False)
+        out, nd6, snap = dp.pipeline(b, sc.now + bi)
+        torch.cuda.synchronize()
+        ro, rn6, rs = ref.pipeline(pk, sc.now + bi)
+        _cmp_struct(to_numpy(out, PIPE_OUT), ro, f"pipeline dir24 b{bi}")
+        assert np.array_equal(snap.cpu().numpy(), rs), f"rewritten frames b{bi}"
+        assert (ro["stage"] == 1).any()
+    assert dp.dump_map("ct4") == ref.dump("ct4")
+
+
 def test_pipeline_checksum_rewrites():
     """Frames with valid checksums through LB translations and port maps: the
     device rewrites equal the oracle's (which keep the checksums valid)."""
