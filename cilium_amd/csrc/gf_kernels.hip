@@ -77,6 +77,10 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #ifndef GF_EG_LEAN
 #define GF_EG_LEAN 1        // egress: the deferred-entry sets sized by the logged count, empty-family and no-IPv6 blocks skipped
 #endif
+#define GF_RUN_ITEMS 4096u  // keys per tile of the run-start / single-bucket count-scan-write passes
+#ifndef GF_SINGLE_ORDER
+#define GF_SINGLE_ORDER 1   // egress passes: single-packet buckets scheduled in packet-index order
+#endif
 #ifndef GF_REC_NT
 #define GF_REC_NT 0         // k_ing_groups: packet records read with nontemporal loads
 #endif
@@ -1924,7 +1928,7 @@ __global__ __launch_bounds__(GF_LCAP) void k_bucket_base(uint32_t *sched) {
 // counts per bin, one global reservation per (block, bin).
 __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32_t *off, const uint32_t *skeys,
                                                         const gf_rec *rec, const uint32_t *perm, uint32_t *sched,
-                                                        uint2 *order) {
+                                                        uint2 *order, uint32_t skip1) {
     extern __shared__ uint32_t h[];                     // GF_SCHED_HBYTES
     for (uint32_t k = threadIdx.x; k < GF_NL * (GF_LCAP + 1); k += blockDim.x) h[k] = 0;
     __syncthreads();
@@ -1935,7 +1939,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         const uint32_t key = skeys[off[q]];
         uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q];
-        if (c && key != GF_KEY_SKIP)
+        if (c && key != GF_KEY_SKIP && !(skip1 && c == 1))
             atomicAdd(&h[sched_list(key, rec, perm, off[q]) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u);
     }
     __syncthreads();
@@ -1945,9 +1949,70 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
     for (uint32_t q = b0 + threadIdx.x; q < b0 + GF_SCHED_ITEMS && q < nq; q += blockDim.x) {
         const uint32_t key = skeys[off[q]];
         uint32_t c = (q + 1 < nq ? off[q + 1] : n) - off[q];
-        if (c && key != GF_KEY_SKIP)
+        if (c && key != GF_KEY_SKIP && !(skip1 && c == 1))
             order[atomicAdd(&h[sched_list(key, rec, perm, off[q]) * (GF_LCAP + 1) + (c < GF_LCAP ? c : GF_LCAP)], 1u)] =
                 make_uint2(off[q], c);
+    }
+}
+// Single-packet buckets in packet-index order (GF_SINGLE_ORDER, the egress passes,
+// whose connection groups are mostly one packet a step): the tail of each family's
+// list (bin c = 1) is filled by packet index, so a wave's lanes read neighbouring
+// records, frames and output rows instead of 64 random ones.  k_single_mark flags
+// each such packet (1 + family) and keeps its bucket start; k_single_count /
+// k_run_scan / k_single_write rank them per family in index order.
+__global__ __launch_bounds__(BLOCK) void k_single_mark(uint32_t n, const uint32_t *off, const uint32_t *skeys,
+                                                       const uint32_t *perm, const uint32_t *sched, uint8_t *sflag,
+                                                       uint32_t *sb) {
+    const uint32_t nq = *GF_SCHED_NRUNS(sched);
+    for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < nq; q += gridDim.x * BLOCK) {
+        const uint32_t b = off[q], key = skeys[b];
+        if ((q + 1 < nq ? off[q + 1] : n) - b != 1u || key == GF_KEY_SKIP) continue;
+        const uint32_t i = perm[b];
+        sflag[i] = (uint8_t)(1u + (key >> (GF_KEY_BITS - 1)));
+        sb[i] = b;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_single_count(uint32_t n, const uint8_t *sflag, uint32_t *t0, uint32_t *t1) {
+    __shared__ uint32_t wc[2][BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u;
+    uint32_t c0 = 0, c1 = 0;
+    for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
+        const uint32_t j = b0 + k * BLOCK + threadIdx.x;
+        const uint32_t f = j < n ? sflag[j] : 0u;
+        c0 += (uint32_t)__popcll(__ballot(f == 1u));
+        c1 += (uint32_t)__popcll(__ballot(f == 2u));
+    }
+    if (lane == 0) { wc[0][threadIdx.x >> 6] = c0; wc[1][threadIdx.x >> 6] = c1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, z = 0;
+        for (uint32_t w = 0; w < BLOCK / 64; w++) { a += wc[0][w]; z += wc[1][w]; }
+        t0[blockIdx.x] = a; t1[blockIdx.x] = z;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_single_write(uint32_t n, const uint8_t *sflag, const uint32_t *sb,
+                                                        const uint32_t *t0, const uint32_t *t1, const uint32_t *sched,
+                                                        uint2 *order) {
+    __shared__ uint32_t wc[2][BLOCK / 64];
+    const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t *base = GF_SCHED_BASE(sched);         // bin c = 1 of family f's list (GF_NCLS == 1)
+    uint32_t p0 = base[0 * (GF_LCAP + 1) + 1] + t0[blockIdx.x], p1 = base[1 * (GF_LCAP + 1) + 1] + t1[blockIdx.x];
+    for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
+        const uint32_t j = b0 + k * BLOCK + threadIdx.x;
+        const uint32_t f = j < n ? sflag[j] : 0u;
+        const uint64_t m0 = __ballot(f == 1u), m1 = __ballot(f == 2u);
+        if (lane == 0) { wc[0][wv] = (uint32_t)__popcll(m0); wc[1][wv] = (uint32_t)__popcll(m1); }
+        __syncthreads();
+        uint32_t e0 = 0, e1 = 0, a0 = 0, a1 = 0;
+        for (uint32_t w = 0; w < BLOCK / 64; w++) {
+            e0 += w < wv ? wc[0][w] : 0u; e1 += w < wv ? wc[1][w] : 0u;
+            a0 += wc[0][w]; a1 += wc[1][w];
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (f == 1u) order[p0 + e0 + (uint32_t)__popcll(m0 & below)] = make_uint2(sb[j], 1u);
+        if (f == 2u) order[p1 + e1 + (uint32_t)__popcll(m1 & below)] = make_uint2(sb[j], 1u);
+        p0 += a0; p1 += a1;
+        __syncthreads();
     }
 }
 
@@ -4414,6 +4479,7 @@ void prof_drain() {
 
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
+    DevBuf sflag, sb, st0, st1;        // single-packet buckets in index order (GF_SINGLE_ORDER)
 };
 // GF_HOST_PROF (diagnosis): the host time of a classify call's phases, one line
 // per call on stderr (where a call waits on the device, or spends its launches).
@@ -4953,7 +5019,6 @@ using GfSortCfg = rocprim::radix_sort_config<
 // Run starts of the sorted keys in three passes over GF_RUN_ITEMS-key tiles:
 // count the starts per tile, scan the tile counts (one block), write each
 // tile's starts at its offset in position order (wave ballots + LDS scan).
-#define GF_RUN_ITEMS 4096u
 __device__ __forceinline__ bool run_start(const uint32_t *k, uint32_t j) { return j == 0 || k[j] != k[j - 1]; }
 __global__ __launch_bounds__(BLOCK) void k_run_count(uint32_t n, const uint32_t *skeys, uint32_t *tcnt) {
     __shared__ uint32_t wc[BLOCK / 64];
@@ -5014,7 +5079,8 @@ __global__ __launch_bounds__(BLOCK) void k_run_write(uint32_t n, const uint32_t 
 }
 // rec: the packets' handle_policy records (the bucket's endpoint class), or null
 // (every bucket in class 0: the egress from-container pass).
-static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullptr) {
+// single: single-packet buckets in packet-index order (the egress passes).
+static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullptr, bool single = false) {
     Workspace &w = ws();
     auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
     int r;
@@ -5057,8 +5123,29 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
         hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
                            (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched);
         hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
+        single = single && GF_SINGLE_ORDER && GF_NCLS == 1;
         hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
-                           (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched, (uint2 *)w.order.p);
+                           (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched, (uint2 *)w.order.p,
+                           single ? 1u : 0u);
+        if (single) {
+            auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
+            const uint32_t nt = (n + GF_RUN_ITEMS - 1) / GF_RUN_ITEMS;
+            int r2;
+            if ((r2 = grow(w.sflag, n)) || (r2 = grow(w.sb, (size_t)n * 4)) || (r2 = grow(w.st0, (size_t)nt * 4 + 16)) ||
+                (r2 = grow(w.st1, (size_t)nt * 4 + 16)))
+                return r2;
+            if (hip_ok(hipMemsetAsync(w.sflag.p, 0, n, s), "single flags")) return -EIO;
+            hipLaunchKernelGGL(k_single_mark, dim3(std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 8192u)), dim3(BLOCK), 0, s, n,
+                               (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, (const uint32_t *)w.perm.p,
+                               (const uint32_t *)d_sched, (uint8_t *)w.sflag.p, (uint32_t *)w.sb.p);
+            hipLaunchKernelGGL(k_single_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
+                               (uint32_t *)w.st0.p, (uint32_t *)w.st1.p);
+            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st0.p, (uint32_t *)w.st0.p + nt);
+            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st1.p, (uint32_t *)w.st1.p + nt);
+            hipLaunchKernelGGL(k_single_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
+                               (const uint32_t *)w.sb.p, (const uint32_t *)w.st0.p, (const uint32_t *)w.st1.p,
+                               (const uint32_t *)d_sched, (uint2 *)w.order.p);
+        }
     }
     return hip_ok(hipGetLastError(), "k_bucket_sched");
 }
@@ -5387,7 +5474,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         if ((r = hip_ok(hipGetLastError(), "k_ing_pack"))) return r;
     }
     host_mark("pack");
-    if (!prepared && (r = schedule_groups(n, s, (const gf_rec *)w.rec.p))) return r;
+    if (!prepared && (r = schedule_groups(n, s, (const gf_rec *)w.rec.p, ta && ta->kind == 2))) return r;
     host_mark("sched");
     uint32_t *d_sched = (uint32_t *)w.sched.p;
     // 4. handle_policy: one bucket per lane, buckets from the longest-first queue
@@ -6295,7 +6382,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             hip_ok(hipEventRecord(ew.ev_hz, s), "hz record"))
             return -EIO;
     }
-    if ((r = schedule_groups(n, s))) return r;           // (reads only the front's keys: harmless on a flagged batch)
+    if ((r = schedule_groups(n, s, nullptr, true))) return r;   // (reads only the front's keys: harmless on a flagged batch)
     uint32_t hz = 0, hz_first = 0;
     host_mark("front+sched");
     if (check) {
