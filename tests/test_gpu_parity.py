@@ -753,3 +753,86 @@ def test_empty_and_ragged_batches():
         assert np.array_equal(snap.cpu().numpy(), rs), f"egress frames n={n}"
     for m in ("ct4", "ct6", "cilium_proxy4", "cilium_proxy6"):
         assert dp.dump_map(m) == ref.dump(m), m
+
+
+def test_classify_argument_checks():
+    """The classify calls' argument checks (the C ABI returns -errno the way the
+    bpf(2) wrappers see the kernel, before anything is launched): a handle of the
+    wrong kind is -EBADF, a missing column or output -EFAULT, a batch over 2^30
+    packets -E2BIG, a frame stride too short for the headers -EINVAL; an empty
+    batch is 0 with null pointers.  No failed call writes an output or changes the
+    CT (gf_kernels.hip check_cols, gf_xdp_classify, gf_lb_classify,
+    gf_policy_ingress_classify, gf_pipeline_classify, gf_lxc_egress_classify)."""
+    import ctypes as C
+    import errno
+    from cilium_amd._lib import lib, gf_frames, gf_pkt_cols, gf_pipe_batch, gf_lxc_batch
+    sc = synth.pipeline_fuzz(seed=44, n_packets=1000, n_batches=1)
+    dp = Datapath(sc, pin_prefix=None)
+    assert dp.xdp_prog and dp.lb_prog and dp.policy_array and dp.pipe
+    b = DeviceBatch(sc.batches[0])
+    torch.cuda.synchronize()
+    n, stride = b.n, b.frames.shape[1]
+    out = torch.full((n, 24), 0xAB, dtype=torch.uint8, device="cuda")
+    nd6 = torch.full((n, 16), 0xAB, dtype=torch.uint8, device="cuda")
+    o, d6 = out.data_ptr(), nd6.data_ptr()
+    ct0 = dp.dump_map("ct4"), dp.dump_map("ct6")
+    now = sc.now
+    c = b.cols()
+
+    def fr(k=n, st=stride, snap=b.frames.data_ptr(), ln=b.len.data_ptr()):
+        return gf_frames(k, st, snap, ln)
+
+    E = lambda e: -getattr(errno, e)
+    # a handle of another kind, or none
+    assert lib.gf_xdp_classify(dp.lb_prog, C.byref(c), o, None) == E("EBADF")
+    assert lib.gf_lb_classify(dp.xdp_prog, C.byref(c), o, d6, None) == E("EBADF")
+    assert lib.gf_policy_ingress_classify(dp.pipe, C.byref(c), now, o, None) == E("EBADF")
+    assert lib.gf_pipeline_classify(dp.policy_array, C.byref(gf_pipe_batch(fr(), None, None)), now, o, d6, None,
+                                    None) == E("EBADF")
+    assert lib.gf_lxc_egress_classify(dp.xdp_prog, C.byref(gf_lxc_batch(fr(), None, None)), now, o, None,
+                                      None) == E("EBADF")
+    assert lib.gf_xdp_classify(987654, C.byref(c), o, None) == E("EBADF")
+    # missing outputs / columns
+    assert lib.gf_xdp_classify(dp.xdp_prog, C.byref(c), None, None) == E("EFAULT")
+    assert lib.gf_lb_classify(dp.lb_prog, C.byref(c), None, d6, None) == E("EFAULT")
+    assert lib.gf_policy_ingress_classify(dp.policy_array, C.byref(c), now, None, None) == E("EFAULT")
+    assert lib.gf_policy_ingress_classify(dp.policy_array, None, now, o, None) == E("EFAULT")
+    nc = b.cols()
+    nc.saddr4 = None
+    assert lib.gf_xdp_classify(dp.xdp_prog, C.byref(nc), o, None) == E("EFAULT")
+    assert lib.gf_pipeline_classify(dp.pipe, C.byref(gf_pipe_batch(fr(ln=None), None, None)), now, o, d6, None,
+                                    None) == E("EFAULT")
+    assert lib.gf_lxc_egress_classify(dp.policy_array, C.byref(gf_lxc_batch(fr(snap=None), None, None)), now, o,
+                                      None, None) == E("EFAULT")
+    # too many packets for one call (checked before any launch reads the columns)
+    big = b.cols()
+    big.n = (1 << 30) + 1
+    assert lib.gf_policy_ingress_classify(dp.policy_array, C.byref(big), now, o, None) == E("E2BIG")
+    assert lib.gf_pipeline_classify(dp.pipe, C.byref(gf_pipe_batch(fr(k=(1 << 30) + 1), None, None)), now, o, d6,
+                                    None, None) == E("E2BIG")
+    assert lib.gf_lxc_egress_classify(dp.policy_array, C.byref(gf_lxc_batch(fr(k=(1 << 30) + 1), None, None)), now,
+                                      o, None, None) == E("E2BIG")
+    # a stride that cannot hold the headers the program parses
+    assert lib.gf_pipeline_classify(dp.pipe, C.byref(gf_pipe_batch(fr(st=13), None, None)), now, o, d6, None,
+                                    None) == E("EINVAL")
+    assert lib.gf_lxc_egress_classify(dp.policy_array, C.byref(gf_lxc_batch(fr(st=33), None, None)), now, o, None,
+                                      None) == E("EINVAL")
+    # an empty batch: nothing to read or write
+    z = gf_pkt_cols()
+    z.n = 0
+    assert lib.gf_xdp_classify(dp.xdp_prog, C.byref(z), None, None) == 0
+    assert lib.gf_lb_classify(dp.lb_prog, C.byref(z), None, None, None) == 0
+    assert lib.gf_policy_ingress_classify(dp.policy_array, C.byref(z), now, None, None) == 0
+    assert lib.gf_pipeline_classify(dp.pipe, C.byref(gf_pipe_batch(gf_frames(0, 0, None, None), None, None)), now,
+                                    None, None, None, None) == 0
+    assert lib.gf_lxc_egress_classify(dp.policy_array, C.byref(gf_lxc_batch(gf_frames(0, 0, None, None), None, None)),
+                                      now, None, None, None) == 0
+    torch.cuda.synchronize()
+    assert bool((out == 0xAB).all()) and bool((nd6 == 0xAB).all()), "a refused call wrote its output"
+    assert (dp.dump_map("ct4"), dp.dump_map("ct6")) == ct0
+    # and the program still classifies afterwards
+    ref = OracleDP(sc)
+    got, _, _ = dp.pipeline(DeviceBatch(sc.batches[0], parse=False), now)
+    torch.cuda.synchronize()
+    ro, _, _ = ref.pipeline(sc.batches[0], now)
+    _cmp_struct(to_numpy(got, PIPE_OUT), ro, "pipeline after refused calls")
