@@ -527,6 +527,17 @@ int main(int argc, char **argv) {
     uint8_t *big; CK(hipMalloc(&big, BIG)); CK(hipMemset(big, 0, BIG));
     if (!strcmp(mode, "legacy") || !strcmp(mode, "all")) legacy(big, BIG);
     if (!strcmp(mode, "matrix") || !strcmp(mode, "all")) matrix(big, BIG, cus);
+    if (!strcmp(mode, "foot")) {       // random-read rate against footprint: the L2 and MALL steps
+        Timer T;
+        uint32_t *sink; CK(hipMalloc(&sink, 4096));
+        printf("# random 16-B / 64-B reads (1 and 4 loads per lane) against table footprint; 16.8M accesses per launch\n");
+        for (uint64_t fp = 1ull << 20; fp <= (16ull << 30); fp <<= 1) {
+            run_rd<16, 1>(T, reinterpret_cast<const uint4 *>(big), fp, sink);
+            run_rd<16, 4>(T, reinterpret_cast<const uint4 *>(big), fp, sink);
+            run_rd<64, 1>(T, reinterpret_cast<const uint4 *>(big), fp, sink);
+        }
+        CK(hipFree(sink));
+    }
     CK(hipDeviceSynchronize());
     CK(hipFree(big));
     return 0;
