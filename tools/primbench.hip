@@ -147,6 +147,17 @@ __global__ __launch_bounds__(256) void k_mrd(const uint4 *__restrict__ tab, uint
         for (int j = 0; j < V; j++) acc ^= v[k][j].x + v[k][j].w;
     if (acc == 0x9e3779b9u) sink[t & 1023] = acc;
 }
+// xcd: the table split into 8 slices, block b reading only slice b % 8 — the XCD the
+// dispatcher places it on — so each XCD's L2 holds one slice (an endpoint-partitioned
+// policy layout's best case).
+__global__ __launch_bounds__(256) void k_mrd_xcd(const uint4 *__restrict__ tab, uint64_t slice_mask, uint32_t *sink,
+                                                 uint32_t salt) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t line = (mix(t + salt) & slice_mask) + (uint64_t)(blockIdx.x & 7u) * (slice_mask + 1);
+    const uint4 v = tab[line * 4];
+    const uint32_t acc = v.x + v.w;
+    if (acc == 0x9e3779b9u) sink[t & 1023] = acc;
+}
 // coop: the 64-B line read cooperatively, 4 consecutive lanes per line and one
 // 16-B load each (16 lines per wave-instruction instead of 64)
 __global__ __launch_bounds__(256) void k_mrd_coop(const uint4 *__restrict__ tab, uint64_t lmask, uint32_t *sink, uint32_t salt) {
@@ -527,6 +538,20 @@ int main(int argc, char **argv) {
     uint8_t *big; CK(hipMalloc(&big, BIG)); CK(hipMemset(big, 0, BIG));
     if (!strcmp(mode, "legacy") || !strcmp(mode, "all")) legacy(big, BIG);
     if (!strcmp(mode, "matrix") || !strcmp(mode, "all")) matrix(big, BIG, cus);
+    if (!strcmp(mode, "xcd")) {        // per-XCD slices against one shared table of the same size
+        Timer T;
+        uint32_t *sink; CK(hipMalloc(&sink, 4096));
+        printf("# random 16-B reads, 16.8M per launch: whole table per block vs 1/8 slice per XCD (block %% 8)\n");
+        const uint64_t acc = 1ull << 24;
+        for (uint64_t fp = 8ull << 20; fp <= (128ull << 20); fp <<= 1) {
+            run_rd<16, 1>(T, reinterpret_cast<const uint4 *>(big), fp, sink);
+            const uint64_t sm = fp / 8 / 64 - 1;
+            double ms = T.best([&](int r) { hipLaunchKernelGGL(k_mrd_xcd, dim3(acc / 256), dim3(256), 0, 0,
+                                                               reinterpret_cast<const uint4 *>(big), sm, sink, 1000u * r); });
+            line("rd  W= 16B per-XCD slice", fp, ms, (double)acc, 1.0);
+        }
+        CK(hipFree(sink));
+    }
     if (!strcmp(mode, "foot")) {       // random-read rate against footprint: the L2 and MALL steps
         Timer T;
         uint32_t *sink; CK(hipMalloc(&sink, 4096));
