@@ -133,7 +133,7 @@ class Gpu:
         from cilium_amd._lib import lib, gf_ct_evict_rec
         recs = (gf_ct_evict_rec * 4096)()
         n = lib.gf_ct_evict_log(dp.fd[name], recs, 4096)
-        return [(r.seq, r.now_sec, r.cut_closing, r.cut_other, r.evicted) for r in recs[:max(0, min(n, 4096))]]
+        return [(r.seq, r.now_sec, r.age_cut, r.hand_line, r.lines, r.evicted) for r in recs[:max(0, min(n, 4096))]]
 
     def table_sampled(self, dp, name, ksz, div, pred):
         from oracle import parity as PY
@@ -392,7 +392,7 @@ def lru_replay(B, dp, ref):
     """The device's LRU evictions (gf_ct_evict_log) replayed by a sampled oracle:
     eviction cutoffs depend on the whole table, which a sample does not hold."""
     for name in ref.lru_maps:
-        ref.lru_replay[name] = {seq: (cc, co) for seq, _, cc, co, _ in B.evict_log(dp, name)}
+        ref.lru_replay[name] = {e[0]: (e[2], e[3], e[4]) for e in B.evict_log(dp, name)}
 
 
 def compare_ct(B, par, dp, ref, name, ksz, div, pred=None):
@@ -451,8 +451,9 @@ def bench_config2(args, B, rank, world, local_world=1):
     S0 = 3
     # the long-horizon continuation (N = 1): steps W + K .. L - 1 run after the headline's
     # timed steps on the same datapath, timed on their own, into the LRU sweeps a node
-    # reaches once its CT holds max_entries
-    L = max(args.long_steps, W + K) if world == 1 else W + K
+    # reaches once its CT holds max_entries (not with --pipeline: the continuation
+    # runs through dp.ingress only, so the steps the device ran are exactly W + K)
+    L = max(args.long_steps, W + K) if world == 1 and not args.pipeline else W + K
     rk, rv = st.reply_ct_entries(S0 + L)
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
     log(f"rank {rank}: tables {sum(m.n() for m in sc.maps.values())} entries, {len(rk)} pre-inserted CT, "
@@ -478,7 +479,7 @@ def bench_config2(args, B, rank, world, local_world=1):
                                                                          outs[a:b]), W, K, world, ranged=True)
     total_pkts = int(c[268])
     long_h = None
-    if L > W + K and not args.pipeline:
+    if L > W + K:
         C_ = L - W - K
         el2, c2, _, kern2 = timed(B, lambda s: dp.ingress(batches[W + K + s], now + W + K + s, out=outs[W + K + s]),
                                   0, C_, world)
@@ -575,8 +576,9 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
     from cilium_amd.datapath import ING_OUT
     from oracle.scenario import OracleDP
     from oracle import parity as PY
-    T, div = cpu_threads(local_world), parity_div(args, world)
     L = L or W + K
+    T = cpu_threads(local_world)
+    div = parity_div(args, world, T, sum(b.n for b in batches[:L]))
     t0 = time.time()
     ref = OracleDP(sc, shards=T)
     if div > 1:
@@ -637,17 +639,32 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
         ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get("cilium_ct4_global", [])]
         res["evictions"] = {"cilium_ct4_global": {
             "evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log), "sweeps_oracle": len(ora_log),
-            "entries_evicted": int(sum(e[4] for e in dev_log)),
+            "entries_evicted": int(sum(e[5] for e in dev_log)),
             "oracle": "own cutoffs from its whole table (never saw the device log)"}}
     return cpu, res
 
 
-def parity_div(args, world):
+# Per-thread rate the parity budget assumes for the oracle (the config-2 CPU
+# baseline ran 7.6 Mpps on 16 threads of the GPU box, 0.48 per thread: a margin
+# below that) and the wall time one rank's parity leg may take at N>1.
+ORACLE_MPPS_PER_THREAD = 0.4
+PARITY_LEG_S = 60.0
+
+
+def parity_div(args, world, threads=None, packets=None):
     """The flow-group sample of the parity legs: every pair at N=1 (the whole
-    stream), half of each rank's pairs at N>1 (eight oracles share one host)."""
+    stream).  At N>1 the N oracles share one host: each rank checks 1/div of its
+    own pairs, div >= 2 and large enough that `packets` (the rank's packets over
+    the leg's steps) / div run within PARITY_LEG_S on its `threads` host threads
+    (its share of the host's cores, cpu_threads(local_world))."""
     if args.parity_div:
         return args.parity_div
-    return 1 if world == 1 else 2
+    if world == 1:
+        return 1
+    if not threads or not packets:
+        return 2
+    need = packets / (threads * ORACLE_MPPS_PER_THREAD * 1e6 * PARITY_LEG_S)
+    return max(2, int(np.ceil(need)))
 
 
 # ----------------------------------------------------------------------------- config 1 / 3 (stateless)
@@ -787,7 +804,8 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
     dp = B.datapath(sc)
     exch = ingest == "exchange" and world > 1
-    div = parity_div(args, world) * 2
+    # the pipeline oracle is ~2x the per-packet cost of ingress: half the sample
+    div = parity_div(args, world, cpu_threads(local_world), 2 * (W + K) * args.flows_per_step * 4) * 2
     sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
     pm = torch.from_numpy(PY.pair_sampled(sa, da, div).astype(np.uint8) |
                           (PY.pair_sampled(sa, da, div * 8).astype(np.uint8) << 1)).to(B.dev)
@@ -909,7 +927,7 @@ def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global
             ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get(name, [])]
             res.setdefault("evictions", {})[name] = {
                 "evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log), "sweeps_oracle": len(ora_log),
-                "entries_evicted": int(sum(e[4] for e in dev_log)),
+                "entries_evicted": int(sum(e[5] for e in dev_log)),
                 "oracle": "own cutoffs from its whole table (never saw the device log)"}
     return cpu, res
 
@@ -1196,9 +1214,20 @@ def add_bounds(cfg, r):
                            "valu_busy": round(2 * valu / t / ISSUE_PEAK, 4),
                            "wave_insts_per_s": (valu + salu) / t, "peak": ISSUE_PEAK,
                            "wave_insts_per_64_packets": round((valu + salu) * 64 / float(pk), 1), "source": src}
+        # the same algorithmic bytes over the profiled run's own kernel average
+        # (rocprofv3 --stats of this build), beside the live HIP-event frac
+        ns = [k.get("rocprof_avg_ns") for k in ks]
+        ab = rf.get("algorithmic_bytes_per_launch")
+        if ab and ns and all(ns):
+            ms_p = sum(k["rocprof_avg_ns"] * k.get("dispatches_per_step", 1.0) for k in ks) * 1e-6
+            rf["frac_rocprof"] = round(ab / (ms_p * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            rf["rocprof_avg_launch_ms"] = round(ms_p, 4)
+            rf["rocprof_source"] = j.get("kernel_stats_source", src)
         tb = sum(k.get("traffic_bytes_per_packet") or 0.0 for k in ks) * float(pk)
         if tb:
             rf["traffic"] = tb
+            rf["traffic_kind"] = ("EA-request bytes (MALL hits included): L2->fabric requests priced by their size, "
+                                  "not DRAM bytes")
             rf["traffic_source"] = src
             rf["traffic_model"] = ks[0].get("traffic_model") if ks else None
             hits = cs("TCC_HIT_sum")

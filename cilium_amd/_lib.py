@@ -160,8 +160,8 @@ _sig("gf_ct_gc", C.c_int, C.c_int, C.c_uint32, VP)
 
 
 class gf_ct_evict_rec(C.Structure):
-    _fields_ = [("seq", C.c_uint32), ("now_sec", C.c_uint32), ("cut_closing", C.c_uint64),
-                ("cut_other", C.c_uint64), ("evicted", C.c_uint64)]
+    _fields_ = [("seq", C.c_uint32), ("now_sec", C.c_uint32), ("age_cut", C.c_uint32), ("pad", C.c_uint32),
+                ("hand_line", C.c_uint64), ("lines", C.c_uint64), ("evicted", C.c_uint64)]
 
 
 _sig("gf_ct_evict_log", C.c_int, C.c_int, C.POINTER(gf_ct_evict_rec), C.c_uint32)
@@ -218,7 +218,7 @@ if os.path.isdir(os.path.join(_HERE, "csrc")):
     if os.environ.get("GPUFLOW_DIAG_LIB"):
         if not BUILD_ID.startswith(_want + "+"):
             raise ImportError(f"variant library {LIB_PATH} was built from sources {BUILD_ID}, the tree holds "
-                              f"{_want}: rebuild it with tools/variants.sh build")
+                              f"{_want}: rebuild it with tools/variant.sh")
     elif BUILD_ID != _want:
         raise ImportError(f"libgpuflow.so was built from sources {BUILD_ID}, the tree holds {_want}: "
                           "run `python -c 'import __graft_entry__ as g; g.build()'`")

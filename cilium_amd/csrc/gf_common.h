@@ -19,8 +19,12 @@
 //     vals: 24 B per slot (packets, bytes, the reference's pad bytes)
 //
 // state: 0 empty, 1 full, 2 deleted (tombstone), 3 busy (device insert in
-// flight).  Device inserts only ever claim EMPTY slots; tombstones are reused
-// by host-side rebuilds only (see the CT concurrency note in DESIGN.md).
+// flight), 4 free (a slot the LRU eviction pass emptied between two classify
+// calls, with its key bytes zeroed).  Probes walk past tombstones and free slots
+// alike and end at an EMPTY one.  Device inserts claim EMPTY and FREE slots, never
+// a tombstone (a key deleted inside the running launch may still be re-probed by
+// its own lane); tombstones turn FREE or EMPTY in the eviction pass and the GC
+// sweep, or are reused by host-side rebuilds (the CT concurrency note in DESIGN.md).
 //
 // The hash is a murmur3-style mix over the key as little-endian u32 words
 // (zero-padded), identical on host and device.
@@ -41,7 +45,7 @@
 #define GF_HD inline
 #endif
 
-enum : uint8_t { GF_SLOT_EMPTY = 0, GF_SLOT_FULL = 1, GF_SLOT_TOMB = 2, GF_SLOT_BUSY = 3 };
+enum : uint8_t { GF_SLOT_EMPTY = 0, GF_SLOT_FULL = 1, GF_SLOT_TOMB = 2, GF_SLOT_BUSY = 3, GF_SLOT_FREE = 4 };
 
 struct gf_htab_desc {
     uint8_t  *slots;       // nslots * slot_size (hash mode: see gf_key_hash)

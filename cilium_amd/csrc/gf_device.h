@@ -280,8 +280,9 @@ __device__ __forceinline__ void ProbeLine<KSZ, U, XW>::load_quad(const gf_htab_d
 }
 
 // Outcome of a probe walk: the slot of key A, else of key B (is_b), else -1;
-// plus the EMPTY slot that ended the walk — where an absent key is inserted —
-// and the header word holding its state byte as it was observed.
+// plus where an absent key is inserted — the first FREE slot the walk passed,
+// else the EMPTY slot that ended it — and the header word holding its state
+// byte as it was observed.
 struct ProbeRes {
     int64_t f, empty;
     uint32_t empty_word;
@@ -290,7 +291,8 @@ struct ProbeRes {
 };
 
 // ht_find2 continuing from a preloaded home line (key B only when has_b).  The
-// walk ends at the first EMPTY slot, as in ht_find2.
+// walk ends at the first EMPTY slot, as in ht_find2; the first FREE slot before
+// it (the LRU eviction pass's reusable slots, gf_common.h) is the insert slot.
 template <int KSZ, int U, int XW>
 __device__ __forceinline__ ProbeRes probe2(const gf_htab_desc &d, const uint32_t *ka, const uint32_t *kb,
                                            ProbeLine<KSZ, U, XW> &L, bool has_b = true) {
@@ -310,7 +312,11 @@ __device__ __forceinline__ ProbeRes probe2(const gf_htab_desc &d, const uint32_t
         for (int u = 0; u < U; u++) {
             uint32_t st = L.hd[u].state();
             int64_t slot = (int64_t)((i + u) & d.mask);
-            if (st == GF_SLOT_EMPTY) { r.empty = slot; r.empty_word = L.hd[u].w[SW]; goto done; }
+            if (st == GF_SLOT_EMPTY) {
+                if (r.empty < 0) { r.empty = slot; r.empty_word = L.hd[u].w[SW]; }
+                goto done;
+            }
+            if (st == GF_SLOT_FREE && r.empty < 0) { r.empty = slot; r.empty_word = L.hd[u].w[SW]; }
             if (st == GF_SLOT_FULL) {
                 if (L.hd[u].eq(ka)) { r.f = slot; r.u = u; return r; }
                 if (has_b && fb < 0 && L.hd[u].eq(kb)) { fb = slot; ub = u; }
@@ -414,7 +420,13 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         store_value<VW>(d, i, vw);
         if (!strict) (*added)++;
     };
-    if (hint >= 0 && ((hint_word >> (8 * SB)) & 0xffu) == GF_SLOT_EMPTY) {
+    // EMPTY or FREE (reusable between launches, gf_common.h) slots are claimed;
+    // the key is absent from the whole walk, so any of them keeps every probe exact
+    auto claimable = [&](uint32_t w) {
+        const uint32_t st = (w >> (8 * SB)) & 0xffu;
+        return st == GF_SLOT_EMPTY || st == GF_SLOT_FREE;
+    };
+    if (hint >= 0 && claimable(hint_word)) {
         uint8_t *sw = d.slots + (uint64_t)hint * d.slot_size + 4 * SW;
         if (gcas(sw, hint_word, busy) == hint_word) { fill((uint64_t)hint); return hint; }
     }
@@ -423,7 +435,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         uint8_t *sw = d.slots + i * d.slot_size + 4 * SW;
         uint32_t cur = gload<uint32_t>(sw);            // a stale view only makes the CAS fail and retry
         for (;;) {
-            if (((cur >> (8 * SB)) & 0xffu) != GF_SLOT_EMPTY) break;
+            if (!claimable(cur)) break;
             uint32_t seen = gcas(sw, cur, busy);
             if (seen == cur) { fill(i); return (int64_t)i; }
             cur = seen;

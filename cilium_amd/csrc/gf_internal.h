@@ -101,8 +101,14 @@ struct Map : Obj {
     uint64_t xfer_d2h = 0, xfer_h2d = 0;   // bytes the map API moved over PCIe (gf_map_info)
     DevBuf d_slots, d_vals, d_count;
     DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits
-    DevBuf d_lrucodes;          // LRU CT maps: per-slot sweep codes (k_lru_hist -> k_lru_clusters)
     uint32_t lru_seq = 0;       // classify calls that used this map (the eviction log's batch number)
+    // LRU CT maps: the count the last eviction chain left, written by the device to
+    // pinned host memory behind ev_count; cnt_add sums the increments of
+    // dev_count_hi (ct_limits), cnt_add_ev its value when ev_count was recorded
+    uint32_t *h_evcount = nullptr;
+    hipEvent_t ev_count = nullptr;
+    bool ev_pending = false;
+    uint64_t cnt_add = 0, cnt_add_ev = 0;
     // get_next_key over a device-authoritative map: a host copy of one chunk of
     // slot headers, and the slot of the key returned last (the dump loop's next
     // argument) so a walk is not needed to resume.
@@ -127,6 +133,7 @@ struct Map : Obj {
     bool dir_big = false;
 
     Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f);
+    ~Map();
     bool is_lpm() const { return type == GF_MAP_TYPE_LPM_TRIE; }
     uint32_t lpm_bits() const { return (ksz - 4) * 8; }
     uint32_t n_entries() const { return is_lpm() ? (uint32_t)lpm.size() : (uint32_t)ht.count; }
@@ -206,6 +213,16 @@ struct ProgPipe : Obj {
     std::shared_ptr<PolicyArray> policy;
     ProgPipe() : Obj(ObjKind::ProgPipe) {}
 };
+
+// Element ceiling of an insert through the map API (single updates, the host
+// path and the device bulk load alike): HASH maps end at max_entries (-E2BIG).
+// LRU conntrack maps (which the kernel never lets fail: it evicts) take entries
+// up to the slot array's 7/8 load and are brought back under max_entries by the
+// eviction sweep of the next classify call that binds them (lru_evict); other
+// LRU maps have no eviction path here and end at max_entries like HASH maps.
+inline uint64_t dev_insert_limit(const Map &m) {
+    return m.type == GF_MAP_TYPE_LRU_HASH && m.ht.codec == GF_VCODEC_CT ? m.ht.nslots / 8 * 7 : m.max_entries;
+}
 
 std::shared_ptr<Obj> get_obj(int handle);
 std::shared_ptr<Map> get_map(int handle);

@@ -2422,7 +2422,7 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
                 uint8_t *sl = d.slots + j * d.slot_size;
                 const uint32_t st = sl[d.ksz];
                 if (st == GF_SLOT_EMPTY) break;
-                if (st == GF_SLOT_TOMB) {
+                if (st == GF_SLOT_TOMB || st == GF_SLOT_FREE) {
                     sl[d.ksz] = GF_SLOT_EMPTY;
                     tombs++;
                     hole = true;
@@ -2456,149 +2456,128 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 }
 
 // ---- LRU stand-in (CT maps are BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:53-75;
-// ctmap.go:38-39).  The kernel never fails an LRU insert: it evicts an entry
-// from its per-CPU LRU lists, in an order that is not reproducible.  Here an
-// LRU CT map may exceed max_entries inside a batch (the slot array has room);
-// at the end of every classify call that inserts into it, if the device count
-// exceeds max_entries, the least recently used entries are evicted until the
-// count is at most the low watermark max_entries - max_entries/8.  Age order:
-// closing entries (rx_closing or tx_closing: the connection is being torn down)
-// first, then the others, each by ascending last use (ct_last_use) in whole
-// one-second bins relative to `now` (bin 0 holds everything last used 65535 s
-// or more ago).  The smallest prefix of that order that reaches the watermark
-// is deleted by the GC sweep above — a deterministic rule the oracle restates
-// (o_ct_lru_cutoffs), and every eviction is logged (gf_ct_evict_log).
+// ctmap.go:38-39).  The kernel never fails an LRU insert: it evicts from per-CPU
+// LRU lists, taking entries off the tail of an inactive list it keeps about as
+// long as the active one (kernel/bpf/bpf_lru_list.c, not in /root/reference) — in
+// effect from the older half of the entries, in an order nothing reproduces.
+// Here an LRU CT map may exceed max_entries inside a batch (the slot array has
+// room); at the end of every classify call that inserts into it, if the device
+// count exceeds max_entries, a deterministic *hand* evicts (the oracle restates it,
+// o_ct_lru_evict):
+//  * age key of an entry: 0 if its last use (ct_last_use) lies before time 0,
+//    else closing entries (rx_closing | tx_closing) in [0, 65536) and the others
+//    in [65536, 131072), each by last use in one-second bins relative to now (bin
+//    0 = last used 65535 s or more ago);
+//  * home line of an entry: its key's home slot in this table (gf_home_slot of the
+//    CT hash) / slots per 128-B line; NL lines in all;
+//  * the sample: the entries whose home line is below SL = NL >> 6 (SL = NL when
+//    NL <= 65536).  K = the smallest age key covering half of the sample (its older
+//    half is eligible); es = the sample entries with age key <= K;
+//  * a round: Q = count - (max_entries - max_entries / 8); the hand advances over
+//    lines = min(NL, ceil(Q * SL / es)) home lines (NL if es = 0) and deletes every
+//    entry with age key <= K whose home line it passes.  A second round runs only
+//    if the count is still above max_entries (the hand never passes a line twice in
+//    one call).
+// The work is proportional to what a call evicts (the lines passed hold about 2Q
+// entries), not to the table: the whole-table histogram + compaction sweep this
+// replaces read all 16 GB of the 2^29-slot CT per eviction (~7.3 ms).  A deleted
+// slot turns EMPTY when every slot after it up to the end of its probe cluster
+// is gone too (the probe invariant holds), else FREE (claimed by later device
+// inserts, gf_common.h); tombstones the hand passes are cleared the same way.
+// Key bytes of the cleared slots are zeroed.  Every eviction is logged
+// (gf_ct_evict_log: batch number, now, K, the hand's first line, lines passed,
+// entries deleted).
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
-struct LruLog { uint32_t seq, now; unsigned long long cut_c, cut_o, evicted; };
+#define GF_LRU_SAMPLE_SHIFT 6
+#define GF_LRU_HT 256u                  // k_lru_hand block
+#define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (4 per thread)
+struct LruLog { uint32_t seq, now, age_cut, pad; unsigned long long hand, lines, evicted; };
 struct LruDev {
-    uint32_t hist[2 * GF_LRU_BINS];
-    GcCut cut;
-    unsigned long long res[2];
-    unsigned long long target;
-    unsigned long long moves[2];  // k_lru_clusters: entries moved found by the masks / by the table (GF_LRU_STATS)
-    uint32_t flag, nlog;
-    uint32_t cut_key;             // k_lru_cut: age keys [0, cut_key] are evicted
+    uint32_t hist[2 * GF_LRU_BINS];     // the sample's age histogram
+    GcCut cut;                          // gf_ct_gc (k_gc_*)
+    unsigned long long res[2];          // gf_ct_gc: entries deleted, tombstones cleared
+    uint32_t flag;                      // this call evicts
+    uint32_t K;                         // age keys [0, K] are eligible
+    unsigned long long es, target;      // eligible sample entries; max_entries - max_entries / 8
+    unsigned long long hand;            // the hand's next home line (kept across calls)
+    unsigned long long h0, lines;       // this round: home lines [h0, h0 + lines)
+    unsigned long long ev_h0, ev_lines, evicted;   // this call so far
+    unsigned long long kills, cleared;  // this round: entries deleted, tombstones / FREE slots rewritten
+    uint32_t nlog, pad;
     LruLog log[GF_LRU_LOGCAP];
 };
-__device__ __forceinline__ uint32_t lru_key(uint32_t lt, uint32_t fl, uint32_t now) {
-    const long long base = (long long)now - (long long)(GF_LRU_BINS - 1);
-    long long b = ct_last_use(lt, fl) - base;
+__device__ __forceinline__ uint32_t lru_age_key(uint32_t lt, uint32_t fl, uint32_t now) {
+    const long long lu = ct_last_use(lt, fl);
+    if (lu < 0) return 0u;
+    long long b = lu - ((long long)now - (long long)(GF_LRU_BINS - 1));
     b = b < 0 ? 0 : (b > (long long)(GF_LRU_BINS - 1) ? (long long)(GF_LRU_BINS - 1) : b);
     return ((fl & (F_RX_CLOSING | F_TX_CLOSING)) ? 0u : GF_LRU_BINS) + (uint32_t)b;
+}
+// One CT slot as the eviction pass reads it.  KIND 1: the CT v4 slot (32 B: key
+// 14, state at 14, hot value at 16 with the lifetime first) as two 16-B loads;
+// KIND 2: the CT v6 slot (64 B: key 40, state at 40, hot value at 48) as four.
+template <int KIND>
+struct LruSlot {
+    static constexpr uint32_t SZ = KIND == 2 ? 64u : 32u, SPL = 128u / SZ, KW = KIND == 2 ? 10 : 4;
+    uint32_t kw[KW];
+    uint32_t st = GF_SLOT_EMPTY, lt = 0, fl = 0;
+    __device__ __forceinline__ void load(const gf_htab_desc &d, uint64_t i) {
+        const uint8_t *p = d.slots + i * SZ;
+        if constexpr (KIND == 2) {
+            const uint4 a = gload<uint4>(p), b = gload<uint4>(p + 16), c = gload<uint4>(p + 32), e = gload<uint4>(p + 48);
+            kw[0] = a.x; kw[1] = a.y; kw[2] = a.z; kw[3] = a.w; kw[4] = b.x; kw[5] = b.y; kw[6] = b.z; kw[7] = b.w;
+            kw[8] = c.x; kw[9] = c.y;
+            st = c.z & 0xffu; lt = e.x; fl = e.y & 0xffffu;
+        } else {
+            const uint4 a = gload<uint4>(p), b = gload<uint4>(p + 16);
+            kw[0] = a.x; kw[1] = a.y; kw[2] = a.z; kw[3] = a.w & 0xffffu;
+            st = (a.w >> 16) & 0xffu; lt = b.x; fl = b.y & 0xffffu;
+        }
+    }
+    __device__ __forceinline__ uint64_t home_line(const gf_htab_desc &d, uint32_t mode) const {
+        return gf_home_slot(gf_key_hash(kw, KIND == 2 ? 40u : 14u, mode), d.mask, SZ) / SPL;
+    }
+};
+// A deleted / cleared slot: key bytes zeroed, state EMPTY or FREE (16-B stores).
+template <int KIND>
+__device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j, uint32_t st) {
+    uint8_t *p = d.slots + j * LruSlot<KIND>::SZ;
+    if constexpr (KIND == 2) {
+        gstore<uint4>(p + 32, make_uint4(0u, 0u, st, 0u));
+        gstore<uint4>(p, make_uint4(0u, 0u, 0u, 0u));
+        gstore<uint4>(p + 16, make_uint4(0u, 0u, 0u, 0u));
+    } else {
+        gstore<uint4>(p, make_uint4(0u, 0u, 0u, st << 16));
+    }
 }
 __global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev *L) {
     const uint32_t c = *count;
     const bool f = c > max_entries;
-    if (threadIdx.x == 0) {
-        L->flag = f ? 1u : 0u;
-        L->cut.active = 0;
-        L->res[0] = L->res[1] = 0;
-        L->moves[0] = L->moves[1] = 0;
-        L->target = (unsigned long long)(max_entries - max_entries / 8u);
-    }
+    if (threadIdx.x == 0) L->flag = f ? 1u : 0u;
     if (f)
         for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
 }
-// Age histogram: wave-aggregated (a wave's entries mostly share a bin), then
-// counted per block in LDS and flushed with one global add per non-zero bin.
-// The last GF_LRU_WIN seconds of each class are counted directly (one LDS slot
-// per bin, no collisions): a steady stream's live entries were all last used
-// within its flows' lifetimes, tens of seconds.  Older bins go through a
-// block-local LDS cache: a 64-bit {bin, count} word per line (Fibonacci-hashed),
-// updated by CAS; a bin that misses takes the line over and flushes the previous
-// bin's count with one global add.  (The cache alone, with an XOR-folded index,
-// mapped a closing bin and the non-closing bin 32 s from it to one line: once a
-// stream's live ages spanned more than 32 s, every wave alternated them and sent
-// a global add to a few hot addresses — 27-76 ms per 2^29-slot sweep.)
+// Age histogram of the sample: wave-aggregated (a wave's entries mostly share a
+// bin), then counted per block in LDS and flushed with one global add per
+// non-zero bin.  The last GF_LRU_WIN seconds of each class are counted directly
+// (one LDS slot per bin, no collisions): a steady stream's live entries were all
+// last used within its flows' lifetimes.  Older bins go through a block-local
+// LDS cache: a 64-bit {bin, count} word per line (Fibonacci-hashed), updated by
+// CAS; a bin that misses takes the line over and flushes the previous bin's
+// count with one global add.  (An XOR-folded index once mapped a closing bin and
+// the non-closing bin 32 s from it to one line: every wave alternated them and
+// sent a global add to a few hot addresses.)
 #define GF_LRU_LDS 2048u
 #define GF_LRU_WIN 4096u
-#define GF_LRU_HB 1024u               // k_lru_hist block: 16 waves share the LDS bins
-// Per-slot sweep codes (k_lru_hist -> k_lru_clusters): the slot's state and, for
-// an entry, its age key (bits 0-17, + 2), whether its last use lies before time 0
-// (bit 20) and its distance from its home slot (bits 24-31; 255 = 255 or more).
-#define GF_LRU_C_EMPTY 0u
-#define GF_LRU_C_TOMB 1u
-#define GF_LRU_C_KEY 2u
-#define GF_LRU_C_KMASK 0x3ffffu
-#define GF_LRU_C_NEG (1u << 20)
-#define GF_LRU_C_DSH 24
-// Each thread takes GF_LRU_U slots per trip (BLOCK apart, so a wave still
-// covers 64 consecutive slots) and issues all their loads before using any:
-// the state byte and, for maps whose hot value sits in the slot, the lifetime
-// and flags words of the same line (read whether or not the slot is FULL).
-#define GF_LRU_U 4
-// An entry's home slot from its key bytes in the slot: the CT key sizes read with
-// constant indices (registers, not a scratch array).
-__device__ __forceinline__ uint64_t lru_home_any(const gf_htab_desc &d, uint64_t i, uint32_t mode) {
-    const uint32_t *k = reinterpret_cast<const uint32_t *>(d.slots + i * d.slot_size);
-    uint32_t w[10];
-#pragma unroll
-    for (uint32_t q = 0; q < 10; q++) {                  // constant indices: registers
-        const uint32_t x = 4 * q < d.ksz ? k[q] : 0u;
-        w[q] = d.ksz >= 4 * q + 4 ? x : (4 * q < d.ksz ? x & ((1u << (8 * (d.ksz - 4 * q))) - 1u) : 0u);
-    }
-    return gf_home_slot(gf_key_hash(w, d.ksz, mode), d.mask, d.slot_size);
-}
-__device__ __forceinline__ uint64_t lru_home(const gf_htab_desc &d, uint64_t i, uint32_t mode) {
-    const uint32_t *k = reinterpret_cast<const uint32_t *>(d.slots + i * d.slot_size);
-    if (d.ksz == 14) {
-        const uint32_t w[4] = {k[0], k[1], k[2], k[3] & 0xffffu};
-        return gf_home_slot(gf_key_hash(w, 14, mode), d.mask, d.slot_size);
-    }
-    if (d.ksz == 40) {
-        const uint32_t w[10] = {k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9]};
-        return gf_home_slot(gf_key_hash(w, 40, mode), d.mask, d.slot_size);
-    }
-    return lru_home_any(d, i, mode);
-}
-// One slot of k_lru_hist (called once per unrolled slot, so the per-trip values
-// stay in registers).
-template <int KIND>
-__device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mode, uint32_t lt_off, uint32_t now,
-                                              LruDev *L, uint32_t *bits, uint32_t *codes, unsigned long long *line,
-                                              uint32_t *win, uint64_t i, uint32_t st, uint32_t lt, uint32_t fl,
-                                              const uint32_t (&kw)[10]) {
-    const uint64_t ns = d.mask + 1, nw = (ns + 31) / 32;
+#define GF_LRU_HB 1024u                 // k_lru_sample block: 16 waves share the LDS bins
+// key: the entry's age key, ~0u for none.  Wave-uniform call.
+__device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line, uint32_t *win, uint32_t key) {
     const uint32_t lane = threadIdx.x & 63u;
-    const bool inl = d.vin != 0;
-    uint32_t key = ~0u, code = st == GF_SLOT_EMPTY ? GF_LRU_C_EMPTY : GF_LRU_C_TOMB;
-    if (st != GF_SLOT_EMPTY && st != GF_SLOT_TOMB) {
-        if (!inl) {
-            const uint8_t *v = ht_val(d, i) + lt_off;
-            lt = *reinterpret_cast<const uint32_t *>(v);
-            fl = *reinterpret_cast<const uint16_t *>(v + 4);
-        }
-        const uint32_t k = lru_key(lt, fl, now);
-        uint64_t home;
-        if (KIND == 1) {                                 // CT v4: the key came with the slot
-            const uint32_t w[4] = {kw[0], kw[1], kw[2], kw[3] & 0xffffu};
-            home = gf_home_slot(gf_key_hash(w, 14, mode), d.mask, d.slot_size);
-        } else if (KIND == 2) {                          // CT v6
-            home = gf_home_slot(gf_key_hash(kw, 40, mode), d.mask, d.slot_size);
-        } else {
-            home = lru_home(d, i, mode);
-        }
-        const uint64_t dist = (i - home) & d.mask;
-        code = GF_LRU_C_KEY + k + (ct_last_use(lt, fl) < 0 ? GF_LRU_C_NEG : 0u) +
-               ((uint32_t)(dist < 255 ? dist : 255) << GF_LRU_C_DSH);
-        if (st == GF_SLOT_FULL) key = k;
-    }
-    if (i < ns) codes[i] = code;
-    {
-        const uint64_t w0 = i - lane;             // the wave's first slot
-        uint32_t pv = 0;
-        if (lane == 0 && w0 < ns) pv = d.slots[((w0 - 1) & d.mask) * d.slot_size + d.ksz] != GF_SLOT_EMPTY;
-        pv = __shfl(pv, 0);
-        const uint64_t ne = __ballot(st != GF_SLOT_EMPTY);
-        const uint64_t starts = ne & ~((ne << 1) | (uint64_t)pv);
-        const uint64_t wd = w0 / 32 + lane;
-        if (lane < 2 && w0 < ns && wd < nw) bits[wd] = (uint32_t)(starts >> (32 * lane));
-    }
     const uint32_t kb = key & (GF_LRU_BINS - 1u);
     const bool inwin = key != ~0u && kb >= GF_LRU_BINS - GF_LRU_WIN;
     if (inwin) atomicAdd(&win[(key >> 16) * GF_LRU_WIN + kb - (GF_LRU_BINS - GF_LRU_WIN)], 1u);
-    uint64_t rem = __ballot(key != ~0u && !inwin);  // older bins: wave-aggregated, cached
+    uint64_t rem = __ballot(key != ~0u && !inwin);
     while (rem) {
         const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
         const uint32_t k = __shfl(key, (int)lead);
@@ -2620,67 +2599,42 @@ __device__ __forceinline__ void lru_hist_slot(const gf_htab_desc &d, uint32_t mo
         rem &= ~m;
     }
 }
-// KIND 1: the CT v4 slot (32 B: key 14, state at 14, hot value at 16 with the
-// lifetime first) read as two 16-B loads; KIND 2: the CT v6 slot (64 B: key 40,
-// state at 40, hot value at 48) as four; KIND 0: any layout, field by field.
+// The sample: slots [0, sl * SPL) and the rest of the probe cluster running past
+// them (entries homed in the sampled lines; one wave walks it, up to the table's
+// end — wrapped positions below sl * SPL are the main loop's).
 template <int KIND>
-__global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t mode, uint32_t lt_off, uint32_t now,
-                                                        LruDev *L, uint32_t *bits, uint32_t *codes) {
+__global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                          uint64_t sl) {
     if (!L->flag) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
     __syncthreads();
-    const uint64_t ns = d.mask + 1;
-    const bool inl = d.vin != 0;
-    static_assert(GF_LRU_U == 4, "k_lru_hist: four slots a trip");
-    constexpr uint32_t UT = KIND == 2 ? 2u : GF_LRU_U;
-    const uint64_t stride_k = (uint64_t)gridDim.x * GF_LRU_HB * UT;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB * UT; b0 < ns; b0 += stride_k) {   // wave-uniform trips
-        constexpr int UK = KIND == 2 ? 2 : GF_LRU_U;     // slots a trip (v6: 64 B each, fewer registers)
-        uint32_t st[GF_LRU_U], lt[GF_LRU_U], fl[GF_LRU_U], kw[GF_LRU_U][10];
-#pragma unroll
-        for (int u = 0; u < GF_LRU_U; u++) {
-            const uint64_t i = b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x;
-            st[u] = GF_SLOT_EMPTY;
-            lt[u] = fl[u] = 0;
-#pragma unroll
-            for (int q = 0; q < 10; q++) kw[u][q] = 0;
-            if (KIND == 2) {
-                if (i < ns && u < UK) {
-                    const uint4 *q = reinterpret_cast<const uint4 *>(d.slots + i * 64);
-                    const uint4 a = q[0], b = q[1], c = q[2], e = q[3];
-                    kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
-                    kw[u][4] = b.x; kw[u][5] = b.y; kw[u][6] = b.z; kw[u][7] = b.w;
-                    kw[u][8] = c.x; kw[u][9] = c.y;
-                    st[u] = c.z & 0xffu;
-                    lt[u] = e.x;
-                    fl[u] = e.y & 0xffffu;
-                }
-            } else if (KIND == 1) {
-                if (i < ns) {
-                    const uint4 *q = reinterpret_cast<const uint4 *>(d.slots + i * 32);
-                    const uint4 a = q[0], b = q[1];
-                    kw[u][0] = a.x; kw[u][1] = a.y; kw[u][2] = a.z; kw[u][3] = a.w;
-                    st[u] = (a.w >> 16) & 0xffu;
-                    lt[u] = b.x;
-                    fl[u] = b.y & 0xffffu;
-                }
-            } else {
-                st[u] = i < ns ? d.slots[i * d.slot_size + d.ksz] : (uint32_t)GF_SLOT_EMPTY;
-                if (inl && i < ns) {
-                    const uint8_t *v = ht_val(d, i) + lt_off;
-                    lt[u] = *reinterpret_cast<const uint32_t *>(v);
-                    fl[u] = *reinterpret_cast<const uint16_t *>(v + 4);
-                }
-            }
+    const uint64_t ns = d.mask + 1, n = sl * LruSlot<KIND>::SPL;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB; b0 < n; b0 += (uint64_t)gridDim.x * GF_LRU_HB) {  // uniform trips
+        const uint64_t i = b0 + threadIdx.x;
+        uint32_t key = ~0u;
+        if (i < n) {
+            LruSlot<KIND> s;
+            s.load(d, i);
+            if (s.st == GF_SLOT_FULL && s.home_line(d, mode) < sl) key = lru_age_key(s.lt, s.fl, now);
         }
-#pragma unroll
-        for (int u = 0; u < GF_LRU_U; u++)
-            if (u < UK)
-                lru_hist_slot<KIND>(d, mode, lt_off, now, L, bits, codes, line, win, b0 + (uint64_t)u * GF_LRU_HB + threadIdx.x,
-                                    st[u], lt[u], fl[u], kw[u]);
+        lru_hist_add(L, line, win, key);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 64 && n < ns) {
+        for (uint64_t q = n;; q += 64) {
+            const uint64_t i = q + threadIdx.x;
+            LruSlot<KIND> s;
+            if (i < ns) s.load(d, i);
+            const uint64_t em = __ballot(s.st == GF_SLOT_EMPTY);
+            const uint32_t stop = em ? (uint32_t)__ffsll((unsigned long long)em) - 1u : 64u;
+            uint32_t key = ~0u;
+            if (threadIdx.x < stop && s.st == GF_SLOT_FULL && s.home_line(d, mode) < sl)
+                key = lru_age_key(s.lt, s.fl, now);
+            lru_hist_add(L, line, win, key);
+            if (em) break;
+        }
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
@@ -2690,172 +2644,183 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_hist(gf_htab_desc d, uint32_t
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
         if (win[k]) atomicAdd(&L->hist[(k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN], win[k]);
 }
-// The smallest prefix of the age order whose removal leaves <= target entries:
-// one block scans the 2 x 65536 bins (128 per thread, then a block scan).
-__global__ __launch_bounds__(1024) void k_lru_cut(const uint32_t *count, uint32_t now, LruDev *L) {
+// Round `round` of a call: K and es from the sample (round 0), then the lines
+// the hand passes.  One block (128 bins per thread, then a block scan).
+__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
+                                                   uint64_t sl, uint32_t round) {
     if (!L->flag) return;
     __shared__ unsigned long long part[1024];
-    constexpr uint32_t PER = 2 * GF_LRU_BINS / 1024;
+    __shared__ uint32_t s_k;
+    __shared__ unsigned long long s_es;
     const uint32_t t = threadIdx.x;
-    unsigned long long s = 0;
-    for (uint32_t k = 0; k < PER; k++) s += L->hist[t * PER + k];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan
-        unsigned long long v = t >= o ? part[t - o] : 0ull;
+    if (round == 0) {
+        constexpr uint32_t PER = 2 * GF_LRU_BINS / 1024;
+        unsigned long long s = 0;
+        for (uint32_t k = 0; k < PER; k++) s += L->hist[t * PER + k];
+        part[t] = s;
+        if (t == 0) { s_k = 2 * GF_LRU_BINS - 1; s_es = 0; }
         __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    const unsigned long long c = *count, need = c > L->target ? c - L->target : 0ull;
-    const unsigned long long before = t ? part[t - 1] : 0ull;
-    if (need == 0) { if (t == 0) L->flag = 0; return; }
-    if (before < need && part[t] >= need) {              // the cut bin lies in this thread's range
-        unsigned long long acc = before;
-        uint32_t kb = t * PER;
-        for (uint32_t k = 0; k < PER; k++) {
-            acc += L->hist[t * PER + k];
-            if (acc >= need) { kb = t * PER + k; break; }
+        for (uint32_t o = 1; o < 1024; o <<= 1) {       // inclusive scan
+            const unsigned long long v = t >= o ? part[t - o] : 0ull;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
         }
-        // delete bins [0, kb]: cutoffs in last-use terms
-        const long long base = (long long)now - (long long)(GF_LRU_BINS - 1);
-        auto cut_of = [&](uint32_t b) -> unsigned long long {   // bins [0, b] of a class -> lifetime < cut
-            const long long v = base + (long long)b + 1;
-            return b == GF_LRU_BINS - 1 ? (1ull << 32) : (v <= 0 ? 0ull : (unsigned long long)v);
-        };
-        if (kb < GF_LRU_BINS) { L->cut.c = cut_of(kb); L->cut.o = 0; }
-        else { L->cut.c = 1ull << 32; L->cut.o = cut_of(kb - GF_LRU_BINS); }
-        L->cut.lru = 1;
-        L->cut_key = kb;
-        L->cut.active = 1;
-    }
-}
-// The eviction sweep of the LRU stand-in: k_gc_clusters' compaction (one lane
-// per 32-slot word, walking the clusters that start in it) decided from the codes
-// k_lru_hist wrote instead of the table: an entry is evicted iff its age key is at
-// most cut_key or its last use lies before time 0 (gc_kill with the cutoffs
-// k_lru_cut derived from cut_key, in key terms).  The lane reads its word's 32
-// codes with eight 16-B loads and works on bit masks (EMPTY, TOMB, evicted, and
-// the occupancy of its chunk and the one before as the walk changes it); the table
-// is touched only where it changes — the state byte of an evicted entry or a
-// tombstone, and the entries that move.  A live entry after a hole moves to the
-// first EMPTY slot in [home, j), found from its code's home distance in the
-// occupancy masks (from the table's state bytes when the home lies further back).
-// Within a cluster all deletions of a chunk are applied before its moves, in slot
-// order: a move at j searches [home(j), j) only, where the deletions and earlier
-// moves are exactly those of k_gc_clusters' interleaved walk.  Needs nslots % 32
-// == 0 (LRU maps: >= 64, 2^k).
-struct LruMasks { uint32_t emp, tmb, kil; };
-__device__ __forceinline__ LruMasks lru_code_masks(const uint32_t *__restrict__ codes, uint64_t w, uint32_t ck) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(codes + w * 32);
-    uint4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = q[i];
-    uint32_t emp = 0, tmb = 0, kil = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint32_t c4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const uint32_t x = c4[c], bit = 1u << (4 * i + c);
-            const bool e = x == GF_LRU_C_EMPTY, t = x == GF_LRU_C_TOMB;
-            const bool k = !e && !t && ((x & GF_LRU_C_NEG) || (x & GF_LRU_C_KMASK) - GF_LRU_C_KEY <= ck);
-            emp |= e ? bit : 0u;
-            tmb |= t ? bit : 0u;
-            kil |= k ? bit : 0u;
-        }
-    }
-    return {emp, tmb, kil};
-}
-__global__ __launch_bounds__(BLOCK) void k_lru_clusters(gf_htab_desc d, uint32_t mode, const uint32_t *__restrict__ codes,
-                                                        const uint32_t *__restrict__ bits, LruDev *L) {
-    if (!L->cut.active) return;
-    const uint32_t ck = L->cut_key;
-    const uint64_t nw = (d.mask + 1) / 32;
-    const uint32_t vstride = d.vals ? (d.sstride ? d.sstride : d.vsz) : 0u;
-    uint32_t dead = 0, tombs = 0, nmv0 = 0, nmv1 = 0;
-    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t m = bits[w];
-        if (!m) continue;
-        const LruMasks m0 = lru_code_masks(codes, w, ck);
-        while (m) {
-            uint32_t from = (uint32_t)__builtin_ctz(m);
-            uint64_t cw = w;
-            uint32_t emp = m0.emp, tmb = m0.tmb, kil = m0.kil;
-            uint32_t prev = ~0u;                             // occupancy of the chunk before (none in reach)
-            bool hole = false;
-            for (;;) {
-                const uint32_t rng = ~0u << from, e = emp & rng;
-                const uint32_t in = e ? rng & ((1u << __builtin_ctz(e)) - 1u) : rng;   // this chunk's part
-                const uint32_t gone = (tmb | kil) & in;
-                tombs += (uint32_t)__popc(tmb & in);
-                dead += (uint32_t)__popc(kil & in);
-                for (uint32_t g = gone; g; g &= g - 1)
-                    d.slots[(cw * 32 + (uint32_t)__builtin_ctz(g)) * d.slot_size + d.ksz] = GF_SLOT_EMPTY;
-                uint32_t cur = ~emp & ~gone;                 // non-EMPTY slots of the chunk now
-                uint32_t mv = in & ~gone;
-                if (!hole) mv = gone ? mv & ~((2u << __builtin_ctz(gone)) - 1u) : 0u;
-                for (; mv; mv &= mv - 1) {                   // live entries after a hole, in slot order
-                    const uint32_t t = (uint32_t)__builtin_ctz(mv);
-                    const uint64_t j = cw * 32 + t;
-                    const uint32_t dist = codes[j] >> GF_LRU_C_DSH;
-                    if (dist <= 32 + t && dist < 255) {          // home within this chunk or the one before
-                        const uint64_t win = ((uint64_t)cur << 32) | prev;
-                        const uint32_t pj = 32 + t, ph = pj - dist;
-                        const uint64_t span = ((1ull << pj) - 1ull) & ~((1ull << ph) - 1ull);
-                        const uint64_t fr = ~win & span;
-                        if (fr) {
-                            const uint32_t pp = (uint32_t)__builtin_ctzll(fr);
-                            const uint64_t p = pp >= 32 ? cw * 32 + (pp - 32) : (cw ? cw - 1 : nw - 1) * 32 + pp;
-                            gc_move(d, j, p, vstride);
-                            nmv0++;
-                            cur &= ~(1u << t);
-                            if (pp >= 32) cur |= 1u << (pp - 32); else prev |= 1u << pp;
-                        }
-                    } else {                                     // further back: the table's state bytes
-                        uint64_t home = (j - dist) & d.mask;
-                        if (dist == 255) home = lru_home(d, j, mode);    // capped: the home from the key
-                        for (uint64_t p = home; p != j; p = (p + 1) & d.mask) {
-                            if (d.slots[p * d.slot_size + d.ksz] == GF_SLOT_EMPTY) {
-                                gc_move(d, j, p, vstride);
-                                nmv1++;
-                                cur &= ~(1u << t);
-                                if (p / 32 == cw) cur |= 1u << (p % 32);
-                                else if (p / 32 == (cw ? cw - 1 : nw - 1)) prev |= 1u << (p % 32);
-                                break;
-                            }
-                        }
-                    }
-                }
-                if (gone) hole = true;
-                if (e) break;                                // the cluster ended in this chunk
-                // it continues into the next word (wrapping; a start implies an
-                // EMPTY slot before it, so the walk ends by word w at the latest)
-                cw = cw + 1 == nw ? 0 : cw + 1;
-                const LruMasks mc = lru_code_masks(codes, cw, ck);
-                emp = mc.emp; tmb = mc.tmb; kil = mc.kil;
-                prev = cur;
-                from = 0;
+        const unsigned long long total = part[1023], need = (total + 1) / 2, before = t ? part[t - 1] : 0ull;
+        if (total && before < need && part[t] >= need) {  // the median bin lies in this thread's range
+            unsigned long long acc = before;
+            for (uint32_t k = 0; k < PER; k++) {
+                acc += L->hist[t * PER + k];
+                if (acc >= need) { s_k = t * PER + k; s_es = acc; break; }
             }
-            m = cw != w ? 0u : m & (m - 1);                  // past the word: no later start in it
+        }
+        __syncthreads();
+        if (t == 0) {
+            L->K = s_k; L->es = s_es;
+            L->target = (unsigned long long)(max_entries - max_entries / 8u);
+            L->ev_h0 = L->hand; L->ev_lines = 0; L->evicted = 0;
         }
     }
-    if (dead) atomicAdd(&L->res[0], (unsigned long long)dead);
-    if (tombs) atomicAdd(&L->res[1], (unsigned long long)tombs);
-    if (nmv0) atomicAdd(&L->moves[0], (unsigned long long)nmv0);
-    if (nmv1) atomicAdd(&L->moves[1], (unsigned long long)nmv1);
-}
-__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L) {
-    if (!L->cut.active) return;
-    const unsigned long long ev = L->res[0];
-    *count = (uint32_t)(*count - ev);
-    const uint32_t k = L->nlog;
-    if (k < GF_LRU_LOGCAP) {
-        L->log[k].seq = seq; L->log[k].now = now;
-        L->log[k].cut_c = L->cut.c; L->log[k].cut_o = L->cut.o; L->log[k].evicted = ev;
+    if (t == 0) {
+        const unsigned long long c = *count;
+        unsigned long long lines = 0;
+        if (c > max_entries && L->ev_lines < nl) {
+            const unsigned long long q = c - L->target;
+            lines = L->es ? (q * sl + L->es - 1) / L->es : nl;
+            lines = lines < nl - L->ev_lines ? lines : nl - L->ev_lines;
+        }
+        L->h0 = L->hand; L->lines = lines; L->kills = 0; L->cleared = 0;
+        L->hand = (L->hand + lines) % nl;
+        L->ev_lines += lines;
     }
-    L->nlog = k + 1;
-    L->cut.active = 0;
+}
+// The hand over this round's lines: the slots from the first line's first slot,
+// lines * SPL of them, in chunks of GF_LRU_CHUNK, plus the cluster running past
+// the last one (entries homed in the range).  Launched twice, PAR = 0 for the
+// even chunks and 1 for the odd ones: a chunk's last slots turn EMPTY only if the
+// slots after it, up to the cluster's end, are all gone too, which the block
+// reads from the next chunk (at most one chunk ahead, else it keeps them FREE) —
+// untouched in the even launch, final in the odd one, so no read races a write.
+// The slots past the last chunk are read and written by its block alone (there
+// deleted entries turn FREE).  Codes: 0 EMPTY, 1 kept, 2 deleted now, 3 a
+// tombstone or FREE slot (cleared).
+template <int KIND, int PAR>
+__global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                        uint64_t nl) {
+    if (!L->flag) return;
+    const unsigned long long lines = L->lines;
+    if (!lines) return;
+    using S = LruSlot<KIND>;
+    constexpr uint32_t U = GF_LRU_CHUNK / GF_LRU_HT;
+    const uint32_t K = L->K;
+    const unsigned long long h0 = L->h0;
+    const uint64_t ns = d.mask + 1, P0 = h0 * S::SPL, NP = lines * S::SPL;
+    const bool whole = NP >= ns;
+    const uint64_t nch = (NP + GF_LRU_CHUNK - 1) / GF_LRU_CHUNK;
+    __shared__ uint8_t code[GF_LRU_CHUNK];
+    __shared__ uint32_t s_ef, s_kills, s_clr;
+    auto code_of = [&](const S &s) -> uint32_t {
+        if (s.st == GF_SLOT_EMPTY) return 0u;
+        if (s.st == GF_SLOT_TOMB || s.st == GF_SLOT_FREE) return 3u;
+        if (s.st != GF_SLOT_FULL || lru_age_key(s.lt, s.fl, now) > K) return 1u;
+        const uint64_t hl = s.home_line(d, mode);
+        return (hl + nl - h0) % nl < lines ? 2u : 1u;
+    };
+    if (threadIdx.x == 0) { s_kills = 0; s_clr = 0; }
+    uint32_t kills = 0, clr = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t c = 2 * (uint64_t)blockIdx.x + PAR; c < nch; c += 2 * (uint64_t)gridDim.x) {
+        const uint64_t base = c * GF_LRU_CHUNK;
+        const uint32_t cnt = (uint32_t)(NP - base < GF_LRU_CHUNK ? NP - base : GF_LRU_CHUNK);
+        uint32_t mine[U], ost[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t off = u * GF_LRU_HT + threadIdx.x;
+            mine[u] = 1u; ost[u] = GF_SLOT_FULL;
+            if (off < cnt) {
+                S s;
+                s.load(d, (P0 + base + off) & d.mask);
+                mine[u] = code_of(s);
+                ost[u] = s.st;
+                code[off] = (uint8_t)mine[u];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {                          // wave 0: the slots after the chunk
+            const bool last = base + cnt == NP;
+            bool ef = false, decided = false;
+            if (!(last && whole)) {
+                for (uint64_t q = 0;; q += 64) {
+                    if (!last && q >= GF_LRU_CHUNK) break;                 // undecided: the chunk's run stays FREE
+                    const uint64_t o = base + cnt + q + lane;              // offset from P0
+                    uint32_t cd = 0;
+                    if (o < ns) {                                          // never back into the range
+                        S s;
+                        const uint64_t j = (P0 + o) & d.mask;
+                        s.load(d, j);
+                        cd = code_of(s);
+                        if (last && cd == 2) { lru_clear_slot<KIND>(d, j, GF_SLOT_FREE); kills++; }
+                    }
+                    const uint64_t stop_m = __ballot(cd <= 1u);
+                    if (!decided && stop_m) {
+                        ef = __shfl(cd, (int)((uint32_t)__ffsll((unsigned long long)stop_m) - 1u)) == 0u;
+                        decided = true;
+                    }
+                    if (!last && decided) break;
+                    if (last && __ballot(cd == 0u)) break;                 // the cluster past the range ends
+                }
+            }
+            if (lane == 0) s_ef = decided && ef ? 1u : 0u;
+        }
+        __syncthreads();
+        const bool ef = s_ef != 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t off = u * GF_LRU_HT + threadIdx.x;
+            if (off >= cnt || mine[u] < 2u) continue;
+            bool to_empty = ef;
+            for (uint32_t k = off + 1; k < cnt; k++) {
+                const uint32_t x = code[k];
+                if (x <= 1u) { to_empty = x == 0u; break; }
+            }
+            const uint32_t nst = to_empty ? GF_SLOT_EMPTY : GF_SLOT_FREE;
+            if (mine[u] == 2u) kills++;
+            else if (ost[u] != nst) clr++;
+            if (mine[u] == 2u || ost[u] != nst) lru_clear_slot<KIND>(d, (P0 + base + off) & d.mask, nst);
+        }
+        __syncthreads();                                 // code[] is the next chunk's
+    }
+    if (kills) atomicAdd(&s_kills, kills);
+    if (clr) atomicAdd(&s_clr, clr);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_kills) atomicAdd(&L->kills, (unsigned long long)s_kills);
+        if (s_clr) atomicAdd(&L->cleared, (unsigned long long)s_clr);
+    }
+}
+// After a round: the count, and after the last one the log (hcount: the count
+// for the host's bound, pinned host memory, may be null).
+__global__ void k_lru_round_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t last,
+                                uint32_t *hcount) {
+    if (!L->flag) {
+        if (last && hcount) *hcount = *count;
+        return;
+    }
+    const unsigned long long k = L->kills;
+    *count = (uint32_t)(*count - k);
+    L->evicted += k;
+    L->kills = 0;
+    if (last) {
+        const uint32_t n = L->nlog;
+        if (n < GF_LRU_LOGCAP) {
+            LruLog &g = L->log[n];
+            g.seq = seq; g.now = now; g.age_cut = L->K; g.pad = 0;
+            g.hand = L->ev_h0; g.lines = L->ev_lines; g.evicted = L->evicted;
+        }
+        L->nlog = n + 1;
+        L->flag = 0;
+        if (hcount) *hcount = *count;
+    }
 }
 
 // ================================================================ drop notifications
@@ -5317,6 +5282,15 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
     return 0;
 }
 
+// The host's bound of a CT map's device count (ct_limits, lru_evict) tightened
+// from the count the last eviction chain wrote to pinned host memory, once the
+// event behind it has fired (a query, never a wait): that count plus what the
+// calls enqueued since may have added.
+static void ct_count_refresh(Map &m) {
+    if (!m.ev_pending || !m.ev_count || hipEventQuery(m.ev_count) != hipSuccess) return;
+    m.ev_pending = false;
+    m.dev_count_hi = std::min<uint64_t>(m.dev_count_hi, (uint64_t)*m.h_evcount + (m.cnt_add - m.cnt_add_ev));
+}
 // Element accounting mode of the CT maps for a batch of n packets inserting at
 // most per_pkt entries each (see ingress_run); fills the launch descriptors.
 static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map> &ct6m, uint32_t n, uint32_t per_pkt,
@@ -5326,10 +5300,12 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
     if (ct6m) cfg_ct6 = ct6m->hdesc();
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
-        // LRU: never fails in the kernel (it evicts); here no eviction in classify, the
-        // entries stay until GC, bounded by the slot array (7/8 load = 3.5 x max_entries)
-        uint64_t limit = m->type == GF_MAP_TYPE_LRU_HASH ? m->ht.nslots / 8 * 7 : m->max_entries;
-        if (m->host_valid) m->dev_count_hi = m->ht.count;
+        // LRU: never fails in the kernel (it evicts); here no eviction inside a classify
+        // call, the entries stay until the eviction pass after it (lru_evict), bounded by
+        // the slot array (7/8 load = 3.5 x max_entries)
+        const uint64_t limit = dev_insert_limit(*m);
+        if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = false; }
+        ct_count_refresh(*m);
         // (no readback when the batch alone could exceed the limit: strict either way)
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && (uint64_t)per_pkt * n <= limit && !m->host_valid) {
             if (getenv("GF_SYNC_DEBUG"))
@@ -5340,9 +5316,11 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
                 hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
                 return -EIO;
             m->dev_count_hi = dc;
+            m->ev_pending = false;
         }
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit) strict |= m == ct4m ? 1u : 2u;
         m->dev_count_hi += (uint64_t)per_pkt * n;
+        m->cnt_add += (uint64_t)per_pkt * n;
         if (m->type == GF_MAP_TYPE_LRU_HASH) {
             if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
             else cfg_ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
@@ -5364,58 +5342,73 @@ static int ct_sweep_bufs(Map &m, LruDev *&L, uint32_t *&bits) {
     bits = (uint32_t *)m.d_gcbits.p;
     return 0;
 }
-// starts_done: the cluster-start bits were written by k_lru_hist.
-static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s, bool starts_done = false) {
+static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
     const gf_htab_desc d = m.hdesc();
     const uint32_t lt_off = m.ht.codec == GF_VCODEC_CT ? 0u : 32u;
     const uint64_t nw = (d.mask + 1 + 31) / 32;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, 65535u * 8);
-    if (!starts_done)
-        hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, bits, (const GcCut *)&L->cut);
+    hipLaunchKernelGGL(k_gc_starts, dim3(grid), dim3(BLOCK), 0, s, d, bits, (const GcCut *)&L->cut);
     hipLaunchKernelGGL(k_gc_clusters, dim3(grid), dim3(BLOCK), 0, s, d, m.ht.mode, lt_off, (const GcCut *)&L->cut,
                        (const uint32_t *)bits, L->res);
 }
 // The LRU stand-in after a classify call (k_lru_*: see the kernels): fully on the
-// device, a no-op launch chain unless the map's count exceeds max_entries.
+// device, a chain of launches that exit at once unless the map's count exceeds
+// max_entries.
 static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s) {
     if (!m || m->type != GF_MAP_TYPE_LRU_HASH || !m->d_slots.p) return 0;
     m->lru_seq++;
+    ct_count_refresh(*m);
     if (m->dev_count_hi <= m->max_entries) return 0;    // cannot have crossed max_entries
     LruDev *L;
     uint32_t *bits;
     int r;
     if ((r = ct_sweep_bufs(*m, L, bits))) return r;
-    if (m->d_lrucodes.bytes < m->ht.nslots * 4 && m->d_lrucodes.ensure(m->ht.nslots * 4)) return -ENOMEM;
-    uint32_t *codes = (uint32_t *)m->d_lrucodes.p;
     const gf_htab_desc d = m->hdesc();
-    const uint32_t lt_off = m->ht.codec == GF_VCODEC_CT ? 0u : 32u;
-    ProfScope ps("k_lru_evict", s);
-    if ((d.mask + 1) % 32) return -EIO;                  // k_lru_clusters' word walk (LRU maps: >= 64, 2^k)
-    hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, (const uint32_t *)d.count, m->max_entries, L);
-    const uint32_t gh = (uint32_t)std::min<uint64_t>((d.mask + 1 + GF_LRU_HB * GF_LRU_U - 1) / (GF_LRU_HB * GF_LRU_U),
-                                                     resident_blocks(2));   // 48 KB of LDS a block
-    if (d.slot_size == 32 && d.ksz == 14 && d.vin && d.voff + lt_off == 16)
-        hipLaunchKernelGGL(k_lru_hist<1>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
-    else if (d.slot_size == 64 && d.ksz == 40 && d.vin && d.voff + lt_off == 48)
-        hipLaunchKernelGGL(k_lru_hist<2>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
-    else
-        hipLaunchKernelGGL(k_lru_hist<0>, dim3(gh), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, lt_off, now, L, bits, codes);
-    hipLaunchKernelGGL(k_lru_cut, dim3(1), dim3(1024), 0, s, (const uint32_t *)d.count, now, L);
-    const uint64_t nw = (d.mask + 1) / 32;
-    hipLaunchKernelGGL(k_lru_clusters, dim3((uint32_t)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK, resident_blocks(8))),
-                       dim3(BLOCK), 0, s, d, m->ht.mode, (const uint32_t *)codes, (const uint32_t *)bits, L);
-    hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L);
-    // the chain leaves the device count at most max_entries (it evicts down to 7/8 of
-    // it when above): a tighter host bound, so ct_limits of the next calls does not
-    // read the count back (a stream sync) while the map runs near its capacity
-    m->dev_count_hi = std::min<uint64_t>(m->dev_count_hi, m->max_entries);
+    const int kind = d.slot_size == 32 && d.ksz == 14 && d.vin == 16 && d.voff == 16 ? 1
+                   : d.slot_size == 64 && d.ksz == 40 && d.vin == 16 && d.voff == 48 ? 2 : 0;
+    if (!kind) return -EIO;                              // the CT codec's layouts only
+    if (!m->h_evcount) {
+        void *p = nullptr;
+        if (hip_ok(hipHostMalloc(&p, 64, hipHostMallocMapped), "lru count word") ||
+            hip_ok(hipEventCreateWithFlags(&m->ev_count, hipEventDisableTiming), "lru count event"))
+            return -ENOMEM;
+        m->h_evcount = (uint32_t *)p;
+    }
+    uint32_t *hc = nullptr;
+    if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount, 0), "lru count word")) return -EIO;
+    const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size, nl = ns / spl;
+    const uint64_t sl = nl <= 65536 ? nl : nl >> GF_LRU_SAMPLE_SHIFT;
+    const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
+    const uint32_t gh = resident_blocks(8);
+    const uint32_t *cnt = (const uint32_t *)d.count;
+    {
+        ProfScope ps("k_lru_evict", s);
+        hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, cnt, m->max_entries, L);
+        if (kind == 1) hipLaunchKernelGGL(k_lru_sample<1>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl);
+        else hipLaunchKernelGGL(k_lru_sample<2>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl);
+        for (uint32_t round = 0; round < 2; round++) {
+            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, m->max_entries, L, nl, sl, round);
+            if (kind == 1) {
+                hipLaunchKernelGGL((k_lru_hand<1, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<1, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+            } else {
+                hipLaunchKernelGGL((k_lru_hand<2, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<2, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+            }
+            hipLaunchKernelGGL(k_lru_round_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, round, hc);
+        }
+    }
+    if (hip_ok(hipEventRecord(m->ev_count, s), "lru count event")) return -EIO;
+    m->ev_pending = true;
+    m->cnt_add_ev = m->cnt_add;
     static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
     if (stats) {
         LruDev h;
         if (!hip_ok(hipMemcpyAsync(&h, L, offsetof(LruDev, log), hipMemcpyDeviceToHost, s), "lru stats") &&
-            !hip_ok(hipStreamSynchronize(s), "lru stats") && h.res[0] + h.res[1])
-            fprintf(stderr, "[lru] seq %u now %u: evicted %llu tombs %llu moved %llu (masks) + %llu (table)\n",
-                    m->lru_seq, now, h.res[0], h.res[1], h.moves[0], h.moves[1]);
+            !hip_ok(hipStreamSynchronize(s), "lru stats") && h.ev_lines)
+            fprintf(stderr, "[lru] seq %u now %u: K %u es %llu lines %llu of %llu (hand %llu) evicted %llu, last round "
+                    "cleared %llu\n", m->lru_seq, now, h.K, h.es, h.ev_lines, (unsigned long long)nl, h.ev_h0,
+                    h.evicted, h.cleared);
     }
     return hip_ok(hipGetLastError(), "k_lru_evict");
 }
@@ -5881,6 +5874,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     cnt = cnt >= r[0] ? cnt - (uint32_t)r[0] : 0u;
     if (hip_ok(hipMemcpy(m->d_count.p, &cnt, 4, hipMemcpyHostToDevice), "gc count")) return -EIO;
     m->dev_count_hi = cnt;
+    m->ev_pending = false;
     m->device_modified();
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
@@ -6000,8 +5994,7 @@ int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n
     const bool had = m.dev_auth();
     uint64_t before = 0;
     if (had) { uint32_t c; if (m.dev_count(c)) return 0; before = c; }
-    const uint64_t limit = m.type == GF_MAP_TYPE_LRU_HASH ? m.ht.nslots / 8 * 7 : m.max_entries;
-    if (before + n > limit) return 0;                   // the host path reports E2BIG at the exact element
+    if (before + n > dev_insert_limit(m)) return 0;     // the host path reports E2BIG at the exact element
     static std::mutex mu;
     std::lock_guard<std::mutex> lk(mu);
     static DevBuf dk, dv, dh, dhs, didx, tmp, dflag;
@@ -6046,6 +6039,7 @@ int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n
     m.host_valid = false;
     m.dev_gen++;
     m.dev_count_hi = before + n;
+    m.ev_pending = false;
     fallback = false;
     return 0;
 }

@@ -133,8 +133,8 @@ int64_t HTab::insert_new(const uint8_t *key, const uint8_t *value) {
     uint64_t mask = nslots - 1, i = gf_home_slot(hash(key), mask, slot_size);
     for (uint64_t p = 0; p < nslots; p++) {
         uint8_t st = state(i);
-        if (st == GF_SLOT_EMPTY || st == GF_SLOT_TOMB) {
-            if (st == GF_SLOT_TOMB) tombs--;
+        if (st == GF_SLOT_EMPTY || st == GF_SLOT_TOMB || st == GF_SLOT_FREE) {
+            if (st != GF_SLOT_EMPTY) tombs--;
             uint8_t *s = &slots[i * slot_size];
             memset(s, 0, slot_size);
             memcpy(s, key, ksz);
@@ -213,6 +213,11 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
     }
 }
 
+Map::~Map() {
+    if (ev_count) (void)hipEventDestroy(ev_count);
+    if (h_evcount) (void)hipHostFree(h_evcount);
+}
+
 // Fixed-capacity maps are materialized lazily: slots.size()==0 means all-empty.
 static void materialize(HTab &h) {
     if (h.slots.empty() && h.nslots) {
@@ -286,7 +291,7 @@ int Map::pull() {
     for (uint64_t i = 0; i < ht.nslots; i++) {
         uint8_t st = ht.state(i);
         if (st == GF_SLOT_FULL) c++;
-        else if (st == GF_SLOT_TOMB) t++;
+        else if (st == GF_SLOT_TOMB || st == GF_SLOT_FREE) t++;
     }
     ht.count = c; ht.tombs = t;
     host_valid = true;
@@ -323,12 +328,6 @@ int Map::push(hipStream_t s) {
     if ((r = d_slots.ensure(ht.nslots * ht.slot_size))) return r;
     if (ht.sstride && (r = d_vals.ensure(ht.nslots * ht.sstride))) return r;
     if ((r = d_count.ensure(8))) return r;
-    // LRU conntrack maps: the eviction sweep's 4-B code per slot (k_lru_hist ->
-    // k_lru_clusters), allocated with the slots so its cost shows at the push and
-    // a classify call never fails on it after its inserts are on the device
-    if (type == GF_MAP_TYPE_LRU_HASH && ht.codec == GF_VCODEC_CT && d_lrucodes.bytes < ht.nslots * 4 &&
-        (r = d_lrucodes.ensure(ht.nslots * 4)))
-        return r;
     if (ht.slots.empty()) {
         if (hip_ok(hipMemsetAsync(d_slots.p, 0, d_slots.bytes, s), "memset slots")) return -EIO;
         if (ht.sstride && hip_ok(hipMemsetAsync(d_vals.p, 0, d_vals.bytes, s), "memset vals")) return -EIO;
@@ -485,7 +484,7 @@ int Map::dev_find(const uint8_t *key, int64_t &slot, int64_t &ins) {
             const uint8_t *sl = &buf[k * ss];
             const uint8_t st = sl[ksz];
             if (st == GF_SLOT_EMPTY) { if (ins < 0) ins = (int64_t)(i + k); return 0; }
-            if (st == GF_SLOT_TOMB) { if (ins < 0) ins = (int64_t)(i + k); continue; }
+            if (st == GF_SLOT_TOMB || st == GF_SLOT_FREE) { if (ins < 0) ins = (int64_t)(i + k); continue; }
             if (st == GF_SLOT_FULL && memcmp(sl, key, ksz) == 0) { slot = (int64_t)(i + k); return 0; }
         }
         p += nr;
@@ -525,6 +524,7 @@ int Map::dev_count(uint32_t &c) {
 
 int Map::dev_set_count(uint32_t c) {
     dev_count_hi = c;
+    ev_pending = false;
     return dev_wr(*this, d_count.p, &c, 4);
 }
 
@@ -550,15 +550,6 @@ int Map::dev_next_full(uint64_t start, int64_t &slot) {
         c = base + nk_n;
     }
     return 0;
-}
-
-// Element ceiling of an insert: HASH maps end at max_entries (-E2BIG).  LRU
-// conntrack maps (which the kernel never lets fail: it evicts) take entries up to
-// the slot array's 7/8 load and are brought back under max_entries by the
-// eviction sweep of the next classify call that binds them (lru_evict); other LRU
-// maps have no eviction path here and end at max_entries like HASH maps.
-static uint64_t dev_insert_limit(const Map &m) {
-    return m.type == GF_MAP_TYPE_LRU_HASH && m.ht.codec == GF_VCODEC_CT ? m.ht.nslots / 8 * 7 : m.max_entries;
 }
 
 static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t fl, bool &fallback) {

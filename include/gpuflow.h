@@ -485,19 +485,24 @@ int gf_pipeline_partition(int pipe, const gf_pipe_batch *batch, uint32_t self_ra
 int gf_ct_gc(int map, uint32_t filter_time, void *stream);
 
 /* ---- LRU CT maps (BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:53-75) ----
- * The kernel evicts from per-CPU LRU lists in a nondeterministic order and
- * never fails an insert.  libgpuflow's deterministic stand-in:
- * inside a batch an LRU CT map may exceed max_entries (up to the 7/8 load of
- * its slot array, 4 x max_entries); at the end of every classify call that
- * uses it, if the count exceeds max_entries, the oldest entries are deleted
- * until at most max_entries - max_entries/8 remain — closing entries first,
- * then the others, each by ascending last use (lifetime minus the timeout its
- * flags select) in one-second bins.  Every eviction is logged: */
+ * The kernel evicts from per-CPU LRU lists (the tail of an inactive list kept
+ * about as long as the active one) in a nondeterministic order and never fails
+ * an insert.  libgpuflow's deterministic stand-in: inside a batch an
+ * LRU CT map may exceed max_entries (up to the 7/8 load of its slot array, 4 x
+ * max_entries); at the end of every classify call that uses it, if the count
+ * exceeds max_entries, a hand sweeping the table's home lines deletes the
+ * entries of the older half (age key <= age_cut: the median age of a fixed
+ * 1/64 sample of the lines — closing entries older than all others, then by
+ * last use in one-second bins) homed in the lines it passes, as many lines as
+ * bring the count to max_entries - max_entries/8 by the sample's density.
+ * Every eviction is logged: */
 typedef struct gf_ct_evict_rec {
     uint32_t seq;              /* the map's classify call (1 = first call that used the map) */
     uint32_t now_sec;          /* that call's now_sec */
-    uint64_t cut_closing;      /* closing entries last used before cut_closing were deleted */
-    uint64_t cut_other;        /* other entries last used before cut_other were deleted */
+    uint32_t age_cut;          /* entries with age key <= age_cut were eligible */
+    uint32_t pad;
+    uint64_t hand_line;        /* the first home line the hand passed */
+    uint64_t lines;            /* home lines passed (from hand_line, wrapping) */
     uint64_t evicted;          /* entries deleted */
 } gf_ct_evict_rec;
 /* Copies up to max records (oldest first) and returns the number logged. */

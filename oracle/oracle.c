@@ -99,6 +99,7 @@ struct om_map {
     uint32_t type, ksz, vsz, max_entries, nshards;
     uint32_t koff, rs;              /* value offset in a record, record stride */
     uint32_t count;                 /* total elements (atomic across shards) */
+    uint64_t lru_hand;              /* LRU CT maps: the eviction hand's next home line */
     uint8_t lens_present[129];      /* LPM: prefix lengths present (count) */
     uint32_t lens_cnt[129];
     om_shard *sh;
@@ -1855,73 +1856,179 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
 
 /* ------------------------------------------------------------------ */
 /* LRU stand-in (the CT maps are BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:  */
-/* 53-75).  The kernel evicts from per-CPU LRU lists in an order that   */
-/* is not reproducible; libgpuflow and this restatement share one       */
-/* deterministic rule instead: after a batch, if count >     */
-/* max_entries, delete the smallest prefix of the age order — closing   */
-/* entries (rx_closing | tx_closing) first, then the others, each by    */
-/* ascending last use in one-second bins relative to now (bin 0 =       */
-/* last used 65535 s or more ago) — that leaves at most                 */
-/* max_entries - max_entries / 8 entries.  Last use = lifetime minus   */
-/* the timeout the entry's flags select (every lifetime writer sets it  */
-/* to now + that timeout, conntrack.h:47-62,127,527).                   */
+/* 53-75).  The kernel evicts from per-CPU LRU lists — the tail of an   */
+/* inactive list kept about as long as the active one — in an order    */
+/* that is not reproducible; libgpuflow and this restatement share one  */
+/* deterministic rule instead (include/gpuflow.h):        */
+/* after a batch, if count > max_entries, a hand sweeping the home      */
+/* lines of libgpuflow's slot array deletes the entries of the older    */
+/* half homed in the lines it passes:                                   */
+/*  * age key: 0 if the last use lies before time 0, else closing       */
+/*    entries (rx_closing | tx_closing) in [0, 65536), the others in    */
+/*    [65536, 131072), by last use in one-second bins relative to now   */
+/*    (bin 0 = last used 65535 s or more ago).  Last use = lifetime     */
+/*    minus the timeout the entry's flags select (every lifetime writer */
+/*    sets it to now + that timeout, conntrack.h:47-62,127,527);        */
+/*  * home line: (CT hash of the key & (NS - 1)) / SPL, NS = the slot   */
+/*    array (pow2ceil(max(64, 4 x max_entries))), SPL = 128-B line /    */
+/*    slot (4 for ipv4_ct_tuple, 2 for ipv6_ct_tuple); NL = NS / SPL;   */
+/*  * sample = entries homed below SL = NL >> 6 (NL when NL <= 65536);  */
+/*    K = the smallest age key with at least half of the sample at or   */
+/*    below it, es = the sample's entries with age key <= K;            */
+/*  * up to two rounds while count > max_entries: Q = count - (max -    */
+/*    max / 8), lines = min(NL - lines so far, ceil(Q SL / es)) (NL if  */
+/*    es = 0); delete every entry with age key <= K homed in           */
+/*    [hand, hand + lines) (mod NL); hand += lines.                     */
 /* ------------------------------------------------------------------ */
 #define LRU_BINS 65536u
-typedef struct lru_ctx { uint32_t now; uint64_t *hist; } lru_ctx;
 static int64_t ct_last_use(uint32_t lt, uint16_t fl) {
     const uint32_t to = ((fl & 1u) && (fl & 2u)) ? CT_CLOSE_TIMEOUT : ((fl & 16u) ? CT_DEFAULT_LIFETIME : CT_SYN_TIMEOUT);
     return (int64_t)lt - (int64_t)to;
 }
-static uint32_t lru_key(uint32_t lt, uint16_t fl, uint32_t now) {
-    const int64_t base = (int64_t)now - (int64_t)(LRU_BINS - 1);
-    int64_t b = ct_last_use(lt, fl) - base;
+static uint32_t lru_age_key(const uint8_t *v, uint32_t now) {
+    uint32_t lt; uint16_t fl;
+    memcpy(&lt, v + 32, 4); memcpy(&fl, v + 36, 2);
+    const int64_t lu = ct_last_use(lt, fl);
+    if (lu < 0) return 0u;
+    int64_t b = lu - ((int64_t)now - (int64_t)(LRU_BINS - 1));
     b = b < 0 ? 0 : (b > (int64_t)(LRU_BINS - 1) ? (int64_t)(LRU_BINS - 1) : b);
     return ((fl & 3u) ? 0u : LRU_BINS) + (uint32_t)b;
 }
-static void lru_visit(const void *k, const void *v, void *c_) {
-    (void)k;
-    lru_ctx *c = (lru_ctx *)c_;
-    uint32_t lt; uint16_t fl;
-    memcpy(&lt, (const uint8_t *)v + 32, 4); memcpy(&fl, (const uint8_t *)v + 36, 2);
-    c->hist[lru_key(lt, fl, c->now)]++;
+/* libgpuflow's CT hash (gf_common.h gf_key_hash, mode CT): a murmur3-style mix
+ * of the canonical tuple — addresses and ports unordered, flags without
+ * TUPLE_F_IN — as little-endian u32 words. */
+static uint32_t gfh_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static uint32_t gfh_words(const uint32_t *w, int nw, uint32_t nbytes) {
+    uint32_t h = 0x9747b28cu ^ nbytes;
+    for (int i = 0; i < nw; i++) {
+        uint32_t k = w[i] * 0xcc9e2d51u;
+        k = gfh_rotl(k, 15);
+        k *= 0x1b873593u;
+        h ^= k;
+        h = gfh_rotl(h, 13);
+        h = h * 5u + 0xe6546b64u;
+    }
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
 }
-int o_ct_lru_cutoffs(om_map *m, uint32_t now, uint64_t *cut_c, uint64_t *cut_o) {
-    *cut_c = *cut_o = 0;
+static uint32_t gf_ct_hash(const uint8_t *key, uint32_t ksz) {
+    uint32_t w[10] = {0};
+    memcpy(w, key, ksz);
+    if (ksz == 14) {
+        const uint32_t a = w[0], b = w[1], p0 = w[2] & 0xffffu, p1 = w[2] >> 16;
+        const uint32_t c[4] = {a < b ? a : b, a < b ? b : a, (p0 < p1 ? p0 : p1) | ((p0 < p1 ? p1 : p0) << 16),
+                               (w[3] & 0xffu) | (((w[3] >> 8) & 0xfeu) << 8)};
+        return gfh_words(c, 4, 14);
+    }
+    int less = 0;                                   /* word-wise compare of the two addresses */
+    for (int i = 0; i < 4; i++) if (w[i] != w[4 + i]) { less = w[i] < w[4 + i]; break; }
+    const uint32_t p0 = w[8] & 0xffffu, p1 = w[8] >> 16;
+    uint32_t c[10];
+    for (int i = 0; i < 4; i++) { c[i] = less ? w[i] : w[4 + i]; c[4 + i] = less ? w[4 + i] : w[i]; }
+    c[8] = (p0 < p1 ? p0 : p1) | ((p0 < p1 ? p1 : p0) << 16);
+    c[9] = (w[9] & 0xffu) | (((w[9] >> 8) & 0xfeu) << 8);
+    return gfh_words(c, 10, 40);
+}
+typedef struct lru_geo { uint64_t ns, nl, sl; uint32_t spl; } lru_geo;
+static lru_geo lru_geometry(const om_map *m) {
+    lru_geo g;
+    uint64_t want = 4ull * m->max_entries;
+    g.ns = 64;
+    while (g.ns < want) g.ns <<= 1;
+    g.spl = m->ksz == 14 ? 4u : 2u;
+    g.nl = g.ns / g.spl;
+    g.sl = g.nl <= 65536 ? g.nl : g.nl >> 6;
+    return g;
+}
+static uint64_t lru_home_line(const om_map *m, const lru_geo *g, const uint8_t *key) {
+    return ((uint64_t)gf_ct_hash(key, m->ksz) & (g->ns - 1)) / g->spl;
+}
+/* the passes run one thread per shard group */
+typedef struct lru_job {
+    om_map *m; const lru_geo *g; uint32_t now, s0, s1, K;
+    int kill;                                       /* 0: sample histogram, 1: delete */
+    uint64_t h0, lines, done;
+    uint64_t *hist;
+} lru_job;
+static void *lru_worker(void *a_) {
+    lru_job *a = (lru_job *)a_;
+    om_map *m = a->m;
+    for (uint32_t s = a->s0; s < a->s1; s++) {
+        om_shard *h = &m->sh[s];
+        for (uint64_t i = 0; i < h->cap; i++) {
+            if (SH_ST(m, h, i) != 1) continue;
+            const uint8_t *k = SH_KEY(m, h, i);
+            if (!a->kill) {
+                const uint64_t hl = lru_home_line(m, a->g, k);
+                if (hl < a->g->sl) a->hist[lru_age_key(SH_VAL(m, h, i), a->now)]++;
+                continue;
+            }
+            if (lru_age_key(SH_VAL(m, h, i), a->now) > a->K) continue;
+            const uint64_t hl = lru_home_line(m, a->g, k);
+            if ((hl + a->g->nl - a->h0) % a->g->nl >= a->lines) continue;
+            SH_ST(m, h, i) = 2; h->used--; h->tomb++;
+            a->done++;
+        }
+    }
+    return NULL;
+}
+static uint64_t lru_pass(om_map *m, const lru_geo *g, uint32_t now, int kill, uint32_t K, uint64_t h0, uint64_t lines,
+                         uint64_t *hist) {
+    uint32_t nt = m->nshards < 64 ? m->nshards : 64;
+    lru_job jobs[64];
+    pthread_t th[64];
+    for (uint32_t t = 0; t < nt; t++) {
+        jobs[t] = (lru_job){m, g, now, m->nshards * t / nt, m->nshards * (t + 1) / nt, K, kill, h0, lines, 0,
+                            kill ? NULL : (uint64_t *)calloc(2 * LRU_BINS, sizeof(uint64_t))};
+        if (nt > 1) pthread_create(&th[t], NULL, lru_worker, &jobs[t]);
+        else lru_worker(&jobs[t]);
+    }
+    uint64_t done = 0;
+    for (uint32_t t = 0; t < nt; t++) {
+        if (nt > 1) pthread_join(th[t], NULL);
+        done += jobs[t].done;
+        if (!kill) {
+            for (uint32_t k = 0; k < 2 * LRU_BINS; k++) hist[k] += jobs[t].hist[k];
+            free(jobs[t].hist);
+        }
+    }
+    if (kill) __atomic_sub_fetch(&m->count, (uint32_t)done, __ATOMIC_RELAXED);
+    return done;
+}
+/* The hand after a batch: 1 and the log record (age_cut, first line, lines,
+ * evicted) if it evicted, else 0.  The hand's position lives in the map. */
+int o_ct_lru_evict(om_map *m, uint32_t now, uint32_t *age_cut, uint64_t *hand, uint64_t *lines, uint64_t *evicted) {
     if (m->count <= m->max_entries) return 0;
-    const uint64_t target = m->max_entries - m->max_entries / 8u, need = m->count - target;
-    uint64_t *h = (uint64_t *)calloc(2 * LRU_BINS, sizeof(uint64_t));
-    lru_ctx c = {now, h};
-    om_foreach(m, lru_visit, &c);
-    uint64_t acc = 0;
-    uint32_t kb = 2 * LRU_BINS - 1;
-    for (uint32_t k = 0; k < 2 * LRU_BINS; k++) { acc += h[k]; if (acc >= need) { kb = k; break; } }
-    free(h);
-    const int64_t base = (int64_t)now - (int64_t)(LRU_BINS - 1);
-    #define CUT_OF(b) ((b) == LRU_BINS - 1 ? (1ull << 32) : (base + (int64_t)(b) + 1 <= 0 ? 0ull : (uint64_t)(base + (int64_t)(b) + 1)))
-    if (kb < LRU_BINS) { *cut_c = CUT_OF(kb); *cut_o = 0; }
-    else { *cut_c = 1ull << 32; *cut_o = CUT_OF(kb - LRU_BINS); }
-    #undef CUT_OF
+    const lru_geo g = lru_geometry(m);
+    uint64_t *hist = (uint64_t *)calloc(2 * LRU_BINS, sizeof(uint64_t));
+    lru_pass(m, &g, now, 0, 0, 0, 0, hist);
+    uint64_t total = 0, acc = 0, es = 0;
+    for (uint32_t k = 0; k < 2 * LRU_BINS; k++) total += hist[k];
+    uint32_t K = 2 * LRU_BINS - 1;
+    const uint64_t need = (total + 1) / 2;
+    if (total)
+        for (uint32_t k = 0; k < 2 * LRU_BINS; k++) { acc += hist[k]; if (acc >= need) { K = k; es = acc; break; } }
+    free(hist);
+    const uint64_t target = m->max_entries - m->max_entries / 8u;
+    *age_cut = K; *hand = m->lru_hand; *lines = 0; *evicted = 0;
+    for (int round = 0; round < 2 && m->count > m->max_entries && *lines < g.nl; round++) {
+        const uint64_t q = m->count - target;
+        uint64_t l = es ? (q * g.sl + es - 1) / es : g.nl;
+        if (l > g.nl - *lines) l = g.nl - *lines;
+        *evicted += lru_pass(m, &g, now, 1, K, m->lru_hand, l, NULL);
+        m->lru_hand = (m->lru_hand + l) % g.nl;
+        *lines += l;
+    }
     return 1;
 }
-typedef struct gc2_ctx { uint64_t cc, co; uint32_t n, cap, ksz; uint8_t *keys; } gc2_ctx;
-static void gc2_visit(const void *k, const void *v, void *c_) {
-    gc2_ctx *c = (gc2_ctx *)c_;
-    uint32_t lt; uint16_t fl;
-    memcpy(&lt, (const uint8_t *)v + 32, 4); memcpy(&fl, (const uint8_t *)v + 36, 2);
-    const int64_t age = ct_last_use(lt, fl);
-    if (age >= 0 && (uint64_t)age >= ((fl & 3u) ? c->cc : c->co)) return;
-    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 1024; c->keys = (uint8_t *)realloc(c->keys, (size_t)c->cap * c->ksz); }
-    memcpy(c->keys + (size_t)c->n * c->ksz, k, c->ksz);
-    c->n++;
-}
-/* The sweep of the rule above: closing entries last used before cut_c, the others before cut_o. */
-uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o) {
-    gc2_ctx c = {cut_c, cut_o, 0, 0, m->ksz, NULL};
-    om_foreach(m, gc2_visit, &c);
-    uint32_t dead = 0;
-    for (uint32_t i = 0; i < c.n; i++) if (om_delete(m, c.keys + (size_t)i * c.ksz) == 0) dead++;
-    free(c.keys);
-    return dead;
+/* The device's logged eviction replayed (a sampled oracle cannot derive K and
+ * the lines from the whole table): deletes entries with age key <= age_cut homed
+ * in [hand, hand + lines); returns how many. */
+uint64_t o_ct_lru_replay(om_map *m, uint32_t now, uint32_t age_cut, uint64_t hand, uint64_t lines) {
+    const lru_geo g = lru_geometry(m);
+    const uint64_t ev = lru_pass(m, &g, now, 1, age_cut, hand, lines, NULL);
+    m->lru_hand = (hand + lines) % g.nl;
+    return ev;
 }
 
 /* Drop notifications of an ingress batch: one record per dropped packet, in

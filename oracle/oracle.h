@@ -194,10 +194,11 @@ void o_egress_batch(const o_prog_array *a, const o_batch *b, uint32_t now_sec, o
 
 /* ctmap.GC (GCFilterByTime): deletes entries with lifetime < filter_time. */
 uint32_t o_ct_gc(om_map *m, uint32_t filter_time);
-/* LRU stand-in (== libgpuflow): 1 and the cutoffs if count > max_entries. */
-int o_ct_lru_cutoffs(om_map *m, uint32_t now, uint64_t *cut_c, uint64_t *cut_o);
-/* Deletes closing entries last used before cut_c and the others last used before cut_o. */
-uint32_t o_ct_gc2(om_map *m, uint64_t cut_c, uint64_t cut_o);
+/* LRU stand-in (== libgpuflow): after a batch, 1 and the eviction's
+ * log record if count > max_entries (the map keeps the hand's position). */
+int o_ct_lru_evict(om_map *m, uint32_t now, uint32_t *age_cut, uint64_t *hand, uint64_t *lines, uint64_t *evicted);
+/* A logged eviction replayed: entries with age key <= age_cut homed in [hand, hand + lines). */
+uint64_t o_ct_lru_replay(om_map *m, uint32_t now, uint32_t age_cut, uint64_t hand, uint64_t lines);
 void o_rows_fp(const uint8_t *keys, const uint8_t *vals, uint64_t n, uint32_t ksz, uint32_t vsz, uint64_t *out);
 
 /* Shard of a CT key (unordered address pair), exposed for pre-population. */

@@ -93,8 +93,9 @@ _s("o_ingress_events", None, VP, C.POINTER(o_batch), VP, VP)
 _s("o_set_trace_sink", None, VP, VP, C.c_uint32, C.c_int)
 _s("o_egress_batch", None, VP, C.POINTER(o_batch), C.c_uint32, VP, VP, VP)
 _s("o_ct_gc", C.c_uint32, VP, C.c_uint32)
-_s("o_ct_lru_cutoffs", C.c_int, VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
-_s("o_ct_gc2", C.c_uint32, VP, C.c_uint64, C.c_uint64)
+_s("o_ct_lru_evict", C.c_int, VP, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+   C.POINTER(C.c_uint64))
+_s("o_ct_lru_replay", C.c_uint64, VP, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64)
 _s("o_rows_fp", None, VP, VP, C.c_uint64, C.c_uint32, C.c_uint32, VP)
 _s("o_get_prefix", C.c_uint32, C.c_int)
 _s("o_ipv6_addr_clear_suffix", None, VP, C.c_int)
@@ -168,15 +169,17 @@ class OMap:
     def ct_gc(self, filter_time):
         return lib.o_ct_gc(self.ptr, filter_time)
 
-    def lru_cutoffs(self, now):
-        """The LRU stand-in's cutoffs for this map's own contents (None: no eviction)."""
-        cc, co = C.c_uint64(0), C.c_uint64(0)
-        if not lib.o_ct_lru_cutoffs(self.ptr, now, C.byref(cc), C.byref(co)):
+    def lru_evict(self, now):
+        """The LRU stand-in after a batch on this map's own contents: None (no
+        eviction) or the log record (age_cut, hand_line, lines, evicted)."""
+        k, h, ln, ev = C.c_uint32(0), C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        if not lib.o_ct_lru_evict(self.ptr, now, C.byref(k), C.byref(h), C.byref(ln), C.byref(ev)):
             return None
-        return cc.value, co.value
+        return k.value, h.value, ln.value, ev.value
 
-    def gc2(self, cut_c, cut_o):
-        return lib.o_ct_gc2(self.ptr, cut_c, cut_o)
+    def lru_replay(self, now, age_cut, hand, lines):
+        """A logged eviction replayed; returns the entries deleted."""
+        return lib.o_ct_lru_replay(self.ptr, now, age_cut, hand, lines)
 
     def dump_arrays(self):
         """All entries as (keys uint8[n, ksz], values uint8[n, vsz])."""

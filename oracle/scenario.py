@@ -60,8 +60,8 @@ class OracleDP:
         self._pipe = None
         self.cfgs = []
         # LRU stand-in: the CT maps the programs bind, each with its
-        # classify-call counter; lru_replay[name] = {seq: (cut_c, cut_o)} replays the
-        # GPU's logged evictions instead (a sampled run holds only part of the table)
+        # classify-call counter; lru_replay[name] = {seq: (age_cut, hand, lines)} replays
+        # the GPU's logged evictions instead (a sampled run holds only part of the table)
         self.lru_maps = sorted({e[k] for e in sc.lxc for k in ("ct4", "ct6") if e.get(k)
                                 and sc.maps[e[k]].type == 9})
         self.lru_seq = {n: 0 for n in self.lru_maps}
@@ -105,12 +105,14 @@ class OracleDP:
             self.lru_seq[n] += 1
             seq = self.lru_seq[n]
             if n in self.lru_replay:
-                cut = self.lru_replay[n].get(seq)
+                e = self.lru_replay[n].get(seq)
+                if e is not None:
+                    ev = self.m[n].lru_replay(now, *e)
+                    self.lru_log[n].append((seq, now) + tuple(e) + (ev,))
             else:
-                cut = self.m[n].lru_cutoffs(now)
-            if cut is not None:
-                ev = self.m[n].gc2(*cut)
-                self.lru_log[n].append((seq, now, cut[0], cut[1], ev))
+                r = self.m[n].lru_evict(now)
+                if r is not None:
+                    self.lru_log[n].append((seq, now) + r)
 
     def ingress(self, pk, now, threads=1, lru=True):
         """handle_policy over the batch; lru=False: part of a call whose LRU step

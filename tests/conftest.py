@@ -13,6 +13,10 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: long-running")
+    # before collection: test modules import cilium_amd, which refuses a library
+    # built from other sources (the session fixture below keeps the same guarantee)
+    import __graft_entry__
+    __graft_entry__.build()
 
 
 @pytest.fixture(scope="session", autouse=True)

@@ -159,7 +159,7 @@ def _evict_log(fd):
     recs = (gf_ct_evict_rec * 4096)()
     n = lib.gf_ct_evict_log(fd, recs, 4096)
     assert n >= 0
-    return [(r.seq, r.now_sec, r.cut_closing, r.cut_other, r.evicted) for r in recs[:n]]
+    return [(r.seq, r.now_sec, r.age_cut, r.hand_line, r.lines, r.evicted) for r in recs[:n]]
 
 
 @pytest.mark.parametrize("seed,dt", [(4, 40), (6, 40), (5, 6000)])

@@ -111,7 +111,7 @@ def test_config5_real_shape_parity_with_eviction():
     assert set(np.unique(r["stage"])) >= {1, 4} and len(np.unique(r["ct_ret"][r["stage"] == 4])) >= 3
     recs = (gf_ct_evict_rec * 64)()
     nlog = lib.gf_ct_evict_log(dp.fd["cilium_ct6_global"], recs, 64)
-    glog = [(x.seq, x.now_sec, x.cut_closing, x.cut_other, x.evicted) for x in recs[:nlog]]
+    glog = [(x.seq, x.now_sec, x.age_cut, x.hand_line, x.lines, x.evicted) for x in recs[:nlog]]
     assert glog == ref.lru_log["cilium_ct6_global"] and len(glog) >= 1
     m = bpf.Map("ct6", 9, 40, 48, 10_485_760)
     m.fd = dp.fd["cilium_ct6_global"]

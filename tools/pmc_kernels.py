@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--bench-json", required=True, help="the bench line of one pass (steps, warmup, packets)")
     ap.add_argument("--packets", type=int, default=0, help="packets per step (default: from the bench line)")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--kernel-stats", default="", help="rocprofv3 --stats CSV of the same configuration: each "
+                    "kernel's average duration goes into the summary (bench.py's roofline.frac_rocprof)")
     a = ap.parse_args()
     b = json.loads(open(a.bench_json).read().strip().splitlines()[-1])
     nsteps = int(b["steps"]) + int(b["warmup"])
@@ -106,6 +108,17 @@ def main():
             e["wave_insts"] = c["SQ_INSTS_VALU"] + c.get("SQ_INSTS_SALU", 0.0)
             e["wave_insts_per_64_packets"] = e["wave_insts"] * 64 / pk if pk else None
         res["kernels"][k] = e
+    if a.kernel_stats:
+        res["kernel_stats_source"] = os.path.relpath(a.kernel_stats)
+        tot = collections.defaultdict(lambda: [0, 0.0])
+        for r in csv.DictReader(open(a.kernel_stats)):
+            k = short(r["Name"])
+            tot[k][0] += int(r["Calls"])
+            tot[k][1] += float(r["TotalDurationNs"])
+        for k, (n, t) in tot.items():
+            if k in res["kernels"] and n:
+                res["kernels"][k]["rocprof_calls"] = n
+                res["kernels"][k]["rocprof_avg_ns"] = round(t / n, 1)
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps({k: {x: y for x, y in v.items() if x != "counters_per_step"} for k, v in res["kernels"].items()},
                      indent=1))
