@@ -119,6 +119,8 @@ class Gpu:
         self.c = torch.zeros(512, dtype=torch.int64, device=self.dev)
         lib.gf_set_stats_sink(C.c_void_p(self.c.data_ptr()))
         lib.gf_prof_enable(1)
+        if hasattr(lib, "gf_diag_wrstats"):              # GF_WRSTATS diagnostic builds only
+            lib.gf_diag_wrstats((C.c_ulonglong * 16)(), 16)
 
     def end(self):
         """(counter block, {kernel: (launches, total_ms)}) of the timed region."""
@@ -127,6 +129,14 @@ class Gpu:
         recs = (gf_prof_rec * 32)()
         nrec = lib.gf_prof_read(recs, 32)
         lib.gf_prof_enable(0)
+        self.wr = None
+        if hasattr(lib, "gf_diag_wrstats"):
+            import ctypes as C
+            v = (C.c_ulonglong * 16)()
+            lib.gf_diag_wrstats(v, 16)
+            names = ["out", "hit_hot", "carry", "claim_cas", "slot_header", "slot_hot", "side_cold", "related_hot",
+                     "related_full", "related_new", "delete", "policy_counter_atomics", "related_log", "strict_count"]
+            self.wr = {n: int(v[k]) for k, n in enumerate(names)}
         return self.c, {recs[i].name.decode(): (recs[i].count, recs[i].total_ms) for i in range(nrec)}
 
     def evict_log(self, dp, name):
@@ -478,6 +488,7 @@ def bench_config2(args, B, rank, world, local_world=1):
         elapsed, c, lc, kern = timed(B, lambda a, b: dp.ingress_batches(batches[a:b], [now + s for s in range(a, b)],
                                                                          outs[a:b]), W, K, world, ranged=True)
     total_pkts = int(c[268])
+    wr = getattr(B, "wr", None)                          # GF_WRSTATS builds: writes by source, timed steps
     long_h = None
     if L > W + K:
         C_ = L - W - K
@@ -545,6 +556,7 @@ def bench_config2(args, B, rank, world, local_world=1):
         "verdicts": verdicts(c),
         "cpu_baseline": cpu,
         "parity": par,
+        **({"diag_writes_per_packet": {k: round(v / max(total_pkts, 1), 4) for k, v in wr.items()}} if wr else {}),
     }
 
 

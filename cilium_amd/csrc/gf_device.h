@@ -10,6 +10,26 @@
 
 namespace gfd {
 
+// Diagnostic build only (GF_WRSTATS=1, tools/variant.sh): every global write of
+// the handle_policy path counted by its source, one wave-aggregated add per write
+// site (gf_diag_wrstats reads them).  The product build compiles GF_WR away.
+#ifndef GF_WRSTATS
+#define GF_WRSTATS 0
+#endif
+enum { WR_OUT = 0, WR_HIT = 1, WR_CARRY = 2, WR_CAS = 3, WR_HDR = 4, WR_HOT = 5, WR_COLD = 6, WR_REL_HOT = 7,
+       WR_REL_FULL = 8, WR_REL_NEW = 9, WR_DEL = 10, WR_POLCNT = 11, WR_RLOG = 12, WR_STRICT = 13, WR_N = 16 };
+#if GF_WRSTATS
+__device__ unsigned long long g_wrstat[WR_N];
+__device__ __forceinline__ void wr_count(int k) {
+    const uint64_t m = __ballot(1);
+    if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)m) - 1u)
+        atomicAdd(&g_wrstat[k], (unsigned long long)__popcll(m));
+}
+#define GF_WR(k) wr_count(k)
+#else
+#define GF_WR(k) ((void)0)
+#endif
+
 // Table pointers reach the kernels inside descriptor structs (kernel arguments
 // passed by value, or loaded from the program table), where the compiler can no
 // longer see that they point to global memory and would emit flat_* accesses.
@@ -361,6 +381,7 @@ __device__ __forceinline__ void store_value(const gf_htab_desc &d, uint64_t i, c
     if (d.vin == 16 && VW > 4) {                        // hot-split: 4 words inline, the rest aside
         store_words<4>(d.slots + i * d.slot_size + d.voff, vw);
         store_words<VW - 4>(ht_side(d, i), vw + 4);
+        GF_WR(WR_HOT); GF_WR(WR_COLD);
         return;
     }
     store_words<VW>(d.vals + i * d.vsz, vw);            // full split
@@ -393,6 +414,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         return f;
     }
     if (strict) {
+        GF_WR(WR_STRICT);
         uint32_t old = gadd32(d.count, 1u);
         if (old >= d.max_entries) { gadd32(d.count, ~0u); return -7; }
     }
@@ -412,6 +434,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
             h[SW] = keep | ((uint32_t)GF_SLOT_FULL << (8 * SB));
 #pragma unroll
             for (int k = 0; k < NW; k += 4) gstore<uint4>(s + 4 * k, make_uint4(h[k], h[k + 1], h[k + 2], h[k + 3]));
+            GF_WR(WR_HDR);
         } else {
 #pragma unroll
             for (int k = 0; k < SW; k++) gstore<uint32_t>(s + 4 * k, kw[k]);
@@ -428,6 +451,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
     };
     if (hint >= 0 && claimable(hint_word)) {
         uint8_t *sw = d.slots + (uint64_t)hint * d.slot_size + 4 * SW;
+        GF_WR(WR_CAS);
         if (gcas(sw, hint_word, busy) == hint_word) { fill((uint64_t)hint); return hint; }
     }
     uint64_t i = gf_home_slot(h, d.mask, d.slot_size);
@@ -436,6 +460,7 @@ __device__ __forceinline__ int64_t ht_upsert(const gf_htab_desc &d, const uint32
         uint32_t cur = gload<uint32_t>(sw);            // a stale view only makes the CAS fail and retry
         for (;;) {
             if (!claimable(cur)) break;
+            GF_WR(WR_CAS);
             uint32_t seen = gcas(sw, cur, busy);
             if (seen == cur) { fill(i); return (int64_t)i; }
             cur = seen;
@@ -455,6 +480,7 @@ __device__ __forceinline__ void ht_delete(const gf_htab_desc &d, const uint32_t 
     uint32_t cur = gload<uint32_t>(sw);
     uint32_t nv = (cur & ~(0xffu << (8 * SB))) | ((uint32_t)GF_SLOT_TOMB << (8 * SB));
     gstore<uint32_t>(sw, nv);                          // the key is this lane's (group exclusivity)
+    GF_WR(WR_DEL);
     if (strict) gadd32(d.count, ~0u);
     else (*added)--;
 }

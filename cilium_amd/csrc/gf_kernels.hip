@@ -1002,8 +1002,8 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     if (acct) {                                         // rx_packets += 1, rx_bytes += len (exclusive lane)
         uint32_t pk = hot.z + 1u, by = hot.w + len;
         uint8_t *hi = d.sstride ? ht_side(d, (uint64_t)f) : e + 16;
-        if (pk == 0u) { gstore<uint32_t>(hi, gload<uint32_t>(hi) + 1u); st.carry = 1; }
-        if (by < hot.w) { gstore<uint32_t>(hi + 4, gload<uint32_t>(hi + 4) + 1u); st.carry = 1; }
+        if (pk == 0u) { gstore<uint32_t>(hi, gload<uint32_t>(hi) + 1u); st.carry = 1; GF_WR(WR_CARRY); }
+        if (by < hot.w) { gstore<uint32_t>(hi + 4, gload<uint32_t>(hi + 4) + 1u); st.carry = 1; GF_WR(WR_CARRY); }
         hot.z = pk; hot.w = by;
     }
     if (action == ACT_CREATE) {
@@ -1019,6 +1019,7 @@ __device__ __forceinline__ void ct_hit(const gf_htab_desc &d, int64_t f, uint4 h
     hot.x = life;
     hot.y = (hot.y & 0xffff0000u) | fl;
     gstore<uint4>(e, hot);
+    GF_WR(WR_HIT);
 }
 
 // ct_lookup4/6 (conntrack.h:310-437, dir = CT_INGRESS), resolve part: the home
@@ -1100,6 +1101,7 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     it[NHW] = (KSZ == 40 ? 58u : 1u) | ((tfl | 2u) << 8);
     v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
     if constexpr (KSZ == 14) if (rlog) {                // connection groups: applied after the run, in order
+        GF_WR(WR_RLOG);
         uint32_t *lg = rlog + (size_t)20 * wave_reserve(rlog_n);
         lg[0] = order;
 #pragma unroll
@@ -1112,13 +1114,17 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
 #pragma unroll
     for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
     if (same) {                                         // BPF_ANY over the entry this lane wrote
-        if (d.vin == 16 && rc.sec == src_sec)           // cold part (rx hi, tx, src_sec_id) unchanged
+        if (d.vin == 16 && rc.sec == src_sec) {         // cold part (rx hi, tx, src_sec_id) unchanged
             store_words<4>(d.slots + (uint64_t)rc.slot * d.slot_size + d.voff, v);
-        else
+            GF_WR(WR_REL_HOT);
+        } else {
             store_value<12>(d, (uint64_t)rc.slot, v);
+            GF_WR(WR_REL_FULL);
+        }
         rc.sec = src_sec;
         return 0;
     }
+    GF_WR(WR_REL_NEW);
     int64_t s = ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added);
     if (s < 0) return D_CT_CREATE_FAILED;
 #pragma unroll
@@ -1163,6 +1169,7 @@ struct PolAcc {
             uint8_t *c = side + (uint64_t)fj * GF_POL_SIDE;
             gadd64(c, (unsigned long long)pk[j]);
             gadd64(c + 8, (unsigned long long)by[j]);
+            GF_WR(WR_POLCNT); GF_WR(WR_POLCNT);
         }
         sl[j] = 0; pk[j] = 0; by[j] = 0;
     }
@@ -1728,6 +1735,7 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
         *reinterpret_cast<uint2 *>(q + 8) = b;
     } else if (!(GF_DIAG & 1)) {
         out[i] = o;
+        GF_WR(WR_OUT);
     }
     if (stats && !(GF_DIAG & 2)) {
 #if GF_ING_BINS_WAVE
@@ -3769,6 +3777,7 @@ __device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int 
     hot.x = life;
     hot.y = (hot.y & 0xffff0000u) | fl;
     gstore<uint4>(e, hot);
+    GF_WR(WR_HIT);
 }
 
 // policy_can_egress4 (policy.h:241-264 with POLICY_EGRESS, else :282-289):
@@ -5879,6 +5888,19 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
 
+#if GF_WRSTATS
+// Diagnostic builds only: the write-source counters (gf_device.h WR_*), read and cleared.
+int gf_diag_wrstats(unsigned long long *out, uint32_t n) {
+    if (hip_ok(hipDeviceSynchronize(), "wrstats sync")) return -EIO;
+    unsigned long long v[WR_N] = {0};
+    if (hip_ok(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_wrstat), sizeof v), "wrstats")) return -EIO;
+    const unsigned long long z[WR_N] = {0};
+    if (hip_ok(hipMemcpyToSymbol(HIP_SYMBOL(g_wrstat), z, sizeof z), "wrstats clear")) return -EIO;
+    for (uint32_t k = 0; k < n && k < WR_N; k++) out[k] = v[k];
+    return WR_N;
+}
+#endif
+
 int gf_ct_evict_log(int map, gf_ct_evict_rec *out, uint32_t max) {
     auto m = get_map(map);
     if (!m) return -EBADF;
@@ -6377,18 +6399,11 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             return -EIO;
     }
     if ((r = schedule_groups(n, s, nullptr, true))) return r;   // (reads only the front's keys: harmless on a flagged batch)
-    uint32_t hz = 0, hz_first = 0;
     host_mark("front+sched");
-    if (check) {
-        if (hip_ok(hipEventSynchronize(ew.ev_hz), "hz sync")) return -EIO;
-        host_mark("hzwait");
-        hz = ew.h_hz[0]; hz_first = ew.h_hz[2];
-    }
-    if (hz & 2u) {
-        if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
-        return egress_each(a, b, now_sec, out, snap_out, s, lru);
-    }
-    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru, hz_first, depth);
+    // k_eg_groups is queued before the host looks at the ordering check: it reads the
+    // check's flag itself and idles on a flagged batch (no map state changes then), so
+    // the device has the schedule and the groups to run while the host waits for the
+    // check's verdict and enqueues the rest of the call behind them
     {
         uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
@@ -6403,6 +6418,17 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
                            sink);
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
+    uint32_t hz = 0, hz_first = 0;
+    if (check) {
+        if (hip_ok(hipEventSynchronize(ew.ev_hz), "hz sync")) return -EIO;
+        host_mark("hzwait");
+        hz = ew.h_hz[0]; hz_first = ew.h_hz[2];
+    }
+    if (hz & 2u) {
+        if (getenv("GF_HZ_DEBUG")) fprintf(stderr, "[gf] egress n=%u: a CT map could fill, one packet at a time\n", n);
+        return egress_each(a, b, now_sec, out, snap_out, s, lru);
+    }
+    if (hz) return egress_ordered(a, b, now_sec, out, snap_out, s, lru, hz_first, depth);
     // ct_create4's deferred service entries, in batch order; every count from here
     // on is read on the device (no host round trip inside the call)
     if (check && sink) {

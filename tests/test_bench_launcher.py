@@ -61,6 +61,38 @@ def test_launcher_world_2_rehearsal():
     assert c4["parity"]["packets_compared"] == c4x["parity"]["packets_compared"]
 
 
+def test_launcher_world_8_rehearsal():
+    """The node the driver's scaling run uses: 8 ranks (gloo here, RCCL there), each
+    with its own flow groups and CT partition, parity on every rank, the counter
+    block all-reduced; config 4 owned and re-partitioned (all-to-all over 8 ranks)."""
+    parent, lines, err = _run(8, visible="0,1,2,3,4,5,6,7")
+    assert parent == {"rc": 0, "torch_imported": False}, err[-3000:]
+    r = lines[0]
+    assert r["n_gpus"] == 8 and r["value"] > 0
+    v = r["verdicts"]
+    assert v["pass"] + v["drop"] + v["redirect"] == 8 * r["config"]["packets_per_step_per_gpu"] * r["steps"]
+    p = r["parity"]
+    assert p["ranks"] == 8 and p["mismatches"] == 0 and p["ct_mismatches"] == 0 and p["ranks_with_mismatch"] == 0
+    for k in ("4", "4x"):
+        c = r["configs"][k]
+        assert c["n_gpus"] == 8 and c["parity"]["ranks"] == 8 and c["parity"]["mismatches"] == 0
+        assert c["parity"]["ct_mismatches"] == 0
+    assert r["configs"]["4"]["verdicts"] == r["configs"]["4x"]["verdicts"]
+
+
+def test_parity_div_fits_the_host():
+    """At N>1 each rank's parity sample is sized to its share of the host's cores."""
+    import types
+    sys.path.insert(0, ROOT)
+    import bench
+    a = types.SimpleNamespace(parity_div=0)
+    assert bench.parity_div(a, 1, 2, 10 ** 9) == 1                  # N=1: the whole stream
+    assert bench.parity_div(a, 8, 16, 201_326_592) == 2             # 16 threads a rank: the floor
+    d = bench.parity_div(a, 8, 2, 201_326_592)                      # a 16-core host shared by 8 ranks
+    assert d >= 5 and 201_326_592 / d / (2 * bench.ORACLE_MPPS_PER_THREAD * 1e6) <= bench.PARITY_LEG_S
+    assert bench.parity_div(types.SimpleNamespace(parity_div=3), 8, 2, 10 ** 9) == 3
+
+
 def test_launcher_single_rank_and_device_count():
     parent, lines, err = _run(1)
     assert parent["rc"] == 0 and lines[0]["n_gpus"] == 1 and lines[0]["parity"]["mismatches"] == 0, err[-3000:]
