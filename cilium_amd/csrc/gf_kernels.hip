@@ -770,6 +770,8 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
 struct IngCtx {
     const gf_lxc_dev *cfgs;
     const uint8_t *saddr6, *daddr6;
+    uint32_t a6_stride;      // bytes between two packets' v6 addresses: 16 (the caller's columns) or 32 (the
+                             // pipeline / egress deliveries: both addresses of a packet in one 32-B piece)
     gf_htab_desc ct4, ct6;   // cilium_ct4_global / cilium_ct6_global (shared by every program)
     uint32_t now, host_ifindex;
     uint32_t strict;   // bit0 / bit1: CT4 / CT6 inserts check max_entries with atomics
@@ -1503,8 +1505,8 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (!X.daddr6 || !X.saddr6) return D_INVALID;      // batch built without IPv6 columns
     const uint32_t flags = ep.flags;
     uint32_t nh = r.proto;
-    uint4 d = gload<uint4>(X.daddr6 + 16 * (size_t)i);
-    uint4 s = gload<uint4>(X.saddr6 + 16 * (size_t)i);
+    uint4 d = gload<uint4>(X.daddr6 + (size_t)X.a6_stride * i);
+    uint4 s = gload<uint4>(X.saddr6 + (size_t)X.a6_stride * i);
     uint32_t t[10] = {d.x, d.y, d.z, d.w, s.x, s.y, s.z, s.w, 0u, nh};
     uint32_t co = csum_l4_offset(nh);
     uint32_t rn_new = d.w & 0xffffu;                    // ip6->daddr.s6_addr32[3] & 0xFFFF
@@ -2263,9 +2265,9 @@ __global__ __launch_bounds__(NT, GF_FRONT_MINW) void k_pipe_front(gf_frames fr, 
             parse_row(w.p, cap, len, h2);
             key = pack_rec(i, h2.et, len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto, sec, ifx, slot_of[lxc & 0xffffu],
                            tci, false, true, h2.s6, h2.d6, rr);
-            if (h2.et == 0x86DD) {
-                reinterpret_cast<uint4 *>(s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
-                reinterpret_cast<uint4 *>(d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
+            if (h2.et == 0x86DD) {                       // both addresses in one 32-B piece (a6_stride 32)
+                reinterpret_cast<uint4 *>(s6out)[2 * (size_t)i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
+                reinterpret_cast<uint4 *>(d6out)[2 * (size_t)i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
             }
         } else {
             key = pack_rec(i, et, len, 0, 0, 0, 0, 0, 0, 0, 0, 0, tci, true, true, h.s6, h.d6, rr);
@@ -4314,8 +4316,8 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
                 key2[i] = kk;
                 rec2[i] = rr;
                 if constexpr (v6) {
-                    reinterpret_cast<uint4 *>(E.s6out)[i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
-                    reinterpret_cast<uint4 *>(E.d6out)[i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
+                    reinterpret_cast<uint4 *>(E.s6out)[2 * (size_t)i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
+                    reinterpret_cast<uint4 *>(E.d6out)[2 * (size_t)i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
                     atomicAdd(E.ctlog_n + 1, 1u);       // the ingress pass needs its IPv6 kernel
                 }
                 if (stats) { ls[2] += ab; if (ls[2] >= 0xf0000000u) fold(); }
@@ -5483,6 +5485,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     IngCtx X{};
     X.cfgs = (const gf_lxc_dev *)a->d_cfgs.p;
     X.saddr6 = pkts->saddr6; X.daddr6 = pkts->daddr6;
+    X.a6_stride = ta ? 32u : 16u;                       // the pipeline's / egress' interleaved addresses
     if (ct4m) X.ct4 = cfg_ct4;
     if (ct6m) X.ct6 = cfg_ct6;
     X.now = now_sec; X.host_ifindex = host_ifindex();
@@ -5744,7 +5747,7 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     const size_t lds = (size_t)nt * fr.snap_stride;
     PipeWs &w = pipe_ws();
     auto grow = [](DevBuf &d, size_t want) -> int { return d.bytes >= want ? 0 : d.ensure(want); };
-    if ((r = grow(w.s6, (size_t)n * 16)) || (r = grow(w.d6, (size_t)n * 16))) return r;
+    if ((r = grow(w.s6, (size_t)n * 32))) return r;    // saddr6 | daddr6 per packet (IngCtx::a6_stride 32)
     P.vec_copy = (fr.snap_stride % 16 == 0) && (((uintptr_t)fr.snap | (uintptr_t)snap_out) & 15u) == 0;
     PassArgs ta{};
     ta.kind = 1;
@@ -5757,15 +5760,15 @@ int gf_pipeline_classify(int pipe, const gf_pipe_batch *b, uint32_t now_sec, gf_
     const uint32_t grid = (n + nt - 1) / nt;         // one NT-frame tile per block
     gf_pkt_cols c2{};
     c2.n = n;
-    c2.saddr6 = (const uint8_t *)w.s6.p; c2.daddr6 = (const uint8_t *)w.d6.p;
+    c2.saddr6 = (const uint8_t *)w.s6.p; c2.daddr6 = (const uint8_t *)w.s6.p + 16;
     auto front = [&](const uint16_t *slot_of, gf_rec *rec, uint32_t *keys) -> int {
         ProfScope ps("k_pipe_front", s);
         if (nt == 256)
             hipLaunchKernelGGL(k_pipe_front<256>, dim3(grid), dim3(256), lds, s, fr, b->tc_index, b->flow_hash, P,
-                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.d6.p, out, nd6, snap_out, sink);
+                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.s6.p + 16, out, nd6, snap_out, sink);
         else
             hipLaunchKernelGGL(k_pipe_front<128>, dim3(grid), dim3(128), lds, s, fr, b->tc_index, b->flow_hash, P,
-                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.d6.p, out, nd6, snap_out, sink);
+                               slot_of, rec, keys, (uint8_t *)w.s6.p, (uint8_t *)w.s6.p + 16, out, nd6, snap_out, sink);
         return hip_ok(hipGetLastError(), "k_pipe_front");
     };
     c2.flow_hash = b->flow_hash;
@@ -6276,8 +6279,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     while (check && (uint64_t)amask + 1 < 8ull * n) amask = amask * 2 + 1;
     if ((r = grow(ew.erec, (size_t)n * sizeof(EgRec))) || (r = grow(ew.rec2, (size_t)n * sizeof(gf_rec))) ||
         (r = grow(ew.key2, (size_t)n * 4)) || (r = grow(ew.seq, 16)) || (r = grow(ew.ctlog_n, 8)) ||
-        (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 16)) ||
-        (r = grow(ew.d6, (size_t)n * 16)) || (r = grow(ew.hzst, 272 * 8)) || (r = ws_grow(n)))
+        (r = grow(ew.ctlog, (size_t)n * GF_CTLOG_WORDS * 4)) || (r = grow(ew.s6, (size_t)n * 32)) || (r = grow(ew.hzst, 272 * 8)) || (r = ws_grow(n)))
         return r;
     if (check && ((r = grow(ew.hzk, (size_t)n * 8 * GF_HZ_NK)) || (r = grow(ew.hzfl, (size_t)n)) ||
                   (r = grow(ew.hztk, (size_t)(hmask + 1) * 8)) || (r = grow(ew.hztf, (size_t)(hmask + 1) * 16)) ||
@@ -6304,7 +6306,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     E.ct4 = cfg_ct4; E.ct6 = cfg_ct6;
     if ((r = grow(ew.v6blk, (n + BLOCK - 1) / BLOCK))) return r;
     E.v6blk = GF_EG_LEAN ? (uint8_t *)ew.v6blk.p : nullptr;
-    E.s6out = (uint8_t *)ew.s6.p; E.d6out = (uint8_t *)ew.d6.p;
+    E.s6out = (uint8_t *)ew.s6.p; E.d6out = (uint8_t *)ew.s6.p + 16;   // interleaved (IngCtx::a6_stride 32)
     memcpy(E.router6, node.router_ip6, 16); memcpy(E.host6, node.host_ip6, 16);
     if (lxc) {
         E.lxc = lxc->hdesc();
@@ -6448,7 +6450,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     c2.n = n;
     c2.len = fr.len;
     c2.flow_hash = b->flow_hash;
-    c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.d6.p;   // IPv6 deliveries (if any)
+    c2.saddr6 = (const uint8_t *)ew.s6.p; c2.daddr6 = (const uint8_t *)ew.s6.p + 16;   // IPv6 deliveries (if any)
     // the deliveries' keys: their connections, or address pairs when the run fell back
     // k_eg_groups wrote them in batch order: they become the workspace's records and
     // keys by exchanging the buffers (the workspace's old ones are the next call's
