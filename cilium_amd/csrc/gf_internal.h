@@ -102,13 +102,16 @@ struct Map : Obj {
     DevBuf d_slots, d_vals, d_count;
     DevBuf d_lru, d_gcbits;     // CT maps: LRU stand-in state + eviction log, GC cluster-start bits
     uint32_t lru_seq = 0;       // classify calls that used this map (the eviction log's batch number)
-    // LRU CT maps: the count the last eviction chain left, written by the device to
-    // pinned host memory behind ev_count; cnt_add sums the increments of
-    // dev_count_hi (ct_limits), cnt_add_ev its value when ev_count was recorded
+    // LRU CT maps: the counts the last GF_EVRING eviction chains left, written by the
+    // device to pinned host memory, each behind its own event; cnt_add sums the
+    // increments of dev_count_hi (ct_limits), ev_add[k] its value when event k was
+    // recorded; ev_pending: the slots recorded since the bound was last set directly
+    static constexpr uint32_t GF_EVRING = 8;
     uint32_t *h_evcount = nullptr;
-    hipEvent_t ev_count = nullptr;
-    bool ev_pending = false;
-    uint64_t cnt_add = 0, cnt_add_ev = 0;
+    hipEvent_t ev_count[GF_EVRING] = {};
+    uint64_t ev_add[GF_EVRING] = {};
+    uint32_t ev_head = 0, ev_pending = 0;
+    uint64_t cnt_add = 0;
     // get_next_key over a device-authoritative map: a host copy of one chunk of
     // slot headers, and the slot of the key returned last (the dump loop's next
     // argument) so a walk is not needed to resume.

@@ -767,6 +767,9 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
 #define GF_LXC_DEV_HAS_CT4 (1u << 30)
 #define GF_LXC_DEV_HAS_CT6 (1u << 31)
 
+#ifndef GF_POUT_WO
+#define GF_POUT_WO 1        // gf_pipeline_classify: complete the records without reading them (IngCtx::pout_wo)
+#endif
 struct IngCtx {
     const gf_lxc_dev *cfgs;
     const uint8_t *saddr6, *daddr6;
@@ -776,6 +779,8 @@ struct IngCtx {
     uint32_t now, host_ifindex;
     uint32_t strict;   // bit0 / bit1: CT4 / CT6 inserts check max_entries with atomics
     uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
+    uint32_t pout_wo;  // gf_pipeline_classify: the record's first 10 bytes are written without reading them
+                       // (stage POLICY, the front's GF_PIPE_F_LB / _PORTMAP in gf_rec.cls bits 4-5)
     uint8_t *snap;     // pipeline: the frames as rewritten so far (handle_policy's writes land here)
     uint32_t snap_stride;
     uint32_t *plog, *plog_n;   // cilium_proxy{4,6} update log (16 words per redirect) and its length
@@ -977,13 +982,39 @@ struct Ep {
 // (conntrack.h:563-577) is the same key for the whole group: a lane keeps
 // where it lives.  Only this lane changes keys of its group; a delete by the
 // lane clears the cache.
+// IPv4 (GF_REL_DEFER): the lane also keeps the entry's last hot-part rewrite
+// pending instead of storing each one — the value of an ingress create's related
+// entry is fixed by now (per launch), the protocol's timeout and the packet's
+// length — in the spare high bits of the cached key's last word (bits 16-31: the
+// length, bit 15: TCP), and writes it once: before a packet that could read it (an
+// ICMP packet of the lane: only ct_lookup4's related probe matches the key),
+// before the cache moves to another entry and at the end of the launch.  A group
+// creating 4 flows a step then writes its related entry once instead of 4 times.
+#ifndef GF_REL_DEFER
+#define GF_REL_DEFER 1
+#endif
 template <int TW>
 struct RelCache {
     uint32_t k[TW];
     uint32_t slot;           // ~0u: none (tables of >= 2^32 slots are not cached)
     uint32_t sec;            // src_sec_id of the cold value part this lane wrote there
-    __device__ __forceinline__ void init() { slot = ~0u; sec = 0; }
+    __device__ __forceinline__ void init() { slot = ~0u; sec = 0; k[TW - 1] = 0; }
 };
+// The pending hot-part write of the IPv4 related entry (RelCache<4>::k[3] >> 15), if any.
+__device__ __forceinline__ void rel_flush4(const gf_htab_desc &d, RelCache<4> &rc, uint32_t now) {
+    const uint32_t p = rc.k[3] >> 15;
+    if (!p) return;
+    rc.k[3] &= 0x7fffu;
+    if (rc.slot == ~0u || !d.slots) return;
+    const uint32_t v[4] = {now + ((p & 1u) ? 300u : 43200u), F_SEEN_NON_SYN, 1u, p >> 1};
+    store_words<4>(d.slots + (uint64_t)rc.slot * d.slot_size + d.voff, v);
+    GF_WR(WR_REL_HOT);
+}
+template <int TW>
+__device__ __forceinline__ void rel_drop(const gf_htab_desc &d, RelCache<TW> &rc, uint32_t now) {
+    if constexpr (TW == 4) rel_flush4(d, rc, now);
+    rc.slot = ~0u;
+}
 
 // __ct_lookup, bpf/lib/conntrack.h:75-135 (dir = CT_INGRESS), hit part.  CT
 // values use the GF_VCODEC_CT layout: `hot` = the entry's first 16 B
@@ -1114,18 +1145,24 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     }
     bool same = rc.slot != ~0u;
 #pragma unroll
-    for (int k = 0; k < TW; k++) same &= (rc.k[k] == it[k]);
+    for (int k = 0; k < TW; k++) same &= ((k == TW - 1 ? rc.k[k] & 0x7fffu : rc.k[k]) == it[k]);
     if (same) {                                         // BPF_ANY over the entry this lane wrote
         if (d.vin == 16 && rc.sec == src_sec) {         // cold part (rx hi, tx, src_sec_id) unchanged
-            store_words<4>(d.slots + (uint64_t)rc.slot * d.slot_size + d.voff, v);
-            GF_WR(WR_REL_HOT);
+            if constexpr (TW == 4 && GF_REL_DEFER) {    // (rev_nat is 0 on the ingress path)
+                rc.k[3] = (rc.k[3] & 0x7fffu) | (((len << 1) | (nh == 6 ? 1u : 0u)) << 15);
+            } else {
+                store_words<4>(d.slots + (uint64_t)rc.slot * d.slot_size + d.voff, v);
+                GF_WR(WR_REL_HOT);
+            }
         } else {
+            if constexpr (TW == 4) rc.k[3] &= 0x7fffu;  // superseded
             store_value<12>(d, (uint64_t)rc.slot, v);
             GF_WR(WR_REL_FULL);
         }
         rc.sec = src_sec;
         return 0;
     }
+    if constexpr (TW == 4) rel_flush4(d, rc, now);      // the previous entry's pending write
     GF_WR(WR_REL_NEW);
     int64_t s = ht_upsert<KSZ, 12, GF_HASH_CT, U>(d, it, v, strict, added);
     if (s < 0) return D_CT_CREATE_FAILED;
@@ -1427,6 +1464,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     uint32_t nh = r.proto;
     uint32_t t[4] = {r.daddr, r.saddr, 0u, nh};
     uint32_t tfl = 0;                                   // TUPLE_F_OUT (ingress)
+    if (nh == 1) rel_flush4(X.ct4, rc, X.now);          // its related probe may read the pending entry
     int action; bool syn;
     int e = ct_l4(nh, false, r, t[2], tfl, action, syn);
     if (e < 0) return e;
@@ -1450,7 +1488,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     ProbeRes pr;
     int ret = ct_lookup<14, 4, GF_CT4_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
-    if (st.carry) rc.slot = ~0u;                         // a counter carry touched a cold value part
+    if (st.carry) rel_drop(X.ct4, rc, X.now);           // a counter carry touched a cold value part
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
         const gf_htab_desc rn = gload<gf_htab_desc>(&ep.cfg(X)->revnat4);
         uint32_t kw[1] = {st.rev_nat};
@@ -1471,7 +1509,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
         if (ret == CT_ESTABLISHED) {
             ab += 14;
             ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added);
-            rc.slot = ~0u;
+            rel_drop(X.ct4, rc, X.now);
         }
         return D_POLICY;
     }
@@ -1727,7 +1765,14 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab, rlog);
-    if (X.pout) {                                       // complete the pipeline record
+    if (X.pout && X.pout_wo) {                          // complete the pipeline record: stores only
+        uint8_t *q = X.pout + 24 * (size_t)i;
+        const uint32_t ff = ((r.cls & 16u) ? GF_PIPE_F_LB : 0u) | ((r.cls & 32u) ? GF_PIPE_F_PORTMAP : 0u);
+        *reinterpret_cast<uint32_t *>(q) = GF_STAGE_POLICY | ((uint32_t)o.action << 8) | ((uint32_t)o.reason << 16) |
+                                           ((uint32_t)o.ct_ret << 24);
+        *reinterpret_cast<uint32_t *>(q + 4) = (ff | o.flags) | ((uint32_t)o.proxy_port << 16);
+        *reinterpret_cast<uint16_t *>(q + 8) = o.ifindex_lo;
+    } else if (X.pout) {                                // complete the pipeline / egress record
         uint8_t *q = X.pout + 24 * (size_t)i;
         uint2 a = *reinterpret_cast<const uint2 *>(q), b = *reinterpret_cast<const uint2 *>(q + 8);
         a.x = (a.x & 0xffu) | ((uint32_t)o.action << 8) | ((uint32_t)o.reason << 16) | ((uint32_t)o.ct_ret << 24);
@@ -1840,7 +1885,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = ld_rec(rec, i);
-        ln.rc.slot = ~0u;                                // a new bucket: new flow groups
+        rel_drop(X.ct4, ln.rc, X.now);                   // a new bucket: new flow groups
 #if GF_PERM_VEC
         uint4 pw = make_uint4(0, 0, 0, 0);               // perm[j & ~3 .. +3], j = b + k + 2
         if (c > 2) pw = *reinterpret_cast<const uint4 *>(perm + ((b + 2) & ~3u));
@@ -1865,6 +1910,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
     }
     }
     ln.acc.flush(X);
+    rel_drop(X.ct4, ln.rc, X.now);                      // the pending related-entry write (IPv4)
     if (stats) ln.sc.fold(st);
     flush_added(X, F ? 2u : 1u, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
@@ -2265,6 +2311,8 @@ __global__ __launch_bounds__(NT, GF_FRONT_MINW) void k_pipe_front(gf_frames fr, 
             parse_row(w.p, cap, len, h2);
             key = pack_rec(i, h2.et, len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto, sec, ifx, slot_of[lxc & 0xffffu],
                            tci, false, true, h2.s6, h2.d6, rr);
+            // the front's record flags ride along for k_ing_groups' write-only completion (IngCtx::pout_wo)
+            rr.cls |= ((o.flags & GF_PIPE_F_LB) ? 16u : 0u) | ((o.flags & GF_PIPE_F_PORTMAP) ? 32u : 0u);
             if (h2.et == 0x86DD) {                       // both addresses in one 32-B piece (a6_stride 32)
                 reinterpret_cast<uint4 *>(s6out)[2 * (size_t)i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
                 reinterpret_cast<uint4 *>(d6out)[2 * (size_t)i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
@@ -5012,9 +5060,13 @@ __global__ __launch_bounds__(BLOCK) void k_run_count(uint32_t n, const uint32_t 
         tcnt[blockIdx.x] = t;
     }
 }
-__global__ __launch_bounds__(1024) void k_run_scan(uint32_t nt, uint32_t *tcnt, uint32_t *nruns) {
+// zero / nzero: words to clear on the way (the schedule's bucket histogram: one
+// launch fewer than a fill of its own)
+__global__ __launch_bounds__(1024) void k_run_scan(uint32_t nt, uint32_t *tcnt, uint32_t *nruns, uint32_t *zero = nullptr,
+                                                   uint32_t nzero = 0) {
     __shared__ uint32_t part[1024];
     __shared__ uint32_t carry;
+    for (uint32_t k = threadIdx.x; k < nzero; k += 1024) zero[k] = 0;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     for (uint32_t c0 = 0; c0 < nt; c0 += 1024) {         // exclusive scan in place, 1024 tiles at a time
@@ -5079,14 +5131,14 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
         ProfScope ps("bucket_runs", s);
         if (nt) hipLaunchKernelGGL(k_run_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
                                    (uint32_t *)w.tcnt.p);
-        hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.tcnt.p, d_nruns);
+        hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.tcnt.p, d_nruns,
+                           GF_SCHED_HIST(d_sched), GF_SCHED_HBYTES / 4u);   // (+ the bucket histogram cleared)
         if (nt) hipLaunchKernelGGL(k_run_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
                                    (const uint32_t *)w.tcnt.p, (uint32_t *)w.off.p);
         if ((r = hip_ok(hipGetLastError(), "run starts"))) return r;
     }
     {
         ProfScope ps("k_bucket_sched", s);
-        if (hip_ok(hipMemsetAsync(GF_SCHED_HIST(d_sched), 0, GF_SCHED_HBYTES, s), "memset hist")) return -EIO;
         static const bool lds_ok = [] {                  // the bins are > 64 KB of dynamic LDS
             return hipFuncSetAttribute((const void *)k_bucket_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)GF_SCHED_HBYTES) == hipSuccess &&
@@ -5116,8 +5168,10 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
                                (const uint32_t *)d_sched, (uint8_t *)w.sflag.p, (uint32_t *)w.sb.p);
             hipLaunchKernelGGL(k_single_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
                                (uint32_t *)w.st0.p, (uint32_t *)w.st1.p);
-            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st0.p, (uint32_t *)w.st0.p + nt);
-            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st1.p, (uint32_t *)w.st1.p + nt);
+            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st0.p, (uint32_t *)w.st0.p + nt,
+                               nullptr, 0u);
+            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st1.p, (uint32_t *)w.st1.p + nt,
+                               nullptr, 0u);
             hipLaunchKernelGGL(k_single_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
                                (const uint32_t *)w.sb.p, (const uint32_t *)w.st0.p, (const uint32_t *)w.st1.p,
                                (const uint32_t *)d_sched, (uint2 *)w.order.p);
@@ -5294,13 +5348,21 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
 }
 
 // The host's bound of a CT map's device count (ct_limits, lru_evict) tightened
-// from the count the last eviction chain wrote to pinned host memory, once the
-// event behind it has fired (a query, never a wait): that count plus what the
-// calls enqueued since may have added.
+// from the counts the recent eviction chains wrote to pinned host memory: the
+// newest one whose event has fired (a query, never a wait), plus what the calls
+// enqueued since may have added.  A ring of events, so a host that runs several
+// calls ahead of the device still finds a fired one.
 static void ct_count_refresh(Map &m) {
-    if (!m.ev_pending || !m.ev_count || hipEventQuery(m.ev_count) != hipSuccess) return;
-    m.ev_pending = false;
-    m.dev_count_hi = std::min<uint64_t>(m.dev_count_hi, (uint64_t)*m.h_evcount + (m.cnt_add - m.cnt_add_ev));
+    if (!m.ev_pending || !m.h_evcount) return;
+    for (uint32_t k = 1; k <= Map::GF_EVRING; k++) {
+        const uint32_t j = (m.ev_head + Map::GF_EVRING - k) % Map::GF_EVRING;
+        if (!(m.ev_pending & (1u << j))) continue;
+        if (hipEventQuery(m.ev_count[j]) != hipSuccess) continue;
+        m.dev_count_hi = std::min<uint64_t>(m.dev_count_hi, (uint64_t)m.h_evcount[j] + (m.cnt_add - m.ev_add[j]));
+        // this slot and every older one are used up
+        for (uint32_t q = k; q <= Map::GF_EVRING; q++) m.ev_pending &= ~(1u << ((m.ev_head + Map::GF_EVRING - q) % Map::GF_EVRING));
+        return;
+    }
 }
 // Element accounting mode of the CT maps for a batch of n packets inserting at
 // most per_pkt entries each (see ingress_run); fills the launch descriptors.
@@ -5315,7 +5377,7 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
         // call, the entries stay until the eviction pass after it (lru_evict), bounded by
         // the slot array (7/8 load = 3.5 x max_entries)
         const uint64_t limit = dev_insert_limit(*m);
-        if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = false; }
+        if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = 0; }
         ct_count_refresh(*m);
         // (no readback when the batch alone could exceed the limit: strict either way)
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && (uint64_t)per_pkt * n <= limit && !m->host_valid) {
@@ -5327,7 +5389,7 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
                 hip_ok(hipMemcpy(&dc, m->d_count.p, 4, hipMemcpyDeviceToHost), "read ct count"))
                 return -EIO;
             m->dev_count_hi = dc;
-            m->ev_pending = false;
+            m->ev_pending = 0;
         }
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit) strict |= m == ct4m ? 1u : 2u;
         m->dev_count_hi += (uint64_t)per_pkt * n;
@@ -5380,13 +5442,14 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     if (!kind) return -EIO;                              // the CT codec's layouts only
     if (!m->h_evcount) {
         void *p = nullptr;
-        if (hip_ok(hipHostMalloc(&p, 64, hipHostMallocMapped), "lru count word") ||
-            hip_ok(hipEventCreateWithFlags(&m->ev_count, hipEventDisableTiming), "lru count event"))
-            return -ENOMEM;
+        if (hip_ok(hipHostMalloc(&p, 4 * Map::GF_EVRING, hipHostMallocMapped | hipHostMallocCoherent), "lru count words")) return -ENOMEM;
         m->h_evcount = (uint32_t *)p;
+        for (auto &e : m->ev_count)
+            if (hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "lru count event")) return -ENOMEM;
     }
+    const uint32_t slot = m->ev_head;
     uint32_t *hc = nullptr;
-    if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount, 0), "lru count word")) return -EIO;
+    if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount + slot, 0), "lru count word")) return -EIO;
     const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size, nl = ns / spl;
     const uint64_t sl = nl <= 65536 ? nl : nl >> GF_LRU_SAMPLE_SHIFT;
     const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
@@ -5409,9 +5472,10 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
             hipLaunchKernelGGL(k_lru_round_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, round, hc);
         }
     }
-    if (hip_ok(hipEventRecord(m->ev_count, s), "lru count event")) return -EIO;
-    m->ev_pending = true;
-    m->cnt_add_ev = m->cnt_add;
+    if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
+    m->ev_pending |= 1u << slot;
+    m->ev_add[slot] = m->cnt_add;
+    m->ev_head = (slot + 1) % Map::GF_EVRING;
     static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
     if (stats) {
         LruDev h;
@@ -5491,6 +5555,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.now = now_sec; X.host_ifindex = host_ifindex();
     X.strict = strict;
     X.pout = pout;
+    X.pout_wo = GF_POUT_WO && pout && ta && ta->kind == 1 ? 1u : 0u;
     X.snap = wsnap; X.snap_stride = ev_stride;
     const gf_node_cfg &node = node_cfg();
     X.gw = node.ipv4_gateway;
@@ -5886,7 +5951,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     cnt = cnt >= r[0] ? cnt - (uint32_t)r[0] : 0u;
     if (hip_ok(hipMemcpy(m->d_count.p, &cnt, 4, hipMemcpyHostToDevice), "gc count")) return -EIO;
     m->dev_count_hi = cnt;
-    m->ev_pending = false;
+    m->ev_pending = 0;
     m->device_modified();
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
@@ -6064,7 +6129,7 @@ int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n
     m.host_valid = false;
     m.dev_gen++;
     m.dev_count_hi = before + n;
-    m.ev_pending = false;
+    m.ev_pending = 0;
     fallback = false;
     return 0;
 }
@@ -6226,6 +6291,19 @@ static int vip_sets(const std::vector<std::shared_ptr<ProgLxc>> &progs, EgWs &ew
     ew.vip_stamp = stamp;
     return 0;
 }
+// The per-call words of egress_call in one launch instead of four fills: the
+// sequence words (seq[1] the ordering check's flag, seq[3] its first hazard,
+// ~0 = none), both log counts and the front's scratch counter block.
+__global__ __launch_bounds__(256) void k_eg_init(uint32_t *seq, uint32_t *ctlog_n, uint32_t *rlog_n,
+                                                 unsigned long long *hzst) {
+    const uint32_t t = threadIdx.x;
+    if (t < 3) seq[t] = 0u;
+    if (t == 3) seq[3] = ~0u;
+    if (t < 2) ctlog_n[t] = 0u;
+    if (t < 2 && rlog_n) rlog_n[t] = 0u;
+    if (hzst)
+        for (uint32_t k = t; k < 272; k += 256) hzst[k] = 0ull;
+}
 // A log of deferred CT4 writes {order, key[4], value[12], pad[3]} applied in
 // order (k_ctlog_max / k_ctlog_apply: the last writer of a key wins).
 // nlog: an upper bound of the entry count (*d_n, read by the kernels): no host
@@ -6335,7 +6413,6 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
             (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4)))
             return r;
         d_rn = (uint32_t *)ew.rlog_n.p;
-        if (hip_ok(hipMemsetAsync(d_rn, 0, 8, s), "rlog count")) return -EIO;
         E.conn = 1; E.cflag = d_rn + 1;
         E.keysP = (uint32_t *)ew.keysP.p; E.key2P = (uint32_t *)ew.key2P.p;
         E.rlog = (uint32_t *)ew.rlog.p; E.rlog_n = d_rn;
@@ -6351,16 +6428,13 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     memcpy(E.X.host6, node.host_ip6, 16);
     if (ta.on) { E.X.tmark = (uint8_t *)trace_ws().mark.p; E.X.tcap = (uint8_t *)trace_ws().px.p; }
     if ((r = px_log_begin(n, s, E.X))) return r;
-    if (hip_ok(hipMemsetAsync(ew.seq.p, 0, 12, s), "eg seq") || hip_ok(hipMemsetAsync(d_hz + 2, 0xff, 4, s), "eg hz") || hip_ok(hipMemsetAsync(ew.ctlog_n.p, 0, 8, s), "eg ctlog"))
-        return -EIO;
     unsigned long long *sink = (unsigned long long *)stats_sink();
     // With the check, the front counts into a scratch block folded into the sink
     // only when the batch runs as it is (a flagged batch's runs count themselves).
     unsigned long long *fsink = sink;
-    if (check && sink) {
-        fsink = (unsigned long long *)ew.hzst.p;
-        if (hip_ok(hipMemsetAsync(fsink, 0, 272 * 8, s), "hz stats")) return -EIO;
-    }
+    if (check && sink) fsink = (unsigned long long *)ew.hzst.p;
+    hipLaunchKernelGGL(k_eg_init, dim3(1), dim3(256), 0, s, (uint32_t *)ew.seq.p, (uint32_t *)ew.ctlog_n.p, d_rn,
+                       fsink != sink ? fsink : nullptr);
     Workspace &w = ws();
     {
         ProfScope ps("k_eg_front", s);

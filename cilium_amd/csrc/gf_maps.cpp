@@ -214,7 +214,7 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
 }
 
 Map::~Map() {
-    if (ev_count) (void)hipEventDestroy(ev_count);
+    for (auto &e : ev_count) if (e) (void)hipEventDestroy(e);
     if (h_evcount) (void)hipHostFree(h_evcount);
 }
 
@@ -524,7 +524,7 @@ int Map::dev_count(uint32_t &c) {
 
 int Map::dev_set_count(uint32_t c) {
     dev_count_hi = c;
-    ev_pending = false;
+    ev_pending = 0;
     return dev_wr(*this, d_count.p, &c, 4);
 }
 
