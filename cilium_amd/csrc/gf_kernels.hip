@@ -2609,13 +2609,10 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
         gstore<uint4>(p, make_uint4(0u, 0u, 0u, st << 16));
     }
 }
-__global__ void k_lru_begin(const uint32_t *count, uint32_t max_entries, LruDev *L) {
-    const uint32_t c = *count;
-    const bool f = c > max_entries;
-    if (threadIdx.x == 0) L->flag = f ? 1u : 0u;
-    if (f)
-        for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_BINS; k += blockDim.x) L->hist[k] = 0;
-}
+// The chain after a classify call: k_lru_sample, k_lru_plan (round 0), k_lru_hand
+// x 2, k_lru_mid (round 0's count + round 1's plan), k_lru_hand x 2, k_lru_round_end.
+// Each launch exits at once unless the count exceeds max_entries.  The histogram
+// is zero between calls (cleared by k_lru_plan after its scan; zero at allocation).
 // Age histogram of the sample: wave-aggregated (a wave's entries mostly share a
 // bin), then counted per block in LDS and flushed with one global add per
 // non-zero bin.  The last GF_LRU_WIN seconds of each class are counted directly
@@ -2662,8 +2659,8 @@ __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line
 // end — wrapped positions below sl * SPL are the main loop's).
 template <int KIND>
 __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                          uint64_t sl) {
-    if (!L->flag) return;
+                                                          uint64_t sl, uint32_t max_entries) {
+    if (*d.count <= max_entries) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
@@ -2704,9 +2701,8 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
 }
 // Round `round` of a call: K and es from the sample (round 0), then the lines
 // the hand passes.  One block (128 bins per thread, then a block scan).
-__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
-                                                   uint64_t sl, uint32_t round) {
-    if (!L->flag) return;
+__device__ __forceinline__ void lru_plan_body(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
+                                              uint64_t sl, uint32_t round) {
     __shared__ unsigned long long part[1024];
     __shared__ uint32_t s_k;
     __shared__ unsigned long long s_es;
@@ -2733,6 +2729,7 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
             }
         }
         __syncthreads();
+        for (uint32_t k = 0; k < PER; k++) L->hist[t * PER + k] = 0;   // clear for the next call's sample
         if (t == 0) {
             L->K = s_k; L->es = s_es;
             L->target = (unsigned long long)(max_entries - max_entries / 8u);
@@ -2751,6 +2748,28 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         L->hand = (L->hand + lines) % nl;
         L->ev_lines += lines;
     }
+}
+__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
+                                                   uint64_t sl) {
+    const bool f = *count > max_entries;
+    if (threadIdx.x == 0) L->flag = f ? 1u : 0u;
+    if (!f) return;
+    lru_plan_body(count, max_entries, L, nl, sl, 0);
+}
+// Round 0's deletions off the count, then round 1's lines.
+__global__ __launch_bounds__(1024) void k_lru_mid(uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
+                                                  uint64_t sl) {
+    if (!L->flag) return;
+    __shared__ uint32_t s_c;
+    if (threadIdx.x == 0) {
+        const unsigned long long k = L->kills;
+        s_c = (uint32_t)(*count - k);
+        *count = s_c;
+        L->evicted += k;
+        L->kills = 0;
+    }
+    __syncthreads();
+    lru_plan_body(&s_c, max_entries, L, nl, sl, 1);
 }
 // The hand over this round's lines: the slots from the first line's first slot,
 // lines * SPL of them, in chunks of GF_LRU_CHUNK, plus the cluster running past
@@ -2864,6 +2883,7 @@ __global__ void k_lru_round_end(uint32_t *count, uint32_t seq, uint32_t now, Lru
         if (last && hcount) *hcount = *count;
         return;
     }
+    // (last == 0 is k_lru_mid's part now; kept for the chain's readers)
     const unsigned long long k = L->kills;
     *count = (uint32_t)(*count - k);
     L->evicted += k;
@@ -5352,8 +5372,15 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
 // newest one whose event has fired (a query, never a wait), plus what the calls
 // enqueued since may have added.  A ring of events, so a host that runs several
 // calls ahead of the device still finds a fired one.
-static void ct_count_refresh(Map &m) {
+// wait: block on the oldest pending event instead (the device only has to reach
+// that earlier call, not drain the queue) — ct_limits' alternative to a readback.
+static void ct_count_refresh(Map &m, bool wait = false) {
     if (!m.ev_pending || !m.h_evcount) return;
+    if (wait)
+        for (uint32_t k = Map::GF_EVRING; k >= 1; k--) {
+            const uint32_t j = (m.ev_head + Map::GF_EVRING - k) % Map::GF_EVRING;
+            if (m.ev_pending & (1u << j)) { (void)hipEventSynchronize(m.ev_count[j]); break; }
+        }
     for (uint32_t k = 1; k <= Map::GF_EVRING; k++) {
         const uint32_t j = (m.ev_head + Map::GF_EVRING - k) % Map::GF_EVRING;
         if (!(m.ev_pending & (1u << j))) continue;
@@ -5379,6 +5406,10 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
         const uint64_t limit = dev_insert_limit(*m);
         if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = 0; }
         ct_count_refresh(*m);
+        // near the limit: the count of an eviction chain a few calls back first (no
+        // queue drain), then, if that is not enough, a readback
+        if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && (uint64_t)per_pkt * n <= limit && !m->host_valid)
+            ct_count_refresh(*m, true);
         // (no readback when the batch alone could exceed the limit: strict either way)
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit && (uint64_t)per_pkt * n <= limit && !m->host_valid) {
             if (getenv("GF_SYNC_DEBUG"))
@@ -5457,20 +5488,25 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     const uint32_t *cnt = (const uint32_t *)d.count;
     {
         ProfScope ps("k_lru_evict", s);
-        hipLaunchKernelGGL(k_lru_begin, dim3(1), dim3(256), 0, s, cnt, m->max_entries, L);
-        if (kind == 1) hipLaunchKernelGGL(k_lru_sample<1>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl);
-        else hipLaunchKernelGGL(k_lru_sample<2>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl);
+        if (kind == 1)
+            hipLaunchKernelGGL(k_lru_sample<1>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, m->max_entries);
+        else
+            hipLaunchKernelGGL(k_lru_sample<2>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, m->max_entries);
+        hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, m->max_entries, L, nl, sl);
         for (uint32_t round = 0; round < 2; round++) {
-            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, m->max_entries, L, nl, sl, round);
+            // round 1 is rare (the count still above max_entries): a smaller grid, the same chunks
+            const dim3 g(round ? gh / 8 : gh);
             if (kind == 1) {
-                hipLaunchKernelGGL((k_lru_hand<1, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-                hipLaunchKernelGGL((k_lru_hand<1, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
             } else {
-                hipLaunchKernelGGL((k_lru_hand<2, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-                hipLaunchKernelGGL((k_lru_hand<2, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
+                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
             }
-            hipLaunchKernelGGL(k_lru_round_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, round, hc);
+            if (round == 0)
+                hipLaunchKernelGGL(k_lru_mid, dim3(1), dim3(1024), 0, s, d.count, m->max_entries, L, nl, sl);
         }
+        hipLaunchKernelGGL(k_lru_round_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, 1u, hc);
     }
     if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
     m->ev_pending |= 1u << slot;

@@ -17,6 +17,8 @@
 #                           from the flags it was built with (tools/_bin/libgpuflow_VAR.flags)
 #   prof:CFG                rocprofv3 --kernel-trace --stats, then three --pmc passes (one counter
 #                           group each) of bench configuration CFG       -> prof_CFG/
+#   trace:NAME[:ARGS]       rocprofv3 --kernel-trace --stats of bench.py ARGS, the trace kept
+#                           (tools/ktrace_gaps.py)                       -> trace_NAME/
 #   primbench:MODE          tools/_bin/primbench MODE                    -> primbench_MODE.txt
 #   env:K=V                 export K=V for the steps after it
 #
@@ -81,6 +83,11 @@ for S in "$@"; do
       echo "vbench $a1 $a2 ok" ;;
     prof)
       prof "$a1" ;;
+    trace)
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$a1" -o run -- \
+           python "$R/bench.py" $(args "$a2") > "$O/trace_$a1.json" 2> "$O/trace_$a1.err")
+      echo "trace $a1 ok" ;;
     primbench)
       timeout -k 10 180 "$R/tools/_bin/primbench" "$a1" > "$O/primbench_$a1.txt" 2>&1
       echo "primbench $a1 ok" ;;
