@@ -4448,10 +4448,15 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const u
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
+    // plain reads first: a slot's representative never changes once set and its
+    // highest order only grows, so a stale 0 costs the CAS it would have taken and a
+    // stale order only an atomic — a key's later entries mostly skip both atomics
     for (uint32_t p = key_hash<14, GF_HASH_CT>(e + 1) & tmask;; p = (p + 1) & tmask) {
-        const uint32_t rep = atomicCAS(&tab[p].x, 0u, j + 1u);
+        uint32_t rep = tab[p].x;
+        if (rep == 0u) rep = atomicCAS(&tab[p].x, 0u, j + 1u);
         if (rep == 0u || ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (rep - 1u), e)) {
-            atomicMax(&tab[p].y, e[0] + 1u);
+            const uint32_t want = e[0] + 1u;
+            if (rep == 0u || tab[p].y < want) atomicMax(&tab[p].y, want);
             return;
         }
     }

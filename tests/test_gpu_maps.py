@@ -203,6 +203,32 @@ def test_lru_many_sweeps_match_oracle(seed):
     assert len(ref.lru_log["ct4"]) >= 4
 
 
+def test_lru_hand_wraps_and_reuses_free_slots():
+    """Many evicting batches over small LRU CT maps: the hand passes the whole ring of
+    home lines several times, the slots it frees are claimed again by later inserts
+    (FREE), and tombstones of ct_delete are cleared on its way.  After every batch the
+    verdicts and the count, and at the end both tables and both eviction logs, equal
+    the oracle's restatement of the rule."""
+    sc = synth.fuzz(seed=33, n_packets=24000, n_batches=16, ct_max=600, ct6_max=200)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        now = sc.now + 20 * bi
+        io = dp.ingress(DeviceBatch(pk), now)
+        torch.cuda.synchronize()
+        _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, now), f"ingress b{bi}")
+        for name in ("ct4", "ct6"):
+            assert bpf.GetMapInfo(dp.fd[name]).Entries == ref.m[name].count(), (bi, name)
+    for name, ksz in (("ct4", 14), ("ct6", 40)):
+        assert dp.dump_map(name) == ref.dump(name), name
+        log = _evict_log(dp.fd[name])
+        assert log == ref.lru_log[name], name
+        ns = 64
+        while ns < 4 * (600 if name == "ct4" else 200):
+            ns *= 2
+        nl = ns // (4 if ksz == 14 else 2)
+        assert len(log) >= 6 and sum(e[4] for e in log) > 2 * nl, (name, len(log), sum(e[4] for e in log), nl)
+
+
 def test_concurrent_classify_two_streams():
     """Two host threads, each running its own programs (a cilium_policy array with
     its own CT, policy, CIDR and LB maps, its own prefilter) on its own HIP stream,
