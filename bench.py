@@ -311,13 +311,15 @@ def timed(B, run_step, W, K, world=1, ranged=False):
     return float(tt.item()), counters.cpu().numpy(), local.cpu().numpy(), kern
 
 
-def roofline(kern, names, ab_per_step, label):
-    """achieved = algorithmic bytes per step / the summed average launch time of
-    `names` (HIP events on the launch stream)."""
+def roofline(kern, names, ab_per_step, label, steps):
+    """achieved = algorithmic bytes per step / the device time per step of `names`
+    (HIP events on the launch stream around each launch scope, summed over the
+    timed steps and divided by their number: a scope launched twice per step
+    counts twice)."""
     ms = 0.0
     for n in names:
         c, t = kern.get(n, (0, 0.0))
-        ms += t / max(c, 1)
+        ms += t / max(steps, 1)
     ach = ab_per_step / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "kernel": label, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": ab_per_step,
@@ -330,8 +332,10 @@ def verdicts(c):
             "drop_reasons": {str(r): int(c[r]) for r in range(1, 256) if c[r]}, "wire_bytes": int(c[269])}
 
 
-def kms(kern):
-    return {k: round(v[1] / max(v[0], 1), 4) for k, v in kern.items()}
+def kms(kern, steps):
+    """Device time per step of each launch scope (its launches' summed HIP-event time
+    over the timed steps)."""
+    return {k: round(v[1] / max(steps, 1), 4) for k, v in kern.items()}
 
 
 def cpu_loop(fn, seconds):
@@ -498,7 +502,7 @@ def bench_config2(args, B, rank, world, local_world=1):
         long_h = {"steps": K + C_, "after_warmup": W, "mpps": round(lp / (elapsed + el2) / 1e6, 3),
                   "ms_per_step": round((elapsed + el2) / (K + C_) * 1e3, 4),
                   "continuation": {"steps": C_, "mpps": round(int(c2[268]) / el2 / 1e6, 3),
-                                   "kernels_ms_per_step": kms(kern2)}}
+                                   "kernels_ms_per_step": kms(kern2, C_)}}
         log(f"long horizon: {long_h['mpps']} Mpps over {K + C_} steps (continuation {long_h['continuation']['mpps']})")
     local_pkts = sum(batches[s].n for s in range(W, W + K))
     if not os.environ.get("GPUFLOW_DIAG_LIB"):
@@ -552,7 +556,7 @@ def bench_config2(args, B, rank, world, local_world=1):
             "algorithmic_bytes_per_launch": ab_per_launch,
             "avg_launch_ms": round(avg_ms, 4),
         },
-        "kernels_ms_per_step": kms(kern),
+        "kernels_ms_per_step": kms(kern, K),
         "verdicts": verdicts(c),
         "cpu_baseline": cpu,
         "parity": par,
@@ -717,7 +721,7 @@ def bench_config1(args, B):
     return {"workload": "config1: bpf_xdp CIDR prefilter (10k LPM prefixes + 2k /32, 1025 endpoints), 1M packets/step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
-            "roofline": roofline(kern, ["k_xdp"], float(c[270]) / K, "k_xdp"), "kernels_ms_per_step": kms(kern),
+            "roofline": roofline(kern, ["k_xdp"], float(c[270]) / K, "k_xdp", K), "kernels_ms_per_step": kms(kern, K),
             "verdicts": {"pass": int(c[258]), "drop": int(c[257])},
             "cpu_baseline": cpu, "parity": par}
 
@@ -764,7 +768,7 @@ def bench_config3(args, B):
                         "16M packets/step (Zipf 1.1)",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
-            "roofline": roofline(kern, ["k_lb"], float(c[270]) / K, "k_lb"), "kernels_ms_per_step": kms(kern),
+            "roofline": roofline(kern, ["k_lb"], float(c[270]) / K, "k_lb", K), "kernels_ms_per_step": kms(kern, K),
             "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
@@ -870,8 +874,8 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
          "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
          "packets_per_step": int(c[268]) // K, "warmup": W, "n_gpus": world,
          "roofline": roofline(kern, [k for k in names if k != "k_partition"], float(lc[270]) / K,
-                              "all pipeline kernels (frames -> verdicts), this rank"),
-         "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+                              "all pipeline kernels (frames -> verdicts), this rank", K),
+         "kernels_ms_per_step": kms(kern, K), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
     if world == 1 and not B.rehearsal and not args.no_h2d:
         r["h2d"] = config4_h2d(args, B, sc, fbs, [g[2] for g in got], W, K)
     return r
@@ -1045,8 +1049,8 @@ def bench_config5(args, B):
             "packets_per_step": int(c[268]) // K, "warmup": W,
             "ct6_entries_at_end": ct6_end,
             "ct6_evictions": evictions,
-            "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)"),
-            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+            "roofline": roofline(kern, names, float(c[270]) / K, "all pipeline kernels (frames -> verdicts)", K),
+            "kernels_ms_per_step": kms(kern, K), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
 # ----------------------------------------------------------------------------- endpoint egress
@@ -1089,8 +1093,8 @@ def bench_egress(args, B):
                         "VIPs), 1/4 new per step",
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
-            "roofline": roofline(kern, list(kern), float(c[270]) / K, "all egress kernels (frames -> verdicts)"),
-            "kernels_ms_per_step": kms(kern), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+            "roofline": roofline(kern, list(kern), float(c[270]) / K, "all egress kernels (frames -> verdicts)", K),
+            "kernels_ms_per_step": kms(kern, K), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
 def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
