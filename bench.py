@@ -332,6 +332,17 @@ def verdicts(c):
             "drop_reasons": {str(r): int(c[r]) for r in range(1, 256) if c[r]}, "wire_bytes": int(c[269])}
 
 
+def peak_rss_gb():
+    """This process's peak resident set (VmHWM), GB; None where /proc is absent."""
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith("VmHWM:"):
+                return int(line.split()[1]) * 1024 / 1e9
+    except OSError:
+        pass
+    return None
+
+
 def kms(kern, steps):
     """Device time per step of each launch scope (its launches' summed HIP-event time
     over the timed steps)."""
@@ -1402,7 +1413,12 @@ def main():
                "cpu_baseline": r["cpu_baseline"], "parity": r.get("parity")}
         if "h2d" in r:
             res["h2d"] = r["h2d"]
+    hwm = peak_rss_gb()
+    if hwm is not None:
+        log(f"rank {rank}: peak host memory {hwm:.1f} GB")
     if rank == 0:
+        if hwm is not None:
+            res["host_peak_rss_gb"] = round(hwm, 2)      # this rank's VmHWM (the N=8 host-memory budget)
         if rehearsal:
             res["data"] = "rehearsal (GPUFLOW_BENCH_SELFTEST): the oracle stood in for the device; not a measurement"
         else:
