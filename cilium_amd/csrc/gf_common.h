@@ -163,11 +163,18 @@ GF_HD void gf_pol_decode(const uint8_t *in, uint8_t *ext) {
     __builtin_memcpy(ext + 2, in + 18, 6);
 }
 #define GF_CT_VSZ 48u
-// CT maps (the datapath inserts into them) get a fixed slot array of
-// GF_CT_SLOT_FACTOR x max_entries slots (a 1/4-loaded table; HBM is plentiful).
-#ifndef GF_CT_SLOT_FACTOR
-#define GF_CT_SLOT_FACTOR 4
+// CT maps (the datapath inserts into them) get a fixed slot array of a power of two
+// >= factor x max_entries slots: 8 for ipv4_ct_tuple (a 1/8-loaded table: HBM is
+// plentiful, and the hit path's probes stay in the home line as the table fills —
+// DESIGN.md, round 5), 4 for ipv6_ct_tuple (64-B slots; the LRU hand walks twice
+// the lines at 8, and config 5 evicts on most calls).
+#ifndef GF_CT4_SLOT_FACTOR
+#define GF_CT4_SLOT_FACTOR 8
 #endif
+#ifndef GF_CT6_SLOT_FACTOR
+#define GF_CT6_SLOT_FACTOR 4
+#endif
+GF_HD uint32_t gf_ct_slot_factor(uint32_t ksz) { return ksz == 14 ? GF_CT4_SLOT_FACTOR : GF_CT6_SLOT_FACTOR; }
 GF_HD void gf_ct_encode(const uint8_t *ext, uint8_t *in) {
     const int map[12] = {8, 9, 0, 2, 1, 3, 4, 5, 6, 7, 10, 11};   // internal word k <- reference word map[k]
     uint32_t w[12];

@@ -1774,7 +1774,9 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
         *reinterpret_cast<uint16_t *>(q + 8) = o.ifindex_lo;
     } else if (X.pout) {                                // complete the pipeline / egress record
         uint8_t *q = X.pout + 24 * (size_t)i;
-        uint2 a = *reinterpret_cast<const uint2 *>(q), b = *reinterpret_cast<const uint2 *>(q + 8);
+        // (GF_DIAG & 128: ablation, the record's kept bytes not read — records wrong)
+        uint2 a = (GF_DIAG & 128) ? make_uint2(0u, 0u) : *reinterpret_cast<const uint2 *>(q);
+        uint2 b = (GF_DIAG & 128) ? make_uint2(0u, 0u) : *reinterpret_cast<const uint2 *>(q + 8);
         a.x = (a.x & 0xffu) | ((uint32_t)o.action << 8) | ((uint32_t)o.reason << 16) | ((uint32_t)o.ct_ret << 24);
         a.y = ((a.y & 0xffu) | o.flags) | (a.y & 0xff00u) | ((uint32_t)o.proxy_port << 16);
         b.x = (b.x & 0xffff0000u) | o.ifindex_lo;
@@ -3829,7 +3831,7 @@ __device__ __forceinline__ void ct_hit_eg(const gf_htab_desc &d, int64_t f, int 
     }
     st.rev_nat = hot.y >> 16;
     st.loopback = (fl >> 3) & 1u;
-    if (acct) {                                         // tx_packets += 1, tx_bytes += len
+    if (acct && !(GF_DIAG & 64)) {                      // tx_packets += 1, tx_bytes += len (GF_DIAG & 64: ablation)
         uint8_t *base = d.sstride ? ht_side(d, (uint64_t)f) - 16 : e;   // internal value word k at base + 4k
         gstore<unsigned long long>(base + 24, gload<unsigned long long>(base + 24) + 1ull);
         gstore<unsigned long long>(base + 32, gload<unsigned long long>(base + 32) + (unsigned long long)len);
@@ -4917,8 +4919,8 @@ int gf_lxc_prog_load(const gf_lxc_cfg *cfg) {
     MapLocks L;
     lock_lxc_maps(L, p);
     L.lock();
-    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
-    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(GF_CT_SLOT_FACTOR); }
+    if (p->ct4) { p->ct4->set_hash_mode(GF_HASH_CT); p->ct4->set_value_codec(GF_VCODEC_CT); p->ct4->make_fixed_capacity(gf_ct_slot_factor(p->ct4->ksz)); }
+    if (p->ct6) { p->ct6->set_hash_mode(GF_HASH_CT); p->ct6->set_value_codec(GF_VCODEC_CT); p->ct6->make_fixed_capacity(gf_ct_slot_factor(p->ct6->ksz)); }
     if (p->policy) { p->policy->set_hash_mode(GF_HASH_POLICY); p->policy->set_value_codec(GF_VCODEC_POL); }
     return new_handle(p);
 }

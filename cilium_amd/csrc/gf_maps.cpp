@@ -197,7 +197,7 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
     : Obj(ObjKind::Map), type(t), ksz(k), vsz(v), max_entries(m), flags(f),
       lpm(LpmKeyLess{k > 4 ? k - 4 : 0}) {
     if (!is_lpm()) {
-        // LRU maps: a fixed slot array of 4 x max_entries (the CT maps' factor), whose
+        // LRU maps: a fixed slot array of 4 x max_entries (CT-shaped ones take theirs below), whose
         // 7/8 load bounds inserts between two eviction sweeps (dev_insert_limit)
         if (type == GF_MAP_TYPE_LRU_HASH) { fixed_capacity = true; ht.init(k, v, 0); ht.nslots = pow2ceil64(std::max<uint64_t>(64, 4ull * m)); }
         else ht.init(k, v, 64);
@@ -206,7 +206,7 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
         // they are empty: it is invisible through the API (the codecs convert) and saves the
         // re-layout of a filled table when a program binds the map later.
         if ((k == 14 || k == 40) && v == GF_CT_VSZ) {
-            set_hash_mode(GF_HASH_CT); set_value_codec(GF_VCODEC_CT); make_fixed_capacity(GF_CT_SLOT_FACTOR);
+            set_hash_mode(GF_HASH_CT); set_value_codec(GF_VCODEC_CT); make_fixed_capacity(gf_ct_slot_factor(k));
         } else if (k == 8 && v == GF_POL_VSZ) {
             set_hash_mode(GF_HASH_POLICY); set_value_codec(GF_VCODEC_POL);
         }
@@ -266,13 +266,16 @@ void Map::set_hash_mode(uint32_t m) {
 
 
 // Maps the device inserts into (CT) get a slot array sized from max_entries
-// once, never rehashed by the device.  `factor` slots per entry: 4 for CT maps
-// (HBM is plentiful on MI355X; a 1/4-loaded table resolves almost every probe
-// in the home 64-B request).
+// once, never rehashed by the device.  `factor` slots per entry (gf_ct_slot_factor:
+// HBM is plentiful on MI355X; a lightly loaded table resolves almost every probe
+// in the home line).  A map already at that capacity is left alone:
+// binding a program to it must not pull the table into host memory (tens of GB
+// for the bench's CT) nor invalidate the device copy.
 void Map::make_fixed_capacity(uint32_t factor) {
     if (is_lpm()) return;
-    pull();
     uint64_t want = pow2ceil64(std::max<uint64_t>(64, (uint64_t)factor * max_entries));
+    if (fixed_capacity && want == ht.nslots) return;
+    pull();
     fixed_capacity = true;
     if (want != ht.nslots) ht.rehash(want);
     host_gen++;

@@ -488,8 +488,8 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream);
  * The kernel evicts from per-CPU LRU lists (the tail of an inactive list kept
  * about as long as the active one) in a nondeterministic order and never fails
  * an insert.  libgpuflow's deterministic stand-in: inside a batch an
- * LRU CT map may exceed max_entries (up to the 7/8 load of its slot array, 4 x
- * max_entries); at the end of every classify call that uses it, if the count
+ * LRU CT map may exceed max_entries (up to the 7/8 load of its slot array: a power
+ * of two >= 8 x max_entries for ipv4_ct_tuple, 4 x for ipv6_ct_tuple); at the end of every classify call that uses it, if the count
  * exceeds max_entries, a hand sweeping the table's home lines deletes the
  * entries of the older half (age key <= age_cut: the median age of a fixed
  * 1/64 sample of the lines — closing entries older than all others, then by

@@ -248,12 +248,18 @@ int om_lookup(om_map *m, const void *key, void *value_out) {
  * LRU_HASH: the kernel never fails an LRU insert (it evicts).  libgpuflow evicts
  * only the conntrack maps (ipv4/ipv6_ct_tuple -> ct_entry, the maps a classify
  * call binds, LRU stand-in above): those may exceed max_entries inside a batch, up
- * to the 7/8 load of their slot array (4 x max_entries rounded up to a power of
- * 2).  Any other LRU map has no eviction path there and stops at max_entries. */
+ * to the 7/8 load of their slot array (ct_slots: 8 x max_entries for ipv4_ct_tuple,
+ * 4 x for ipv6_ct_tuple, rounded up to a power of 2, gf_common.h
+ * gf_ct_slot_factor).  Any other LRU map has no eviction path there and stops at
+ * max_entries. */
+static uint64_t ct_slots(const om_map *m) {
+    uint64_t want = (m->ksz == 14 ? 8ull : 4ull) * m->max_entries, p = 64;
+    while (p < want) p <<= 1;
+    return p;
+}
 static uint32_t om_insert_limit(const om_map *m) {
     if (m->type != OM_LRU_HASH || !((m->ksz == 14 || m->ksz == 40) && m->vsz == 48)) return m->max_entries;
-    uint64_t want = 4ull * m->max_entries, p = 64;
-    while (p < want) p <<= 1;
+    uint64_t p = ct_slots(m);
     return (uint32_t)(p / 8 * 7 > 0xffffffffull ? 0xffffffffu : p / 8 * 7);
 }
 
@@ -1870,7 +1876,8 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
 /*    minus the timeout the entry's flags select (every lifetime writer */
 /*    sets it to now + that timeout, conntrack.h:47-62,127,527);        */
 /*  * home line: (CT hash of the key & (NS - 1)) / SPL, NS = the slot   */
-/*    array (pow2ceil(max(64, 4 x max_entries))), SPL = 128-B line /    */
+/*    array (ct_slots: pow2ceil(max(64, 8 or 4 x max_entries))), SPL  */
+/*    = 128-B line /                                                    */
 /*    slot (4 for ipv4_ct_tuple, 2 for ipv6_ct_tuple); NL = NS / SPL;   */
 /*  * sample = entries homed below SL = NL >> 6 (NL when NL <= 65536);  */
 /*    K = the smallest age key with at least half of the sample at or   */
@@ -1932,9 +1939,7 @@ static uint32_t gf_ct_hash(const uint8_t *key, uint32_t ksz) {
 typedef struct lru_geo { uint64_t ns, nl, sl; uint32_t spl; } lru_geo;
 static lru_geo lru_geometry(const om_map *m) {
     lru_geo g;
-    uint64_t want = 4ull * m->max_entries;
-    g.ns = 64;
-    while (g.ns < want) g.ns <<= 1;
+    g.ns = ct_slots(m);
     g.spl = m->ksz == 14 ? 4u : 2u;
     g.nl = g.ns / g.spl;
     g.sl = g.nl <= 65536 ? g.nl : g.nl >> 6;

@@ -225,7 +225,7 @@ def test_lru_hand_wraps_and_reuses_free_slots():
         log = _evict_log(dp.fd[name])
         assert log == ref.lru_log[name], name
         ns = 64
-        while ns < 4 * (600 if name == "ct4" else 400):
+        while ns < (8 * 600 if name == "ct4" else 4 * 400):      # gf_ct_slot_factor
             ns *= 2
         nl = ns // (4 if ksz == 14 else 2)
         assert len(log) >= 6 and sum(e[4] for e in log) > 2 * nl, (name, len(log), sum(e[4] for e in log), nl)

@@ -77,7 +77,7 @@ class Hand:
     def __init__(self, ksz, max_entries):
         self.ksz, self.max = ksz, max_entries
         self.ns = 64
-        while self.ns < 4 * max_entries:
+        while self.ns < (8 if ksz == 14 else 4) * max_entries:    # gf_ct_slot_factor
             self.ns *= 2
         self.spl = 4 if ksz == 14 else 2
         self.nl = self.ns // self.spl
@@ -138,7 +138,7 @@ def test_hand_matches_independent_restatement(ksz, max_entries, n0):
     keys, vals = _table(rng, ksz, n0, now)
     m.update_many(keys, vals)
     events = 0
-    for step in range(6):
+    for step in range(8):
         keep, rec = ref.evict(keys, vals, now)
         got = m.lru_evict(now)
         assert got == rec, (step, got, rec)

@@ -163,14 +163,15 @@ def test_errors_and_limits():
 def test_lru_insert_never_fails_below_slot_limit(ksz, vsz):
     """BPF_MAP_TYPE_LRU_HASH never fails an insert in the kernel (it evicts).  For
     the conntrack shapes (ipv4/ipv6_ct_tuple -> ct_entry) the stand-in accepts
-    inserts past max_entries up to 7/8 of its 4 x max_entries slot array and evicts
+    inserts past max_entries up to 7/8 of its slot array (8 x max_entries for
+    ipv4_ct_tuple, 4 x for ipv6_ct_tuple, rounded up to a power of 2) and evicts
     at the next classify call that binds the map as ct4 / ct6, so
     GetMapInfo may exceed max_entries in between.  Any other LRU map has no
     eviction path and stops at max_entries with E2BIG, like a HASH map.  The
     oracle's OMap has the same ceilings."""
     maxe = 100
     ct_shape = ksz in (14, 40) and vsz == 48
-    lim = 512 // 8 * 7 if ct_shape else maxe               # pow2ceil(4 * 100) = 512 slots
+    lim = (1024 if ksz == 14 else 512) // 8 * 7 if ct_shape else maxe   # pow2ceil(8 / 4 * 100) slots
     fd = bpf.CreateMap(bpf.BPF_MAP_TYPE_LRU_HASH, ksz, vsz, maxe)
     om = O.OMap(bpf.BPF_MAP_TYPE_LRU_HASH, ksz, vsz, maxe)
     rnd = random.Random(ksz)
