@@ -71,6 +71,12 @@ def main():
                 "config4_exchange_s": c4_leg and round(c4_leg * 1.1, 1), "config4_parity_div": div4}
         total = a.startup_s + (c2 + (2.1 * c4_leg if c4_leg else 0.0)) * a.contention
         out["projection"][f"T{T}"] = dict(legs, total_s=round(total, 1), within_390s=total <= 390)
+    rss = r.get("host_peak_rss_gb")
+    if rss:
+        # every rank holds what the N=1 run held at its peak, less the part of its oracle
+        # sample the larger parity divisor removes (not modelled: an upper bound)
+        out["host_memory"] = {"n1_peak_rss_gb": rss, "node_upper_bound_gb": round(8 * rss, 1),
+                              "note": "8 ranks x the N=1 peak; each rank's parity sample is smaller at N=8"}
     print(json.dumps(out, indent=1))
 
 
