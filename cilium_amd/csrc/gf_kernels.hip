@@ -2551,7 +2551,7 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 #define GF_LRU_LOGCAP 4096u
 #define GF_LRU_SAMPLE_SHIFT 6
 #define GF_LRU_HT 256u                  // k_lru_hand block
-#define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (4 per thread)
+#define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (CT6; CT4 twice that)
 struct LruLog { uint32_t seq, now, age_cut, pad; unsigned long long hand, lines, evicted; };
 struct LruDev {
     uint32_t hist[2 * GF_LRU_BINS];     // the sample's age histogram
@@ -2774,7 +2774,7 @@ __global__ __launch_bounds__(1024) void k_lru_mid(uint32_t *count, uint32_t max_
     lru_plan_body(&s_c, max_entries, L, nl, sl, 1);
 }
 // The hand over this round's lines: the slots from the first line's first slot,
-// lines * SPL of them, in chunks of GF_LRU_CHUNK, plus the cluster running past
+// lines * SPL of them, in chunks (GF_LRU_CHUNK slots, twice that for CT4), plus the cluster running past
 // the last one (entries homed in the range).  Launched twice, PAR = 0 for the
 // even chunks and 1 for the odd ones: a chunk's last slots turn EMPTY only if the
 // slots after it, up to the cluster's end, are all gone too, which the block
@@ -2790,13 +2790,15 @@ __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t
     const unsigned long long lines = L->lines;
     if (!lines) return;
     using S = LruSlot<KIND>;
-    constexpr uint32_t U = GF_LRU_CHUNK / GF_LRU_HT;
+    // slots a block decides together: 8 per thread for the 32-B CT4 slots, 4 for the
+    // 64-B CT6 slots (the same 64 KB of loads in flight per block)
+    constexpr uint32_t CH = KIND == 2 ? GF_LRU_CHUNK : 2 * GF_LRU_CHUNK, U = CH / GF_LRU_HT;
     const uint32_t K = L->K;
     const unsigned long long h0 = L->h0;
     const uint64_t ns = d.mask + 1, P0 = h0 * S::SPL, NP = lines * S::SPL;
     const bool whole = NP >= ns;
-    const uint64_t nch = (NP + GF_LRU_CHUNK - 1) / GF_LRU_CHUNK;
-    __shared__ uint8_t code[GF_LRU_CHUNK];
+    const uint64_t nch = (NP + CH - 1) / CH;
+    __shared__ uint8_t code[2 * GF_LRU_CHUNK];
     __shared__ uint32_t s_ef, s_kills, s_clr;
     auto code_of = [&](const S &s) -> uint32_t {
         if (s.st == GF_SLOT_EMPTY) return 0u;
@@ -2809,9 +2811,19 @@ __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t
     uint32_t kills = 0, clr = 0;
     const uint32_t lane = threadIdx.x & 63u;
     for (uint64_t c = 2 * (uint64_t)blockIdx.x + PAR; c < nch; c += 2 * (uint64_t)gridDim.x) {
-        const uint64_t base = c * GF_LRU_CHUNK;
-        const uint32_t cnt = (uint32_t)(NP - base < GF_LRU_CHUNK ? NP - base : GF_LRU_CHUNK);
+        const uint64_t base = c * CH;
+        const uint32_t cnt = (uint32_t)(NP - base < CH ? NP - base : CH);
+        const bool last = base + cnt == NP;
         uint32_t mine[U], ost[U];
+        // wave 0 also loads the first 64 slots after the chunk with the chunk's own
+        // loads (at low load they decide the chunk's trailing run): one round trip
+        // less per chunk.  Nothing writes them during this launch before wave 0 reads
+        // them below (the next chunk is the other launch's, and past the last chunk
+        // only this block writes, after reading).
+        S la;
+        const bool look = threadIdx.x < 64 && !(last && whole);
+        const uint64_t o0 = base + cnt + lane;
+        if (look && o0 < ns) la.load(d, (P0 + o0) & d.mask);
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             const uint32_t off = u * GF_LRU_HT + threadIdx.x;
@@ -2826,18 +2838,16 @@ __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t
         }
         __syncthreads();
         if (threadIdx.x < 64) {                          // wave 0: the slots after the chunk
-            const bool last = base + cnt == NP;
             bool ef = false, decided = false;
-            if (!(last && whole)) {
+            if (look) {
                 for (uint64_t q = 0;; q += 64) {
-                    if (!last && q >= GF_LRU_CHUNK) break;                 // undecided: the chunk's run stays FREE
+                    if (!last && q >= CH) break;                           // undecided: the chunk's run stays FREE
                     const uint64_t o = base + cnt + q + lane;              // offset from P0
                     uint32_t cd = 0;
                     if (o < ns) {                                          // never back into the range
-                        S s;
                         const uint64_t j = (P0 + o) & d.mask;
-                        s.load(d, j);
-                        cd = code_of(s);
+                        if (q) la.load(d, j);
+                        cd = code_of(la);
                         if (last && cd == 2) { lru_clear_slot<KIND>(d, j, GF_SLOT_FREE); kills++; }
                     }
                     const uint64_t stop_m = __ballot(cd <= 1u);
