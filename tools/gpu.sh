@@ -22,7 +22,7 @@
 #   primbench:MODE          tools/_bin/primbench MODE                    -> primbench_MODE.txt
 #   env:K=V                 export K=V for the steps after it
 #
-# Host side afterwards: tools/summarize.sh TAG ROUND (profiles/ROUND_* from the prof steps).
+# Host side afterwards: tools/summarize.sh TAG ROUND (profiles/ROUND_* from the prof steps' summaries).
 set -e
 T=$1; shift
 R=$(pwd)
@@ -60,6 +60,12 @@ prof() {
          python "$R/bench.py" $A > "$P/pmc/p$i.json" 2> "$P/pmc/p$i.err")
     echo "prof $C: pmc pass $i done"
   done
+  # the per-dispatch counter CSVs of six configurations exceed what a call may bring
+  # back (64 MiB): summarize here (tools/pmc_kernels.py, no GPU) and keep the summary
+  python "$R/tools/pmc_kernels.py" "$P/pmc" --bench-json "$P/pmc/p1.json" --kernel-stats "$P/ks/run_kernel_stats.csv" \
+      --out "$P/pmc_kernels.json" > "$P/pmc_kernels.txt"
+  find "$P/pmc" -name '*.csv' -delete
+  echo "prof $C: summarized"
 }
 
 for S in "$@"; do
