@@ -1206,8 +1206,10 @@ struct PolAcc {
             // (GF_DIAG & 32: the slot came from program 0's map; counted in the endpoint's own array)
             const uint32_t fj = (GF_DIAG & 32) ? f[j] & (uint32_t)gload<uint64_t>(&X.cfgs[sl[j] - 1].policy.mask) : f[j];
             uint8_t *c = side + (uint64_t)fj * GF_POL_SIDE;
-            gadd64(c, (unsigned long long)pk[j]);
-            gadd64(c + 8, (unsigned long long)by[j]);
+            if (!(GF_DIAG & 256)) {                      // (GF_DIAG & 256: ablation, no counter atomics)
+                gadd64(c, (unsigned long long)pk[j]);
+                gadd64(c + 8, (unsigned long long)by[j]);
+            }
             GF_WR(WR_POLCNT); GF_WR(WR_POLCNT);
         }
         sl[j] = 0; pk[j] = 0; by[j] = 0;
@@ -4434,12 +4436,13 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
 // The logged ct_create entries (service entries of the from-container pass,
 // related entries of connection groups), applied last-writer-wins per CT key:
 // k_ctlog_max enters every entry into a scratch open-addressing set keyed by the
-// logged tuple — a 16-B slot holds 1 + the index of the first entry seen for its
-// key (the key's representative) and, as one u64, (1 + the highest order entered
-// for the key) << 32 | that entry's index — and k_ctlog_apply walks the set's
-// slots and upserts each key's winning entry: one upsert per distinct key, the
-// entries read once more only as winners.  Log entry: [0] order, [1..4] the 14-B
-// key, [5..16] the 48-B value.
+// logged tuple.  A slot is one u64: (1 + the highest order entered for its key)
+// << 32 | that entry's index, 0 = empty; the key of a slot is its current entry's
+// (every entry ever held by a slot has the slot's key).  A key's first entry
+// claims a slot with one CAS, a later one raises it with atomicMax (the order in
+// the high half), so a key logged once — most of them — costs one atomic.
+// k_ctlog_apply walks the set's slots and upserts each key's winning entry.  Log
+// entry: [0] order, [1..4] the 14-B key, [5..16] the 48-B value.
 __device__ __forceinline__ bool ctlog_same(const uint32_t *a, const uint32_t *b) {
     return a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && (a[4] & 0xffffu) == (b[4] & 0xffffu);
 }
@@ -4452,38 +4455,40 @@ __global__ void k_ctlog_size(const uint32_t *n_, uint32_t cap_mask, uint32_t *tm
     while ((uint64_t)t + 1 < want && t < cap_mask) t = t * 2 + 1;
     *tm = t < cap_mask ? t : cap_mask;
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_clear(uint4 *tab, const uint32_t *tm) {
+__global__ __launch_bounds__(BLOCK) void k_ctlog_clear(unsigned long long *tab, const uint32_t *tm) {
     const uint64_t m = *tm;
     for (uint64_t k = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; k <= m; k += (uint64_t)gridDim.x * BLOCK)
-        tab[k] = make_uint4(0u, 0u, 0u, 0u);
+        tab[k] = 0ull;
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, uint4 *tab, const uint32_t *tm) {
+__global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, unsigned long long *tab,
+                                                     const uint32_t *tm) {
     const uint32_t n = *n_, tmask = *tm;
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
-    // plain reads first: a slot's representative never changes once set and its
-    // highest order only grows, so a stale 0 costs the CAS it would have taken and a
-    // stale order only an atomic — a key's later entries mostly skip both atomics
+    const unsigned long long want = ((unsigned long long)(e[0] + 1u) << 32) | j;
     for (uint32_t p = key_hash<14, GF_HASH_CT>(e + 1) & tmask;; p = (p + 1) & tmask) {
-        uint32_t rep = tab[p].x;
-        if (rep == 0u) rep = atomicCAS(&tab[p].x, 0u, j + 1u);
-        if (rep == 0u || ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (rep - 1u), e)) {
-            unsigned long long *mx = reinterpret_cast<unsigned long long *>(&tab[p].z);
-            const unsigned long long want = ((unsigned long long)(e[0] + 1u) << 32) | j;
-            if (rep == 0u || *mx < want) atomicMax(mx, want);
+        // plain read first: a stale 0 only makes the CAS fail, a stale value only
+        // costs the atomicMax it would have skipped
+        unsigned long long cur = tab[p];
+        if (cur == 0ull) {
+            cur = atomicCAS(&tab[p], 0ull, want);
+            if (cur == 0ull) return;                    // claimed for this key
+        }
+        if (ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (uint32_t)cur, e)) {
+            if (cur < want) atomicMax(&tab[p], want);
             return;
         }
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint4 *tab, const uint32_t *tm,
-                                                       gf_htab_desc ct, uint32_t *ct_count) {
+__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const unsigned long long *tab,
+                                                       const uint32_t *tm, gf_htab_desc ct, uint32_t *ct_count) {
     const uint32_t tmask = *tm;
     int added = 0;
     for (uint64_t p = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; p <= tmask; p += (uint64_t)gridDim.x * BLOCK) {
-        const uint4 t = tab[p];
-        if (t.x == 0u) continue;                        // an empty slot
-        const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * t.z;   // the key's last entry in order
+        const unsigned long long t = tab[p];
+        if (t == 0ull) continue;                        // an empty slot
+        const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * (uint32_t)t;   // the key's last entry in order
         ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
     }
     if (!ct_count || !__any(added != 0)) return;
@@ -6366,17 +6371,19 @@ static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32
     if (!nlog) return 0;
     uint32_t cap = 1023;                               // the set for the bound, at <= 1/2 load
     while ((uint64_t)cap + 1 < 2ull * nlog) cap = cap * 2 + 1;
-    const size_t tb = (size_t)(cap + 1) * 16;
+    const size_t tb = (size_t)(cap + 1) * 8;
     if (ew.ckey.bytes < tb && ew.ckey.ensure(tb)) return -ENOMEM;
     if (ew.ctm.bytes < 4 && ew.ctm.ensure(4)) return -ENOMEM;
     ProfScope ps("k_ctlog_apply", s);
     uint32_t *tm = (uint32_t *)ew.ctm.p;
     hipLaunchKernelGGL(k_ctlog_size, dim3(1), dim3(1), 0, s, d_n, cap, tm);
     const uint32_t gs = std::min<uint32_t>((cap + BLOCK) / BLOCK, 2048u);   // grid-stride over the set
-    hipLaunchKernelGGL(k_ctlog_clear, dim3(gs), dim3(BLOCK), 0, s, (uint4 *)ew.ckey.p, (const uint32_t *)tm);
+    hipLaunchKernelGGL(k_ctlog_clear, dim3(gs), dim3(BLOCK), 0, s, (unsigned long long *)ew.ckey.p, (const uint32_t *)tm);
     const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (uint4 *)ew.ckey.p, (const uint32_t *)tm);
-    hipLaunchKernelGGL(k_ctlog_apply, dim3(gs), dim3(BLOCK), 0, s, lg, (const uint4 *)ew.ckey.p, (const uint32_t *)tm, ct,
+    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p,
+                       (const uint32_t *)tm);
+    hipLaunchKernelGGL(k_ctlog_apply, dim3(gs), dim3(BLOCK), 0, s, lg, (const unsigned long long *)ew.ckey.p,
+                       (const uint32_t *)tm, ct,
                        ct_count);
     return hip_ok(hipGetLastError(), "k_ctlog_apply");
 }
