@@ -1193,6 +1193,38 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // consecutive packets that hit the same entry in registers and applies them
 // with one pair of atomics when the entry changes and at the end — the same
 // totals with a fraction of the memory-side atomics.
+// policy_entry packets += pk, bytes += by at c (two u64 atomics; agent-scope atomics
+// go to the memory side, ~17 G/s on MI355X).  GF_POL_WAVE: the active lanes that add
+// to the same entry as the first active lane sum their counts in registers first
+// and that lane adds once (a wave's local deliveries mostly meet few policy
+// entries); the other lanes add their own.  Counter sums commute: the final
+// values are the reference's.
+#ifndef GF_POL_WAVE
+#define GF_POL_WAVE 1
+#endif
+__device__ __forceinline__ void pol_count_add(uint8_t *c, uint32_t pk, uint32_t by) {
+#if GF_POL_WAVE
+    const uint64_t act = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63u, lead = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+    const uint64_t lc = (uint64_t)(uintptr_t)c;
+    const uint32_t clo = (uint32_t)__shfl((int)(uint32_t)lc, (int)lead);
+    const uint32_t chi = (uint32_t)__shfl((int)(uint32_t)(lc >> 32), (int)lead);
+    const bool same = (uint32_t)lc == clo && (uint32_t)(lc >> 32) == chi;
+    const uint64_t m = __ballot(same) & act;
+    if (same) {                                         // (only the lanes of m run this: sources active)
+        unsigned long long sp = 0, sb = 0;
+        for (uint64_t mm = m; mm; mm &= mm - 1ull) {
+            const int l = __ffsll((unsigned long long)mm) - 1;
+            sp += (uint32_t)__shfl((int)pk, l);
+            sb += (uint32_t)__shfl((int)by, l);
+        }
+        if (lane == lead) { gadd64(c, sp); gadd64(c + 8, sb); }
+        return;
+    }
+#endif
+    gadd64(c, (unsigned long long)pk);
+    gadd64(c + 8, (unsigned long long)by);
+}
 struct PolAcc {
     uint32_t f[2];                           // policy slots of the open sums
     uint16_t sl[2];                          // their program slot + 1 (0: sum not open)
@@ -1206,10 +1238,7 @@ struct PolAcc {
             // (GF_DIAG & 32: the slot came from program 0's map; counted in the endpoint's own array)
             const uint32_t fj = (GF_DIAG & 32) ? f[j] & (uint32_t)gload<uint64_t>(&X.cfgs[sl[j] - 1].policy.mask) : f[j];
             uint8_t *c = side + (uint64_t)fj * GF_POL_SIDE;
-            if (!(GF_DIAG & 256)) {                      // (GF_DIAG & 256: ablation, no counter atomics)
-                gadd64(c, (unsigned long long)pk[j]);
-                gadd64(c + 8, (unsigned long long)by[j]);
-            }
+            if (!(GF_DIAG & 256)) pol_count_add(c, pk[j], by[j]);   // (GF_DIAG & 256: ablation, no counter atomics)
             GF_WR(WR_POLCNT); GF_WR(WR_POLCNT);
         }
         sl[j] = 0; pk[j] = 0; by[j] = 0;
@@ -3903,8 +3932,7 @@ __device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, ui
     }
     if (f >= 0) {
         uint8_t *cnt = pd.vals + (uint64_t)f * GF_POL_SIDE;          // packets / bytes (policy.h:67-92)
-        gadd64(cnt, 1ull);
-        gadd64(cnt + 8, (unsigned long long)len);
+        pol_count_add(cnt, 1u, len);
         ab += 40;
         if (l4hit) {
             const uint32_t pp = gload<uint16_t>(ht_val(pd, (uint64_t)f));
