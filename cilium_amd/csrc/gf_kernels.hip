@@ -780,6 +780,7 @@ struct IngCtx {
     uint32_t strict;   // bit0 / bit1: CT4 / CT6 inserts check max_entries with atomics
     uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
     uint32_t pout_wo;  // gf_pipeline_classify: the record's first 10 bytes are written without reading them
+    uint32_t pol_wave; // policy counter adds summed per wave first (pol_count_add): the egress deliveries' pass
                        // (stage POLICY, the front's GF_PIPE_F_LB / _PORTMAP in gf_rec.cls bits 4-5)
     uint8_t *snap;     // pipeline: the frames as rewritten so far (handle_policy's writes land here)
     uint32_t snap_stride;
@@ -1194,16 +1195,20 @@ __device__ __forceinline__ int l4_proxy_lookup(const gf_lxc_dev *c, uint32_t nh,
 // with one pair of atomics when the entry changes and at the end — the same
 // totals with a fraction of the memory-side atomics.
 // policy_entry packets += pk, bytes += by at c (two u64 atomics; agent-scope atomics
-// go to the memory side, ~17 G/s on MI355X).  GF_POL_WAVE: the active lanes that add
-// to the same entry as the first active lane sum their counts in registers first
-// and that lane adds once (a wave's local deliveries mostly meet few policy
-// entries); the other lanes add their own.  Counter sums commute: the final
+// go to the memory side, ~17 G/s on MI355X).  wave (IngCtx::pol_wave): the active
+// lanes that add to the same entry as the first active lane sum their counts in
+// registers first and that lane adds once; the other lanes add their own.  It pays
+// on the egress deliveries' pass, whose lanes take neighbouring packets of few
+// endpoints (deliveries' k_ing_groups 0.662 -> 0.625 ms), and costs the ingress
+// configurations, whose lanes rarely share an entry (config 2 2.535 -> 2.565 ms,
+// config 4 1.902 -> 1.957: profiles/r5q_*.json).  Counter sums commute: the final
 // values are the reference's.
 #ifndef GF_POL_WAVE
 #define GF_POL_WAVE 1
 #endif
-__device__ __forceinline__ void pol_count_add(uint8_t *c, uint32_t pk, uint32_t by) {
+__device__ __forceinline__ void pol_count_add(uint8_t *c, uint32_t pk, uint32_t by, bool wave) {
 #if GF_POL_WAVE
+  if (wave) {
     const uint64_t act = __ballot(1);
     const uint32_t lane = threadIdx.x & 63u, lead = (uint32_t)__ffsll((unsigned long long)act) - 1u;
     const uint64_t lc = (uint64_t)(uintptr_t)c;
@@ -1221,6 +1226,7 @@ __device__ __forceinline__ void pol_count_add(uint8_t *c, uint32_t pk, uint32_t 
         if (lane == lead) { gadd64(c, sp); gadd64(c + 8, sb); }
         return;
     }
+  }
 #endif
     gadd64(c, (unsigned long long)pk);
     gadd64(c + 8, (unsigned long long)by);
@@ -1238,7 +1244,7 @@ struct PolAcc {
             // (GF_DIAG & 32: the slot came from program 0's map; counted in the endpoint's own array)
             const uint32_t fj = (GF_DIAG & 32) ? f[j] & (uint32_t)gload<uint64_t>(&X.cfgs[sl[j] - 1].policy.mask) : f[j];
             uint8_t *c = side + (uint64_t)fj * GF_POL_SIDE;
-            if (!(GF_DIAG & 256)) pol_count_add(c, pk[j], by[j]);   // (GF_DIAG & 256: ablation, no counter atomics)
+            if (!(GF_DIAG & 256)) pol_count_add(c, pk[j], by[j], X.pol_wave != 0);   // (GF_DIAG & 256: ablation)
             GF_WR(WR_POLCNT); GF_WR(WR_POLCNT);
         }
         sl[j] = 0; pk[j] = 0; by[j] = 0;
@@ -3932,7 +3938,7 @@ __device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, ui
     }
     if (f >= 0) {
         uint8_t *cnt = pd.vals + (uint64_t)f * GF_POL_SIDE;          // packets / bytes (policy.h:67-92)
-        pol_count_add(cnt, 1u, len);
+        pol_count_add(cnt, 1u, len, false);
         ab += 40;
         if (l4hit) {
             const uint32_t pp = gload<uint16_t>(ht_val(pd, (uint64_t)f));
@@ -5642,6 +5648,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.strict = strict;
     X.pout = pout;
     X.pout_wo = GF_POUT_WO && pout && ta && ta->kind == 1 ? 1u : 0u;
+    X.pol_wave = ta && ta->kind == 2 ? 1u : 0u;
     X.snap = wsnap; X.snap_stride = ev_stride;
     const gf_node_cfg &node = node_cfg();
     X.gw = node.ipv4_gateway;
