@@ -335,3 +335,29 @@ def test_prefilter_and_endpoint_edits_between_calls_on_two_streams():
         ro, _, rs = ref.pipeline(pk, sc.now + bi)
         _cmp(to_numpy(out, PIPE_OUT), ro, f"pipeline b{bi}")
         assert np.array_equal(snap.cpu().numpy(), rs), f"rewritten frames b{bi}"
+
+
+def _rss_gb():
+    for line in open("/proc/self/status"):
+        if line.startswith("VmRSS:"):
+            return int(line.split()[1]) * 1024 / 1e9
+    return 0.0
+
+
+def test_binding_a_large_ct_map_keeps_it_off_the_host():
+    """A CT map is sized once at creation (gf_ct_slot_factor x max_entries slots).
+    Binding programs to it and classifying must not build the host shadow of the
+    table (Map::make_fixed_capacity returns early when the capacity is in place): at
+    2^22 entries the CT4 array is 2^25 slots, 2 GB with its side array, which a pull
+    would copy into this process.  The GPU's answers still equal the oracle's."""
+    sc = synth.fuzz(seed=5, n_packets=4000, n_batches=2, ct_max=1 << 22, ct6_max=1 << 16)
+    before = _rss_gb()
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        now = sc.now + bi
+        io = dp.ingress(DeviceBatch(pk), now)
+        torch.cuda.synchronize()
+        _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, now), f"ingress b{bi}")
+    grown = _rss_gb() - before
+    assert grown < 1.0, f"host memory grew by {grown:.2f} GB"
+    assert bpf.GetMapInfo(dp.fd["ct4"]).Entries == ref.m["ct4"].count()
