@@ -56,13 +56,36 @@ struct LpmKeyLess {
 };
 
 // ---- exact-match hash table (host shadow, same layout as the device) ----
+// Host shadow storage: calloc'd (large blocks come from mmap as untouched zero
+// pages) and not value-initialised by the vector, so a table of gigabytes costs
+// host memory only in the pages an update or a pull writes.
+template <class T>
+struct ZeroAlloc {
+    using value_type = T;
+    ZeroAlloc() = default;
+    template <class U> ZeroAlloc(const ZeroAlloc<U> &) {}
+    T *allocate(size_t n) {
+        void *p = calloc(n, sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return (T *)p;
+    }
+    void deallocate(T *p, size_t) { free(p); }
+    template <class U> void construct(U *) noexcept {}            // calloc'd: already zero
+    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+    template <class U> bool operator==(const ZeroAlloc<U> &) const { return true; }
+    template <class U> bool operator!=(const ZeroAlloc<U> &) const { return false; }
+};
+using ZBytes = std::vector<uint8_t, ZeroAlloc<uint8_t>>;
+// n zero bytes in a fresh allocation (never the old one's contents)
+inline void zbytes_reset(ZBytes &v, size_t n) { ZBytes().swap(v); v.resize(n); }
+
 struct HTab {
     uint32_t ksz = 0, vsz = 0, slot_size = 0, voff = 0, split = 0, mode = GF_HASH_PLAIN;
     uint32_t codec = GF_VCODEC_IDENT;   // value layout in the slots (gf_common.h)
     uint32_t hot_split = 0;             // 1: hot-split layout (CT maps, gf_common.h)
     uint32_t vin = 0, sstride = 0;      // inline value bytes / side-array bytes per slot
     uint64_t nslots = 0;
-    std::vector<uint8_t> slots, vals;
+    ZBytes slots, vals;
     uint64_t count = 0, tombs = 0;
     void init(uint32_t k, uint32_t v, uint64_t n);
     uint32_t hash(const uint8_t *key) const;

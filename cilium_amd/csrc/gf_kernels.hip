@@ -3310,7 +3310,13 @@ struct EgDev {
 // The header bytes the IPv4 egress programs touch (< l4_off + 18 <= 92) are staged
 // per lane in LDS: one vector load per row instead of a global access per byte.
 #define GF_EG_STAGE 128u
-__device__ __forceinline__ uint32_t eg_stage_bytes(uint32_t S) { return S < GF_EG_STAGE ? S : GF_EG_STAGE; }
+GF_HD uint32_t eg_stage_bytes(uint32_t S) { return S < GF_EG_STAGE ? S : GF_EG_STAGE; }
+#ifndef GF_EG_GROUPS_DYN
+#define GF_EG_GROUPS_DYN 1  // k_eg_groups: LDS rows sized by the snap stride (0: GF_EG_STAGE-byte rows)
+#endif
+GF_HD uint32_t eg_row_bytes(uint32_t S) {           // k_eg_groups' LDS row
+    return GF_EG_GROUPS_DYN ? (eg_stage_bytes(S) + 15u) & ~15u : GF_EG_STAGE;
+}
 __device__ __forceinline__ void eg_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
     if (!(n & 15u) && !(((uintptr_t)src | (uintptr_t)dst) & 15u)) {
         for (uint32_t k = 0; k < n; k += 16) *reinterpret_cast<uint4 *>(dst + k) = *reinterpret_cast<const uint4 *>(src + k);
@@ -4360,7 +4366,10 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
     if (GF_EG_LEAN && !GF_SCHED_NFAM(sched)[FAM == 6 ? 1 : 0]) return;   // no bucket of this family (nothing to count)
     __shared__ uint32_t sl[272];
     __shared__ uint32_t sadd;
-    __shared__ uint4 lds[FAM == 6 ? 1 : BLOCK * (GF_EG_STAGE / 16)];
+    // FAM 4: one LDS row per lane of the staged header bytes, sized by the snap
+    // (eg_row_bytes: 64-B snaps take half the LDS of 128-B rows, so more blocks
+    // fit a CU — the LDS, not the registers, bounded the waves); FAM 6: unused
+    extern __shared__ uint4 lds[];
     __shared__ uint32_t lsum[3 * BLOCK];                // the lane's packets / wire bytes / algorithmic bytes
     Stats st{sl};
     uint32_t *ls = lsum + 3 * threadIdx.x;
@@ -4368,8 +4377,8 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
     auto fold = [&]() { st.add_n(268, ls[0]); st.add_n(269, ls[1]); st.add_n(270, ls[2]); ls[0] = ls[1] = ls[2] = 0; };
     if (threadIdx.x == 0) sadd = 0;
     if (stats) st.init(); else __syncthreads();
-    uint8_t *row = reinterpret_cast<uint8_t *>(lds + (FAM == 6 ? 0 : threadIdx.x * (GF_EG_STAGE / 16)));
     const uint32_t K = eg_stage_bytes(E.stride);
+    uint8_t *row = reinterpret_cast<uint8_t *>(lds) + (FAM == 6 ? 0 : threadIdx.x * eg_row_bytes(E.stride));
     constexpr int F = FAM == 6 ? 1 : 0;
     // the from-container pass schedules without records: every bucket is in class 0
     const uint32_t nb = GF_SCHED_LCNT(sched)[F * GF_NCLS], lane = threadIdx.x & 63u;
@@ -6579,11 +6588,11 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
         ProfScope ps("k_eg_groups", s);
-        hipLaunchKernelGGL(k_eg_groups<4>, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p,
+        hipLaunchKernelGGL(k_eg_groups<4>, dim3(grid), dim3(BLOCK), BLOCK * eg_row_bytes(S), s, E, (uint32_t *)w.sched.p,
                            (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
                            (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr,
                            sink);
-        hipLaunchKernelGGL(k_eg_groups<6>, dim3(grid), dim3(BLOCK), 0, s, E, (uint32_t *)w.sched.p,
+        hipLaunchKernelGGL(k_eg_groups<6>, dim3(grid), dim3(BLOCK), 16, s, E, (uint32_t *)w.sched.p,
                            (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
                            (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct6m ? (uint32_t *)ct6m->d_count.p : nullptr,
                            sink);

@@ -96,8 +96,8 @@ void HTab::init(uint32_t k, uint32_t v, uint64_t n) {
     ksz = k; vsz = v;
     relayout();
     nslots = n;
-    slots.assign(nslots * slot_size, 0);
-    if (sstride) vals.assign(nslots * sstride, 0); else vals.clear();
+    zbytes_reset(slots, nslots * slot_size);
+    if (sstride) zbytes_reset(vals, nslots * sstride); else ZBytes().swap(vals);
     count = 0; tombs = 0;
 }
 
@@ -221,8 +221,8 @@ Map::~Map() {
 // Fixed-capacity maps are materialized lazily: slots.size()==0 means all-empty.
 static void materialize(HTab &h) {
     if (h.slots.empty() && h.nslots) {
-        h.slots.assign(h.nslots * h.slot_size, 0);
-        if (h.sstride) h.vals.assign(h.nslots * h.sstride, 0);
+        zbytes_reset(h.slots, h.nslots * h.slot_size);
+        if (h.sstride) zbytes_reset(h.vals, h.nslots * h.sstride);
     }
 }
 
