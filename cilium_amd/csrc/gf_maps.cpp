@@ -586,6 +586,23 @@ static int dev_update(Map &m, const uint8_t *key, const uint8_t *value, uint64_t
     return m.dev_set_count(c + 1);
 }
 
+// A large table the datapath inserts into (fixed capacity, >= 64 MB of slots) that
+// holds nothing yet is written in HBM from its first element on: its replica is
+// created there (zeroed) and made authoritative, instead of building a host shadow
+// of the whole slot array for a few host writes.  Needs a GPU; without one the host
+// path is taken.
+static bool go_device(Map &m) {
+    if (m.dev_auth() || !m.fixed_capacity || m.is_lpm() || !m.ht.slots.empty() || m.ht.count != 0 || m.ht.tombs != 0)
+        return m.dev_auth();
+    if (m.ht.nslots * m.ht.slot_size < (64ull << 20)) return false;
+    int dc = 0;
+    if (hipGetDeviceCount(&dc) != hipSuccess || dc == 0) return false;
+    m.dev_valid = false;
+    if (m.push((hipStream_t)0)) return false;          // memset replica, count 0
+    m.host_valid = false;
+    return m.dev_auth();
+}
+
 int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
     host_gen++;
     if (fl > GF_EXIST) return -EINVAL;
@@ -608,7 +625,7 @@ int Map::update(const uint8_t *key, const uint8_t *value, uint64_t fl) {
         trie_dirty = true;
         return 0;
     }
-    if (dev_auth()) {
+    if (go_device(*this)) {
         bool fallback;
         int r = dev_update(*this, key, value, fl, fallback);
         if (!fallback) return r;
