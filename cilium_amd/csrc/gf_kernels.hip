@@ -78,6 +78,17 @@ __device__ __forceinline__ uint32_t gf_key_live(uint32_t k) { return (k & GF_KEY
 #define GF_EG_LEAN 1        // egress: the deferred-entry sets sized by the logged count, empty-family and no-IPv6 blocks skipped
 #endif
 #define GF_RUN_ITEMS 4096u  // keys per tile of the run-start / single-bucket count-scan-write passes
+// Buckets per lane per queue grab once a wave reaches the single-packet buckets
+// (the lists are longest first, so from there on every bucket is one packet): one
+// queue atomic per 64 x GF_GRAB_* buckets instead of per 64, and a lane runs several
+// independent packets back to back.  Longer buckets keep one per lane per grab (a
+// lane holding four long buckets would stretch the tail: config 2 4.8 vs 2.4 ms).
+#ifndef GF_GRAB_ING
+#define GF_GRAB_ING 4       // k_ing_groups
+#endif
+#ifndef GF_GRAB_EG
+#define GF_GRAB_EG 2        // k_eg_groups
+#endif
 #ifndef GF_SINGLE_ORDER
 #define GF_SINGLE_ORDER 1   // egress passes: single-packet buckets scheduled in packet-index order
 #endif
@@ -1887,7 +1898,10 @@ __device__ __forceinline__ uint32_t sched_list(uint32_t key, const gf_rec *rec, 
     return f * GF_NCLS + x;
 }
 
-template <int FAM>
+// GRAB: buckets per lane per queue grab in the single-packet tail (GF_GRAB_ING for the
+// egress deliveries' pass, whose buckets are mostly single packets; 1 elsewhere,
+// where the extra state costs the kernel registers it cannot spare)
+template <int FAM, int GRAB = 1>
 __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
                                                       const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
@@ -1912,14 +1926,33 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
     uint32_t *queue = GF_SCHED_QUEUE(sched) + L;
     const uint32_t nb = lcnt[L];
     const uint2 *lorder = order + lstart[L];
+    // the wave's grab: [base, base + 64 * left) of the list, one 64-bucket round at a
+    // time (wave-uniform values); grab = buckets per lane of the next grab
+    uint32_t grab = 1, gbase = 0, left = 0;
     for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(queue, 64u);
-        base = __shfl(base, 0);
-        if (base >= nb) break;
-        const uint32_t t = base + lane;
+        uint32_t t;
+        bool first = false;
+        if constexpr (GRAB == 1) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(queue, 64u);
+            base = __shfl(base, 0);
+            if (base >= nb) break;
+            t = base + lane;
+        } else {
+            if (!left) {
+                uint32_t b0 = 0;
+                if (lane == 0) b0 = atomicAdd(queue, 64u * grab);
+                gbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+                left = grab;
+            }
+            if (gbase >= nb) break;
+            t = gbase + lane;
+            first = left == grab;
+            gbase += 64u; left--;
+        }
         if (t >= nb) continue;
         const uint2 oc = lorder[t];
+        if (GRAB > 1 && first && (uint32_t)__builtin_amdgcn_readfirstlane((int)oc.y) == 1u) grab = GRAB;   // single-packet tail
         const uint32_t b = oc.x, c = oc.y;
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
@@ -4387,14 +4420,23 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
     const bool seq = *E.seq != 0;
     const bool rlog = FAM == 4 && E.conn && !seq && !*E.cflag;   // connection groups: related entries logged
     int added = 0;
+    // the wave's grab: [base, base + 64 * left) of the list, one 64-bucket round at a
+    // time (wave-uniform values); grab = buckets per lane of the next grab
+    uint32_t grab = 1, base = 0, left = 0;
     for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(queue, 64u);
-        base = __shfl(base, 0);
+        if (!left) {
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(queue, 64u * grab);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+            left = grab;
+        }
         if (base >= nb) break;
         const uint32_t tq = base + lane;
+        const bool first = left == grab;
+        base += 64u; left--;
         if (tq >= nb) continue;
         const uint2 oc = order[tq];
+        if (first && (uint32_t)__builtin_amdgcn_readfirstlane((int)oc.y) == 1u) grab = GF_GRAB_EG;   // single-packet tail
         for (uint32_t k = 0; k < oc.y; k++) {
             const uint32_t i = perm[oc.x + k];
             const EgRec r = erec[i];
@@ -5675,9 +5717,14 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         if (grid > need) grid = need;
         {
             ProfScope ps("k_ing_groups", s);
-            hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
-                               (const uint32_t *)w.perm.p,
-                               (const gf_rec *)w.rec.p, out, cnt4, sink);
+            if (X.pol_wave)                             // the egress deliveries' pass (single-packet buckets)
+                hipLaunchKernelGGL((k_ing_groups<4, GF_GRAB_ING>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
+                                   (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cnt4,
+                                   sink);
+            else
+                hipLaunchKernelGGL(k_ing_groups<4>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
+                                   (const uint32_t *)w.perm.p,
+                                   (const gf_rec *)w.rec.p, out, cnt4, sink);
         }
         if (pkts->saddr6) {    // IPv6 packets reach conntrack only with v6 columns
             ProfScope ps("k_ing_groups6", s);
