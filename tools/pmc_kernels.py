@@ -29,6 +29,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import os
 
 STEP_ENTRY = {"k_pipe_front", "k_eg_front", "k_ing_pack", "k_xdp", "k_xdp_lds", "k_lb", "k_parse"}
@@ -38,7 +39,11 @@ def short(name):
     s = name.split("(")[0].replace("void ", "").strip()
     if "rocprim" in s or "ROCPRIM" in name:
         return "rocprim"
-    return s.replace("<4>", "").replace("<6>", "6") if s.startswith("k_ing_groups") or s.startswith("k_eg_") else s
+    if s.startswith("k_ing_groups") or s.startswith("k_eg_"):
+        # the family template argument names the kernel (k_ing_groups / k_ing_groups6);
+        # a second one (k_ing_groups' queue grab) does not
+        s = re.sub(r"<([46])(, *\d+)?>", lambda m: "6" if m.group(1) == "6" else "", s)
+    return s
 
 
 def per_kernel(path, nsteps):
