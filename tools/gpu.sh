@@ -20,6 +20,7 @@
 #   trace:NAME[:ARGS]       rocprofv3 --kernel-trace --stats of bench.py ARGS, the trace kept
 #                           (tools/ktrace_gaps.py)                       -> trace_NAME/
 #   primbench:MODE          tools/_bin/primbench MODE                    -> primbench_MODE.txt
+#   pmc:CFG:C1,C2,..:NAME   one rocprofv3 --pmc pass (<= 8 SQ_, 4 TCC_ counters) of configuration CFG -> pmc_NAME/
 #   env:K=V                 export K=V for the steps after it
 #
 # Host side afterwards: tools/summarize.sh TAG ROUND (profiles/ROUND_* from the prof steps' summaries).
@@ -89,6 +90,17 @@ for S in "$@"; do
       echo "vbench $a1 $a2 ok" ;;
     prof)
       prof "$a1" ;;
+    pmc)
+      # one --pmc pass of bench configuration a1 with the counters a2 (comma-separated,
+      # at most 8 SQ_ / 4 TCC_ ...: one pass, no splitting) -> pmc_NAME/ (a3 = NAME)
+      P=$O/pmc_$a3; mkdir -p "$P"
+      A="--no-cpu --config $a1"; [ "$a1" = 2 ] && A="--no-cpu --no-extra --steps 4 --warmup 3 --long-steps 0"
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -s KILL 240 rocprofv3 --pmc $(args "$a2") --output-format csv -d "$P/p1" -o run -- \
+           python "$R/bench.py" $A > "$P/run.json" 2> "$P/run.err")
+      python "$R/tools/pmc_kernels.py" "$P" --bench-json "$P/run.json" --out "$P/summary.json" > "$P/summary.txt" || true
+      find "$P" -name '*counter_collection.csv' -size +20M -delete
+      echo "pmc $a3 ok" ;;
     trace)
       (cd /tmp && export TMPDIR=/tmp &&
        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$a1" -o run -- \
