@@ -254,10 +254,11 @@ class StandIn:
         from cilium_amd.synth import Packets
         pk = Packets(fb.frames.numpy(), fb.len.numpy().view(np.uint32),
                      tc_index=None if fb.tc_index is None else fb.tc_index.numpy())
-        r = self.ref.pipeline(pk, now)[0]
+        r, _, rs = self.ref.pipeline(pk, now)
         self._put(out, r)
         self.be.count(r, pk.lens)
-        return out, None, None
+        import torch
+        return out, None, torch.from_numpy(np.ascontiguousarray(rs)) if snap_out else None
 
     def egress(self, fb, now, out, snap_out=False):
         from cilium_amd.synth import Packets
@@ -304,11 +305,35 @@ def timed(B, run_step, W, K, world=1, ranged=False):
         dist.barrier()
     counters, kern = B.end()
     local = counters.clone()
+    B.local_elapsed = t1 - t0
     tt = torch.tensor([t1 - t0], dtype=torch.float64, device=B.dev)
+    B.allreduce_ms = None
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        B.sync()
+        a = time.perf_counter()
         dist.all_reduce(counters, op=dist.ReduceOp.SUM)        # RCCL over xGMI: verdict counter block
+        B.sync()
+        B.allreduce_ms = (time.perf_counter() - a) * 1e3
     return float(tt.item()), counters.cpu().numpy(), local.cpu().numpy(), kern
+
+
+def rank_diag(B, world, vals):
+    """Each rank's figures side by side (one all_gather): {name: [rank 0, ..]}
+    plus min / max, so an N>1 line shows which rank set the max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    names = list(vals)
+    t = torch.tensor([float(vals[k] if vals[k] is not None else float("nan")) for k in names], dtype=torch.float64,
+                     device=B.dev)
+    g = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(g, t)
+    rows = [x.cpu().tolist() for x in g]
+    out = {}
+    for i, k in enumerate(names):
+        col = [round(r[i], 4) for r in rows]
+        out[k] = {"per_rank": col, "min": min(col), "max": max(col)}
+    return out
 
 
 def roofline(kern, names, ab_per_step, label, steps):
@@ -322,8 +347,8 @@ def roofline(kern, names, ab_per_step, label, steps):
         ms += t / max(steps, 1)
     ach = ab_per_step / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "kernel": label, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": ab_per_step,
-            "avg_launch_ms": round(ms, 4)}
+            "frac": round(ach / HBM_PEAK_GBS, 4), "frac_source": "HIP events on the launch stream (this run)",
+            "traffic": None, "algorithmic_bytes_per_launch": ab_per_step, "avg_launch_ms": round(ms, 4)}
 
 
 def verdicts(c):
@@ -402,11 +427,14 @@ def reduce_parity(B, par, rank, world):
     t = torch.tensor([par["packets_compared"], par["mismatches"], par.get("ct_entries_compared", 0),
                       par.get("ct_mismatches", 0), 1 if par.get("first_mismatch") else 0], dtype=torch.int64,
                      device=B.dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    v = t.cpu().tolist()
+    g = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(g, t)
+    per = [x.cpu().tolist() for x in g]
+    v = [sum(p[i] for p in per) for i in range(5)]
     r = dict(par)
     r.update({"packets_compared": v[0], "mismatches": v[1], "ct_entries_compared": v[2], "ct_mismatches": v[3],
               "ranks": world, "ranks_with_mismatch": v[4],
+              "packets_compared_per_rank": [p[0] for p in per], "ct_entries_compared_per_rank": [p[2] for p in per],
               "sample": par["sample"] + f", on each of the {world} ranks (its own flow groups and CT partition)"})
     if "tables" in r:
         r["tables_rank0"] = r.pop("tables")
@@ -521,6 +549,11 @@ def bench_config2(args, B, rank, world, local_world=1):
     # roofline of the dominant kernel (k_ing_groups), this rank
     ki = kern.get("k_ing_groups", (0, 0.0))
     avg_ms = ki[1] / max(ki[0], 1)
+    ranks = None
+    if world > 1:
+        # which rank set the max-over-ranks time, and what the counter all-reduce cost
+        ranks = rank_diag(B, world, {"ms_per_step": B.local_elapsed / K * 1e3, "k_ing_groups_avg_ms": avg_ms,
+                                     "counter_allreduce_ms": B.allreduce_ms, "packets": int(lc[268])})
     ab_per_launch = float(lc[270]) / max(K, 1)
     achieved = ab_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     cpu = par = None
@@ -563,11 +596,13 @@ def bench_config2(args, B, rank, world, local_world=1):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac_source": "HIP events on the launch stream (this run)",
             "traffic": None,
             "algorithmic_bytes_per_launch": ab_per_launch,
             "avg_launch_ms": round(avg_ms, 4),
         },
         "kernels_ms_per_step": kms(kern, K),
+        **({"ranks": ranks} if ranks else {}),
         "verdicts": verdicts(c),
         "cpu_baseline": cpu,
         "parity": par,
@@ -821,7 +856,8 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
     import torch
     from cilium_amd import synth, stream
     from oracle import parity as PY
-    W, K = 4, max(4, args.steps // 2)
+    W = 4
+    K = max(4, args.c4_steps - W) if args.c4_steps else max(4, args.steps // 2)
     ct_max = min(args.ct_max, B.ct_max_cap or args.ct_max)
     kw = dict(B.tables_kw, n_svc=1000, n_lpm=500, n_fix=100) if B.rehearsal else {}
     sc, P, vip = synth.config4_tables(n_pairs=args.pairs * world, ct_max=ct_max, **kw)
@@ -831,8 +867,17 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
     dp = B.datapath(sc)
     exch = ingest == "exchange" and world > 1
-    # the pipeline oracle is ~2x the per-packet cost of ingress: half the sample
-    div = parity_div(args, world, cpu_threads(local_world), 2 * (W + K) * args.flows_per_step * 4) * 2
+    # N=1: the whole stream (every packet, the whole CT, the oracle's own eviction
+    # cutoffs); N>1: the pipeline oracle is ~2x the per-packet cost of ingress, half
+    # the per-rank sample
+    div = parity_div(args, world, cpu_threads(local_world), 2 * (W + K) * args.flows_per_step * 4)
+    if world > 1 and not args.parity_div:
+        div *= 2
+    # steps whose rewritten frames are fingerprinted on the device (snap_out) and
+    # compared with the oracle's: the warm-up steps (untimed) by default, every
+    # step with --c4-frames all (then the timed steps also write the snaps)
+    fp_steps = {"none": 0, "warmup": W, "all": W + K}[args.c4_frames] if not args.no_cpu else 0
+    fps = [None] * (W + K)
     sa, da = st.p_saddr.cpu().numpy(), st.p_daddr.cpu().numpy()
     pm = torch.from_numpy(PY.pair_sampled(sa, da, div).astype(np.uint8) |
                           (PY.pair_sampled(sa, da, div * 8).astype(np.uint8) << 1)).to(B.dev)
@@ -865,13 +910,21 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
         outs = [torch.empty((b.n, 24), dtype=torch.uint8, device=B.dev) for b in fbs]
 
         def step(s):
-            dp.pipeline(fbs[s], sc.now + s, out=outs[s], snap_out=False)
+            _, _, snap = dp.pipeline(fbs[s], sc.now + s, out=outs[s], snap_out=s < fp_steps)
+            if snap is not None:
+                fps[s] = PY.frame_fingerprints_torch(snap)
             got[s] = (fbs[s], samps[s], outs[s])
     el, c, lc, kern = timed(B, step, W, K, world)
     names = [k for k in kern]
+    ranks = None
+    if world > 1:
+        ki = kern.get("k_ing_groups", (0, 0.0))
+        ranks = rank_diag(B, world, {"ms_per_step": B.local_elapsed / K * 1e3,
+                                     "k_ing_groups_avg_ms": ki[1] / max(ki[0], 1),
+                                     "counter_allreduce_ms": B.allreduce_ms, "packets": int(lc[268])})
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, local_world=local_world)
+        cpu, par = oracle_config4(args, B, sc, dp, got, W, K, div, local_world=local_world, replay=div > 1, fps=fps)
         if world > 1:
             cpu = None
     par = reduce_parity(B, par, rank, world)
@@ -884,15 +937,19 @@ def bench_config4(args, B, rank=0, world=1, ingest="owned", local_world=1):
                    "frames arrive on the rank that owns their flow group (RSS by the owner hash)",
          "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
          "packets_per_step": int(c[268]) // K, "warmup": W, "n_gpus": world,
+         **({"note": "--c4-frames all: every timed step also writes and fingerprints its rewritten frames "
+                     "(a parity run, not the configuration's throughput)"} if fp_steps > W else {}),
          "roofline": roofline(kern, [k for k in names if k != "k_partition"], float(lc[270]) / K,
                               "all pipeline kernels (frames -> verdicts), this rank", K),
-         "kernels_ms_per_step": kms(kern, K), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
+         "kernels_ms_per_step": kms(kern, K), **({"ranks": ranks} if ranks else {}),
+         "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
     if world == 1 and not B.rehearsal and not args.no_h2d:
         r["h2d"] = config4_h2d(args, B, sc, fbs, [g[2] for g in got], W, K)
     return r
 
 
-def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global",), local_world=1, replay=True):
+def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global",), local_world=1, replay=True,
+                   fps=None):
     """The oracle pipeline over the flow-group sample of every step (the flow group
     is the post-LB address pair, i.e. the stream's pair), records and the sampled
     pairs' CT entries compared; timed steps give the CPU baseline.  got[s] = (the
@@ -900,13 +957,18 @@ def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global
     post-LB pair is in the 1/div sample, bit 1: in the 1/(8 div) single-core subsample.
     replay=False (div must be 1: the oracle holds the whole table): the oracle's LRU
     stand-in derives its own eviction cutoffs from its own table, and its eviction
-    log must equal the device's (gf_ct_evict_log) entry for entry."""
+    log must equal the device's (gf_ct_evict_log) entry for entry.  fps[s] (device
+    int64 tensor or None): the fingerprints of step s's rewritten frames
+    (oracle.parity.frame_fingerprints), compared with those of the oracle's frames."""
     import torch
     from cilium_amd.datapath import PIPE_OUT
     from cilium_amd.synth import Packets
     from oracle.scenario import OracleDP
+    from oracle import parity as PY
     T = cpu_threads(local_world)
     ref = OracleDP(sc, shards=T)
+    fr_n = fr_bad = 0
+    fr_first = None
     if replay:
         lru_replay(B, dp, ref)
     else:
@@ -926,21 +988,34 @@ def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global
             # 1/8 of the sampled groups (sample bit 1) on one core first (exact: groups are independent)
             m1 = (sbits[idx] & 2) != 0
             a = time.perf_counter()
-            r1 = ref.pipeline(_sub(pk, np.nonzero(m1)[0]), sc.now + s, threads=1, lru=False)[0]
+            o1 = ref.pipeline(_sub(pk, np.nonzero(m1)[0]), sc.now + s, threads=1, lru=False)
             single_t, single_n = time.perf_counter() - a, int(m1.sum())
             a = time.perf_counter()
-            r2 = ref.pipeline(_sub(pk, np.nonzero(~m1)[0]), sc.now + s, threads=T)[0]
+            o2 = ref.pipeline(_sub(pk, np.nonzero(~m1)[0]), sc.now + s, threads=T)
             tt += time.perf_counter() - a
             done += pk.n - single_n
-            r = np.empty(pk.n, r1.dtype)
-            r[m1], r[~m1] = r1, r2
+            r = np.empty(pk.n, o1[0].dtype)
+            r[m1], r[~m1] = o1[0], o2[0]
+            rs = np.empty((pk.n,) + o1[2].shape[1:], o1[2].dtype)
+            rs[m1], rs[~m1] = o1[2], o2[2]
         else:
             a = time.perf_counter()
-            r = ref.pipeline(pk, sc.now + s, threads=T)[0]
+            o = ref.pipeline(pk, sc.now + s, threads=T)
+            r, rs = o[0], o[2]
             if s >= W:
                 tt += time.perf_counter() - a
                 done += pk.n
         par.records(gout, r, f"step {s}")
+        if fps is not None and fps[s] is not None:
+            gf = fps[s][it].cpu().numpy().view(np.uint64)
+            bad = np.nonzero(gf != PY.frame_fingerprints(rs))[0]
+            fr_n += len(gf)
+            fr_bad += len(bad)
+            if len(bad) and fr_first is None:
+                fr_first = f"step {s} sampled row {int(bad[0])}"
+        if (s + 1) % 8 == 0:
+            log(f"config-4 parity: {s + 1} of {W + K} steps, {par.packets} packets, {par.bad} mismatches, "
+                f"{fr_n} frames, {fr_bad} frame mismatches")
     for name in ct_names:
         compare_ct(B, par, dp, ref, name, 14 if "4" in name else 40, div)
     cpu = cpu_base(done / tt / 1e6 if tt else 0.0, T,
@@ -948,6 +1023,12 @@ def oracle_config4(args, B, sc, dp, got, W, K, div, ct_names=("cilium_ct4_global
                    f"warm-up), {T} threads; single core: {single_n} packets of step {W}",
                    single_n / single_t / 1e6 if single_t else None)
     res = par.result(W + K)
+    if fr_n:
+        res["frames_compared"], res["frame_mismatches"] = int(fr_n), int(fr_bad)
+        res["frames"] = ("64-bit fingerprints of the rewritten frames (snap_out; oracle.parity.frame_fingerprints), "
+                         "device vs oracle, on the steps that wrote them")
+        if fr_first:
+            res["first_frame_mismatch"] = fr_first
     if not replay:
         for name in ct_names:
             dev_log = [tuple(int(x) for x in e) for e in B.evict_log(dp, name)]
@@ -1247,7 +1328,14 @@ def add_bounds(cfg, r):
         ab = rf.get("algorithmic_bytes_per_launch")
         if ab and ns and all(ns):
             ms_p = sum(k["rocprof_avg_ns"] * k.get("dispatches_per_step", 1.0) for k in ks) * 1e-6
-            rf["frac_rocprof"] = round(ab / (ms_p * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            # one frac per line: the profile's (the rocprofv3 --stats average this line
+            # cites), so frac = algorithmic_bytes_per_launch / rocprof_avg_launch_ms
+            # reproduces from profiles/; the live HIP-event figure stays beside it
+            rf["frac_hip_events"], rf["achieved_hip_events"] = rf["frac"], rf["achieved"]
+            rf["achieved"] = round(ab / (ms_p * 1e-3) / 1e9, 2)
+            rf["frac"] = rf["frac_rocprof"] = round(ab / (ms_p * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            rf["frac_source"] = ("algorithmic_bytes_per_launch / rocprof_avg_launch_ms (rocprofv3 --kernel-trace "
+                                 "--stats of this build: rocprof_source)")
             rf["rocprof_avg_launch_ms"] = round(ms_p, 4)
             rf["rocprof_source"] = j.get("kernel_stats_source", src)
         tb = sum(k.get("traffic_bytes_per_packet") or 0.0 for k in ks) * float(pk)
@@ -1353,6 +1441,10 @@ def main():
     ap.add_argument("--parity-div", type=int, default=0,
                     help="parity sample: 1 in N address pairs (default: every pair at N=1, 1 in 2 per rank at N>1)")
     ap.add_argument("--egress-flows", type=int, default=4 << 20)
+    ap.add_argument("--c4-steps", type=int, default=0,
+                    help="config 4: steps in all, warm-up included (default: 4 + max(4, --steps / 2))")
+    ap.add_argument("--c4-frames", default="warmup", choices=["none", "warmup", "all"],
+                    help="config 4: steps whose rewritten frames are fingerprinted and compared with the oracle's")
     args = ap.parse_args()
 
     rehearsal = bool(os.environ.get("GPUFLOW_BENCH_SELFTEST"))

@@ -241,7 +241,8 @@ GF_HD uint32_t gf_pair_hash6(const uint32_t *a, const uint32_t *b) {
 
 // Packed per-packet record used by the ingress kernel after grouping
 // (32 B, one dwordx4 x2 load).  cls: bits0-1 L3 class (0 other, 1 v4, 2 v6),
-// bit 2 TC_INDEX_F_SKIP_PROXY.
+// bit 2 TC_INDEX_F_SKIP_PROXY, bit 3 the pipeline packet ended before the tail
+// call, bits 4-6 the pipeline front's GF_PIPE_F_* flags (flags byte bits 5-7).
 struct __attribute__((aligned(16))) gf_rec {
     uint32_t saddr, daddr, len, l4w0, src_identity, ifindex;
     uint16_t ep;           // cilium_policy slot of the packet's lxc_id: program index + 1, 0 = empty

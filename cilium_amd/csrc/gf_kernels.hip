@@ -792,7 +792,7 @@ struct IngCtx {
     uint8_t *pout;     // pipeline records (gf_pipeline_out) to complete instead of gf_ingress_out
     uint32_t pout_wo;  // gf_pipeline_classify: the record's first 10 bytes are written without reading them
     uint32_t pol_wave; // policy counter adds summed per wave first (pol_count_add): the egress deliveries' pass
-                       // (stage POLICY, the front's GF_PIPE_F_LB / _PORTMAP in gf_rec.cls bits 4-5)
+                       // (stage POLICY, the front's GF_PIPE_F_* bits 5-7 in gf_rec.cls bits 4-6)
     uint8_t *snap;     // pipeline: the frames as rewritten so far (handle_policy's writes land here)
     uint32_t snap_stride;
     uint32_t *plog, *plog_n;   // cilium_proxy{4,6} update log (16 words per redirect) and its length
@@ -1815,7 +1815,7 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
     gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab, rlog);
     if (X.pout && X.pout_wo) {                          // complete the pipeline record: stores only
         uint8_t *q = X.pout + 24 * (size_t)i;
-        const uint32_t ff = ((r.cls & 16u) ? GF_PIPE_F_LB : 0u) | ((r.cls & 32u) ? GF_PIPE_F_PORTMAP : 0u);
+        const uint32_t ff = ((uint32_t)(r.cls >> 4) & 7u) << 5;   // the front's whole GF_PIPE_F_* byte
         *reinterpret_cast<uint32_t *>(q) = GF_STAGE_POLICY | ((uint32_t)o.action << 8) | ((uint32_t)o.reason << 16) |
                                            ((uint32_t)o.ct_ret << 24);
         *reinterpret_cast<uint32_t *>(q + 4) = (ff | o.flags) | ((uint32_t)o.proxy_port << 16);
@@ -2383,8 +2383,11 @@ __global__ __launch_bounds__(NT, GF_FRONT_MINW) void k_pipe_front(gf_frames fr, 
             parse_row(w.p, cap, len, h2);
             key = pack_rec(i, h2.et, len, h2.sa, h2.da, h2.w0, h2.w3, h2.l4, h2.proto, sec, ifx, slot_of[lxc & 0xffffu],
                            tci, false, true, h2.s6, h2.d6, rr);
-            // the front's record flags ride along for k_ing_groups' write-only completion (IngCtx::pout_wo)
-            rr.cls |= ((o.flags & GF_PIPE_F_LB) ? 16u : 0u) | ((o.flags & GF_PIPE_F_PORTMAP) ? 32u : 0u);
+            // the front's record flags (every GF_PIPE_F_* bit: the top three of the byte)
+            // ride along in cls bits 4-6 for k_ing_groups' write-only completion (IngCtx::pout_wo)
+            static_assert(((GF_PIPE_F_ICMP6_TE | GF_PIPE_F_LB | GF_PIPE_F_PORTMAP) & ~0xE0u) == 0,
+                          "the pipeline's front flags must fit the top three bits of the flags byte");
+            rr.cls |= (uint8_t)(((o.flags & 0xE0u) >> 5) << 4);
             if (h2.et == 0x86DD) {                       // both addresses in one 32-B piece (a6_stride 32)
                 reinterpret_cast<uint4 *>(s6out)[2 * (size_t)i] = make_uint4(h2.s6[0], h2.s6[1], h2.s6[2], h2.s6[3]);
                 reinterpret_cast<uint4 *>(d6out)[2 * (size_t)i] = make_uint4(h2.d6[0], h2.d6[1], h2.d6[2], h2.d6[3]);
@@ -2591,35 +2594,41 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 // long as the active one (kernel/bpf/bpf_lru_list.c, not in /root/reference) — in
 // effect from the older half of the entries, in an order nothing reproduces.
 // Here an LRU CT map may exceed max_entries inside a batch (the slot array has
-// room); at the end of every classify call that inserts into it, if the device
-// count exceeds max_entries, a deterministic *hand* evicts (the oracle restates it,
-// o_ct_lru_evict):
+// room); at the end of every classify call that inserts into it, once the device
+// count exceeds the high-water mark HW = max_entries - max_entries / 8, a
+// deterministic *hand* evicts (the oracle restates it, o_ct_lru_evict):
 //  * age key of an entry: 0 if its last use (ct_last_use) lies before time 0,
 //    else closing entries (rx_closing | tx_closing) in [0, 65536) and the others
 //    in [65536, 131072), each by last use in one-second bins relative to now (bin
 //    0 = last used 65535 s or more ago);
 //  * home line of an entry: its key's home slot in this table (gf_home_slot of the
 //    CT hash) / slots per 128-B line; NL lines in all;
-//  * the sample: the entries whose home line is below SL = NL >> 6 (SL = NL when
-//    NL <= 65536).  K = the smallest age key covering half of the sample (its older
-//    half is eligible); es = the sample entries with age key <= K;
-//  * a round: Q = count - (max_entries - max_entries / 8); the hand advances over
-//    lines = min(NL, ceil(Q * SL / es)) home lines (NL if es = 0) and deletes every
-//    entry with age key <= K whose home line it passes.  A second round runs only
-//    if the count is still above max_entries (the hand never passes a line twice in
-//    one call).
-// The work is proportional to what a call evicts (the lines passed hold about 2Q
-// entries), not to the table: the whole-table histogram + compaction sweep this
-// replaces read all 16 GB of the 2^29-slot CT per eviction (~7.3 ms).  A deleted
-// slot turns EMPTY when every slot after it up to the end of its probe cluster
-// is gone too (the probe invariant holds), else FREE (claimed by later device
-// inserts, gf_common.h); tombstones the hand passes are cleared the same way.
-// Key bytes of the cleared slots are zeroed.  Every eviction is logged
+//  * the sample: the entries homed in the SL lines from where the hand stands (SL
+//    = NL when NL <= 65536, else max(65536, NL >> 8)), the lines it passes next.  K = the smallest age key covering half of
+//    the sample (its older half is eligible); es = the sample entries with age key
+//    <= K.  A window that holds no entry (only keys chosen to avoid those lines)
+//    is replaced by the whole table (SL = NL);
+//  * the lines for q entries: ceil(q * SL / es);
+//  * round 0 (count > HW): q = count - HW; round 1 (only while count >
+//    max_entries): q = count - HW again, for what round 0's estimate left; round 2
+//    (only while count > max_entries still): the rest of the table.  Each round
+//    passes its lines (at most NL - the lines already passed) from where the hand
+//    stands and deletes every entry with age key <= K homed in them.
+// A map that runs at HW deletes in each call about what the call inserted, so
+// the work per call follows the call's inserts, not the table; the count is back
+// at <= max_entries after every call unless fewer than count - max_entries
+// entries are eligible in the whole table (documented bound, include/gpuflow.h).
+// A deleted slot turns EMPTY when every slot after it up to the end of its probe
+// cluster is gone too (the probe invariant holds), else FREE (claimed by later
+// device inserts, gf_common.h); tombstones the hand passes are cleared the same
+// way.  Key bytes of the cleared slots are zeroed.  Every eviction is logged
 // (gf_ct_evict_log: batch number, now, K, the hand's first line, lines passed,
 // entries deleted).
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
-#define GF_LRU_SAMPLE_SHIFT 6
+#define GF_LRU_SAMPLE_SHIFT 8
+#define GF_LRU_SAMPLE_MIN 65536ull
+#define GF_LRU_ROUNDS 3u
 #define GF_LRU_HT 256u                  // k_lru_hand block
 #define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (CT6; CT4 twice that)
 struct LruLog { uint32_t seq, now, age_cut, pad; unsigned long long hand, lines, evicted; };
@@ -2627,16 +2636,54 @@ struct LruDev {
     uint32_t hist[2 * GF_LRU_BINS];     // the sample's age histogram
     GcCut cut;                          // gf_ct_gc (k_gc_*)
     unsigned long long res[2];          // gf_ct_gc: entries deleted, tombstones cleared
-    uint32_t flag;                      // this call evicts
+    uint32_t flag;                      // this call evicts (count > HW)
     uint32_t K;                         // age keys [0, K] are eligible
-    unsigned long long es, target;      // eligible sample entries; max_entries - max_entries / 8
+    unsigned long long es;              // eligible sample entries (0: empty sample, age-blind)
     unsigned long long hand;            // the hand's next home line (kept across calls)
-    unsigned long long h0, lines;       // this round: home lines [h0, h0 + lines)
-    unsigned long long ev_h0, ev_lines, evicted;   // this call so far
-    unsigned long long kills, cleared;  // this round: entries deleted, tombstones / FREE slots rewritten
+    unsigned long long cnt0;            // the count when this call's eviction began
+    unsigned long long sl;              // the lines the sample covered (the window, or the table)
+    uint32_t wide, pad1;                // the window held no entry: sample the whole table
+    unsigned long long kills[GF_LRU_ROUNDS];   // entries deleted by each round
+    unsigned long long cleared;         // tombstones / FREE slots rewritten (diagnostics)
     uint32_t nlog, pad;
     LruLog log[GF_LRU_LOGCAP];
 };
+// The sampled home lines of a table of nl lines.
+__host__ __device__ __forceinline__ uint64_t lru_sample_lines(uint64_t nl) {
+    if (nl <= GF_LRU_SAMPLE_MIN) return nl;
+    const uint64_t s = nl >> GF_LRU_SAMPLE_SHIFT;
+    return s > GF_LRU_SAMPLE_MIN ? s : GF_LRU_SAMPLE_MIN;
+}
+__host__ __device__ __forceinline__ unsigned long long lru_high_water(uint32_t max_entries) {
+    return (unsigned long long)(max_entries - max_entries / 8u);
+}
+// Round r of this call: the hand's first line and the lines it passes, from the
+// call's state (count at the start, K / es, the earlier rounds' deletions).  Every
+// block of a round's launches computes the same values; nothing is written.
+struct LruRound { unsigned long long h0, lines; };
+__device__ __forceinline__ LruRound lru_round(const LruDev *L, uint32_t r, uint32_t max_entries, uint64_t nl) {
+    const unsigned long long hw = lru_high_water(max_entries), es = L->es, sl = L->sl;
+    unsigned long long c = L->cnt0, passed = 0, h = L->hand;
+    LruRound o{h, 0ull};
+    if (!L->flag) return o;
+    for (uint32_t j = 0; j <= r; j++) {
+        if (j) c -= L->kills[j - 1];
+        unsigned long long ln = 0;
+        if ((j == 0 ? c > hw : c > (unsigned long long)max_entries) && passed < nl) {
+            if (j + 1 < GF_LRU_ROUNDS) {
+                const unsigned long long q = c - hw;
+                ln = es ? (q * sl + es - 1) / es : nl;  // es >= 1: the sample holds entries
+                if (ln > nl - passed) ln = nl - passed;
+            } else {
+                ln = nl - passed;
+            }
+        }
+        if (j == r) { o.h0 = h; o.lines = ln; return o; }
+        h = (h + ln) % nl;
+        passed += ln;
+    }
+    return o;
+}
 __device__ __forceinline__ uint32_t lru_age_key(uint32_t lt, uint32_t fl, uint32_t now) {
     const long long lu = ct_last_use(lt, fl);
     if (lu < 0) return 0u;
@@ -2681,10 +2728,10 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
         gstore<uint4>(p, make_uint4(0u, 0u, 0u, st << 16));
     }
 }
-// The chain after a classify call: k_lru_sample, k_lru_plan (round 0), k_lru_hand
-// x 2, k_lru_mid (round 0's count + round 1's plan), k_lru_hand x 2, k_lru_round_end.
-// Each launch exits at once unless the count exceeds max_entries.  The histogram
-// is zero between calls (cleared by k_lru_plan after its scan; zero at allocation).
+// The chain after a classify call: k_lru_sample, k_lru_plan, k_lru_hand x 2 per
+// round (GF_LRU_ROUNDS), k_lru_end.  Each launch exits at once unless the count
+// exceeds HW (and a round's, unless the round passes lines).  The histogram is zero
+// between calls (cleared by k_lru_plan after its scan; zero at allocation).
 // Age histogram of the sample: wave-aggregated (a wave's entries mostly share a
 // bin), then counted per block in LDS and flushed with one global add per
 // non-zero bin.  The last GF_LRU_WIN seconds of each class are counted directly
@@ -2726,26 +2773,33 @@ __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line
         rem &= ~m;
     }
 }
-// The sample: slots [0, sl * SPL) and the rest of the probe cluster running past
-// them (entries homed in the sampled lines; one wave walks it, up to the table's
-// end — wrapped positions below sl * SPL are the main loop's).
+// The sample: the sl home lines just ahead of the hand (the lines it passes next,
+// so their density is the one its rounds are planned with; the whole table when
+// sl = nl): slots [hand * SPL, (hand + sl) * SPL) mod NS and the rest of the probe
+// cluster running past them (entries homed in the window; one wave walks it, at
+// most to where the window starts again).
+// wide: the whole table (launched after k_lru_plan found the window empty).
 template <int KIND>
 __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                          uint64_t sl, uint32_t max_entries) {
-    if (*d.count <= max_entries) return;
+                                                          uint64_t sl, uint32_t max_entries, uint32_t wide) {
+    if (wide ? !L->wide : (unsigned long long)*d.count <= lru_high_water(max_entries)) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
     __syncthreads();
-    const uint64_t ns = d.mask + 1, n = sl * LruSlot<KIND>::SPL;
+    constexpr uint32_t SPL = LruSlot<KIND>::SPL;
+    const uint64_t ns = d.mask + 1, nl = ns / SPL;
+    if (wide) sl = nl;
+    const uint64_t n = sl * SPL, h0 = sl >= nl ? 0 : L->hand, P0 = h0 * SPL;
+    auto in_window = [&](const LruSlot<KIND> &s) { return (s.home_line(d, mode) + nl - h0) % nl < sl; };
     for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB; b0 < n; b0 += (uint64_t)gridDim.x * GF_LRU_HB) {  // uniform trips
         const uint64_t i = b0 + threadIdx.x;
         uint32_t key = ~0u;
         if (i < n) {
             LruSlot<KIND> s;
-            s.load(d, i);
-            if (s.st == GF_SLOT_FULL && s.home_line(d, mode) < sl) key = lru_age_key(s.lt, s.fl, now);
+            s.load(d, (P0 + i) & d.mask);
+            if (s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
         }
         lru_hist_add(L, line, win, key);
     }
@@ -2753,14 +2807,13 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
         for (uint64_t q = n;; q += 64) {
             const uint64_t i = q + threadIdx.x;
             LruSlot<KIND> s;
-            if (i < ns) s.load(d, i);
+            if (i < ns) s.load(d, (P0 + i) & d.mask);
             const uint64_t em = __ballot(s.st == GF_SLOT_EMPTY);
             const uint32_t stop = em ? (uint32_t)__ffsll((unsigned long long)em) - 1u : 64u;
             uint32_t key = ~0u;
-            if (threadIdx.x < stop && s.st == GF_SLOT_FULL && s.home_line(d, mode) < sl)
-                key = lru_age_key(s.lt, s.fl, now);
+            if (threadIdx.x < stop && s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
             lru_hist_add(L, line, win, key);
-            if (em) break;
+            if (em || q + 64 >= ns) break;
         }
     }
     __syncthreads();
@@ -2771,77 +2824,75 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
         if (win[k]) atomicAdd(&L->hist[(k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN], win[k]);
 }
-// Round `round` of a call: K and es from the sample (round 0), then the lines
-// the hand passes.  One block (128 bins per thread, then a block scan).
-__device__ __forceinline__ void lru_plan_body(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
-                                              uint64_t sl, uint32_t round) {
+// K and es from the sample's histogram, the count the call starts from, and the
+// histogram cleared for the next call.  One block: wave w sums bins [w * 8192,
+// (w + 1) * 8192) in 128 coalesced groups of 64 (group sums to LDS), a block scan
+// over the 2048 group sums finds the median's group, one wave finds its bin.
+// wide = 0: the window's sample; an empty one (sl < nl) sets L->wide for the
+// whole-table sample and its plan (wide = 1) instead of planning.
+__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
+                                                   uint64_t nl, uint32_t wide) {
+    const uint32_t c = *count;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (wide) {
+        if (!L->wide) return;
+        sl = nl;
+    } else if ((unsigned long long)c <= lru_high_water(max_entries)) {
+        if (t == 0) L->flag = 0u;
+        return;
+    }
+    constexpr uint32_t NB = 2 * GF_LRU_BINS, PW = NB / 16, IT = PW / 64, NG = NB / 64;
+    __shared__ uint32_t gs[NG];                         // group sums (< 2^32: a sample's entries)
     __shared__ unsigned long long part[1024];
-    __shared__ uint32_t s_k;
-    __shared__ unsigned long long s_es;
-    const uint32_t t = threadIdx.x;
-    if (round == 0) {
-        constexpr uint32_t PER = 2 * GF_LRU_BINS / 1024;
-        unsigned long long s = 0;
-        for (uint32_t k = 0; k < PER; k++) s += L->hist[t * PER + k];
-        part[t] = s;
-        if (t == 0) { s_k = 2 * GF_LRU_BINS - 1; s_es = 0; }
-        __syncthreads();
-        for (uint32_t o = 1; o < 1024; o <<= 1) {       // inclusive scan
-            const unsigned long long v = t >= o ? part[t - o] : 0ull;
-            __syncthreads();
-            part[t] += v;
-            __syncthreads();
-        }
-        const unsigned long long total = part[1023], need = (total + 1) / 2, before = t ? part[t - 1] : 0ull;
-        if (total && before < need && part[t] >= need) {  // the median bin lies in this thread's range
-            unsigned long long acc = before;
-            for (uint32_t k = 0; k < PER; k++) {
-                acc += L->hist[t * PER + k];
-                if (acc >= need) { s_k = t * PER + k; s_es = acc; break; }
-            }
-        }
-        __syncthreads();
-        for (uint32_t k = 0; k < PER; k++) L->hist[t * PER + k] = 0;   // clear for the next call's sample
-        if (t == 0) {
-            L->K = s_k; L->es = s_es;
-            L->target = (unsigned long long)(max_entries - max_entries / 8u);
-            L->ev_h0 = L->hand; L->ev_lines = 0; L->evicted = 0;
-        }
+    __shared__ uint32_t s_g, s_k;
+    __shared__ unsigned long long s_before, s_es;
+    const uint32_t *hp = L->hist + (size_t)w * PW;
+#pragma unroll 16
+    for (uint32_t it = 0; it < IT; it++) {
+        uint32_t v = hp[it * 64 + lane];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) gs[w * IT + it] = v;
     }
-    if (t == 0) {
-        const unsigned long long c = *count;
-        unsigned long long lines = 0;
-        if (c > max_entries && L->ev_lines < nl) {
-            const unsigned long long q = c - L->target;
-            lines = L->es ? (q * sl + L->es - 1) / L->es : nl;
-            lines = lines < nl - L->ev_lines ? lines : nl - L->ev_lines;
-        }
-        L->h0 = L->hand; L->lines = lines; L->kills = 0; L->cleared = 0;
-        L->hand = (L->hand + lines) % nl;
-        L->ev_lines += lines;
+    if (t == 0) { s_g = ~0u; s_k = NB - 1; s_es = 0; s_before = 0; }
+    __syncthreads();
+    part[t] = (unsigned long long)gs[2 * t] + gs[2 * t + 1];
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan of the pair sums
+        const unsigned long long v = t >= o ? part[t - o] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
     }
-}
-__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
-                                                   uint64_t sl) {
-    const bool f = *count > max_entries;
-    if (threadIdx.x == 0) L->flag = f ? 1u : 0u;
-    if (!f) return;
-    lru_plan_body(count, max_entries, L, nl, sl, 0);
-}
-// Round 0's deletions off the count, then round 1's lines.
-__global__ __launch_bounds__(1024) void k_lru_mid(uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t nl,
-                                                  uint64_t sl) {
-    if (!L->flag) return;
-    __shared__ uint32_t s_c;
-    if (threadIdx.x == 0) {
-        const unsigned long long k = L->kills;
-        s_c = (uint32_t)(*count - k);
-        *count = s_c;
-        L->evicted += k;
-        L->kills = 0;
+    const unsigned long long total = part[1023], need = (total + 1) / 2, before = t ? part[t - 1] : 0ull;
+    if (!total && sl < nl) {                            // no entry in the window (histogram still all zero)
+        if (t == 0) { L->wide = 1u; L->flag = 0u; }
+        return;
+    }
+    if (total && before < need && part[t] >= need) {    // the median lies in groups 2t, 2t + 1
+        const bool first = before + gs[2 * t] >= need;
+        s_g = first ? 2 * t : 2 * t + 1;
+        s_before = first ? before : before + gs[2 * t];
     }
     __syncthreads();
-    lru_plan_body(&s_c, max_entries, L, nl, sl, 1);
+    if (w == 0 && s_g != ~0u) {                          // the median group's bins, one per lane
+        const uint32_t v = L->hist[(size_t)s_g * 64 + lane];
+        uint32_t inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o);
+            if (lane >= (uint32_t)o) inc += u;
+        }
+        const unsigned long long acc = s_before + inc;
+        const uint64_t hit = __ballot(acc >= need);
+        if (lane == (uint32_t)__ffsll((unsigned long long)hit) - 1u) { s_k = s_g * 64 + lane; s_es = acc; }
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < NB; k += 1024) L->hist[k] = 0;   // clear for the next call's sample
+    if (t == 0) {
+        L->K = s_k; L->es = s_es; L->cnt0 = c; L->sl = sl; L->wide = 0u; L->flag = 1u; L->cleared = 0;
+        for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) L->kills[r] = 0;
+    }
 }
 // The hand over this round's lines: the slots from the first line's first slot,
 // lines * SPL of them, in chunks (GF_LRU_CHUNK slots, twice that for CT4), plus the cluster running past
@@ -2855,16 +2906,17 @@ __global__ __launch_bounds__(1024) void k_lru_mid(uint32_t *count, uint32_t max_
 // tombstone or FREE slot (cleared).
 template <int KIND, int PAR>
 __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                        uint64_t nl) {
+                                                        uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t round) {
     if (!L->flag) return;
-    const unsigned long long lines = L->lines;
+    const LruRound R = lru_round(L, round, max_entries, nl);
+    const unsigned long long lines = R.lines;
     if (!lines) return;
     using S = LruSlot<KIND>;
     // slots a block decides together: 8 per thread for the 32-B CT4 slots, 4 for the
     // 64-B CT6 slots (the same 64 KB of loads in flight per block)
     constexpr uint32_t CH = KIND == 2 ? GF_LRU_CHUNK : 2 * GF_LRU_CHUNK, U = CH / GF_LRU_HT;
     const uint32_t K = L->K;
-    const unsigned long long h0 = L->h0;
+    const unsigned long long h0 = R.h0;
     const uint64_t ns = d.mask + 1, P0 = h0 * S::SPL, NP = lines * S::SPL;
     const bool whole = NP >= ns;
     const uint64_t nch = (NP + CH - 1) / CH;
@@ -2953,34 +3005,34 @@ __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t
     if (clr) atomicAdd(&s_clr, clr);
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (s_kills) atomicAdd(&L->kills, (unsigned long long)s_kills);
+        if (s_kills) atomicAdd(&L->kills[round], (unsigned long long)s_kills);
         if (s_clr) atomicAdd(&L->cleared, (unsigned long long)s_clr);
     }
 }
-// After a round: the count, and after the last one the log (hcount: the count
-// for the host's bound, pinned host memory, may be null).
-__global__ void k_lru_round_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t last,
-                                uint32_t *hcount) {
+// After the last round: the count, the hand, the log (hcount: the count for the
+// host's bound, pinned host memory, may be null).
+__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t max_entries, uint64_t nl,
+                          uint32_t *hcount) {
     if (!L->flag) {
-        if (last && hcount) *hcount = *count;
+        if (hcount) *hcount = *count;
         return;
     }
-    // (last == 0 is k_lru_mid's part now; kept for the chain's readers)
-    const unsigned long long k = L->kills;
-    *count = (uint32_t)(*count - k);
-    L->evicted += k;
-    L->kills = 0;
-    if (last) {
-        const uint32_t n = L->nlog;
-        if (n < GF_LRU_LOGCAP) {
-            LruLog &g = L->log[n];
-            g.seq = seq; g.now = now; g.age_cut = L->K; g.pad = 0;
-            g.hand = L->ev_h0; g.lines = L->ev_lines; g.evicted = L->evicted;
-        }
-        L->nlog = n + 1;
-        L->flag = 0;
-        if (hcount) *hcount = *count;
+    unsigned long long killed = 0, lines = 0;
+    for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) {
+        lines += lru_round(L, r, max_entries, nl).lines;
+        killed += L->kills[r];
     }
+    *count = (uint32_t)(*count - killed);
+    const uint32_t n = L->nlog;
+    if (n < GF_LRU_LOGCAP) {
+        LruLog &g = L->log[n];
+        g.seq = seq; g.now = now; g.age_cut = L->K; g.pad = 0;
+        g.hand = L->hand; g.lines = lines; g.evicted = killed;
+    }
+    L->nlog = n + 1;
+    L->hand = (L->hand + lines) % nl;
+    L->flag = 0;
+    if (hcount) *hcount = *count;
 }
 
 // ================================================================ drop notifications
@@ -5563,57 +5615,74 @@ static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
                        (const uint32_t *)bits, L->res);
 }
 // The LRU stand-in after a classify call (k_lru_*: see the kernels): fully on the
-// device, a chain of launches that exit at once unless the map's count exceeds
-// max_entries.
+// device, a chain of launches that exit at once unless the map's count exceeds its
+// high-water mark; not launched at all while the host's bound of the count is at or
+// below it.
 static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s) {
     if (!m || m->type != GF_MAP_TYPE_LRU_HASH || !m->d_slots.p) return 0;
     m->lru_seq++;
     ct_count_refresh(*m);
-    if (m->dev_count_hi <= m->max_entries) return 0;    // cannot have crossed max_entries
-    LruDev *L;
-    uint32_t *bits;
-    int r;
-    if ((r = ct_sweep_bufs(*m, L, bits))) return r;
+    if (m->dev_count_hi <= lru_high_water(m->max_entries)) return 0;   // cannot have crossed HW
+    if (!m->d_lru.p) {
+        if (m->d_lru.ensure(sizeof(LruDev))) return -ENOMEM;
+        if (hip_ok(hipMemset(m->d_lru.p, 0, sizeof(LruDev)), "lru init")) return -EIO;
+    }
+    LruDev *L = (LruDev *)m->d_lru.p;
     const gf_htab_desc d = m->hdesc();
     const int kind = d.slot_size == 32 && d.ksz == 14 && d.vin == 16 && d.voff == 16 ? 1
                    : d.slot_size == 64 && d.ksz == 40 && d.vin == 16 && d.voff == 48 ? 2 : 0;
     if (!kind) return -EIO;                              // the CT codec's layouts only
     if (!m->h_evcount) {
+        // every event first, the count words last: a failure leaves nothing half made
+        hipEvent_t ev[Map::GF_EVRING] = {};
+        bool ok = true;
+        for (auto &e : ev)
+            if (ok && hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "lru count event")) ok = false;
         void *p = nullptr;
-        if (hip_ok(hipHostMalloc(&p, 4 * Map::GF_EVRING, hipHostMallocMapped | hipHostMallocCoherent), "lru count words")) return -ENOMEM;
+        if (ok && hip_ok(hipHostMalloc(&p, 4 * Map::GF_EVRING, hipHostMallocMapped | hipHostMallocCoherent),
+                         "lru count words"))
+            ok = false;
+        if (!ok) {
+            for (auto &e : ev)
+                if (e) (void)hipEventDestroy(e);
+            return -ENOMEM;
+        }
+        for (uint32_t k = 0; k < Map::GF_EVRING; k++) m->ev_count[k] = ev[k];
         m->h_evcount = (uint32_t *)p;
-        for (auto &e : m->ev_count)
-            if (hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "lru count event")) return -ENOMEM;
     }
     const uint32_t slot = m->ev_head;
     uint32_t *hc = nullptr;
     if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount + slot, 0), "lru count word")) return -EIO;
     const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size, nl = ns / spl;
-    const uint64_t sl = nl <= 65536 ? nl : nl >> GF_LRU_SAMPLE_SHIFT;
+    const uint64_t sl = lru_sample_lines(nl);
     const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
     const uint32_t gh = resident_blocks(8);
     const uint32_t *cnt = (const uint32_t *)d.count;
+    const uint32_t mx = m->max_entries;
     {
         ProfScope ps("k_lru_evict", s);
-        if (kind == 1)
-            hipLaunchKernelGGL(k_lru_sample<1>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, m->max_entries);
-        else
-            hipLaunchKernelGGL(k_lru_sample<2>, dim3(gs), dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, m->max_entries);
-        hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, m->max_entries, L, nl, sl);
-        for (uint32_t round = 0; round < 2; round++) {
-            // round 1 is rare (the count still above max_entries): a smaller grid, the same chunks
-            const dim3 g(round ? gh / 8 : gh);
-            if (kind == 1) {
-                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-            } else {
-                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl);
-            }
-            if (round == 0)
-                hipLaunchKernelGGL(k_lru_mid, dim3(1), dim3(1024), 0, s, d.count, m->max_entries, L, nl, sl);
+        // the window's sample and plan, then (large tables only) the whole-table
+        // pair, which runs only when the window held no entry
+        for (uint32_t wide = 0; wide < (sl < nl ? 2u : 1u); wide++) {
+            const dim3 g(wide ? gh : gs);
+            if (kind == 1)
+                hipLaunchKernelGGL(k_lru_sample<1>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
+            else
+                hipLaunchKernelGGL(k_lru_sample<2>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
+            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, mx, L, sl, nl, wide);
         }
-        hipLaunchKernelGGL(k_lru_round_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, 1u, hc);
+        for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
+            // round 1 is rare and short (what round 0's estimate left): a smaller grid, the same chunks
+            const dim3 g(round == 1 ? gh / 8 : gh);
+            if (kind == 1) {
+                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+            } else {
+                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+            }
+        }
+        hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, mx, nl, hc);
     }
     if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
     m->ev_pending |= 1u << slot;
@@ -5623,10 +5692,15 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     if (stats) {
         LruDev h;
         if (!hip_ok(hipMemcpyAsync(&h, L, offsetof(LruDev, log), hipMemcpyDeviceToHost, s), "lru stats") &&
-            !hip_ok(hipStreamSynchronize(s), "lru stats") && h.ev_lines)
-            fprintf(stderr, "[lru] seq %u now %u: K %u es %llu lines %llu of %llu (hand %llu) evicted %llu, last round "
-                    "cleared %llu\n", m->lru_seq, now, h.K, h.es, h.ev_lines, (unsigned long long)nl, h.ev_h0,
-                    h.evicted, h.cleared);
+            !hip_ok(hipStreamSynchronize(s), "lru stats") && h.nlog) {
+            uint32_t n = h.nlog;
+            LruLog g{};
+            if (!hip_ok(hipMemcpy(&g, &L->log[std::min(n, GF_LRU_LOGCAP) - 1], sizeof g, hipMemcpyDeviceToHost),
+                        "lru stats log") && g.seq == m->lru_seq)
+                fprintf(stderr, "[lru] seq %u now %u: K %u es %llu lines %llu of %llu (hand %llu) evicted %llu "
+                        "(rounds %llu / %llu / %llu), cleared %llu\n", g.seq, now, g.age_cut, h.es, g.lines,
+                        (unsigned long long)nl, g.hand, g.evicted, h.kills[0], h.kills[1], h.kills[2], h.cleared);
+        }
     }
     return hip_ok(hipGetLastError(), "k_lru_evict");
 }

@@ -489,13 +489,21 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream);
  * about as long as the active one) in a nondeterministic order and never fails
  * an insert.  libgpuflow's deterministic stand-in: inside a batch an
  * LRU CT map may exceed max_entries (up to the 7/8 load of its slot array: a power
- * of two >= 8 x max_entries for ipv4_ct_tuple, 4 x for ipv6_ct_tuple); at the end of every classify call that uses it, if the count
- * exceeds max_entries, a hand sweeping the table's home lines deletes the
- * entries of the older half (age key <= age_cut: the median age of a fixed
- * 1/64 sample of the lines — closing entries older than all others, then by
- * last use in one-second bins) homed in the lines it passes, as many lines as
- * bring the count to max_entries - max_entries/8 by the sample's density.
- * Every eviction is logged: */
+ * of two >= 8 x max_entries for ipv4_ct_tuple, 4 x for ipv6_ct_tuple).  At the end
+ * of every classify call that uses it, once the count exceeds the high-water mark
+ * HW = max_entries - max_entries/8, a hand sweeping the table's home lines deletes
+ * the entries of the older half (age key <= age_cut: the median age of a sample —
+ * the max(65536, lines/256) home lines just ahead of the hand, or the whole table if
+ * no entry is homed there; closing entries older than all others, then by last use
+ * in one-second bins) homed in the lines it passes, as many lines as bring the count
+ * back to HW by the sample's density.  A map running at HW so deletes in each call
+ * about what the call inserted: the eviction's work per call follows the call's
+ * inserts, not the table.  If the count is still above max_entries, a second round
+ * passes more lines by the same estimate and a third the rest of the table.
+ * Bound: after a call the count is <= max_entries unless the whole table held
+ * fewer than count - max_entries entries of the sample's older half (a single call
+ * inserting more than about half of max_entries beyond HW); it never falls below
+ * the entries younger than age_cut.  Every eviction is logged: */
 typedef struct gf_ct_evict_rec {
     uint32_t seq;              /* the map's classify call (1 = first call that used the map) */
     uint32_t now_sec;          /* that call's now_sec */

@@ -1866,9 +1866,9 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
 /* inactive list kept about as long as the active one — in an order    */
 /* that is not reproducible; libgpuflow and this restatement share one  */
 /* deterministic rule instead (include/gpuflow.h):        */
-/* after a batch, if count > max_entries, a hand sweeping the home      */
-/* lines of libgpuflow's slot array deletes the entries of the older    */
-/* half homed in the lines it passes:                                   */
+/* after a batch, if count > HW = max_entries - max_entries / 8, a hand */
+/* sweeping the home lines of libgpuflow's slot array deletes the       */
+/* entries of the older half homed in the lines it passes:              */
 /*  * age key: 0 if the last use lies before time 0, else closing       */
 /*    entries (rx_closing | tx_closing) in [0, 65536), the others in    */
 /*    [65536, 131072), by last use in one-second bins relative to now   */
@@ -1879,13 +1879,18 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
 /*    array (ct_slots: pow2ceil(max(64, 8 or 4 x max_entries))), SPL  */
 /*    = 128-B line /                                                    */
 /*    slot (4 for ipv4_ct_tuple, 2 for ipv6_ct_tuple); NL = NS / SPL;   */
-/*  * sample = entries homed below SL = NL >> 6 (NL when NL <= 65536);  */
-/*    K = the smallest age key with at least half of the sample at or   */
-/*    below it, es = the sample's entries with age key <= K;            */
-/*  * up to two rounds while count > max_entries: Q = count - (max -    */
-/*    max / 8), lines = min(NL - lines so far, ceil(Q SL / es)) (NL if  */
-/*    es = 0); delete every entry with age key <= K homed in           */
-/*    [hand, hand + lines) (mod NL); hand += lines.                     */
+/*  * sample = entries homed in [hand, hand + SL) (mod NL), SL =        */
+/*    max(65536, NL >> 8) (NL when NL <= 65536), the lines the hand     */
+/*    passes next; K = the smallest age key with at least half of the  */
+/*    sample at or below it, es = the sample's entries with age key     */
+/*    <= K; a window holding no entry is replaced by the whole table    */
+/*    (SL = NL, hand 0);                                                */
+/*  * lines for q entries: ceil(q SL / es);                             */
+/*  * round 0 (count > HW): q = count - HW; round 1 (count still >      */
+/*    max_entries): q = count - HW; round 2 (count still > max_entries):*/
+/*    the rest of the table; each round at most NL - lines so far,      */
+/*    deleting every entry with age key <= K homed in [hand, hand +     */
+/*    lines) (mod NL); hand += lines.                                   */
 /* ------------------------------------------------------------------ */
 #define LRU_BINS 65536u
 static int64_t ct_last_use(uint32_t lt, uint16_t fl) {
@@ -1942,7 +1947,7 @@ static lru_geo lru_geometry(const om_map *m) {
     g.ns = ct_slots(m);
     g.spl = m->ksz == 14 ? 4u : 2u;
     g.nl = g.ns / g.spl;
-    g.sl = g.nl <= 65536 ? g.nl : g.nl >> 6;
+    g.sl = g.nl <= 65536 ? g.nl : ((g.nl >> 8) > 65536 ? (g.nl >> 8) : 65536);
     return g;
 }
 static uint64_t lru_home_line(const om_map *m, const lru_geo *g, const uint8_t *key) {
@@ -1965,7 +1970,7 @@ static void *lru_worker(void *a_) {
             const uint8_t *k = SH_KEY(m, h, i);
             if (!a->kill) {
                 const uint64_t hl = lru_home_line(m, a->g, k);
-                if (hl < a->g->sl) a->hist[lru_age_key(SH_VAL(m, h, i), a->now)]++;
+                if ((hl + a->g->nl - a->h0) % a->g->nl < a->lines) a->hist[lru_age_key(SH_VAL(m, h, i), a->now)]++;
                 continue;
             }
             if (lru_age_key(SH_VAL(m, h, i), a->now) > a->K) continue;
@@ -2003,23 +2008,38 @@ static uint64_t lru_pass(om_map *m, const lru_geo *g, uint32_t now, int kill, ui
 /* The hand after a batch: 1 and the log record (age_cut, first line, lines,
  * evicted) if it evicted, else 0.  The hand's position lives in the map. */
 int o_ct_lru_evict(om_map *m, uint32_t now, uint32_t *age_cut, uint64_t *hand, uint64_t *lines, uint64_t *evicted) {
-    if (m->count <= m->max_entries) return 0;
+    const uint64_t hw = m->max_entries - m->max_entries / 8u;
+    if (m->count <= hw) return 0;
     const lru_geo g = lru_geometry(m);
     uint64_t *hist = (uint64_t *)calloc(2 * LRU_BINS, sizeof(uint64_t));
-    lru_pass(m, &g, now, 0, 0, 0, 0, hist);
-    uint64_t total = 0, acc = 0, es = 0;
+    /* the sample: the window of SL lines ahead of the hand (the histogram pass's
+     * "lines" argument is the window size); if no entry is homed there, the
+     * whole table */
+    uint64_t sl = g.sl, total = 0, acc = 0, es = 0;
+    lru_pass(m, &g, now, 0, 0, sl >= g.nl ? 0 : m->lru_hand, sl, hist);
     for (uint32_t k = 0; k < 2 * LRU_BINS; k++) total += hist[k];
+    if (!total && sl < g.nl) {
+        sl = g.nl;
+        lru_pass(m, &g, now, 0, 0, 0, sl, hist);
+        for (uint32_t k = 0; k < 2 * LRU_BINS; k++) total += hist[k];
+    }
     uint32_t K = 2 * LRU_BINS - 1;
     const uint64_t need = (total + 1) / 2;
     if (total)
         for (uint32_t k = 0; k < 2 * LRU_BINS; k++) { acc += hist[k]; if (acc >= need) { K = k; es = acc; break; } }
     free(hist);
-    const uint64_t target = m->max_entries - m->max_entries / 8u;
     *age_cut = K; *hand = m->lru_hand; *lines = 0; *evicted = 0;
-    for (int round = 0; round < 2 && m->count > m->max_entries && *lines < g.nl; round++) {
-        const uint64_t q = m->count - target;
-        uint64_t l = es ? (q * g.sl + es - 1) / es : g.nl;
-        if (l > g.nl - *lines) l = g.nl - *lines;
+    for (int round = 0; round < 3; round++) {
+        const uint64_t c = m->count;
+        if (!(round == 0 ? c > hw : c > m->max_entries) || *lines >= g.nl) continue;
+        uint64_t l;
+        if (round < 2) {
+            const uint64_t q = c - hw;
+            l = es ? (q * sl + es - 1) / es : g.nl;         /* es >= 1: the table holds entries */
+            if (l > g.nl - *lines) l = g.nl - *lines;
+        } else {
+            l = g.nl - *lines;
+        }
         *evicted += lru_pass(m, &g, now, 1, K, m->lru_hand, l, NULL);
         m->lru_hand = (m->lru_hand + l) % g.nl;
         *lines += l;

@@ -71,6 +71,39 @@ def compare_records(gpu, ref):
     return int(len(bad)), int(bad[0]) if len(bad) else -1
 
 
+# Frame fingerprints: one 64-bit value per rewritten frame row (snap_out), so that
+# whole-stream runs compare the LB / rev-NAT / netdev rewrites without keeping
+# every frame.  h = sum over the row's little-endian u64 words w_j of
+# w_j * FP_MUL^(m-1-j) (mod 2^64), Horner form; FP_MUL is odd, so a change of any
+# single word always changes h.  The numpy form runs on the oracle's frames, the
+# torch form on the device's snap buffer (wrapping int64 arithmetic, same bits).
+FP_MUL = 0x9E3779B97F4A7C15
+
+
+def frame_fingerprints(rows):
+    """uint64[n] fingerprints of uint8[n, stride] rows (stride a multiple of 8)."""
+    rows = np.ascontiguousarray(rows, np.uint8)
+    w = rows.view("<u8")
+    h = np.zeros(len(rows), np.uint64)
+    m = np.uint64(FP_MUL)
+    with np.errstate(over="ignore"):
+        for j in range(w.shape[1]):
+            h = h * m + w[:, j]
+    return h
+
+
+def frame_fingerprints_torch(rows):
+    """The same fingerprints of a uint8 [n, stride] torch tensor, on its device;
+    returned as int64 (view the numpy copy as uint64)."""
+    import torch
+    w = rows.contiguous().view(torch.int64)
+    m = FP_MUL - (1 << 64) if FP_MUL >= 1 << 63 else FP_MUL
+    h = torch.zeros(rows.shape[0], dtype=torch.int64, device=rows.device)
+    for j in range(w.shape[1]):
+        h = h * m + w[:, j]
+    return h
+
+
 def _sort_rows(k, v):
     """Rows sorted by key bytes (lexicographic)."""
     if len(k) == 0:

@@ -78,6 +78,17 @@ def test_launcher_world_8_rehearsal():
         assert c["n_gpus"] == 8 and c["parity"]["ranks"] == 8 and c["parity"]["mismatches"] == 0
         assert c["parity"]["ct_mismatches"] == 0
     assert r["configs"]["4"]["verdicts"] == r["configs"]["4x"]["verdicts"]
+    # the line a first 8-GPU run is diagnosed from: every rank's step time, its
+    # k_ing_groups average and the counter all-reduce's cost, and what each rank compared
+    rk = r["ranks"]
+    for k in ("ms_per_step", "k_ing_groups_avg_ms", "counter_allreduce_ms", "packets"):
+        assert len(rk[k]["per_rank"]) == 8 and rk[k]["min"] <= rk[k]["max"], (k, rk[k])
+    assert rk["packets"]["per_rank"] == [r["config"]["packets_per_step_per_gpu"] * r["steps"]] * 8
+    assert abs(rk["ms_per_step"]["max"] - r["ms_per_step"]) <= 1e-3 * r["ms_per_step"] + 1e-3
+    assert len(p["packets_compared_per_rank"]) == 8 and sum(p["packets_compared_per_rank"]) == p["packets_compared"]
+    assert min(p["packets_compared_per_rank"]) > 0
+    for k in ("4", "4x"):
+        assert len(r["configs"][k]["ranks"]["ms_per_step"]["per_rank"]) == 8
 
 
 def test_parity_div_fits_the_host():

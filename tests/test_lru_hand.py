@@ -1,9 +1,10 @@
 """The LRU stand-in's eviction rule (the hand): the oracle's C
 restatement (oracle.c o_ct_lru_evict) against a second, independent numpy
 restatement written here from the rule's statement in include/gpuflow.h — age
-keys, libgpuflow's CT hash and home lines, the 1/64 line sample and its median,
-the lines the hand passes per round, wrap-around of the hand — on random CT4 and
-CT6 tables over several consecutive evictions.  The GPU's side of the same rule
+keys, libgpuflow's CT hash and home lines, the line sample and its median, the
+high-water trigger, the lines the hand passes per round, wrap-around of the hand,
+the age-blind fallback of an empty sample — on random CT4 and CT6 tables over
+several consecutive evictions.  The GPU's side of the same rule
 is pinned against the oracle by tests/test_gpu_maps.py (eviction logs equal)."""
 import numpy as np
 import pytest
@@ -81,31 +82,39 @@ class Hand:
             self.ns *= 2
         self.spl = 4 if ksz == 14 else 2
         self.nl = self.ns // self.spl
-        self.sl = self.nl if self.nl <= 65536 else self.nl >> 6
+        self.sl = self.nl if self.nl <= 65536 else max(65536, self.nl >> 8)
+        self.hw = max_entries - max_entries // 8          # the high-water mark
         self.hand = 0
+
+    def home_lines(self, keys):
+        return (ct_hash(keys) & np.uint64(self.ns - 1)).astype(np.int64) // self.spl
 
     def evict(self, keys, vals, now):
         """(kept mask, log record or None)."""
         n = len(keys)
         keep = np.ones(n, bool)
-        if n <= self.max:
+        if n <= self.hw:
             return keep, None
-        hl = (ct_hash(keys) & np.uint64(self.ns - 1)).astype(np.int64) // self.spl
+        hl = self.home_lines(keys)
         ak = age_keys(vals, now)
-        samp = np.sort(ak[hl < self.sl])
-        if len(samp):
-            K = int(samp[(len(samp) + 1) // 2 - 1])
-            es = int((samp <= K).sum())
-        else:
-            K, es = 2 * BINS - 1, 0
-        target = self.max - self.max // 8
+        sl = self.sl
+        h0 = 0 if sl >= self.nl else self.hand          # the window ahead of the hand
+        samp = np.sort(ak[((hl - h0) % self.nl) < sl])
+        if not len(samp):                               # an empty window: the whole table
+            sl = self.nl
+            samp = np.sort(ak)
+        K = int(samp[(len(samp) + 1) // 2 - 1])
+        es = int((samp <= K).sum())
         h0, lines, ev, count = self.hand, 0, 0, n
-        for _ in range(2):
-            if count <= self.max or lines >= self.nl:
-                break
-            q = count - target
-            ln = -(-q * self.sl // es) if es else self.nl
-            ln = min(ln, self.nl - lines)
+        for rnd in range(3):
+            if (count <= self.hw if rnd == 0 else count <= self.max) or lines >= self.nl:
+                continue
+            if rnd < 2:
+                q = count - self.hw
+                ln = -(-q * sl // es)
+                ln = min(ln, self.nl - lines)
+            else:
+                ln = self.nl - lines
             kill = keep & (ak <= K) & (((hl - self.hand) % self.nl) < ln)
             keep &= ~kill
             count -= int(kill.sum())
@@ -152,6 +161,8 @@ def test_hand_matches_independent_restatement(ksz, max_entries, n0):
             events += 1
             K, h0, lines, ev = rec
             assert m.count() <= max_entries and ev > 0
+        else:
+            assert m.count() <= ref.hw
         # more traffic: new entries at `now`, a later batch boundary
         now += 7
         nk, nv = _table(rng, ksz, max_entries // 6, now)
@@ -182,3 +193,63 @@ def test_hand_evicts_the_older_half_only():
     samp = np.sort(ak[hl < h.sl])
     assert (samp <= K).sum() * 2 >= len(samp) and (samp < K).sum() * 2 < len(samp)
     assert (inr & (ak > K)).sum() > 0          # the younger entries of the passed lines stay
+
+
+def test_hand_sampled_table_and_steady_state():
+    """A table large enough to be sampled (NL > 65536 lines: SL = max(65536, NL >> 8)):
+    once the count has crossed the high-water mark, each batch boundary deletes about
+    what the batch inserted — the lines passed follow the inserts, not the table —
+    and the count stays at or below max_entries after every call."""
+    rng = np.random.default_rng(11)
+    now, mx = 60_000, 40_000
+    h = Hand(14, mx)
+    assert h.nl > 65536 and h.sl == max(65536, h.nl >> 8) and h.sl < h.nl
+    m = O.OMap(9, 14, 48, mx)
+    keys, vals = _table(rng, 14, h.hw - 500, now)
+    m.update_many(keys, vals)
+    assert m.lru_evict(now) is None                     # below the high-water mark: nothing
+    per_call = []
+    for step in range(6):
+        now += 5
+        nk, nv = _table(rng, 14, 3000, now)
+        fresh = ~np.isin(nk.view("V14").ravel(), keys.view("V14").ravel())
+        nk, nv = nk[fresh], nv[fresh]
+        m.update_many(nk, nv)
+        keys, vals = np.concatenate([keys, nk]), np.concatenate([vals, nv])
+        keep, rec = h.evict(keys, vals, now)
+        got = m.lru_evict(now)
+        assert got == rec, (step, got, rec)
+        keys, vals = keys[keep], vals[keep]
+        assert m.count() == len(keys) <= mx
+        if rec:
+            per_call.append((len(nk), rec[2], rec[3]))
+    # steady state: every call evicts, each about what it inserted (the sample's
+    # density estimate), passing far fewer lines than the table holds
+    assert len(per_call) >= 5
+    for ins, lines, ev in per_call[1:]:
+        assert 0.8 * ins <= ev <= 1.25 * ins + 200 and lines < h.nl // 4, (ins, lines, ev)
+
+
+def test_hand_empty_sample_is_not_a_flush():
+    """Keys chosen so that none is homed in the sampled window (the CT hash is fixed
+    and public): the sample falls back to the whole table, K is its median age, and
+    at most its older half can go — never a flush (advisor r5: the old rule passed
+    every line with every age eligible)."""
+    rng = np.random.default_rng(5)
+    now, mx = 70_000, 40_000
+    h = Hand(14, mx)
+    keys, vals = _table(rng, 14, 3 * mx, now)
+    out = h.home_lines(keys) >= h.sl                  # the hand stands at line 0: the window is [0, SL)
+    keys, vals = keys[out][: mx + 2000], vals[out][: mx + 2000]
+    assert len(keys) == mx + 2000
+    m = O.OMap(9, 14, 48, mx)
+    m.update_many(keys, vals)
+    keep, rec = h.evict(keys, vals, now)
+    got = m.lru_evict(now)
+    assert got == rec
+    K, h0, lines, ev = got
+    ak = age_keys(vals, now)
+    srt = np.sort(ak)
+    assert K == int(srt[(len(srt) + 1) // 2 - 1]) < 2 * BINS - 1      # the whole table's median age
+    assert ev <= (ak <= K).sum() and m.count() == len(keys) - ev <= mx
+    assert m.count() >= len(keys) - (ak <= K).sum() >= len(keys) // 3
