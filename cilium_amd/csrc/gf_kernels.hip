@@ -2699,15 +2699,18 @@ struct LruSlot {
     static constexpr uint32_t SZ = KIND == 2 ? 64u : 32u, SPL = 128u / SZ, KW = KIND == 2 ? 10 : 4;
     uint32_t kw[KW];
     uint32_t st = GF_SLOT_EMPTY, lt = 0, fl = 0;
+    // nontemporal loads: the eviction passes stream GBs of slots per call, which must
+    // not push the policy maps and hot CT lines of the next launch out of L2 / MALL
+    __device__ __forceinline__ static uint4 ld(const uint8_t *p) { return gload_nt16(p); }
     __device__ __forceinline__ void load(const gf_htab_desc &d, uint64_t i) {
         const uint8_t *p = d.slots + i * SZ;
         if constexpr (KIND == 2) {
-            const uint4 a = gload<uint4>(p), b = gload<uint4>(p + 16), c = gload<uint4>(p + 32), e = gload<uint4>(p + 48);
+            const uint4 a = ld(p), b = ld(p + 16), c = ld(p + 32), e = ld(p + 48);
             kw[0] = a.x; kw[1] = a.y; kw[2] = a.z; kw[3] = a.w; kw[4] = b.x; kw[5] = b.y; kw[6] = b.z; kw[7] = b.w;
             kw[8] = c.x; kw[9] = c.y;
             st = c.z & 0xffu; lt = e.x; fl = e.y & 0xffffu;
         } else {
-            const uint4 a = gload<uint4>(p), b = gload<uint4>(p + 16);
+            const uint4 a = ld(p), b = ld(p + 16);
             kw[0] = a.x; kw[1] = a.y; kw[2] = a.z; kw[3] = a.w & 0xffffu;
             st = (a.w >> 16) & 0xffu; lt = b.x; fl = b.y & 0xffffu;
         }
@@ -2825,15 +2828,13 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
         if (win[k]) atomicAdd(&L->hist[(k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN], win[k]);
 }
 // K and es from the sample's histogram, the count the call starts from, and the
-// histogram cleared for the next call.  One block: wave w sums bins [w * 8192,
-// (w + 1) * 8192) in 128 coalesced groups of 64 (group sums to LDS), a block scan
-// over the 2048 group sums finds the median's group, one wave finds its bin.
+// histogram cleared for the next call (one block).
 // wide = 0: the window's sample; an empty one (sl < nl) sets L->wide for the
 // whole-table sample and its plan (wide = 1) instead of planning.
 __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
                                                    uint64_t nl, uint32_t wide) {
     const uint32_t c = *count;
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t t = threadIdx.x;
     if (wide) {
         if (!L->wide) return;
         sl = nl;
@@ -2841,24 +2842,26 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         if (t == 0) L->flag = 0u;
         return;
     }
-    constexpr uint32_t NB = 2 * GF_LRU_BINS, PW = NB / 16, IT = PW / 64, NG = NB / 64;
-    __shared__ uint32_t gs[NG];                         // group sums (< 2^32: a sample's entries)
+    // thread t owns bins [t * 128, t * 128 + 128): 32 16-B loads, eight in flight at a
+    // time, then a block scan of the 1024 sums; the median's thread re-reads its bins
+    constexpr uint32_t NB = 2 * GF_LRU_BINS, PER = NB / 1024, V = PER / 4;
     __shared__ unsigned long long part[1024];
-    __shared__ uint32_t s_g, s_k;
-    __shared__ unsigned long long s_before, s_es;
-    const uint32_t *hp = L->hist + (size_t)w * PW;
-#pragma unroll 16
-    for (uint32_t it = 0; it < IT; it++) {
-        uint32_t v = hp[it * 64 + lane];
+    __shared__ uint32_t s_k;
+    __shared__ unsigned long long s_es;
+    const uint4 *hv = reinterpret_cast<const uint4 *>(L->hist) + (size_t)t * V;
+    uint32_t sum = 0;
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) gs[w * IT + it] = v;
+    for (uint32_t k = 0; k < V; k += 8) {
+        uint4 a[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) a[j] = hv[k + j];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) sum += a[j].x + a[j].y + a[j].z + a[j].w;
     }
-    if (t == 0) { s_g = ~0u; s_k = NB - 1; s_es = 0; s_before = 0; }
+    if (t == 0) { s_k = NB - 1; s_es = 0; }
+    part[t] = sum;
     __syncthreads();
-    part[t] = (unsigned long long)gs[2 * t] + gs[2 * t + 1];
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan of the pair sums
+    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan
         const unsigned long long v = t >= o ? part[t - o] : 0ull;
         __syncthreads();
         part[t] += v;
@@ -2869,26 +2872,22 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         if (t == 0) { L->wide = 1u; L->flag = 0u; }
         return;
     }
-    if (total && before < need && part[t] >= need) {    // the median lies in groups 2t, 2t + 1
-        const bool first = before + gs[2 * t] >= need;
-        s_g = first ? 2 * t : 2 * t + 1;
-        s_before = first ? before : before + gs[2 * t];
-    }
-    __syncthreads();
-    if (w == 0 && s_g != ~0u) {                          // the median group's bins, one per lane
-        const uint32_t v = L->hist[(size_t)s_g * 64 + lane];
-        uint32_t inc = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(inc, o);
-            if (lane >= (uint32_t)o) inc += u;
+    if (total && before < need && part[t] >= need) {    // the median bin lies in this thread's range
+        unsigned long long acc = before;
+        for (uint32_t k = 0; k < V; k++) {
+            const uint4 a = hv[k];
+            const uint32_t c4[4] = {a.x, a.y, a.z, a.w};
+            bool done = false;
+            for (uint32_t j = 0; j < 4; j++) {
+                acc += c4[j];
+                if (acc >= need) { s_k = t * PER + 4 * k + j; s_es = acc; done = true; break; }
+            }
+            if (done) break;
         }
-        const unsigned long long acc = s_before + inc;
-        const uint64_t hit = __ballot(acc >= need);
-        if (lane == (uint32_t)__ffsll((unsigned long long)hit) - 1u) { s_k = s_g * 64 + lane; s_es = acc; }
     }
     __syncthreads();
-    for (uint32_t k = t; k < NB; k += 1024) L->hist[k] = 0;   // clear for the next call's sample
+    uint4 *hw4 = reinterpret_cast<uint4 *>(L->hist);
+    for (uint32_t k = t; k < NB / 4; k += 1024) hw4[k] = make_uint4(0u, 0u, 0u, 0u);   // clear for the next sample
     if (t == 0) {
         L->K = s_k; L->es = s_es; L->cnt0 = c; L->sl = sl; L->wide = 0u; L->flag = 1u; L->cleared = 0;
         for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) L->kills[r] = 0;

@@ -1,5 +1,6 @@
 """Per-event account of the LRU stand-in's launch chains in a rocprofv3 kernel
-trace (tools/gpu.sh trace:...): one chain = k_lru_sample .. k_lru_round_end.
+trace (tools/gpu.sh trace:...): one chain = the first k_lru_sample .. k_lru_end
+(k_lru_round_end in round-5 traces).
 
     python tools/lru_chains.py gpurun_out/TAG/trace_NAME/run_kernel_trace.csv [--active-us 100]
 
@@ -24,12 +25,12 @@ def main():
     chains, cur = [], None
     for r in rows:
         n = name(r["Kernel_Name"])
-        if n.startswith("k_lru_sample"):
+        if n.startswith("k_lru_sample") and cur is None:
             cur = []
             chains.append(cur)
         if cur is not None and n.startswith("k_lru"):
             cur.append((n, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
-        if n.startswith("k_lru_round_end"):
+        if n.startswith("k_lru_round_end") or n.startswith("k_lru_end"):
             cur = None
     tot = lambda c: sum(d for _, d in c)
     act = [c for c in chains if tot(c) > a.active_us]
@@ -39,6 +40,8 @@ def main():
         print(f"  {tot(c) / 1e3:.3f} ms: " + " ".join(f"{n.replace('k_lru_', '')}={d / 1e3:.3f}" for n, d in c))
     if idle:
         print(f"  no-op chains: {len(idle)}, mean {sum(idle) / len(idle):.1f} us")
+    if act:
+        print(f"  longest evicting chain {max(map(tot, act)) / 1e3:.3f} ms, mean {sum(map(tot, act)) / len(act) / 1e3:.3f} ms")
 
 
 if __name__ == "__main__":
