@@ -361,3 +361,40 @@ def test_binding_a_large_ct_map_keeps_it_off_the_host():
     grown = _rss_gb() - before
     assert grown < 1.0, f"host memory grew by {grown:.2f} GB"
     assert bpf.GetMapInfo(dp.fd["ct4"]).Entries == ref.m["ct4"].count()
+
+
+def test_lru_empty_sample_window_falls_back_to_whole_table():
+    """keys chosen so that none is homed in the sample window (the SL lines
+    ahead of the hand, the CT hash being public) on a table large enough to be sampled
+    (NL > 65,536 lines).  The device finds the window empty, samples the whole table
+    instead (k_lru_sample / k_lru_plan, wide) and evicts from its older half — never a
+    flush — exactly as the oracle's restatement: the same eviction log, the same table."""
+    import test_lru_hand as TH
+    mx = 40_000
+    rng = np.random.default_rng(21)
+    sc = synth.fuzz(seed=12, n_packets=2000, n_batches=1, ct_max=mx, ct6_max=400)
+    h = TH.Hand(14, mx)
+    assert h.nl > 65536 and h.sl < h.nl
+    now = sc.now
+    keys, vals = TH._table(rng, 14, 3 * mx, now)
+    out = h.home_lines(keys) >= h.sl                 # the hand stands at line 0: nothing homed in [0, SL)
+    keys, vals = keys[out][: mx + 3000], vals[out][: mx + 3000]
+    assert len(keys) == mx + 3000
+    ct = sc.maps["ct4"]
+    ct.keys, ct.vals = keys, vals
+    pk = sc.batches[0]
+    pk.frames[:, 12], pk.frames[:, 13] = 0x88, 0xB5  # an unknown ethertype: no packet reaches conntrack
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    io = dp.ingress(DeviceBatch(pk), now)
+    torch.cuda.synchronize()
+    _cmp(to_numpy(io, ING_OUT), ref.ingress(pk, now), "ingress")
+    log = _evict_log(dp.fd["ct4"])
+    assert log == ref.lru_log["ct4"] and len(log) == 1, (log, ref.lru_log["ct4"])
+    K, evicted = log[0][2], log[0][5]
+    ak = TH.age_keys(vals, now)
+    srt = np.sort(ak)
+    assert K == int(srt[(len(srt) + 1) // 2 - 1])     # the whole table's median age
+    n_after = bpf.GetMapInfo(dp.fd["ct4"]).Entries
+    assert n_after == ref.m["ct4"].count() == len(keys) - evicted <= mx
+    assert evicted <= (ak <= K).sum() and n_after >= len(keys) // 3
+    assert dp.dump_map("ct4") == ref.dump("ct4")

@@ -9,7 +9,7 @@
 # GPU.  Output goes to gpurun_out/TAG/.  A STEP is one word, its arguments
 # separated by ':' (bench arguments by ',', e.g. bench:c2:--no-cpu,--steps,8):
 #
-#   tests[:EXPR]            pytest -m gpu [-k EXPR]                      -> tests.txt
+#   tests[:EXPR]            pytest -m gpu [-k EXPR] ('+' for spaces)     -> tests.txt
 #   smoke                   __graft_entry__.smoke()                      -> smoke.txt
 #   bench:NAME[:ARGS]       python bench.py ARGS                         -> NAME.json, NAME.err
 #   vbench:VAR:NAME[:ARGS]  bench.py on the variant library VAR (tools/variant.sh build VAR ...):
@@ -73,7 +73,7 @@ for S in "$@"; do
   IFS=: read -r op a1 a2 a3 <<< "$S"
   case $op in
     tests)
-      K=(); [ -n "$a1" ] && K=(-k "$a1")
+      K=(); [ -n "$a1" ] && K=(-k "${a1//+/ }")        # '+' separates words: tests:lru+or+evict
       timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
           > "$O/tests.txt" 2>&1
       tail -1 "$O/tests.txt" ;;
