@@ -2085,28 +2085,28 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_order(uint32_t n, const uint32
 // Single-packet buckets in packet-index order (GF_SINGLE_ORDER, the egress passes,
 // whose connection groups are mostly one packet a step): the tail of each family's
 // list (bin c = 1) is filled by packet index, so a wave's lanes read neighbouring
-// records, frames and output rows instead of 64 random ones.  k_single_mark flags
-// each such packet (1 + family) and keeps its bucket start; k_single_count /
-// k_run_scan / k_single_write rank them per family in index order.
+// records, frames and output rows instead of 64 random ones.  k_single_mark writes
+// each such packet's word sw[i] = (bucket start + 1) << 1 | family (one 4-B store;
+// 0 = not a single-packet bucket); k_single_count / k_run_scan / k_single_write
+// rank them per family in index order.
 __global__ __launch_bounds__(BLOCK) void k_single_mark(uint32_t n, const uint32_t *off, const uint32_t *skeys,
-                                                       const uint32_t *perm, const uint32_t *sched, uint8_t *sflag,
-                                                       uint32_t *sb) {
+                                                       const uint32_t *perm, const uint32_t *sched, uint32_t *sw) {
     const uint32_t nq = *GF_SCHED_NRUNS(sched);
     for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < nq; q += gridDim.x * BLOCK) {
         const uint32_t b = off[q], key = skeys[b];
         if ((q + 1 < nq ? off[q + 1] : n) - b != 1u || key == GF_KEY_SKIP) continue;
-        const uint32_t i = perm[b];
-        sflag[i] = (uint8_t)(1u + (key >> (GF_KEY_BITS - 1)));
-        sb[i] = b;
+        sw[perm[b]] = ((b + 1u) << 1) | (key >> (GF_KEY_BITS - 1));
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_single_count(uint32_t n, const uint8_t *sflag, uint32_t *t0, uint32_t *t1) {
+// the family of a packet's single-bucket word: 1 / 2, 0 = none
+__device__ __forceinline__ uint32_t single_fam(uint32_t w) { return w ? 1u + (w & 1u) : 0u; }
+__global__ __launch_bounds__(BLOCK) void k_single_count(uint32_t n, const uint32_t *sw, uint32_t *t0, uint32_t *t1) {
     __shared__ uint32_t wc[2][BLOCK / 64];
     const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u;
     uint32_t c0 = 0, c1 = 0;
     for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
         const uint32_t j = b0 + k * BLOCK + threadIdx.x;
-        const uint32_t f = j < n ? sflag[j] : 0u;
+        const uint32_t f = j < n ? single_fam(sw[j]) : 0u;
         c0 += (uint32_t)__popcll(__ballot(f == 1u));
         c1 += (uint32_t)__popcll(__ballot(f == 2u));
     }
@@ -2118,27 +2118,26 @@ __global__ __launch_bounds__(BLOCK) void k_single_count(uint32_t n, const uint8_
         t0[blockIdx.x] = a; t1[blockIdx.x] = z;
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_single_write(uint32_t n, const uint8_t *sflag, const uint32_t *sb,
-                                                        const uint32_t *t0, const uint32_t *t1, const uint32_t *sched,
-                                                        uint2 *order) {
+__global__ __launch_bounds__(BLOCK) void k_single_write(uint32_t n, const uint32_t *sw, const uint32_t *t0,
+                                                        const uint32_t *t1, const uint32_t *sched, uint2 *order) {
     __shared__ uint32_t wc[2][BLOCK / 64];
     const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t *base = GF_SCHED_BASE(sched);         // bin c = 1 of family f's list (GF_NCLS == 1)
     uint32_t p0 = base[0 * (GF_LCAP + 1) + 1] + t0[blockIdx.x], p1 = base[1 * (GF_LCAP + 1) + 1] + t1[blockIdx.x];
     for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
         const uint32_t j = b0 + k * BLOCK + threadIdx.x;
-        const uint32_t f = j < n ? sflag[j] : 0u;
+        const uint32_t w = j < n ? sw[j] : 0u, f = single_fam(w);
         const uint64_t m0 = __ballot(f == 1u), m1 = __ballot(f == 2u);
         if (lane == 0) { wc[0][wv] = (uint32_t)__popcll(m0); wc[1][wv] = (uint32_t)__popcll(m1); }
         __syncthreads();
         uint32_t e0 = 0, e1 = 0, a0 = 0, a1 = 0;
-        for (uint32_t w = 0; w < BLOCK / 64; w++) {
-            e0 += w < wv ? wc[0][w] : 0u; e1 += w < wv ? wc[1][w] : 0u;
-            a0 += wc[0][w]; a1 += wc[1][w];
+        for (uint32_t q = 0; q < BLOCK / 64; q++) {
+            e0 += q < wv ? wc[0][q] : 0u; e1 += q < wv ? wc[1][q] : 0u;
+            a0 += wc[0][q]; a1 += wc[1][q];
         }
         const uint64_t below = (1ull << lane) - 1ull;
-        if (f == 1u) order[p0 + e0 + (uint32_t)__popcll(m0 & below)] = make_uint2(sb[j], 1u);
-        if (f == 2u) order[p1 + e1 + (uint32_t)__popcll(m1 & below)] = make_uint2(sb[j], 1u);
+        if (f == 1u) order[p0 + e0 + (uint32_t)__popcll(m0 & below)] = make_uint2((w >> 1) - 1u, 1u);
+        if (f == 2u) order[p1 + e1 + (uint32_t)__popcll(m1 & below)] = make_uint2((w >> 1) - 1u, 1u);
         p0 += a0; p1 += a1;
         __syncthreads();
     }
@@ -4681,7 +4680,7 @@ void prof_drain() {
 
 struct Workspace {
     DevBuf rec, keys, skeys, perm, tcnt, off, tmp, sched, order;
-    DevBuf sflag, sb, st0, st1;        // single-packet buckets in index order (GF_SINGLE_ORDER)
+    DevBuf sb, st0, st1;               // single-packet buckets in index order (GF_SINGLE_ORDER)
 };
 // GF_HOST_PROF (diagnosis): the host time of a classify call's phases, one line
 // per call on stderr (where a call waits on the device, or spends its launches).
@@ -5222,13 +5221,17 @@ using GfSortCfg = rocprim::radix_sort_config<
 // count the starts per tile, scan the tile counts (one block), write each
 // tile's starts at its offset in position order (wave ballots + LDS scan).
 __device__ __forceinline__ bool run_start(const uint32_t *k, uint32_t j) { return j == 0 || k[j] != k[j - 1]; }
-__global__ __launch_bounds__(BLOCK) void k_run_count(uint32_t n, const uint32_t *skeys, uint32_t *tcnt) {
+// zero: n words to clear on the way (the single-bucket words of an egress schedule,
+// k_single_mark: one launch fewer than a fill of their own), or null
+__global__ __launch_bounds__(BLOCK) void k_run_count(uint32_t n, const uint32_t *skeys, uint32_t *tcnt,
+                                                     uint32_t *zero = nullptr) {
     __shared__ uint32_t wc[BLOCK / 64];
     const uint32_t b0 = blockIdx.x * GF_RUN_ITEMS, lane = threadIdx.x & 63u;
     uint32_t c = 0;
     for (uint32_t k = 0; k < GF_RUN_ITEMS / BLOCK; k++) {
         const uint32_t j = b0 + k * BLOCK + threadIdx.x;
         c += (uint32_t)__popcll(__ballot(j < n && run_start(skeys, j)));
+        if (zero && j < n) zero[j] = 0u;
     }
     if (lane == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -5297,6 +5300,10 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
                                                GF_KEY_BITS, s);
     const uint32_t nt = (n + GF_RUN_ITEMS - 1) / GF_RUN_ITEMS;
     if ((r = grow(w.tmp, sort_bytes + 256)) || (r = grow(w.tcnt, (size_t)nt * 4 + 16))) return r;
+    single = single && GF_SINGLE_ORDER && GF_NCLS == 1;
+    if (single && ((r = grow(w.sb, (size_t)n * 4)) || (r = grow(w.st0, (size_t)nt * 4 + 16)) ||
+                   (r = grow(w.st1, (size_t)nt * 4 + 16))))
+        return r;
     size_t tb = w.tmp.bytes;
     {
         ProfScope ps("rocprim_radix_sort", s);
@@ -5308,7 +5315,7 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
     {
         ProfScope ps("bucket_runs", s);
         if (nt) hipLaunchKernelGGL(k_run_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
-                                   (uint32_t *)w.tcnt.p);
+                                   (uint32_t *)w.tcnt.p, single ? (uint32_t *)w.sb.p : nullptr);
         hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.tcnt.p, d_nruns,
                            GF_SCHED_HIST(d_sched), GF_SCHED_HBYTES / 4u);   // (+ the bucket histogram cleared)
         if (nt) hipLaunchKernelGGL(k_run_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.skeys.p,
@@ -5329,30 +5336,22 @@ static int schedule_groups(uint32_t n, hipStream_t s, const gf_rec *rec = nullpt
         hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
                            (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched);
         hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(GF_LCAP), 0, s, d_sched);
-        single = single && GF_SINGLE_ORDER && GF_NCLS == 1;
         hipLaunchKernelGGL(k_bucket_order, dim3(g), dim3(BLOCK), GF_SCHED_HBYTES, s, n, (const uint32_t *)w.off.p,
                            (const uint32_t *)w.skeys.p, lrec, (const uint32_t *)w.perm.p, d_sched, (uint2 *)w.order.p,
                            single ? 1u : 0u);
-        if (single) {
-            auto grow = [](DevBuf &b, size_t want) -> int { return b.bytes >= want ? 0 : b.ensure(want); };
-            const uint32_t nt = (n + GF_RUN_ITEMS - 1) / GF_RUN_ITEMS;
-            int r2;
-            if ((r2 = grow(w.sflag, n)) || (r2 = grow(w.sb, (size_t)n * 4)) || (r2 = grow(w.st0, (size_t)nt * 4 + 16)) ||
-                (r2 = grow(w.st1, (size_t)nt * 4 + 16)))
-                return r2;
-            if (hip_ok(hipMemsetAsync(w.sflag.p, 0, n, s), "single flags")) return -EIO;
+        if (single) {                                   // (the words were cleared by k_run_count)
             hipLaunchKernelGGL(k_single_mark, dim3(std::min<uint32_t>((n + BLOCK - 1) / BLOCK, 8192u)), dim3(BLOCK), 0, s, n,
                                (const uint32_t *)w.off.p, (const uint32_t *)w.skeys.p, (const uint32_t *)w.perm.p,
-                               (const uint32_t *)d_sched, (uint8_t *)w.sflag.p, (uint32_t *)w.sb.p);
-            hipLaunchKernelGGL(k_single_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
+                               (const uint32_t *)d_sched, (uint32_t *)w.sb.p);
+            hipLaunchKernelGGL(k_single_count, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.sb.p,
                                (uint32_t *)w.st0.p, (uint32_t *)w.st1.p);
             hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st0.p, (uint32_t *)w.st0.p + nt,
                                nullptr, 0u);
             hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(1024), 0, s, nt, (uint32_t *)w.st1.p, (uint32_t *)w.st1.p + nt,
                                nullptr, 0u);
-            hipLaunchKernelGGL(k_single_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint8_t *)w.sflag.p,
-                               (const uint32_t *)w.sb.p, (const uint32_t *)w.st0.p, (const uint32_t *)w.st1.p,
-                               (const uint32_t *)d_sched, (uint2 *)w.order.p);
+            hipLaunchKernelGGL(k_single_write, dim3(nt), dim3(BLOCK), 0, s, n, (const uint32_t *)w.sb.p,
+                               (const uint32_t *)w.st0.p, (const uint32_t *)w.st1.p, (const uint32_t *)d_sched,
+                               (uint2 *)w.order.p);
         }
     }
     return hip_ok(hipGetLastError(), "k_bucket_sched");
