@@ -1505,6 +1505,8 @@ def main():
                "cpu_baseline": r["cpu_baseline"], "parity": r.get("parity")}
         if "h2d" in r:
             res["h2d"] = r["h2d"]
+        if "note" in r:
+            res["note"] = r["note"]
     hwm = peak_rss_gb()
     if hwm is not None:
         log(f"rank {rank}: peak host memory {hwm:.1f} GB")

@@ -4582,22 +4582,19 @@ __device__ __forceinline__ bool ctlog_same(const uint32_t *a, const uint32_t *b)
     return a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && (a[4] & 0xffffu) == (b[4] & 0xffffu);
 }
 // The set is sized for the entries actually logged (<= 1/2 load; the count is on
-// the device) inside an allocation made for the call's upper bound: k_ctlog_size
-// writes the mask, k_ctlog_clear clears only that part.
-__global__ void k_ctlog_size(const uint32_t *n_, uint32_t cap_mask, uint32_t *tm) {
-    const uint64_t want = GF_EG_LEAN ? 2ull * *n_ : (uint64_t)cap_mask + 1;
+// the device) inside an allocation made for the call's upper bound: both kernels
+// derive the mask from the count themselves, and k_ctlog_apply leaves every slot it
+// walks zero again — the set is all zero between applies (zeroed once when it is
+// allocated), so no launch of its own clears it.
+__device__ __forceinline__ uint32_t ctlog_mask(uint32_t n, uint32_t cap_mask) {
+    const uint64_t want = GF_EG_LEAN ? 2ull * n : (uint64_t)cap_mask + 1;
     uint32_t t = 1023u;
     while ((uint64_t)t + 1 < want && t < cap_mask) t = t * 2 + 1;
-    *tm = t < cap_mask ? t : cap_mask;
-}
-__global__ __launch_bounds__(BLOCK) void k_ctlog_clear(unsigned long long *tab, const uint32_t *tm) {
-    const uint64_t m = *tm;
-    for (uint64_t k = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; k <= m; k += (uint64_t)gridDim.x * BLOCK)
-        tab[k] = 0ull;
+    return t < cap_mask ? t : cap_mask;
 }
 __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, unsigned long long *tab,
-                                                     const uint32_t *tm) {
-    const uint32_t n = *n_, tmask = *tm;
+                                                     uint32_t cap_mask) {
+    const uint32_t n = *n_, tmask = ctlog_mask(n, cap_mask);
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
@@ -4616,13 +4613,14 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const u
         }
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const unsigned long long *tab,
-                                                       const uint32_t *tm, gf_htab_desc ct, uint32_t *ct_count) {
-    const uint32_t tmask = *tm;
+__global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, unsigned long long *tab,
+                                                       uint32_t cap_mask, gf_htab_desc ct, uint32_t *ct_count) {
+    const uint32_t tmask = ctlog_mask(*n_, cap_mask);
     int added = 0;
     for (uint64_t p = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; p <= tmask; p += (uint64_t)gridDim.x * BLOCK) {
         const unsigned long long t = tab[p];
         if (t == 0ull) continue;                        // an empty slot
+        tab[p] = 0ull;                                  // the set is clean for its next use
         const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * (uint32_t)t;   // the key's last entry in order
         ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
     }
@@ -6433,7 +6431,7 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 
 // ---- endpoint egress (from-container) ----
 namespace {
-struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, ctm, s6, d6,
+struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
              hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n, v6blk;
              uint32_t hz_gen = 0, hz_cap = 0;
              uint32_t *h_hz = nullptr;          // pinned: the ordering check's words, read back without a stream sync
@@ -6535,18 +6533,15 @@ static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32
     uint32_t cap = 1023;                               // the set for the bound, at <= 1/2 load
     while ((uint64_t)cap + 1 < 2ull * nlog) cap = cap * 2 + 1;
     const size_t tb = (size_t)(cap + 1) * 8;
-    if (ew.ckey.bytes < tb && ew.ckey.ensure(tb)) return -ENOMEM;
-    if (ew.ctm.bytes < 4 && ew.ctm.ensure(4)) return -ENOMEM;
+    if (ew.ckey.bytes < tb) {                           // a new set: zero once (k_ctlog_apply keeps it zero)
+        if (ew.ckey.ensure(tb)) return -ENOMEM;
+        if (hip_ok(hipMemsetAsync(ew.ckey.p, 0, tb, s), "ct log set")) return -EIO;
+    }
     ProfScope ps("k_ctlog_apply", s);
-    uint32_t *tm = (uint32_t *)ew.ctm.p;
-    hipLaunchKernelGGL(k_ctlog_size, dim3(1), dim3(1), 0, s, d_n, cap, tm);
     const uint32_t gs = std::min<uint32_t>((cap + BLOCK) / BLOCK, 2048u);   // grid-stride over the set
-    hipLaunchKernelGGL(k_ctlog_clear, dim3(gs), dim3(BLOCK), 0, s, (unsigned long long *)ew.ckey.p, (const uint32_t *)tm);
     const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p,
-                       (const uint32_t *)tm);
-    hipLaunchKernelGGL(k_ctlog_apply, dim3(gs), dim3(BLOCK), 0, s, lg, (const unsigned long long *)ew.ckey.p,
-                       (const uint32_t *)tm, ct,
+    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap);
+    hipLaunchKernelGGL(k_ctlog_apply, dim3(gs), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap, ct,
                        ct_count);
     return hip_ok(hipGetLastError(), "k_ctlog_apply");
 }
