@@ -2623,6 +2623,9 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 // way.  Key bytes of the cleared slots are zeroed.  Every eviction is logged
 // (gf_ct_evict_log: batch number, now, K, the hand's first line, lines passed,
 // entries deleted).
+#ifndef GF_LRU_NT
+#define GF_LRU_NT 1         // the eviction passes' slot loads nontemporal (config 2 continuation k_ing_groups 2.56 -> 2.45 ms)
+#endif
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
 #define GF_LRU_SAMPLE_SHIFT 8
@@ -2631,8 +2634,10 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 #define GF_LRU_HT 256u                  // k_lru_hand block
 #define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (CT6; CT4 twice that)
 struct LruLog { uint32_t seq, now, age_cut, pad; unsigned long long hand, lines, evicted; };
+#define GF_LRU_GROUPS (2u * GF_LRU_BINS / 64u)
 struct LruDev {
     uint32_t hist[2 * GF_LRU_BINS];     // the sample's age histogram
+    uint32_t coarse[GF_LRU_GROUPS];     // its sums per group of 64 bins (k_lru_plan reads these first)
     GcCut cut;                          // gf_ct_gc (k_gc_*)
     unsigned long long res[2];          // gf_ct_gc: entries deleted, tombstones cleared
     uint32_t flag;                      // this call evicts (count > HW)
@@ -2700,7 +2705,7 @@ struct LruSlot {
     uint32_t st = GF_SLOT_EMPTY, lt = 0, fl = 0;
     // nontemporal loads: the eviction passes stream GBs of slots per call, which must
     // not push the policy maps and hot CT lines of the next launch out of L2 / MALL
-    __device__ __forceinline__ static uint4 ld(const uint8_t *p) { return gload_nt16(p); }
+    __device__ __forceinline__ static uint4 ld(const uint8_t *p) { return GF_LRU_NT ? gload_nt16(p) : gload<uint4>(p); }
     __device__ __forceinline__ void load(const gf_htab_desc &d, uint64_t i) {
         const uint8_t *p = d.slots + i * SZ;
         if constexpr (KIND == 2) {
@@ -2747,6 +2752,11 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
 #define GF_LRU_LDS 2048u
 #define GF_LRU_WIN 4096u
 #define GF_LRU_HB 1024u                 // k_lru_sample block: 16 waves share the LDS bins
+// One histogram add, mirrored into its group's sum.
+__device__ __forceinline__ void lru_hist_put(LruDev *L, uint32_t bin, uint32_t c) {
+    atomicAdd(&L->hist[bin], c);
+    atomicAdd(&L->coarse[bin >> 6], c);
+}
 // key: the entry's age key, ~0u for none.  Wave-uniform call.
 __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line, uint32_t *win, uint32_t key) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -2766,7 +2776,7 @@ __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line
                 const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
                 const unsigned long long seen = atomicCAS(&line[h], cur, want);
                 if (seen == cur) {
-                    if (ck != k && ck != ~0u && (uint32_t)cur) atomicAdd(&L->hist[ck], (uint32_t)cur);
+                    if (ck != k && ck != ~0u && (uint32_t)cur) lru_hist_put(L, ck, (uint32_t)cur);
                     break;
                 }
                 cur = seen;
@@ -2821,10 +2831,10 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
         const unsigned long long v = line[k];
-        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) atomicAdd(&L->hist[(uint32_t)(v >> 32)], (uint32_t)v);
+        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) lru_hist_put(L, (uint32_t)(v >> 32), (uint32_t)v);
     }
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
-        if (win[k]) atomicAdd(&L->hist[(k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN], win[k]);
+        if (win[k]) lru_hist_put(L, (k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN, win[k]);
 }
 // K and es from the sample's histogram, the count the call starts from, and the
 // histogram cleared for the next call (one block).
@@ -2841,29 +2851,28 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         if (t == 0) L->flag = 0u;
         return;
     }
-    // thread t owns bins [t * 128, t * 128 + 128): 32 16-B loads, eight in flight at a
-    // time, then a block scan of the 1024 sums; the median's thread re-reads its bins
-    constexpr uint32_t NB = 2 * GF_LRU_BINS, PER = NB / 1024, V = PER / 4;
+    // the 2048 group sums (two per thread), a block scan, then one wave finds the
+    // median's bin among its group's 64; only the groups that hold entries are cleared
+    constexpr uint32_t NB = 2 * GF_LRU_BINS;
     __shared__ unsigned long long part[1024];
-    __shared__ uint32_t s_k;
-    __shared__ unsigned long long s_es;
-    const uint4 *hv = reinterpret_cast<const uint4 *>(L->hist) + (size_t)t * V;
-    uint32_t sum = 0;
+    __shared__ uint32_t s_k, s_g;
+    __shared__ unsigned long long s_es, s_before;
+    const uint32_t g0 = L->coarse[2 * t], g1 = L->coarse[2 * t + 1];
+    if (t == 0) { s_k = NB - 1; s_es = 0; s_g = ~0u; s_before = 0; }
+    {                                                   // inclusive scan: in each wave, then over the 16 waves
+        const uint32_t lane = t & 63u, wv = t >> 6;
+        unsigned long long v = (unsigned long long)g0 + g1;
 #pragma unroll
-    for (uint32_t k = 0; k < V; k += 8) {
-        uint4 a[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) a[j] = hv[k + j];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) sum += a[j].x + a[j].y + a[j].z + a[j].w;
-    }
-    if (t == 0) { s_k = NB - 1; s_es = 0; }
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {           // inclusive scan
-        const unsigned long long v = t >= o ? part[t - o] : 0ull;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(v, o);
+            if (lane >= (uint32_t)o) v += u;
+        }
+        __shared__ unsigned long long wsum[16];
+        if (lane == 63) wsum[wv] = v;
         __syncthreads();
-        part[t] += v;
+        unsigned long long off = 0;
+        for (uint32_t q = 0; q < wv; q++) off += wsum[q];
+        part[t] = v + off;
         __syncthreads();
     }
     const unsigned long long total = part[1023], need = (total + 1) / 2, before = t ? part[t - 1] : 0ull;
@@ -2871,22 +2880,33 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         if (t == 0) { L->wide = 1u; L->flag = 0u; }
         return;
     }
-    if (total && before < need && part[t] >= need) {    // the median bin lies in this thread's range
-        unsigned long long acc = before;
-        for (uint32_t k = 0; k < V; k++) {
-            const uint4 a = hv[k];
-            const uint32_t c4[4] = {a.x, a.y, a.z, a.w};
-            bool done = false;
-            for (uint32_t j = 0; j < 4; j++) {
-                acc += c4[j];
-                if (acc >= need) { s_k = t * PER + 4 * k + j; s_es = acc; done = true; break; }
-            }
-            if (done) break;
-        }
+    if (total && before < need && part[t] >= need) {    // the median lies in group 2t or 2t + 1
+        const bool first = before + g0 >= need;
+        s_g = first ? 2 * t : 2 * t + 1;
+        s_before = first ? before : before + g0;
     }
     __syncthreads();
-    uint4 *hw4 = reinterpret_cast<uint4 *>(L->hist);
-    for (uint32_t k = t; k < NB / 4; k += 1024) hw4[k] = make_uint4(0u, 0u, 0u, 0u);   // clear for the next sample
+    if (t < 64 && s_g != ~0u) {                          // wave 0: the median group's bins, one per lane
+        const uint32_t v = L->hist[s_g * 64u + t];
+        uint32_t inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o);
+            if (t >= (uint32_t)o) inc += u;
+        }
+        const uint64_t hit = __ballot(s_before + inc >= need);
+        if (t == (uint32_t)__ffsll((unsigned long long)hit) - 1u) { s_k = s_g * 64u + t; s_es = s_before + inc; }
+    }
+    __syncthreads();
+    // clear for the next sample: the bins of the groups that hold entries, and the sums
+    for (uint32_t q = 0; q < 2; q++) {
+        const uint32_t g = 2 * t + q;
+        if (!(q ? g1 : g0)) continue;
+        uint4 *hb = reinterpret_cast<uint4 *>(L->hist + g * 64u);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) hb[k] = make_uint4(0u, 0u, 0u, 0u);
+        L->coarse[g] = 0u;
+    }
     if (t == 0) {
         L->K = s_k; L->es = s_es; L->cnt0 = c; L->sl = sl; L->wide = 0u; L->flag = 1u; L->cleared = 0;
         for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) L->kills[r] = 0;
