@@ -2624,7 +2624,8 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 // (gf_ct_evict_log: batch number, now, K, the hand's first line, lines passed,
 // entries deleted).
 #ifndef GF_LRU_NT
-#define GF_LRU_NT 1         // the eviction passes' slot loads nontemporal (config 2 continuation k_ing_groups 2.56 -> 2.45 ms)
+#define GF_LRU_NT 0         // the eviction passes' slot loads nontemporal (same-box A/B r6e: the hand 7-12 % slower,
+                            // the next k_ing_groups unchanged: off)
 #endif
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
@@ -2752,13 +2753,16 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
 #define GF_LRU_LDS 2048u
 #define GF_LRU_WIN 4096u
 #define GF_LRU_HB 1024u                 // k_lru_sample block: 16 waves share the LDS bins
-// One histogram add, mirrored into its group's sum.
-__device__ __forceinline__ void lru_hist_put(LruDev *L, uint32_t bin, uint32_t c) {
+// One histogram add; its group's sum goes to the block's LDS copy of the sums
+// (flushed once per block: a sample's entries fall in a few groups, whose global
+// words every block would otherwise hit for each of its bins).
+__device__ __forceinline__ void lru_hist_put(LruDev *L, uint32_t *cg, uint32_t bin, uint32_t c) {
     atomicAdd(&L->hist[bin], c);
-    atomicAdd(&L->coarse[bin >> 6], c);
+    atomicAdd(&cg[bin >> 6], c);
 }
 // key: the entry's age key, ~0u for none.  Wave-uniform call.
-__device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line, uint32_t *win, uint32_t key) {
+__device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line, uint32_t *win, uint32_t *cg,
+                                             uint32_t key) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t kb = key & (GF_LRU_BINS - 1u);
     const bool inwin = key != ~0u && kb >= GF_LRU_BINS - GF_LRU_WIN;
@@ -2776,7 +2780,7 @@ __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line
                 const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
                 const unsigned long long seen = atomicCAS(&line[h], cur, want);
                 if (seen == cur) {
-                    if (ck != k && ck != ~0u && (uint32_t)cur) lru_hist_put(L, ck, (uint32_t)cur);
+                    if (ck != k && ck != ~0u && (uint32_t)cur) lru_hist_put(L, cg, ck, (uint32_t)cur);
                     break;
                 }
                 cur = seen;
@@ -2797,8 +2801,10 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
     if (wide ? !L->wide : (unsigned long long)*d.count <= lru_high_water(max_entries)) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
+    __shared__ uint32_t cg[GF_LRU_GROUPS];             // the block's group sums
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
+    for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x) cg[k] = 0;
     __syncthreads();
     constexpr uint32_t SPL = LruSlot<KIND>::SPL;
     const uint64_t ns = d.mask + 1, nl = ns / SPL;
@@ -2813,7 +2819,7 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
             s.load(d, (P0 + i) & d.mask);
             if (s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
         }
-        lru_hist_add(L, line, win, key);
+        lru_hist_add(L, line, win, cg, key);
     }
     if (blockIdx.x == 0 && threadIdx.x < 64 && n < ns) {
         for (uint64_t q = n;; q += 64) {
@@ -2824,17 +2830,20 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
             const uint32_t stop = em ? (uint32_t)__ffsll((unsigned long long)em) - 1u : 64u;
             uint32_t key = ~0u;
             if (threadIdx.x < stop && s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
-            lru_hist_add(L, line, win, key);
+            lru_hist_add(L, line, win, cg, key);
             if (em || q + 64 >= ns) break;
         }
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
         const unsigned long long v = line[k];
-        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) lru_hist_put(L, (uint32_t)(v >> 32), (uint32_t)v);
+        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) lru_hist_put(L, cg, (uint32_t)(v >> 32), (uint32_t)v);
     }
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
-        if (win[k]) lru_hist_put(L, (k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN, win[k]);
+        if (win[k]) lru_hist_put(L, cg, (k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN, win[k]);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x)
+        if (cg[k]) atomicAdd(&L->coarse[k], cg[k]);
 }
 // K and es from the sample's histogram, the count the call starts from, and the
 // histogram cleared for the next call (one block).
