@@ -2603,7 +2603,7 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 //  * home line of an entry: its key's home slot in this table (gf_home_slot of the
 //    CT hash) / slots per 128-B line; NL lines in all;
 //  * the sample: the entries homed in the SL lines from where the hand stands (SL
-//    = NL when NL <= 65536, else max(65536, NL >> 8)), the lines it passes next.  K = the smallest age key covering half of
+//    = NL when NL <= 65536, else max(65536, NL >> 10)), the lines it passes next.  K = the smallest age key covering half of
 //    the sample (its older half is eligible); es = the sample entries with age key
 //    <= K.  A window that holds no entry (only keys chosen to avoid those lines)
 //    is replaced by the whole table (SL = NL);
@@ -2629,7 +2629,7 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 #endif
 #define GF_LRU_BINS 65536u
 #define GF_LRU_LOGCAP 4096u
-#define GF_LRU_SAMPLE_SHIFT 8
+#define GF_LRU_SAMPLE_SHIFT 10
 #define GF_LRU_SAMPLE_MIN 65536ull
 #define GF_LRU_ROUNDS 3u
 #define GF_LRU_HT 256u                  // k_lru_hand block

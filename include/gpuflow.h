@@ -493,7 +493,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream);
  * of every classify call that uses it, once the count exceeds the high-water mark
  * HW = max_entries - max_entries/8, a hand sweeping the table's home lines deletes
  * the entries of the older half (age key <= age_cut: the median age of a sample —
- * the max(65536, lines/256) home lines just ahead of the hand, or the whole table if
+ * the max(65536, lines/1024) home lines just ahead of the hand, or the whole table if
  * no entry is homed there; closing entries older than all others, then by last use
  * in one-second bins) homed in the lines it passes, as many lines as bring the count
  * back to HW by the sample's density.  A map running at HW so deletes in each call

@@ -1880,7 +1880,7 @@ uint32_t o_ct_gc(om_map *m, uint32_t filter_time) {
 /*    = 128-B line /                                                    */
 /*    slot (4 for ipv4_ct_tuple, 2 for ipv6_ct_tuple); NL = NS / SPL;   */
 /*  * sample = entries homed in [hand, hand + SL) (mod NL), SL =        */
-/*    max(65536, NL >> 8) (NL when NL <= 65536), the lines the hand     */
+/*    max(65536, NL >> 10) (NL when NL <= 65536), the lines the hand    */
 /*    passes next; K = the smallest age key with at least half of the  */
 /*    sample at or below it, es = the sample's entries with age key     */
 /*    <= K; a window holding no entry is replaced by the whole table    */
@@ -1947,7 +1947,7 @@ static lru_geo lru_geometry(const om_map *m) {
     g.ns = ct_slots(m);
     g.spl = m->ksz == 14 ? 4u : 2u;
     g.nl = g.ns / g.spl;
-    g.sl = g.nl <= 65536 ? g.nl : ((g.nl >> 8) > 65536 ? (g.nl >> 8) : 65536);
+    g.sl = g.nl <= 65536 ? g.nl : ((g.nl >> 10) > 65536 ? (g.nl >> 10) : 65536);
     return g;
 }
 static uint64_t lru_home_line(const om_map *m, const lru_geo *g, const uint8_t *key) {

@@ -82,7 +82,7 @@ class Hand:
             self.ns *= 2
         self.spl = 4 if ksz == 14 else 2
         self.nl = self.ns // self.spl
-        self.sl = self.nl if self.nl <= 65536 else max(65536, self.nl >> 8)
+        self.sl = self.nl if self.nl <= 65536 else max(65536, self.nl >> 10)
         self.hw = max_entries - max_entries // 8          # the high-water mark
         self.hand = 0
 
@@ -196,14 +196,14 @@ def test_hand_evicts_the_older_half_only():
 
 
 def test_hand_sampled_table_and_steady_state():
-    """A table large enough to be sampled (NL > 65536 lines: SL = max(65536, NL >> 8)):
+    """A table large enough to be sampled (NL > 65536 lines: SL = max(65536, NL >> 10)):
     once the count has crossed the high-water mark, each batch boundary deletes about
     what the batch inserted — the lines passed follow the inserts, not the table —
     and the count stays at or below max_entries after every call."""
     rng = np.random.default_rng(11)
     now, mx = 60_000, 40_000
     h = Hand(14, mx)
-    assert h.nl > 65536 and h.sl == max(65536, h.nl >> 8) and h.sl < h.nl
+    assert h.nl > 65536 and h.sl == max(65536, h.nl >> 10) and h.sl < h.nl
     m = O.OMap(9, 14, 48, mx)
     keys, vals = _table(rng, 14, h.hw - 500, now)
     m.update_many(keys, vals)
