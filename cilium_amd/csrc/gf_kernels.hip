@@ -5722,11 +5722,21 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
         grid_of[kind] = per_cu * cus;
     }
     {
+        // Two cooperative grids sized to the whole device must never be resident
+        // together (each would wait at its barrier for blocks the other holds): every
+        // chain, from any stream, waits for the previous one to finish.
+        static std::mutex coop_mu;
+        static hipEvent_t coop_last = nullptr;
+        std::lock_guard<std::mutex> cg(coop_mu);
+        if (!coop_last && hip_ok(hipEventCreateWithFlags(&coop_last, hipEventDisableTiming), "lru chain event"))
+            return -EIO;
+        if (hip_ok(hipStreamWaitEvent(s, coop_last, 0), "lru chain order")) return -EIO;
         ProfScope ps("k_lru_evict", s);
         void *args[] = {(void *)&d, (void *)&mode, (void *)&now, (void *)&L, (void *)&nl, (void *)&sl, (void *)&mx,
                         (void *)&seq, (void *)&hc};
         const void *fn = kind == 1 ? (const void *)k_lru_chain<1> : (const void *)k_lru_chain<2>;
-        if (hip_ok(hipLaunchCooperativeKernel(fn, dim3(grid_of[kind]), dim3(GF_LRU_CT), args, 0, s), "k_lru_chain"))
+        if (hip_ok(hipLaunchCooperativeKernel(fn, dim3(grid_of[kind]), dim3(GF_LRU_CT), args, 0, s), "k_lru_chain") ||
+            hip_ok(hipEventRecord(coop_last, s), "lru chain event"))
             return -EIO;
     }
     if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
