@@ -11,7 +11,6 @@
 //   k_ing_tail  the remaining ranks of the few deepest buckets, sequentially
 #include "gf_internal.h"
 #include "gf_device.h"
-#include <hip/hip_cooperative_groups.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
@@ -2633,7 +2632,8 @@ __global__ __launch_bounds__(BLOCK) void k_gc_clusters(gf_htab_desc d, uint32_t 
 #define GF_LRU_SAMPLE_SHIFT 10
 #define GF_LRU_SAMPLE_MIN 65536ull
 #define GF_LRU_ROUNDS 3u
-#define GF_LRU_CHUNK 1024u              // the hand: slots a block decides together (CT6; CT4 twice that)
+#define GF_LRU_HT 256u                  // k_lru_hand block
+#define GF_LRU_CHUNK 1024u              // k_lru_hand: slots a block decides together (CT6; CT4 twice that)
 struct LruLog { uint32_t seq, now, age_cut, pad; unsigned long long hand, lines, evicted; };
 #define GF_LRU_GROUPS (2u * GF_LRU_BINS / 64u)
 struct LruDev {
@@ -2736,14 +2736,10 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
         gstore<uint4>(p, make_uint4(0u, 0u, 0u, st << 16));
     }
 }
-// The eviction after a classify call is one cooperative launch, k_lru_chain: every
-// block reads the count first and the whole grid returns at once unless it exceeds
-// HW (no other launch for the common case); otherwise its phases — the sample, the
-// plan (block 0), the whole-table sample and plan if the window was empty, the hand
-// rounds (even chunks, odd chunks) and the log (block 0) — are separated by grid
-// barriers (cooperative groups: agent-scope release / acquire, so a phase reads what
-// the previous one wrote on any XCD).  The histogram is zero between calls (the plan
-// clears the groups it used; zero at allocation).
+// The chain after a classify call: k_lru_sample, k_lru_plan, k_lru_hand x 2 per
+// round (GF_LRU_ROUNDS), k_lru_end.  Each launch exits at once unless the count
+// exceeds HW (and a round's, unless the round passes lines).  The histogram is zero
+// between calls (cleared by k_lru_plan after its scan; zero at allocation).
 // Age histogram of the sample: wave-aggregated (a wave's entries mostly share a
 // bin), then counted per block in LDS and flushed with one global add per
 // non-zero bin.  The last GF_LRU_WIN seconds of each class are counted directly
@@ -2754,21 +2750,9 @@ __device__ __forceinline__ void lru_clear_slot(const gf_htab_desc &d, uint64_t j
 // count with one global add.  (An XOR-folded index once mapped a closing bin and
 // the non-closing bin 32 s from it to one line: every wave alternated them and
 // sent a global add to a few hot addresses.)
-#define GF_LRU_LDS_LOG2 10u
-#define GF_LRU_LDS (1u << GF_LRU_LDS_LOG2)
-#define GF_LRU_WIN 1024u
-#define GF_LRU_CT 256u                  // k_lru_chain block
-// The chain's LDS, one set per block (the phases use disjoint parts).
-struct LruSmem {
-    unsigned long long line[GF_LRU_LDS];    // sample: bin << 32 | count; bin ~0 = empty
-    uint32_t win[2 * GF_LRU_WIN];           // sample: class * WIN + bin - (BINS - WIN)
-    uint32_t cg[GF_LRU_GROUPS];             // sample: the block's group sums
-    unsigned long long part[GF_LRU_CT];     // plan
-    unsigned long long s_es, s_before;
-    uint32_t s_k, s_g;
-    uint8_t code[2 * GF_LRU_CHUNK];         // hand
-    uint32_t s_ef, s_kills, s_clr;
-};
+#define GF_LRU_LDS 2048u
+#define GF_LRU_WIN 4096u
+#define GF_LRU_HB 1024u                 // k_lru_sample block: 16 waves share the LDS bins
 // One histogram add; its group's sum goes to the block's LDS copy of the sums
 // (flushed once per block: a sample's entries fall in a few groups, whose global
 // words every block would otherwise hit for each of its bins).
@@ -2777,50 +2761,57 @@ __device__ __forceinline__ void lru_hist_put(LruDev *L, uint32_t *cg, uint32_t b
     atomicAdd(&cg[bin >> 6], c);
 }
 // key: the entry's age key, ~0u for none.  Wave-uniform call.
-__device__ __forceinline__ void lru_hist_add(LruDev *L, LruSmem &m, uint32_t key) {
+__device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line, uint32_t *win, uint32_t *cg,
+                                             uint32_t key) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t kb = key & (GF_LRU_BINS - 1u);
     const bool inwin = key != ~0u && kb >= GF_LRU_BINS - GF_LRU_WIN;
-    if (inwin) atomicAdd(&m.win[(key >> 16) * GF_LRU_WIN + kb - (GF_LRU_BINS - GF_LRU_WIN)], 1u);
+    if (inwin) atomicAdd(&win[(key >> 16) * GF_LRU_WIN + kb - (GF_LRU_BINS - GF_LRU_WIN)], 1u);
     uint64_t rem = __ballot(key != ~0u && !inwin);
     while (rem) {
         const uint32_t lead = (uint32_t)__ffsll((unsigned long long)rem) - 1u;
         const uint32_t k = __shfl(key, (int)lead);
-        const uint64_t msk = __ballot(key == k) & rem;
+        const uint64_t m = __ballot(key == k) & rem;
         if (lane == lead) {
-            const uint32_t n = (uint32_t)__popcll(msk), h = (k * 0x9E3779B1u) >> (32 - GF_LRU_LDS_LOG2);
-            unsigned long long cur = m.line[h];
+            const uint32_t n = (uint32_t)__popcll(m), h = (k * 0x9E3779B1u) >> (32 - 11);
+            unsigned long long cur = line[h];
             for (;;) {
                 const uint32_t ck = (uint32_t)(cur >> 32);
                 const unsigned long long want = ck == k ? cur + n : (((unsigned long long)k << 32) | n);
-                const unsigned long long seen = atomicCAS(&m.line[h], cur, want);
+                const unsigned long long seen = atomicCAS(&line[h], cur, want);
                 if (seen == cur) {
-                    if (ck != k && ck != ~0u && (uint32_t)cur) lru_hist_put(L, m.cg, ck, (uint32_t)cur);
+                    if (ck != k && ck != ~0u && (uint32_t)cur) lru_hist_put(L, cg, ck, (uint32_t)cur);
                     break;
                 }
                 cur = seen;
             }
         }
-        rem &= ~msk;
+        rem &= ~m;
     }
 }
 // The sample: the sl home lines just ahead of the hand (the lines it passes next,
 // so their density is the one its rounds are planned with; the whole table when
 // sl = nl): slots [hand * SPL, (hand + sl) * SPL) mod NS and the rest of the probe
 // cluster running past them (entries homed in the window; one wave walks it, at
-// most to where the window starts again).  Every block of the grid.
+// most to where the window starts again).
+// wide: the whole table (launched after k_lru_plan found the window empty).
 template <int KIND>
-__device__ __forceinline__ void lru_sample(const gf_htab_desc &d, uint32_t mode, uint32_t now, LruDev *L, uint64_t sl,
-                                           LruSmem &m) {
-    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) m.line[k] = 0xffffffff00000000ull;
-    for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) m.win[k] = 0;
-    for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x) m.cg[k] = 0;
+__global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                          uint64_t sl, uint32_t max_entries, uint32_t wide) {
+    if (wide ? !L->wide : (unsigned long long)*d.count <= lru_high_water(max_entries)) return;
+    __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
+    __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
+    __shared__ uint32_t cg[GF_LRU_GROUPS];             // the block's group sums
+    for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) line[k] = 0xffffffff00000000ull;
+    for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x) win[k] = 0;
+    for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x) cg[k] = 0;
     __syncthreads();
     constexpr uint32_t SPL = LruSlot<KIND>::SPL;
     const uint64_t ns = d.mask + 1, nl = ns / SPL;
+    if (wide) sl = nl;
     const uint64_t n = sl * SPL, h0 = sl >= nl ? 0 : L->hand, P0 = h0 * SPL;
     auto in_window = [&](const LruSlot<KIND> &s) { return (s.home_line(d, mode) + nl - h0) % nl < sl; };
-    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_CT; b0 < n; b0 += (uint64_t)gridDim.x * GF_LRU_CT) {  // uniform trips
+    for (uint64_t b0 = (uint64_t)blockIdx.x * GF_LRU_HB; b0 < n; b0 += (uint64_t)gridDim.x * GF_LRU_HB) {  // uniform trips
         const uint64_t i = b0 + threadIdx.x;
         uint32_t key = ~0u;
         if (i < n) {
@@ -2828,7 +2819,7 @@ __device__ __forceinline__ void lru_sample(const gf_htab_desc &d, uint32_t mode,
             s.load(d, (P0 + i) & d.mask);
             if (s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
         }
-        lru_hist_add(L, m, key);
+        lru_hist_add(L, line, win, cg, key);
     }
     if (blockIdx.x == 0 && threadIdx.x < 64 && n < ns) {
         for (uint64_t q = n;; q += 64) {
@@ -2839,112 +2830,125 @@ __device__ __forceinline__ void lru_sample(const gf_htab_desc &d, uint32_t mode,
             const uint32_t stop = em ? (uint32_t)__ffsll((unsigned long long)em) - 1u : 64u;
             uint32_t key = ~0u;
             if (threadIdx.x < stop && s.st == GF_SLOT_FULL && in_window(s)) key = lru_age_key(s.lt, s.fl, now);
-            lru_hist_add(L, m, key);
+            lru_hist_add(L, line, win, cg, key);
             if (em || q + 64 >= ns) break;
         }
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_LDS; k += blockDim.x) {
-        const unsigned long long v = m.line[k];
-        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) lru_hist_put(L, m.cg, (uint32_t)(v >> 32), (uint32_t)v);
+        const unsigned long long v = line[k];
+        if ((uint32_t)(v >> 32) != ~0u && (uint32_t)v) lru_hist_put(L, cg, (uint32_t)(v >> 32), (uint32_t)v);
     }
     for (uint32_t k = threadIdx.x; k < 2 * GF_LRU_WIN; k += blockDim.x)
-        if (m.win[k]) lru_hist_put(L, m.cg, (k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN,
-                                   m.win[k]);
+        if (win[k]) lru_hist_put(L, cg, (k / GF_LRU_WIN) * GF_LRU_BINS + GF_LRU_BINS - GF_LRU_WIN + k % GF_LRU_WIN, win[k]);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x)
-        if (m.cg[k]) atomicAdd(&L->coarse[k], m.cg[k]);
+        if (cg[k]) atomicAdd(&L->coarse[k], cg[k]);
 }
 // K and es from the sample's histogram, the count the call starts from, and the
-// histogram cleared for the next call (block 0): the 2048 group sums (eight per
-// thread), a block scan, then one wave finds the median's bin among its group's 64.
-// An empty window (sl < nl) sets L->wide instead of planning.
-__device__ __forceinline__ void lru_plan(uint32_t c, LruDev *L, uint64_t sl, uint64_t nl, LruSmem &m) {
-    constexpr uint32_t NB = 2 * GF_LRU_BINS, GPT = GF_LRU_GROUPS / GF_LRU_CT;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    uint32_t g[GPT];
-    unsigned long long v = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < GPT; q++) { g[q] = L->coarse[GPT * t + q]; v += g[q]; }
-    if (t == 0) { m.s_k = NB - 1; m.s_es = 0; m.s_g = ~0u; m.s_before = 0; }
-    {                                                   // inclusive scan: in each wave, then over the waves
+// histogram cleared for the next call (one block).
+// wide = 0: the window's sample; an empty one (sl < nl) sets L->wide for the
+// whole-table sample and its plan (wide = 1) instead of planning.
+__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
+                                                   uint64_t nl, uint32_t wide) {
+    const uint32_t c = *count;
+    const uint32_t t = threadIdx.x;
+    if (wide) {
+        if (!L->wide) return;
+        sl = nl;
+    } else if ((unsigned long long)c <= lru_high_water(max_entries)) {
+        if (t == 0) L->flag = 0u;
+        return;
+    }
+    // the 2048 group sums (two per thread), a block scan, then one wave finds the
+    // median's bin among its group's 64; only the groups that hold entries are cleared
+    constexpr uint32_t NB = 2 * GF_LRU_BINS;
+    __shared__ unsigned long long part[1024];
+    __shared__ uint32_t s_k, s_g;
+    __shared__ unsigned long long s_es, s_before;
+    const uint32_t g0 = L->coarse[2 * t], g1 = L->coarse[2 * t + 1];
+    if (t == 0) { s_k = NB - 1; s_es = 0; s_g = ~0u; s_before = 0; }
+    {                                                   // inclusive scan: in each wave, then over the 16 waves
+        const uint32_t lane = t & 63u, wv = t >> 6;
+        unsigned long long v = (unsigned long long)g0 + g1;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const unsigned long long u = __shfl_up(v, o);
             if (lane >= (uint32_t)o) v += u;
         }
-        __shared__ unsigned long long wsum[GF_LRU_CT / 64];
+        __shared__ unsigned long long wsum[16];
         if (lane == 63) wsum[wv] = v;
         __syncthreads();
         unsigned long long off = 0;
         for (uint32_t q = 0; q < wv; q++) off += wsum[q];
-        m.part[t] = v + off;
+        part[t] = v + off;
         __syncthreads();
     }
-    const unsigned long long total = m.part[GF_LRU_CT - 1], need = (total + 1) / 2, before = t ? m.part[t - 1] : 0ull;
+    const unsigned long long total = part[1023], need = (total + 1) / 2, before = t ? part[t - 1] : 0ull;
     if (!total && sl < nl) {                            // no entry in the window (histogram still all zero)
         if (t == 0) { L->wide = 1u; L->flag = 0u; }
         return;
     }
-    if (total && before < need && m.part[t] >= need) {  // the median lies in one of this thread's groups
-        unsigned long long acc = before;
-        for (uint32_t q = 0; q < GPT; q++) {
-            if (acc + g[q] >= need) { m.s_g = GPT * t + q; m.s_before = acc; break; }
-            acc += g[q];
-        }
+    if (total && before < need && part[t] >= need) {    // the median lies in group 2t or 2t + 1
+        const bool first = before + g0 >= need;
+        s_g = first ? 2 * t : 2 * t + 1;
+        s_before = first ? before : before + g0;
     }
     __syncthreads();
-    if (t < 64 && m.s_g != ~0u) {                        // wave 0: the median group's bins, one per lane
-        const uint32_t x = L->hist[m.s_g * 64u + t];
-        uint32_t inc = x;
+    if (t < 64 && s_g != ~0u) {                          // wave 0: the median group's bins, one per lane
+        const uint32_t v = L->hist[s_g * 64u + t];
+        uint32_t inc = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t u = __shfl_up(inc, o);
             if (t >= (uint32_t)o) inc += u;
         }
-        const uint64_t hit = __ballot(m.s_before + inc >= need);
-        if (t == (uint32_t)__ffsll((unsigned long long)hit) - 1u) { m.s_k = m.s_g * 64u + t; m.s_es = m.s_before + inc; }
+        const uint64_t hit = __ballot(s_before + inc >= need);
+        if (t == (uint32_t)__ffsll((unsigned long long)hit) - 1u) { s_k = s_g * 64u + t; s_es = s_before + inc; }
     }
     __syncthreads();
     // clear for the next sample: the bins of the groups that hold entries, and the sums
-#pragma unroll
-    for (uint32_t q = 0; q < GPT; q++) {
-        if (!g[q]) continue;
-        const uint32_t gi = GPT * t + q;
-        uint4 *hb = reinterpret_cast<uint4 *>(L->hist + gi * 64u);
+    for (uint32_t q = 0; q < 2; q++) {
+        const uint32_t g = 2 * t + q;
+        if (!(q ? g1 : g0)) continue;
+        uint4 *hb = reinterpret_cast<uint4 *>(L->hist + g * 64u);
 #pragma unroll
         for (uint32_t k = 0; k < 16; k++) hb[k] = make_uint4(0u, 0u, 0u, 0u);
-        L->coarse[gi] = 0u;
+        L->coarse[g] = 0u;
     }
     if (t == 0) {
-        L->K = m.s_k; L->es = m.s_es; L->cnt0 = c; L->sl = sl; L->wide = 0u; L->flag = 1u; L->cleared = 0;
+        L->K = s_k; L->es = s_es; L->cnt0 = c; L->sl = sl; L->wide = 0u; L->flag = 1u; L->cleared = 0;
         for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) L->kills[r] = 0;
     }
 }
-// The hand over a round's lines: the slots from the first line's first slot,
-// lines * SPL of them, in chunks (GF_LRU_CHUNK slots, twice that for CT4), plus the
-// cluster running past the last one (entries homed in the range).  Two phases, PAR =
-// 0 for the even chunks and 1 for the odd ones (a grid barrier between): a chunk's
-// last slots turn EMPTY only if the slots after it, up to the cluster's end, are all
-// gone too, which the block reads from the next chunk (at most one chunk ahead, else
-// it keeps them FREE) — untouched in the even phase, final in the odd one, so no read
-// races a write.  The slots past the last chunk are read and written by its block
-// alone (there deleted entries turn FREE).  Codes: 0 EMPTY, 1 kept, 2 deleted now, 3
-// a tombstone or FREE slot (cleared).
+// The hand over this round's lines: the slots from the first line's first slot,
+// lines * SPL of them, in chunks (GF_LRU_CHUNK slots, twice that for CT4), plus the cluster running past
+// the last one (entries homed in the range).  Launched twice, PAR = 0 for the
+// even chunks and 1 for the odd ones: a chunk's last slots turn EMPTY only if the
+// slots after it, up to the cluster's end, are all gone too, which the block
+// reads from the next chunk (at most one chunk ahead, else it keeps them FREE) —
+// untouched in the even launch, final in the odd one, so no read races a write.
+// The slots past the last chunk are read and written by its block alone (there
+// deleted entries turn FREE).  Codes: 0 EMPTY, 1 kept, 2 deleted now, 3 a
+// tombstone or FREE slot (cleared).
 template <int KIND, int PAR>
-__device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, uint32_t now, LruDev *L, uint64_t nl,
-                                         const LruRound R, uint32_t round, LruSmem &m) {
+__global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                        uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t round) {
+    if (!L->flag) return;
+    const LruRound R = lru_round(L, round, max_entries, nl);
     const unsigned long long lines = R.lines;
+    if (!lines) return;
     using S = LruSlot<KIND>;
     // slots a block decides together: 8 per thread for the 32-B CT4 slots, 4 for the
     // 64-B CT6 slots (the same 64 KB of loads in flight per block)
-    constexpr uint32_t CH = KIND == 2 ? GF_LRU_CHUNK : 2 * GF_LRU_CHUNK, U = CH / GF_LRU_CT;
+    constexpr uint32_t CH = KIND == 2 ? GF_LRU_CHUNK : 2 * GF_LRU_CHUNK, U = CH / GF_LRU_HT;
     const uint32_t K = L->K;
     const unsigned long long h0 = R.h0;
     const uint64_t ns = d.mask + 1, P0 = h0 * S::SPL, NP = lines * S::SPL;
     const bool whole = NP >= ns;
     const uint64_t nch = (NP + CH - 1) / CH;
-    uint8_t *code = m.code;
+    __shared__ uint8_t code[2 * GF_LRU_CHUNK];
+    __shared__ uint32_t s_ef, s_kills, s_clr;
     auto code_of = [&](const S &s) -> uint32_t {
         if (s.st == GF_SLOT_EMPTY) return 0u;
         if (s.st == GF_SLOT_TOMB || s.st == GF_SLOT_FREE) return 3u;
@@ -2952,8 +2956,7 @@ __device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, u
         const uint64_t hl = s.home_line(d, mode);
         return (hl + nl - h0) % nl < lines ? 2u : 1u;
     };
-    if (threadIdx.x == 0) { m.s_kills = 0; m.s_clr = 0; }
-    __syncthreads();
+    if (threadIdx.x == 0) { s_kills = 0; s_clr = 0; }
     uint32_t kills = 0, clr = 0;
     const uint32_t lane = threadIdx.x & 63u;
     for (uint64_t c = 2 * (uint64_t)blockIdx.x + PAR; c < nch; c += 2 * (uint64_t)gridDim.x) {
@@ -2963,8 +2966,8 @@ __device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, u
         uint32_t mine[U], ost[U];
         // wave 0 also loads the first 64 slots after the chunk with the chunk's own
         // loads (at low load they decide the chunk's trailing run): one round trip
-        // less per chunk.  Nothing writes them during this phase before wave 0 reads
-        // them below (the next chunk is the other phase's, and past the last chunk
+        // less per chunk.  Nothing writes them during this launch before wave 0 reads
+        // them below (the next chunk is the other launch's, and past the last chunk
         // only this block writes, after reading).
         S la;
         const bool look = threadIdx.x < 64 && !(last && whole);
@@ -2972,7 +2975,7 @@ __device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, u
         if (look && o0 < ns) la.load(d, (P0 + o0) & d.mask);
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t off = u * GF_LRU_CT + threadIdx.x;
+            const uint32_t off = u * GF_LRU_HT + threadIdx.x;
             mine[u] = 1u; ost[u] = GF_SLOT_FULL;
             if (off < cnt) {
                 S s;
@@ -3005,13 +3008,13 @@ __device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, u
                     if (last && __ballot(cd == 0u)) break;                 // the cluster past the range ends
                 }
             }
-            if (lane == 0) m.s_ef = decided && ef ? 1u : 0u;
+            if (lane == 0) s_ef = decided && ef ? 1u : 0u;
         }
         __syncthreads();
-        const bool ef = m.s_ef != 0;
+        const bool ef = s_ef != 0;
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t off = u * GF_LRU_CT + threadIdx.x;
+            const uint32_t off = u * GF_LRU_HT + threadIdx.x;
             if (off >= cnt || mine[u] < 2u) continue;
             bool to_empty = ef;
             for (uint32_t k = off + 1; k < cnt; k++) {
@@ -3025,17 +3028,22 @@ __device__ __forceinline__ void lru_hand(const gf_htab_desc &d, uint32_t mode, u
         }
         __syncthreads();                                 // code[] is the next chunk's
     }
-    if (kills) atomicAdd(&m.s_kills, kills);
-    if (clr) atomicAdd(&m.s_clr, clr);
+    if (kills) atomicAdd(&s_kills, kills);
+    if (clr) atomicAdd(&s_clr, clr);
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (m.s_kills) atomicAdd(&L->kills[round], (unsigned long long)m.s_kills);
-        if (m.s_clr) atomicAdd(&L->cleared, (unsigned long long)m.s_clr);
+        if (s_kills) atomicAdd(&L->kills[round], (unsigned long long)s_kills);
+        if (s_clr) atomicAdd(&L->cleared, (unsigned long long)s_clr);
     }
 }
-// After the last round (block 0, one thread): the count, the hand, the log.
-__device__ __forceinline__ void lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t max_entries,
-                                        uint64_t nl) {
+// After the last round: the count, the hand, the log (hcount: the count for the
+// host's bound, pinned host memory, may be null).
+__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t max_entries, uint64_t nl,
+                          uint32_t *hcount) {
+    if (!L->flag) {
+        if (hcount) *hcount = *count;
+        return;
+    }
     unsigned long long killed = 0, lines = 0;
     for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) {
         lines += lru_round(L, r, max_entries, nl).lines;
@@ -3051,41 +3059,7 @@ __device__ __forceinline__ void lru_end(uint32_t *count, uint32_t seq, uint32_t 
     L->nlog = n + 1;
     L->hand = (L->hand + lines) % nl;
     L->flag = 0;
-}
-// hcount: the count for the host's bound (pinned host memory, may be null).
-template <int KIND>
-__global__ __launch_bounds__(GF_LRU_CT, 5) void k_lru_chain(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                         uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t seq,
-                                                         uint32_t *hcount) {
-    const uint32_t c0 = *d.count;                       // every block reads the same count: nothing writes it before the end
-    if ((unsigned long long)c0 <= lru_high_water(max_entries)) {
-        if (blockIdx.x == 0 && threadIdx.x == 0 && hcount) *hcount = c0;
-        return;                                          // the whole grid: no barrier is reached
-    }
-    __shared__ LruSmem m;
-    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-    lru_sample<KIND>(d, mode, now, L, sl, m);
-    grid.sync();
-    if (blockIdx.x == 0) lru_plan(c0, L, sl, nl, m);
-    grid.sync();
-    if (L->wide) {                                       // the window held no entry: the whole table
-        lru_sample<KIND>(d, mode, now, L, nl, m);
-        grid.sync();
-        if (blockIdx.x == 0) lru_plan(c0, L, nl, nl, m);
-        grid.sync();
-    }
-    for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) {
-        const LruRound R = lru_round(L, r, max_entries, nl);   // the same in every block
-        if (!R.lines) continue;
-        lru_hand<KIND, 0>(d, mode, now, L, nl, R, r, m);
-        grid.sync();
-        lru_hand<KIND, 1>(d, mode, now, L, nl, R, r, m);
-        grid.sync();
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        lru_end(d.count, seq, now, L, max_entries, nl);
-        if (hcount) *hcount = *d.count;
-    }
+    if (hcount) *hcount = *count;
 }
 
 // ================================================================ drop notifications
@@ -5706,38 +5680,34 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
     if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount + slot, 0), "lru count word")) return -EIO;
     const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size, nl = ns / spl;
     const uint64_t sl = lru_sample_lines(nl);
-    uint32_t mx = m->max_entries, seq = m->lru_seq, mode = m->ht.mode;
-    // one cooperative launch (its blocks meet at grid barriers): as many blocks as can
-    // be resident at once, every one of them
-    static int grid_of[3] = {0, 0, 0};
-    if (!grid_of[kind]) {
-        int per_cu = 0, dev = 0, cus = 0, coop = 0;
-        const void *fn = kind == 1 ? (const void *)k_lru_chain<1> : (const void *)k_lru_chain<2>;
-        if (hip_ok(hipGetDevice(&dev), "lru device") ||
-            hip_ok(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev), "lru coop attr") ||
-            hip_ok(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "lru cus") ||
-            hip_ok(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, GF_LRU_CT, 0), "lru occupancy"))
-            return -EIO;
-        if (!coop || per_cu < 1 || cus < 1) return -EOPNOTSUPP;
-        grid_of[kind] = per_cu * cus;
-    }
+    const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
+    const uint32_t gh = resident_blocks(8);
+    const uint32_t *cnt = (const uint32_t *)d.count;
+    const uint32_t mx = m->max_entries;
     {
-        // Two cooperative grids sized to the whole device must never be resident
-        // together (each would wait at its barrier for blocks the other holds): every
-        // chain, from any stream, waits for the previous one to finish.
-        static std::mutex coop_mu;
-        static hipEvent_t coop_last = nullptr;
-        std::lock_guard<std::mutex> cg(coop_mu);
-        if (!coop_last && hip_ok(hipEventCreateWithFlags(&coop_last, hipEventDisableTiming), "lru chain event"))
-            return -EIO;
-        if (hip_ok(hipStreamWaitEvent(s, coop_last, 0), "lru chain order")) return -EIO;
         ProfScope ps("k_lru_evict", s);
-        void *args[] = {(void *)&d, (void *)&mode, (void *)&now, (void *)&L, (void *)&nl, (void *)&sl, (void *)&mx,
-                        (void *)&seq, (void *)&hc};
-        const void *fn = kind == 1 ? (const void *)k_lru_chain<1> : (const void *)k_lru_chain<2>;
-        if (hip_ok(hipLaunchCooperativeKernel(fn, dim3(grid_of[kind]), dim3(GF_LRU_CT), args, 0, s), "k_lru_chain") ||
-            hip_ok(hipEventRecord(coop_last, s), "lru chain event"))
-            return -EIO;
+        // the window's sample and plan, then (large tables only) the whole-table
+        // pair, which runs only when the window held no entry
+        for (uint32_t wide = 0; wide < (sl < nl ? 2u : 1u); wide++) {
+            const dim3 g(wide ? gh : gs);
+            if (kind == 1)
+                hipLaunchKernelGGL(k_lru_sample<1>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
+            else
+                hipLaunchKernelGGL(k_lru_sample<2>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
+            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, mx, L, sl, nl, wide);
+        }
+        for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
+            // round 1 is rare and short (what round 0's estimate left): a smaller grid, the same chunks
+            const dim3 g(round == 1 ? gh / 8 : gh);
+            if (kind == 1) {
+                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+            } else {
+                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
+            }
+        }
+        hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, mx, nl, hc);
     }
     if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
     m->ev_pending |= 1u << slot;

@@ -1,6 +1,6 @@
 """Per-event account of the LRU stand-in's launch chains in a rocprofv3 kernel
-trace (tools/gpu.sh trace:...): one chain = the first k_lru_sample .. k_lru_end
-(k_lru_round_end in round-5 traces).
+trace (tools/gpu.sh trace:...): one chain = one k_lru_chain launch (round 6), or the
+first k_lru_sample .. k_lru_end (k_lru_round_end in round-5 traces).
 
     python tools/lru_chains.py gpurun_out/TAG/trace_NAME/run_kernel_trace.csv [--active-us 100]
 
@@ -25,6 +25,9 @@ def main():
     chains, cur = [], None
     for r in rows:
         n = name(r["Kernel_Name"])
+        if n.startswith("k_lru_chain"):                 # round 6 on: the whole chain is one cooperative launch
+            chains.append([(n, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)])
+            continue
         if n.startswith("k_lru_sample") and cur is None:
             cur = []
             chains.append(cur)
