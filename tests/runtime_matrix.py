@@ -67,6 +67,12 @@ def load():
         return json.load(f)
 
 
+def case_endpoints(doc, case):
+    """A case's endpoints: its own set when it names one (the conntrack suite's
+    containers), else the document's."""
+    return case.get("endpoints") or doc["endpoints"]
+
+
 class Topology:
     """Endpoints of the runtime suite: IPv4 10.15.0.<lxc_id>, IPv6
     f00d::a0f:0:0:<lxc_id> (inside ROUTER_IP's /64 and the IPv6Gateway/112 the
@@ -196,10 +202,17 @@ def expand(case):
 
 
 class Flow:
+    """One request: ping / ping6 (ICMP echo + reply), http / http6 (TCP handshake to
+    port 80), or tcp:P / tcp6:P (TCP handshake to port P) and udp:P / udp6:P (a
+    datagram to port P and its reply)."""
+
     def __init__(self, j, client, server, req):
         self.client, self.server, self.req = client, server, req
-        self.v6 = req in ("ping6", "http6", "http6Private")
-        self.tcp = req.startswith("http")
+        kind, _, port = req.partition(":")
+        self.v6 = kind in ("ping6", "http6", "http6Private", "tcp6", "udp6")
+        self.tcp = kind.startswith("http") or kind.startswith("tcp")
+        self.udp = kind.startswith("udp")
+        self.dport = int(port) if port else 80
         self.sport = 40000 + j
         self.steps = list(TCP_SEQ) if self.tcp else [(None, "c"), (None, "s")]
         self.delivered = 0                   # packets of the sequence that got through
@@ -210,12 +223,13 @@ def _frame(topo, f, step):
     flags, side = f.steps[step]
     src, dst = (f.client, f.server) if side == "c" else (f.server, f.client)
     sa, da = topo.addr(src, f.v6), topo.addr(dst, f.v6)
-    sp, dp = (f.sport, 80) if side == "c" else (80, f.sport)
+    sp, dp = (f.sport, f.dport) if side == "c" else (f.dport, f.sport)
     if f.v6:
         fr, ln = S.frames_v6(1, STRIDE, np.frombuffer(sa, np.uint8)[None], np.frombuffer(da, np.uint8)[None],
-                             S.TCP if f.tcp else S.ICMPV6, sp, dp, flags or 0, 128 if side == "c" else 129)
+                             S.TCP if f.tcp else S.UDP if f.udp else S.ICMPV6, sp, dp, flags or 0,
+                             128 if side == "c" else 129)
     else:
-        fr, ln = S.frames_v4(1, STRIDE, sa, da, S.TCP if f.tcp else S.ICMP, sp, dp, flags or 0,
+        fr, ln = S.frames_v4(1, STRIDE, sa, da, S.TCP if f.tcp else S.UDP if f.udp else S.ICMP, sp, dp, flags or 0,
                              8 if side == "c" else 0)
     if src in topo.mac:
         fr[0, 6:12] = np.frombuffer(topo.mac[src], np.uint8)

@@ -46,7 +46,7 @@ def test_agent_restatement_flags():
 
 @pytest.mark.parametrize("case", CASES, ids=_ids())
 def test_oracle_matches_reference_matrix(case):
-    topo = RM.Topology(DOC["endpoints"])
+    topo = RM.Topology(RM.case_endpoints(DOC, case))
     res, _ = RM.run_case(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
     bad = RM.outcome_mismatches(case, res)
     assert not bad, bad
@@ -59,7 +59,7 @@ ONE_BATCH = [c for c in CASES if not any(s.startswith("host") for _, s, *_ in c[
 def test_oracle_one_batch_request_and_reply(case):
     """Requests, replies and ACKs in one batch: the per-packet order of the
     reference gives the reference's outcomes."""
-    topo = RM.Topology(DOC["endpoints"])
+    topo = RM.Topology(RM.case_endpoints(DOC, case))
     res, _ = RM.run_case_one_batch(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
     bad = RM.outcome_mismatches(case, res)
     assert not bad, bad
@@ -74,8 +74,8 @@ def test_gpu_one_batch_request_and_reply_ordered():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     from oracle import parity as PY
-    topo = RM.Topology(DOC["endpoints"])
     for case in ONE_BATCH:
+        topo = RM.Topology(RM.case_endpoints(DOC, case))
         gpu = RM.GpuBackend(RM.compile_case(case, topo))
         ref = RM.OracleBackend(RM.compile_case(case, topo))
         try:
@@ -100,8 +100,8 @@ def test_gpu_matches_reference_matrix_and_oracle():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     from oracle import parity as PY
-    topo = RM.Topology(DOC["endpoints"])
     for case in CASES:
+        topo = RM.Topology(RM.case_endpoints(DOC, case))
         sc = RM.compile_case(case, topo)
         gpu = RM.GpuBackend(sc)
         try:
@@ -114,3 +114,26 @@ def test_gpu_matches_reference_matrix_and_oracle():
         for (kind, step, g), (_, _, o) in zip(glog, olog):
             bad, first = PY.compare_records(g, o)
             assert bad == 0, (case["name"], kind, step, g[first], o[first])
+
+
+def test_conntrack_case_replies_pass_on_the_ct():
+    """RuntimeValidatedConntrackTest (connectivity.go:294-478): the server's replies
+    leave it under PolicyEnforcement=always with no egress rule of its own, and enter
+    the client with no ingress rule, only because both CT lookups find the request's
+    entries (CT_REPLY on the server's from-container lookup and on the client's
+    handle_policy); a new connection the other way (server -> client ping) is dropped
+    by the server's egress policy (DROP_POLICY)."""
+    case = next(c for c in CASES if c["name"].startswith("Conntrack"))
+    topo = RM.Topology(RM.case_endpoints(DOC, case))
+    res, log = RM.run_case(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
+    assert not RM.outcome_mismatches(case, res)
+    flows = [RM.Flow(j, c, s, r) for j, (c, s, r, _) in enumerate(RM.expand(case))]
+    # wave 1 holds the second packet of every flow that survived wave 0, in flow order
+    alive = [f for f, ok in zip(flows, [RM.expected(case)[(f.client, f.server, f.req)] for f in flows]) if ok]
+    kind, step, rec = log[1]
+    assert kind == "egress" and step == 1 and len(rec) == len(alive)
+    for f, r in zip(alive, rec):
+        assert r["eg_ct_ret"] == 2 and r["ct_ret"] == 2, (f.client, f.server, f.req, r)   # CT_REPLY both ways
+    kind, step, rec = log[0]
+    drops = [r for f, r in zip(flows, rec) if f.client == "server"]
+    assert drops and all(r["action"] == 2 and r["reason"] == 133 for r in drops)          # DROP_POLICY
