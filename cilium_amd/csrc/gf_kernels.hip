@@ -990,6 +990,19 @@ struct Ep {
     }
 };
 
+// The CT map a packet's program binds (CT_MAP4 / CT_MAP6 of its endpoint).
+// PCT = false: every program binds the global map (cilium_ct4_global /
+// cilium_ct6_global), passed once in the launch context.  PCT = true: the
+// ConntrackLocal layout (pkg/endpoint/bpf.go:268-276, cilium_ct4_<id>): each
+// program's own map, read from the program table per packet.
+template <int FAM, bool PCT>
+__device__ __forceinline__ gf_htab_desc ing_ct(const IngCtx &X, const Ep &ep) {
+    constexpr uint32_t has = FAM == 6 ? GF_LXC_DEV_HAS_CT6 : GF_LXC_DEV_HAS_CT4;
+    if (!(ep.flags & has)) return gf_htab_desc{};
+    if constexpr (PCT) return gload<gf_htab_desc>(FAM == 6 ? &ep.cfg(X)->ct6 : &ep.cfg(X)->ct4);
+    else return FAM == 6 ? X.ct6 : X.ct4;
+}
+
 // The ICMP-related entry ct_create writes for every new flow of a group
 // (conntrack.h:563-577) is the same key for the whole group: a lane keeps
 // where it lives.  Only this lane changes keys of its group; a delete by the
@@ -1503,6 +1516,7 @@ __device__ __attribute__((noinline)) void pol_redirect_ol(PolCtx X, uint32_t i, 
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
 // rlog: X.rlog unless the run fell back to pair groups (read once per kernel, k_ing_groups)
+template <bool PCT>
 __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
                            uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo<GF_MEMO4> &pm,
                            uint32_t *rlog) {
@@ -1517,7 +1531,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     int e = ct_l4(nh, false, r, t[2], tfl, action, syn);
     if (e < 0) return e;
     t[3] = nh | (tfl << 8);
-    const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT4) ? X.ct4 : gf_htab_desc{};
+    const gf_htab_desc ct = ing_ct<4, PCT>(X, ep);
     // the CT home line and the policy home line of the source identity go out together
     ProbeLine<14, GF_CT4_U, 4> cl;
 #if GF_CT_COOP
@@ -1583,6 +1597,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
 }
 
 // ipv6_policy, bpf/bpf_lxc.c:745-862
+template <bool PCT>
 __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl,
                            uint16_t &proxy, uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc,
                            RelCache<10> &rc, PolMemo<GF_MEMO6> &pm) {
@@ -1605,7 +1620,7 @@ __device__ int ipv6_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     int e = ct_l4(nh, true, r, t[8], tfl, action, syn);
     if (e < 0) return e;
     t[9] = nh | (tfl << 8);
-    const gf_htab_desc ct = (flags & GF_LXC_DEV_HAS_CT6) ? X.ct6 : gf_htab_desc{};
+    const gf_htab_desc ct = ing_ct<6, PCT>(X, ep);
     ProbeLine<40, GF_CT6_U, 4> cl;
 #if GF_CT_COOP6
     cl.load_quad(ct, key_hash<40, GF_HASH_CT>(t));
@@ -1710,7 +1725,7 @@ struct Lane {
 // 4 = the IPv4 path plus every packet that cannot reach conntrack (no IP
 // header: their early returns need no CT code), 6 = IPv6 packets that reach
 // conntrack.  The sort key keeps the two sets in different buckets.
-template <int FAM>
+template <int FAM, bool PCT>
 __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane<FAM> &ln,
                                                        uint32_t &ab, uint32_t *rlog) {
     gf_ingress_out o{};
@@ -1726,12 +1741,12 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     if (flags & GF_LXC_F_DROP_ALL) ret = D_POLICY;
     else if (cls == 2) {
         ab += 47;
-        if constexpr (FAM == 6) ret = ipv6_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
+        if constexpr (FAM == 6) ret = ipv6_policy<PCT>(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm);
         else ret = D_INVALID;                       // ipv6_policy: short frame or batch without v6 columns
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if constexpr (FAM == 4) ret = ipv4_policy(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm,
+        if constexpr (FAM == 4) ret = ipv4_policy<PCT>(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm,
                                                   rlog);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
@@ -1807,12 +1822,19 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 // (LPT): k_bucket_order lists them by packet count, descending, and waves take
 // the next 64 entries of that list from a device queue, so the lanes of a wave
 // carry equal work and the deepest buckets start first.
-template <int FAM>
+template <int FAM, bool PCT>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
                                         Stats &st, bool stats, Lane<FAM> &ln, uint32_t *rlog) {
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy<FAM>(X, r, i, ln, ab, rlog);
+    gf_ingress_out o = handle_policy<FAM, PCT>(X, r, i, ln, ab, rlog);
+    if constexpr (PCT) {
+        // per-endpoint CT maps: the lane's related-entry cache is the packet's own
+        // (the next packet of the bucket may be another endpoint's, another map)
+        if constexpr (FAM == 4)
+            if (ln.rc.k[3] >> 15) rel_flush4(ing_ct<4, true>(X, ln.ep), ln.rc, X.now);
+        ln.rc.slot = ~0u;
+    }
     if (X.pout && X.pout_wo) {                          // complete the pipeline record: stores only
         uint8_t *q = X.pout + 24 * (size_t)i;
         const uint32_t ff = ((uint32_t)(r.cls >> 4) & 7u) << 5;   // the front's whole GF_PIPE_F_* byte
@@ -1901,7 +1923,7 @@ __device__ __forceinline__ uint32_t sched_list(uint32_t key, const gf_rec *rec, 
 // GRAB: buckets per lane per queue grab in the single-packet tail (GF_GRAB_ING for the
 // egress deliveries' pass, whose buckets are mostly single packets; 1 elsewhere,
 // where the extra state costs the kernel registers it cannot spare)
-template <int FAM, int GRAB = 1>
+template <int FAM, int GRAB = 1, bool PCT = false>
 __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
                                                       const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
@@ -1975,7 +1997,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
 #else
             if (k + 2 < c) in2 = perm[b + k + 2];
 #endif
-            ing_one<FAM>(X, i, r, out, st, stats != nullptr, ln, rlog);
+            ing_one<FAM, PCT>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2;
             if (k + 1 < c) r = ld_rec(rec, i);
         }
@@ -5474,6 +5496,15 @@ static int px_log_apply(const IngCtx &X, hipStream_t s, uint8_t *wsnap, const ui
     return 0;
 }
 
+// A CT map's launch descriptor: an LRU conntrack map's inserts are limited by its
+// slot array (dev_insert_limit), not by max_entries (the eviction pass after the
+// call brings the count back).
+static gf_htab_desc ct_dev_desc(Map &m) {
+    gf_htab_desc d = m.hdesc();
+    if (m.type == GF_MAP_TYPE_LRU_HASH) d.max_entries = (uint32_t)std::min<uint64_t>(dev_insert_limit(m), 0xffffffffu);
+    return d;
+}
+
 // The device program table of a cilium_policy array (every bound map pushed to
 // HBM first); uploaded only when it changed (programs, bindings, or a map's
 // device storage moved).  progs: the distinct programs, slot k+1 = progs[k].
@@ -5507,8 +5538,8 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
             d.l4[j].nexthdr = p->cfg.l4_ingress[j].nexthdr;
         }
         if (p->policy) d.policy = p->policy->hdesc();
-        if (p->ct4) { d.ct4 = p->ct4->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT4; }
-        if (p->ct6) { d.ct6 = p->ct6->hdesc(); d.flags |= GF_LXC_DEV_HAS_CT6; }
+        if (p->ct4) { d.ct4 = ct_dev_desc(*p->ct4); d.flags |= GF_LXC_DEV_HAS_CT4; }
+        if (p->ct6) { d.ct6 = ct_dev_desc(*p->ct6); d.flags |= GF_LXC_DEV_HAS_CT6; }
         if (p->cidr4) d.cidr4 = p->cidr4->tdesc();
         if (p->cidr6) d.cidr6 = p->cidr6->tdesc();
         if (p->revnat4) d.revnat4 = p->revnat4->hdesc();
@@ -5580,8 +5611,8 @@ static void ct_count_refresh(Map &m, bool wait = false) {
 static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map> &ct6m, uint32_t n, uint32_t per_pkt,
                      hipStream_t s, uint32_t &strict, gf_htab_desc &cfg_ct4, gf_htab_desc &cfg_ct6) {
     strict = 0;
-    if (ct4m) cfg_ct4 = ct4m->hdesc();
-    if (ct6m) cfg_ct6 = ct6m->hdesc();
+    if (ct4m) cfg_ct4 = ct_dev_desc(*ct4m);
+    if (ct6m) cfg_ct6 = ct_dev_desc(*ct6m);
     for (auto &m : {ct4m, ct6m}) {
         if (!m) continue;
         // LRU: never fails in the kernel (it evicts); here no eviction inside a classify
@@ -5609,11 +5640,44 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit) strict |= m == ct4m ? 1u : 2u;
         m->dev_count_hi += (uint64_t)per_pkt * n;
         m->cnt_add += (uint64_t)per_pkt * n;
-        if (m->type == GF_MAP_TYPE_LRU_HASH) {
-            if (m == ct4m) cfg_ct4.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
-            else cfg_ct6.max_entries = (uint32_t)std::min<uint64_t>(limit, 0xffffffffu);
-        }
     }
+    return 0;
+}
+
+// The CT maps the programs of a call bind, per family, each once.  pct: some family
+// has more than one (endpoints with the ConntrackLocal option, cilium_ct4_<id>,
+// pkg/endpoint/bpf.go:268-276) — the per-endpoint kernels (ing_ct<FAM, true>).
+struct CtMaps {
+    std::vector<std::shared_ptr<Map>> m4, m6;
+    bool pct = false;
+    std::shared_ptr<Map> one(int fam) const {
+        const auto &v = fam == 6 ? m6 : m4;
+        return v.empty() ? nullptr : v[0];
+    }
+};
+static int ct_maps_of(const std::vector<std::shared_ptr<ProgLxc>> &progs, CtMaps &cm) {
+    std::set<const Map *> s4, s6;
+    for (auto &p : progs) {
+        if (p->ct4 && s4.insert(p->ct4.get()).second) cm.m4.push_back(p->ct4);
+        if (p->ct6 && s6.insert(p->ct6.get()).second) cm.m6.push_back(p->ct6);
+    }
+    for (auto *m : s4)
+        if (s6.count(m)) return -EINVAL;                // one map bound as both families' CT map
+    cm.pct = cm.m4.size() > 1 || cm.m6.size() > 1;
+    return 0;
+}
+// Per-endpoint maps: each map's host bound moves as if the whole batch could insert
+// into it, and every insert is counted exactly into its own map (strict), whose
+// count and insert limit the program table's descriptor carries (ct_dev_desc).
+static int ct_limits_pct(const CtMaps &cm, uint32_t n, uint32_t per_pkt, hipStream_t s, uint32_t &strict) {
+    gf_htab_desc d4{}, d6{};
+    uint32_t st = 0;
+    int r;
+    for (auto &m : cm.m4)
+        if ((r = ct_limits(m, nullptr, n, per_pkt, s, st, d4, d6))) return r;
+    for (auto &m : cm.m6)
+        if ((r = ct_limits(nullptr, m, n, per_pkt, s, st, d4, d6))) return r;
+    strict = 3u;
     return 0;
 }
 
@@ -5748,14 +5812,12 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     host_mark("ing");
     if ((r = prog_table(a, s, progs))) return r;
     host_mark("prog");
-    // CT maps: one counter is tracked in non-strict mode, so all programs must share
-    // one CT map per family (the production layout: cilium_ct4_global / ct6_global).
-    std::shared_ptr<Map> ct4m, ct6m;
-    for (auto &p : progs) {
-        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
-        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
-    }
-    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
+    // CT maps: the global layout (every program binds cilium_ct4_global / ct6_global)
+    // or per-endpoint maps (ConntrackLocal, ct_maps_of: the PCT kernels)
+    CtMaps cm;
+    if ((r = ct_maps_of(progs, cm))) return r;
+    if (cm.pct && ta && ta->kind == 2) return -EOPNOTSUPP;   // (egress_call refuses such an array first)
+    std::shared_ptr<Map> ct4m = cm.pct ? nullptr : cm.one(4), ct6m = cm.pct ? nullptr : cm.one(6);
     // Strict (exact, atomic per insert) element accounting only when this batch could
     // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
     // fail in the kernel (they evict); here they keep entries past max_entries until
@@ -5763,9 +5825,12 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     // The decision uses a host-side upper bound of the device element count (each
     // packet inserts at most 2 entries), read back from the device only when the
     // bound gets near the limit — steady-state batches never wait on the GPU here.
+    // Per-endpoint maps count every insert exactly, into the packet's own map (the
+    // descriptors in the program table carry each map's count and insert limit).
     uint32_t strict = 0;
     gf_htab_desc cfg_ct4{}, cfg_ct6{};
     if ((r = ct_limits(ct4m, ct6m, pkts->n, 2, s, strict, cfg_ct4, cfg_ct6))) return r;
+    if (cm.pct && (r = ct_limits_pct(cm, pkts->n, 2, s, strict))) return r;
     host_mark("ctlim");
     // 2. group by flow group (records and keys first), 3. longest-first bucket order
     uint32_t n = pkts->n;
@@ -5816,7 +5881,11 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         if (grid > need) grid = need;
         {
             ProfScope ps("k_ing_groups", s);
-            if (X.pol_wave)                             // the egress deliveries' pass (single-packet buckets)
+            if (cm.pct)                                 // per-endpoint CT maps (ConntrackLocal)
+                hipLaunchKernelGGL((k_ing_groups<4, 1, true>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
+                                   (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out,
+                                   nullptr, sink);
+            else if (X.pol_wave)                        // the egress deliveries' pass (single-packet buckets)
                 hipLaunchKernelGGL((k_ing_groups<4, GF_GRAB_ING>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
                                    (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cnt4,
                                    sink);
@@ -5827,9 +5896,14 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
         }
         if (pkts->saddr6) {    // IPv6 packets reach conntrack only with v6 columns
             ProfScope ps("k_ing_groups6", s);
-            hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
-                               (const uint32_t *)w.perm.p,
-                               (const gf_rec *)w.rec.p, out, cnt6, sink);
+            if (cm.pct)
+                hipLaunchKernelGGL((k_ing_groups<6, 1, true>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
+                                   (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out,
+                                   nullptr, sink);
+            else
+                hipLaunchKernelGGL(k_ing_groups<6>, dim3(grid), dim3(BLOCK), 0, s, X, d_sched, (const uint2 *)w.order.p,
+                                   (const uint32_t *)w.perm.p,
+                                   (const gf_rec *)w.rec.p, out, cnt6, sink);
         }
     }
     if ((r = hip_ok(hipGetLastError(), "k_ing_groups"))) return r;
@@ -5862,10 +5936,12 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
-    if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
+    for (auto *v : {&cm.m4, &cm.m6})
+        for (auto &m : *v)
+            if (lru && (r = lru_evict(m, now_sec, s))) return r;
     host_mark("lru");
-    if (ct4m) ct4m->device_modified();
-    if (ct6m) ct6m->device_modified();
+    for (auto *v : {&cm.m4, &cm.m6})
+        for (auto &m : *v) m->device_modified();
     return 0;
 }
 
@@ -6586,12 +6662,10 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     int r;
     std::vector<std::shared_ptr<ProgLxc>> progs;
     if ((r = prog_table(a, s, progs))) return r;
-    std::shared_ptr<Map> ct4m, ct6m;
-    for (auto &p : progs) {
-        if (p->ct4) { if (ct4m && ct4m != p->ct4) return -EOPNOTSUPP; ct4m = p->ct4; }
-        if (p->ct6) { if (ct6m && ct6m != p->ct6) return -EOPNOTSUPP; ct6m = p->ct6; }
-    }
-    if (ct4m && ct6m && ct4m == ct6m) return -EINVAL;
+    CtMaps cm;
+    if ((r = ct_maps_of(progs, cm))) return r;
+    if (cm.pct) return -EOPNOTSUPP;                   // from-container with per-endpoint CT maps: not here
+    std::shared_ptr<Map> ct4m = cm.one(4), ct6m = cm.one(6);
     uint32_t strict = 0;
     gf_htab_desc cfg_ct4{}, cfg_ct6{};
     if ((r = ct_limits(ct4m, ct6m, n, 3, s, strict, cfg_ct4, cfg_ct6))) return r;

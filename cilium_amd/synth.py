@@ -868,6 +868,32 @@ def fuzz(seed=1, n_packets=20000, n_batches=3, stride=128, ct_max=100000, ct6_ma
     return sc
 
 
+def conntrack_local(sc, every=1, max_entries=None):
+    """The ConntrackLocal endpoint option (pkg/endpoint/bpf.go:268-276): every
+    `every`-th endpoint of the scenario binds CT maps of its own,
+    `<ct map>_<lxc_id>` (cilium_ct4_<id> / cilium_ct6_<id>), created like the map
+    it had (type, sizes, the prefilled entries copied), with `max_entries` if given;
+    the other endpoints keep the shared ones.  Returns the new map names."""
+    made = []
+    for j, e in enumerate(sc.lxc):
+        if j % every:
+            continue
+        for fam in ("ct4", "ct6"):
+            name = e.get(fam)
+            if not name:
+                continue
+            src = sc.maps[name]
+            local = f"{name}_{e['lxc_id']}"
+            keys = None if src.keys is None else src.keys.copy()
+            vals = None if src.vals is None else src.vals.copy()
+            if max_entries is not None and keys is not None and len(keys) > max_entries:
+                keys, vals = keys[:max_entries], vals[:max_entries]
+            sc.add_map(MapSpec(local, src.type, src.ksz, src.vsz, max_entries or src.max_entries, src.flags, keys, vals))
+            e[fam] = local
+            made.append(local)
+    return made
+
+
 def pipeline_fuzz(seed=3, n_packets=20000, n_batches=3, lb_redirect=False, fixed_secctx=None, proxy_max=524288):
     """The fuzz scenario run through the whole pipeline (bpf_xdp -> bpf_lb ->
     bpf_netdev -> handle_policy): endpoint MACs and port maps (duplicated and
