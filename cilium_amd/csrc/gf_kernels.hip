@@ -4101,9 +4101,18 @@ __device__ __forceinline__ int eg_policy(const gf_lxc_dev *c, uint32_t flags, ui
     return verdict;
 }
 
+// The from-container program's CT map (CT_MAP4 / CT_MAP6 of the sending endpoint):
+// the global one of the launch, or (PCT, ConntrackLocal) the program's own.
+template <int FAM, bool PCT>
+__device__ __forceinline__ gf_htab_desc eg_ct(const EgDev &E, const gf_lxc_dev *c) {
+    if constexpr (PCT) return gload<gf_htab_desc>(FAM == 6 ? &c->ct6 : &c->ct4);
+    else return FAM == 6 ? E.ct6 : E.ct4;
+}
+
 // The CT / policy part of handle_ipv4_from_lxc (bpf_lxc.c:499-658) for packet i.
 // Returns TC_OK / TC_REDIRECT / ND_TAILCALL (local delivery; ifx, lxc, mapped
 // filled) or an error.
+template <bool PCT>
 __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o, uint32_t &ifx,
                           uint32_t &lxc, int *added, bool seq, bool rlog, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
@@ -4126,8 +4135,8 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
     int e = ct_l4(nh, false, hr, t[2], tfl, action, syn);
     if (e < 0) return e;
     t[3] = nh | (tfl << 8);
-    const gf_htab_desc &ct = E.ct4;
     if (!(flags & GF_LXC_DEV_HAS_CT4)) return D_CT_CREATE_FAILED;   // (no CT map bound: never in a valid config)
+    const gf_htab_desc ct = eg_ct<4, PCT>(E, c);
     const bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     uint32_t tf[4] = {t[1], t[0], (t[2] >> 16) | (t[2] << 16), nh | ((tfl ^ 1u) << 8)};
     bool isb = false;
@@ -4188,6 +4197,10 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
                 lg[0] = i;
                 for (int k = 0; k < 4; k++) lg[1 + k] = t2[k];
                 for (int k = 0; k < 12; k++) lg[5 + k] = v[k];
+                if constexpr (PCT) {                    // the entry's map: its program and its slot array
+                    lg[17] = r.ep;
+                    lg[18] = (uint32_t)(uintptr_t)ct.slots; lg[19] = (uint32_t)((uintptr_t)ct.slots >> 32);
+                }
             }
         }
         uint32_t it[4] = {t[0], t[1], 0u, 1u | ((((t[3] >> 8) & 0xffu) | 2u) << 8)};
@@ -4317,6 +4330,7 @@ __device__ __forceinline__ int eg_ipv6_l3(Row &w, const uint32_t *smac, const ui
 
 // The CT / policy part of ipv6_l3_from_lxc (bpf_lxc.c:186-386) for packet i, on
 // the frame in HBM (extension headers may put the L4 header anywhere in the snap).
+template <bool PCT>
 __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint32_t i, Row &w, gf_egress_out &o,
                                            uint32_t &ifx, uint32_t &lxc, int *added, uint32_t &ab) {
     const uint32_t len = r.len, nh = r.nh;
@@ -4342,7 +4356,7 @@ __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint3
     if (e < 0) return e;
     t[9] = nh | (tfl << 8);
     if (!(flags & GF_LXC_DEV_HAS_CT6)) return D_CT_CREATE_FAILED;
-    const gf_htab_desc &ct = E.ct6;
+    const gf_htab_desc ct = eg_ct<6, PCT>(E, c);
     const bool acct = (flags & GF_LXC_F_CT_ACCOUNTING) != 0;
     uint32_t tf[10];
     for (int k = 0; k < 4; k++) { tf[k] = t[4 + k]; tf[4 + k] = t[k]; }
@@ -4492,7 +4506,9 @@ __device__ __forceinline__ int eg_ct_part6(const EgDev &E, const EgRec &r, uint3
 // handle_policy record + flow-group key of the ingress pass (rec2 / key2).
 // FAM 4 runs the schedule's family 0 (IPv4 buckets and every packet the front
 // finished), FAM 6 family 1 (IPv6); the two touch disjoint state.
-template <int FAM>
+// PCT: per-endpoint CT maps (ConntrackLocal): each packet's net element change goes
+// to its own program's map as the packet ends (ct_count unused).
+template <int FAM, bool PCT = false>
 __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32_t *sched, const uint2 *order, const uint32_t *perm,
                                                      const EgRec *erec, gf_egress_out *out, gf_rec *rec2, uint32_t *key2,
                                                      uint32_t *ct_count, unsigned long long *stats) {
@@ -4553,16 +4569,23 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
             PktHdr h2;                                  // the delivered header, re-parsed (local deliveries)
             if constexpr (v6) {                         // the frame in HBM
                 Row w{g, E.stride < r.len ? E.stride : r.len};
-                ret = eg_ct_part6(E, r, i, w, o, ifx, lxc, &added, ab);
+                ret = eg_ct_part6<PCT>(E, r, i, w, o, ifx, lxc, &added, ab);
                 if (ret == ND_TAILCALL) parse_row(w.p, w.cap, r.len, h2);
             } else {                                    // the LDS copy of the header bytes
                 eg_copy(row, g, K);
                 Row w{row, K < r.len ? K : r.len};
-                ret = eg_ct_part(E, r, i, w, o, ifx, lxc, &added, seq, rlog, ab);
+                ret = eg_ct_part<PCT>(E, r, i, w, o, ifx, lxc, &added, seq, rlog, ab);
                 if (ret == ND_TAILCALL) parse_row(w.p, w.cap, r.len, h2);
                 eg_copy(g, row, K);
             }
             o.ct_ret = o.eg_ct_ret;
+            if constexpr (PCT) {
+                if (added && !(E.strict & (FAM == 6 ? 2u : 1u))) {
+                    const gf_lxc_dev *c = E.cfgs + (r.ep - 1);
+                    atomicAdd(gload<uint32_t *>(FAM == 6 ? &c->ct6.count : &c->ct4.count), (uint32_t)added);
+                }
+                added = 0;
+            }
             if (ret == ND_ICMP6_TE) {                   // ipv6_l3 -> icmp6_send_time_exceeded: the reply goes out
                 ret = TC_REDIRECT; ifx = 0;
                 o.eg_flags |= GF_EG_F_ICMP6_TE;
@@ -4629,7 +4652,9 @@ __global__ __launch_bounds__(BLOCK, GF_EG_MINW) void k_eg_groups(EgDev E, uint32
 // the high half), so a key logged once — most of them — costs one atomic.
 // k_ctlog_apply walks the set's slots and upserts each key's winning entry.  Log
 // entry: [0] order, [1..4] the 14-B key, [5..16] the 48-B value.
+template <bool PCT = false>
 __device__ __forceinline__ bool ctlog_same(const uint32_t *a, const uint32_t *b) {
+    if (PCT && (a[18] != b[18] || a[19] != b[19])) return false;   // per-endpoint maps: the same map too
     return a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && (a[4] & 0xffffu) == (b[4] & 0xffffu);
 }
 // The set is sized for the entries actually logged (<= 1/2 load; the count is on
@@ -4643,6 +4668,7 @@ __device__ __forceinline__ uint32_t ctlog_mask(uint32_t n, uint32_t cap_mask) {
     while ((uint64_t)t + 1 < want && t < cap_mask) t = t * 2 + 1;
     return t < cap_mask ? t : cap_mask;
 }
+template <bool PCT = false>
 __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const uint32_t *n_, unsigned long long *tab,
                                                      uint32_t cap_mask) {
     const uint32_t n = *n_, tmask = ctlog_mask(n, cap_mask);
@@ -4650,7 +4676,9 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const u
     if (j >= n) return;
     const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * j;
     const unsigned long long want = ((unsigned long long)(e[0] + 1u) << 32) | j;
-    for (uint32_t p = key_hash<14, GF_HASH_CT>(e + 1) & tmask;; p = (p + 1) & tmask) {
+    uint32_t h0 = key_hash<14, GF_HASH_CT>(e + 1);
+    if constexpr (PCT) h0 ^= gf_hash_words(e + 18, 2, 8);   // (the same tuple in two maps: two keys)
+    for (uint32_t p = h0 & tmask;; p = (p + 1) & tmask) {
         // plain read first: a stale 0 only makes the CAS fail, a stale value only
         // costs the atomicMax it would have skipped
         unsigned long long cur = tab[p];
@@ -4658,14 +4686,17 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_max(const uint32_t *lg, const u
             cur = atomicCAS(&tab[p], 0ull, want);
             if (cur == 0ull) return;                    // claimed for this key
         }
-        if (ctlog_same(lg + (size_t)GF_CTLOG_WORDS * (uint32_t)cur, e)) {
+        if (ctlog_same<PCT>(lg + (size_t)GF_CTLOG_WORDS * (uint32_t)cur, e)) {
             if (cur < want) atomicMax(&tab[p], want);
             return;
         }
     }
 }
+// PCT: each entry into its program's own map (cfgs; ct, ct_count unused).
+template <bool PCT = false>
 __global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const uint32_t *n_, unsigned long long *tab,
-                                                       uint32_t cap_mask, gf_htab_desc ct, uint32_t *ct_count) {
+                                                       uint32_t cap_mask, gf_htab_desc ct, uint32_t *ct_count,
+                                                       const gf_lxc_dev *cfgs = nullptr) {
     const uint32_t tmask = ctlog_mask(*n_, cap_mask);
     int added = 0;
     for (uint64_t p = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; p <= tmask; p += (uint64_t)gridDim.x * BLOCK) {
@@ -4673,7 +4704,14 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const
         if (t == 0ull) continue;                        // an empty slot
         tab[p] = 0ull;                                  // the set is clean for its next use
         const uint32_t *e = lg + (size_t)GF_CTLOG_WORDS * (uint32_t)t;   // the key's last entry in order
-        ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
+        if constexpr (PCT) {
+            const gf_htab_desc d = gload<gf_htab_desc>(&cfgs[e[17] - 1].ct4);
+            int a = 0;
+            ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(d, e + 1, e + 5, false, &a);
+            if (a) atomicAdd(d.count, (uint32_t)a);
+        } else {
+            ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, e + 1, e + 5, false, &added);
+        }
     }
     if (!ct_count || !__any(added != 0)) return;
     uint32_t tot = (uint32_t)added;                     // one count add per wave
@@ -5816,7 +5854,6 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     // or per-endpoint maps (ConntrackLocal, ct_maps_of: the PCT kernels)
     CtMaps cm;
     if ((r = ct_maps_of(progs, cm))) return r;
-    if (cm.pct && ta && ta->kind == 2) return -EOPNOTSUPP;   // (egress_call refuses such an array first)
     std::shared_ptr<Map> ct4m = cm.pct ? nullptr : cm.one(4), ct6m = cm.pct ? nullptr : cm.one(6);
     // Strict (exact, atomic per insert) element accounting only when this batch could
     // reach the limit.  HASH maps are limited by max_entries (E2BIG).  LRU maps never
@@ -6632,8 +6669,9 @@ __global__ __launch_bounds__(256) void k_eg_init(uint32_t *seq, uint32_t *ctlog_
 // order (k_ctlog_max / k_ctlog_apply: the last writer of a key wins).
 // nlog: an upper bound of the entry count (*d_n, read by the kernels): no host
 // round trip for the count.
+// cfgs (per-endpoint CT maps): each entry into its program's own map instead of ct.
 static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32_t nlog, const gf_htab_desc &ct,
-                       uint32_t *ct_count, hipStream_t s) {
+                       uint32_t *ct_count, hipStream_t s, const gf_lxc_dev *cfgs = nullptr) {
     if (!nlog) return 0;
     uint32_t cap = 1023;                               // the set for the bound, at <= 1/2 load
     while ((uint64_t)cap + 1 < 2ull * nlog) cap = cap * 2 + 1;
@@ -6645,9 +6683,15 @@ static int ctlog_apply(EgWs &ew, const uint32_t *lg, const uint32_t *d_n, uint32
     ProfScope ps("k_ctlog_apply", s);
     const uint32_t gs = std::min<uint32_t>((cap + BLOCK) / BLOCK, 2048u);   // grid-stride over the set
     const uint32_t gl = (nlog + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ctlog_max, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap);
-    hipLaunchKernelGGL(k_ctlog_apply, dim3(gs), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap, ct,
-                       ct_count);
+    if (cfgs) {
+        hipLaunchKernelGGL(k_ctlog_max<true>, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap);
+        hipLaunchKernelGGL(k_ctlog_apply<true>, dim3(gs), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap,
+                           gf_htab_desc{}, nullptr, cfgs);
+    } else {
+        hipLaunchKernelGGL(k_ctlog_max<false>, dim3(gl), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p, cap);
+        hipLaunchKernelGGL(k_ctlog_apply<false>, dim3(gs), dim3(BLOCK), 0, s, lg, d_n, (unsigned long long *)ew.ckey.p,
+                           cap, ct, ct_count, nullptr);
+    }
     return hip_ok(hipGetLastError(), "k_ctlog_apply");
 }
 // One ordered run of an egress batch: check = run the ordering check first (a
@@ -6664,11 +6708,24 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     if ((r = prog_table(a, s, progs))) return r;
     CtMaps cm;
     if ((r = ct_maps_of(progs, cm))) return r;
-    if (cm.pct) return -EOPNOTSUPP;                   // from-container with per-endpoint CT maps: not here
-    std::shared_ptr<Map> ct4m = cm.one(4), ct6m = cm.one(6);
+    const bool pct = cm.pct;                           // per-endpoint CT maps (ConntrackLocal)
+    std::shared_ptr<Map> ct4m = pct ? nullptr : cm.one(4), ct6m = pct ? nullptr : cm.one(6);
     uint32_t strict = 0;
     gf_htab_desc cfg_ct4{}, cfg_ct6{};
     if ((r = ct_limits(ct4m, ct6m, n, 3, s, strict, cfg_ct4, cfg_ct6))) return r;
+    if (pct) {                                          // a family's bit: one of its maps could fill
+        gf_htab_desc d4{}, d6{};
+        for (auto &m : cm.m4) {
+            uint32_t st = 0;
+            if ((r = ct_limits(m, nullptr, n, 3, s, st, d4, d6))) return r;
+            strict |= st;
+        }
+        for (auto &m : cm.m6) {
+            uint32_t st = 0;
+            if ((r = ct_limits(nullptr, m, n, 3, s, st, d4, d6))) return r;
+            strict |= st;
+        }
+    }
     auto lxc = node_map(1), tun = node_map(2);
     if ((r = push_map(lxc, s)) || (r = push_map(tun, s))) return r;
     EgWs &ew = eg_ws();
@@ -6805,14 +6862,23 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         uint32_t grid = resident_blocks(8), need = (n + BLOCK - 1) / BLOCK;
         if (grid > need) grid = need;
         ProfScope ps("k_eg_groups", s);
-        hipLaunchKernelGGL(k_eg_groups<4>, dim3(grid), dim3(BLOCK), BLOCK * eg_row_bytes(S), s, E, (uint32_t *)w.sched.p,
-                           (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
-                           (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct4m ? (uint32_t *)ct4m->d_count.p : nullptr,
-                           sink);
-        hipLaunchKernelGGL(k_eg_groups<6>, dim3(grid), dim3(BLOCK), 16, s, E, (uint32_t *)w.sched.p,
-                           (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
-                           (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct6m ? (uint32_t *)ct6m->d_count.p : nullptr,
-                           sink);
+        if (pct) {
+            hipLaunchKernelGGL((k_eg_groups<4, true>), dim3(grid), dim3(BLOCK), BLOCK * eg_row_bytes(S), s, E,
+                               (uint32_t *)w.sched.p, (const uint2 *)w.order.p, (const uint32_t *)w.perm.p,
+                               (const EgRec *)ew.erec.p, out, (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, nullptr, sink);
+            hipLaunchKernelGGL((k_eg_groups<6, true>), dim3(grid), dim3(BLOCK), 16, s, E, (uint32_t *)w.sched.p,
+                               (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
+                               (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, nullptr, sink);
+        } else {
+            hipLaunchKernelGGL(k_eg_groups<4>, dim3(grid), dim3(BLOCK), BLOCK * eg_row_bytes(S), s, E,
+                               (uint32_t *)w.sched.p, (const uint2 *)w.order.p, (const uint32_t *)w.perm.p,
+                               (const EgRec *)ew.erec.p, out, (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p,
+                               ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, sink);
+            hipLaunchKernelGGL(k_eg_groups<6>, dim3(grid), dim3(BLOCK), 16, s, E, (uint32_t *)w.sched.p,
+                               (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const EgRec *)ew.erec.p, out,
+                               (gf_rec *)ew.rec2.p, (uint32_t *)ew.key2.p, ct6m ? (uint32_t *)ct6m->d_count.p : nullptr,
+                               sink);
+        }
         if ((r = hip_ok(hipGetLastError(), "k_eg_groups"))) return r;
     }
     uint32_t hz = 0, hz_first = 0;
@@ -6835,8 +6901,12 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     if (ct4m && (r = ctlog_apply(ew, (const uint32_t *)ew.ctlog.p, (const uint32_t *)ew.ctlog_n.p, n, cfg_ct4,
                                  (uint32_t *)ct4m->d_count.p, s)))
         return r;
-    if (ct4m) ct4m->device_modified();
-    if (ct6m) ct6m->device_modified();
+    if (pct && !cm.m4.empty() &&
+        (r = ctlog_apply(ew, (const uint32_t *)ew.ctlog.p, (const uint32_t *)ew.ctlog_n.p, n, gf_htab_desc{}, nullptr, s,
+                         (const gf_lxc_dev *)a->d_cfgs.p)))
+        return r;
+    for (auto *v : {&cm.m4, &cm.m6})
+        for (auto &m : *v) m->device_modified();
     // The egress redirects' cilium_proxy{4,6} updates stay in the log: the
     // deliveries' handle_policy appends theirs and the whole log is applied in
     // packet order after it (nothing on these paths reads the proxy maps).

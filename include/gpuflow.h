@@ -269,13 +269,14 @@ typedef struct gf_lxc_cfg {
     uint32_t seclabel;         /* SECLABEL */
     int policy_map;            /* POLICY_MAP (key policy_key 8 B, value policy_entry 24 B) */
     int ct_map4;               /* CT_MAP4 (key ipv4_ct_tuple 14 B, value ct_entry 48 B) */
-    int ct_map6;               /* CT_MAP6 (key ipv6_ct_tuple 40 B, value ct_entry 48 B).  The programs of one
-                                  classify call share one CT map per family (the agent's default,
-                                  cilium_ct4_global / cilium_ct6_global, pkg/endpoint/bpf.go:268-276): the
-                                  lane-quad CT probes and the per-launch insert accounting are per map, so a
-                                  call whose programs bind different CT maps (ConntrackLocal endpoints,
-                                  cilium_ct4_<id>) returns -EOPNOTSUPP; such endpoints classify in calls of
-                                  their own (a policy array per CT map). */
+    int ct_map6;               /* CT_MAP6 (key ipv6_ct_tuple 40 B, value ct_entry 48 B).  Either every
+                                  program binds the same map per family (the agent's default,
+                                  cilium_ct4_global / cilium_ct6_global) or programs bind maps of their own
+                                  (the ConntrackLocal option, cilium_ct4_<id>, pkg/endpoint/bpf.go:268-276),
+                                  mixed freely in one array.  With more than one map per family a call runs
+                                  the per-endpoint kernels: each packet's program's own map, inserts counted
+                                  into that map, the LRU eviction pass on each map after the call.  One map
+                                  bound as both a CT_MAP4 and a CT_MAP6: -EINVAL. */
     int cidr4_ingress_map;     /* CIDR4_INGRESS_MAP (LPM_TRIE), 0 = undefined */
     int cidr6_ingress_map;     /* CIDR6_INGRESS_MAP (LPM_TRIE), 0 = undefined */
     int revnat4_map;           /* cilium_lb4_reverse_nat (key u16, value 6 B) */

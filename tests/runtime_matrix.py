@@ -117,6 +117,11 @@ def compile_case(case, topo, ct_max=1 << 16):
     always = case["enforcement"] == "always"
     sc.add_map(S.MapSpec("ct4", S.LRU_HASH, 14, 48, ct_max))
     sc.add_map(S.MapSpec("ct6", S.LRU_HASH, 40, 48, ct_max))
+    # endpoints with the ConntrackLocal option: CT maps of their own (pkg/endpoint/bpf.go:268-276)
+    local = set(case.get("conntrack_local", []))
+    for n in sorted(local):
+        sc.add_map(S.MapSpec(f"ct4_{n}", S.LRU_HASH, 14, 48, ct_max))
+        sc.add_map(S.MapSpec(f"ct6_{n}", S.LRU_HASH, 40, 48, ct_max))
     names = topo.names
     ip4 = np.array([topo.ip4[n] for n in names], np.uint32)
     ip6 = np.array([np.frombuffer(topo.ip6[n], np.uint8) for n in names])
@@ -169,7 +174,8 @@ def compile_case(case, topo, ct_max=1 << 16):
         else:
             pk, pv = np.zeros((0, 8), np.uint8), np.zeros((0, 24), np.uint8)
         sc.add_map(S.MapSpec(f"pol_{n}", S.HASH, 8, 24, 16384, 0, pk if len(pk) else None, pv if len(pv) else None))
-        cfg = {"lxc_id": topo.lxc_id[n], "seclabel": topo.ident[n], "policy": f"pol_{n}", "ct4": "ct4", "ct6": "ct6",
+        ct4, ct6 = (f"ct4_{n}", f"ct6_{n}") if n in local else ("ct4", "ct6")
+        cfg = {"lxc_id": topo.lxc_id[n], "seclabel": topo.ident[n], "policy": f"pol_{n}", "ct4": ct4, "ct6": ct6,
                "flags": S.LXC_HAVE_L4_POLICY | S.LXC_CT_ACCOUNTING | S.LXC_LXC_IPV4
                | (S.LXC_POLICY_INGRESS if pol_in else 0) | (S.LXC_POLICY_EGRESS if pol_eg else 0),
                "lxc_mac": topo.mac[n], "node_mac": NODE_MAC, "lxc_ipv4": raw_be(topo.ip4[n]),

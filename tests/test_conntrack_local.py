@@ -8,7 +8,6 @@ CPU: the oracle's per-endpoint semantics (each program's CT_MAP4 / CT_MAP6, bpf_
 ct_lookup4/ct_create4 on &CT_MAP4).  GPU: libgpuflow's per-endpoint kernels
 (k_ing_groups<FAM, 1, true>) against the oracle, records and every CT map bit-exact.
 """
-import errno
 
 import numpy as np
 import pytest
@@ -140,16 +139,31 @@ def test_gpu_conntrack_local_batches_api():
 
 
 @pytest.mark.gpu
-def test_gpu_conntrack_local_egress_refused():
-    """from-container with per-endpoint CT maps is not implemented: the egress call
-    says so (-EOPNOTSUPP) and changes nothing."""
+@pytest.mark.parametrize("seed,every,kw", [(5, 1, {"hazard": False}), (6, 2, {"hazard": True}),
+                                           (11, 1, {"hazard": False, "icmp": False}), (12, 3, {"hazard": True})])
+def test_gpu_conntrack_local_egress(seed, every, kw):
+    """From-container (handle_ipv4_from_lxc / ipv6_l3_from_lxc on the sender's own
+    CT_MAP4 / CT_MAP6, service entries included) and the local deliveries'
+    handle_policy on the receiver's maps: records, rewritten frames, every CT map,
+    policy counters and proxy maps equal the oracle's."""
     _gpu()
-    from cilium_amd.datapath import Datapath, DeviceBatch
-    sc = synth.egress_fuzz(seed=5, n_packets=2000, n_batches=1, hazard=False)
-    synth.conntrack_local(sc, every=2)
-    dp = Datapath(sc, pin_prefix=None)
-    before = dp.dump_map("ct4")
-    with pytest.raises(OSError) as ei:
-        dp.egress(DeviceBatch(sc.batches[0], parse=False), sc.now)
-    assert ei.value.errno == errno.EOPNOTSUPP
-    assert dp.dump_map("ct4") == before
+    from cilium_amd.datapath import Datapath, DeviceBatch, EG_OUT, to_numpy
+    sc = synth.egress_fuzz(seed=seed, n_packets=20000, n_batches=3, **kw)
+    made = synth.conntrack_local(sc, every=every)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    for bi, pk in enumerate(sc.batches):
+        out, snap = dp.egress(DeviceBatch(pk, parse=False), sc.now + bi)
+        torch.cuda.synchronize()
+        ro, rs = ref.egress(pk, sc.now + bi)
+        got = to_numpy(out, EG_OUT)
+        bad = np.nonzero(got != ro)[0]
+        assert len(bad) == 0, f"egress b{bi}: {len(bad)} records differ, first {bad[:1]}"
+        assert not (snap.cpu().numpy() != rs).any(), f"frames b{bi}"
+    for name in made + ["ct4", "ct6"]:
+        assert dp.dump_map(name) == ref.dump(name), name
+    grown = [n for n in made if n.startswith("ct4_") and len(ref.dump(n))]
+    assert grown, "the senders' own maps should hold their connections"
+    for e in range(16):
+        assert dp.dump_map(f"pol{e}") == ref.dump(f"pol{e}"), f"pol{e}"
+    assert dp.dump_map("cilium_proxy4") == ref.dump("cilium_proxy4")
+    assert dp.dump_map("cilium_proxy6") == ref.dump("cilium_proxy6")

@@ -84,7 +84,8 @@ def test_gpu_one_batch_request_and_reply_ordered():
             bad, first = PY.compare_records(g, o)
             assert bad == 0, (case["name"], first, g[first], o[first])
             assert not RM.outcome_mismatches(case, gres), case["name"]
-            for name, ksz in (("ct4", 14), ("ct6", 40)):
+            cts = [(m, 14 if m.startswith("ct4") else 40) for m in ref.dp.m if m.startswith(("ct4", "ct6"))]
+            for name, ksz in cts:
                 gk, gv = gpu.dump(name, ksz)
                 ok, ov = ref.dp.m[name].dump_arrays()
                 n, badc = PY.compare_tables(gk, gv, ok, ov)
@@ -116,16 +117,24 @@ def test_gpu_matches_reference_matrix_and_oracle():
             assert bad == 0, (case["name"], kind, step, g[first], o[first])
 
 
-def test_conntrack_case_replies_pass_on_the_ct():
-    """RuntimeValidatedConntrackTest (connectivity.go:294-478): the server's replies
-    leave it under PolicyEnforcement=always with no egress rule of its own, and enter
-    the client with no ingress rule, only because both CT lookups find the request's
-    entries (CT_REPLY on the server's from-container lookup and on the client's
-    handle_policy); a new connection the other way (server -> client ping) is dropped
-    by the server's egress policy (DROP_POLICY)."""
-    case = next(c for c in CASES if c["name"].startswith("Conntrack"))
+CT_CASES = [c for c in CASES if c["name"].startswith("Conntrack")]
+
+
+@pytest.mark.parametrize("case", CT_CASES, ids=[c["name"] for c in CT_CASES])
+def test_conntrack_case_replies_pass_on_the_ct(case):
+    """RuntimeValidatedConntrackTest (connectivity.go:294-478), ConntrackLocal off and
+    on (:672-690): the server's replies leave it under PolicyEnforcement=always with no
+    egress rule of its own, and enter the client with no ingress rule, only because
+    both CT lookups find the request's entries (CT_REPLY on the server's from-container
+    lookup and on the client's handle_policy); a new connection the other way (server
+    -> client ping) is dropped by the server's egress policy (DROP_POLICY).  With the
+    option on, those entries are in the server's and the client's own maps."""
     topo = RM.Topology(RM.case_endpoints(DOC, case))
-    res, log = RM.run_case(case, topo, RM.OracleBackend(RM.compile_case(case, topo)))
+    be = RM.OracleBackend(RM.compile_case(case, topo))
+    res, log = RM.run_case(case, topo, be)
+    local = case.get("conntrack_local", [])
+    for n in local:
+        assert len(be.dp.dump(f"ct4_{n}")) and len(be.dp.dump(f"ct6_{n}")), n
     assert not RM.outcome_mismatches(case, res)
     flows = [RM.Flow(j, c, s, r) for j, (c, s, r, _) in enumerate(RM.expand(case))]
     # wave 1 holds the second packet of every flow that survived wave 0, in flow order
