@@ -1282,7 +1282,7 @@ EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_
 #            frac = the largest of the four: the kind closest to its own ceiling.
 ISSUE_PEAK = 256 * 4 * 2.4e9
 MEM_CEIL = {"line_reads": 54.0e9, "partial_writes": 21.7e9, "full_writes_64B": 60.5e9, "atomics": 17.3e9}
-PMC_ROUND = "r5"          # the round whose per-kernel PMC summaries price this run (built from the same sources)
+PMC_ROUND = "r6"          # the round whose per-kernel PMC summaries price this run (built from the same sources)
 PMC_KERNELS = {"2": ["k_ing_groups"], "1": ["k_xdp", "k_xdp_lds"], "3": ["k_lb"]}   # else: every kernel
 
 
