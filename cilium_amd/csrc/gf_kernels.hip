@@ -781,6 +781,23 @@ __global__ __launch_bounds__(BLOCK) void k_lb(gf_pkt_cols c, LbDev L, gf_lb_out 
 #ifndef GF_POUT_WO
 #define GF_POUT_WO 1        // gf_pipeline_classify: complete the records without reading them (IngCtx::pout_wo)
 #endif
+#ifndef GF_EG_RSET
+#define GF_EG_RSET 1        // egress connection groups: related entries through RelSet (0: the r5 write log)
+#endif
+// The ICMP-related entries of an egress connection-group run: the
+// only CT keys two connections of one address pair share, written (BPF_ANY) by every
+// new connection of the pair in both passes and read by nothing in the run.  Only the
+// last write of each key in batch order survives, so each write enters its key here
+// instead of a log: the key {daddr, saddr} of the related tuple (its ports are 0 and
+// its flags byte is 2 | direction, which picks one of the slot's two words) claims a
+// slot (open addressing, 0 = empty; key 0 has the extra slot mask + 1), and the word
+// keeps 1 + the highest order written (2i: packet i's from-container create, 2i + 1:
+// its delivery's).  k_rset_apply rebuilds each winner's value from its packet.
+struct RelSet {
+    unsigned long long *slot;          // mask + 2 slots of 16 B: the key, then its two words
+    uint32_t *list, *list_n;           // the claimed slots, for the apply
+    uint32_t mask;
+};
 struct IngCtx {
     const gf_lxc_dev *cfgs;
     const uint8_t *saddr6, *daddr6;
@@ -800,6 +817,7 @@ struct IngCtx {
     uint8_t *tmark, *tcap;     // trace notifications: per-packet GF_TR_* marks, 128-B captures (null: off)
     uint32_t *rlog, *rlog_n;   // egress connection groups: ct_create4's related entries logged (null: written)
     const uint32_t *rlog_off;  // device word: nonzero = the run fell back to pair groups (entries written inline)
+    RelSet rs;                 // GF_EG_RSET: the related entries' set (rlog non-null: in use)
 };
 
 // ---- handle_policy's own header writes (kept out of line: cold paths of the
@@ -1132,6 +1150,34 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t *ctr) {
     base = __shfl(base, (int)lead);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+// One related-entry write into the run's set (RelSet).
+__device__ __forceinline__ void rset_put(const RelSet &R, uint32_t w0, uint32_t w1, uint32_t side, uint32_t order) {
+    const unsigned long long k = ((unsigned long long)w0 << 32) | w1;
+    uint32_t p;
+    const uint32_t want = order + 1u;
+    uint32_t seen = 0;                                  // the key's word as last read (stale: lower)
+    if (k == 0ull) {
+        p = R.mask + 1u;
+        if (atomicCAS(&R.slot[2u * p], 0ull, 1ull) == 0ull) R.list[atomicAdd(R.list_n, 1u)] = p;
+    } else {
+        const uint32_t w[2] = {w0, w1};
+        p = gf_hash_words(w, 2, 8) & R.mask;
+        for (;;) {
+            // plain read first (key and words together): within a run a key only goes
+            // from 0 to its value and a word only up, so a stale read only makes the
+            // CAS fail or costs the atomicMax it would have skipped
+            const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2u * p);
+            unsigned long long cur = ((unsigned long long)sl.y << 32) | sl.x;
+            if (cur == 0ull) {
+                cur = atomicCAS(&R.slot[2u * p], 0ull, k);
+                if (cur == 0ull) { R.list[atomicAdd(R.list_n, 1u)] = p; break; }
+            }
+            if (cur == k) { seen = side ? sl.w : sl.z; break; }
+            p = (p + 1u) & R.mask;
+        }
+    }
+    if (seen < want) atomicMax(reinterpret_cast<uint32_t *>(R.slot + 2u * p + 1u) + side, want);
+}
 
 // ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0).  The
 // tuple goes to the EMPTY slot the lookup walk ended on (one CAS), the related
@@ -1142,7 +1188,7 @@ template <int KSZ, int TW, int U>
 __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uint32_t rev_nat, uint32_t src_sec,
                                          uint32_t len, uint32_t now, bool strict, const ProbeRes &pr, int *added,
                                          RelCache<TW> &rc, uint32_t &ab, uint32_t *rlog = nullptr,
-                                         uint32_t *rlog_n = nullptr, uint32_t order = 0) {
+                                         uint32_t *rlog_n = nullptr, uint32_t order = 0, const RelSet *rs = nullptr) {
     constexpr int NHW = TW - 1;                         // word holding nexthdr | flags << 8
     ab += 2 * (KSZ + 48);                               // tuple + ICMP-related entry written
     uint32_t nh = t[NHW] & 0xffu, tfl = (t[NHW] >> 8) & 0xffu;
@@ -1160,6 +1206,10 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
     if constexpr (KSZ == 14) if (rlog) {                // connection groups: applied after the run, in order
         GF_WR(WR_RLOG);
+        if (GF_EG_RSET) {
+            rset_put(*rs, it[0], it[1], (it[NHW] >> 8) & 1u, order);
+            return 0;
+        }
         uint32_t *lg = rlog + (size_t)20 * wave_reserve(rlog_n);
         lg[0] = order;
 #pragma unroll
@@ -1515,8 +1565,10 @@ __device__ __attribute__((noinline)) void pol_redirect_ol(PolCtx X, uint32_t i, 
 }
 
 // ipv4_policy, bpf/bpf_lxc.c:865-970
-// rlog: X.rlog unless the run fell back to pair groups (read once per kernel, k_ing_groups)
-template <bool PCT>
+// rlog: X.rlog unless the run fell back to pair groups (read once per kernel, k_ing_groups);
+// RL: the instance has the egress connection groups' related-entry path at all (the
+// egress deliveries' pass), kept out of the others' registers
+template <bool PCT, bool RL = false>
 __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i, int &fwd, uint8_t &ofl, uint16_t &proxy,
                            uint32_t &ifindex, int *added, uint32_t &ab, PolAcc &acc, RelCache<4> &rc, PolMemo<GF_MEMO4> &pm,
                            uint32_t *rlog) {
@@ -1578,7 +1630,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     if (r.cls & 4) verdict = 0;                         // skip_proxy
     if (ret == CT_NEW && !(GF_DIAG & 8)) {
         ret = ct_create<14, 4, GF_CT4_U>(ct, t, 0u, r.src_identity, len, X.now, X.strict & 1, pr, added, rc, ab,
-                                         rlog, X.rlog_n, 2u * i + 1u);
+                                         RL ? rlog : nullptr, X.rlog_n, 2u * i + 1u, &X.rs);
         if (ret < 0) return ret;
         ofl |= GF_INGRESS_F_CREATED;
     }
@@ -1725,7 +1777,7 @@ struct Lane {
 // 4 = the IPv4 path plus every packet that cannot reach conntrack (no IP
 // header: their early returns need no CT code), 6 = IPv6 packets that reach
 // conntrack.  The sort key keeps the two sets in different buckets.
-template <int FAM, bool PCT>
+template <int FAM, bool PCT, bool RL>
 __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const gf_rec &r, uint32_t i, Lane<FAM> &ln,
                                                        uint32_t &ab, uint32_t *rlog) {
     gf_ingress_out o{};
@@ -1746,7 +1798,7 @@ __device__ __forceinline__ gf_ingress_out handle_policy(const IngCtx &X, const g
     }
     else if (cls == 1 && (flags & GF_LXC_F_LXC_IPV4)) {
         ab += 23;
-        if constexpr (FAM == 4) ret = ipv4_policy<PCT>(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm,
+        if constexpr (FAM == 4) ret = ipv4_policy<PCT, RL>(X, ln.ep, r, i, fwd, fl, proxy, ifindex, &ln.added, ab, ln.acc, ln.rc, ln.pm,
                                                   rlog);
         else ret = D_INVALID;                       // (not reached: v4 packets sort into FAM 4 buckets)
     }
@@ -1822,12 +1874,12 @@ __global__ __launch_bounds__(BLOCK) void k_ing_pack(gf_pkt_cols c, const uint16_
 // (LPT): k_bucket_order lists them by packet count, descending, and waves take
 // the next 64 entries of that list from a device queue, so the lanes of a wave
 // carry equal work and the deepest buckets start first.
-template <int FAM, bool PCT>
+template <int FAM, bool PCT, bool RL>
 __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_rec &r, gf_ingress_out *out,
                                         Stats &st, bool stats, Lane<FAM> &ln, uint32_t *rlog) {
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy<FAM, PCT>(X, r, i, ln, ab, rlog);
+    gf_ingress_out o = handle_policy<FAM, PCT, RL>(X, r, i, ln, ab, rlog);
     if constexpr (PCT) {
         // per-endpoint CT maps: the lane's related-entry cache is the packet's own
         // (the next packet of the bucket may be another endpoint's, another map)
@@ -1923,7 +1975,7 @@ __device__ __forceinline__ uint32_t sched_list(uint32_t key, const gf_rec *rec, 
 // GRAB: buckets per lane per queue grab in the single-packet tail (GF_GRAB_ING for the
 // egress deliveries' pass, whose buckets are mostly single packets; 1 elsewhere,
 // where the extra state costs the kernel registers it cannot spare)
-template <int FAM, int GRAB = 1, bool PCT = false>
+template <int FAM, int GRAB = 1, bool PCT = false, bool RL = false>
 __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void k_ing_groups(IngCtx X, uint32_t *sched, const uint2 *order,
                                                       const uint32_t *perm,
                                                       const gf_rec *rec, gf_ingress_out *out, uint32_t *ct_count,
@@ -1941,7 +1993,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
     __shared__ Lane<FAM> lanes[BLOCK];
     Lane<FAM> &ln = lanes[threadIdx.x];
     ln.init();
-    uint32_t *const rlog = X.rlog && !(X.rlog_off && *X.rlog_off) ? X.rlog : nullptr;
+    uint32_t *const rlog = RL && X.rlog && !(X.rlog_off && *X.rlog_off) ? X.rlog : nullptr;
     const uint32_t x0 = blockIdx.x % GF_NCLS;           // this workgroup's XCD class first
     for (uint32_t xi = 0; xi < GF_NCLS; xi++) {
     const uint32_t L = F * GF_NCLS + (x0 + xi) % GF_NCLS;
@@ -1997,7 +2049,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
 #else
             if (k + 2 < c) in2 = perm[b + k + 2];
 #endif
-            ing_one<FAM, PCT>(X, i, r, out, st, stats != nullptr, ln, rlog);
+            ing_one<FAM, PCT, RL>(X, i, r, out, st, stats != nullptr, ln, rlog);
             i = inx; inx = in2;
             if (k + 1 < c) r = ld_rec(rec, i);
         }
@@ -3398,6 +3450,7 @@ struct EgDev {
     uint32_t *cflag;                    // device word: 1 = pair groups (an IPv4 ICMP packet reaches conntrack)
     uint32_t *keysP, *key2P;            // the pair keys of the front / of the deliveries (fallback)
     uint32_t *rlog, *rlog_n;            // logged related entries {order, key[4], value[12], pad[3]}
+    RelSet rs;                          // GF_EG_RSET: their set instead
     gf_rec *rec2;                       // the handle_policy pass's records: the front writes every packet's
     uint32_t *key2;                     //   as "not delivered" in batch order, k_eg_groups only the deliveries
 };
@@ -4205,7 +4258,9 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
         }
         uint32_t it[4] = {t[0], t[1], 0u, 1u | ((((t[3] >> 8) & 0xffu) | 2u) << 8)};
         v[1] |= F_SEEN_NON_SYN;
-        if (rlog) {                                     // applied after the run, in packet order (the pair's
+        if (rlog && GF_EG_RSET) {                       // the run's set (RelSet), applied after the run
+            rset_put(E.rs, it[0], it[1], (it[3] >> 8) & 1u, 2u * i);
+        } else if (rlog) {                              // applied after the run, in packet order (the pair's
             uint32_t *lg = E.rlog + (size_t)GF_CTLOG_WORDS * wave_reserve(E.rlog_n);   // other connections
             lg[0] = 2u * i;                                                             // never read it)
             for (int k = 0; k < 4; k++) lg[1 + k] = it[k];
@@ -4719,6 +4774,51 @@ __global__ __launch_bounds__(BLOCK) void k_ctlog_apply(const uint32_t *lg, const
     if ((threadIdx.x & 63u) == 0u) atomicAdd(ct_count, tot);
 }
 
+// The winners of a connection-group run's related-entry set (RelSet), written after
+// the run: each claimed slot's one or two keys get the value their last writer's
+// ct_create4 builds (conntrack.h:563-577) — order 2i: packet i's from-container create
+// (the sender's SECLABEL and tx counters, bpf_lxc.c:534), 2i + 1: its delivery's
+// handle_policy create (src_sec_id the source identity, rx counters, bpf_lxc.c:941) —
+// and the slot is left zero for the next run.
+__global__ __launch_bounds__(BLOCK) void k_rset_apply(RelSet R, const EgRec *erec, const gf_rec *rec,
+                                                      const gf_lxc_dev *cfgs, gf_htab_desc ct, uint32_t *ct_count,
+                                                      uint32_t now) {
+    const uint32_t n = *R.list_n;
+    int added = 0;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
+        const uint32_t p = R.list[j];
+        const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2u * p);
+        const unsigned long long k = p == R.mask + 1u ? 0ull : ((unsigned long long)sl.y << 32) | sl.x;
+        for (uint32_t side = 0; side < 2; side++) {
+            const uint32_t w = side ? sl.w : sl.z;
+            if (!w) continue;
+            const uint32_t o = w - 1u, i = o >> 1;
+            const uint32_t it[4] = {(uint32_t)(k >> 32), (uint32_t)k, 0u, 1u | ((2u | side) << 8)};
+            uint32_t v[12] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            if (o & 1u) {                               // handle_policy (rev_nat 0 on ingress)
+                const gf_rec r = rec[i];
+                const uint32_t fl = r.proto == 6 ? 0u : F_SEEN_NON_SYN;
+                v[0] = now + ((fl & F_SEEN_NON_SYN) ? 43200u : 300u);
+                v[1] = fl | F_SEEN_NON_SYN;
+                v[2] = 1u; v[3] = r.len; v[11] = r.src_identity;
+            } else {                                    // from-container
+                const EgRec r = erec[i];
+                uint32_t efl = r.nh == 6 ? 0u : F_SEEN_NON_SYN;
+                if (r.eflags & GF_EG_F_LOOPBACK) efl |= F_LB_LOOPBACK;
+                v[0] = now + ((efl & F_SEEN_NON_SYN) ? 43200u : 300u);
+                v[1] = efl | F_SEEN_NON_SYN | ((uint32_t)r.rev_nat << 16);
+                v[6] = 1u; v[8] = r.len; v[11] = gload<uint32_t>(&cfgs[r.ep - 1].seclabel);
+            }
+            ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, it, v, false, &added);
+        }
+        *reinterpret_cast<uint4 *>(R.slot + 2u * p) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (!ct_count || !__any(added != 0)) return;
+    uint32_t tot = (uint32_t)added;                     // one count add per wave
+    for (int d = 32; d >= 1; d >>= 1) tot += (uint32_t)__shfl_xor((int)tot, d);
+    if ((threadIdx.x & 63u) == 0u) atomicAdd(ct_count, tot);
+}
+
 // ================================================================ host: programs
 namespace {
 
@@ -5225,6 +5325,7 @@ struct PassArgs {                  // what the pipeline / egress callers pass to
     uint32_t kind;                 // 1 pipeline, 2 egress
     uint32_t *rlog, *rlog_n;       // egress connection groups: the related-entry log (null: written inline)
     const uint32_t *rlog_off;      // device word: the run fell back to pair groups (the log is not used)
+    RelSet rs;                     // GF_EG_RSET: the related entries' set (rlog then only marks it in use)
     bool on;                       // this call traces (a ring is set and a program / the netdev traces)
     uint32_t nd_trace, nd_ifindex; // pipeline: GF_NETDEV_F_TRACE_NOTIFY, skb->ingress_ifindex
     const uint8_t *orig;           // egress: the frames as sent
@@ -5906,7 +6007,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     X.gw = node.ipv4_gateway;
     memcpy(X.host6, node.host_ip6, 16);
     if (tracing) { X.tmark = (uint8_t *)trace_ws().mark.p; X.tcap = (uint8_t *)trace_ws().px.p; }
-    if (ta) { X.rlog = ta->rlog; X.rlog_n = ta->rlog_n; X.rlog_off = ta->rlog_off; }
+    if (ta) { X.rlog = ta->rlog; X.rlog_n = ta->rlog_n; X.rlog_off = ta->rlog_off; X.rs = ta->rs; }
     if ((r = px_log_begin(n, s, X, px_keep))) return r;
     // Non-strict mode accounts each kernel's net element change into its family's map.
     uint32_t *cnt4 = ct4m ? (uint32_t *)ct4m->d_count.p : nullptr, *cnt6 = ct6m ? (uint32_t *)ct6m->d_count.p : nullptr;
@@ -5923,7 +6024,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
                                    (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out,
                                    nullptr, sink);
             else if (X.pol_wave)                        // the egress deliveries' pass (single-packet buckets)
-                hipLaunchKernelGGL((k_ing_groups<4, GF_GRAB_ING>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
+                hipLaunchKernelGGL((k_ing_groups<4, GF_GRAB_ING, false, true>), dim3(grid), dim3(BLOCK), 0, s, X, d_sched,
                                    (const uint2 *)w.order.p, (const uint32_t *)w.perm.p, (const gf_rec *)w.rec.p, out, cnt4,
                                    sink);
             else
@@ -6574,7 +6675,8 @@ int dev_dump(Map &m, uint64_t start, uint32_t max, uint8_t *keys, uint8_t *vals,
 // ---- endpoint egress (from-container) ----
 namespace {
 struct EgWs { DevBuf erec, rec2, key2, seq, ctlog, ctlog_n, snap, ckey, s6, d6,
-             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n, v6blk;
+             hzk, hzfl, hztk, hztf, hzak, hzaf, hzst, vip4, vip6, keysP, key2P, rlog, rlog_n, v6blk,
+             rsslot, rslist;
              uint32_t hz_gen = 0, hz_cap = 0;
              uint32_t *h_hz = nullptr;          // pinned: the ordering check's words, read back without a stream sync
              hipEvent_t ev_hz = nullptr;
@@ -6788,12 +6890,29 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     uint32_t *d_rn = nullptr;                          // [0] related entries logged, [1] pair-group fallback
     if (conn) {
         if ((r = grow(ew.keysP, (size_t)n * 4)) || (r = grow(ew.key2P, (size_t)n * 4)) || (r = grow(ew.rlog_n, 8)) ||
-            (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4)))
+            (!GF_EG_RSET && (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4))))
             return r;
         d_rn = (uint32_t *)ew.rlog_n.p;
         E.conn = 1; E.cflag = d_rn + 1;
         E.keysP = (uint32_t *)ew.keysP.p; E.key2P = (uint32_t *)ew.key2P.p;
         E.rlog = (uint32_t *)ew.rlog.p; E.rlog_n = d_rn;
+        if (GF_EG_RSET) {
+            // the set: <= 2n related writes (one per new connection in each pass), so
+            // 4n slots keep it at most half full; zeroed when allocated, and left zero
+            // by k_rset_apply, which clears every slot a run claimed
+            uint64_t ns = 1024;
+            while (ns < 4ull * n) ns *= 2;
+            if (ns > (1ull << 31)) return -E2BIG;
+            const size_t sb = (size_t)(ns + 1) * 16;
+            if (ew.rsslot.bytes < sb) {
+                if (ew.rsslot.ensure(sb)) return -ENOMEM;
+                if (hip_ok(hipMemsetAsync(ew.rsslot.p, 0, sb, s), "related set")) return -EIO;
+            }
+            if ((r = grow(ew.rslist, (size_t)2 * n * 4 + 4))) return r;
+            E.rs.slot = (unsigned long long *)ew.rsslot.p;
+            E.rs.list = (uint32_t *)ew.rslist.p; E.rs.list_n = d_rn; E.rs.mask = (uint32_t)(ns - 1);
+            E.rlog = E.rs.list;                          // (marks the set in use for the deliveries' pass)
+        }
     }
     uint32_t *d_hz = (uint32_t *)ew.seq.p + 1;           // word 1 of the seq buffer: the hazard flag
     if (check) {
@@ -6932,13 +7051,22 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
         }
         return 0;
     };
-    if (conn) { ta.rlog = (uint32_t *)ew.rlog.p; ta.rlog_n = d_rn; ta.rlog_off = E.cflag; }
+    if (conn) { ta.rlog = E.rlog; ta.rlog_n = d_rn; ta.rlog_off = E.cflag; ta.rs = E.rs; }
     if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru && !conn, true,
                          false, &ta)))
         return r;
-    if (conn) {                                        // both passes' related entries, in packet order
+    if (conn && GF_EG_RSET) {                          // both passes' related entries: each key's last writer
+        ProfScope ps("k_ctlog_apply", s);
+        // the deliveries' records are the workspace's now (the pack swap above)
+        hipLaunchKernelGGL(k_rset_apply, dim3(std::min<uint32_t>(grid_for(2 * n), 2048u)), dim3(BLOCK), 0, s, E.rs,
+                           (const EgRec *)ew.erec.p, (const gf_rec *)ws().rec.p, E.cfgs, cfg_ct4,
+                           (uint32_t *)ct4m->d_count.p, now_sec);
+        if ((r = hip_ok(hipGetLastError(), "k_rset_apply"))) return r;
+    } else if (conn) {                                 // both passes' related entries, in packet order
         if ((r = ctlog_apply(ew, (const uint32_t *)ew.rlog.p, d_rn, 2 * n, cfg_ct4, (uint32_t *)ct4m->d_count.p, s)))
             return r;
+    }
+    if (conn) {
         ct4m->device_modified();
         if (lru && ((r = lru_evict(ct4m, now_sec, s)) || (r = lru_evict(ct6m, now_sec, s)))) return r;
     }
