@@ -41,9 +41,10 @@ def short(name):
         return "rocprim"
     if s.startswith("k_ing_groups") or s.startswith("k_eg_"):
         # the family template argument names the kernel (k_ing_groups / k_ing_groups6);
-        # a second one (k_ing_groups' queue grab) does not; the per-endpoint-CT
-        # instances (a last `true`) are k_ing_groups_pct / k_ing_groups6_pct
-        s = re.sub(r"<([46])(, *\d+)?(, *(true|false))?>",
+        # a second one (k_ing_groups' queue grab) does not; of the flags after it, the
+        # first (per-endpoint CT maps) names the _pct instances, the second (the egress
+        # related-entry set) does not
+        s = re.sub(r"<([46])(, *\d+)?(, *(true|false))?(, *(true|false))?>",
                    lambda m: ("6" if m.group(1) == "6" else "") + ("_pct" if m.group(4) == "true" else ""), s)
     return s
 
