@@ -1158,7 +1158,7 @@ __device__ __forceinline__ void rset_put(const RelSet &R, uint32_t w0, uint32_t 
     uint32_t seen = 0;                                  // the key's word as last read (stale: lower)
     if (k == 0ull) {
         p = R.mask + 1u;
-        if (atomicCAS(&R.slot[2u * p], 0ull, 1ull) == 0ull) R.list[atomicAdd(R.list_n, 1u)] = p;
+        if (atomicCAS(&R.slot[2ull * p], 0ull, 1ull) == 0ull) R.list[atomicAdd(R.list_n, 1u)] = p;
     } else {
         const uint32_t w[2] = {w0, w1};
         p = gf_hash_words(w, 2, 8) & R.mask;
@@ -1166,17 +1166,17 @@ __device__ __forceinline__ void rset_put(const RelSet &R, uint32_t w0, uint32_t 
             // plain read first (key and words together): within a run a key only goes
             // from 0 to its value and a word only up, so a stale read only makes the
             // CAS fail or costs the atomicMax it would have skipped
-            const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2u * p);
+            const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2ull * p);
             unsigned long long cur = ((unsigned long long)sl.y << 32) | sl.x;
             if (cur == 0ull) {
-                cur = atomicCAS(&R.slot[2u * p], 0ull, k);
+                cur = atomicCAS(&R.slot[2ull * p], 0ull, k);
                 if (cur == 0ull) { R.list[atomicAdd(R.list_n, 1u)] = p; break; }
             }
             if (cur == k) { seen = side ? sl.w : sl.z; break; }
             p = (p + 1u) & R.mask;
         }
     }
-    if (seen < want) atomicMax(reinterpret_cast<uint32_t *>(R.slot + 2u * p + 1u) + side, want);
+    if (seen < want) atomicMax(reinterpret_cast<uint32_t *>(R.slot + 2ull * p + 1u) + side, want);
 }
 
 // ct_create4/6 (conntrack.h:446-580) for ingress (ct_state->addr == 0).  The
@@ -1206,7 +1206,7 @@ __device__ __forceinline__ int ct_create(const gf_htab_desc &d, uint32_t *t, uin
     v[1] = (fl | F_SEEN_NON_SYN) | (rev_nat << 16);
     if constexpr (KSZ == 14) if (rlog) {                // connection groups: applied after the run, in order
         GF_WR(WR_RLOG);
-        if (GF_EG_RSET) {
+        if (GF_EG_RSET && rs->slot) {
             rset_put(*rs, it[0], it[1], (it[NHW] >> 8) & 1u, order);
             return 0;
         }
@@ -4258,7 +4258,7 @@ __device__ __forceinline__ int eg_ct_part(const EgDev &E, const EgRec &r, uint32
         }
         uint32_t it[4] = {t[0], t[1], 0u, 1u | ((((t[3] >> 8) & 0xffu) | 2u) << 8)};
         v[1] |= F_SEEN_NON_SYN;
-        if (rlog && GF_EG_RSET) {                       // the run's set (RelSet), applied after the run
+        if (rlog && GF_EG_RSET && E.rs.slot) {          // the run's set (RelSet), applied after the run
             rset_put(E.rs, it[0], it[1], (it[3] >> 8) & 1u, 2u * i);
         } else if (rlog) {                              // applied after the run, in packet order (the pair's
             uint32_t *lg = E.rlog + (size_t)GF_CTLOG_WORDS * wave_reserve(E.rlog_n);   // other connections
@@ -4787,7 +4787,7 @@ __global__ __launch_bounds__(BLOCK) void k_rset_apply(RelSet R, const EgRec *ere
     int added = 0;
     for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
         const uint32_t p = R.list[j];
-        const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2u * p);
+        const uint4 sl = *reinterpret_cast<const uint4 *>(R.slot + 2ull * p);
         const unsigned long long k = p == R.mask + 1u ? 0ull : ((unsigned long long)sl.y << 32) | sl.x;
         for (uint32_t side = 0; side < 2; side++) {
             const uint32_t w = side ? sl.w : sl.z;
@@ -4811,7 +4811,7 @@ __global__ __launch_bounds__(BLOCK) void k_rset_apply(RelSet R, const EgRec *ere
             }
             ht_upsert<14, 12, GF_HASH_CT, GF_CT4_U>(ct, it, v, false, &added);
         }
-        *reinterpret_cast<uint4 *>(R.slot + 2u * p) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4 *>(R.slot + 2ull * p) = make_uint4(0u, 0u, 0u, 0u);
     }
     if (!ct_count || !__any(added != 0)) return;
     uint32_t tot = (uint32_t)added;                     // one count add per wave
@@ -6889,20 +6889,22 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     const bool conn = ct4m && !(strict & 1u) && !no_conn;
     uint32_t *d_rn = nullptr;                          // [0] related entries logged, [1] pair-group fallback
     if (conn) {
+        // the related entries' set (GF_EG_RSET): 4n slots keep it at most half full (<= 2n
+        // writes, one per new connection in each pass); batches too large for 32-bit slot
+        // numbers keep the write log
+        uint64_t ns = 1024;
+        while (ns < 4ull * n) ns *= 2;
+        const bool rset = GF_EG_RSET && ns <= (1ull << 31);
         if ((r = grow(ew.keysP, (size_t)n * 4)) || (r = grow(ew.key2P, (size_t)n * 4)) || (r = grow(ew.rlog_n, 8)) ||
-            (!GF_EG_RSET && (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4))))
+            (!rset && (r = grow(ew.rlog, (size_t)2 * n * GF_CTLOG_WORDS * 4))))
             return r;
         d_rn = (uint32_t *)ew.rlog_n.p;
         E.conn = 1; E.cflag = d_rn + 1;
         E.keysP = (uint32_t *)ew.keysP.p; E.key2P = (uint32_t *)ew.key2P.p;
         E.rlog = (uint32_t *)ew.rlog.p; E.rlog_n = d_rn;
-        if (GF_EG_RSET) {
-            // the set: <= 2n related writes (one per new connection in each pass), so
-            // 4n slots keep it at most half full; zeroed when allocated, and left zero
-            // by k_rset_apply, which clears every slot a run claimed
-            uint64_t ns = 1024;
-            while (ns < 4ull * n) ns *= 2;
-            if (ns > (1ull << 31)) return -E2BIG;
+        if (rset) {
+            // zeroed when allocated, and left zero by k_rset_apply, which clears every
+            // slot a run claimed
             const size_t sb = (size_t)(ns + 1) * 16;
             if (ew.rsslot.bytes < sb) {
                 if (ew.rsslot.ensure(sb)) return -ENOMEM;
@@ -7055,7 +7057,7 @@ static int egress_call(const std::shared_ptr<PolicyArray> &a, const gf_lxc_batch
     if ((r = ingress_run(a, &c2, now_sec, nullptr, s, pack, (uint8_t *)out, fr.len, wsnap, S, wsnap, lru && !conn, true,
                          false, &ta)))
         return r;
-    if (conn && GF_EG_RSET) {                          // both passes' related entries: each key's last writer
+    if (conn && E.rs.slot) {                           // both passes' related entries: each key's last writer
         ProfScope ps("k_ctlog_apply", s);
         // the deliveries' records are the workspace's now (the pack swap above)
         hipLaunchKernelGGL(k_rset_apply, dim3(std::min<uint32_t>(grid_for(2 * n), 2048u)), dim3(BLOCK), 0, s, E.rs,
