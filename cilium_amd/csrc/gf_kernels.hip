@@ -2870,8 +2870,8 @@ __device__ __forceinline__ void lru_hist_add(LruDev *L, unsigned long long *line
 // most to where the window starts again).
 // wide: the whole table (launched after k_lru_plan found the window empty).
 template <int KIND>
-__global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                          uint64_t sl, uint32_t max_entries, uint32_t wide) {
+__device__ __forceinline__ void lru_sample_body(const gf_htab_desc &d, uint32_t mode, uint32_t now, LruDev *L,
+                                                uint64_t sl, uint32_t max_entries, uint32_t wide) {
     if (wide ? !L->wide : (unsigned long long)*d.count <= lru_high_water(max_entries)) return;
     __shared__ unsigned long long line[GF_LRU_LDS];    // bin << 32 | count; bin ~0 = empty
     __shared__ uint32_t win[2 * GF_LRU_WIN];           // class * WIN + bin - (BINS - WIN)
@@ -2919,12 +2919,17 @@ __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32
     for (uint32_t k = threadIdx.x; k < GF_LRU_GROUPS; k += blockDim.x)
         if (cg[k]) atomicAdd(&L->coarse[k], cg[k]);
 }
+template <int KIND>
+__global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                          uint64_t sl, uint32_t max_entries, uint32_t wide) {
+    lru_sample_body<KIND>(d, mode, now, L, sl, max_entries, wide);
+}
 // K and es from the sample's histogram, the count the call starts from, and the
 // histogram cleared for the next call (one block).
 // wide = 0: the window's sample; an empty one (sl < nl) sets L->wide for the
 // whole-table sample and its plan (wide = 1) instead of planning.
-__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
-                                                   uint64_t nl, uint32_t wide) {
+__device__ __forceinline__ void lru_plan_body(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
+                                              uint64_t nl, uint32_t wide) {
     const uint32_t c = *count;
     const uint32_t t = threadIdx.x;
     if (wide) {
@@ -2995,6 +3000,10 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
         for (uint32_t r = 0; r < GF_LRU_ROUNDS; r++) L->kills[r] = 0;
     }
 }
+__global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32_t max_entries, LruDev *L, uint64_t sl,
+                                                   uint64_t nl, uint32_t wide) {
+    lru_plan_body(count, max_entries, L, sl, nl, wide);
+}
 // The hand over this round's lines: the slots from the first line's first slot,
 // lines * SPL of them, in chunks (GF_LRU_CHUNK slots, twice that for CT4), plus the cluster running past
 // the last one (entries homed in the range).  Launched twice, PAR = 0 for the
@@ -3006,8 +3015,8 @@ __global__ __launch_bounds__(1024) void k_lru_plan(const uint32_t *count, uint32
 // deleted entries turn FREE).  Codes: 0 EMPTY, 1 kept, 2 deleted now, 3 a
 // tombstone or FREE slot (cleared).
 template <int KIND, int PAR>
-__global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
-                                                        uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t round) {
+__device__ __forceinline__ void lru_hand_body(const gf_htab_desc &d, uint32_t mode, uint32_t now, LruDev *L,
+                                              uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t round) {
     if (!L->flag) return;
     const LruRound R = lru_round(L, round, max_entries, nl);
     const unsigned long long lines = R.lines;
@@ -3110,10 +3119,15 @@ __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t
         if (s_clr) atomicAdd(&L->cleared, (unsigned long long)s_clr);
     }
 }
+template <int KIND, int PAR>
+__global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand(gf_htab_desc d, uint32_t mode, uint32_t now, LruDev *L,
+                                                        uint64_t nl, uint64_t sl, uint32_t max_entries, uint32_t round) {
+    lru_hand_body<KIND, PAR>(d, mode, now, L, nl, sl, max_entries, round);
+}
 // After the last round: the count, the hand, the log (hcount: the count for the
 // host's bound, pinned host memory, may be null).
-__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t max_entries, uint64_t nl,
-                          uint32_t *hcount) {
+__device__ __forceinline__ void lru_end_body(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L,
+                                             uint32_t max_entries, uint64_t nl, uint32_t *hcount) {
     if (!L->flag) {
         if (hcount) *hcount = *count;
         return;
@@ -3134,6 +3148,49 @@ __global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L
     L->hand = (L->hand + lines) % nl;
     L->flag = 0;
     if (hcount) *hcount = *count;
+}
+__global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L, uint32_t max_entries, uint64_t nl,
+                          uint32_t *hcount) {
+    lru_end_body(count, seq, now, L, max_entries, nl, hcount);
+}
+
+// The same chain over several maps of one slot kind at once (per-endpoint CT maps,
+// the ConntrackLocal option): one launch per phase for up to GF_LRU_MULTI maps, each
+// block running every map's share in turn (the plan and the end: one block / one
+// thread per map).  The maps travel in the kernel arguments.
+#define GF_LRU_MULTI 16u
+struct LruMap {
+    gf_htab_desc d;
+    LruDev *L;
+    uint64_t nl, sl;
+    uint32_t mode, max_entries, seq, pad;
+    uint32_t *hcount;
+};
+struct LruBatch { LruMap m[GF_LRU_MULTI]; uint32_t n; };
+template <int KIND>
+__global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample_multi(LruBatch B, uint32_t now, uint32_t wide) {
+    for (uint32_t k = 0; k < B.n; k++) {
+        const LruMap &M = B.m[k];
+        lru_sample_body<KIND>(M.d, M.mode, now, M.L, M.sl, M.max_entries, wide);
+        __syncthreads();                                // the LDS bins are the next map's
+    }
+}
+__global__ __launch_bounds__(1024) void k_lru_plan_multi(LruBatch B, uint32_t wide) {
+    const LruMap &M = B.m[blockIdx.x];
+    lru_plan_body(M.d.count, M.max_entries, M.L, M.sl, M.nl, wide);
+}
+template <int KIND, int PAR>
+__global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand_multi(LruBatch B, uint32_t now, uint32_t round) {
+    for (uint32_t k = 0; k < B.n; k++) {
+        const LruMap &M = B.m[k];
+        lru_hand_body<KIND, PAR>(M.d, M.mode, now, M.L, M.nl, M.sl, M.max_entries, round);
+        __syncthreads();                                // code[] and the block's counts are the next map's
+    }
+}
+__global__ void k_lru_end_multi(LruBatch B, uint32_t now) {
+    if (threadIdx.x >= B.n) return;
+    const LruMap &M = B.m[threadIdx.x];
+    lru_end_body(M.d.count, M.seq, now, M.L, M.max_entries, M.nl, M.hcount);
 }
 
 // ================================================================ drop notifications
@@ -5846,7 +5903,11 @@ static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
 // device, a chain of launches that exit at once unless the map's count exceeds its
 // high-water mark; not launched at all while the host's bound of the count is at or
 // below it.
-static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s) {
+// One map's part of an eviction pass: its state, this call's count word, and the
+// descriptor the kernels read (kind 0: nothing to launch for it).
+struct LruPrep { Map *m = nullptr; int kind = 0; uint32_t slot = 0; LruMap lm{}; };
+static int lru_prepare(const std::shared_ptr<Map> &m, LruPrep &P) {
+    P = LruPrep{};
     if (!m || m->type != GF_MAP_TYPE_LRU_HASH || !m->d_slots.p) return 0;
     m->lru_seq++;
     ct_count_refresh(*m);
@@ -5855,7 +5916,6 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
         if (m->d_lru.ensure(sizeof(LruDev))) return -ENOMEM;
         if (hip_ok(hipMemset(m->d_lru.p, 0, sizeof(LruDev)), "lru init")) return -EIO;
     }
-    LruDev *L = (LruDev *)m->d_lru.p;
     const gf_htab_desc d = m->hdesc();
     const int kind = d.slot_size == 32 && d.ksz == 14 && d.vin == 16 && d.voff == 16 ? 1
                    : d.slot_size == 64 && d.ksz == 40 && d.vin == 16 && d.voff == 48 ? 2 : 0;
@@ -5878,47 +5938,25 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
         for (uint32_t k = 0; k < Map::GF_EVRING; k++) m->ev_count[k] = ev[k];
         m->h_evcount = (uint32_t *)p;
     }
-    const uint32_t slot = m->ev_head;
-    uint32_t *hc = nullptr;
-    if (hip_ok(hipHostGetDevicePointer((void **)&hc, m->h_evcount + slot, 0), "lru count word")) return -EIO;
-    const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size, nl = ns / spl;
-    const uint64_t sl = lru_sample_lines(nl);
-    const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
-    const uint32_t gh = resident_blocks(8);
-    const uint32_t *cnt = (const uint32_t *)d.count;
-    const uint32_t mx = m->max_entries;
-    {
-        ProfScope ps("k_lru_evict", s);
-        // the window's sample and plan, then (large tables only) the whole-table
-        // pair, which runs only when the window held no entry
-        for (uint32_t wide = 0; wide < (sl < nl ? 2u : 1u); wide++) {
-            const dim3 g(wide ? gh : gs);
-            if (kind == 1)
-                hipLaunchKernelGGL(k_lru_sample<1>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
-            else
-                hipLaunchKernelGGL(k_lru_sample<2>, g, dim3(GF_LRU_HB), 0, s, d, m->ht.mode, now, L, sl, mx, wide);
-            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, mx, L, sl, nl, wide);
-        }
-        for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
-            // round 1 is rare and short (what round 0's estimate left): a smaller grid, the same chunks
-            const dim3 g(round == 1 ? gh / 8 : gh);
-            if (kind == 1) {
-                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
-                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
-            } else {
-                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
-                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, m->ht.mode, now, L, nl, sl, mx, round);
-            }
-        }
-        hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, m->lru_seq, now, L, mx, nl, hc);
-    }
-    if (hip_ok(hipEventRecord(m->ev_count[slot], s), "lru count event")) return -EIO;
-    m->ev_pending |= 1u << slot;
-    m->ev_add[slot] = m->cnt_add;
-    m->ev_head = (slot + 1) % Map::GF_EVRING;
+    P.m = m.get(); P.kind = kind; P.slot = m->ev_head;
+    LruMap &M = P.lm;
+    if (hip_ok(hipHostGetDevicePointer((void **)&M.hcount, m->h_evcount + P.slot, 0), "lru count word")) return -EIO;
+    const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size;
+    M.d = d; M.L = (LruDev *)m->d_lru.p; M.nl = ns / spl; M.sl = lru_sample_lines(M.nl);
+    M.mode = m->ht.mode; M.max_entries = m->max_entries; M.seq = m->lru_seq;
+    return 0;
+}
+// After the chain: the count word's event, for the host's bound (ct_count_refresh).
+static int lru_post(const LruPrep &P, uint32_t now, hipStream_t s) {
+    Map *m = P.m;
+    if (hip_ok(hipEventRecord(m->ev_count[P.slot], s), "lru count event")) return -EIO;
+    m->ev_pending |= 1u << P.slot;
+    m->ev_add[P.slot] = m->cnt_add;
+    m->ev_head = (P.slot + 1) % Map::GF_EVRING;
     static const bool stats = getenv("GF_LRU_STATS") != nullptr;   // diagnostics: syncs the stream
     if (stats) {
         LruDev h;
+        LruDev *L = P.lm.L;
         if (!hip_ok(hipMemcpyAsync(&h, L, offsetof(LruDev, log), hipMemcpyDeviceToHost, s), "lru stats") &&
             !hip_ok(hipStreamSynchronize(s), "lru stats") && h.nlog) {
             uint32_t n = h.nlog;
@@ -5927,10 +5965,111 @@ static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s)
                         "lru stats log") && g.seq == m->lru_seq)
                 fprintf(stderr, "[lru] seq %u now %u: K %u es %llu lines %llu of %llu (hand %llu) evicted %llu "
                         "(rounds %llu / %llu / %llu), cleared %llu\n", g.seq, now, g.age_cut, h.es, g.lines,
-                        (unsigned long long)nl, g.hand, g.evicted, h.kills[0], h.kills[1], h.kills[2], h.cleared);
+                        (unsigned long long)P.lm.nl, g.hand, g.evicted, h.kills[0], h.kills[1], h.kills[2], h.cleared);
         }
     }
+    return 0;
+}
+// The LRU stand-in after a classify call (k_lru_*: see the kernels): fully on the
+// device, a chain of launches that exit at once unless the map's count exceeds its
+// high-water mark; not launched at all while the host's bound of the count is at or
+// below it.
+static int lru_evict(const std::shared_ptr<Map> &m, uint32_t now, hipStream_t s) {
+    LruPrep P;
+    int r;
+    if ((r = lru_prepare(m, P)) || !P.kind) return r;
+    const LruMap &M = P.lm;
+    const gf_htab_desc &d = M.d;
+    LruDev *L = M.L;
+    const int kind = P.kind;
+    const uint64_t spl = 128 / d.slot_size, nl = M.nl, sl = M.sl;
+    const uint32_t gs = (uint32_t)std::min<uint64_t>((sl * spl + GF_LRU_HB - 1) / GF_LRU_HB, resident_blocks(2));
+    const uint32_t gh = resident_blocks(8);
+    const uint32_t *cnt = (const uint32_t *)d.count;
+    const uint32_t mx = M.max_entries, mode = M.mode;
+    {
+        ProfScope ps("k_lru_evict", s);
+        // the window's sample and plan, then (large tables only) the whole-table
+        // pair, which runs only when the window held no entry
+        for (uint32_t wide = 0; wide < (sl < nl ? 2u : 1u); wide++) {
+            const dim3 g(wide ? gh : gs);
+            if (kind == 1)
+                hipLaunchKernelGGL(k_lru_sample<1>, g, dim3(GF_LRU_HB), 0, s, d, mode, now, L, sl, mx, wide);
+            else
+                hipLaunchKernelGGL(k_lru_sample<2>, g, dim3(GF_LRU_HB), 0, s, d, mode, now, L, sl, mx, wide);
+            hipLaunchKernelGGL(k_lru_plan, dim3(1), dim3(1024), 0, s, cnt, mx, L, sl, nl, wide);
+        }
+        for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
+            // round 1 is rare and short (what round 0's estimate left): a smaller grid, the same chunks
+            const dim3 g(round == 1 ? gh / 8 : gh);
+            if (kind == 1) {
+                hipLaunchKernelGGL((k_lru_hand<1, 0>), g, dim3(GF_LRU_HT), 0, s, d, mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<1, 1>), g, dim3(GF_LRU_HT), 0, s, d, mode, now, L, nl, sl, mx, round);
+            } else {
+                hipLaunchKernelGGL((k_lru_hand<2, 0>), g, dim3(GF_LRU_HT), 0, s, d, mode, now, L, nl, sl, mx, round);
+                hipLaunchKernelGGL((k_lru_hand<2, 1>), g, dim3(GF_LRU_HT), 0, s, d, mode, now, L, nl, sl, mx, round);
+            }
+        }
+        hipLaunchKernelGGL(k_lru_end, dim3(1), dim3(1), 0, s, d.count, M.seq, now, L, mx, nl, M.hcount);
+    }
+    if ((r = lru_post(P, now, s))) return r;
     return hip_ok(hipGetLastError(), "k_lru_evict");
+}
+// The pass over several maps (per-endpoint CT maps): the maps that may be above their
+// high-water marks, GF_LRU_MULTI of one slot kind per chain of launches (a single one
+// takes the one-map chain).  Each map's rounds, cutoffs and log are its own, exactly
+// as with its own chain.
+static int lru_evict_maps(const std::vector<std::shared_ptr<Map>> &ms, uint32_t now, hipStream_t s) {
+    if (ms.empty()) return 0;
+    if (ms.size() == 1) return lru_evict(ms[0], now, s);
+    std::vector<LruPrep> ps;
+    int r;
+    for (auto &m : ms) {
+        LruPrep P;
+        if ((r = lru_prepare(m, P))) return r;
+        if (P.kind) ps.push_back(P);
+    }
+    if (ps.empty()) return 0;
+    const uint32_t gh = resident_blocks(8);
+    ProfScope prof("k_lru_evict", s);
+    for (int kind = 1; kind <= 2; kind++) {
+        std::vector<const LruPrep *> ks;
+        for (auto &P : ps)
+            if (P.kind == kind) ks.push_back(&P);
+        for (size_t b = 0; b < ks.size(); b += GF_LRU_MULTI) {
+            LruBatch B{};
+            B.n = (uint32_t)std::min<size_t>(GF_LRU_MULTI, ks.size() - b);
+            uint64_t gs = 1;
+            bool big = false;
+            for (uint32_t k = 0; k < B.n; k++) {
+                B.m[k] = ks[b + k]->lm;
+                const uint64_t spl = 128 / B.m[k].d.slot_size;
+                gs = std::max<uint64_t>(gs, (B.m[k].sl * spl + GF_LRU_HB - 1) / GF_LRU_HB);
+                big |= B.m[k].sl < B.m[k].nl;
+            }
+            const dim3 g1((uint32_t)std::min<uint64_t>(gs, resident_blocks(2)));
+            for (uint32_t wide = 0; wide < (big ? 2u : 1u); wide++) {
+                const dim3 g(wide ? gh : g1.x);
+                if (kind == 1) hipLaunchKernelGGL(k_lru_sample_multi<1>, g, dim3(GF_LRU_HB), 0, s, B, now, wide);
+                else hipLaunchKernelGGL(k_lru_sample_multi<2>, g, dim3(GF_LRU_HB), 0, s, B, now, wide);
+                hipLaunchKernelGGL(k_lru_plan_multi, dim3(B.n), dim3(1024), 0, s, B, wide);
+            }
+            for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
+                if (kind == 1) {
+                    hipLaunchKernelGGL((k_lru_hand_multi<1, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<1, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                } else {
+                    hipLaunchKernelGGL((k_lru_hand_multi<2, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<2, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                }
+            }
+            hipLaunchKernelGGL(k_lru_end_multi, dim3(1), dim3(64), 0, s, B, now);
+            if ((r = hip_ok(hipGetLastError(), "k_lru_*_multi"))) return r;
+        }
+    }
+    for (auto &P : ps)
+        if ((r = lru_post(P, now, s))) return r;
+    return 0;
 }
 
 // pack (may be empty): fills the records and bucket keys itself (the fused
@@ -6074,9 +6213,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     for (auto &p : progs) {
         if (p->policy) p->policy->device_modified();
     }
-    for (auto *v : {&cm.m4, &cm.m6})
-        for (auto &m : *v)
-            if (lru && (r = lru_evict(m, now_sec, s))) return r;
+    if (lru && ((r = lru_evict_maps(cm.m4, now_sec, s)) || (r = lru_evict_maps(cm.m6, now_sec, s)))) return r;
     host_mark("lru");
     for (auto *v : {&cm.m4, &cm.m6})
         for (auto &m : *v) m->device_modified();

@@ -121,6 +121,35 @@ def test_gpu_conntrack_local_pipeline(seed, every):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_ep,mx", [(40, 1500), (20, 600)])
+def test_gpu_conntrack_local_many_maps(n_ep, mx):
+    """More per-endpoint maps than one multi-map eviction chain takes (GF_LRU_MULTI = 16:
+    40 maps run as chains of 16, 16 and 8), each small enough to evict on every call:
+    the config-2 stream in four calls, records and all 40 maps equal the oracle's."""
+    _gpu()
+    from cilium_amd.datapath import Datapath, DeviceBatch, ING_OUT, to_numpy
+    sc = synth.config2(n_flows=120_000, n_pairs=12_000, n_ep=n_ep, n_ids=512, n_l3=200, n_l4=400, n_wc=8,
+                       n_cidr=32, ct_max=400_000)
+    made = synth.conntrack_local(sc, max_entries=mx)
+    assert len(made) == n_ep
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    q = (pk.n + 3) // 4
+    for k in range(4):
+        part = pk.slice(k * q, min(pk.n, (k + 1) * q))
+        io = dp.ingress(DeviceBatch(part), sc.now + k)
+        torch.cuda.synchronize()
+        got, want = to_numpy(io, ING_OUT), ref.ingress(part, sc.now + k)
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, f"call {k}: {len(bad)} records differ, first {bad[:1]}"
+    for name in made:
+        assert dp.dump_map(name) == ref.dump(name), name
+    # every map evicted after every call (a map holding more than one call's inserts
+    # also ends at or below max_entries: include/gpuflow.h's bound)
+    assert all(len(ref.lru_log[name]) == 4 for name in made), {n: len(ref.lru_log[n]) for n in made}
+
+
+@pytest.mark.gpu
 def test_gpu_conntrack_local_batches_api():
     """gf_policy_ingress_classify_batches (schedules built on the aux stream) with
     per-endpoint maps: the same records and maps as the oracle."""
