@@ -509,6 +509,7 @@ def bench_config2(args, B, rank, world, local_world=1):
     L = max(args.long_steps, W + K) if world == 1 and not args.pipeline else W + K
     rk, rv = st.reply_ct_entries(S0 + L)
     sc.maps["cilium_ct4_global"].keys, sc.maps["cilium_ct4_global"].vals = rk, rv
+    ct_names = ct_local_split(sc, P, ct_max) if args.ct_local else ["cilium_ct4_global"]
     log(f"rank {rank}: tables {sum(m.n() for m in sc.maps.values())} entries, {len(rk)} pre-inserted CT, "
         f"{len(st.own)} owned pairs ({time.time() - t0:.1f}s)")
     dp = B.datapath(sc)
@@ -559,11 +560,11 @@ def bench_config2(args, B, rank, world, local_world=1):
     cpu = par = None
     if not args.no_cpu:
         # every rank checks its own flow groups; the CPU baseline is rank 0's at N=1 only
-        cpu, par = oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world, local_world, L)
+        cpu, par = oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world, local_world, L, ct_names)
         if world > 1:
             cpu = None
     par = reduce_parity(B, par, rank, world)
-    ct_end = int(B.entries(dp, "cilium_ct4_global"))
+    ct_end = sum(int(B.entries(dp, name)) for name in ct_names)
     B.close(dp)
     return {
         "metric": METRIC,
@@ -580,7 +581,8 @@ def bench_config2(args, B, rank, world, local_world=1):
         "data": "synthetic (seeded config-2 stream generated on device; tables from cilium_amd.synth)",
         "config": {
             "workload": "config2: bpf_lxc ingress handle_policy (ct_lookup4 + policy_can_access), steady-state "
-                        "stream, 4M new flows/step (16M active), 256 endpoints, 4352 identities",
+                        "stream, 4M new flows/step (16M active), 256 endpoints, 4352 identities"
+                        + (f", per-endpoint CT maps (ConntrackLocal, {len(ct_names)} maps)" if args.ct_local else ""),
             "packets_per_step_per_gpu": int(batches[W].n),
             "address_pairs_per_gpu": int(args.pairs),
             "address_pairs": int(args.pairs) * world,
@@ -626,7 +628,31 @@ class ColBatch:
         return self._cols(self)
 
 
-def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_world=1, L=None):
+def ct_local_split(sc, P, ct_max):
+    """--ct-local: every endpoint binds a CT map of its own (the ConntrackLocal option,
+    pkg/endpoint/bpf.go:268-276: cilium_ct4_<id>, max_entries ct_max / endpoints), holding
+    the pre-inserted entries of its address (the tuple's daddr); the global map goes."""
+    from cilium_amd import synth
+    g = sc.maps.pop("cilium_ct4_global")
+    ep_ip, lxc_id = np.asarray(P["ep_ip"], np.uint32), np.asarray(P["lxc_id"])
+    order = np.argsort(ep_ip)
+    d = g.keys[:, 0:4].copy().view(">u4").ravel().astype(np.uint32)
+    pos = np.clip(np.searchsorted(ep_ip[order], d), 0, len(ep_ip) - 1)
+    own = np.where(ep_ip[order][pos] == d, order[pos], -1)
+    names = []
+    per = max(1, ct_max // len(sc.lxc))
+    for e in sc.lxc:
+        j = int(np.nonzero(lxc_id == e["lxc_id"])[0][0])
+        m = own == j
+        name = f"cilium_ct4_{e['lxc_id']}"
+        sc.add_map(synth.MapSpec(name, g.type, g.ksz, g.vsz, per, g.flags, g.keys[m], g.vals[m]))
+        e["ct4"] = name
+        names.append(name)
+    return names
+
+
+def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_world=1, L=None,
+                   ct_names=("cilium_ct4_global",)):
     """The CPU restatement (oracle, multi-threaded, RSS-style partition by flow
     group) over the flow-group sample of every step (warm-up included): its
     records must equal the GPU's for every sampled packet and, after the last
@@ -687,8 +713,11 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
             log(f"parity: {s + 1} of {L} steps, {par.packets} packets compared, {par.bad} mismatches "
                 f"({time.time() - t0:.1f}s)")
     prep.shutdown()
-    compare_ct(B, par, dp, ref, "cilium_ct4_global", 14, div)
-    log(f"cpu baseline + parity: {par.packets} packets compared, {par.bad} mismatches; CT {par.ct}; "
+    for name in ct_names:
+        compare_ct(B, par, dp, ref, name, 14, div)
+    ctl = par.ct if len(par.ct) <= 4 else {f"{len(par.ct)} maps": {k: sum(v[k] for v in par.ct.values())
+                                                                  for k in ("entries_compared", "mismatches")}}
+    log(f"cpu baseline + parity: {par.packets} packets compared, {par.bad} mismatches; CT {ctl}; "
         f"{done} packets in {tt:.2f}s on {T} threads ({time.time() - t0:.1f}s)")
     cpu = cpu_base(done / tt / 1e6 if tt else 0.0, T,
                    f"{done} packets of the same config-2 stream (flows of 1/{div} of the address pairs, the "
@@ -696,13 +725,26 @@ def oracle_config2(args, B, sc, st, dp, batches, ps, outs, W, K, world=1, local_
                    f"partition over {T} threads; single core: {single_n} packets of step {W}",
                    single_n / single_t / 1e6 if single_t else None)
     res = par.result(L)
+    if len(res.get("tables", {})) > 4:                  # per-endpoint maps: one summary
+        t = res["tables"]
+        res["tables"] = {f"{len(t)} per-endpoint maps": {k: sum(v[k] for v in t.values())
+                                                         for k in ("entries_compared", "mismatches", "gpu_entries_total")}}
     if div == 1:
-        dev_log = [tuple(int(x) for x in e) for e in B.evict_log(dp, "cilium_ct4_global")]
-        ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get("cilium_ct4_global", [])]
-        res["evictions"] = {"cilium_ct4_global": {
-            "evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log), "sweeps_oracle": len(ora_log),
-            "entries_evicted": int(sum(e[5] for e in dev_log)),
-            "oracle": "own cutoffs from its whole table (never saw the device log)"}}
+        ev = {}
+        for name in ct_names:
+            dev_log = [tuple(int(x) for x in e) for e in B.evict_log(dp, name)]
+            ora_log = [tuple(int(x) for x in e) for e in ref.lru_log.get(name, [])]
+            ev[name] = {"evict_log_equal": dev_log == ora_log, "sweeps_device": len(dev_log),
+                        "sweeps_oracle": len(ora_log), "entries_evicted": int(sum(e[5] for e in dev_log)),
+                        "oracle": "own cutoffs from its whole table (never saw the device log)"}
+        if len(ev) > 4:                                 # per-endpoint maps: one summary
+            ev = {f"{len(ev)} per-endpoint maps": {
+                "evict_log_equal": all(v["evict_log_equal"] for v in ev.values()),
+                "sweeps_device": sum(v["sweeps_device"] for v in ev.values()),
+                "sweeps_oracle": sum(v["sweeps_oracle"] for v in ev.values()),
+                "entries_evicted": sum(v["entries_evicted"] for v in ev.values()),
+                "oracle": "own cutoffs from each whole table (never saw the device logs)"}}
+        res["evictions"] = ev
     return cpu, res
 
 
@@ -1437,6 +1479,8 @@ def main():
                     help="config 2: the steps through gf_policy_ingress_classify_batches (schedule overlap)")
     ap.add_argument("--no-extra", action="store_true", help="config 2 only (skip the other configurations)")
     ap.add_argument("--no-h2d", action="store_true", help="config 4: skip the leg with the host->device copy")
+    ap.add_argument("--ct-local", action="store_true",
+                    help="config 2: every endpoint on a CT map of its own (the ConntrackLocal option)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-div", type=int, default=0,
                     help="parity sample: 1 in N address pairs (default: every pair at N=1, 1 in 2 per rank at N>1)")

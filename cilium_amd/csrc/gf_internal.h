@@ -132,6 +132,7 @@ struct Map : Obj {
     // recorded; ev_pending: the slots recorded since the bound was last set directly
     static constexpr uint32_t GF_EVRING = 8;
     uint32_t *h_evcount = nullptr;
+    uint32_t *d_evcount = nullptr;    // its device address (hipHostGetDevicePointer, once)
     hipEvent_t ev_count[GF_EVRING] = {};
     uint64_t ev_add[GF_EVRING] = {};
     uint32_t ev_head = 0, ev_pending = 0;

@@ -1578,7 +1578,10 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     uint32_t nh = r.proto;
     uint32_t t[4] = {r.daddr, r.saddr, 0u, nh};
     uint32_t tfl = 0;                                   // TUPLE_F_OUT (ingress)
-    if (nh == 1) rel_flush4(X.ct4, rc, X.now);          // its related probe may read the pending entry
+    if (nh == 1) {                                      // its related probe may read the pending entry
+        if constexpr (PCT) rel_flush4(ing_ct<4, true>(X, ep), rc, X.now);   // (the lane's cache is this map's)
+        else rel_flush4(X.ct4, rc, X.now);
+    }
     int action; bool syn;
     int e = ct_l4(nh, false, r, t[2], tfl, action, syn);
     if (e < 0) return e;
@@ -1602,7 +1605,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
     ProbeRes pr;
     int ret = ct_lookup<14, 4, GF_CT4_U>(ct, cl, t, nh, tfl, action, syn, len, X.now, acct, st, pr, ab);
     fwd = ret;
-    if (st.carry) rel_drop(X.ct4, rc, X.now);           // a counter carry touched a cold value part
+    if (st.carry) rel_drop(PCT ? ct : X.ct4, rc, X.now);   // a counter carry touched a cold value part
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {
         const gf_htab_desc rn = gload<gf_htab_desc>(&ep.cfg(X)->revnat4);
         uint32_t kw[1] = {st.rev_nat};
@@ -1623,7 +1626,7 @@ __device__ int ipv4_policy(const IngCtx &X, Ep &ep, const gf_rec &r, uint32_t i,
         if (ret == CT_ESTABLISHED) {
             ab += 14;
             ht_delete<14, GF_HASH_CT, GF_CT4_U>(ct, t, X.strict & 1, added);
-            rel_drop(X.ct4, rc, X.now);
+            rel_drop(PCT ? ct : X.ct4, rc, X.now);
         }
         return D_POLICY;
     }
@@ -1772,6 +1775,27 @@ struct Lane {
     LaneCnt sc;
     __device__ __forceinline__ void init() { ep.init(); acc.init(); pm.init(); rc.init(); added = 0; sc.init(); }
 };
+// Per-endpoint CT maps, non-strict accounting: the lane's net inserts belong to its
+// current program's map, added to that map's count (no return value) when the lane
+// moves to another program and at the end of the launch.
+template <int FAM, bool PCT>
+__device__ __forceinline__ void lane_flush_added(const IngCtx &X, Lane<FAM> &ln) {
+    if constexpr (PCT) {
+        if (ln.added && ln.ep.sl && !(X.strict & (FAM == 6 ? 2u : 1u)))
+            atomicAdd(ing_ct<FAM, true>(X, ln.ep).count, (uint32_t)ln.added);
+        ln.added = 0;
+    }
+}
+// The lane's pending related-entry write (IPv4), to its map, and the cache dropped.
+template <int FAM, bool PCT>
+__device__ __forceinline__ void lane_rel_drop(const IngCtx &X, Lane<FAM> &ln) {
+    if constexpr (PCT) {
+        if (ln.ep.sl) rel_drop(ing_ct<FAM, true>(X, ln.ep), ln.rc, X.now);
+        else ln.rc.slot = ~0u;                          // (nothing is pending before a program ran)
+    } else {
+        rel_drop(X.ct4, ln.rc, X.now);
+    }
+}
 
 // handle_policy, bpf/bpf_lxc.c:980-1024.  FAM selects the CT path compiled in:
 // 4 = the IPv4 path plus every packet that cannot reach conntrack (no IP
@@ -1879,14 +1903,12 @@ __device__ __forceinline__ void ing_one(const IngCtx &X, uint32_t i, const gf_re
                                         Stats &st, bool stats, Lane<FAM> &ln, uint32_t *rlog) {
     if (r.cls & 8) return;                              // pipeline: ended before the tail call
     uint32_t ab = 8;                                    // output record
-    gf_ingress_out o = handle_policy<FAM, PCT, RL>(X, r, i, ln, ab, rlog);
     if constexpr (PCT) {
-        // per-endpoint CT maps: the lane's related-entry cache is the packet's own
-        // (the next packet of the bucket may be another endpoint's, another map)
-        if constexpr (FAM == 4)
-            if (ln.rc.k[3] >> 15) rel_flush4(ing_ct<4, true>(X, ln.ep), ln.rc, X.now);
-        ln.rc.slot = ~0u;
+        // per-endpoint CT maps: the lane's related-entry cache belongs to its current
+        // program's map; a packet of another program writes the pending entry first
+        if (r.ep != ln.ep.sl) { lane_rel_drop<FAM, true>(X, ln); lane_flush_added<FAM, true>(X, ln); }
     }
+    gf_ingress_out o = handle_policy<FAM, PCT, RL>(X, r, i, ln, ab, rlog);
     if (X.pout && X.pout_wo) {                          // complete the pipeline record: stores only
         uint8_t *q = X.pout + 24 * (size_t)i;
         const uint32_t ff = ((uint32_t)(r.cls >> 4) & 7u) << 5;   // the front's whole GF_PIPE_F_* byte
@@ -2031,7 +2053,7 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
         uint32_t i = perm[b];
         uint32_t inx = c > 1 ? perm[b + 1] : 0u;
         gf_rec r = ld_rec(rec, i);
-        rel_drop(X.ct4, ln.rc, X.now);                   // a new bucket: new flow groups
+        lane_rel_drop<FAM, PCT>(X, ln);                  // a new bucket: new flow groups
 #if GF_PERM_VEC
         uint4 pw = make_uint4(0, 0, 0, 0);               // perm[j & ~3 .. +3], j = b + k + 2
         if (c > 2) pw = *reinterpret_cast<const uint4 *>(perm + ((b + 2) & ~3u));
@@ -2056,7 +2078,8 @@ __global__ __launch_bounds__(BLOCK, FAM == 6 ? GF_ING_MINW6 : GF_ING_MINW) void 
     }
     }
     ln.acc.flush(X);
-    rel_drop(X.ct4, ln.rc, X.now);                      // the pending related-entry write (IPv4)
+    lane_rel_drop<FAM, PCT>(X, ln);                     // the pending related-entry write (IPv4)
+    lane_flush_added<FAM, PCT>(X, ln);                  // (per-endpoint maps: the lane's own count add)
     if (stats) ln.sc.fold(st);
     flush_added(X, F ? 2u : 1u, ln.added, ct_count, &sadd);
     if (stats) st.flush(stats);
@@ -3158,7 +3181,7 @@ __global__ void k_lru_end(uint32_t *count, uint32_t seq, uint32_t now, LruDev *L
 // the ConntrackLocal option): one launch per phase for up to GF_LRU_MULTI maps, each
 // block running every map's share in turn (the plan and the end: one block / one
 // thread per map).  The maps travel in the kernel arguments.
-#define GF_LRU_MULTI 16u
+#define GF_LRU_MULTI 32u
 struct LruMap {
     gf_htab_desc d;
     LruDev *L;
@@ -3167,9 +3190,31 @@ struct LruMap {
     uint32_t *hcount;
 };
 struct LruBatch { LruMap m[GF_LRU_MULTI]; uint32_t n; };
+static_assert(GF_LRU_MULTI <= 32, "lru_active keeps one bit per map in a 32-bit mask");
+static_assert(sizeof(LruBatch) + 64 <= 4096, "the maps travel in the kernel arguments");
+// The batch's maps a phase has work for, read by one lane per map at once (a block
+// would otherwise pay one dependent round trip per map): what 0 = over the high-water
+// mark (the sample; wide: the window was empty), 1 = evicting this call (the hand).
+__device__ __forceinline__ uint32_t lru_active(const LruBatch &B, uint32_t what, uint32_t wide) {
+    __shared__ uint32_t s_mask;
+    if (threadIdx.x < 64) {
+        bool a = false;
+        if (threadIdx.x < B.n) {
+            const LruMap &M = B.m[threadIdx.x];
+            if (what) a = M.L->flag != 0u;
+            else a = wide ? M.L->wide != 0u : (unsigned long long)*M.d.count > lru_high_water(M.max_entries);
+        }
+        const uint64_t b = __ballot(a);
+        if (threadIdx.x == 0) s_mask = (uint32_t)b;
+    }
+    __syncthreads();
+    return s_mask;
+}
 template <int KIND>
 __global__ __launch_bounds__(GF_LRU_HB) void k_lru_sample_multi(LruBatch B, uint32_t now, uint32_t wide) {
+    const uint32_t act = lru_active(B, 0u, wide);
     for (uint32_t k = 0; k < B.n; k++) {
+        if (!((act >> k) & 1u)) continue;
         const LruMap &M = B.m[k];
         lru_sample_body<KIND>(M.d, M.mode, now, M.L, M.sl, M.max_entries, wide);
         __syncthreads();                                // the LDS bins are the next map's
@@ -3181,7 +3226,9 @@ __global__ __launch_bounds__(1024) void k_lru_plan_multi(LruBatch B, uint32_t wi
 }
 template <int KIND, int PAR>
 __global__ __launch_bounds__(GF_LRU_HT) void k_lru_hand_multi(LruBatch B, uint32_t now, uint32_t round) {
+    const uint32_t act = lru_active(B, 1u, 0u);
     for (uint32_t k = 0; k < B.n; k++) {
+        if (!((act >> k) & 1u)) continue;
         const LruMap &M = B.m[k];
         lru_hand_body<KIND, PAR>(M.d, M.mode, now, M.L, M.nl, M.sl, M.max_entries, round);
         __syncthreads();                                // code[] and the block's counts are the next map's
@@ -5863,17 +5910,24 @@ static int ct_maps_of(const std::vector<std::shared_ptr<ProgLxc>> &progs, CtMaps
     return 0;
 }
 // Per-endpoint maps: each map's host bound moves as if the whole batch could insert
-// into it, and every insert is counted exactly into its own map (strict), whose
-// count and insert limit the program table's descriptor carries (ct_dev_desc).
+// into it; a family whose maps could any of them fill counts every insert exactly
+// (strict: the count and insert limit the program table's descriptor carries,
+// ct_dev_desc), else each lane adds its net inserts to its program's map
+// (lane_flush_added).
 static int ct_limits_pct(const CtMaps &cm, uint32_t n, uint32_t per_pkt, hipStream_t s, uint32_t &strict) {
     gf_htab_desc d4{}, d6{};
-    uint32_t st = 0;
     int r;
-    for (auto &m : cm.m4)
+    strict = 0;
+    for (auto &m : cm.m4) {
+        uint32_t st = 0;
         if ((r = ct_limits(m, nullptr, n, per_pkt, s, st, d4, d6))) return r;
-    for (auto &m : cm.m6)
+        strict |= st;
+    }
+    for (auto &m : cm.m6) {
+        uint32_t st = 0;
         if ((r = ct_limits(nullptr, m, n, per_pkt, s, st, d4, d6))) return r;
-    strict = 3u;
+        strict |= st;
+    }
     return 0;
 }
 
@@ -5906,7 +5960,10 @@ static void ct_sweep_launch(Map &m, LruDev *L, uint32_t *bits, hipStream_t s) {
 // One map's part of an eviction pass: its state, this call's count word, and the
 // descriptor the kernels read (kind 0: nothing to launch for it).
 struct LruPrep { Map *m = nullptr; int kind = 0; uint32_t slot = 0; LruMap lm{}; };
-static int lru_prepare(const std::shared_ptr<Map> &m, LruPrep &P) {
+// track: the chain writes the count to the map's pinned ring behind an event, for the
+// host's bound (the multi-map pass does not: one event record per map per call costs
+// more host time than the bound saves there).
+static int lru_prepare(const std::shared_ptr<Map> &m, LruPrep &P, bool track = true) {
     P = LruPrep{};
     if (!m || m->type != GF_MAP_TYPE_LRU_HASH || !m->d_slots.p) return 0;
     m->lru_seq++;
@@ -5935,12 +5992,19 @@ static int lru_prepare(const std::shared_ptr<Map> &m, LruPrep &P) {
                 if (e) (void)hipEventDestroy(e);
             return -ENOMEM;
         }
+        uint32_t *dp = nullptr;
+        if (hip_ok(hipHostGetDevicePointer((void **)&dp, p, 0), "lru count words")) {
+            for (auto &e : ev) (void)hipEventDestroy(e);
+            (void)hipHostFree(p);
+            return -EIO;
+        }
         for (uint32_t k = 0; k < Map::GF_EVRING; k++) m->ev_count[k] = ev[k];
         m->h_evcount = (uint32_t *)p;
+        m->d_evcount = dp;
     }
     P.m = m.get(); P.kind = kind; P.slot = m->ev_head;
     LruMap &M = P.lm;
-    if (hip_ok(hipHostGetDevicePointer((void **)&M.hcount, m->h_evcount + P.slot, 0), "lru count word")) return -EIO;
+    M.hcount = track ? m->d_evcount + P.slot : nullptr;
     const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size;
     M.d = d; M.L = (LruDev *)m->d_lru.p; M.nl = ns / spl; M.sl = lru_sample_lines(M.nl);
     M.mode = m->ht.mode; M.max_entries = m->max_entries; M.seq = m->lru_seq;
@@ -6026,7 +6090,7 @@ static int lru_evict_maps(const std::vector<std::shared_ptr<Map>> &ms, uint32_t 
     int r;
     for (auto &m : ms) {
         LruPrep P;
-        if ((r = lru_prepare(m, P))) return r;
+        if ((r = lru_prepare(m, P, false))) return r;
         if (P.kind) ps.push_back(P);
     }
     if (ps.empty()) return 0;
@@ -6049,26 +6113,28 @@ static int lru_evict_maps(const std::vector<std::shared_ptr<Map>> &ms, uint32_t 
             }
             const dim3 g1((uint32_t)std::min<uint64_t>(gs, resident_blocks(2)));
             for (uint32_t wide = 0; wide < (big ? 2u : 1u); wide++) {
-                const dim3 g(wide ? gh : g1.x);
+                // (the whole-table pass runs only for a map whose window held no entry: a
+                // smaller grid, which costs little on the many calls where it has no work)
+                const dim3 g(wide ? std::max<uint32_t>(gh / 8, 1) : g1.x);
                 if (kind == 1) hipLaunchKernelGGL(k_lru_sample_multi<1>, g, dim3(GF_LRU_HB), 0, s, B, now, wide);
                 else hipLaunchKernelGGL(k_lru_sample_multi<2>, g, dim3(GF_LRU_HB), 0, s, B, now, wide);
                 hipLaunchKernelGGL(k_lru_plan_multi, dim3(B.n), dim3(1024), 0, s, B, wide);
             }
             for (uint32_t round = 0; round < GF_LRU_ROUNDS; round++) {
+                // rounds 1 and 2 run only for what round 0's estimate left: smaller grids
+                const dim3 g(round ? std::max<uint32_t>(gh / 8, 1) : gh);
                 if (kind == 1) {
-                    hipLaunchKernelGGL((k_lru_hand_multi<1, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
-                    hipLaunchKernelGGL((k_lru_hand_multi<1, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<1, 0>), g, dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<1, 1>), g, dim3(GF_LRU_HT), 0, s, B, now, round);
                 } else {
-                    hipLaunchKernelGGL((k_lru_hand_multi<2, 0>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
-                    hipLaunchKernelGGL((k_lru_hand_multi<2, 1>), dim3(gh), dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<2, 0>), g, dim3(GF_LRU_HT), 0, s, B, now, round);
+                    hipLaunchKernelGGL((k_lru_hand_multi<2, 1>), g, dim3(GF_LRU_HT), 0, s, B, now, round);
                 }
             }
             hipLaunchKernelGGL(k_lru_end_multi, dim3(1), dim3(64), 0, s, B, now);
             if ((r = hip_ok(hipGetLastError(), "k_lru_*_multi"))) return r;
         }
     }
-    for (auto &P : ps)
-        if ((r = lru_post(P, now, s))) return r;
     return 0;
 }
 
@@ -6102,8 +6168,7 @@ static int ingress_run(const std::shared_ptr<PolicyArray> &a, const gf_pkt_cols 
     // The decision uses a host-side upper bound of the device element count (each
     // packet inserts at most 2 entries), read back from the device only when the
     // bound gets near the limit — steady-state batches never wait on the GPU here.
-    // Per-endpoint maps count every insert exactly, into the packet's own map (the
-    // descriptors in the program table carry each map's count and insert limit).
+    // Per-endpoint maps: the same per family, over every map of it (ct_limits_pct).
     uint32_t strict = 0;
     gf_htab_desc cfg_ct4{}, cfg_ct6{};
     if ((r = ct_limits(ct4m, ct6m, pkts->n, 2, s, strict, cfg_ct4, cfg_ct6))) return r;

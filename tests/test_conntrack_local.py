@@ -123,8 +123,8 @@ def test_gpu_conntrack_local_pipeline(seed, every):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_ep,mx", [(40, 1500), (20, 600)])
 def test_gpu_conntrack_local_many_maps(n_ep, mx):
-    """More per-endpoint maps than one multi-map eviction chain takes (GF_LRU_MULTI = 16:
-    40 maps run as chains of 16, 16 and 8), each small enough to evict on every call:
+    """More per-endpoint maps than one multi-map eviction chain takes (GF_LRU_MULTI = 32:
+    40 maps run as chains of 32 and 8), each small enough to evict on every call:
     the config-2 stream in four calls, records and all 40 maps equal the oracle's."""
     _gpu()
     from cilium_amd.datapath import Datapath, DeviceBatch, ING_OUT, to_numpy
