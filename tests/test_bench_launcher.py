@@ -158,3 +158,23 @@ def test_config5_independent_eviction_rehearsal():
     ev = r["parity"]["evictions"]["cilium_ct6_global"]
     assert ev["evict_log_equal"] and ev["sweeps_device"] >= 3 and ev["entries_evicted"] > 10_000, ev
     assert r["parity"]["mismatches"] == 0 and r["parity"]["ct_mismatches"] == 0
+
+
+def test_config2_ct_local_rehearsal():
+    """bench.py --ct-local (config 2 with every endpoint on a CT map of its own, the
+    ConntrackLocal option): the pre-inserted entries split by their endpoint address,
+    every map compared with the oracle's and the evictions of every map equal
+    (rehearsed with maps small enough to evict)."""
+    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--ct-local", "--no-extra", "--pairs", "4096",
+                        "--flows-per-step", "16384", "--steps", "4", "--warmup", "3", "--long-steps", "12",
+                        "--ct-max", "65536"], env=env, capture_output=True, text=True, timeout=600, cwd="/tmp")
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    par = r["parity"]
+    (name, t), = par["tables"].items()
+    assert name.endswith("per-endpoint maps") and t["mismatches"] == 0 and t["entries_compared"] > 10_000, par
+    (_, ev), = par["evictions"].items()
+    assert ev["evict_log_equal"] and ev["sweeps_device"] > 0, ev
+    assert par["mismatches"] == 0 and "ConntrackLocal" in r["config"]["workload"]
