@@ -22,6 +22,19 @@ KEY6 = struct.Struct("<16s16sHHBB2s")
 ENTRY = struct.Struct("<QQQQIHHHHI")
 
 
+def MapNames(ep_id=None, local=False):
+    """The CT maps an endpoint's program binds (pkg/endpoint/bpf.go:268-276): with the
+    ConntrackLocal option its own cilium_ct6_<id> / cilium_ct4_<id> of CT_MAP_SIZE
+    MapNumEntriesLocal, else the global ones of MapNumEntriesGlobal.  Returns
+    (CT_MAP6 name, CT_MAP4 name, CT_MAP_SIZE); the classify calls take either kind, mixed
+    in one program array (include/gpuflow.h, gf_lxc_cfg.ct_map4)."""
+    if local:
+        if ep_id is None:
+            raise ValueError("a per-endpoint CT map needs the endpoint ID")
+        return MapName6 + str(int(ep_id)), MapName4 + str(int(ep_id)), MapNumEntriesLocal
+    return MapName6Global, MapName4Global, MapNumEntriesGlobal
+
+
 def ct_key4(daddr_be, saddr_be, dport_be, sport_be, nexthdr, flags):
     return KEY4.pack(daddr_be, saddr_be, dport_be, sport_be, nexthdr, flags)
 

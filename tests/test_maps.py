@@ -282,3 +282,13 @@ def test_ctmap_gc_and_flush_host_shadow(v6):
     assert ctmap.Flush(fd, v6=v6) == len(left)
     assert ctmap.Dump(fd, v6) == []
     bpf.ObjClose(fd)
+
+
+def test_ct_map_names_global_and_local():
+    """pkg/endpoint/bpf.go:268-276: CT_MAP4/6 are the global maps unless the endpoint
+    has ConntrackLocal, which gives it cilium_ct4_<id> / cilium_ct6_<id> of
+    MapNumEntriesLocal entries (pkg/maps/ctmap/ctmap.go:34-41)."""
+    assert ctmap.MapNames() == ("cilium_ct6_global", "cilium_ct4_global", 1000000)
+    assert ctmap.MapNames(111, local=True) == ("cilium_ct6_111", "cilium_ct4_111", 64000)
+    with pytest.raises(ValueError):
+        ctmap.MapNames(local=True)
