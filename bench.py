@@ -1199,6 +1199,12 @@ def bench_egress(args, B):
     n = args.egress_flows
     t0 = time.time()
     sc, meta = synth.egress_tables(ct_max=args.ct_max)
+    ct_names = ["ct4"]
+    if args.ct_local:                                   # every endpoint on CT maps of its own (ConntrackLocal)
+        made = synth.conntrack_local(sc, max_entries=max(1, args.ct_max // len(sc.lxc)))
+        sc.maps.pop("ct4", None)
+        sc.maps.pop("ct6", None)
+        ct_names = [m for m in made if m.startswith("ct4_")]
     f, lens, lid, fh = synth.egress_flows(meta, n)
     dp = B.datapath(sc)
     log(f"egress: tables and {n} flows ({time.time() - t0:.1f}s)")
@@ -1220,18 +1226,19 @@ def bench_egress(args, B):
     log(f"egress: timed {K} steps ({time.time() - t0:.1f}s)")
     cpu = par = None
     if not args.no_cpu:
-        cpu, par = oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K)
+        cpu, par = oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K, ct_names)
     B.close(dp)
     return {"workload": "egress: bpf_lxc from-container handle_ipv4_from_lxc (+ handle_policy of local deliveries), "
                         f"256 endpoints, {n} flows/step (35% world, 20% tunnel, 25% local, 20% service "
-                        "VIPs), 1/4 new per step",
+                        "VIPs), 1/4 new per step"
+                        + (f", per-endpoint CT maps (ConntrackLocal, {len(ct_names)} CT4 maps)" if args.ct_local else ""),
             "mpps": round(int(c[268]) / el / 1e6, 1), "ms_per_step": round(el / K * 1e3, 4), "steps": K,
             "packets_per_step": int(c[268]) // K, "warmup": W,
             "roofline": roofline(kern, list(kern), float(c[270]) / K, "all egress kernels (frames -> verdicts)", K),
             "kernels_ms_per_step": kms(kern, K), "verdicts": verdicts(c), "cpu_baseline": cpu, "parity": par}
 
 
-def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
+def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K, ct_names=("ct4",)):
     """Parity and the CPU baseline from one pass: T oracle instances side by side,
     one per closed share of the flow groups (a tenant's local and service flows
     stay together; flows to world and tunnel peers, whose CT keys are their own
@@ -1252,7 +1259,7 @@ def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
     ep_idx = lid.astype(np.int64) - int(meta["lxc_id"][0])
     ten = ep_idx // TENANT
     T = cpu_threads()
-    evicted = B.evict_log(dp, "ct4")
+    evicted = any(len(B.evict_log(dp, name)) for name in ct_names)
     if evicted:
         T = 1                                           # LRU evictions depend on the whole table: one instance
     f0 = frames[0].cpu().numpy()
@@ -1289,11 +1296,12 @@ def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
         for t in range(T):
             r[shares[t]] = recs[t]
         par.records(outs[s].cpu().numpy().view(EG_OUT).ravel(), r, f"step {s}")
-    gk, gv, gtot = B.table_sampled(dp, "ct4", 14, 1, lambda k, div: np.ones(len(k), bool))
-    dumps = [ref.m["ct4"].dump_arrays() for ref in insts]
-    rk = np.concatenate([d[0] for d in dumps]) if dumps else np.zeros((0, 14), np.uint8)
-    rv = np.concatenate([d[1] for d in dumps]) if dumps else np.zeros((0, 48), np.uint8)
-    par.table("ct4", gk, gv, rk, rv, gtot)
+    for name in ct_names:                               # (each map: the union of the instances' copies)
+        gk, gv, gtot = B.table_sampled(dp, name, 14, 1, lambda k, div: np.ones(len(k), bool))
+        dumps = [ref.m[name].dump_arrays() for ref in insts]
+        rk = np.concatenate([d[0] for d in dumps]) if dumps else np.zeros((0, 14), np.uint8)
+        rv = np.concatenate([d[1] for d in dumps]) if dumps else np.zeros((0, 48), np.uint8)
+        par.table(name, gk, gv, rk, rv, gtot)
     one = OracleDP(sc)
     sh = shares[0][: max(1, len(shares[0]) // 4)]
     host0 = frames[0].cpu().numpy()
@@ -1304,7 +1312,12 @@ def oracle_egress(args, B, sc, meta, dp, frames, lens, lid, fh, outs, W, K):
                    f"{done} packets (every flow of the {K} timed steps after {W} warm-up steps), {T} oracle instances "
                    f"over closed flow-group shares; single core: {len(sh)} frames of step 0",
                    len(sh) / t1 / 1e6 if t1 else None)
-    return cpu, par.result(W + K)
+    res = par.result(W + K)
+    if len(res.get("tables", {})) > 4:                  # per-endpoint maps: one summary
+        t = res["tables"]
+        res["tables"] = {f"{len(t)} per-endpoint maps": {k: sum(v[k] for v in t.values())
+                                                         for k in ("entries_compared", "mismatches", "gpu_entries_total")}}
+    return cpu, res
 
 
 EXTRA = {"1": bench_config1, "3": bench_config3, "4": bench_config4, "5": bench_config5, "egress": bench_egress}
@@ -1480,7 +1493,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="config 2 only (skip the other configurations)")
     ap.add_argument("--no-h2d", action="store_true", help="config 4: skip the leg with the host->device copy")
     ap.add_argument("--ct-local", action="store_true",
-                    help="config 2: every endpoint on a CT map of its own (the ConntrackLocal option)")
+                    help="configs 2 and egress: every endpoint on CT maps of its own (the ConntrackLocal option)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-div", type=int, default=0,
                     help="parity sample: 1 in N address pairs (default: every pair at N=1, 1 in 2 per rank at N>1)")

@@ -178,3 +178,20 @@ def test_config2_ct_local_rehearsal():
     (_, ev), = par["evictions"].items()
     assert ev["evict_log_equal"] and ev["sweeps_device"] > 0, ev
     assert par["mismatches"] == 0 and "ConntrackLocal" in r["config"]["workload"]
+
+
+def test_egress_ct_local_sharded_parity_rehearsal():
+    """The egress leg with every endpoint on CT maps of its own: the oracle instances'
+    shares stay closed per map (a map's entries come from its endpoint's own sends and
+    deliveries), so the union of their copies of each map equals the sequential run's."""
+    env = dict(os.environ, GPUFLOW_BENCH_SELFTEST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "egress", "--ct-local",
+                        "--egress-flows", "65536", "--steps", "8"], env=env, capture_output=True, text=True,
+                       timeout=600, cwd="/tmp")
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    par = r["parity"]
+    (name, t), = par["tables"].items()
+    assert name == "256 per-endpoint maps" and t["mismatches"] == 0 and t["entries_compared"] > 100_000, par
+    assert par["mismatches"] == 0 and par["packets_compared"] == 65536 * par["steps"]
