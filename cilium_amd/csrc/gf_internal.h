@@ -137,6 +137,15 @@ struct Map : Obj {
     uint64_t ev_add[GF_EVRING] = {};
     uint32_t ev_head = 0, ev_pending = 0;
     uint64_t cnt_add = 0;
+    // The multi-map eviction pass (per-endpoint CT maps) records no events: its end
+    // kernel stamps the map's count with the call's lru_seq (seq << 32 | count) in
+    // pinned memory, st_add[] keeps cnt_add per recent seq, and stamps of calls at or
+    // before st_floor (the last time the bound was set directly) are ignored.
+    static constexpr uint32_t GF_STRING = 8;
+    unsigned long long *h_stamp = nullptr, *d_stamp = nullptr;
+    uint32_t st_seq[GF_STRING] = {};
+    uint64_t st_add[GF_STRING] = {};
+    uint32_t st_floor = 0;
     // get_next_key over a device-authoritative map: a host copy of one chunk of
     // slot headers, and the slot of the key returned last (the dump loop's next
     // argument) so a walk is not needed to resume.

@@ -3188,6 +3188,7 @@ struct LruMap {
     uint64_t nl, sl;
     uint32_t mode, max_entries, seq, pad;
     uint32_t *hcount;
+    unsigned long long *stamp;          // multi-map pass: seq << 32 | count after the pass (pinned), or null
 };
 struct LruBatch { LruMap m[GF_LRU_MULTI]; uint32_t n; };
 static_assert(GF_LRU_MULTI <= 32, "lru_active keeps one bit per map in a 32-bit mask");
@@ -3238,6 +3239,7 @@ __global__ void k_lru_end_multi(LruBatch B, uint32_t now) {
     if (threadIdx.x >= B.n) return;
     const LruMap &M = B.m[threadIdx.x];
     lru_end_body(M.d.count, M.seq, now, M.L, M.max_entries, M.nl, M.hcount);
+    if (M.stamp) *M.stamp = ((unsigned long long)M.seq << 32) | *M.d.count;
 }
 
 // ================================================================ drop notifications
@@ -5833,6 +5835,12 @@ static int prog_table(const std::shared_ptr<PolicyArray> &a, hipStream_t s,
 // wait: block on the oldest pending event instead (the device only has to reach
 // that earlier call, not drain the queue) — ct_limits' alternative to a readback.
 static void ct_count_refresh(Map &m, bool wait = false) {
+    if (m.h_stamp) {                                    // the multi-map pass's stamp (no wait: read as it is)
+        const unsigned long long v = *reinterpret_cast<volatile unsigned long long *>(m.h_stamp);
+        const uint32_t seq = (uint32_t)(v >> 32), j = seq % Map::GF_STRING;
+        if (seq > m.st_floor && m.st_seq[j] == seq)
+            m.dev_count_hi = std::min<uint64_t>(m.dev_count_hi, (uint64_t)(uint32_t)v + (m.cnt_add - m.st_add[j]));
+    }
     if (!m.ev_pending || !m.h_evcount) return;
     if (wait)
         for (uint32_t k = Map::GF_EVRING; k >= 1; k--) {
@@ -5862,7 +5870,7 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
         // call, the entries stay until the eviction pass after it (lru_evict), bounded by
         // the slot array (7/8 load = 3.5 x max_entries)
         const uint64_t limit = dev_insert_limit(*m);
-        if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = 0; }
+        if (m->host_valid) { m->dev_count_hi = m->ht.count; m->ev_pending = 0; m->st_floor = m->lru_seq; }
         ct_count_refresh(*m);
         // near the limit: the count of an eviction chain a few calls back first (no
         // queue drain), then, if that is not enough, a readback
@@ -5879,6 +5887,7 @@ static int ct_limits(const std::shared_ptr<Map> &ct4m, const std::shared_ptr<Map
                 return -EIO;
             m->dev_count_hi = dc;
             m->ev_pending = 0;
+            m->st_floor = m->lru_seq;
         }
         if (m->dev_count_hi + (uint64_t)per_pkt * n > limit) strict |= m == ct4m ? 1u : 2u;
         m->dev_count_hi += (uint64_t)per_pkt * n;
@@ -6002,9 +6011,24 @@ static int lru_prepare(const std::shared_ptr<Map> &m, LruPrep &P, bool track = t
         m->h_evcount = (uint32_t *)p;
         m->d_evcount = dp;
     }
+    if (!track && !m->h_stamp) {
+        void *p = nullptr;
+        unsigned long long *dp = nullptr;
+        if (hip_ok(hipHostMalloc(&p, 8, hipHostMallocMapped | hipHostMallocCoherent), "lru stamp")) return -ENOMEM;
+        *(unsigned long long *)p = 0ull;
+        if (hip_ok(hipHostGetDevicePointer((void **)&dp, p, 0), "lru stamp")) { (void)hipHostFree(p); return -EIO; }
+        m->h_stamp = (unsigned long long *)p;
+        m->d_stamp = dp;
+    }
     P.m = m.get(); P.kind = kind; P.slot = m->ev_head;
     LruMap &M = P.lm;
     M.hcount = track ? m->d_evcount + P.slot : nullptr;
+    M.stamp = track ? nullptr : m->d_stamp;
+    if (!track) {                                       // the stamp's reference point: cnt_add at this call
+        const uint32_t j = m->lru_seq % Map::GF_STRING;
+        m->st_seq[j] = m->lru_seq;
+        m->st_add[j] = m->cnt_add;
+    }
     const uint64_t ns = d.mask + 1, spl = 128 / d.slot_size;
     M.d = d; M.L = (LruDev *)m->d_lru.p; M.nl = ns / spl; M.sl = lru_sample_lines(M.nl);
     M.mode = m->ht.mode; M.max_entries = m->max_entries; M.seq = m->lru_seq;
@@ -6616,6 +6640,7 @@ int gf_ct_gc(int map, uint32_t filter_time, void *stream) {
     if (hip_ok(hipMemcpy(m->d_count.p, &cnt, 4, hipMemcpyHostToDevice), "gc count")) return -EIO;
     m->dev_count_hi = cnt;
     m->ev_pending = 0;
+    m->st_floor = m->lru_seq;
     m->device_modified();
     return (int)std::min<unsigned long long>(r[0], 0x7fffffff);
 }
@@ -6794,6 +6819,7 @@ int dev_bulk_insert(Map &m, const uint8_t *keys, const uint8_t *vals, uint32_t n
     m.dev_gen++;
     m.dev_count_hi = before + n;
     m.ev_pending = 0;
+    m.st_floor = m.lru_seq;
     fallback = false;
     return 0;
 }

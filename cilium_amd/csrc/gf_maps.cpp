@@ -216,6 +216,7 @@ Map::Map(uint32_t t, uint32_t k, uint32_t v, uint32_t m, uint32_t f)
 Map::~Map() {
     for (auto &e : ev_count) if (e) (void)hipEventDestroy(e);
     if (h_evcount) (void)hipHostFree(h_evcount);
+    if (h_stamp) (void)hipHostFree(h_stamp);
 }
 
 // Fixed-capacity maps are materialized lazily: slots.size()==0 means all-empty.
@@ -528,6 +529,7 @@ int Map::dev_count(uint32_t &c) {
 int Map::dev_set_count(uint32_t c) {
     dev_count_hi = c;
     ev_pending = 0;
+    st_floor = lru_seq;
     return dev_wr(*this, d_count.p, &c, 4);
 }
 
