@@ -150,6 +150,38 @@ def test_gpu_conntrack_local_many_maps(n_ep, mx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("every,mx", [(1, 500), (2, 800)])
+def test_gpu_conntrack_local_queued_calls(every, mx):
+    """Eight calls queued back to back, no host sync between them, on 40 small
+    per-endpoint maps (all or every 2nd endpoint; the rest on the global map): the host's
+    count bound of each map refreshes only from the counts the multi-map eviction pass
+    stamps (`seq << 32 | count`), which may be a call or more behind the host.  Every
+    call's records and every map equal the oracle's once the queue drains."""
+    _gpu()
+    from cilium_amd.datapath import Datapath, DeviceBatch, ING_OUT, to_numpy
+    sc = synth.config2(n_flows=160_000, n_pairs=16_000, n_ep=40, n_ids=512, n_l3=200, n_l4=400, n_wc=8,
+                       n_cidr=32, ct_max=400_000)
+    made = synth.conntrack_local(sc, every=every, max_entries=mx)
+    dp, ref = Datapath(sc, pin_prefix=None), OracleDP(sc)
+    pk = sc.batches[0]
+    q = (pk.n + 7) // 8
+    parts = [pk.slice(k * q, min(pk.n, (k + 1) * q)) for k in range(8)]
+    dbs = [DeviceBatch(p) for p in parts]
+    torch.cuda.synchronize()
+    outs = [dp.ingress(db, sc.now + k) for k, db in enumerate(dbs)]
+    torch.cuda.synchronize()
+    for k, part in enumerate(parts):
+        got, want = to_numpy(outs[k], ING_OUT), ref.ingress(part, sc.now + k)
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, f"call {k}: {len(bad)} records differ, first {bad[:1]}"
+    for name in made + ["cilium_ct4_global"]:
+        assert dp.dump_map(name) == ref.dump(name), name
+    # every local map evicted on every call (the oracle's log; the device's equal maps
+    # say its evictions matched)
+    assert all(len(ref.lru_log[n]) == 8 for n in made), {n: len(ref.lru_log[n]) for n in made}
+
+
+@pytest.mark.gpu
 def test_gpu_conntrack_local_batches_api():
     """gf_policy_ingress_classify_batches (schedules built on the aux stream) with
     per-endpoint maps: the same records and maps as the oracle."""
